@@ -1,0 +1,764 @@
+// exo_env.hip -- vectorised exoskeleton environment for MI355X (gfx950).
+//
+// Kernels
+//   exo_reset_kernel : one wavefront per env.  Lanes sweep the tremor samples
+//                      (generate_parkinson_tremor.py:31-73), the domain-
+//                      randomised matrices (Exoskeleton_env.py:208-210) and the
+//                      dummy shift (Exoskeleton_sim_pybullet.py:98-107); lane 0
+//                      inverts the two diagonal blocks of I and packs the reset
+//                      observation (Exoskeleton_env.py:220-254).
+//   exo_step_kernel  : two lanes per env.  Both lanes run the kinematics and
+//                      torque model (Exoskeleton_env.py:369-406); lane 0 solves
+//                      the actuated joint ODE, lane 1 the tremor-only ODE
+//                      (:409-414), then lane 0 finishes the step (targets,
+//                      motor update, reward, observation; :417-471).
+//
+// C ABI: include/exo_amd.h.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "exo_amd.h"
+#include "exo_model.h"
+
+using namespace exo;
+
+namespace {
+
+__device__ __forceinline__ double cfg(const Dev &S, int k, int e) { return S.cfg[(size_t)k * S.N + e]; }
+
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+struct Draws {
+    const double *buf; // injected stream or nullptr (Philox)
+    uint64_t seed;
+    uint32_t env, episode;
+    __device__ __forceinline__ double operator()(int p) const {
+        return buf ? buf[p] : philox_u01(seed, env, episode, (uint32_t)p);
+    }
+};
+
+// Invert a small dense matrix (Gauss-Jordan, partial pivoting), fp64.
+template <int n>
+__device__ void invert(double *a /* n*n, destroyed */, double *inv) {
+    for (int i = 0; i < n * n; ++i) inv[i] = (i % (n + 1) == 0) ? 1.0 : 0.0;
+    for (int k = 0; k < n; ++k) {
+        int p = k;
+        for (int i = k + 1; i < n; ++i)
+            if (fabs(a[i * n + k]) > fabs(a[p * n + k])) p = i;
+        if (p != k)
+            for (int j = 0; j < n; ++j) {
+                double t = a[k * n + j]; a[k * n + j] = a[p * n + j]; a[p * n + j] = t;
+                t = inv[k * n + j]; inv[k * n + j] = inv[p * n + j]; inv[p * n + j] = t;
+            }
+        const double r = 1.0 / a[k * n + k];
+        for (int j = 0; j < n; ++j) { a[k * n + j] *= r; inv[k * n + j] *= r; }
+        for (int i = 0; i < n; ++i) {
+            if (i == k) continue;
+            const double m = a[i * n + k];
+            for (int j = 0; j < n; ++j) { a[i * n + j] -= m * a[k * n + j]; inv[i * n + j] -= m * inv[k * n + j]; }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// reset: initialize_movement (Exoskeleton_env.py:193-254).  The draw stream
+// follows the reference's np.random call order:
+//   0 magnitude, 1 f1, 2 f2, 3..3+L-1 white noise,
+//   per axis i: base_i = 3+L+i(L+2): a1, a2, L signs,
+//   17+8L: I noise (49), D noise (49), S noise (49), 164+8L: shift (42),
+//   206+8L: shoulder force scale, elbow force scale.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void exo_reset_kernel(Dev S, Urdf U, const uint8_t *mask, const int32_t *ids,
+                                                       const double *draws, int draw_stride, uint64_t seed,
+                                                       float *obs) {
+    const int e = ids ? ids[blockIdx.x] : (int)blockIdx.x;
+    if (e >= S.N) return;
+    if (!ids && mask && !mask[e]) return;
+    const int lane = threadIdx.x;
+    const int N = S.N, L = S.L[e], seq = S.seq[e];
+    const uint32_t ep = S.episode[e];
+    const Draws D{draws ? draws + (size_t)blockIdx.x * draw_stride : nullptr, seed, (uint32_t)e, ep};
+
+    __shared__ double sI[49], sD[49], sS[49], sShift[42], sTrem[3][4], sInv[NINV];
+
+    // ---- tremor (generate_parkinson_tremor.py:5-28, :31-73) -------------
+    const double amp0 = cfg(S, C_AMP0, e), amp1 = cfg(S, C_AMP1, e);
+    const double mag = amp0 + (D(0) * (amp1 - amp0)); // :198-199
+    const double h1a = cfg(S, C_H1A, e), h1b = cfg(S, C_H1B, e), h2a = cfg(S, C_H2A, e), h2b = cfg(S, C_H2B, e);
+    const double f1 = h1a + (h1b - h1a) * D(1);
+    const double f2 = h2a + (h2b - h2a) * D(2);
+    const double stop = L * DT, step = stop / (L - 1); // np.linspace(0, L*dt, L)
+    const double w1 = 2 * PI * f1, w2 = 2 * PI * f2;
+    double a1[7], a2[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+        const int b = 3 + L + i * (L + 2);
+        a1[i] = pow(10.0, (-5.0 + (0.0 - (-5.0)) * D(b)) / 20);
+        a2[i] = pow(10.0, (-20.0 + (-10.0 - (-20.0)) * D(b + 1)) / 20);
+    }
+    double wv1[T_PER_LANE], wv2[T_PER_LANE], nz[T_PER_LANE];
+    double mn[7], mx[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) { mn[i] = INFINITY; mx[i] = -INFINITY; }
+#pragma unroll
+    for (int k = 0; k < T_PER_LANE; ++k) {
+        const int t = lane + 64 * k;
+        if (t < L) {
+            const double tt = (t == L - 1) ? stop : t * step;
+            wv1[k] = sin(w1 * tt);
+            wv2[k] = sin(w2 * tt);
+            nz[k] = D(3 + t) * 0.001;
+#pragma unroll
+            for (int i = 0; i < 7; ++i) {
+                const double acc = (a1[i] * wv1[k] + a2[i] * wv2[k] + nz[k]) * (double)((seq >> i) & 1);
+                mn[i] = fmin(mn[i], acc);
+                mx[i] = fmax(mx[i], acc);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 7; ++i) { mn[i] = wave_min(mn[i]); mx[i] = wave_max(mx[i]); }
+    const double jmax0[7] = {2.5, 5, 10, 5, 5, 0.5, 0.5};
+#pragma unroll
+    for (int k = 0; k < T_PER_LANE; ++k) {
+        const int t = lane + 64 * k;
+        if (t < L) {
+#pragma unroll
+            for (int i = 0; i < 7; ++i) {
+                const double acc = (a1[i] * wv1[k] + a2[i] * wv2[k] + nz[k]) * (double)((seq >> i) & 1);
+                double v = (-1 + 2 * (acc - mn[i]) / (mx[i] - mn[i])) * (jmax0[i] * mag);
+                if (!isfinite(v)) v = 0.0; // np.nan_to_num (:67)
+                const double sgn = (D(3 + L + i * (L + 2) + 2 + t) < 0.5) ? -1.0 : 1.0;
+                v *= sgn;
+                S.tremor[((size_t)t * 7 + i) * N + e] = v;
+                if (t < 3 && i < 4) sTrem[t][i] = v;
+            }
+        }
+    }
+
+    // ---- domain-randomised matrices (domain_randomization_...py:4-27) ----
+    const double mf = cfg(S, C_MATF, e);
+    const int pI = 17 + 8 * L;
+    if (lane < 49) {
+        const int r = lane / 7, c = lane % 7, tr = c * 7 + r;
+        double n0, n1, s;
+        n0 = -mf + (mf - (-mf)) * D(pI + lane); n1 = -mf + (mf - (-mf)) * D(pI + tr);
+        s = (n0 + n1) / 2; sI[lane] = I0[lane] + s * I0[lane];
+        n0 = -mf + (mf - (-mf)) * D(pI + 49 + lane); n1 = -mf + (mf - (-mf)) * D(pI + 49 + tr);
+        s = (n0 + n1) / 2; sD[lane] = D0[lane] + s * D0[lane];
+        n0 = -mf + (mf - (-mf)) * D(pI + 98 + lane); n1 = -mf + (mf - (-mf)) * D(pI + 98 + tr);
+        s = (n0 + n1) / 2; sS[lane] = S0[lane] + s * S0[lane];
+    }
+    const double sr = cfg(S, C_SHIFT, e);
+    if (lane < 42) {
+        const double v = -sr + (sr - (-sr)) * D(pI + 147 + lane);
+        sShift[lane] = v;
+        S.shift[(size_t)lane * N + e] = v;
+    }
+    __syncthreads();
+    if (lane < NSYM) { // the upper-triangle non-zeros of D and S
+        int r = 0, c = 0;
+#pragma unroll
+        for (int k = 0; k < NSYM; ++k)
+            if (k == lane) { r = SYM_R[k]; c = SYM_C[k]; }
+        S.dnz[(size_t)lane * N + e] = sD[r * 7 + c];
+        S.snz[(size_t)lane * N + e] = sS[r * 7 + c];
+    }
+    if (lane == 0) {
+        double a3[9], i3[9], a4[16], i4[16];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) a3[i * 3 + j] = sI[B1[i] * 7 + B1[j]];
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j) a4[i * 4 + j] = sI[B2[i] * 7 + B2[j]];
+        invert<3>(a3, i3);
+        invert<4>(a4, i4);
+        for (int i = 0; i < 3; ++i)
+            for (int j = i; j < 3; ++j) sInv[B1U[i][j]] = i3[i * 3 + j];
+        for (int i = 0; i < 4; ++i)
+            for (int j = i; j < 4; ++j) sInv[B2U[i][j]] = i4[i * 4 + j];
+    }
+    __syncthreads();
+    if (lane < NINV) S.iinv[(size_t)lane * N + e] = sInv[lane];
+
+    if (lane != 0) return;
+    // ---- actuator force scale (:216-217) --------------------------------
+    const double ar = cfg(S, C_ACTR, e), lo = 1 - ar, hi = 1 + ar;
+    const double maxS = cfg(S, C_MAXS0, e) * (lo + (hi - lo) * D(pI + 189));
+    const double maxE = cfg(S, C_MAXE0, e) * (lo + (hi - lo) * D(pI + 190));
+    S.maxSE[e] = maxS;
+    S.maxSE[(size_t)N + e] = maxE;
+    S.counts[e] = 2;
+    S.episode[e] = ep + 1;
+
+    // ---- reset observation (:229-254).  No stepSimulation in between, so
+    // both reads see the same physics state; prev_position_vectors uses the
+    // reference positions cached by the previous read.
+    double q[5], act[14][3], ref[6], refc[6];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) q[j] = S.phys_q[(size_t)j * N + e];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) refc[j] = S.ref[(size_t)j * N + e];
+    link_coms(U, q, act, ref);
+    float *o = obs + (size_t)e * OBS;
+    float ob[OBS];
+#pragma unroll
+    for (int i = 0; i < 14; ++i) ob[i] = 0.0f; // ep_state_values forces are zero at c-2, c-1
+    const double tn[4] = {10, 10, 10, 5};
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ob[14 + t * 4 + i] = (float)(sTrem[t][i] / tn[i]);
+#pragma unroll
+    for (int j = 0; j < 7; ++j)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const double p = act[2 * j + 1][a] + sShift[(2 * j + 1) * 3 + a];
+            const double rc = (j < 2) ? refc[3 + a] : refc[a];
+            const double rn = (j < 2) ? ref[3 + a] : ref[a];
+            ob[26 + j * 3 + a] = (float)(p - rc);
+            const float pv = (float)(p - rn);
+            ob[47 + j * 3 + a] = pv;
+            S.posv[(size_t)(j * 3 + a) * N + e] = pv;
+        }
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        ob[68 + j] = (float)ref[j];
+        ob[74 + j] = (float)ref[j];
+        S.ref[(size_t)j * N + e] = ref[j];
+    }
+    if (o) {
+#pragma unroll
+        for (int i = 0; i < OBS; i += 4) *reinterpret_cast<float4 *>(o + i) = make_float4(ob[i], ob[i + 1], ob[i + 2], ob[i + 3]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// step (Exoskeleton_env.py:368-471).  Thread pair per env.  Everything the
+// step returns except the joint-angle part of `info` depends only on the
+// physics state read at the start of the step (the observation never sees the
+// ODE result), so role 0 finishes observation, reward, done and the carried
+// state BEFORE the solves; only the joint targets / motor update (role 0) and
+// the two `ampl` info blocks need the ODE.  That keeps the epilogue out of the
+// register budget of the RK45 loop.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void exo_step_kernel(Dev S, Urdf U, const float *__restrict__ act,
+                                                       float *__restrict__ obs, float *__restrict__ rew,
+                                                       uint8_t *__restrict__ done, float *__restrict__ info,
+                                                       const uint8_t *__restrict__ active) {
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const int e = gid >> 1, role = gid & 1;
+    if (e >= S.N) return;
+    const int N = S.N, c = S.counts[e], L = S.L[e];
+    if ((active && !active[e]) || c >= L - 1) return; // both lanes of the pair agree
+
+    double T[7];
+    {
+        const double maxS = S.maxSE[e], maxE = S.maxSE[(size_t)N + e];
+        // transform_action (:256-266)
+        double F[7];
+        const float *a = act + (size_t)e * ACT;
+#pragma unroll
+        for (int j = 0; j < 7; ++j) F[j] = (((double)a[j] + 1) / 2) * (j < 2 ? maxE : maxS);
+        // link reads of the state left by the last stepSimulation
+        double q[5], ak[14][3], refn[6], refo[6];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) q[j] = S.phys_q[(size_t)j * N + e];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) refo[j] = S.ref[(size_t)j * N + e];
+        link_coms(U, q, ak, refn);
+#pragma unroll
+        for (int k = 0; k < 14; ++k)
+#pragma unroll
+            for (int a3 = 0; a3 < 3; ++a3) ak[k][a3] += S.shift[(size_t)(k * 3 + a3) * N + e];
+
+        // get_force_components (sim:207-298) and get_torques (:177-187)
+        double tau[7][3];
+#pragma unroll
+        for (int j = 0; j < 7; ++j) {
+            const double *k1 = ak[2 * j], *k2 = ak[2 * j + 1];
+            const double dx = (k2[0] + 5) - (k1[0] + 5), dy = (k2[1] + 5) - (k1[1] + 5), dz = (k2[2] + 5) - (k1[2] + 5);
+            const double fx = cos_atan2(dy, dx) * F[j], fy = cos_atan2(dx, dy) * F[j], fz = cos_atan2(dz, dx) * F[j];
+            const double *rn = (j < 2) ? &refn[3] : &refn[0];
+            const double r0 = rn[0] - k2[0], r1 = rn[1] - k2[1], r2 = rn[2] - k2[2];
+            tau[j][0] = fy * r2 - fz * r1; // np.cross(F, r)
+            tau[j][1] = fz * r0 - fx * r2;
+            tau[j][2] = fx * r1 - fy * r0;
+        }
+        // :394-400, summed in the reference's actuator order 3, 4, 5, 7, 6
+        double at[4];
+        at[0] = tau[2][1] + tau[3][1] + tau[4][1] + tau[6][1] + tau[5][1];
+        at[1] = tau[2][0] + tau[3][0] + tau[4][0] + tau[6][0] + tau[5][0];
+        at[2] = tau[2][2] + tau[3][2] + tau[4][2] + tau[6][2] + tau[5][2];
+        at[3] = fabs(tau[0][1]) - fabs(tau[1][1]);
+
+        double tr[7], Ta[7];
+#pragma unroll
+        for (int j = 0; j < 7; ++j) {
+            tr[j] = S.tremor[((size_t)c * 7 + j) * N + e];
+            Ta[j] = tr[j] + (j < 4 ? at[j] : 0.0); // :406
+            T[j] = role == 0 ? Ta[j] : tr[j];
+        }
+
+        if (role == 0) {
+            // get_reward (:268-366)
+            const int seq = S.seq[e];
+            const double eps = 1e-10, Msum = maxE + maxS, naxes = cfg(S, C_NAXES, e);
+            double pa[7], pa2[7];
+#pragma unroll
+            for (int j = 0; j < 7; ++j) { pa[j] = S.prev_a[(size_t)j * N + e]; pa2[j] = S.prev2_a[(size_t)j * N + e]; }
+            double unw = 0.0, st = 0.0;
+            int nred = 0;
+#pragma unroll
+            for (int j = 0; j < 7; ++j) {
+                const double Tabs = fabs(Ta[j]), tabs = fabs(tr[j]);
+                if (j < 4) {
+                    if ((seq >> j) & 1) st += (Tabs - tabs) / tabs + 1;
+                    else unw += Tabs;
+                }
+                const double v = (Tabs - tabs) / (tabs + eps) * 100;
+                if (isfinite(v) && v < 0) nred++; // nan_to_num then "< 0"
+            }
+            const double r_unw = exp(-(unw / (Msum / 4 / naxes)) + eps) * 0.5;
+            const double r_tor = exp((-st + eps) / naxes) * 0.9;
+            const double r_axis = nred * 0.5;
+            double sa = 0.0, sm = 0.0;
+#pragma unroll
+            for (int j = 0; j < 7; ++j) {
+                sa += F[j];
+                const double d = F[j] - 2 * pa[j] + pa2[j];
+                sm += d * d;
+            }
+            sm /= 7;
+            const double r_ctl = exp(-(sa / (Msum / 2)) + eps) * 0.05;
+            const double r_sm = 0.05 * exp(-(sm / (Msum / 4)) + eps);
+            rew[e] = (float)((r_axis + r_tor + r_sm + r_ctl + r_unw) / cfg(S, C_MAXREW, e));
+            done[e] = (uint8_t)(c + 1 >= L - 1); // :457-458
+
+            // update_state_vector (:487-570) with counts = c + 1
+            float ob[OBS];
+            const double maxS0 = cfg(S, C_MAXS0, e), maxE0 = cfg(S, C_MAXE0, e);
+#pragma unroll
+            for (int j = 0; j < 7; ++j) {
+                const double nrm = j < 2 ? maxE0 : maxS0;
+                ob[j] = (float)((c > 2 ? pa[j] : 0.0) / nrm); // ep_state_values[c-1] is 0 on the first step
+                ob[7 + j] = (float)(F[j] / nrm);
+            }
+            const double tn[4] = {10, 10, 10, 5};
+#pragma unroll
+            for (int b = 0; b < 3; ++b)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const double v = (b == 1) ? tr[i] : S.tremor[((size_t)(c - 1 + b) * 7 + i) * N + e];
+                    ob[14 + b * 4 + i] = (float)(v / tn[i]);
+                }
+#pragma unroll
+            for (int j = 0; j < 7; ++j)
+#pragma unroll
+                for (int a3 = 0; a3 < 3; ++a3) {
+                    const int i = j * 3 + a3;
+                    // get_actuator_pos_vect uses the reference positions cached by the previous read (sim:300-336)
+                    const float p = (float)(ak[2 * j + 1][a3] - (j < 2 ? refo[3 + a3] : refo[a3]));
+                    ob[26 + i] = S.posv[(size_t)i * N + e];
+                    ob[47 + i] = p;
+                    S.posv[(size_t)i * N + e] = p;
+                }
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                ob[68 + j] = (float)refo[j];
+                ob[74 + j] = (float)refn[j];
+                S.ref[(size_t)j * N + e] = refn[j];
+            }
+            float *o = obs + (size_t)e * OBS;
+#pragma unroll
+            for (int i = 0; i < OBS; i += 4) *reinterpret_cast<float4 *>(o + i) = make_float4(ob[i], ob[i + 1], ob[i + 2], ob[i + 3]);
+            if (info) {
+                float *io = info + (size_t)e * INFO;
+#pragma unroll
+                for (int j = 0; j < 7; ++j) {
+                    io[j] = (float)(j < 4 ? at[j] : 0.0);
+                    io[7 + j] = (float)Ta[j];
+                    io[21 + j] = (float)tr[j];
+                }
+                io[35] = (float)r_unw; io[36] = (float)r_tor; io[37] = (float)r_axis; io[38] = (float)r_ctl;
+                io[39] = (float)r_sm;
+            }
+            S.counts[e] = c + 1;
+#pragma unroll
+            for (int j = 0; j < 7; ++j) { S.prev2_a[(size_t)j * N + e] = pa[j]; S.prev_a[(size_t)j * N + e] = F[j]; }
+        }
+    }
+
+    // ---- the two joint ODE solves (:409-414) ------------------------------
+    OdeM M;
+#pragma unroll
+    for (int k = 0; k < NINV; ++k) M.ii[k] = S.iinv[(size_t)k * N + e];
+#pragma unroll
+    for (int k = 0; k < NSYM; ++k) { M.dn[k] = S.dnz[(size_t)k * N + e]; M.sn[k] = S.snz[(size_t)k * N + e]; }
+    double qs[7];
+    if (!rk45_solve(M, T, qs)) atomicOr(S.err, 1);
+    const double r2d = 180 / PI, d2r = PI / 180;
+#pragma unroll
+    for (int j = 0; j < 7; ++j) qs[j] *= r2d; // :417-418
+    if (info) {
+        float *io = info + (size_t)e * INFO + (role == 0 ? 14 : 28); // ampl_val / tremor_ampl_val
+#pragma unroll
+        for (int j = 0; j < 7; ++j) io[j] = (float)qs[j];
+    }
+    if (role != 0) return;
+    // :421-433 joint targets, then the motors move (idealised Bullet)
+    const double *imu = S.imu + (size_t)S.motion[e] * 5 * S.Lmax;
+    const double ang[4] = {imu[4 * S.Lmax + c] + qs[2], imu[3 * S.Lmax + c] + qs[0], imu[2 * S.Lmax + c] + qs[1],
+                           imu[0 * S.Lmax + c] + qs[3]}; // shoulder z, y, x, elbow y (deg)
+    const double tgt[5] = {ang[0] * d2r, ang[1] * d2r, ang[2] * d2r, ang[3] * d2r, imu[1 * S.Lmax + c] * d2r};
+    // check_movement_boundaries (:594-605) prints; the build counts the steps with a violation
+    if (!(-80 < ang[0] && ang[0] < 80) || !(-40 < ang[1] && ang[1] < 160.5) || !(-151.5 < ang[2] && ang[2] < 33.5) ||
+        !(-10 < ang[3] && ang[3] < 150))
+        S.viol[e] += 1;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        const double q0 = S.phys_q[(size_t)j * N + e];
+        const double nq = q0 + 0.1 * (tgt[j] - q0);
+        S.phys_q[(size_t)j * N + e] = fmin(fmax(nq, U.lo[j]), U.hi[j]);
+    }
+}
+
+} // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+struct exo_ctx {
+    int device = 0;
+    int N = 0, n_motions = 0, Lmax = 0;
+    uint64_t seed = 0;
+    Dev S{};
+    Urdf U{};
+    std::vector<int32_t> L_host, motion_host;
+    std::vector<double> imu_host;
+    std::vector<void *> allocs;
+    float *obs_scratch = nullptr;
+    std::string err;
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) == hipSuccess && prev != dev) (void)hipSetDevice(dev);
+        else prev = -1;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+int fail(exo_ctx *c, int code, const std::string &msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+int check(exo_ctx *c, hipError_t e, const char *what) {
+    if (e == hipSuccess) return EXO_OK;
+    return fail(c, EXO_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+template <class T>
+T *dalloc(exo_ctx *c, size_t n) {
+    void *p = nullptr;
+    if (hipMalloc(&p, n * sizeof(T)) != hipSuccess) return nullptr;
+    (void)hipMemset(p, 0, n * sizeof(T));
+    c->allocs.push_back(p);
+    return static_cast<T *>(p);
+}
+
+} // namespace
+
+namespace {
+template <class T>
+int read1(exo_ctx *c, const T *base, size_t idx, T *out) {
+    return check(c, hipMemcpy(out, base + idx, sizeof(T), hipMemcpyDeviceToHost), "read-back");
+}
+template <class T>
+int write1(exo_ctx *c, T *base, size_t idx, T v) {
+    return check(c, hipMemcpy(base + idx, &v, sizeof(T), hipMemcpyHostToDevice), "write");
+}
+} // namespace
+
+extern "C" {
+
+int exo_create(const exo_env_config *cfgs, int32_t n_envs, const double *motion_angles, const int32_t *motion_lengths,
+               int32_t n_motions, int32_t max_len, uint64_t seed, int32_t device, exo_ctx **out) {
+    if (!out || !cfgs || !motion_angles || !motion_lengths || n_envs <= 0 || n_motions <= 0 || max_len <= 2 ||
+        max_len > MAX_L)
+        return EXO_EINVAL;
+    *out = nullptr;
+    for (int m = 0; m < n_motions; ++m)
+        if (motion_lengths[m] < 4 || motion_lengths[m] > max_len) return EXO_EINVAL;
+    std::vector<double> cfg((size_t)C_COUNT * n_envs);
+    std::vector<int32_t> seq(n_envs), L(n_envs), mot(n_envs);
+    for (int e = 0; e < n_envs; ++e) {
+        const exo_env_config &c = cfgs[e];
+        if (c.motion < 0 || c.motion >= n_motions) return EXO_EINVAL;
+        int bits = 0, n = 0;
+        for (int i = 0; i < 7; ++i) {
+            if (c.tremor_sequence[i] != 0 && c.tremor_sequence[i] != 1) return EXO_EINVAL;
+            bits |= c.tremor_sequence[i] << i;
+            n += c.tremor_sequence[i];
+        }
+        if (n == 0) return EXO_EINVAL; // reward divides by the tremor axis count (:320, :337)
+        seq[e] = bits;
+        mot[e] = c.motion;
+        L[e] = motion_lengths[c.motion];
+        const double v[C_COUNT] = {c.tremor_amplitude_range[0], c.tremor_amplitude_range[1],
+                                   c.first_harmonics_interval[0], c.first_harmonics_interval[1],
+                                   c.second_harmonics_interval[0], c.second_harmonics_interval[1],
+                                   c.max_force_shoulder, c.max_force_elbow, c.dr_actuator_end_pos_shift,
+                                   c.dr_actuator_range, c.matrix_noise_fraction,
+                                   n * 0.5 + 0.9 + 0.05 + 0.05 + 0.5, (double)n}; // max_reward :167-169
+        for (int k = 0; k < C_COUNT; ++k) cfg[(size_t)k * n_envs + e] = v[k];
+    }
+    exo_ctx *c = new exo_ctx();
+    c->device = device;
+    c->N = n_envs;
+    c->n_motions = n_motions;
+    c->Lmax = max_len;
+    c->seed = seed;
+    c->L_host = L;
+    c->motion_host = mot;
+    c->imu_host.assign(motion_angles, motion_angles + (size_t)n_motions * 5 * max_len);
+    build_urdf(c->U);
+    DeviceGuard g(device);
+    const size_t N = n_envs;
+    Dev &S = c->S;
+    S.N = n_envs; S.n_motions = n_motions; S.Lmax = max_len;
+    int32_t *motion_d = dalloc<int32_t>(c, N), *L_d = dalloc<int32_t>(c, N), *seq_d = dalloc<int32_t>(c, N);
+    double *cfg_d = dalloc<double>(c, cfg.size()), *imu_d = dalloc<double>(c, c->imu_host.size());
+    S.tremor = dalloc<double>(c, (size_t)max_len * 7 * N);
+    S.iinv = dalloc<double>(c, NINV * N);
+    S.dnz = dalloc<double>(c, NSYM * N);
+    S.snz = dalloc<double>(c, NSYM * N);
+    S.shift = dalloc<double>(c, 42 * N);
+    S.maxSE = dalloc<double>(c, 2 * N);
+    S.episode = dalloc<uint32_t>(c, N);
+    S.counts = dalloc<int32_t>(c, N);
+    S.phys_q = dalloc<double>(c, 5 * N);
+    S.ref = dalloc<double>(c, 6 * N);
+    S.posv = dalloc<float>(c, 21 * N);
+    S.prev_a = dalloc<double>(c, 7 * N);
+    S.prev2_a = dalloc<double>(c, 7 * N);
+    S.err = dalloc<int32_t>(c, 1);
+    S.viol = dalloc<int32_t>(c, N);
+    c->obs_scratch = dalloc<float>(c, N * OBS);
+    for (void *p : c->allocs)
+        if (!p) { exo_destroy(c); return EXO_ENOMEM; }
+    if (!motion_d || !L_d || !seq_d || !cfg_d || !imu_d || !S.tremor || !S.iinv ||
+        !S.dnz || !S.snz || !S.shift || !S.maxSE || !S.episode || !S.counts || !S.phys_q || !S.ref || !S.posv ||
+        !S.prev_a || !S.prev2_a || !S.err || !S.viol || !c->obs_scratch) {
+        exo_destroy(c);
+        return EXO_ENOMEM;
+    }
+    S.motion = motion_d; S.L = L_d; S.seq = seq_d; S.cfg = cfg_d; S.imu = imu_d;
+    hipError_t e = hipMemcpy(motion_d, mot.data(), N * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(L_d, L.data(), N * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(seq_d, seq.data(), N * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(cfg_d, cfg.data(), cfg.size() * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(imu_d, c->imu_host.data(), c->imu_host.size() * 8, hipMemcpyHostToDevice);
+    if (e != hipSuccess) { exo_destroy(c); return EXO_EDEVICE; }
+    // the constructor runs initialize_movement() once (Exoskeleton_env.py:172)
+    int rc = exo_reset(c, nullptr, c->obs_scratch, nullptr);
+    if (rc == EXO_OK) rc = check(c, hipDeviceSynchronize(), "exo_create");
+    if (rc != EXO_OK) { exo_destroy(c); return rc; }
+    *out = c;
+    return EXO_OK;
+}
+
+int exo_reset(exo_ctx *c, const uint8_t *mask_dev, float *obs_dev, void *stream) {
+    if (!c) return EXO_EINVAL;
+    DeviceGuard g(c->device);
+    hipLaunchKernelGGL(exo_reset_kernel, dim3(c->N), dim3(64), 0, (hipStream_t)stream, c->S, c->U, mask_dev,
+                       (const int32_t *)nullptr, (const double *)nullptr, 0, c->seed, obs_dev);
+    return check(c, hipGetLastError(), "exo_reset");
+}
+
+int exo_reset_from_draws(exo_ctx *c, const int32_t *env_ids_host, int32_t n, const double *draws_host, float *obs_dev,
+                         void *stream) {
+    if (!c || !env_ids_host || !draws_host || n <= 0) return EXO_EINVAL;
+    for (int k = 0; k < n; ++k)
+        if (env_ids_host[k] < 0 || env_ids_host[k] >= c->N) return fail(c, EXO_EINVAL, "env id out of range");
+    DeviceGuard g(c->device);
+    const int stride = EXO_DRAWS_PER_EPISODE(c->Lmax);
+    int32_t *ids = nullptr;
+    double *dr = nullptr;
+    if (hipMalloc(&ids, n * 4) != hipSuccess || hipMalloc(&dr, (size_t)n * stride * 8) != hipSuccess) {
+        (void)hipFree(ids);
+        return fail(c, EXO_ENOMEM, "exo_reset_from_draws: out of memory");
+    }
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e = hipMemcpyAsync(ids, env_ids_host, n * 4, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(dr, draws_host, (size_t)n * stride * 8, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(exo_reset_kernel, dim3(n), dim3(64), 0, s, c->S, c->U, (const uint8_t *)nullptr, ids, dr,
+                           stride, c->seed, obs_dev);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    (void)hipFree(ids);
+    (void)hipFree(dr);
+    return check(c, e, "exo_reset_from_draws");
+}
+
+int exo_step(exo_ctx *c, const float *act_dev, float *obs_dev, float *rew_dev, uint8_t *done_dev, float *info_dev,
+             const uint8_t *active_dev, void *stream) {
+    if (!c || !act_dev || !obs_dev || !rew_dev || !done_dev) return EXO_EINVAL;
+    DeviceGuard g(c->device);
+    const int threads = 256, lanes = 2 * c->N;
+    hipLaunchKernelGGL(exo_step_kernel, dim3((lanes + threads - 1) / threads), dim3(threads), 0, (hipStream_t)stream,
+                       c->S, c->U, act_dev, obs_dev, rew_dev, done_dev, info_dev, active_dev);
+    return check(c, hipGetLastError(), "exo_step");
+}
+
+int32_t exo_num_envs(const exo_ctx *c) { return c ? c->N : 0; }
+
+int exo_episode_length(const exo_ctx *c, int32_t env, int32_t *L_out) {
+    if (!c || env < 0 || env >= c->N || !L_out) return EXO_EINVAL;
+    *L_out = c->L_host[env];
+    return EXO_OK;
+}
+
+int exo_tremor_host(exo_ctx *c, int32_t env, double *out) {
+    if (!c || env < 0 || env >= c->N || !out) return EXO_EINVAL;
+    DeviceGuard g(c->device);
+    const int L = c->L_host[env];
+    int rc = check(c, hipDeviceSynchronize(), "sync");
+    // strided gather: [t][axis][env]
+    std::vector<double> col((size_t)L * 7);
+    for (int t = 0; t < L && rc == EXO_OK; ++t)
+        for (int i = 0; i < 7 && rc == EXO_OK; ++i) rc = read1(c, (const double *)c->S.tremor, ((size_t)t * 7 + i) * c->N + env, &col[(size_t)i * L + t]);
+    if (rc == EXO_OK) std::memcpy(out, col.data(), col.size() * 8);
+    return rc;
+}
+
+int exo_original_joint_angles_host(exo_ctx *c, int32_t env, double *out7) {
+    // return_original_joint_angles (:580-592): x, y, z, elbow y, elbow z, 0, 0 at counts
+    if (!c || env < 0 || env >= c->N || !out7) return EXO_EINVAL;
+    DeviceGuard g(c->device);
+    int32_t cnt = 0;
+    int rc = read1(c, (const int32_t *)c->S.counts, env, &cnt);
+    if (rc) return rc;
+    const double *imu = c->imu_host.data() + (size_t)c->motion_host[env] * 5 * c->Lmax;
+    const int col[5] = {2, 3, 4, 0, 1};
+    for (int k = 0; k < 5; ++k) out7[k] = imu[col[k] * c->Lmax + cnt];
+    out7[5] = out7[6] = 0.0;
+    return EXO_OK;
+}
+
+int exo_episode_host(exo_ctx *c, int32_t env, double *D49, double *S49, double *Iinv49, double *shift42, double *maxSE2) {
+    if (!c || env < 0 || env >= c->N) return EXO_EINVAL;
+    DeviceGuard g(c->device);
+    int rc = check(c, hipDeviceSynchronize(), "sync");
+    const size_t N = c->N;
+    double dn[NSYM], sn[NSYM], ii[NINV];
+    for (int k = 0; k < NSYM && !rc; ++k) rc = read1(c, (const double *)c->S.dnz, k * N + env, &dn[k]);
+    for (int k = 0; k < NSYM && !rc; ++k) rc = read1(c, (const double *)c->S.snz, k * N + env, &sn[k]);
+    for (int k = 0; k < NINV && !rc; ++k) rc = read1(c, (const double *)c->S.iinv, k * N + env, &ii[k]);
+    if (rc) return rc;
+    if (D49 || S49) {
+        for (int k = 0; k < 49; ++k) { if (D49) D49[k] = 0; if (S49) S49[k] = 0; }
+        for (int k = 0; k < NNZ; ++k) {
+            if (D49) D49[NZ_R[k] * 7 + NZ_C[k]] = dn[NZ_U[k]];
+            if (S49) S49[NZ_R[k] * 7 + NZ_C[k]] = sn[NZ_U[k]];
+        }
+    }
+    if (Iinv49) {
+        for (int k = 0; k < 49; ++k) Iinv49[k] = 0;
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) Iinv49[B1[i] * 7 + B1[j]] = ii[B1U[i][j]];
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j) Iinv49[B2[i] * 7 + B2[j]] = ii[B2U[i][j]];
+    }
+    for (int k = 0; k < 42 && shift42 && !rc; ++k) rc = read1(c, (const double *)c->S.shift, k * N + env, &shift42[k]);
+    for (int k = 0; k < 2 && maxSE2 && !rc; ++k) rc = read1(c, (const double *)c->S.maxSE, k * N + env, &maxSE2[k]);
+    return rc;
+}
+
+int exo_get_state_host(exo_ctx *c, int32_t env, double *out) {
+    if (!c || env < 0 || env >= c->N || !out) return EXO_EINVAL;
+    DeviceGuard g(c->device);
+    int rc = check(c, hipDeviceSynchronize(), "sync");
+    const size_t N = c->N;
+    int32_t cnt = 0;
+    uint32_t ep = 0;
+    if (!rc) rc = read1(c, (const int32_t *)c->S.counts, env, &cnt);
+    if (!rc) rc = read1(c, (const uint32_t *)c->S.episode, env, &ep);
+    out[0] = cnt;
+    for (int j = 0; j < 5 && !rc; ++j) rc = read1(c, (const double *)c->S.phys_q, j * N + env, &out[1 + j]);
+    for (int j = 0; j < 6 && !rc; ++j) rc = read1(c, (const double *)c->S.ref, j * N + env, &out[6 + j]);
+    for (int j = 0; j < 21 && !rc; ++j) {
+        float v = 0;
+        rc = read1(c, (const float *)c->S.posv, j * N + env, &v);
+        out[12 + j] = v;
+    }
+    for (int j = 0; j < 7 && !rc; ++j) rc = read1(c, (const double *)c->S.prev_a, j * N + env, &out[33 + j]);
+    for (int j = 0; j < 7 && !rc; ++j) rc = read1(c, (const double *)c->S.prev2_a, j * N + env, &out[40 + j]);
+    for (int j = 0; j < 2 && !rc; ++j) rc = read1(c, (const double *)c->S.maxSE, j * N + env, &out[47 + j]);
+    int32_t viol = 0;
+    if (!rc) rc = read1(c, (const int32_t *)c->S.viol, env, &viol);
+    out[49] = ep;
+    out[50] = c->L_host[env];
+    out[51] = c->motion_host[env];
+    out[52] = viol;
+    return rc;
+}
+
+int exo_set_state_host(exo_ctx *c, int32_t env, const double *in) {
+    if (!c || env < 0 || env >= c->N || !in) return EXO_EINVAL;
+    DeviceGuard g(c->device);
+    int rc = check(c, hipDeviceSynchronize(), "sync");
+    const size_t N = c->N;
+    if (!rc) rc = write1(c, c->S.counts, env, (int32_t)in[0]);
+    if (!rc) rc = write1(c, c->S.episode, env, (uint32_t)in[49]);
+    if (!rc) rc = write1(c, c->S.viol, env, (int32_t)in[52]);
+    for (int j = 0; j < 5 && !rc; ++j) rc = write1(c, c->S.phys_q, j * N + env, in[1 + j]);
+    for (int j = 0; j < 6 && !rc; ++j) rc = write1(c, c->S.ref, j * N + env, in[6 + j]);
+    for (int j = 0; j < 21 && !rc; ++j) rc = write1(c, c->S.posv, j * N + env, (float)in[12 + j]);
+    for (int j = 0; j < 7 && !rc; ++j) rc = write1(c, c->S.prev_a, j * N + env, in[33 + j]);
+    for (int j = 0; j < 7 && !rc; ++j) rc = write1(c, c->S.prev2_a, j * N + env, in[40 + j]);
+    for (int j = 0; j < 2 && !rc; ++j) rc = write1(c, c->S.maxSE, j * N + env, in[47 + j]);
+    return rc;
+}
+
+int exo_set_seed(exo_ctx *c, uint64_t seed) {
+    if (!c) return EXO_EINVAL;
+    c->seed = seed;
+    return EXO_OK;
+}
+
+const char *exo_last_error(const exo_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+void exo_destroy(exo_ctx *c) {
+    if (!c) return;
+    {
+        DeviceGuard g(c->device);
+        (void)hipDeviceSynchronize();
+        for (void *p : c->allocs)
+            if (p) (void)hipFree(p);
+    }
+    delete c;
+}
+
+} // extern "C"

@@ -1,0 +1,114 @@
+"""ctypes binding of libexo_amd.so (include/exo_amd.h).
+
+The library is the MI355X product path.  It is loaded AFTER torch so that it
+binds to the HIP runtime torch already loaded (both carry the SONAME
+libamdhip64.so.7), which makes torch streams and device pointers valid in it.
+There is no CPU fallback: if the library is missing or no GPU is present the
+env/replay classes raise.
+"""
+import ctypes
+import os
+import subprocess
+
+import torch  # noqa: F401  (must be imported before the HIP library is loaded)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "_lib", "libexo_amd.so")
+CSRC = os.path.join(PKG_ROOT, "csrc")
+
+EXO_OK = 0
+ERRORS = {-22: "EINVAL", -12: "ENOMEM", -5: "EDEVICE", -34: "ERANGE"}
+
+c_int32, c_double, c_void_p, c_uint64 = ctypes.c_int32, ctypes.c_double, ctypes.c_void_p, ctypes.c_uint64
+P = ctypes.POINTER
+
+
+class ExoEnvConfig(ctypes.Structure):
+    """exo_env_config: the constructor arguments of ExoskeletonEnv_train
+    (Environment/Exoskeleton_env.py:38-48)."""
+    _fields_ = [("motion", c_int32), ("tremor_sequence", c_int32 * 7),
+                ("tremor_amplitude_range", c_double * 2), ("first_harmonics_interval", c_double * 2),
+                ("second_harmonics_interval", c_double * 2), ("max_force_shoulder", c_double),
+                ("max_force_elbow", c_double), ("dr_actuator_end_pos_shift", c_double),
+                ("dr_actuator_range", c_double), ("matrix_noise_fraction", c_double)]
+
+
+EXPORTS = {
+    "exo_create": (c_int32, [P(ExoEnvConfig), c_int32, P(c_double), P(c_int32), c_int32, c_int32, c_uint64, c_int32,
+                             P(c_void_p)]),
+    "exo_reset": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "exo_reset_from_draws": (c_int32, [c_void_p, P(c_int32), c_int32, P(c_double), c_void_p, c_void_p]),
+    "exo_step": (c_int32, [c_void_p] * 8),
+    "exo_num_envs": (c_int32, [c_void_p]),
+    "exo_episode_length": (c_int32, [c_void_p, c_int32, P(c_int32)]),
+    "exo_tremor_host": (c_int32, [c_void_p, c_int32, P(c_double)]),
+    "exo_original_joint_angles_host": (c_int32, [c_void_p, c_int32, P(c_double)]),
+    "exo_episode_host": (c_int32, [c_void_p, c_int32, P(c_double), P(c_double), P(c_double), P(c_double),
+                                   P(c_double)]),
+    "exo_get_state_host": (c_int32, [c_void_p, c_int32, P(c_double)]),
+    "exo_set_state_host": (c_int32, [c_void_p, c_int32, P(c_double)]),
+    "exo_set_seed": (c_int32, [c_void_p, c_uint64]),
+    "exo_last_error": (ctypes.c_char_p, [c_void_p]),
+    "exo_destroy": (None, [c_void_p]),
+    "lap_create": (c_int32, [c_int32, c_int32, c_int32, P(c_void_p)]),
+    "lap_destroy": (None, [c_void_p]),
+    "lap_priorities": (c_void_p, [c_void_p]),
+    "lap_tree_stride": (c_int32, [c_void_p]),
+    "lap_max_priority": (c_void_p, [c_void_p]),
+    "lap_add": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p]),
+    "lap_sample": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
+    "lap_update": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p]),
+    "lap_reset_max": (c_int32, [c_void_p, c_void_p]),
+    "lap_totals": (c_int32, [c_void_p, c_void_p, c_void_p]),
+}
+
+_lib = None
+
+
+def build(force=False):
+    """Compile csrc/*.hip for gfx950 into exo_amd/_lib/libexo_amd.so."""
+    if force:
+        subprocess.run(["make", "-s", "-C", CSRC, "clean"], check=True)
+    subprocess.run(["make", "-s", "-j4", "-C", CSRC], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: build it with `make -C {CSRC}` (hipcc, gfx950)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in EXPORTS.items():
+            fn = getattr(L, name)
+            fn.restype, fn.argtypes = res, args
+        _lib = L
+    return _lib
+
+
+def check(rc, what, ctx=None):
+    if rc != EXO_OK:
+        msg = ""
+        if ctx is not None:
+            m = lib().exo_last_error(ctx)
+            msg = m.decode() if m else ""
+        raise RuntimeError(f"{what} failed: {ERRORS.get(rc, rc)} {msg}")
+
+
+def require_gpu(device):
+    if not torch.cuda.is_available():
+        raise RuntimeError("exo_amd runs on an MI355X (HIP) device; no GPU is visible and there is no CPU fallback")
+    dev = torch.device(device if device is not None else "cuda")
+    if dev.type != "cuda":
+        raise RuntimeError(f"exo_amd tensors live on the GPU, got device {dev}")
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    return dev
+
+
+def stream_ptr(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None

@@ -1,0 +1,223 @@
+"""VecExoskeletonEnv: N exoskeleton envs stepped by one HIP kernel launch.
+
+Host-side mirror of ``ExoskeletonEnv_train`` (Environment/Exoskeleton_env.py:34)
+for many envs at once.  All tensors live on the GPU; step/reset are
+stream-ordered launches on torch's current stream (no host sync).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _native as nat
+from . import motions as motion_data
+
+OBS_DIM, ACT_DIM, INFO_DIM = 80, 7, 40
+STATE_DOUBLES = 53
+
+# Defaults of Simulation/Exoskeleton_agent_train.py:28-44.  The reference env
+# has no default for tremor_amplitude_range (Exoskeleton_env.py:41); [0.95,
+# 1.05] is what both evaluation scripts pass.
+DEFAULTS = dict(tremor_sequence=(0, 1, 0, 1, 0, 0, 0), tremor_amplitude_range=(0.95, 1.05),
+                first_harmonics_interval=(4.0, 6.0), second_harmonics_interval=(8.0, 10.0),
+                max_force_shoulder=40.0, max_force_elbow=20.0, dr_actuator_end_pos_shift=0.02,
+                dr_actuator_range=0.03, matrix_noise_fraction=0.1)
+
+INFO_SLICES = {"actuator_torques": slice(0, 7), "torque_val": slice(7, 14), "ampl_val": slice(14, 21),
+               "tremor_torque_val": slice(21, 28), "tremor_ampl_val": slice(28, 35), "reward_unwanted": 35,
+               "reward_torque": 36, "reward_axis": 37, "reward_control": 38, "reward_smoothness": 39}
+
+
+def draws_per_episode(L):
+    """np.random draws one reset consumes."""
+    return 208 + 8 * int(L)
+
+
+def _per_env(value, n, shape):
+    a = np.asarray(value, dtype=np.float64)
+    if a.shape == shape:
+        return np.broadcast_to(a, (n,) + shape)
+    if a.shape == (n,) + shape:
+        return a
+    raise ValueError(f"expected shape {shape} or {(n,) + shape}, got {a.shape}")
+
+
+class VecExoskeletonEnv:
+    """N independent envs; env i follows motion ``motions[i]`` (default i mod 8).
+
+    Every constructor argument of ExoskeletonEnv_train may be given per env
+    (leading dimension N) for domain-randomisation sweeps.
+    """
+
+    observation_dim, action_dim = OBS_DIM, ACT_DIM
+
+    def __init__(self, n_envs, motions=None, seed=0, device=None, **kwargs):
+        self.device = nat.require_gpu(device)
+        self.n = int(n_envs)
+        unknown = set(kwargs) - set(DEFAULTS)
+        if unknown:
+            raise TypeError(f"unknown env arguments {sorted(unknown)}")
+        p = dict(DEFAULTS, **kwargs)
+        angles, lengths = motion_data.load()
+        n_mot = lengths.size
+        mot = np.arange(self.n) % n_mot if motions is None else np.asarray(motions, dtype=np.int64)
+        if mot.shape != (self.n,) or mot.min() < 0 or mot.max() >= n_mot:
+            raise ValueError("motions must hold one motion index in [0, 8) per env")
+        seq = _per_env(p["tremor_sequence"], self.n, (7,))
+        amp = _per_env(p["tremor_amplitude_range"], self.n, (2,))
+        h1 = _per_env(p["first_harmonics_interval"], self.n, (2,))
+        h2 = _per_env(p["second_harmonics_interval"], self.n, (2,))
+        scal = {k: _per_env(p[k], self.n, ()) for k in ("max_force_shoulder", "max_force_elbow",
+                                                       "dr_actuator_end_pos_shift", "dr_actuator_range",
+                                                       "matrix_noise_fraction")}
+        cfgs = (nat.ExoEnvConfig * self.n)()
+        for i in range(self.n):
+            c = cfgs[i]
+            c.motion = int(mot[i])
+            for j in range(7):
+                c.tremor_sequence[j] = int(seq[i, j])
+            for j in range(2):
+                c.tremor_amplitude_range[j] = amp[i, j]
+                c.first_harmonics_interval[j] = h1[i, j]
+                c.second_harmonics_interval[j] = h2[i, j]
+            for k, v in scal.items():
+                setattr(c, k, float(v[i]))
+        self.motions = mot
+        self.tremor_sequence = np.asarray(seq, dtype=np.int64)
+        self.max_force = (scal["max_force_shoulder"].copy(), scal["max_force_elbow"].copy())
+        self.lengths_host = lengths[mot].astype(np.int64)
+        self._ctx = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            rc = nat.lib().exo_create(cfgs, self.n, angles.ctypes.data_as(nat.P(ctypes.c_double)),
+                                      lengths.ctypes.data_as(nat.P(ctypes.c_int32)), n_mot, angles.shape[2],
+                                      ctypes.c_uint64(int(seed) & (2 ** 64 - 1)), self.device.index,
+                                      ctypes.byref(self._ctx))
+        nat.check(rc, "exo_create")
+        self.max_len = int(angles.shape[2])
+        self.lengths = torch.as_tensor(self.lengths_host, device=self.device)
+        n_axes = self.tremor_sequence.sum(1)
+        self.max_reward = n_axes * 0.5 + 0.9 + 0.05 + 0.05 + 0.5  # Exoskeleton_env.py:167-169
+
+    # ------------------------------------------------------------------ core
+    def _stream(self):
+        return nat.stream_ptr(self.device)
+
+    def reset(self, mask=None, obs_out=None):
+        """initialize_movement for envs with mask[i] (bool/uint8 [N] on device; None = all).
+        Returns the observation tensor [N, 80] (rows of masked-out envs are left untouched
+        when obs_out is given, uninitialised otherwise)."""
+        obs = obs_out if obs_out is not None else torch.empty((self.n, OBS_DIM), dtype=torch.float32,
+                                                               device=self.device)
+        m = None
+        if mask is not None:
+            m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
+            assert m.numel() == self.n
+        self._check_out(obs, (self.n, OBS_DIM), torch.float32)
+        nat.check(nat.lib().exo_reset(self._ctx, nat.ptr(m), nat.ptr(obs), self._stream()), "exo_reset", self._ctx)
+        return obs
+
+    def step(self, actions, active=None, out=None, with_info=True):
+        """One step for every env (Exoskeleton_env.py:368-471).
+
+        actions: float32 [N, 7] device tensor in [-1, 1].  active: optional
+        bool/uint8 [N]; inactive envs and envs already done are skipped and
+        their rows in the outputs are left untouched.  Returns
+        (obs [N,80] f32, reward [N] f32, done [N] bool, info [N,40] f32 or None)."""
+        a = actions
+        if a.dtype != torch.float32 or not a.is_contiguous() or a.device != self.device:
+            a = a.to(device=self.device, dtype=torch.float32).contiguous()
+        assert a.shape == (self.n, ACT_DIM), a.shape
+        if out is None:
+            out = self.new_outputs(with_info)
+        obs, rew, done, info = out
+        act = None
+        if active is not None:
+            act = active.to(device=self.device, dtype=torch.uint8).contiguous()
+        rc = nat.lib().exo_step(self._ctx, nat.ptr(a), nat.ptr(obs), nat.ptr(rew), nat.ptr(done),
+                                nat.ptr(info) if with_info else None, nat.ptr(act), self._stream())
+        nat.check(rc, "exo_step", self._ctx)
+        return obs, rew, done.view(torch.bool), info
+
+    def new_outputs(self, with_info=True):
+        d = self.device
+        return (torch.empty((self.n, OBS_DIM), dtype=torch.float32, device=d),
+                torch.empty((self.n,), dtype=torch.float32, device=d),
+                torch.zeros((self.n,), dtype=torch.uint8, device=d),
+                torch.empty((self.n, INFO_DIM), dtype=torch.float32, device=d) if with_info else None)
+
+    @staticmethod
+    def _check_out(t, shape, dtype):
+        if tuple(t.shape) != shape or t.dtype != dtype or not t.is_contiguous():
+            raise ValueError(f"output buffer must be contiguous {dtype} {shape}")
+
+    # ------------------------------------------------------- parity / debug
+    def reset_from_draws(self, env_ids, draws, obs_out=None):
+        """Reset envs from explicit unit-uniform draw streams (the reference's
+        np.random call order).  draws: list/array of 1-D float64 streams."""
+        ids = np.ascontiguousarray(env_ids, dtype=np.int32)
+        stride = draws_per_episode(self.max_len)
+        buf = np.zeros((ids.size, stride))
+        for k, d in enumerate(draws):
+            d = np.asarray(d, dtype=np.float64)
+            need = draws_per_episode(self.lengths_host[ids[k]])
+            if d.size != need:
+                raise ValueError(f"env {ids[k]} needs {need} draws, got {d.size}")
+            buf[k, :need] = d
+        obs = obs_out if obs_out is not None else torch.empty((self.n, OBS_DIM), dtype=torch.float32,
+                                                               device=self.device)
+        rc = nat.lib().exo_reset_from_draws(self._ctx, ids.ctypes.data_as(nat.P(ctypes.c_int32)), ids.size,
+                                            buf.ctypes.data_as(nat.P(ctypes.c_double)), nat.ptr(obs),
+                                            self._stream())
+        nat.check(rc, "exo_reset_from_draws", self._ctx)
+        return obs
+
+    def tremor(self, env):
+        L = int(self.lengths_host[env])
+        out = np.zeros((7, L))
+        nat.check(nat.lib().exo_tremor_host(self._ctx, env, out.ctypes.data_as(nat.P(ctypes.c_double))),
+                  "exo_tremor_host", self._ctx)
+        return out
+
+    def episode(self, env):
+        """(D, S, I^-1, dummy shift [14,3], (max_output_shoulder, max_output_elbow))"""
+        D, S, Ii, sh, m = np.zeros(49), np.zeros(49), np.zeros(49), np.zeros(42), np.zeros(2)
+        dp = lambda a: a.ctypes.data_as(nat.P(ctypes.c_double))  # noqa: E731
+        nat.check(nat.lib().exo_episode_host(self._ctx, env, dp(D), dp(S), dp(Ii), dp(sh), dp(m)),
+                  "exo_episode_host", self._ctx)
+        return D.reshape(7, 7), S.reshape(7, 7), Ii.reshape(7, 7), sh.reshape(14, 3), m
+
+    def get_state(self, env):
+        out = np.zeros(STATE_DOUBLES)
+        nat.check(nat.lib().exo_get_state_host(self._ctx, env, out.ctypes.data_as(nat.P(ctypes.c_double))),
+                  "exo_get_state_host", self._ctx)
+        return out
+
+    def set_state(self, env, state):
+        st = np.ascontiguousarray(state, dtype=np.float64)
+        assert st.size == STATE_DOUBLES
+        nat.check(nat.lib().exo_set_state_host(self._ctx, env, st.ctypes.data_as(nat.P(ctypes.c_double))),
+                  "exo_set_state_host", self._ctx)
+
+    def original_joint_angles(self, env):
+        out = np.zeros(7)
+        nat.check(nat.lib().exo_original_joint_angles_host(self._ctx, env,
+                                                           out.ctypes.data_as(nat.P(ctypes.c_double))),
+                  "exo_original_joint_angles_host", self._ctx)
+        return out
+
+    def close(self):
+        if getattr(self, "_ctx", None) and self._ctx.value:
+            nat.lib().exo_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def unpack_info(info_row):
+        """info dict of one env from a [40] info row (Exoskeleton_env.py:464-469)."""
+        r = np.asarray(info_row, dtype=np.float64)
+        return {k: (r[s].copy() if isinstance(s, slice) else float(r[s])) for k, s in INFO_SLICES.items()}

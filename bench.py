@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""Benchmark of the hot path named by BASELINE.json: the vectorised exoskeleton
+env step (HIP) + the TD7 update with LAP replay, 4096 envs per MI355X
+(BASELINE.json configs[1]).
+
+One bench "step" (mode train, default) = one vectorised env step of all envs
+(batched actor inference -> exo_step kernel -> LAP replay insert) followed by
+one TD7 train() grad step at batch 8 strata x 128 = 1024 -- the reference's
+ratio of one grad step per episode-round env step
+(Simulation/Exoskeleton_agent_train.py:208 trains round(mean(ep_len)) steps
+per round of max(ep_len) env steps).  Episodes are synchronous like the
+reference script: all envs reset together, done envs idle until the longest
+motion (344 steps) ends.  `value` counts ACTIVE env-steps only.
+
+mode env: the env alone (random actions), for the sim-kernel roofline.
+
+Multi-GPU: one process per GPU (torchrun); envs shard with no exchange,
+TD7 gradients are all-reduced over RCCL (weak scaling).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "a-deep-reinforcement-learning-enabled-soft-exoskeleton-for-parkinson-s-patients_amd")
+sys.path.insert(0, PKG)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+# Algorithmic bytes of one active env-step of exo_step_kernel (DESIGN.md,
+# "exo_step bytes"): every array the step logically reads or writes once.
+STEP_READ_BYTES = {
+    "action f32[7]": 28, "counts/L/motion/seq i32": 16, "max_output_shoulder/elbow f64[2]": 16,
+    "joint positions f64[5]": 40, "cached reference CoMs f64[6]": 48, "dummy shift f64[42]": 336,
+    "tremor rows f64[15] (7 at c, 4 at c-1, 4 at c+1)": 120, "prev/second-prev action f64[14]": 112,
+    "position vectors f32[21]": 84, "config f64[4]": 32, "I^-1 blocks f64[16]": 128, "D, S sym nnz f64[28]": 224,
+}
+STEP_WRITE_BYTES = {
+    "obs f32[80]": 320, "reward f32": 4, "done u8": 1, "info f32[40]": 160, "counts i32": 4,
+    "joint positions f64[5]": 40, "reference CoMs f64[6]": 48, "position vectors f32[21]": 84,
+    "prev/second-prev action f64[14]": 112,
+}
+BYTES_PER_ENV_STEP = sum(STEP_READ_BYTES.values()) + sum(STEP_WRITE_BYTES.values())
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--mode", choices=["train", "env"], default="train")
+    ap.add_argument("--precision", choices=["bf16", "fp32"], default="bf16")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(seconds):
+    """The oracle (plain C, fp64, one core) stepping 8 envs, one per motion, with
+    random actions -- the 'port' CPU baseline.  Bounded by `seconds`."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    from exo_amd import motions
+    angles, lengths = motions.load()
+    O.bench(8, angles, lengths, 2000)  # warm
+    steps, t0 = 0, time.perf_counter()
+    chunk = 20000
+    while time.perf_counter() - t0 < seconds:
+        steps += O.bench(8, angles, lengths, chunk, seed=steps + 1)
+    dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/exo_oracle.c env.step, 8 envs (one per motion), {steps} env-steps in {dt:.1f} s, "
+                      f"random actions, episode-synchronous resets"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    from exo_amd import VecExoskeletonEnv
+
+    N = args.envs
+    env = VecExoskeletonEnv(N, seed=1000 + rank, device=dev)
+    Ls = env.lengths_host
+    round_len = int(Ls.max()) - 3
+    active_per_k = np.array([(Ls - 3 > k).sum() for k in range(round_len)])
+    agent = None
+    if args.mode == "train":
+        from exo_amd.td7 import Agent, Hyperparameters
+        hp = Hyperparameters()
+        agent = Agent(80, 7, 1, env_num=8, hp=hp, device=dev, precision=args.precision, n_envs=N,
+                      process_group=dist.group.WORLD if world > 1 else None)
+    out = env.new_outputs(True)
+    obs = env.reset()
+    strata = torch.as_tensor(env.motions % 8, dtype=torch.int32, device=dev)
+    state = {"k": 0, "obs": obs}
+    ev = []
+
+    def one_step(timed):
+        k = state["k"]
+        if k == round_len:
+            state["obs"] = env.reset()
+            k = 0
+        if agent is None:
+            act = torch.rand((N, 7), device=dev) * 2 - 1
+        else:
+            act = agent.select_action_batch(state["obs"])
+        e0 = e1 = None
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        nobs, rew, done, info = env.step(act, out=out)
+        if timed:
+            e1.record()
+            ev.append((e0, e1))
+        if agent is not None:
+            active = torch.as_tensor(k < Ls - 3, device=dev)
+            agent.replay_buffer.add_batch(state["obs"], act, nobs, rew, done, strata, active)
+            agent.train()
+            state["obs"] = nobs.clone()
+        else:
+            state["obs"] = nobs
+        state["k"] = k + 1
+        return int(active_per_k[k])
+
+    for _ in range(args.warmup):
+        one_step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    env_steps = 0
+    for _ in range(args.steps):
+        env_steps += one_step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    t = torch.tensor([elapsed, float(env_steps)], device=dev, dtype=torch.float64)
+    if world > 1:
+        tmax = t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = t.clone()
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        elapsed, total_env_steps = float(tmax[0]), float(tsum[1])
+    else:
+        total_env_steps = float(env_steps)
+    if rank == 0:
+        active_avg = env_steps / args.steps
+        achieved = BYTES_PER_ENV_STEP * active_avg / (kern_ms * 1e-3) / 1e9
+        res = {
+            "metric": "env steps/sec (batched exo sim) + TD7 grad-steps/sec at 1/2/4/8 MI355X",
+            "value": total_env_steps / elapsed,
+            "unit": "env-steps/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f64" if agent is None else f"f64 sim + {args.precision} TD7",
+            "data": "synthetic: reference motions 0-7 (env i -> motion i mod 8), Philox tremor/DR draws, "
+                    + ("random actions" if agent is None else "random-init TD7 (reference widths 300/320)"),
+            "config": {"workload": "configs[1]: 4096 vectorised exo envs per MI355X"
+                                   + (", TD7 batch 8x128" if agent else ", env only"),
+                       "envs_per_gpu": N, "mode": args.mode, "parallelism": f"env-shard x{world}"
+                       + (" + TD7 DP all-reduce" if agent and world > 1 else "")},
+            "roofline": {"kernel": "exo_step_kernel", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "bytes_per_env_step": BYTES_PER_ENV_STEP, "avg_kernel_ms": kern_ms,
+                         "active_envs_per_launch": active_avg},
+        }
+        if agent is not None:
+            res["grad_steps_per_sec"] = args.steps / elapsed
+        if not args.no_cpu_baseline and world == 1:
+            res["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds)
+        print(json.dumps(res))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

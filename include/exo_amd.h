@@ -1,0 +1,161 @@
+/*
+ * exo_amd.h -- C ABI of the MI355X-native exoskeleton environment and LAP
+ * replay kernels (libexo_amd.so, built for gfx950).
+ *
+ * The reference (TomasDelaney/A-Deep-Reinforcement-Learning-Enabled-Soft-
+ * Exoskeleton-for-Parkinson-s-Patients) is pure Python and has no FFI; the
+ * entry points below are what its Python call sites would bind through
+ * ctypes.  Each one cites the reference interface it replaces (path:line).
+ * INTEGRATION.md shows the ctypes binding.
+ *
+ * Conventions
+ *   - All functions return 0 on success, a negative errno-style code
+ *     otherwise (EXO_E*); nothing throws across the ABI.  exo_last_error()
+ *     returns a message for the last failing call on that context.
+ *   - Buffers named *_dev are DEVICE pointers (e.g. torch tensor data_ptr()).
+ *     Buffers named *_host are host pointers.  `stream` is a hipStream_t
+ *     (NULL = default stream).  Work is stream ordered; only the *_host
+ *     read-back helpers synchronise.
+ *   - One context per device.  Calls on one context are not thread safe.
+ */
+#ifndef EXO_AMD_H
+#define EXO_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EXO_OK 0
+#define EXO_EINVAL (-22)
+#define EXO_ENOMEM (-12)
+#define EXO_EDEVICE (-5)
+#define EXO_ERANGE (-34)
+
+#define EXO_OBS_DIM 80  /* Exoskeleton_env.py:99-111 */
+#define EXO_ACT_DIM 7   /* Exoskeleton_env.py:74 */
+#define EXO_INFO_DIM 40 /* Exoskeleton_env.py:464-469: 5 x [7] + 5 reward terms */
+#define EXO_STATE_DOUBLES 53
+
+/* Number of unit-uniform draws one reset consumes for an episode of length L
+ * (the np.random call order of Exoskeleton_env.py:198-217). */
+#define EXO_DRAWS_PER_EPISODE(L) (208 + 8 * (L))
+
+/* Constructor arguments of ExoskeletonEnv_train.__init__
+ * (Environment/Exoskeleton_env.py:38-48); one per env, so domain-randomisation
+ * sweeps can vary them per env. */
+typedef struct {
+    int32_t motion;                      /* reference_motion_file_num (index into the motion table) */
+    int32_t tremor_sequence[7];          /* 0/1 per joint axis */
+    double tremor_amplitude_range[2];
+    double first_harmonics_interval[2];
+    double second_harmonics_interval[2];
+    double max_force_shoulder;
+    double max_force_elbow;
+    double dr_actuator_end_pos_shift;
+    double dr_actuator_range;
+    double matrix_noise_fraction;
+} exo_env_config;
+
+typedef struct exo_ctx exo_ctx;
+
+/* Replaces ExoskeletonEnv_train.__init__ (Exoskeleton_env.py:38-175) for n_envs
+ * envs at once, including the constructor's initialize_movement() (:172).
+ * motion_angles_host: [n_motions][5][max_len] degrees, columns elbow_y,
+ * elbow_z, shoulder_x, shoulder_y, shoulder_z (read_txt_env.py:109-113).
+ * Draws for every reset come from Philox4x32-10 keyed by (seed, env, episode). */
+int exo_create(const exo_env_config *cfgs_host, int32_t n_envs, const double *motion_angles_host,
+               const int32_t *motion_lengths_host, int32_t n_motions, int32_t max_len, uint64_t seed,
+               int32_t device, exo_ctx **out);
+
+/* Replaces ExoskeletonEnv_train.reset() (Exoskeleton_env.py:473-478 ->
+ * initialize_movement :193-254) for every env whose mask byte is non-zero
+ * (mask_dev NULL = all envs).  Writes the reset observation of those envs. */
+int exo_reset(exo_ctx *ctx, const uint8_t *mask_dev, float *obs_dev, void *stream);
+
+/* Parity hook: reset the listed envs from explicit draw streams instead of
+ * Philox.  draws_host holds n rows of EXO_DRAWS_PER_EPISODE(max_len) doubles;
+ * row k feeds env env_ids_host[k] (only its first 208+8L entries are read). */
+int exo_reset_from_draws(exo_ctx *ctx, const int32_t *env_ids_host, int32_t n, const double *draws_host,
+                         float *obs_dev, void *stream);
+
+/* Replaces ExoskeletonEnv_train.step(action) (Exoskeleton_env.py:368-471) for
+ * all envs.  act_dev [N][7] in [-1,1]; obs_dev [N][80]; rew_dev [N]; done_dev
+ * [N]; info_dev [N][40] or NULL.  Envs whose active byte is 0 (active_dev
+ * non-NULL), or that already reached the end of their motion, are skipped and
+ * their outputs left untouched (the training script steps only envs that are
+ * not done: Exoskeleton_agent_train.py:139-141). */
+int exo_step(exo_ctx *ctx, const float *act_dev, float *obs_dev, float *rew_dev, uint8_t *done_dev,
+             float *info_dev, const uint8_t *active_dev, void *stream);
+
+/* Accessors mirroring return_max_length (:577), return_generated_tremor_data
+ * (:572-575) and return_original_joint_angles (:580-592). */
+int32_t exo_num_envs(const exo_ctx *ctx);
+int exo_episode_length(const exo_ctx *ctx, int32_t env, int32_t *L_out);
+int exo_tremor_host(exo_ctx *ctx, int32_t env, double *tremor_out /* [7][L] */);
+int exo_original_joint_angles_host(exo_ctx *ctx, int32_t env, double *out7);
+
+/* Episode constants of one env: dense D and S (49 each), dense I^-1 (49),
+ * dummy shift (42), max_output_shoulder, max_output_elbow. */
+int exo_episode_host(exo_ctx *ctx, int32_t env, double *D49, double *S49, double *Iinv49, double *shift42,
+                     double *maxSE2);
+
+/* Checkpoint/inspection of one env's carried state (EXO_STATE_DOUBLES doubles):
+ * [0] counts, [1..5] joint positions, [6..11] cached reference positions,
+ * [12..32] position vectors, [33..39] prev action, [40..46] second prev action,
+ * [47] max_output_shoulder, [48] max_output_elbow, [49] episode index, [50] L, [51] motion,
+ * [52] steps that violated the joint ranges of check_movement_boundaries (:594-605). */
+int exo_get_state_host(exo_ctx *ctx, int32_t env, double *out);
+int exo_set_state_host(exo_ctx *ctx, int32_t env, const double *in);
+
+/* Re-key the Philox draw streams of later resets (ExoskeletonEnv_train.seed, :189-191). */
+int exo_set_seed(exo_ctx *ctx, uint64_t seed);
+
+const char *exo_last_error(const exo_ctx *ctx);
+void exo_destroy(exo_ctx *ctx);
+
+/* ------------------------------------------------------------------------
+ * LAP prioritised replay (Agent/TD7_buffer_multi_agent.py:5-120), one
+ * sum tree per stratum (the reference keeps one priority row per env,
+ * :41, and samples batch_size rows from each, :75-85).
+ * ---------------------------------------------------------------------- */
+typedef struct lap_tree lap_tree;
+
+/* capacity = max_size per stratum (:19); the tree holds priorities in fp32. */
+int lap_create(int32_t n_strata, int32_t capacity, int32_t device, lap_tree **out);
+void lap_destroy(lap_tree *t);
+/* Device pointer to the trees ([n_strata][lap_tree_stride] floats; node 1 of
+ * a stratum is its total, leaf i (the reference's self.priority[s, i]) is
+ * node stride/2 + i) and to the global max_priority scalar (fp32). */
+float *lap_priorities(lap_tree *t);
+int32_t lap_tree_stride(const lap_tree *t);
+float *lap_max_priority(lap_tree *t);
+
+/* LAP.add (:49-63) for n items: stratum_dev[n], slot_dev[n]; every item gets
+ * the current max_priority. */
+int lap_add(lap_tree *t, const int32_t *stratum_dev, const int32_t *slot_dev, int32_t n, void *stream);
+
+/* LAP.sample (:65-85): for every stratum s, batch indices
+ * idx = searchsorted_left(cumsum(p[s, :size[s]]), u * sum) for the
+ * per-stratum uniforms u_dev[s][batch].  size_dev[n_strata] (int32).
+ * Writes idx_dev[s][batch] (int32, within-stratum slot). */
+int lap_sample(lap_tree *t, const float *u_dev, const int32_t *size_dev, int32_t batch, int32_t *idx_dev,
+               void *stream);
+
+/* LAP.update_priority (:113-117): p[s, idx[s][b]] = prio[s*batch+b] (the last
+ * occurrence wins for duplicate indices, as the reference's CPU index_put),
+ * then max_priority = max(max_priority, max(prio)). */
+int lap_update(lap_tree *t, const int32_t *idx_dev, const float *prio_dev, int32_t batch, void *stream);
+
+/* LAP.reset_max_priority (:119-120): max_priority = max over all leaves. */
+int lap_reset_max(lap_tree *t, void *stream);
+
+/* Total priority of each stratum (root of its tree) -> out_dev[n_strata]. */
+int lap_totals(lap_tree *t, float *out_dev, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EXO_AMD_H */

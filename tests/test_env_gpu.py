@@ -1,0 +1,184 @@
+"""GPU parity of the HIP environment kernels (exo_reset_kernel / exo_step_kernel)
+against the reference's golden traces and the CPU oracle.
+
+Tolerances: the kernels compute in fp64 like the reference; they differ from it
+only by rounding (I^-1 multiply instead of LU, cos(atan2(y,x)) = x/hypot(x,y),
+FMA contraction, RK45 stages in second-order storage form).  Observations are
+float32 in the reference (Exoskeleton_env.py:568) and must match to 1 ulp-level
+(atol 2e-6 relative to magnitude); rewards (fp32 output of an fp64 value) to
+2e-6 relative; info (fp32 output) to 1e-5 relative / 1e-6 absolute; joint
+positions (fp64 state) to 1e-9 rad; done indices and tremor tables exactly
+(the tremor table is elementwise fp64 arithmetic with the same draws).
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from helpers import env_kwargs, episode_steps, golden_env, model_host, philox_draws
+
+pytestmark = pytest.mark.gpu
+
+
+def _close_obs(a, b):
+    np.testing.assert_allclose(a, b, rtol=2e-6, atol=2e-6)
+
+
+def _batched_golden_env():
+    from exo_amd import VecExoskeletonEnv
+    gold = [golden_env(m) for m in range(8)]
+    kw = {}
+    per = [env_kwargs(d) for d in gold]
+    for k in per[0]:
+        kw[k] = np.stack([np.asarray(p[k], dtype=np.float64) for p in per])
+    env = VecExoskeletonEnv(8, motions=list(range(8)), seed=5, **kw)
+    return env, gold
+
+
+def test_reset_matches_reference_draws():
+    env, gold = _batched_golden_env()
+    for ep in (0, 1):
+        obs = env.reset_from_draws(list(range(8)), [d[f"ep{ep}_draws"] for d in gold]).cpu().numpy()
+        for m, d in enumerate(gold):
+            _close_obs(obs[m], d[f"ep{ep}_obs"])
+            if ep == 1:
+                np.testing.assert_array_equal(env.tremor(m), d["ep1_tremor"])
+                Dm, S, Iinv, sh, mm = env.episode(m)
+                np.testing.assert_array_equal(Dm, d["ep1_D"])
+                np.testing.assert_array_equal(S, d["ep1_S"])
+                np.testing.assert_allclose(Iinv, np.linalg.inv(d["ep1_I"]), rtol=1e-12, atol=1e-9)
+                np.testing.assert_array_equal(sh, d["ep1_shift"])
+                assert mm[0] == d["ep1_maxS"] and mm[1] == d["ep1_maxE"]
+                st = env.get_state(m)
+                assert st[0] == 2 and st[50] == d["L"] and st[51] == m
+
+
+def test_steps_match_reference_traces_with_active_mask():
+    """All 8 motions in one batch; envs whose golden episode is shorter wait
+    (inactive) like the training script's per-env `done` skip."""
+    env, gold = _batched_golden_env()
+    env.reset_from_draws(list(range(8)), [d["ep0_draws"] for d in gold])
+    out = env.new_outputs(True)
+    for ep in (1, 2):
+        env.reset_from_draws(list(range(8)), [d[f"ep{ep}_draws"] for d in gold])
+        idx = [episode_steps(d, ep) for d in gold]
+        nmax = max(i.size for i in idx)
+        for k in range(nmax):
+            act = np.zeros((8, 7), dtype=np.float32)
+            active = np.zeros(8, dtype=bool)
+            for m in range(8):
+                if k < idx[m].size:
+                    act[m] = gold[m]["step_action"][idx[m][k]]
+                    active[m] = True
+            obs, rew, done, info = env.step(torch.as_tensor(act, device=env.device),
+                                            active=torch.as_tensor(active, device=env.device), out=out)
+            obs, rew, done, info = obs.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy(), info.cpu().numpy()
+            for m in np.nonzero(active)[0]:
+                d, j = gold[m], idx[m][k]
+                _close_obs(obs[m], d["step_obs"][j])
+                np.testing.assert_allclose(rew[m], d["step_reward"][j], rtol=2e-6, atol=1e-7)
+                assert bool(done[m]) == bool(d["step_done"][j]), (ep, k, m)
+                np.testing.assert_allclose(info[m], d["step_info"][j], rtol=1e-5, atol=1e-6)
+                st = env.get_state(int(m)) if k % 37 == 0 or k == idx[m].size - 1 else None
+                if st is not None:
+                    np.testing.assert_allclose(st[1:6], d["step_q_after"][j], rtol=0, atol=1e-9)
+                    assert st[0] == d["step_counts"][j]
+        if ep == 1:
+            for m in range(8):
+                assert gold[m]["step_done"][idx[m][-1]]
+                assert idx[m].size == int(gold[m]["L"]) - 3
+
+
+def test_done_envs_are_skipped():
+    from exo_amd import VecExoskeletonEnv
+    env = VecExoskeletonEnv(8, seed=3)
+    env.reset()
+    out = env.new_outputs(True)
+    a = torch.zeros((8, 7), device=env.device)
+    L = env.lengths_host
+    for k in range(int(L.max()) + 5):
+        env.step(a, out=out)
+    st = np.array([env.get_state(m)[0] for m in range(8)])
+    np.testing.assert_array_equal(st, L - 1)
+
+
+def test_philox_path_matches_oracle_at_scale():
+    """4096 envs on Philox draws; a sample of envs is replayed on the oracle
+    with the same draw streams and random actions."""
+    from exo_amd import VecExoskeletonEnv, motions
+    N, seed = 4096, 99
+    env = VecExoskeletonEnv(N, seed=seed)  # episode 0 drawn by the constructor
+    obs0 = env.reset().cpu().numpy()       # episode 1
+    angles, lengths = motions.load()
+    lib = model_host()
+    rng = np.random.default_rng(0)
+    acts = rng.uniform(-1, 1, (12, N, 7)).astype(np.float32)
+    outs = []
+    o = env.new_outputs(True)
+    for k in range(12):
+        ob, r, dn, inf = env.step(torch.as_tensor(acts[k], device=env.device), out=o)
+        outs.append((ob.cpu().numpy().copy(), r.cpu().numpy().copy(), inf.cpu().numpy().copy()))
+    for e in [0, 1, 7, 8, 1023, 2047, 3001, 4095]:
+        m = e % 8
+        L = int(lengths[m])
+        cfg = env_kwargs_default()
+        oe = O.OracleEnv(angles[m][:, :L], cfg["seq"], cfg["amp"], cfg["h1"], cfg["h2"], 40.0, 20.0, 0.02, 0.03, 0.1)
+        oe.reset(philox_draws(L, seed, e, 0, lib))
+        ob = oe.reset(philox_draws(L, seed, e, 1, lib))
+        _close_obs(obs0[e], ob)
+        for k in range(12):
+            ob, r, dn, info, _ = oe.step(acts[k][e].astype(np.float64))
+            _close_obs(outs[k][0][e], ob)
+            np.testing.assert_allclose(outs[k][1][e], r, rtol=2e-6, atol=1e-7)
+            np.testing.assert_allclose(outs[k][2][e], info, rtol=1e-5, atol=1e-6)
+
+
+def env_kwargs_default():
+    return dict(seq=np.array([0, 1, 0, 1, 0, 0, 0], dtype=np.int32), amp=np.array([0.95, 1.05]),
+                h1=np.array([4.0, 6.0]), h2=np.array([8.0, 10.0]))
+
+
+def test_state_roundtrip_and_reset_mask():
+    from exo_amd import VecExoskeletonEnv
+    env = VecExoskeletonEnv(16, seed=11)
+    env.reset()
+    a = torch.full((16, 7), 0.3, device=env.device)
+    for _ in range(5):
+        env.step(a)
+    st = env.get_state(3)
+    env.set_state(3, st)
+    np.testing.assert_array_equal(env.get_state(3), st)
+    mask = torch.zeros(16, dtype=torch.bool, device=env.device)
+    mask[3] = True
+    env.reset(mask=mask)
+    assert env.get_state(3)[0] == 2 and env.get_state(4)[0] == 7
+    assert env.get_state(3)[49] == st[49] + 1  # episode counter advanced only for env 3
+
+
+def test_drop_in_single_env_api():
+    import Environment.Exoskeleton_env as E
+    np.random.seed(0)
+    env = E.ExoskeletonEnv_train(reference_motion_file_num="2", tremor_sequence=np.array([0, 1, 0, 1, 0, 0, 0]),
+                                 tremor_amplitude_range=np.array([0.95, 1.05]),
+                                 first_harmonics_interval=np.array([4, 6]),
+                                 second_harmonics_interval=np.array([8, 10]), max_force_shoulder=40,
+                                 max_force_elbow=20)
+    assert env.observation_space.shape == (80,) and env.action_space.shape == (7,)
+    obs, score = env.reset()
+    assert obs.shape == (80,) and obs.dtype == np.float32 and score == 2
+    n = 0
+    done = False
+    while not done:
+        obs, r, done, trunc, info = env.step(np.random.uniform(-1, 1, 7))
+        n += 1
+        assert isinstance(r, float) and trunc is False
+        assert set(info) == {"actuator_torques", "torque_val", "ampl_val", "tremor_torque_val", "tremor_ampl_val",
+                             "reward_unwanted", "reward_torque", "reward_axis", "reward_control",
+                             "reward_smoothness"}
+    assert n == env.return_max_length() - 3
+    with pytest.raises(IndexError):
+        env.step(np.zeros(7))
+    seq, mx = env.return_generated_tremor_data()
+    assert mx.shape == (7,) and mx[1] > 0 and mx[0] == 0
+    assert len(env.return_original_joint_angles()) == 7
+    env.close()
