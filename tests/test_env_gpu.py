@@ -32,6 +32,15 @@ def _batched_golden_env():
     for k in per[0]:
         kw[k] = np.stack([np.asarray(p[k], dtype=np.float64) for p in per])
     env = VecExoskeletonEnv(8, motions=list(range(8)), seed=5, **kw)
+    # exo_create already ran the constructor's initialize_movement on Philox
+    # draws; the goldens' episode 0 IS that constructor call, whose link-read
+    # cache is still all zeros (Exoskeleton_sim_pybullet.py:80-81).  Restore
+    # the freshly-loaded state so reset_from_draws(ep0) replays it.
+    for m in range(8):
+        st = env.get_state(m)
+        st[6:12] = 0.0
+        st[49] = 0
+        env.set_state(m, st)
     return env, gold
 
 
