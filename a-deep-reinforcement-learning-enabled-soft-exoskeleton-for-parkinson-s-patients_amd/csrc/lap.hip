@@ -5,7 +5,8 @@
 // batch_size indices from every row with torch.cumsum + torch.searchsorted
 // (:75-78): O(size) work and a host sync per row per training step.  Here
 // every stratum owns a complete binary tree over `cap` (power of two) leaves,
-// tree[s][1] is the row total and leaf i lives at tree[s][cap + i]:
+// tree[s][1] is the row total and leaf i lives at tree[s][cap + i].  The
+// caller owns the memory (torch tensors) and describes it with lap_tree_desc:
 //   sample : one lane per draw descends log2(cap) levels,
 //   update : leaves are written (last duplicate wins, like the reference's CPU
 //            index_put at :115), then the touched ancestors are recomputed
@@ -19,13 +20,6 @@
 #include <string>
 
 #include "exo_amd.h"
-
-struct lap_tree {
-    int device = 0;
-    int n_strata = 0, capacity = 0, cap = 0, levels = 0; // cap = 2^levels >= capacity
-    float *tree = nullptr;                               // [n_strata][2 * cap]
-    float *maxp = nullptr;                               // [1]
-};
 
 namespace {
 
@@ -149,99 +143,71 @@ __global__ void lap_totals_kernel(const float *tree, int cap, int n_strata, floa
 
 __global__ void lap_init_kernel(float *maxp) { *maxp = 1.0f; } // max_priority = 1 (:42)
 
-struct DeviceGuard {
-    int prev = -1;
-    explicit DeviceGuard(int dev) {
-        if (hipGetDevice(&prev) == hipSuccess && prev != dev) (void)hipSetDevice(dev);
-        else prev = -1;
-    }
-    ~DeviceGuard() {
-        if (prev >= 0) (void)hipSetDevice(prev);
-    }
-};
-
 int rc(hipError_t e) { return e == hipSuccess ? EXO_OK : EXO_EDEVICE; }
+
+int levels_of(const lap_tree_desc *t) {
+    int lv = 0;
+    while ((1 << lv) < t->cap) ++lv;
+    return lv;
+}
+
+bool valid(const lap_tree_desc *t) {
+    return t && t->tree && t->max_priority && t->n_strata > 0 && t->capacity > 0 && t->cap >= t->capacity &&
+           (t->cap & (t->cap - 1)) == 0;
+}
 
 } // namespace
 
 extern "C" {
 
-int lap_create(int32_t n_strata, int32_t capacity, int32_t device, lap_tree **out) {
-    if (!out || n_strata <= 0 || capacity <= 0 || capacity > (1 << 26)) return EXO_EINVAL;
-    *out = nullptr;
-    lap_tree *t = new lap_tree();
-    t->device = device;
-    t->n_strata = n_strata;
-    t->capacity = capacity;
-    t->cap = 1;
-    while (t->cap < capacity) { t->cap <<= 1; t->levels++; }
-    DeviceGuard g(device);
-    const size_t bytes = (size_t)n_strata * 2 * t->cap * sizeof(float);
-    if (hipMalloc(&t->tree, bytes) != hipSuccess || hipMalloc(&t->maxp, sizeof(float)) != hipSuccess) {
-        lap_destroy(t);
-        return EXO_ENOMEM;
-    }
-    hipError_t e = hipMemset(t->tree, 0, bytes);
-    if (e == hipSuccess) {
-        hipLaunchKernelGGL(lap_init_kernel, dim3(1), dim3(1), 0, nullptr, t->maxp);
-        e = hipDeviceSynchronize();
-    }
-    if (e != hipSuccess) { lap_destroy(t); return EXO_EDEVICE; }
-    *out = t;
-    return EXO_OK;
+int32_t lap_tree_floats(int32_t n_strata, int32_t capacity) {
+    int cap = 1;
+    while (cap < capacity) cap <<= 1;
+    return n_strata * 2 * cap;
 }
 
-void lap_destroy(lap_tree *t) {
-    if (!t) return;
-    DeviceGuard g(t->device);
-    if (t->tree) (void)hipFree(t->tree);
-    if (t->maxp) (void)hipFree(t->maxp);
-    delete t;
-}
-
-float *lap_priorities(lap_tree *t) { return t ? t->tree : nullptr; }
-int32_t lap_tree_stride(const lap_tree *t) { return t ? 2 * t->cap : 0; }
-float *lap_max_priority(lap_tree *t) { return t ? t->maxp : nullptr; }
-
-int lap_add(lap_tree *t, const int32_t *stratum, const int32_t *slot, int32_t n, void *stream) {
-    if (!t || !stratum || !slot || n < 0) return EXO_EINVAL;
-    if (n == 0) return EXO_OK;
-    DeviceGuard g(t->device);
-    hipLaunchKernelGGL(lap_add_kernel, dim3(t->n_strata), dim3(UPD_THREADS), 0, (hipStream_t)stream,
-                       t->tree, t->maxp, t->cap, t->levels, t->capacity, stratum, slot, n);
+int lap_init(const lap_tree_desc *t, void *stream) {
+    if (!valid(t)) return EXO_EINVAL;
+    hipError_t e = hipMemsetAsync(t->tree, 0, (size_t)t->n_strata * 2 * t->cap * sizeof(float), (hipStream_t)stream);
+    if (e != hipSuccess) return EXO_EDEVICE;
+    hipLaunchKernelGGL(lap_init_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, t->max_priority);
     return rc(hipGetLastError());
 }
 
-int lap_sample(lap_tree *t, const float *u, const int32_t *size, int32_t batch, int32_t *idx, void *stream) {
-    if (!t || !u || !size || !idx || batch <= 0) return EXO_EINVAL;
-    DeviceGuard g(t->device);
+int lap_add(const lap_tree_desc *t, const int32_t *stratum, const int32_t *slot, int32_t n, void *stream) {
+    if (!valid(t) || !stratum || !slot || n < 0) return EXO_EINVAL;
+    if (n == 0) return EXO_OK;
+    hipLaunchKernelGGL(lap_add_kernel, dim3(t->n_strata), dim3(UPD_THREADS), 0, (hipStream_t)stream, t->tree,
+                       t->max_priority, t->cap, levels_of(t), t->capacity, stratum, slot, n);
+    return rc(hipGetLastError());
+}
+
+int lap_sample(const lap_tree_desc *t, const float *u, const int32_t *size, int32_t batch, int32_t *idx, void *stream) {
+    if (!valid(t) || !u || !size || !idx || batch <= 0) return EXO_EINVAL;
     const int th = 128;
     hipLaunchKernelGGL(lap_sample_kernel, dim3((batch + th - 1) / th, t->n_strata), dim3(th), 0, (hipStream_t)stream,
-                       t->tree, t->cap, t->levels, u, size, batch, idx);
+                       t->tree, t->cap, levels_of(t), u, size, batch, idx);
     return rc(hipGetLastError());
 }
 
-int lap_update(lap_tree *t, const int32_t *idx, const float *prio, int32_t batch, void *stream) {
-    if (!t || !idx || !prio || batch <= 0) return EXO_EINVAL;
-    DeviceGuard g(t->device);
+int lap_update(const lap_tree_desc *t, const int32_t *idx, const float *prio, int32_t batch, void *stream) {
+    if (!valid(t) || !idx || !prio || batch <= 0) return EXO_EINVAL;
     hipLaunchKernelGGL(lap_update_kernel, dim3(t->n_strata), dim3(UPD_THREADS), 0, (hipStream_t)stream, t->tree,
-                       t->maxp, t->cap, t->levels, idx, prio, batch);
+                       t->max_priority, t->cap, levels_of(t), idx, prio, batch);
     return rc(hipGetLastError());
 }
 
-int lap_reset_max(lap_tree *t, void *stream) {
-    if (!t) return EXO_EINVAL;
-    DeviceGuard g(t->device);
-    hipError_t e = hipMemsetAsync(t->maxp, 0, sizeof(float), (hipStream_t)stream);
+int lap_reset_max(const lap_tree_desc *t, void *stream) {
+    if (!valid(t)) return EXO_EINVAL;
+    hipError_t e = hipMemsetAsync(t->max_priority, 0, sizeof(float), (hipStream_t)stream);
     if (e != hipSuccess) return EXO_EDEVICE;
-    hipLaunchKernelGGL(lap_reset_max_kernel, dim3(256), dim3(1024), 0, (hipStream_t)stream, t->tree, t->maxp, t->cap,
-                       t->n_strata);
+    hipLaunchKernelGGL(lap_reset_max_kernel, dim3(256), dim3(1024), 0, (hipStream_t)stream, t->tree, t->max_priority,
+                       t->cap, t->n_strata);
     return rc(hipGetLastError());
 }
 
-int lap_totals(lap_tree *t, float *out, void *stream) {
-    if (!t || !out) return EXO_EINVAL;
-    DeviceGuard g(t->device);
+int lap_totals(const lap_tree_desc *t, float *out, void *stream) {
+    if (!valid(t) || !out) return EXO_EINVAL;
     hipLaunchKernelGGL(lap_totals_kernel, dim3((t->n_strata + 63) / 64), dim3(64), 0, (hipStream_t)stream, t->tree,
                        t->cap, t->n_strata, out);
     return rc(hipGetLastError());

@@ -24,6 +24,11 @@ c_int32, c_double, c_void_p, c_uint64 = ctypes.c_int32, ctypes.c_double, ctypes.
 P = ctypes.POINTER
 
 
+class LapTreeDesc(ctypes.Structure):
+    _fields_ = [("tree", c_void_p), ("max_priority", c_void_p), ("n_strata", c_int32), ("capacity", c_int32),
+                ("cap", c_int32)]
+
+
 class ExoEnvConfig(ctypes.Structure):
     """exo_env_config: the constructor arguments of ExoskeletonEnv_train
     (Environment/Exoskeleton_env.py:38-48)."""
@@ -51,11 +56,8 @@ EXPORTS = {
     "exo_set_seed": (c_int32, [c_void_p, c_uint64]),
     "exo_last_error": (ctypes.c_char_p, [c_void_p]),
     "exo_destroy": (None, [c_void_p]),
-    "lap_create": (c_int32, [c_int32, c_int32, c_int32, P(c_void_p)]),
-    "lap_destroy": (None, [c_void_p]),
-    "lap_priorities": (c_void_p, [c_void_p]),
-    "lap_tree_stride": (c_int32, [c_void_p]),
-    "lap_max_priority": (c_void_p, [c_void_p]),
+    "lap_tree_floats": (c_int32, [c_int32, c_int32]),
+    "lap_init": (c_int32, [c_void_p, c_void_p]),
     "lap_add": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p]),
     "lap_sample": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "lap_update": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p]),

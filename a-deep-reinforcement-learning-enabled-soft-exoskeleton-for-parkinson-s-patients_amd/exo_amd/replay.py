@@ -1,0 +1,169 @@
+"""LAP prioritised replay on the GPU (reference: Agent/TD7_buffer_multi_agent.py).
+
+Storage is fp32 on the device ([strata, max_size + 1, dim]; the extra row per
+stratum absorbs writes of inactive envs so batched inserts need no host sync),
+priorities are per-stratum sum trees updated and sampled by the HIP kernels in
+csrc/lap.hip.  The reference stores float64 numpy arrays and converts every
+sampled batch to float32 on the way to the device (:105-111); storing float32
+gives the same training inputs.
+
+Two insert paths:
+* add(...)       -- one transition, the reference's exact pointer semantics
+                    (ptr advances when count % num_envs == 0 BEFORE count is
+                    incremented, :59-63);
+* add_batch(...) -- one vectorised env step: a ring per stratum, one slot per
+                    active env-step (documented divergence).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _native as nat
+
+
+class LAP:
+    def __init__(self, state_dim, action_dim, device, num_envs, max_size=1e6, batch_size=64, max_action=1,
+                 normalize_actions=True, prioritized=True):
+        if not prioritized:
+            raise NotImplementedError("only the prioritized LAP buffer of the TD7 agent is implemented")
+        self.device = nat.require_gpu(device)
+        self.max_size = int(max_size)
+        self.max_action = max_action
+        self.batch_size = int(batch_size)
+        self.num_envs = int(num_envs)
+        self.state_dim, self.action_dim = state_dim, action_dim
+        self.normalize_actions = max_action if normalize_actions else 1
+        self.prioritized = True
+        E, C = self.num_envs, self.max_size
+        f32 = dict(device=self.device, dtype=torch.float32)
+        self.state = torch.zeros((E, C + 1, state_dim), **f32)
+        self.action = torch.zeros((E, C + 1, action_dim), **f32)
+        self.next_state = torch.zeros((E, C + 1, state_dim), **f32)
+        self.reward = torch.zeros((E, C + 1, 1), **f32)
+        self.not_done = torch.zeros((E, C + 1, 1), **f32)
+        cap = 1
+        while cap < C:
+            cap <<= 1
+        self._tree = torch.zeros((E, 2 * cap), **f32)
+        self._maxp = torch.ones((1,), **f32)
+        self._desc = nat.LapTreeDesc(self._tree.data_ptr(), self._maxp.data_ptr(), E, C, cap)
+        self._cap = cap
+        # reference pointer semantics (single add)
+        self.ptr = 0
+        self.count = 0
+        self.size = 0
+        # per-stratum rings (batched add), device-resident
+        i32 = dict(device=self.device, dtype=torch.int32)
+        self.ptr_s = torch.zeros((E,), **i32)
+        self.size_s = torch.zeros((E,), **i32)
+        self._row0 = (torch.arange(E, device=self.device, dtype=torch.int64) * (C + 1))
+        self.ind = None
+        self._u = torch.empty((E, self.batch_size), **f32)
+        self._idx = torch.empty((E, self.batch_size), **i32)
+        self._init_tree()
+
+    def _stream(self):
+        return nat.stream_ptr(self.device)
+
+    def _init_tree(self):
+        nat.check(nat.lib().lap_init(ctypes.byref(self._desc), self._stream()), "lap_init")
+
+    # --------------------------------------------------------------- views
+    @property
+    def priority(self):
+        """[E, max_size] view of the tree leaves (the reference's self.priority)."""
+        return self._tree[:, self._cap:self._cap + self.max_size]
+
+    @property
+    def max_priority(self):
+        return float(self._maxp)
+
+    @property
+    def totals(self):
+        return self._tree[:, 1]
+
+    # ---------------------------------------------------------------- adds
+    def add(self, state, action, next_state, reward, done, tremor_num):
+        """Agent/TD7_buffer_multi_agent.py:49-63."""
+        s, p = int(tremor_num), self.ptr
+        dev = self.device
+        self.state[s, p] = torch.as_tensor(np.asarray(state, dtype=np.float32), device=dev)
+        self.action[s, p] = torch.as_tensor(np.asarray(action, dtype=np.float32) / self.normalize_actions, device=dev)
+        self.next_state[s, p] = torch.as_tensor(np.asarray(next_state, dtype=np.float32), device=dev)
+        self.reward[s, p] = float(reward)
+        self.not_done[s, p] = 1.0 - float(done)
+        st = torch.tensor([s], dtype=torch.int32, device=dev)
+        sl = torch.tensor([p], dtype=torch.int32, device=dev)
+        nat.check(nat.lib().lap_add(ctypes.byref(self._desc), nat.ptr(st), nat.ptr(sl), 1, self._stream()), "lap_add")
+        if self.count % self.num_envs == 0:
+            self.ptr = (self.ptr + 1) % self.max_size
+            self.size = min(self.size + 1, self.max_size)
+        self.count += 1
+        self.size_s.fill_(self.size)
+
+    def add_batch(self, state, action, next_state, reward, done, strata, active=None):
+        """One vectorised env step: row i goes to stratum strata[i] (int32 [N]) if
+        active[i] (bool [N], default all).  No host synchronisation."""
+        E, C = self.num_envs, self.max_size
+        n = state.shape[0]
+        strata = strata.to(torch.int64)
+        act = torch.ones((n,), dtype=torch.int64, device=self.device) if active is None else active.to(torch.int64)
+        onehot = torch.nn.functional.one_hot(strata, E) * act[:, None]          # [N, E]
+        rank = (torch.cumsum(onehot, 0) - onehot)[torch.arange(n, device=self.device), strata]
+        slot = (self.ptr_s.to(torch.int64)[strata] + rank) % C
+        slot = torch.where(act > 0, slot, torch.full_like(slot, C))              # inactive -> trash row
+        rows = self._row0[strata] + slot
+        self.state.view(-1, self.state_dim).index_copy_(0, rows, state.to(torch.float32))
+        self.action.view(-1, self.action_dim).index_copy_(0, rows, action.to(torch.float32) / self.normalize_actions)
+        self.next_state.view(-1, self.state_dim).index_copy_(0, rows, next_state.to(torch.float32))
+        self.reward.view(-1, 1).index_copy_(0, rows, reward.to(torch.float32).view(-1, 1))
+        self.not_done.view(-1, 1).index_copy_(0, rows, 1.0 - done.to(torch.float32).view(-1, 1))
+        cnt = onehot.sum(0)
+        lap_slot = torch.where(act > 0, slot, torch.full_like(slot, -1)).to(torch.int32)
+        st32 = strata.to(torch.int32)
+        nat.check(nat.lib().lap_add(ctypes.byref(self._desc), nat.ptr(st32), nat.ptr(lap_slot), n, self._stream()),
+                  "lap_add")
+        self.ptr_s.copy_(((self.ptr_s.to(torch.int64) + cnt) % C).to(torch.int32))
+        self.size_s.copy_(torch.clamp(self.size_s.to(torch.int64) + cnt, max=C).to(torch.int32))
+
+    # ------------------------------------------------------------- sample
+    def sample(self):
+        """Agent/TD7_buffer_multi_agent.py:65-111: batch_size rows from every
+        stratum, stratum-major, as float32 device tensors."""
+        self._u.uniform_()
+        nat.check(nat.lib().lap_sample(ctypes.byref(self._desc), nat.ptr(self._u), nat.ptr(self.size_s),
+                                       self.batch_size, nat.ptr(self._idx), self._stream()), "lap_sample")
+        self.ind = self._idx
+        rows = (self._row0[:, None] + self._idx.to(torch.int64)).reshape(-1)
+        return (self.state.view(-1, self.state_dim)[rows], self.action.view(-1, self.action_dim)[rows],
+                self.next_state.view(-1, self.state_dim)[rows], self.reward.view(-1, 1)[rows],
+                self.not_done.view(-1, 1)[rows])
+
+    def sample_indices(self, u):
+        """Indices for given uniforms u [E, batch] (parity hook)."""
+        u = u.to(device=self.device, dtype=torch.float32).contiguous()
+        idx = torch.empty(u.shape, dtype=torch.int32, device=self.device)
+        nat.check(nat.lib().lap_sample(ctypes.byref(self._desc), nat.ptr(u), nat.ptr(self.size_s), u.shape[1],
+                                       nat.ptr(idx), self._stream()), "lap_sample")
+        return idx
+
+    def update_priority(self, priority, ind=None):
+        """:113-117 (max_priority stays on the device)."""
+        ind = self.ind if ind is None else ind
+        pr = priority.detach().to(torch.float32).reshape(-1).contiguous()
+        assert pr.numel() == ind.numel()
+        nat.check(nat.lib().lap_update(ctypes.byref(self._desc), nat.ptr(ind), nat.ptr(pr), ind.shape[1],
+                                       self._stream()), "lap_update")
+
+    def reset_max_priority(self):
+        nat.check(nat.lib().lap_reset_max(ctypes.byref(self._desc), self._stream()), "lap_reset_max")
+
+    def reset_buffer(self):
+        """:122-139"""
+        self.ptr = self.count = self.size = 0
+        for t in (self.state, self.action, self.next_state, self.reward, self.not_done):
+            t.zero_()
+        self.ptr_s.zero_()
+        self.size_s.zero_()
+        self._init_tree()

@@ -1,0 +1,483 @@
+"""TD7 (SALE encoder, twin critic, actor, LAP) on PyTorch-ROCm.
+
+Mirrors Agent/TD7_multi_agent.py (nets, losses, schedules, checkpoint policy,
+save/load suffixes) with three MI355X-first changes:
+
+* no host synchronisation inside train(): the running Q-target bounds
+  (:245-246) and max_priority live in device tensors, the target policy noise
+  scale is a device scalar, and LAP sampling/priority updates are HIP sum-tree
+  kernels (exo_amd.replay.LAP, csrc/lap.hip);
+* optional bf16 autocast of the MLPs (BASELINE.json configs[1]: "TD7 bf16");
+  losses, optimiser state and master weights stay fp32;
+* data-parallel training: gradients of encoder/critic/actor are flattened into
+  one bucket per update and all-reduced over RCCL; the scalar bounds are
+  MAX-reduced.
+
+The update math lives in TD7Learner, which is device-agnostic torch code (the
+CPU parity tests run it against the reference's golden train() steps); Agent
+adds the replay buffer, the checkpoint policy and data parallelism.
+"""
+import copy
+from dataclasses import dataclass, field
+from typing import Callable
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+@dataclass
+class Hyperparameters:
+    # Generic (Agent/TD7_multi_agent.py:10-50)
+    batch_size: int = 128
+    buffer_size: int = 2.5e5
+    discount: float = 0.99
+    target_update_rate: int = 250
+    exploration_noise: float = 0.1
+    # TD3
+    target_policy_noise: float = 0.2
+    noise_clip: float = 0.5
+    policy_freq: int = 2
+    # LAP
+    alpha: float = 0.4
+    min_priority: float = 1
+    # TD3+BC
+    lmbda: float = 0.1
+    # Checkpointing
+    max_eps_when_checkpointing: int = 20
+    steps_before_checkpointing: int = 75e4
+    reset_weight: float = 0.9
+    # Encoder Model
+    zs_dim: int = 300
+    enc_hdim: int = 300
+    enc_activ: Callable = field(default=F.elu)
+    encoder_lr: float = 3e-4
+    # Critic Model
+    critic_hdim: int = 320
+    critic_activ: Callable = field(default=F.elu)
+    critic_lr: float = 3e-4
+    # Actor Model
+    actor_hdim: int = 320
+    actor_activ: Callable = field(default=F.relu)
+    actor_lr: float = 3e-4
+    # Pink noise (Agent/TD7_multi_agent_Pink_noise.py:21-24)
+    beta: float = 1
+    noise_scale: float = 0.3
+
+
+def AvgL1Norm(x, eps=1e-8):
+    return x / x.abs().mean(-1, keepdim=True).clamp(min=eps)
+
+
+def LAP_huber(x, min_priority=1):
+    return torch.where(x < min_priority, 0.5 * x.pow(2), min_priority * x).sum(1).mean()
+
+
+class Actor(nn.Module):
+    """Agent/TD7_multi_agent.py:61-77 (same parameter names: state_dicts interchange)."""
+
+    def __init__(self, state_dim, action_dim, zs_dim=286, hdim=286, activ=F.relu):
+        super().__init__()
+        self.activ = activ
+        self.l0 = nn.Linear(state_dim, hdim)
+        self.l1 = nn.Linear(zs_dim + hdim, hdim)
+        self.l2 = nn.Linear(hdim, hdim)
+        self.l3 = nn.Linear(hdim, action_dim)
+
+    def forward(self, state, zs):
+        a = AvgL1Norm(self.l0(state))
+        a = torch.cat([a, zs], 1)
+        a = self.activ(self.l1(a))
+        a = self.activ(self.l2(a))
+        return torch.tanh(self.l3(a))
+
+
+class Encoder(nn.Module):
+    """Agent/TD7_multi_agent.py:80-106"""
+
+    def __init__(self, state_dim, action_dim, zs_dim=286, hdim=286, activ=F.elu):
+        super().__init__()
+        self.activ = activ
+        self.zs1 = nn.Linear(state_dim, hdim)
+        self.zs2 = nn.Linear(hdim, hdim)
+        self.zs3 = nn.Linear(hdim, zs_dim)
+        self.zsa1 = nn.Linear(zs_dim + action_dim, hdim)
+        self.zsa2 = nn.Linear(hdim, hdim)
+        self.zsa3 = nn.Linear(hdim, zs_dim)
+
+    def zs(self, state):
+        zs = self.activ(self.zs1(state))
+        zs = self.activ(self.zs2(zs))
+        return AvgL1Norm(self.zs3(zs))
+
+    def zsa(self, zs, action):
+        zsa = self.activ(self.zsa1(torch.cat([zs, action], 1)))
+        zsa = self.activ(self.zsa2(zsa))
+        return self.zsa3(zsa)
+
+
+class Critic(nn.Module):
+    """Agent/TD7_multi_agent.py:109-140"""
+
+    def __init__(self, state_dim, action_dim, zs_dim=286, hdim=286, activ=F.elu):
+        super().__init__()
+        self.activ = activ
+        self.q01 = nn.Linear(state_dim + action_dim, hdim)
+        self.q1 = nn.Linear(2 * zs_dim + hdim, hdim)
+        self.q2 = nn.Linear(hdim, hdim)
+        self.q3 = nn.Linear(hdim, 1)
+        self.q02 = nn.Linear(state_dim + action_dim, hdim)
+        self.q4 = nn.Linear(2 * zs_dim + hdim, hdim)
+        self.q5 = nn.Linear(hdim, hdim)
+        self.q6 = nn.Linear(hdim, 1)
+
+    def forward(self, state, action, zsa, zs):
+        sa = torch.cat([state, action], 1)
+        embeddings = torch.cat([zsa, zs], 1)
+        q1 = AvgL1Norm(self.q01(sa))
+        q1 = torch.cat([q1, embeddings], 1)
+        q1 = self.activ(self.q1(q1))
+        q1 = self.activ(self.q2(q1))
+        q1 = self.q3(q1)
+        q2 = AvgL1Norm(self.q02(sa))
+        q2 = torch.cat([q2, embeddings], 1)
+        q2 = self.activ(self.q4(q2))
+        q2 = self.activ(self.q5(q2))
+        q2 = self.q6(q2)
+        return torch.cat([q1, q2], 1)
+
+
+class GradSync:
+    """Data-parallel gradient exchange: one flat fp32 bucket per module set,
+    one all-reduce (AVG) per optimiser step (RCCL over xGMI; gloo on CPU)."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group) if group is not None else 1
+
+    @property
+    def active(self):
+        return self.world > 1
+
+    def allreduce_grads(self, params):
+        if not self.active:
+            return
+        grads = [p.grad for p in params if p.grad is not None]
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+        flat /= self.world
+        off = 0
+        for g in grads:
+            n = g.numel()
+            g.copy_(flat[off:off + n].view_as(g))
+            off += n
+
+    def max_(self, t):
+        if self.active:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return t
+
+    def broadcast_module(self, m, src=0):
+        if self.active:
+            for p in m.state_dict().values():
+                dist.broadcast(p, src, group=self.group)
+
+
+class TD7Learner:
+    """Nets, optimisers and one TD7 update (Agent/TD7_multi_agent.py:211-293)."""
+
+    def __init__(self, state_dim, action_dim, hp=None, learning_steps=500000, offline=False, device="cpu",
+                 precision="fp32", sync=None, fused_adam=None):
+        self.hp = hp if hp is not None else Hyperparameters()
+        hp = self.hp
+        self.device = torch.device(device)
+        self.precision = precision
+        self.sync = sync if sync is not None else GradSync(None)
+        self.actor = Actor(state_dim, action_dim, hp.zs_dim, hp.actor_hdim, hp.actor_activ).to(self.device)
+        self.critic = Critic(state_dim, action_dim, hp.zs_dim, hp.critic_hdim, hp.critic_activ).to(self.device)
+        self.encoder = Encoder(state_dim, action_dim, hp.zs_dim, hp.enc_hdim, hp.enc_activ).to(self.device)
+        for m in (self.actor, self.critic, self.encoder):
+            self.sync.broadcast_module(m)
+        if fused_adam is None:
+            fused_adam = self.device.type == "cuda"
+        kw = dict(weight_decay=1e-7, fused=True) if fused_adam else dict(weight_decay=1e-7)
+        self.actor_optimizer = torch.optim.Adam(self.actor.parameters(), lr=hp.actor_lr, **kw)
+        self.critic_optimizer = torch.optim.Adam(self.critic.parameters(), lr=hp.critic_lr, **kw)
+        self.encoder_optimizer = torch.optim.Adam(self.encoder.parameters(), lr=hp.encoder_lr, **kw)
+        self.actor_target = copy.deepcopy(self.actor)
+        self.critic_target = copy.deepcopy(self.critic)
+        self.fixed_encoder = copy.deepcopy(self.encoder)
+        self.fixed_encoder_target = copy.deepcopy(self.encoder)
+        self.checkpoint_actor = copy.deepcopy(self.actor)
+        self.checkpoint_encoder = copy.deepcopy(self.encoder)
+        self.offline = offline
+        self.training_steps = 0
+        # device-resident scalars (:183-186, :236-237)
+        f32 = dict(device=self.device, dtype=torch.float32)
+        self.max = torch.tensor(-1e8, **f32)
+        self.min = torch.tensor(1e8, **f32)
+        self.max_target = torch.tensor(0.0, **f32)
+        self.min_target = torch.tensor(0.0, **f32)
+        self.target_policy_noise = torch.tensor(float(hp.target_policy_noise), **f32)
+        self.policy_noise_decrease = hp.target_policy_noise / learning_steps
+        self.action_noise_decrease = hp.exploration_noise / learning_steps
+        self.exploration_noise = float(hp.exploration_noise)
+
+    def _autocast(self):
+        if self.precision == "bf16":
+            return torch.autocast(device_type=self.device.type, dtype=torch.bfloat16)
+        return torch.autocast(device_type=self.device.type, enabled=False)
+
+    def update(self, state, action, next_state, reward, not_done, noise=None):
+        """One TD7 gradient step on a sampled batch.  Returns the per-sample
+        priorities |td|max.clamp(min_priority)^alpha (:262)."""
+        hp = self.hp
+        self.training_steps += 1
+        # ---- encoder (:219-228)
+        with self._autocast():
+            with torch.no_grad():
+                next_zs = self.encoder.zs(next_state)
+            zs = self.encoder.zs(state)
+            pred_zs = self.encoder.zsa(zs, action)
+        encoder_loss = F.mse_loss(pred_zs.float(), next_zs.float())
+        self.encoder_optimizer.zero_grad(set_to_none=False)
+        encoder_loss.backward()
+        self.sync.allreduce_grads(list(self.encoder.parameters()))
+        self.encoder_optimizer.step()
+        # ---- critic (:233-257)
+        with torch.no_grad():
+            with self._autocast():
+                fixed_target_zs = self.fixed_encoder_target.zs(next_state)
+                if noise is None:
+                    noise = torch.randn_like(action)
+                noise = (noise * self.target_policy_noise).clamp(-hp.noise_clip, hp.noise_clip)
+                self.target_policy_noise -= self.policy_noise_decrease
+                next_action = (self.actor_target(next_state, fixed_target_zs) + noise).clamp(-1, 1)
+                fixed_target_zsa = self.fixed_encoder_target.zsa(fixed_target_zs, next_action)
+                Q_target = self.critic_target(next_state, next_action, fixed_target_zsa,
+                                              fixed_target_zs).float().min(1, keepdim=True)[0]
+            Q_target = reward + not_done * hp.discount * Q_target.clamp(self.min_target, self.max_target)
+            bounds = torch.stack([Q_target.max(), -Q_target.min()])
+            self.sync.max_(bounds)
+            torch.maximum(self.max, bounds[0], out=self.max)
+            torch.minimum(self.min, -bounds[1], out=self.min)
+            with self._autocast():
+                fixed_zs = self.fixed_encoder.zs(state)
+                fixed_zsa = self.fixed_encoder.zsa(fixed_zs, action)
+        with self._autocast():
+            Q = self.critic(state, action, fixed_zsa, fixed_zs)
+        td_loss = (Q.float() - Q_target).abs()
+        critic_loss = LAP_huber(td_loss)
+        self.critic_optimizer.zero_grad(set_to_none=False)
+        critic_loss.backward()
+        self.sync.allreduce_grads(list(self.critic.parameters()))
+        self.critic_optimizer.step()
+        priority = td_loss.detach().max(1)[0].clamp(min=hp.min_priority).pow(hp.alpha)
+        # ---- actor (:268-279)
+        if self.training_steps % hp.policy_freq == 0:
+            with self._autocast():
+                actor = self.actor(state, fixed_zs)
+                fixed_zsa = self.fixed_encoder.zsa(fixed_zs, actor)
+                Q = self.critic(state, actor, fixed_zsa, fixed_zs)
+            actor_loss = -Q.float().mean()
+            if self.offline:
+                actor_loss = actor_loss + hp.lmbda * Q.float().abs().mean().detach() * F.mse_loss(actor.float(), action)
+            self.actor_optimizer.zero_grad(set_to_none=False)
+            actor_loss.backward()
+            self.sync.allreduce_grads(list(self.actor.parameters()))
+            self.actor_optimizer.step()
+        return priority
+
+    def maybe_update_targets(self):
+        """:284-293; returns True when the targets were refreshed."""
+        if self.training_steps % self.hp.target_update_rate != 0:
+            return False
+        self.actor_target.load_state_dict(self.actor.state_dict())
+        self.critic_target.load_state_dict(self.critic.state_dict())
+        self.fixed_encoder_target.load_state_dict(self.fixed_encoder.state_dict())
+        self.fixed_encoder.load_state_dict(self.encoder.state_dict())
+        self.max_target.copy_(self.max)
+        self.min_target.copy_(self.min)
+        return True
+
+    @torch.no_grad()
+    def act(self, state, use_checkpoint=False):
+        with self._autocast():
+            if use_checkpoint:
+                zs = self.checkpoint_encoder.zs(state)
+                a = self.checkpoint_actor(state, zs)
+            else:
+                zs = self.fixed_encoder.zs(state)
+                a = self.actor(state, zs)
+        return a.float()
+
+
+class Agent:
+    """Drop-in for Agent/TD7_multi_agent.py:143 (and the batched select_action of
+    TD7_multi_agent_Pink_noise.py:209-228), backed by the HIP LAP replay."""
+
+    def __init__(self, state_dim, action_dim, max_action, learning_steps=500000, offline=False, hp=None,
+                 env_num=15, ep_length=300, device=None, precision="fp32", n_envs=None, process_group=None,
+                 buffer_size=None):
+        from . import _native as nat
+        from .replay import LAP
+        self.device = nat.require_gpu(device)
+        self.hp = hp if hp is not None else Hyperparameters()
+        self.sync = GradSync(process_group)
+        self.learner = TD7Learner(state_dim, action_dim, self.hp, learning_steps, offline, self.device, precision,
+                                  self.sync)
+        self.env_num = env_num
+        self.ep_length = ep_length
+        self.action_dim = action_dim
+        size = int(buffer_size if buffer_size is not None else self.hp.buffer_size)
+        self.replay_buffer = LAP(state_dim, action_dim, self.device, env_num, size, self.hp.batch_size, max_action,
+                                 normalize_actions=True, prioritized=True)
+        self.max_action = max_action
+        self.offline = offline
+        # checkpointing (:175-180)
+        self.eps_since_update = 0
+        self.timesteps_since_update = 0
+        self.max_eps_before_update = 1
+        self.min_return = 1e8
+        self.best_min_return = -1e8
+        self.noise = None
+
+    # the reference exposes the nets and counters on the agent itself
+    def __getattr__(self, name):
+        learner = self.__dict__.get("learner")
+        if learner is not None and hasattr(learner, name):
+            return getattr(learner, name)
+        raise AttributeError(name)
+
+    # ----------------------------------------------------------- acting
+    def select_action(self, state, timestep=None, first_step=True, use_checkpoint=False, use_exploration=True):
+        """Accepts one state (80,) or a batch (N, 80) as numpy; returns numpy."""
+        s = np.asarray(state, dtype=np.float32)
+        single = s.ndim == 1
+        st = torch.as_tensor(s.reshape(-1, s.shape[-1]), device=self.device)
+        a = self.learner.act(st, use_checkpoint)
+        a = a.cpu().numpy()
+        if use_exploration:
+            if timestep is not None:
+                # Pink-noise variant (TD7_multi_agent_Pink_noise.py:203-228): one coloured
+                # noise sequence per episode, scaled by exploration_noise
+                if first_step or self.noise is None:
+                    self.init_episode_noise()
+                a = a + self.noise[:, timestep]
+            else:
+                a = a + np.random.randn(*a.shape).astype(np.float32) * self.learner.exploration_noise
+                self.learner.exploration_noise -= self.learner.action_noise_decrease * a.shape[0]
+        a = np.clip(a, -1, 1) * self.max_action
+        return a[0] if single else a
+
+    def init_episode_noise(self):
+        from .pink import powerlaw_psd_gaussian
+        buf = powerlaw_psd_gaussian(self.hp.beta, (self.action_dim, self.ep_length)) * self.hp.noise_scale
+        self.noise = buf / np.max(np.abs(buf)) * self.learner.exploration_noise
+
+    @torch.no_grad()
+    def select_action_batch(self, obs, use_checkpoint=False, use_exploration=True):
+        """Device-resident batched actions for the vectorised loop (no host sync)."""
+        a = self.learner.act(obs, use_checkpoint)
+        if use_exploration:
+            a = a + torch.randn_like(a) * self.learner.exploration_noise
+            self.learner.exploration_noise -= self.learner.action_noise_decrease * a.shape[0]
+        return a.clamp(-1, 1) * self.max_action
+
+    # ---------------------------------------------------------- training
+    def train(self):
+        state, action, next_state, reward, not_done = self.replay_buffer.sample()
+        priority = self.learner.update(state, action, next_state, reward, not_done)
+        self.replay_buffer.update_priority(priority)
+        if self.learner.maybe_update_targets():
+            self.replay_buffer.reset_max_priority()
+
+    def maybe_train_and_checkpoint(self, ep_timesteps, ep_return):
+        """:296-312 (the episode return is MIN-reduced over data-parallel ranks)."""
+        self.eps_since_update += 1
+        self.timesteps_since_update += ep_timesteps
+        r = float(ep_return)
+        if self.sync.active:
+            t = torch.tensor([-r], device=self.device, dtype=torch.float64)
+            self.sync.max_(t)
+            r = -float(t)
+        self.min_return = min(self.min_return, r)
+        if self.min_return < self.best_min_return:
+            self.train_and_reset()
+        elif self.eps_since_update == self.max_eps_before_update:
+            self.best_min_return = self.min_return
+            self.learner.checkpoint_actor.load_state_dict(self.learner.actor.state_dict())
+            self.learner.checkpoint_encoder.load_state_dict(self.learner.fixed_encoder.state_dict())
+            self.train_and_reset()
+
+    def train_and_reset(self):
+        """:315-325"""
+        for _ in range(self.timesteps_since_update):
+            if self.learner.training_steps == self.hp.steps_before_checkpointing:
+                self.best_min_return *= self.hp.reset_weight
+                self.max_eps_before_update = self.hp.max_eps_when_checkpointing
+            self.train()
+        self.eps_since_update = 0
+        self.timesteps_since_update = 0
+        self.min_return = 1e8
+
+    def reset_buffer(self):
+        self.replay_buffer.reset_buffer()
+
+    # ------------------------------------------------------- checkpoints
+    SUFFIXES = ["_critic", "_critic_optimizer", "_actor", "_actor_optimizer", "_encoder", "_encoder_optimizer",
+                "_checkpoint_actor", "_checkpoint_encoder"]
+
+    def save(self, filename):
+        """:330-345 (same 8 files)."""
+        L = self.learner
+        torch.save(L.critic.state_dict(), filename + "_critic")
+        torch.save(L.critic_optimizer.state_dict(), filename + "_critic_optimizer")
+        torch.save(L.actor.state_dict(), filename + "_actor")
+        torch.save(L.actor_optimizer.state_dict(), filename + "_actor_optimizer")
+        torch.save(L.encoder.state_dict(), filename + "_encoder")
+        torch.save(L.encoder_optimizer.state_dict(), filename + "_encoder_optimizer")
+        torch.save(L.checkpoint_actor.state_dict(), filename + "_checkpoint_actor")
+        torch.save(L.checkpoint_encoder.state_dict(), filename + "_checkpoint_encoder")
+
+    def load(self, filename, load_optimizers=True):
+        """:347-366.  weights_only loading; optimizer files are optional (the
+        shipped checkpoints lack _critic_optimizer)."""
+        import os
+        L = self.learner
+        ld = lambda suffix: torch.load(filename + suffix, map_location=self.device, weights_only=True)  # noqa: E731
+        L.critic.load_state_dict(ld("_critic"))
+        L.actor.load_state_dict(ld("_actor"))
+        L.encoder.load_state_dict(ld("_encoder"))
+        if load_optimizers:
+            for suffix, opt in (("_critic_optimizer", L.critic_optimizer), ("_actor_optimizer", L.actor_optimizer),
+                                ("_encoder_optimizer", L.encoder_optimizer)):
+                if os.path.exists(filename + suffix):
+                    opt.load_state_dict(ld(suffix))
+        L.critic_target = copy.deepcopy(L.critic)
+        L.actor_target = copy.deepcopy(L.actor)
+        L.fixed_encoder = copy.deepcopy(L.encoder)
+        L.fixed_encoder_target = copy.deepcopy(L.encoder)
+        L.checkpoint_actor.load_state_dict(ld("_checkpoint_actor"))
+        L.checkpoint_encoder.load_state_dict(ld("_checkpoint_encoder"))
+
+
+def smoke():
+    """One TD7 train() step through the HIP LAP kernels on cuda:0."""
+    hp = Hyperparameters(zs_dim=32, enc_hdim=32, critic_hdim=32, actor_hdim=32, batch_size=16)
+    agent = Agent(80, 7, 1, hp=hp, env_num=8, device="cuda:0", buffer_size=1024)
+    n = 64
+    obs = torch.randn(n, 80, device="cuda:0")
+    act = torch.rand(n, 7, device="cuda:0") * 2 - 1
+    strata = torch.arange(n, device="cuda:0", dtype=torch.int32) % 8
+    for _ in range(4):
+        nobs = torch.randn(n, 80, device="cuda:0")
+        agent.replay_buffer.add_batch(obs, act, nobs, torch.rand(n, device="cuda:0"),
+                                      torch.zeros(n, dtype=torch.bool, device="cuda:0"), strata)
+        obs = nobs
+    agent.train()
+    agent.train()
+    torch.cuda.synchronize()
+    assert torch.isfinite(agent.learner.max)

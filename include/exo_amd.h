@@ -121,39 +121,45 @@ void exo_destroy(exo_ctx *ctx);
  * sum tree per stratum (the reference keeps one priority row per env,
  * :41, and samples batch_size rows from each, :75-85).
  * ---------------------------------------------------------------------- */
-typedef struct lap_tree lap_tree;
+/* Caller-owned sum trees: tree[n_strata][2*cap] fp32 (cap = capacity rounded
+ * up to a power of two; node 1 of a stratum is its total, leaf i -- the
+ * reference's self.priority[s, i] -- is node cap + i) and one fp32
+ * max_priority scalar.  Both are device memory (e.g. torch tensors). */
+typedef struct {
+    float *tree;
+    float *max_priority;
+    int32_t n_strata;
+    int32_t capacity; /* max_size per stratum (:19) */
+    int32_t cap;      /* power of two >= capacity */
+} lap_tree_desc;
 
-/* capacity = max_size per stratum (:19); the tree holds priorities in fp32. */
-int lap_create(int32_t n_strata, int32_t capacity, int32_t device, lap_tree **out);
-void lap_destroy(lap_tree *t);
-/* Device pointer to the trees ([n_strata][lap_tree_stride] floats; node 1 of
- * a stratum is its total, leaf i (the reference's self.priority[s, i]) is
- * node stride/2 + i) and to the global max_priority scalar (fp32). */
-float *lap_priorities(lap_tree *t);
-int32_t lap_tree_stride(const lap_tree *t);
-float *lap_max_priority(lap_tree *t);
+/* floats needed for the trees of n_strata x capacity (= n_strata * 2 * cap). */
+int32_t lap_tree_floats(int32_t n_strata, int32_t capacity);
 
-/* LAP.add (:49-63) for n items: stratum_dev[n], slot_dev[n]; every item gets
- * the current max_priority. */
-int lap_add(lap_tree *t, const int32_t *stratum_dev, const int32_t *slot_dev, int32_t n, void *stream);
+/* zero every tree, max_priority = 1 (LAP.__init__ / reset_buffer, :39-45, :133-137). */
+int lap_init(const lap_tree_desc *t, void *stream);
+
+/* LAP.add (:49-63) for n items: stratum_dev[n], slot_dev[n] (slot < 0: skip);
+ * every item gets the current max_priority. */
+int lap_add(const lap_tree_desc *t, const int32_t *stratum_dev, const int32_t *slot_dev, int32_t n, void *stream);
 
 /* LAP.sample (:65-85): for every stratum s, batch indices
  * idx = searchsorted_left(cumsum(p[s, :size[s]]), u * sum) for the
  * per-stratum uniforms u_dev[s][batch].  size_dev[n_strata] (int32).
  * Writes idx_dev[s][batch] (int32, within-stratum slot). */
-int lap_sample(lap_tree *t, const float *u_dev, const int32_t *size_dev, int32_t batch, int32_t *idx_dev,
+int lap_sample(const lap_tree_desc *t, const float *u_dev, const int32_t *size_dev, int32_t batch, int32_t *idx_dev,
                void *stream);
 
 /* LAP.update_priority (:113-117): p[s, idx[s][b]] = prio[s*batch+b] (the last
  * occurrence wins for duplicate indices, as the reference's CPU index_put),
  * then max_priority = max(max_priority, max(prio)). */
-int lap_update(lap_tree *t, const int32_t *idx_dev, const float *prio_dev, int32_t batch, void *stream);
+int lap_update(const lap_tree_desc *t, const int32_t *idx_dev, const float *prio_dev, int32_t batch, void *stream);
 
 /* LAP.reset_max_priority (:119-120): max_priority = max over all leaves. */
-int lap_reset_max(lap_tree *t, void *stream);
+int lap_reset_max(const lap_tree_desc *t, void *stream);
 
 /* Total priority of each stratum (root of its tree) -> out_dev[n_strata]. */
-int lap_totals(lap_tree *t, float *out_dev, void *stream);
+int lap_totals(const lap_tree_desc *t, float *out_dev, void *stream);
 
 #ifdef __cplusplus
 }

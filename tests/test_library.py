@@ -29,7 +29,7 @@ def lib():
 def test_header_declares_the_boundary():
     names = declared_functions()
     for required in ["exo_create", "exo_reset", "exo_reset_from_draws", "exo_step", "exo_destroy", "exo_last_error",
-                     "exo_get_state_host", "exo_set_state_host", "lap_create", "lap_add", "lap_sample", "lap_update",
+                     "exo_get_state_host", "exo_set_state_host", "lap_init", "lap_add", "lap_sample", "lap_update",
                      "lap_reset_max"]:
         assert required in names
 

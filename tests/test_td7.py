@@ -1,0 +1,117 @@
+"""TD7 update math (exo_amd.td7.TD7Learner, device-agnostic torch) against the
+reference's golden train() steps (tests/golden/td7_small.npz: reduced widths,
+injected batch and target-policy noise).  fp32 on CPU: tolerance 1e-5 rel /
+1e-6 abs on every parameter after each step."""
+import numpy as np
+import pytest
+import torch
+
+from helpers import GOLDEN
+from exo_amd.td7 import Hyperparameters, TD7Learner
+
+
+def _golden():
+    return np.load(f"{GOLDEN}/td7_small.npz", allow_pickle=False)
+
+
+def _learner(g, device="cpu"):
+    zs, enc, crit, act, bs, E = [int(x) for x in g["hp"]]
+    hp = Hyperparameters(zs_dim=zs, enc_hdim=enc, critic_hdim=crit, actor_hdim=act, batch_size=bs)
+    torch.manual_seed(0)
+    L = TD7Learner(80, 7, hp, learning_steps=int(g["learning_steps"]), device=device, fused_adam=False)
+    return L
+
+
+def _sd(g, prefix):
+    return {k[len(prefix) + 1:]: torch.tensor(g[k]) for k in g.files if k.startswith(prefix + ".")}
+
+
+def test_seeded_init_matches_reference():
+    g = _golden()
+    L = _learner(g)
+    for name in ("actor", "critic", "encoder"):
+        ref = _sd(g, f"init_{name}")
+        for k, v in getattr(L, name).state_dict().items():
+            torch.testing.assert_close(v, ref[k], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("device", ["cpu"])
+def test_two_train_steps_match_reference(device):
+    g = _golden()
+    L = _learner(g, device)
+    for step in range(2):
+        b = [torch.tensor(g[f"batch{step}_{k}"], device=device) for k in
+             ("state", "action", "next_state", "reward", "not_done")]
+        noise = torch.tensor(g[f"batch{step}_noise"], device=device)
+        prio = L.update(*b, noise=noise)
+        np.testing.assert_allclose(prio.cpu().numpy(), g[f"priority{step}"], rtol=1e-5, atol=1e-6)
+        for name in ("actor", "critic", "encoder"):
+            ref = _sd(g, f"step{step}_{name}")
+            for k, v in getattr(L, name).state_dict().items():
+                np.testing.assert_allclose(v.cpu().numpy(), ref[k].numpy(), rtol=1e-5, atol=1e-6,
+                                           err_msg=f"step {step} {name}.{k}")
+        assert abs(float(L.max) - g[f"step{step}_max"]) <= 1e-5 * max(1, abs(g[f"step{step}_max"]))
+        assert abs(float(L.min) - g[f"step{step}_min"]) <= 1e-5 * max(1, abs(g[f"step{step}_min"]))
+        assert abs(float(L.target_policy_noise) - g[f"step{step}_target_policy_noise"]) < 1e-7
+
+
+def test_target_update_schedule():
+    hp = Hyperparameters(zs_dim=8, enc_hdim=8, critic_hdim=8, actor_hdim=8, batch_size=4, target_update_rate=3)
+    L = TD7Learner(80, 7, hp, device="cpu", fused_adam=False)
+    b = [torch.randn(4, 80), torch.rand(4, 7) * 2 - 1, torch.randn(4, 80), torch.rand(4, 1), torch.ones(4, 1)]
+    for i in range(1, 7):
+        L.update(*b)
+        refreshed = L.maybe_update_targets()
+        assert refreshed == (i % 3 == 0)
+        if refreshed:
+            for p, q in zip(L.critic.parameters(), L.critic_target.parameters()):
+                assert torch.equal(p, q)
+            assert float(L.max_target) == float(L.max)
+
+
+def test_select_action_matches_reference_pink_variant():
+    g = np.load(f"{GOLDEN}/select_action.npz", allow_pickle=False)
+    hp = Hyperparameters(zs_dim=16, enc_hdim=24, critic_hdim=20, actor_hdim=18)
+    L = TD7Learner(80, 7, hp, device="cpu", fused_adam=False)
+    for name in ("checkpoint_actor", "checkpoint_encoder", "actor", "fixed_encoder"):
+        getattr(L, name).load_state_dict(_sd(g, name))
+    st = torch.tensor(g["state"])
+    np.testing.assert_allclose(L.act(st, use_checkpoint=True).numpy(), g["action_ckpt"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(L.act(st, use_checkpoint=False).numpy(), g["action_live"], rtol=1e-6, atol=1e-6)
+
+
+def test_pink_noise_statistics():
+    from exo_amd.pink import powerlaw_psd_gaussian
+    x = powerlaw_psd_gaussian(1.0, (7, 4096), rng=np.random.default_rng(0))
+    assert x.shape == (7, 4096)
+    assert abs(x.std() - 1) < 0.2
+    # 1/f: low-frequency power dominates
+    p = np.abs(np.fft.rfft(x, axis=-1)) ** 2
+    assert p[:, 1:20].mean() > 10 * p[:, 1000:1200].mean()
+
+
+@pytest.mark.gpu
+def test_two_train_steps_match_reference_on_gpu():
+    """Same golden steps with the nets on the MI355X (fp32, hipBLASLt GEMMs)."""
+    g = _golden()
+    L = _learner(g, "cpu")
+    L2 = TD7Learner(80, 7, L.hp, learning_steps=int(g["learning_steps"]), device="cuda")
+    for name in ("actor", "critic", "encoder", "actor_target", "critic_target", "fixed_encoder",
+                 "fixed_encoder_target"):
+        getattr(L2, name).load_state_dict(getattr(L, name).state_dict())
+    for step in range(2):
+        b = [torch.tensor(g[f"batch{step}_{k}"], device="cuda") for k in
+             ("state", "action", "next_state", "reward", "not_done")]
+        prio = L2.update(*b, noise=torch.tensor(g[f"batch{step}_noise"], device="cuda"))
+        np.testing.assert_allclose(prio.cpu().numpy(), g[f"priority{step}"], rtol=1e-4, atol=1e-5)
+        for name in ("actor", "critic", "encoder"):
+            ref = _sd(g, f"step{step}_{name}")
+            for k, v in getattr(L2, name).state_dict().items():
+                np.testing.assert_allclose(v.cpu().numpy(), ref[k].numpy(), rtol=1e-4, atol=1e-5,
+                                           err_msg=f"step {step} {name}.{k}")
+
+
+@pytest.mark.gpu
+def test_agent_train_step_through_lap_kernels():
+    from exo_amd import td7
+    td7.smoke()
