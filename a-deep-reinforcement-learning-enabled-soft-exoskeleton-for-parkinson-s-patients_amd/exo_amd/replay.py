@@ -107,10 +107,15 @@ class LAP:
         active[i] (bool [N], default all).  No host synchronisation."""
         E, C = self.num_envs, self.max_size
         n = state.shape[0]
+        if getattr(self, "_ar_n", None) is None or self._ar_n.numel() != n:
+            self._ar_n = torch.arange(n, device=self.device)
+            self._ar_e = torch.arange(E, device=self.device)
         strata = strata.to(torch.int64)
         act = torch.ones((n,), dtype=torch.int64, device=self.device) if active is None else active.to(torch.int64)
-        onehot = torch.nn.functional.one_hot(strata, E) * act[:, None]          # [N, E]
-        rank = (torch.cumsum(onehot, 0) - onehot)[torch.arange(n, device=self.device), strata]
+        # one-hot by comparison (F.one_hot validates its input with a host sync),
+        # stratum-major so the rank scan runs along the contiguous dimension
+        onehot = (self._ar_e[:, None] == strata[None, :]).to(torch.int32) * act[None, :].to(torch.int32)  # [E, N]
+        rank = (torch.cumsum(onehot, 1, dtype=torch.int32) - onehot)[strata, self._ar_n].to(torch.int64)
         slot = (self.ptr_s.to(torch.int64)[strata] + rank) % C
         slot = torch.where(act > 0, slot, torch.full_like(slot, C))              # inactive -> trash row
         rows = self._row0[strata] + slot
@@ -119,7 +124,7 @@ class LAP:
         self.next_state.view(-1, self.state_dim).index_copy_(0, rows, next_state.to(torch.float32))
         self.reward.view(-1, 1).index_copy_(0, rows, reward.to(torch.float32).view(-1, 1))
         self.not_done.view(-1, 1).index_copy_(0, rows, 1.0 - done.to(torch.float32).view(-1, 1))
-        cnt = onehot.sum(0)
+        cnt = onehot.sum(1, dtype=torch.int64)
         lap_slot = torch.where(act > 0, slot, torch.full_like(slot, -1)).to(torch.int32)
         st32 = strata.to(torch.int32)
         nat.check(nat.lib().lap_add(ctypes.byref(self._desc), nat.ptr(st32), nat.ptr(lap_slot), n, self._stream()),

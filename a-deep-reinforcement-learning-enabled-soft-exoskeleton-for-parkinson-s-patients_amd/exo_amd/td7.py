@@ -189,7 +189,7 @@ class TD7Learner:
     """Nets, optimisers and one TD7 update (Agent/TD7_multi_agent.py:211-293)."""
 
     def __init__(self, state_dim, action_dim, hp=None, learning_steps=500000, offline=False, device="cpu",
-                 precision="fp32", sync=None, fused_adam=None):
+                 precision="fp32", sync=None, fused_adam=None, graph_safe=False):
         self.hp = hp if hp is not None else Hyperparameters()
         hp = self.hp
         self.device = torch.device(device)
@@ -203,6 +203,8 @@ class TD7Learner:
         if fused_adam is None:
             fused_adam = self.device.type == "cuda"
         kw = dict(weight_decay=1e-7, fused=True) if fused_adam else dict(weight_decay=1e-7)
+        if graph_safe:
+            kw["capturable"] = True  # optimiser step counters on the device (HIP graph replay)
         self.actor_optimizer = torch.optim.Adam(self.actor.parameters(), lr=hp.actor_lr, **kw)
         self.critic_optimizer = torch.optim.Adam(self.critic.parameters(), lr=hp.critic_lr, **kw)
         self.encoder_optimizer = torch.optim.Adam(self.encoder.parameters(), lr=hp.encoder_lr, **kw)
@@ -223,18 +225,25 @@ class TD7Learner:
         self.target_policy_noise = torch.tensor(float(hp.target_policy_noise), **f32)
         self.policy_noise_decrease = hp.target_policy_noise / learning_steps
         self.action_noise_decrease = hp.exploration_noise / learning_steps
-        self.exploration_noise = float(hp.exploration_noise)
+        self.exploration_noise_t = torch.tensor(float(hp.exploration_noise), **f32)
+
+    @property
+    def exploration_noise(self):
+        return float(self.exploration_noise_t)
 
     def _autocast(self):
         if self.precision == "bf16":
             return torch.autocast(device_type=self.device.type, dtype=torch.bfloat16)
         return torch.autocast(device_type=self.device.type, enabled=False)
 
-    def update(self, state, action, next_state, reward, not_done, noise=None):
-        """One TD7 gradient step on a sampled batch.  Returns the per-sample
-        priorities |td|max.clamp(min_priority)^alpha (:262)."""
+    # One TD7 update (:211-293) is split into phases so a data-parallel step
+    # needs only two collectives and every phase can be captured in a HIP
+    # graph.  Encoder and critic gradients are independent (the critic only
+    # sees fixed_encoder / fixed_encoder_target, :233-251), so both are
+    # computed before either optimiser steps -- the same arithmetic as the
+    # reference's encoder-then-critic order.
+    def phase_grads(self, state, action, next_state, reward, not_done, noise=None):
         hp = self.hp
-        self.training_steps += 1
         # ---- encoder (:219-228)
         with self._autocast():
             with torch.no_grad():
@@ -244,8 +253,6 @@ class TD7Learner:
         encoder_loss = F.mse_loss(pred_zs.float(), next_zs.float())
         self.encoder_optimizer.zero_grad(set_to_none=False)
         encoder_loss.backward()
-        self.sync.allreduce_grads(list(self.encoder.parameters()))
-        self.encoder_optimizer.step()
         # ---- critic (:233-257)
         with torch.no_grad():
             with self._autocast():
@@ -259,10 +266,9 @@ class TD7Learner:
                 Q_target = self.critic_target(next_state, next_action, fixed_target_zsa,
                                               fixed_target_zs).float().min(1, keepdim=True)[0]
             Q_target = reward + not_done * hp.discount * Q_target.clamp(self.min_target, self.max_target)
-            bounds = torch.stack([Q_target.max(), -Q_target.min()])
-            self.sync.max_(bounds)
-            torch.maximum(self.max, bounds[0], out=self.max)
-            torch.minimum(self.min, -bounds[1], out=self.min)
+            # running bounds (:245-246); kept per rank, MAX-reduced when the targets refresh
+            torch.maximum(self.max, Q_target.max(), out=self.max)
+            torch.minimum(self.min, Q_target.min(), out=self.min)
             with self._autocast():
                 fixed_zs = self.fixed_encoder.zs(state)
                 fixed_zsa = self.fixed_encoder.zsa(fixed_zs, action)
@@ -272,23 +278,57 @@ class TD7Learner:
         critic_loss = LAP_huber(td_loss)
         self.critic_optimizer.zero_grad(set_to_none=False)
         critic_loss.backward()
-        self.sync.allreduce_grads(list(self.critic.parameters()))
+        self._fixed_zs = fixed_zs
+        return td_loss.detach().max(1)[0].clamp(min=hp.min_priority).pow(hp.alpha)  # :262
+
+    def phase_steps(self):
+        self.encoder_optimizer.step()
         self.critic_optimizer.step()
-        priority = td_loss.detach().max(1)[0].clamp(min=hp.min_priority).pow(hp.alpha)
-        # ---- actor (:268-279)
-        if self.training_steps % hp.policy_freq == 0:
-            with self._autocast():
-                actor = self.actor(state, fixed_zs)
-                fixed_zsa = self.fixed_encoder.zsa(fixed_zs, actor)
-                Q = self.critic(state, actor, fixed_zsa, fixed_zs)
-            actor_loss = -Q.float().mean()
-            if self.offline:
-                actor_loss = actor_loss + hp.lmbda * Q.float().abs().mean().detach() * F.mse_loss(actor.float(), action)
-            self.actor_optimizer.zero_grad(set_to_none=False)
-            actor_loss.backward()
-            self.sync.allreduce_grads(list(self.actor.parameters()))
-            self.actor_optimizer.step()
+
+    def phase_actor_grads(self, state, action):
+        """:268-277 with the just-updated critic."""
+        fixed_zs = self._fixed_zs
+        with self._autocast():
+            actor = self.actor(state, fixed_zs)
+            fixed_zsa = self.fixed_encoder.zsa(fixed_zs, actor)
+            Q = self.critic(state, actor, fixed_zsa, fixed_zs)
+        actor_loss = -Q.float().mean()
+        if self.offline:
+            actor_loss = actor_loss + self.hp.lmbda * Q.float().abs().mean().detach() * F.mse_loss(actor.float(),
+                                                                                               action)
+        self.actor_optimizer.zero_grad(set_to_none=False)
+        actor_loss.backward()
+
+    def phase_actor_step(self):
+        self.actor_optimizer.step()
+
+    def grad_params(self, actor=False):
+        if actor:
+            return list(self.actor.parameters())
+        return list(self.encoder.parameters()) + list(self.critic.parameters())
+
+    def update(self, state, action, next_state, reward, not_done, noise=None, update_actor=None):
+        """One TD7 gradient step on a sampled batch.  Returns the per-sample
+        priorities |td|max.clamp(min_priority)^alpha (:262)."""
+        self.training_steps += 1
+        if update_actor is None:
+            update_actor = self.training_steps % self.hp.policy_freq == 0
+        priority = self.phase_grads(state, action, next_state, reward, not_done, noise)
+        self.sync.allreduce_grads(self.grad_params())
+        self.phase_steps()
+        if update_actor:
+            self.phase_actor_grads(state, action)
+            self.sync.allreduce_grads(self.grad_params(actor=True))
+            self.phase_actor_step()
         return priority
+
+    def sync_bounds(self):
+        """Global running Q-target bounds = MAX over ranks of the local ones."""
+        if self.sync.active:
+            b = torch.stack([self.max, -self.min])
+            self.sync.max_(b)
+            self.max.copy_(b[0])
+            self.min.copy_(-b[1])
 
     def maybe_update_targets(self):
         """:284-293; returns True when the targets were refreshed."""
@@ -298,6 +338,7 @@ class TD7Learner:
         self.critic_target.load_state_dict(self.critic.state_dict())
         self.fixed_encoder_target.load_state_dict(self.fixed_encoder.state_dict())
         self.fixed_encoder.load_state_dict(self.encoder.state_dict())
+        self.sync_bounds()
         self.max_target.copy_(self.max)
         self.min_target.copy_(self.min)
         return True
@@ -320,14 +361,14 @@ class Agent:
 
     def __init__(self, state_dim, action_dim, max_action, learning_steps=500000, offline=False, hp=None,
                  env_num=15, ep_length=300, device=None, precision="fp32", n_envs=None, process_group=None,
-                 buffer_size=None):
+                 buffer_size=None, graph_safe=False):
         from . import _native as nat
         from .replay import LAP
         self.device = nat.require_gpu(device)
         self.hp = hp if hp is not None else Hyperparameters()
         self.sync = GradSync(process_group)
         self.learner = TD7Learner(state_dim, action_dim, self.hp, learning_steps, offline, self.device, precision,
-                                  self.sync)
+                                  self.sync, graph_safe=graph_safe)
         self.env_num = env_num
         self.ep_length = ep_length
         self.action_dim = action_dim
@@ -368,7 +409,7 @@ class Agent:
                 a = a + self.noise[:, timestep]
             else:
                 a = a + np.random.randn(*a.shape).astype(np.float32) * self.learner.exploration_noise
-                self.learner.exploration_noise -= self.learner.action_noise_decrease * a.shape[0]
+                self.learner.exploration_noise_t -= self.learner.action_noise_decrease * a.shape[0]
         a = np.clip(a, -1, 1) * self.max_action
         return a[0] if single else a
 
@@ -382,8 +423,8 @@ class Agent:
         """Device-resident batched actions for the vectorised loop (no host sync)."""
         a = self.learner.act(obs, use_checkpoint)
         if use_exploration:
-            a = a + torch.randn_like(a) * self.learner.exploration_noise
-            self.learner.exploration_noise -= self.learner.action_noise_decrease * a.shape[0]
+            a = a + torch.randn_like(a) * self.learner.exploration_noise_t
+            self.learner.exploration_noise_t -= self.learner.action_noise_decrease * a.shape[0]
         return a.clamp(-1, 1) * self.max_action
 
     # ---------------------------------------------------------- training

@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--precision", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--eager", action="store_true", help="no HIP graph capture of the training iteration")
+    ap.add_argument("--kernel-timing-steps", type=int, default=100,
+                    help="env-only launches timed with HIP events for the roofline line")
     return ap.parse_args()
 
 
@@ -96,44 +99,50 @@ def main():
     Ls = env.lengths_host
     round_len = int(Ls.max()) - 3
     active_per_k = np.array([(Ls - 3 > k).sum() for k in range(round_len)])
-    agent = None
+    agent = trainer = None
     if args.mode == "train":
+        from exo_amd.rollout import VecTrainer
         from exo_amd.td7 import Agent, Hyperparameters
         hp = Hyperparameters()
         agent = Agent(80, 7, 1, env_num=8, hp=hp, device=dev, precision=args.precision, n_envs=N,
-                      process_group=dist.group.WORLD if world > 1 else None)
+                      process_group=dist.group.WORLD if world > 1 else None, graph_safe=not args.eager)
+        trainer = VecTrainer(env, agent, use_graphs=not args.eager)
     out = env.new_outputs(True)
-    obs = env.reset()
-    strata = torch.as_tensor(env.motions % 8, dtype=torch.int32, device=dev)
-    state = {"k": 0, "obs": obs}
+    state = {"k": 0, "obs": env.reset()}
     ev = []
 
     def one_step(timed):
+        if trainer is not None:
+            return trainer.step()
         k = state["k"]
         if k == round_len:
             state["obs"] = env.reset()
             k = 0
-        if agent is None:
-            act = torch.rand((N, 7), device=dev) * 2 - 1
-        else:
-            act = agent.select_action_batch(state["obs"])
+        act = torch.rand((N, 7), device=dev) * 2 - 1
         e0 = e1 = None
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        nobs, rew, done, info = env.step(act, out=out)
+        state["obs"] = env.step(act, out=out)[0]
         if timed:
             e1.record()
             ev.append((e0, e1))
-        if agent is not None:
-            active = torch.as_tensor(k < Ls - 3, device=dev)
-            agent.replay_buffer.add_batch(state["obs"], act, nobs, rew, done, strata, active)
-            agent.train()
-            state["obs"] = nobs.clone()
-        else:
-            state["obs"] = nobs
         state["k"] = k + 1
         return int(active_per_k[k])
+
+    def kernel_timing(n):
+        """exo_step_kernel alone, HIP events on the launch stream, all envs active."""
+        env.reset()
+        evs = []
+        for _ in range(n):
+            act = torch.rand((N, 7), device=dev) * 2 - 1
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            env.step(act, out=out)
+            e1.record()
+            evs.append((e0, e1))
+        torch.cuda.synchronize()
+        return float(np.mean([a.elapsed_time(b) for a, b in evs])), float(min(n, round_len) and N)
 
     for _ in range(args.warmup):
         one_step(False)
@@ -150,7 +159,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if ev:  # env mode: the timed launches themselves
+        kern_ms, kern_active = float(np.mean([a.elapsed_time(b) for a, b in ev])), env_steps / args.steps
+    else:   # train mode: the env kernel is inside graph replays; time it separately afterwards
+        kern_ms, kern_active = kernel_timing(min(args.kernel_timing_steps, int(Ls.min()) - 3))
     t = torch.tensor([elapsed, float(env_steps)], device=dev, dtype=torch.float64)
     if world > 1:
         tmax = t.clone()
@@ -161,7 +173,7 @@ def main():
     else:
         total_env_steps = float(env_steps)
     if rank == 0:
-        active_avg = env_steps / args.steps
+        active_avg = kern_active
         achieved = BYTES_PER_ENV_STEP * active_avg / (kern_ms * 1e-3) / 1e9
         res = {
             "metric": "env steps/sec (batched exo sim) + TD7 grad-steps/sec at 1/2/4/8 MI355X",

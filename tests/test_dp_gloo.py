@@ -48,6 +48,7 @@ def _worker(rank, world, port, outdir):
         half = [x[rank * 8:(rank + 1) * 8] for x in b]
         L.update(*half[:5], noise=half[5])
         L.maybe_update_targets()
+    L.sync_bounds()
     sd = {f"{n}.{k}": v.detach().clone() for n in ("actor", "critic", "encoder")
           for k, v in getattr(L, n).state_dict().items()}
     sd["max"] = L.max.clone()

@@ -7,8 +7,10 @@ FMA contraction, RK45 stages in second-order storage form).  Observations are
 float32 in the reference (Exoskeleton_env.py:568) and must match to 1 ulp-level
 (atol 2e-6 relative to magnitude); rewards (fp32 output of an fp64 value) to
 2e-6 relative; info (fp32 output) to 1e-5 relative / 1e-6 absolute; joint
-positions (fp64 state) to 1e-9 rad; done indices and tremor tables exactly
-(the tremor table is elementwise fp64 arithmetic with the same draws).
+positions (fp64 state) to 1e-9 rad; done indices exactly; tremor tables to
+1e-13 relative (device sin/pow and FMA contraction round differently from
+numpy by a few ulp; the D/S matrices, dummy shift and force scales are
+bit-exact).
 """
 import numpy as np
 import pytest
@@ -51,7 +53,7 @@ def test_reset_matches_reference_draws():
         for m, d in enumerate(gold):
             _close_obs(obs[m], d[f"ep{ep}_obs"])
             if ep == 1:
-                np.testing.assert_array_equal(env.tremor(m), d["ep1_tremor"])
+                np.testing.assert_allclose(env.tremor(m), d["ep1_tremor"], rtol=1e-13, atol=1e-14)
                 Dm, S, Iinv, sh, mm = env.episode(m)
                 np.testing.assert_array_equal(Dm, d["ep1_D"])
                 np.testing.assert_array_equal(S, d["ep1_S"])
