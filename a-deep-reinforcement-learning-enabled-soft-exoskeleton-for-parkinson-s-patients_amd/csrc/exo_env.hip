@@ -85,6 +85,9 @@ __device__ void invert(double *a /* n*n, destroyed */, double *inv) {
 __global__ __launch_bounds__(64) void exo_reset_kernel(Dev S, Urdf U, const uint8_t *mask, const int32_t *ids,
                                                        const double *draws, int draw_stride, uint64_t seed,
                                                        float *obs) {
+    // numpy evaluates every expression of the reset without fused multiply-add;
+    // keep the rounding identical (bit-exact D, S, shift and force scales).
+#pragma clang fp contract(off)
     const int e = ids ? ids[blockIdx.x] : (int)blockIdx.x;
     if (e >= S.N) return;
     if (!ids && mask && !mask[e]) return;
