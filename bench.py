@@ -65,6 +65,19 @@ def parse():
     return ap.parse_args()
 
 
+def pmc_traffic(bytes_per_launch):
+    """HBM bytes per exo_step launch from the newest committed PMC summary
+    (profiles/r*_rocprof_summary.json, FETCH_SIZE x2 + WRITE_SIZE, see
+    profiles/summarize.py) -- only if it was taken on this same workload."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_rocprof_summary.json")))
+    for f in reversed(files):
+        d = json.load(open(f)).get("pmc_exo_step")
+        if d and d.get("algorithmic_bytes_per_launch") == bytes_per_launch:
+            return d["traffic_bytes_per_launch"], os.path.relpath(f, REPO)
+    return None, None
+
+
 def cpu_baseline(seconds):
     """The oracle (plain C, fp64, one core) stepping 8 envs, one per motion, with
     random actions -- the 'port' CPU baseline.  Bounded by `seconds`."""
@@ -175,6 +188,7 @@ def main():
     if rank == 0:
         active_avg = kern_active
         achieved = BYTES_PER_ENV_STEP * active_avg / (kern_ms * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic(float(BYTES_PER_ENV_STEP * active_avg))
         res = {
             "metric": "env steps/sec (batched exo sim) + TD7 grad-steps/sec at 1/2/4/8 MI355X",
             "value": total_env_steps / elapsed,
@@ -190,7 +204,9 @@ def main():
                        "envs_per_gpu": N, "mode": args.mode, "parallelism": f"env-shard x{world}"
                        + (" + TD7 DP all-reduce" if agent and world > 1 else "")},
             "roofline": {"kernel": "exo_step_kernel", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_unit": "bytes per launch", "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": BYTES_PER_ENV_STEP * active_avg,
                          "bytes_per_env_step": BYTES_PER_ENV_STEP, "avg_kernel_ms": kern_ms,
                          "active_envs_per_launch": active_avg},
         }
