@@ -63,6 +63,9 @@ EXPORTS = {
     "lap_update": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p]),
     "lap_reset_max": (c_int32, [c_void_p, c_void_p]),
     "lap_totals": (c_int32, [c_void_p, c_void_p, c_void_p]),
+    "td7_avgl1norm_fwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, ctypes.c_float, c_void_p]),
+    "td7_avgl1norm_bwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, ctypes.c_float,
+                                    c_void_p]),
 }
 
 _lib = None

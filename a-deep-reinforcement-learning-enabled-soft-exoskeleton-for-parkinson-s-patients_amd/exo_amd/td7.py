@@ -27,6 +27,8 @@ import torch.distributed as dist
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .ops import avg_l1_norm
+
 
 @dataclass
 class Hyperparameters:
@@ -68,7 +70,8 @@ class Hyperparameters:
 
 
 def AvgL1Norm(x, eps=1e-8):
-    return x / x.abs().mean(-1, keepdim=True).clamp(min=eps)
+    """Agent/TD7_multi_agent.py:53-54 (one fused HIP kernel each way on the GPU)."""
+    return avg_l1_norm(x, eps)
 
 
 def LAP_huber(x, min_priority=1):
@@ -119,34 +122,57 @@ class Encoder(nn.Module):
 
 
 class Critic(nn.Module):
-    """Agent/TD7_multi_agent.py:109-140"""
+    """Agent/TD7_multi_agent.py:109-140.  The two Q heads share their input, so
+    their parameters are stored stacked ([2, out, in]) and each layer of both
+    heads runs as ONE batched GEMM.  state_dict()/load_state_dict() use the
+    reference's per-head names (q01, q1, q2, q3 / q02, q4, q5, q6), so
+    checkpoints interchange with the reference; seeded initialisation draws
+    in the reference's layer order."""
+
+    HEADS = (("q01", "q02"), ("q1", "q4"), ("q2", "q5"), ("q3", "q6"))
 
     def __init__(self, state_dim, action_dim, zs_dim=286, hdim=286, activ=F.elu):
         super().__init__()
         self.activ = activ
-        self.q01 = nn.Linear(state_dim + action_dim, hdim)
-        self.q1 = nn.Linear(2 * zs_dim + hdim, hdim)
-        self.q2 = nn.Linear(hdim, hdim)
-        self.q3 = nn.Linear(hdim, 1)
-        self.q02 = nn.Linear(state_dim + action_dim, hdim)
-        self.q4 = nn.Linear(2 * zs_dim + hdim, hdim)
-        self.q5 = nn.Linear(hdim, hdim)
-        self.q6 = nn.Linear(hdim, 1)
+        self.hdim, self.zs_dim = hdim, zs_dim
+        dims = [(state_dim + action_dim, hdim), (2 * zs_dim + hdim, hdim), (hdim, hdim), (hdim, 1)]
+        heads = [[nn.Linear(i, o) for i, o in dims] for _ in range(2)]  # reference creation order
+        for k, (i, o) in enumerate(dims):
+            self.register_parameter(f"w{k}", nn.Parameter(torch.stack([heads[0][k].weight.data,
+                                                                       heads[1][k].weight.data])))
+            self.register_parameter(f"b{k}", nn.Parameter(torch.stack([heads[0][k].bias.data,
+                                                                       heads[1][k].bias.data])))
+        self._register_state_dict_hook(Critic._to_reference_keys)
+        self._register_load_state_dict_pre_hook(Critic._from_reference_keys)
+
+    @staticmethod
+    def _to_reference_keys(module, sd, prefix, local_metadata):
+        for k, names in enumerate(Critic.HEADS):
+            w, b = sd.pop(prefix + f"w{k}"), sd.pop(prefix + f"b{k}")
+            for h, name in enumerate(names):
+                sd[prefix + name + ".weight"] = w[h].clone()
+                sd[prefix + name + ".bias"] = b[h].clone()
+        return sd
+
+    @staticmethod
+    def _from_reference_keys(sd, prefix, local_metadata, strict, missing, unexpected, errors):
+        for k, names in enumerate(Critic.HEADS):
+            if prefix + names[0] + ".weight" in sd:
+                sd[prefix + f"w{k}"] = torch.stack([sd.pop(prefix + n + ".weight") for n in names])
+                sd[prefix + f"b{k}"] = torch.stack([sd.pop(prefix + n + ".bias") for n in names])
 
     def forward(self, state, action, zsa, zs):
+        B, h = state.shape[0], self.hdim
         sa = torch.cat([state, action], 1)
         embeddings = torch.cat([zsa, zs], 1)
-        q1 = AvgL1Norm(self.q01(sa))
-        q1 = torch.cat([q1, embeddings], 1)
-        q1 = self.activ(self.q1(q1))
-        q1 = self.activ(self.q2(q1))
-        q1 = self.q3(q1)
-        q2 = AvgL1Norm(self.q02(sa))
-        q2 = torch.cat([q2, embeddings], 1)
-        q2 = self.activ(self.q4(q2))
-        q2 = self.activ(self.q5(q2))
-        q2 = self.q6(q2)
-        return torch.cat([q1, q2], 1)
+        # layer 0 of both heads as one GEMM: [B, in0] x [2h, in0]^T -> [B, 2, h]
+        q = F.linear(sa, self.w0.view(2 * h, -1), self.b0.view(2 * h)).view(B, 2, h)
+        q = AvgL1Norm(q)
+        x = torch.cat([q.transpose(0, 1), embeddings.unsqueeze(0).expand(2, B, embeddings.shape[1])], 2)
+        x = self.activ(torch.baddbmm(self.b1.unsqueeze(1), x, self.w1.transpose(1, 2)))
+        x = self.activ(torch.baddbmm(self.b2.unsqueeze(1), x, self.w2.transpose(1, 2)))
+        x = torch.baddbmm(self.b3.unsqueeze(1), x, self.w3.transpose(1, 2))  # [2, B, 1]
+        return x.squeeze(2).t()
 
 
 class GradSync:
@@ -181,8 +207,9 @@ class GradSync:
 
     def broadcast_module(self, m, src=0):
         if self.active:
-            for p in m.state_dict().values():
-                dist.broadcast(p, src, group=self.group)
+            with torch.no_grad():
+                for p in list(m.parameters()) + list(m.buffers()):
+                    dist.broadcast(p.data, src, group=self.group)
 
 
 class TD7Learner:
@@ -246,12 +273,14 @@ class TD7Learner:
         hp = self.hp
         # ---- encoder (:219-228)
         with self._autocast():
-            with torch.no_grad():
-                next_zs = self.encoder.zs(next_state)
-            zs = self.encoder.zs(state)
+            # zs(state) and zs(next_state) of the live encoder as one pass; the
+            # next-state half is detached (it is computed under no_grad at :220)
+            B = state.shape[0]
+            zs_all = self.encoder.zs(torch.cat([state, next_state], 0))
+            zs, next_zs = zs_all[:B], zs_all[B:].detach()
             pred_zs = self.encoder.zsa(zs, action)
         encoder_loss = F.mse_loss(pred_zs.float(), next_zs.float())
-        self.encoder_optimizer.zero_grad(set_to_none=False)
+        self.encoder_optimizer.zero_grad(set_to_none=True)
         encoder_loss.backward()
         # ---- critic (:233-257)
         with torch.no_grad():
@@ -276,7 +305,7 @@ class TD7Learner:
             Q = self.critic(state, action, fixed_zsa, fixed_zs)
         td_loss = (Q.float() - Q_target).abs()
         critic_loss = LAP_huber(td_loss)
-        self.critic_optimizer.zero_grad(set_to_none=False)
+        self.critic_optimizer.zero_grad(set_to_none=True)
         critic_loss.backward()
         self._fixed_zs = fixed_zs
         return td_loss.detach().max(1)[0].clamp(min=hp.min_priority).pow(hp.alpha)  # :262
@@ -296,7 +325,7 @@ class TD7Learner:
         if self.offline:
             actor_loss = actor_loss + self.hp.lmbda * Q.float().abs().mean().detach() * F.mse_loss(actor.float(),
                                                                                                action)
-        self.actor_optimizer.zero_grad(set_to_none=False)
+        self.actor_optimizer.zero_grad(set_to_none=True)
         actor_loss.backward()
 
     def phase_actor_step(self):
@@ -334,10 +363,10 @@ class TD7Learner:
         """:284-293; returns True when the targets were refreshed."""
         if self.training_steps % self.hp.target_update_rate != 0:
             return False
-        self.actor_target.load_state_dict(self.actor.state_dict())
-        self.critic_target.load_state_dict(self.critic.state_dict())
-        self.fixed_encoder_target.load_state_dict(self.fixed_encoder.state_dict())
-        self.fixed_encoder.load_state_dict(self.encoder.state_dict())
+        for dst, src in ((self.actor_target, self.actor), (self.critic_target, self.critic),
+                         (self.fixed_encoder_target, self.fixed_encoder), (self.fixed_encoder, self.encoder)):
+            with torch.no_grad():
+                torch._foreach_copy_(list(dst.parameters()), list(src.parameters()))
         self.sync_bounds()
         self.max_target.copy_(self.max)
         self.min_target.copy_(self.min)

@@ -161,6 +161,16 @@ int lap_reset_max(const lap_tree_desc *t, void *stream);
 /* Total priority of each stratum (root of its tree) -> out_dev[n_strata]. */
 int lap_totals(const lap_tree_desc *t, float *out_dev, void *stream);
 
+/* ------------------------------------------------------------------------
+ * Fused TD7 net pieces (Agent/TD7_multi_agent.py:53-54, AvgL1Norm).
+ * ---------------------------------------------------------------------- */
+/* y = x / max(mean|x|, eps) per row; mean_out[rows] keeps mean|x| for backward. */
+int td7_avgl1norm_fwd(const float *x_dev, float *y_dev, float *mean_out_dev, int32_t rows, int32_t cols, float eps,
+                      void *stream);
+/* gradient of the above w.r.t. x given dL/dy. */
+int td7_avgl1norm_bwd(const float *x_dev, const float *mean_dev, const float *gy_dev, float *gx_dev, int32_t rows,
+                      int32_t cols, float eps, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

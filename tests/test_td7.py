@@ -115,3 +115,34 @@ def test_two_train_steps_match_reference_on_gpu():
 def test_agent_train_step_through_lap_kernels():
     from exo_amd import td7
     td7.smoke()
+
+
+def test_critic_state_dict_uses_reference_names():
+    from exo_amd.td7 import Critic
+    c = Critic(80, 7, 16, 20)
+    sd = c.state_dict()
+    assert sorted(sd) == sorted(f"{n}.{p}" for n in ("q01", "q1", "q2", "q3", "q02", "q4", "q5", "q6")
+                                for p in ("weight", "bias"))
+    c2 = Critic(80, 7, 16, 20)
+    c2.load_state_dict(sd)
+    for a, b in zip(c.parameters(), c2.parameters()):
+        assert torch.equal(a, b)
+
+
+def test_loads_shipped_reference_checkpoint():
+    """Simulation/AGENT_NNS/[0,0,0,1] (reference, weights_only): the nets load
+    with the reference's names and the Pink-noise widths (actor 300)."""
+    import os
+    path = "/root/reference/Simulation/AGENT_NNS/[0,0,0,1]/[0,0,0,1]"
+    if not os.path.exists(path + "_actor"):
+        pytest.skip("reference checkpoints not present")
+    from exo_amd.td7 import Actor, Critic, Encoder
+    a, c, e = Actor(80, 7, 300, 300), Critic(80, 7, 300, 320), Encoder(80, 7, 300, 300)
+    a.load_state_dict(torch.load(path + "_actor", map_location="cpu", weights_only=True))
+    c.load_state_dict(torch.load(path + "_critic", map_location="cpu", weights_only=True))
+    e.load_state_dict(torch.load(path + "_encoder", map_location="cpu", weights_only=True))
+    s = torch.randn(4, 80)
+    act = a(s, e.zs(s))
+    assert act.shape == (4, 7) and torch.all(act.abs() <= 1)
+    q = c(s, act, e.zsa(e.zs(s), act), e.zs(s))
+    assert q.shape == (4, 2) and torch.isfinite(q).all()
