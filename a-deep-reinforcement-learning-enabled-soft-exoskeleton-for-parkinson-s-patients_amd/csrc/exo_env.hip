@@ -454,6 +454,7 @@ struct exo_ctx {
     std::vector<double> imu_host;
     std::vector<void *> allocs;
     float *obs_scratch = nullptr;
+    int step_variant = EXO_STEP_AUTO;
     std::string err;
 };
 
@@ -629,6 +630,10 @@ int exo_step(exo_ctx *c, const float *act_dev, float *obs_dev, float *rew_dev, u
              const uint8_t *active_dev, void *stream) {
     if (!c || !act_dev || !obs_dev || !rew_dev || !done_dev) return EXO_EINVAL;
     DeviceGuard g(c->device);
+    const bool rows = c->step_variant == EXO_STEP_ROWS || (c->step_variant == EXO_STEP_AUTO && c->N <= 16384);
+    if (rows)
+        return check(c, launch_exo_step_rp(c->S, c->U, act_dev, obs_dev, rew_dev, done_dev, info_dev, active_dev,
+                                           (hipStream_t)stream), "exo_step");
     const int threads = 256, lanes = 2 * c->N;
     hipLaunchKernelGGL(exo_step_kernel, dim3((lanes + threads - 1) / threads), dim3(threads), 0, (hipStream_t)stream,
                        c->S, c->U, act_dev, obs_dev, rew_dev, done_dev, info_dev, active_dev);
@@ -743,6 +748,12 @@ int exo_set_state_host(exo_ctx *c, int32_t env, const double *in) {
     for (int j = 0; j < 7 && !rc; ++j) rc = write1(c, c->S.prev2_a, j * N + env, in[40 + j]);
     for (int j = 0; j < 2 && !rc; ++j) rc = write1(c, c->S.maxSE, j * N + env, in[47 + j]);
     return rc;
+}
+
+int exo_set_step_variant(exo_ctx *c, int32_t variant) {
+    if (!c || variant < EXO_STEP_AUTO || variant > EXO_STEP_ROWS) return EXO_EINVAL;
+    c->step_variant = variant;
+    return EXO_OK;
 }
 
 int exo_set_seed(exo_ctx *c, uint64_t seed) {

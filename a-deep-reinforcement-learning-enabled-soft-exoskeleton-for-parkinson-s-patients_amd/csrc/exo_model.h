@@ -368,6 +368,12 @@ __host__ __device__ inline double philox_u01(uint64_t seed, uint32_t env, uint32
     return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
 }
 
+#ifndef EXO_HOST_ONLY
+// row-parallel step (csrc/exo_step_rp.hip): 16 lanes per env, for small env counts
+hipError_t launch_exo_step_rp(const Dev &S, const Urdf &U, const float *act, float *obs, float *rew, uint8_t *done,
+                              float *info, const uint8_t *active, hipStream_t stream);
+#endif
+
 // URDF numbers, Simulation/exo_v3.urdf (kept literally: 3.141593 is not pi)
 constexpr double J_XYZ[NJ][3] = {
     {0.010000, -0.475000, 1.200000}, {0, 0, 0}, {0, 0, 0}, {0.480000, 0, 0}, {0, 0, -0.000000},

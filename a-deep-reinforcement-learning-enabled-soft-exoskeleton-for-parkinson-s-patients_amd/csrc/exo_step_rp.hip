@@ -1,0 +1,369 @@
+// exo_step_rp.hip -- row-parallel variant of the env step for small env counts.
+//
+// exo_step_kernel (exo_env.hip) gives each ODE solve ONE lane: at 4,096 envs
+// that is 128 wavefronts on a 1,024-SIMD chip, so the step is bound by the
+// serial latency of ~36 RHS evaluations per lane.  Here every env gets 16
+// lanes: lanes 0-7 run the actuated solve, lanes 8-15 the tremor-only solve,
+// and lane r of a group owns joint row r of the 7-DOF ODE (row 7 pads).  The
+// RHS a = I^-1 (T - D v - K q) needs the other rows' q, v and r: they are
+// pulled with wavefront permutes (ds_bpermute) inside the 8-lane group; the
+// RK45 error norm is an 8-lane butterfly sum, so every lane of a group takes
+// the same step-size decisions.  The arithmetic is the same as the one-lane
+// kernel (same per-row summation orders), so the two variants agree to
+// rounding of the error-norm sum.
+//
+// Prologue: all lanes of an env compute the forward kinematics redundantly
+// (same instructions, no divergence); lane j < 7 of the actuated group
+// evaluates actuator j (force components, position/radius vectors, torque)
+// and the torque table is shared by permutes.  Reward, done, observation,
+// info and the carried state are written before the solves (none depends on
+// the ODE), the joint-target motor update after them.
+#include <hip/hip_runtime.h>
+
+#include "exo_amd.h"
+#include "exo_model.h"
+
+using namespace exo;
+
+namespace {
+
+__device__ __forceinline__ double cfg(const Dev &S, int k, int e) { return S.cfg[(size_t)k * S.N + e]; }
+
+// Row-r tables of the sparse RHS (padding entries point at row 7 with a zero coefficient).
+constexpr int RP_DCOL[8][4] = {{0, 1, 2, 3}, {0, 1, 2, 7}, {0, 1, 2, 7}, {0, 3, 7, 7},
+                               {4, 5, 6, 7}, {4, 5, 6, 7}, {4, 5, 6, 7}, {7, 7, 7, 7}};
+constexpr int RP_DSYM[8][4] = {{0, 1, 2, 3}, {1, 4, 5, -1}, {2, 5, 6, -1}, {3, 7, -1, -1},
+                               {8, 9, 10, -1}, {9, 11, 12, -1}, {10, 12, 13, -1}, {-1, -1, -1, -1}};
+constexpr int RP_ICOL[8][4] = {{0, 3, 6, 7}, {1, 2, 4, 5}, {1, 2, 4, 5}, {0, 3, 6, 7},
+                               {1, 2, 4, 5}, {1, 2, 4, 5}, {0, 3, 6, 7}, {7, 7, 7, 7}};
+constexpr int RP_ISYM[8][4] = {{0, 1, 2, -1}, {6, 7, 8, 9}, {7, 10, 11, 12}, {1, 3, 4, -1},
+                               {8, 11, 13, 14}, {9, 12, 14, 15}, {2, 4, 5, -1}, {-1, -1, -1, -1}};
+
+struct RowM {
+    double d[4], s[4], ii[4];
+    int dsrc[4], isrc[4];
+};
+
+__device__ __forceinline__ double shfl_d(double x, int src) { return __shfl(x, src, 64); }
+
+__device__ __forceinline__ double group_sum(double x) { // butterfly over the 8-lane group: identical in all lanes
+    x += __shfl_xor(x, 1, 64);
+    x += __shfl_xor(x, 2, 64);
+    x += __shfl_xor(x, 4, 64);
+    return x;
+}
+
+// acceleration of row r: I^-1 (T - D v - K q), neighbours pulled from the group
+__device__ __forceinline__ double row_acc(const RowM &M, double T, double q, double v) {
+    double dq = 0.0, kq = 0.0;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const double vv = shfl_d(v, M.dsrc[m]), qq = shfl_d(q, M.dsrc[m]);
+        dq += M.d[m] * vv;
+        kq += M.s[m] * qq;
+    }
+    const double r = T - dq - kq;
+    double a = 0.0;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) a += M.ii[m] * shfl_d(r, M.isrc[m]);
+    return a;
+}
+
+// scipy RK45 (common.py select_initial_step, rk.py _step_impl) for the row
+// this lane owns; same second-order storage as rk45_solve in exo_model.h.
+__device__ bool rk45_rows(const RowM &M, double T, double &q_out) {
+    const double rtol = 1e-3, atol = 1e-6, tb = DT, inv_sqrt14 = 1.0 / 3.7416573867739413;
+    double q = 0.0, v = 0.0;
+    double a0 = row_acc(M, T, q, v);
+    double h_abs;
+    {
+        const double x1 = a0 / atol;
+        const double d1 = sqrt(group_sum(x1 * x1)) * inv_sqrt14;
+        const double h0 = 1e-6;
+        const double y1v = h0 * a0;
+        const double a1 = row_acc(M, T, 0.0, y1v);
+        const double xq = y1v / atol, xv = (a1 - a0) / atol;
+        const double d2 = sqrt(group_sum(xq * xq + xv * xv)) * inv_sqrt14 / h0;
+        const double h1 = (d1 <= 1e-15 && d2 <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : pow(0.01 / fmax(d1, d2), 0.2);
+        h_abs = fmin(fmin(100 * h0, h1), tb);
+    }
+    double t = 0.0;
+    int guard = 0;
+    bool ok = true;
+    while (t != tb && ok) {
+        const double min_step = 10 * fabs(nextafter(t, INFINITY) - t);
+        if (h_abs < min_step) h_abs = min_step;
+        bool rejected = false, accepted = false;
+        while (!accepted) {
+            if (h_abs < min_step || ++guard > 4096) { ok = false; break; }
+            double t_new = t + h_abs;
+            if (t_new - tb > 0) t_new = tb;
+            const double h = t_new - t, h2 = h * h;
+            h_abs = fabs(h);
+            double A[7];
+            A[0] = a0;
+            double qs = 0.0, vs = 0.0;
+#pragma unroll
+            for (int st = 1; st < 6; ++st) {
+                double dv = 0.0, dq = 0.0;
+#pragma unroll
+                for (int l = 0; l < st; ++l) { dv += A[l] * RK_A[st][l]; dq += A[l] * RKN.AA[st][l]; }
+                vs = v + dv * h;
+                qs = q + RKN.C[st] * h * v + dq * h2;
+                A[st] = row_acc(M, T, qs, vs);
+            }
+            {
+                double dv = A[0] * RK_B[0], dq = A[0] * RKN.BB[0] + A[1] * RKN.BB[1];
+#pragma unroll
+                for (int l = 2; l < 5; ++l) { dv += A[l] * RK_B[l]; dq += A[l] * RKN.BB[l]; }
+                dv += A[5] * RK_B[5];
+                vs = v + h * dv; // y_new
+                qs = q + h * v + dq * h2;
+            }
+            A[6] = row_acc(M, T, qs, vs);
+            double ev = A[0] * RK_E[0], eq = A[0] * RKN.EE[0] + A[1] * RKN.EE[1];
+#pragma unroll
+            for (int l = 2; l < 6; ++l) { ev += A[l] * RK_E[l]; eq += A[l] * RKN.EE[l]; }
+            ev += A[6] * RK_E[6];
+            const double e_q = eq * h2 / (atol + fmax(fabs(q), fabs(qs)) * rtol);
+            const double e_v = ev * h / (atol + fmax(fabs(v), fabs(vs)) * rtol);
+            const double en = sqrt(group_sum(e_q * e_q + e_v * e_v)) * inv_sqrt14;
+            if (en < 1) {
+                double factor = (en == 0) ? 10.0 : fmin(10.0, 0.9 * pow(en, -0.2));
+                if (rejected) factor = fmin(1.0, factor);
+                h_abs *= factor;
+                t = t_new;
+                q = qs;
+                v = vs;
+                a0 = A[6];
+                accepted = true;
+            } else {
+                h_abs *= fmax(0.2, 0.9 * pow(en, -0.2));
+                rejected = true;
+            }
+        }
+    }
+    q_out = ok ? q : NAN;
+    return ok;
+}
+
+// CoM of link `link` (one of the 14 actuator anchors) given the FK frames.
+__device__ __forceinline__ void anchor(const Urdf &U, int link, const double *R2, const double *p0, const double *R4,
+                                       const double *p3, double *o) {
+    if (link == 5 || link == 6) xform(R4, p3, U.xyz[link], o);
+    else if (link >= 14) { o[0] = U.kbase[link - 14][0]; o[1] = U.kbase[link - 14][1]; o[2] = U.kbase[link - 14][2]; }
+    else xform(R2, p0, U.xyz[link], o);
+}
+
+__global__ __launch_bounds__(64) void exo_step_rp_kernel(Dev S, Urdf U, const float *__restrict__ act,
+                                                         float *__restrict__ obs, float *__restrict__ rew,
+                                                         uint8_t *__restrict__ done, float *__restrict__ info,
+                                                         const uint8_t *__restrict__ active) {
+    const int lane = threadIdx.x;
+    const int sub = lane & 15, grp = sub >> 3, r = sub & 7, gbase = lane & ~7, ebase = lane & ~15;
+    const int e = blockIdx.x * 4 + (lane >> 4);
+    if (e >= S.N) return;
+    const int N = S.N, c = S.counts[e], L = S.L[e];
+    if ((active && !active[e]) || c >= L - 1) return; // uniform over the env's 16 lanes
+
+    const double maxS = S.maxSE[e], maxE = S.maxSE[(size_t)N + e];
+    double F[7];
+    const float *a = act + (size_t)e * ACT;
+#pragma unroll
+    for (int j = 0; j < 7; ++j) F[j] = (((double)a[j] + 1) / 2) * (j < 2 ? maxE : maxS); // :256-266
+
+    // ---- forward kinematics of the state left by the last stepSimulation (all lanes)
+    double q5[5], refo[6], refn[6];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) q5[j] = S.phys_q[(size_t)j * N + e];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) refo[j] = S.ref[(size_t)j * N + e];
+    double R2[9], R4[9], p0[3], p3[3];
+    {
+        double Rt[9], R0[9], R1[9], R3[9], s, cc;
+        p0[0] = U.xyz[0][0]; p0[1] = U.xyz[0][1]; p0[2] = U.xyz[0][2] + 0.1;
+        sincos(q5[0], &s, &cc); mul_rz(U.Ro[0], cc, s, R0);
+        matmul3(R0, U.Ro[1], Rt); sincos(q5[1], &s, &cc); mul_rz(Rt, cc, s, R1);
+        matmul3(R1, U.Ro[2], Rt); sincos(q5[2], &s, &cc); mul_rz(Rt, cc, s, R2);
+        xform(R2, p0, U.xyz[3], p3);
+        matmul3(R2, U.Ro[3], Rt); sincos(q5[3], &s, &cc); mul_rz(Rt, cc, s, R3);
+        matmul3(R3, U.Ro[4], Rt); sincos(q5[4], &s, &cc); mul_rz(Rt, cc, s, R4);
+        refn[0] = p0[0]; refn[1] = p0[1]; refn[2] = p0[2];
+        xform(R3, p3, U.com3, &refn[3]);
+    }
+
+    // ---- actuator j = r (lanes r == 7 duplicate actuator 6 and discard it)
+    const int j = r < 7 ? r : 6;
+    double k1[3], k2[3], tx, ty, tz;
+    float pv[3];
+    {
+        anchor(U, K_LINK[2 * j], R2, p0, R4, p3, k1);
+        anchor(U, K_LINK[2 * j + 1], R2, p0, R4, p3, k2);
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            k1[d] += S.shift[(size_t)((2 * j) * 3 + d) * N + e];
+            k2[d] += S.shift[(size_t)((2 * j + 1) * 3 + d) * N + e];
+        }
+        const double dx = (k2[0] + 5) - (k1[0] + 5), dy = (k2[1] + 5) - (k1[1] + 5), dz = (k2[2] + 5) - (k1[2] + 5);
+        const double Fj = (((double)a[j] + 1) / 2) * (j < 2 ? maxE : maxS);
+        const double fx = cos_atan2(dy, dx) * Fj, fy = cos_atan2(dx, dy) * Fj, fz = cos_atan2(dz, dx) * Fj;
+        const int ro = (j < 2) ? 3 : 0; // elbow reference for actuators 1, 2
+#pragma unroll
+        for (int d = 0; d < 3; ++d) pv[d] = (float)(k2[d] - (ro ? refo[3 + d] : refo[d])); // stale ref (A.3)
+        const double r0 = (ro ? refn[3] : refn[0]) - k2[0], r1 = (ro ? refn[4] : refn[1]) - k2[1],
+                     r2 = (ro ? refn[5] : refn[2]) - k2[2];
+        tx = fy * r2 - fz * r1;
+        ty = fz * r0 - fx * r2;
+        tz = fx * r1 - fy * r0;
+    }
+    // torque table of the env: pull the actuated group's lanes 0..6
+    double tau[7][3];
+#pragma unroll
+    for (int jj = 0; jj < 7; ++jj) {
+        tau[jj][0] = shfl_d(tx, ebase + jj);
+        tau[jj][1] = shfl_d(ty, ebase + jj);
+        tau[jj][2] = shfl_d(tz, ebase + jj);
+    }
+    double at[4]; // :394-400, actuator order 3, 4, 5, 7, 6
+    at[0] = tau[2][1] + tau[3][1] + tau[4][1] + tau[6][1] + tau[5][1];
+    at[1] = tau[2][0] + tau[3][0] + tau[4][0] + tau[6][0] + tau[5][0];
+    at[2] = tau[2][2] + tau[3][2] + tau[4][2] + tau[6][2] + tau[5][2];
+    at[3] = fabs(tau[0][1]) - fabs(tau[1][1]);
+    double tr[7], Ta[7], pa[7], pa2[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+        tr[i] = S.tremor[((size_t)c * 7 + i) * N + e];
+        Ta[i] = tr[i] + (i < 4 ? at[i] : 0.0);
+        pa[i] = S.prev_a[(size_t)i * N + e];
+        pa2[i] = S.prev2_a[(size_t)i * N + e];
+    }
+    // per-lane values of this lane's actuator j / joint row r (dynamic indices
+    // into small register arrays would go to scratch)
+    const double F_j = (((double)a[j] + 1) / 2) * (j < 2 ? maxE : maxS);
+    const double pa_j = S.prev_a[(size_t)j * N + e];
+    const double tr_r = (r < 7) ? S.tremor[((size_t)c * 7 + r) * N + e] : 0.0;
+    const double at_r = (r == 0) ? at[0] : (r == 1) ? at[1] : (r == 2) ? at[2] : (r == 3) ? at[3] : 0.0;
+    const double Ta_r = tr_r + at_r;
+    // every lane has read the carried state it needs; lanes of this env now
+    // overwrite it (counts, ref, posv, prev actions, later the joints)
+    __syncthreads();
+
+    // ---- reward, done, observation, info, carried state (:341-366, :448-469, :487-570)
+    if (grp == 0) {
+        if (r == 0) {
+            const int seq = S.seq[e];
+            const double eps = 1e-10, Msum = maxE + maxS, naxes = cfg(S, C_NAXES, e);
+            double unw = 0.0, st = 0.0, sa = 0.0, sm = 0.0;
+            int nred = 0;
+#pragma unroll
+            for (int i = 0; i < 7; ++i) {
+                const double Tabs = fabs(Ta[i]), tabs = fabs(tr[i]);
+                if (i < 4) {
+                    if ((seq >> i) & 1) st += (Tabs - tabs) / tabs + 1;
+                    else unw += Tabs;
+                }
+                const double vv = (Tabs - tabs) / (tabs + eps) * 100;
+                if (isfinite(vv) && vv < 0) nred++;
+                sa += F[i];
+                const double d = F[i] - 2 * pa[i] + pa2[i];
+                sm += d * d;
+            }
+            sm /= 7;
+            const double r_unw = exp(-(unw / (Msum / 4 / naxes)) + eps) * 0.5;
+            const double r_tor = exp((-st + eps) / naxes) * 0.9;
+            const double r_axis = nred * 0.5;
+            const double r_ctl = exp(-(sa / (Msum / 2)) + eps) * 0.05;
+            const double r_sm = 0.05 * exp(-(sm / (Msum / 4)) + eps);
+            rew[e] = (float)((r_axis + r_tor + r_sm + r_ctl + r_unw) / cfg(S, C_MAXREW, e));
+            done[e] = (uint8_t)(c + 1 >= L - 1);
+            if (info) {
+                float *io = info + (size_t)e * INFO;
+                io[35] = (float)r_unw; io[36] = (float)r_tor; io[37] = (float)r_axis; io[38] = (float)r_ctl;
+                io[39] = (float)r_sm;
+            }
+            S.counts[e] = c + 1;
+        }
+        float *o = obs + (size_t)e * OBS;
+        if (r < 7) {
+            const double nrm = j < 2 ? cfg(S, C_MAXE0, e) : cfg(S, C_MAXS0, e);
+            o[j] = (float)((c > 2 ? pa_j : 0.0) / nrm); // forces at c-1 (zero on an episode's first step)
+            o[7 + j] = (float)(F_j / nrm);
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                const size_t idx = (size_t)(j * 3 + d) * N + e;
+                o[26 + j * 3 + d] = S.posv[idx];
+                o[47 + j * 3 + d] = pv[d];
+                S.posv[idx] = pv[d];
+            }
+            if (info) {
+                float *io = info + (size_t)e * INFO;
+                io[j] = (float)at_r;
+                io[7 + j] = (float)Ta_r;
+                io[21 + j] = (float)tr_r;
+            }
+            S.prev2_a[(size_t)j * N + e] = pa_j;
+            S.prev_a[(size_t)j * N + e] = F_j;
+        } else { // lane 7: the reference link positions
+#pragma unroll
+            for (int d = 0; d < 6; ++d) {
+                o[68 + d] = (float)refo[d];
+                o[74 + d] = (float)refn[d];
+                S.ref[(size_t)d * N + e] = refn[d];
+            }
+        }
+    } else if (r < 4) { // tremor rows 0..3 at c-1, c, c+1
+        const double tn = (r < 3) ? 10.0 : 5.0;
+        float *o = obs + (size_t)e * OBS;
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            const double v = (b == 1) ? tr_r : S.tremor[((size_t)(c - 1 + b) * 7 + r) * N + e];
+            o[14 + b * 4 + r] = (float)(v / tn);
+        }
+    }
+
+    // ---- the two joint ODE solves (:409-414), one row per lane
+    RowM M;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int ds = RP_DSYM[r][m], is = RP_ISYM[r][m];
+        M.d[m] = ds >= 0 ? S.dnz[(size_t)ds * N + e] : 0.0;
+        M.s[m] = ds >= 0 ? S.snz[(size_t)ds * N + e] : 0.0;
+        M.ii[m] = is >= 0 ? S.iinv[(size_t)is * N + e] : 0.0;
+        M.dsrc[m] = gbase + RP_DCOL[r][m];
+        M.isrc[m] = gbase + RP_ICOL[r][m];
+    }
+    const double T = (r < 7) ? (grp == 0 ? Ta_r : tr_r) : 0.0;
+    double qr;
+    if (!rk45_rows(M, T, qr)) atomicOr(S.err, 1);
+    const double qdeg = qr * (180 / PI); // :417-418
+    if (info && r < 7) info[(size_t)e * INFO + (grp == 0 ? 14 : 28) + r] = (float)qdeg;
+    if (grp != 0) return;
+
+    // ---- :421-433 joint targets and the idealised motor step
+    // lane r holds q[r]: joint 0 (shoulder z) <- q[2], 1 (y) <- q[0], 2 (x) <- q[1], 3 (elbow y) <- q[3]
+    const int joint = (r == 0) ? 1 : (r == 1) ? 2 : (r == 2) ? 0 : r; // r = 3, 4 -> joints 3, 4
+    const double *imu = S.imu + (size_t)S.motion[e] * 5 * S.Lmax;
+    const int col = (joint == 0) ? 4 : (joint == 1) ? 3 : (joint == 2) ? 2 : (joint == 3) ? 0 : 1;
+    const double ang = imu[col * S.Lmax + c] + (joint < 4 ? qdeg : 0.0);
+    bool viol = false;
+    if (r < 5) {
+        const double q0 = S.phys_q[(size_t)joint * N + e];
+        const double nq = q0 + 0.1 * (ang * (PI / 180) - q0);
+        S.phys_q[(size_t)joint * N + e] = fmin(fmax(nq, U.lo[joint]), U.hi[joint]);
+        const double lo[4] = {-80, -40, -151.5, -10}, hi[4] = {80, 160.5, 33.5, 150};
+        if (joint < 4) viol = !(lo[joint] < ang && ang < hi[joint]); // check_movement_boundaries (:594-605)
+    }
+    const unsigned long long m = __ballot(viol);
+    if (r == 0 && ((m >> ebase) & 0xFull)) S.viol[e] += 1;
+}
+
+} // namespace
+
+namespace exo {
+hipError_t launch_exo_step_rp(const Dev &S, const Urdf &U, const float *act, float *obs, float *rew, uint8_t *done,
+                              float *info, const uint8_t *active, hipStream_t stream) {
+    hipLaunchKernelGGL(exo_step_rp_kernel, dim3((S.N + 3) / 4), dim3(64), 0, stream, S, U, act, obs, rew, done, info,
+                       active);
+    return hipGetLastError();
+}
+} // namespace exo

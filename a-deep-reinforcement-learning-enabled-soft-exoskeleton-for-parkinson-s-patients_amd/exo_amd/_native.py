@@ -54,6 +54,7 @@ EXPORTS = {
     "exo_get_state_host": (c_int32, [c_void_p, c_int32, P(c_double)]),
     "exo_set_state_host": (c_int32, [c_void_p, c_int32, P(c_double)]),
     "exo_set_seed": (c_int32, [c_void_p, c_uint64]),
+    "exo_set_step_variant": (c_int32, [c_void_p, c_int32]),
     "exo_last_error": (ctypes.c_char_p, [c_void_p]),
     "exo_destroy": (None, [c_void_p]),
     "lap_tree_floats": (c_int32, [c_int32, c_int32]),

@@ -150,6 +150,14 @@ class VecExoskeletonEnv:
         if tuple(t.shape) != shape or t.dtype != dtype or not t.is_contiguous():
             raise ValueError(f"output buffer must be contiguous {dtype} {shape}")
 
+    STEP_VARIANTS = {"auto": 0, "lanes": 1, "rows": 2}
+
+    def set_step_variant(self, name):
+        """exo_step kernel: 'lanes' (one lane per ODE solve), 'rows' (16 lanes per
+        env), 'auto' (rows for N <= 16384)."""
+        nat.check(nat.lib().exo_set_step_variant(self._ctx, self.STEP_VARIANTS[name]), "exo_set_step_variant",
+                  self._ctx)
+
     # ------------------------------------------------------- parity / debug
     def reset_from_draws(self, env_ids, draws, obs_out=None):
         """Reset envs from explicit unit-uniform draw streams (the reference's

@@ -110,6 +110,15 @@ int exo_episode_host(exo_ctx *ctx, int32_t env, double *D49, double *S49, double
 int exo_get_state_host(exo_ctx *ctx, int32_t env, double *out);
 int exo_set_state_host(exo_ctx *ctx, int32_t env, const double *in);
 
+/* Kernel variant of exo_step: EXO_STEP_LANES = one lane per ODE solve (best
+ * throughput at large N), EXO_STEP_ROWS = 16 lanes per env, one joint row per
+ * lane (lowest latency at small N), EXO_STEP_AUTO (default) = ROWS for
+ * N <= 16384.  Both compute the same step. */
+#define EXO_STEP_AUTO 0
+#define EXO_STEP_LANES 1
+#define EXO_STEP_ROWS 2
+int exo_set_step_variant(exo_ctx *ctx, int32_t variant);
+
 /* Re-key the Philox draw streams of later resets (ExoskeletonEnv_train.seed, :189-191). */
 int exo_set_seed(exo_ctx *ctx, uint64_t seed);
 

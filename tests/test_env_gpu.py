@@ -26,7 +26,10 @@ def _close_obs(a, b):
     np.testing.assert_allclose(a, b, rtol=2e-6, atol=2e-6)
 
 
-def _batched_golden_env():
+VARIANTS = ["rows", "lanes"]
+
+
+def _batched_golden_env(variant="auto"):
     from exo_amd import VecExoskeletonEnv
     gold = [golden_env(m) for m in range(8)]
     kw = {}
@@ -34,6 +37,7 @@ def _batched_golden_env():
     for k in per[0]:
         kw[k] = np.stack([np.asarray(p[k], dtype=np.float64) for p in per])
     env = VecExoskeletonEnv(8, motions=list(range(8)), seed=5, **kw)
+    env.set_step_variant(variant)
     # exo_create already ran the constructor's initialize_movement on Philox
     # draws; the goldens' episode 0 IS that constructor call, whose link-read
     # cache is still all zeros (Exoskeleton_sim_pybullet.py:80-81).  Restore
@@ -64,10 +68,11 @@ def test_reset_matches_reference_draws():
                 assert st[0] == 2 and st[50] == d["L"] and st[51] == m
 
 
-def test_steps_match_reference_traces_with_active_mask():
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_steps_match_reference_traces_with_active_mask(variant):
     """All 8 motions in one batch; envs whose golden episode is shorter wait
     (inactive) like the training script's per-env `done` skip."""
-    env, gold = _batched_golden_env()
+    env, gold = _batched_golden_env(variant)
     env.reset_from_draws(list(range(8)), [d["ep0_draws"] for d in gold])
     out = env.new_outputs(True)
     for ep in (1, 2):
@@ -100,9 +105,11 @@ def test_steps_match_reference_traces_with_active_mask():
                 assert idx[m].size == int(gold[m]["L"]) - 3
 
 
-def test_done_envs_are_skipped():
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_done_envs_are_skipped(variant):
     from exo_amd import VecExoskeletonEnv
     env = VecExoskeletonEnv(8, seed=3)
+    env.set_step_variant(variant)
     env.reset()
     out = env.new_outputs(True)
     a = torch.zeros((8, 7), device=env.device)
@@ -113,12 +120,14 @@ def test_done_envs_are_skipped():
     np.testing.assert_array_equal(st, L - 1)
 
 
-def test_philox_path_matches_oracle_at_scale():
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_philox_path_matches_oracle_at_scale(variant):
     """4096 envs on Philox draws; a sample of envs is replayed on the oracle
     with the same draw streams and random actions."""
     from exo_amd import VecExoskeletonEnv, motions
     N, seed = 4096, 99
     env = VecExoskeletonEnv(N, seed=seed)  # episode 0 drawn by the constructor
+    env.set_step_variant(variant)
     obs0 = env.reset().cpu().numpy()       # episode 1
     angles, lengths = motions.load()
     lib = model_host()
@@ -193,3 +202,25 @@ def test_drop_in_single_env_api():
     assert mx.shape == (7,) and mx[1] > 0 and mx[0] == 0
     assert len(env.return_original_joint_angles()) == 7
     env.close()
+
+
+def test_kernel_variants_agree():
+    """Row-parallel and one-lane-per-solve kernels on identical states (N not a
+    multiple of 4 to exercise the partial last block)."""
+    from exo_amd import VecExoskeletonEnv
+    envs = []
+    for v in VARIANTS:
+        e = VecExoskeletonEnv(1030, seed=21)
+        e.set_step_variant(v)
+        e.reset()
+        envs.append(e)
+    rng = np.random.default_rng(4)
+    for k in range(40):
+        a = torch.as_tensor(rng.uniform(-1, 1, (1030, 7)).astype(np.float32), device=envs[0].device)
+        outs = [e.step(a) for e in envs]
+        o0, o1 = [[t.cpu().numpy() for t in (o[0], o[1], o[3])] for o in outs]
+        np.testing.assert_allclose(o0[0], o1[0], rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(o0[1], o1[1], rtol=1e-6, atol=1e-8)
+        np.testing.assert_allclose(o0[2], o1[2], rtol=1e-5, atol=1e-7)
+    for i in (0, 513, 1029):
+        np.testing.assert_allclose(envs[0].get_state(i), envs[1].get_state(i), rtol=1e-9, atol=1e-12)
