@@ -25,6 +25,24 @@
 
 using namespace exo;
 
+// Diagnostic build only (make STAMPS=1 -> libexo_amd_stamps.so): per-wave
+// s_memtime stamps at the phase boundaries of the step; the product build
+// compiles them out.
+#ifdef EXO_STAMPS
+__device__ unsigned long long *g_exo_stamps;
+#define STAMP(k)                                                                                                  \
+    do {                                                                                                          \
+        unsigned long long _t;                                                                                    \
+        __builtin_amdgcn_sched_barrier(0);                                                                        \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                             \
+        __builtin_amdgcn_sched_barrier(0);                                                                        \
+        if (g_exo_stamps && (threadIdx.x & 63) == __builtin_amdgcn_readfirstlane(threadIdx.x & 63))               \
+            g_exo_stamps[(size_t)blockIdx.x * 8 + (k)] = _t;                                                      \
+    } while (0)
+#else
+#define STAMP(k) do {} while (0)
+#endif
+
 namespace {
 
 __device__ __forceinline__ double cfg(const Dev &S, int k, int e) { return S.cfg[(size_t)k * S.N + e]; }
@@ -165,6 +183,7 @@ __global__ __launch_bounds__(64) void exo_step_rp_kernel(Dev S, Urdf U, const fl
     if (e >= S.N) return;
     const int N = S.N, c = S.counts[e], L = S.L[e];
     if ((active && !active[e]) || c >= L - 1) return; // uniform over the env's 16 lanes
+    STAMP(0);
 
     const double maxS = S.maxSE[e], maxE = S.maxSE[(size_t)N + e];
     double F[7];
@@ -192,6 +211,7 @@ __global__ __launch_bounds__(64) void exo_step_rp_kernel(Dev S, Urdf U, const fl
         xform(R3, p3, U.com3, &refn[3]);
     }
 
+    STAMP(1);
     // ---- actuator j = r (lanes r == 7 duplicate actuator 6 and discard it)
     const int j = r < 7 ? r : 6;
     double k1[3], k2[3], tx, ty, tz;
@@ -216,6 +236,7 @@ __global__ __launch_bounds__(64) void exo_step_rp_kernel(Dev S, Urdf U, const fl
         ty = fz * r0 - fx * r2;
         tz = fx * r1 - fy * r0;
     }
+    STAMP(2);
     // torque table of the env: pull the actuated group's lanes 0..6
     double tau[7][3];
 #pragma unroll
@@ -321,6 +342,7 @@ __global__ __launch_bounds__(64) void exo_step_rp_kernel(Dev S, Urdf U, const fl
         }
     }
 
+    STAMP(3);
     // ---- the two joint ODE solves (:409-414), one row per lane
     RowM M;
 #pragma unroll
@@ -335,6 +357,7 @@ __global__ __launch_bounds__(64) void exo_step_rp_kernel(Dev S, Urdf U, const fl
     const double T = (r < 7) ? (grp == 0 ? Ta_r : tr_r) : 0.0;
     double qr;
     if (!rk45_rows(M, T, qr)) atomicOr(S.err, 1);
+    STAMP(4);
     const double qdeg = qr * (180 / PI); // :417-418
     if (info && r < 7) info[(size_t)e * INFO + (grp == 0 ? 14 : 28) + r] = (float)qdeg;
     if (grp != 0) return;
@@ -355,9 +378,16 @@ __global__ __launch_bounds__(64) void exo_step_rp_kernel(Dev S, Urdf U, const fl
     }
     const unsigned long long m = __ballot(viol);
     if (r == 0 && ((m >> ebase) & 0xFull)) S.viol[e] += 1;
+    STAMP(5);
 }
 
 } // namespace
+
+#ifdef EXO_STAMPS
+extern "C" int exo_debug_set_stamps(unsigned long long *buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_exo_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -5;
+}
+#endif
 
 namespace exo {
 hipError_t launch_exo_step_rp(const Dev &S, const Urdf &U, const float *act, float *obs, float *rew, uint8_t *done,

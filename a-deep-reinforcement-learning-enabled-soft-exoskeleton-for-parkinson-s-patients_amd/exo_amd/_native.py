@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must be imported before the HIP library is loaded)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(HERE)
-LIB_PATH = os.path.join(HERE, "_lib", "libexo_amd.so")
+LIB_PATH = os.path.join(HERE, "_lib", os.environ.get("EXO_AMD_LIB", "libexo_amd.so"))
 CSRC = os.path.join(PKG_ROOT, "csrc")
 
 EXO_OK = 0
