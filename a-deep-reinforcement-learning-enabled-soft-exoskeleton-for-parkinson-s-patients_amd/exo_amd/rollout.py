@@ -10,8 +10,8 @@ Everything inside an iteration is device work with no host synchronisation,
 so it is captured once into HIP graphs and replayed:
   * world == 1: one graph per policy-update parity (actor updated or not);
   * world  > 1: the gradient all-reduces (RCCL) run eagerly between graphs
-    (pre: rollout + encoder/critic grads, mid: optimiser steps + priorities +
-    actor grads, post: actor step).
+    on flat buckets the graphs pack and unpack (pre: rollout + encoder/critic
+    grads, mid: optimiser steps + priorities + actor grads, post: actor step).
 Host-side bookkeeping left outside the graphs: the env reset at the end of a
 round, the target-network refresh every 250 steps (:284-293).
 """
@@ -19,6 +19,32 @@ import numpy as np
 import torch
 
 from . import _native as nat
+
+
+def graph_reductions_ok(device, rows=1024, cols=300, replays=3):
+    """Replay a captured multi-block column reduction a few times and compare
+    with eager sums; raise if the HIP runtime replays it wrongly (see
+    exo_amd/__init__.py: DEBUG_CLR_GRAPH_PACKET_CAPTURE must be 0 before the
+    first GPU call of the process).  ~1 ms, once per trainer."""
+    gen = torch.Generator(device=device).manual_seed(0)
+    x = torch.randn(rows, cols, device=device, generator=gen)
+    s = torch.cuda.Stream(device=device)
+    s.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(s):
+        x.sum(0)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            out = x.sum(0)
+    torch.cuda.current_stream(device).wait_stream(s)
+    for _ in range(replays):
+        x.mul_(1.5)
+        g.replay()
+        if not torch.allclose(out, x.sum(0), rtol=1e-4, atol=1e-3):
+            raise RuntimeError(
+                "HIP graph replay of torch reductions is wrong in this process (ROCm CLR graph packet "
+                "capture). Set DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 before the first GPU call -- importing "
+                "exo_amd before touching the GPU does it -- or use VecTrainer(use_graphs=False).")
+    return True
 
 
 class VecTrainer:
@@ -41,8 +67,10 @@ class VecTrainer:
         self.warmup_eager = warmup_eager
         self.iters = 0
         self.graphs = {}
-        self.dp = agent.sync.active
+        self.dp = agent.sync.active  # tests set it to exercise the 3-graph layout at world 1
         self.last_actions = None
+        if use_graphs:
+            graph_reductions_ok(self.device)
 
     # ----------------------------------------------------------- pieces
     def _rollout(self):
@@ -94,19 +122,26 @@ class VecTrainer:
                     self._post(update_actor)
                 parts = [g]
             else:
-                L = self.agent.learner
+                # Each parity's graphs own their gradient buffers (set_to_none
+                # grads are allocated inside the capture), so the all-reduces
+                # work on flat buckets packed/unpacked inside the graphs.
+                L, S = self.agent.learner, self.agent.sync
                 g1, g2, g3 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g1, pool=pool, stream=s):
                     self._pre()
+                    flat_c = S.pack(L.grad_params())
                 pool = g1.pool()
-                L.sync.allreduce_grads(L.grad_params())
+                flat_a = None
                 with torch.cuda.graph(g2, pool=pool, stream=s):
+                    S.unpack(flat_c, L.grad_params())
                     self._mid(update_actor)
-                if update_actor:
-                    L.sync.allreduce_grads(L.grad_params(actor=True))
+                    if update_actor:
+                        flat_a = S.pack(L.grad_params(actor=True))
                 with torch.cuda.graph(g3, pool=pool, stream=s):
+                    if update_actor:
+                        S.unpack(flat_a, L.grad_params(actor=True))
                     self._post(update_actor)
-                parts = [g1, g2, g3]
+                parts = [g1, g2, g3, flat_c, flat_a]
         torch.cuda.current_stream(self.device).wait_stream(s)
         self.graphs[update_actor] = parts
         # capture records but does not execute: run the iteration now
@@ -117,13 +152,14 @@ class VecTrainer:
         if not self.dp:
             parts[0].replay()
             return
-        L = self.agent.learner
-        parts[0].replay()
-        L.sync.allreduce_grads(L.grad_params())
-        parts[1].replay()
+        S = self.agent.sync
+        g1, g2, g3, flat_c, flat_a = parts
+        g1.replay()
+        S.allreduce_flat(flat_c)
+        g2.replay()
         if update_actor:
-            L.sync.allreduce_grads(L.grad_params(actor=True))
-        parts[2].replay()
+            S.allreduce_flat(flat_a)
+        g3.replay()
 
     # ------------------------------------------------------------- step
     def step(self):

@@ -200,6 +200,26 @@ class GradSync:
             g.copy_(flat[off:off + n].view_as(g))
             off += n
 
+    # Graph-friendly split of allreduce_grads: pack/unpack are captured inside
+    # the HIP graphs around an eager all-reduce of the static flat bucket, so
+    # the collective always sees the gradient buffers the graph wrote.
+    @staticmethod
+    def pack(params):
+        return torch.cat([p.grad.reshape(-1) for p in params if p.grad is not None])
+
+    def unpack(self, flat, params):
+        off = 0
+        for p in params:
+            if p.grad is None:
+                continue
+            n = p.grad.numel()
+            torch.mul(flat[off:off + n].view_as(p.grad), 1.0 / self.world, out=p.grad)
+            off += n
+
+    def allreduce_flat(self, flat):
+        if self.active:
+            dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+
     def max_(self, t):
         if self.active:
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
@@ -243,6 +263,9 @@ class TD7Learner:
         self.checkpoint_encoder = copy.deepcopy(self.encoder)
         self.offline = offline
         self.training_steps = 0
+        # True: gradients are freed and re-created by each backward (no zeroing
+        # kernels); False keeps persistent buffers zeroed in place
+        self.grads_to_none = True
         # device-resident scalars (:183-186, :236-237)
         f32 = dict(device=self.device, dtype=torch.float32)
         self.max = torch.tensor(-1e8, **f32)
@@ -280,7 +303,7 @@ class TD7Learner:
             zs, next_zs = zs_all[:B], zs_all[B:].detach()
             pred_zs = self.encoder.zsa(zs, action)
         encoder_loss = F.mse_loss(pred_zs.float(), next_zs.float())
-        self.encoder_optimizer.zero_grad(set_to_none=True)
+        self.encoder_optimizer.zero_grad(set_to_none=self.grads_to_none)
         encoder_loss.backward()
         # ---- critic (:233-257)
         with torch.no_grad():
@@ -305,7 +328,7 @@ class TD7Learner:
             Q = self.critic(state, action, fixed_zsa, fixed_zs)
         td_loss = (Q.float() - Q_target).abs()
         critic_loss = LAP_huber(td_loss)
-        self.critic_optimizer.zero_grad(set_to_none=True)
+        self.critic_optimizer.zero_grad(set_to_none=self.grads_to_none)
         critic_loss.backward()
         self._fixed_zs = fixed_zs
         return td_loss.detach().max(1)[0].clamp(min=hp.min_priority).pow(hp.alpha)  # :262
@@ -325,7 +348,7 @@ class TD7Learner:
         if self.offline:
             actor_loss = actor_loss + self.hp.lmbda * Q.float().abs().mean().detach() * F.mse_loss(actor.float(),
                                                                                                action)
-        self.actor_optimizer.zero_grad(set_to_none=True)
+        self.actor_optimizer.zero_grad(set_to_none=self.grads_to_none)
         actor_loss.backward()
 
     def phase_actor_step(self):

@@ -27,6 +27,9 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(REPO, "a-deep-reinforcement-learning-enabled-soft-exoskeleton-for-parkinson-s-patients_amd")
 sys.path.insert(0, PKG)
 
+# before the HIP runtime initialises (see exo_amd/__init__.py)
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -101,10 +104,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # test hooks: EXO_BENCH_DEVICE pins every rank to one GPU, EXO_DIST_BACKEND=gloo
+    # (tests/test_dp_gpu.py runs 2 ranks on a 1-GPU box); the driver uses RCCL.
+    local = int(os.environ.get("EXO_BENCH_DEVICE", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    backend = os.environ.get("EXO_DIST_BACKEND", "nccl")
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     from exo_amd import VecExoskeletonEnv
 
     N = args.envs
@@ -121,7 +131,7 @@ def main():
                       process_group=dist.group.WORLD if world > 1 else None, graph_safe=not args.eager)
         trainer = VecTrainer(env, agent, use_graphs=not args.eager)
     out = env.new_outputs(True)
-    state = {"k": 0, "obs": env.reset()}
+    state = {"k": 0, "obs": env.reset() if trainer is None else None}  # the trainer resets its envs itself
     ev = []
 
     def one_step(timed):
@@ -178,13 +188,26 @@ def main():
         kern_ms, kern_active = kernel_timing(min(args.kernel_timing_steps, int(Ls.min()) - 3))
     t = torch.tensor([elapsed, float(env_steps)], device=dev, dtype=torch.float64)
     if world > 1:
-        tmax = t.clone()
+        tmax, tsum = t.clone(), t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tsum = t.clone()
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
         elapsed, total_env_steps = float(tmax[0]), float(tsum[1])
     else:
         total_env_steps = float(env_steps)
+    finite = None
+    if agent is not None:
+        finite = {n: bool(torch.isfinite(torch.cat([p.detach().reshape(-1) for p in m.parameters()])).all())
+                  for n, m in (("actor", agent.learner.actor), ("critic", agent.learner.critic),
+                               ("encoder", agent.learner.encoder))}
+    dp_sync = dp_ck = None
+    if agent is not None and world > 1:
+        # data-parallel replicas must hold bit-identical weights
+        ck = torch.stack([torch.cat([p.detach().reshape(-1) for p in m.parameters()]).double().sum()
+                          for m in (agent.learner.actor, agent.learner.critic, agent.learner.encoder)])
+        allck = [torch.zeros_like(ck) for _ in range(world)]
+        dist.all_gather(allck, ck)
+        dp_sync = all(torch.equal(allck[0], x) for x in allck)
+        dp_ck = [x.tolist() for x in allck]
     if rank == 0:
         active_avg = kern_active
         achieved = BYTES_PER_ENV_STEP * active_avg / (kern_ms * 1e-3) / 1e9
@@ -203,7 +226,7 @@ def main():
                                    + (", TD7 batch 8x128" if agent else ", env only"),
                        "envs_per_gpu": N, "mode": args.mode, "parallelism": f"env-shard x{world}"
                        + (" + TD7 DP all-reduce" if agent and world > 1 else "")},
-            "roofline": {"kernel": "exo_step_kernel", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+            "roofline": {"kernel": "exo_step_rp_kernel" if N <= 16384 else "exo_step_kernel", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_unit": "bytes per launch", "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": BYTES_PER_ENV_STEP * active_avg,
@@ -212,6 +235,12 @@ def main():
         }
         if agent is not None:
             res["grad_steps_per_sec"] = args.steps / elapsed
+        if finite is not None:
+            res["weights_finite"] = all(finite.values()) or finite
+        if dp_sync is not None:
+            res["dp_weights_in_sync"] = dp_sync
+            if not dp_sync:
+                res["dp_weight_checksums"] = dp_ck
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds)
         print(json.dumps(res))

@@ -1,6 +1,9 @@
 import os
 import sys
 
+# before the HIP runtime initialises in this process (see exo_amd/__init__.py)
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -48,3 +48,16 @@ def test_graph_replay_is_deterministic_for_identical_seeds():
     torch.cuda.synchronize()
     for p, q in zip(snap, a2.learner.actor.parameters()):
         torch.testing.assert_close(p, q, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("layout", ["single", "split"])
+def test_graph_replay_matches_eager_numerics(layout):
+    """Same seeds -> the graph-replayed iterations (both parities, several
+    replays each) train the nets to the same weights as eager execution.
+    'split' is the data-parallel 3-graph layout (pack/unpack around the
+    gradient all-reduce), exercised here at world size 1."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import graph_vs_eager
+    assert graph_vs_eager.run(layout, iters=10) <= 1e-5

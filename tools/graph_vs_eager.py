@@ -1,0 +1,80 @@
+"""Per-iteration max |w_graph - w_eager| of the TD7 nets for the single-graph
+and split (data-parallel) layouts, same seeds.  Diagnostic for
+tests/test_rollout_gpu.py::test_graph_replay_matches_eager_numerics."""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+import conftest  # noqa: E402,F401  (package path)
+from test_rollout_gpu import _make  # noqa: E402
+
+
+def _snap(ag):
+    return {name: [p.detach().clone() for p in getattr(ag.learner, name).parameters()]
+            for name in ("encoder", "critic", "actor")}
+
+
+def _make_full(use_graphs, seed=0):
+    """bench.py's configuration at 256 envs: reference TD7 widths, batch 8x128."""
+    from exo_amd import VecExoskeletonEnv
+    from exo_amd.rollout import VecTrainer
+    from exo_amd.td7 import Agent
+    from exo_amd.td7 import Hyperparameters
+    torch.manual_seed(seed)
+    dev = torch.device("cuda", 0)
+    env = VecExoskeletonEnv(256, seed=1000, device=dev)
+    agent = Agent(80, 7, 1, env_num=8, hp=Hyperparameters(), device=dev, precision="fp32", n_envs=256,
+                  process_group=None, graph_safe=use_graphs)
+    return VecTrainer(env, agent, use_graphs=use_graphs), env, agent
+
+
+def run(layout, iters=10, full=False, seed=7, quiet=False):
+    mk = _make_full if full else _make
+    # one trainer at a time: both draw from the global torch RNG
+    ref = []
+    if os.environ.get("GVE_SKIP_EAGER") != "1":
+        te, _, ag_e = mk(False, seed=seed)
+        for _ in range(iters):
+            te.step()
+            ref.append(_snap(ag_e))
+        del te, ag_e
+    tg, env_g, ag_g = mk(True, seed=seed)
+    if os.environ.get("GVE_EXTRA_ALLOC") == "1":   # bench.py allocates env outputs here
+        _keep = env_g.new_outputs(True)  # noqa: F841
+    if layout == "split":
+        tg.dp = True
+    worst = 0.0
+    nosync = os.environ.get("GVE_NOSYNC") == "1"   # compare only after the last iteration
+    for it in range(iters):
+        tg.step()
+        if nosync and it != iters - 1:
+            continue
+        torch.cuda.synchronize()
+        cur = _snap(ag_g)
+        diffs = []
+        for name in ("encoder", "critic", "actor"):
+            if not ref:
+                ok = all(bool(torch.isfinite(q).all()) for q in cur[name])
+                d = 0.0 if ok else float("nan")
+            else:
+                d = max(float((p - q).abs().max()) for p, q in zip(ref[it][name], cur[name]))
+            worst = max(worst, d) if d == d else float("inf")
+            diffs.append(f"{name} {d:.3g}")
+        if not quiet or worst > 0:
+            print(f"{layout} seed {seed} iter {it} graphs={sorted(tg.graphs)}  " + "  ".join(diffs), flush=True)
+        if worst > 0 and quiet:
+            break
+    return worst
+
+
+if __name__ == "__main__":
+    if os.environ.get("GVE_SET_DEVICE") == "1":
+        torch.cuda.set_device(0)
+    full = os.environ.get("GVE_FULL") == "1"
+    seeds = [int(x) for x in os.environ.get("GVE_SEEDS", "7").split(",")]
+    for lay in sys.argv[1:] or ["single", "split"]:
+        for sd in seeds:
+            w = run(lay, full=full, seed=sd, quiet=len(seeds) > 1)
+            print(f"{lay} seed {sd} worst {w:.3g}", flush=True)
