@@ -1,0 +1,389 @@
+// td7_dense.hip -- fused dense layers of the TD7 nets on fp32 MFMA (gfx950).
+//
+// Every Linear of Agent/TD7_multi_agent.py:61-140 is followed by an
+// activation (ELU / ReLU / tanh / none).  In PyTorch one layer is a
+// hipBLASLt GEMM plus an elementwise kernel forward and elementwise-backward,
+// two GEMMs, a column reduction and a fill backward.  Here:
+//
+//   forward      Y  = act(X W^T + b)                      1 kernel
+//   bwd-data     dX = (dY * act'(Y)) W                    1 kernel  (act' in the A prologue)
+//   bwd-weight   dW = (dY * act'(Y))^T X,  db = colsum    1 kernel  (db = the GEMM against a ones column)
+//
+// act'(pre) is recovered from the saved output Y: ELU 1|Y+1, ReLU 1|0,
+// tanh 1-Y^2 -- nothing but Y, X and W is kept for backward.
+//
+// All three are one GEMM core: C[i][j] = sum_r A(i,r) B(j,r) with arbitrary
+// element strides on v_mfma_f32_16x16x4_f32 (layout notes at the kernel).
+// Groups (the critic's two Q heads) are the grid's z dimension; an input
+// shared by the groups (stride 0) has its bwd-data reduced over the groups
+// inside the kernel.  fp32 in, fp32 accumulate: exact f32 fma chains.
+#include <hip/hip_runtime.h>
+
+#include "exo_amd.h"
+
+namespace {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_ELU = 2, ACT_TANH = 3 };
+
+// derivative of the activation expressed through its output y
+template <int ACT>
+__device__ __forceinline__ float act_grad_t(float y) {
+    if (ACT == ACT_RELU) return y > 0.f ? 1.f : 0.f;
+    if (ACT == ACT_ELU) return y > 0.f ? 1.f : y + 1.f;
+    if (ACT == ACT_TANH) return 1.f - y * y;
+    return 1.f;
+}
+template <int ACT>
+__device__ __forceinline__ float act_fwd_t(float x) {
+    if (ACT == ACT_RELU) return x > 0.f ? x : 0.f;
+    if (ACT == ACT_ELU) return x > 0.f ? x : expm1f(x);
+    if (ACT == ACT_TANH) return tanhf(x);
+    return x;
+}
+
+// An operand element (i, r) of group g lives at p[g*sg + i*si + r*sr].  When
+// act >= 0 the operand is dY and is multiplied by act'(Y) read at the same
+// (g, i, r) from y (strides ysg/ysi/ysr).
+struct Operand {
+    const float *p;
+    long sg, si, sr;
+    const float *y;
+    long ysg, ysi, ysr;
+    int act; // -1: plain operand
+    int ones_col; // >= 0: index i == ones_col reads 1.0 (bias column of bwd-weight)
+};
+
+struct GemmArgs {
+    Operand A, B;
+    int I, J, R;      // C is I x J, reduction length R
+    int groups_red;   // > 1: also reduce over this many groups (bwd-data of a shared input)
+    // epilogue
+    float *C;
+    long csg, csi, csj;
+    const float *bias; // forward: + bias[g*bsg + j]
+    long bsg;
+    int act;           // forward activation
+    float *bias_grad;  // bwd-weight: column j == J_bias goes to bias_grad[g*bgsg + i]
+    long bgsg;
+    int j_bias;        // -1: none
+};
+
+// Workgroup tile 32x32 (2x2 v_mfma_f32_16x16x4_f32 tiles per wave, four
+// independent accumulators); the NW waves of a workgroup split the reduction
+// dimension in 16-wide steps (step s goes to wave s % NW) and their partial
+// tiles are summed through LDS at the end.  Operands are loaded straight
+// from global memory (L2) into registers -- no LDS staging, no barrier in
+// the loop: each wave streams its steps with the next step group's loads in
+// flight under the current group's MFMAs.  A lane (c, q) feeds MFMA jj of a
+// step with A(i, r0+4q+jj) and B(j, r0+4q+jj) (the same permutation of the
+// step's r on both operands).  Per 16-wide step a wave loads 2 A and 2 B
+// fragments for 16 MFMAs, half the L2 traffic per MFMA of one 16x16 tile
+// per wave, and NW x (I/32)(J/32) waves keep the whole chip busy on these
+// small GEMMs (M <= 4096, N, K <= 921).
+constexpr int BUF_BYTES = 0x7FFFFF00, BUF_OOB = 0x7FFFFF00; // offset past the records -> the load returns 0
+constexpr int SPG = 2;                                      // 16-wide steps per prefetch group
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float *p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(p), 0, BUF_BYTES, 0x00020000);
+}
+
+__device__ __forceinline__ float ldb(__amdgpu_buffer_rsrc_t r, bool ok, int off) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, ok ? off * 4 : BUF_OOB, 0, 0));
+}
+
+// one operand's fragments for SPG steps: [step][tile 0/1][jj]
+struct Frag {
+    float v[SPG][2][4];
+};
+
+// element (i, r) with i = i0 + 16*tile + c, r = r0 + 4q + jj.  VEC (contiguous
+// along r, the step fully inside R): one 16-byte load; else 4 checked dwords.
+template <bool VEC>
+__device__ __forceinline__ void load_step(__amdgpu_buffer_rsrc_t rp, int base_g, int si, int sr, int i0, int c, int I,
+                                          int r0, int R, int q, float (&f)[2][4], bool full) {
+#pragma unroll
+    for (int tl = 0; tl < 2; ++tl) {
+        const int i = i0 + 16 * tl + c;
+        const int r = r0 + 4 * q;
+        if (VEC && full) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rp, i < I ? (base_g + i * si + r) * 4 : BUF_OOB, 0, 0);
+            f[tl][0] = __uint_as_float(v[0]);
+            f[tl][1] = __uint_as_float(v[1]);
+            f[tl][2] = __uint_as_float(v[2]);
+            f[tl][3] = __uint_as_float(v[3]);
+        } else {
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) f[tl][jj] = ldb(rp, (i < I) & (r + jj < R), base_g + i * si + (r + jj) * sr);
+        }
+    }
+}
+
+template <int AG, int EP, bool AV, bool BV, int NW>
+__global__ __launch_bounds__(64 * NW) void dense_gemm_kernel(GemmArgs a) {
+    __shared__ __attribute__((aligned(16))) float red[NW > 1 ? NW - 1 : 1][32][33];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, q = lane >> 4, c = lane & 15;
+    const int i0 = blockIdx.y * 32, j0 = blockIdx.x * 32, g = blockIdx.z;
+    const __amdgpu_buffer_rsrc_t ra = rsrc(a.A.p), rb = rsrc(a.B.p);
+    const __amdgpu_buffer_rsrc_t ry = rsrc(AG >= 0 ? a.A.y : a.A.p);
+    const int nsteps_g = (a.R + 15) >> 4;            // 16-wide steps per reduction group
+    const int nsteps = nsteps_g * a.groups_red;
+    const int full_steps = a.R >> 4;                  // steps entirely inside R
+    // this wave's steps: w, w + NW, ...; processed SPG at a time
+    const int my = nsteps > w ? (nsteps - w + NW - 1) / NW : 0;
+    const int ngrp = (my + SPG - 1) / SPG;
+
+    // epilogue bias fetched up front (its latency hides under the main loop)
+    float bias_pre[2];
+#pragma unroll
+    for (int y = 0; y < 2; ++y) {
+        const int col = j0 + 16 * y + c;
+        bias_pre[y] = (a.bias && col < a.J) ? a.bias[g * a.bsg + col] : 0.f;
+    }
+    floatx4 acc[2][2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) acc[x][y] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    auto load = [&](int grp, Frag &fa, Frag &fy, Frag &fb) {
+#pragma unroll
+        for (int sp = 0; sp < SPG; ++sp) {
+            const int k = grp * SPG + sp;           // k-th step of this wave
+            const int st = w + k * NW;              // global step index
+            const bool live = k < my;
+            const int gg = a.groups_red > 1 ? st / nsteps_g : g;
+            const int sl = live ? st % nsteps_g : 0;
+            const int r0 = live ? sl * 16 : a.R;    // a dead step loads zeros (r >= R)
+            const bool full = live && sl < full_steps;
+            load_step<AV>(ra, gg * (int)a.A.sg, (int)a.A.si, (int)a.A.sr, i0, c, a.I, r0, a.R, q, fa.v[sp], full);
+            if (AG >= 0)
+                load_step<AV>(ry, gg * (int)a.A.ysg, (int)a.A.ysi, (int)a.A.ysr, i0, c, a.I, r0, a.R, q, fy.v[sp], full);
+            load_step<BV>(rb, gg * (int)a.B.sg, (int)a.B.si, (int)a.B.sr, j0, c, a.J, r0, a.R, q, fb.v[sp], full);
+            if (a.B.ones_col >= 0) { // bwd-weight: column ones_col of B is all ones (-> bias gradient)
+#pragma unroll
+                for (int tl = 0; tl < 2; ++tl)
+                    if (j0 + 16 * tl + c == a.B.ones_col)
+#pragma unroll
+                        for (int jj = 0; jj < 4; ++jj) fb.v[sp][tl][jj] = (r0 + 4 * q + jj < a.R) ? 1.f : 0.f;
+            }
+        }
+    };
+    auto mma = [&](const Frag &fa, const Frag &fy, const Frag &fb) {
+#pragma unroll
+        for (int sp = 0; sp < SPG; ++sp)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                float av[2];
+#pragma unroll
+                for (int tl = 0; tl < 2; ++tl)
+                    av[tl] = AG >= 0 ? fa.v[sp][tl][jj] * act_grad_t<AG>(fy.v[sp][tl][jj]) : fa.v[sp][tl][jj];
+#pragma unroll
+                for (int x = 0; x < 2; ++x)
+#pragma unroll
+                    for (int y = 0; y < 2; ++y)
+                        acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[x], fb.v[sp][y][jj], acc[x][y], 0, 0, 0);
+            }
+    };
+    Frag a0, y0, b0, a1, y1, b1;
+    if (ngrp > 0) load(0, a0, y0, b0);
+    for (int grp = 0; grp < ngrp; grp += 2) {
+        if (grp + 1 < ngrp) load(grp + 1, a1, y1, b1);
+        mma(a0, y0, b0);
+        if (grp + 1 >= ngrp) break;
+        if (grp + 2 < ngrp) load(grp + 2, a0, y0, b0);
+        mma(a1, y1, b1);
+    }
+    // sum the NW partial tiles: waves 1.. park theirs in LDS, wave 0 adds them
+    // acc[x][y][k] is C[i0 + 16x + 4q + k][j0 + 16y + c]
+    if (NW > 1) {
+        if (w > 0)
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+#pragma unroll
+                for (int y = 0; y < 2; ++y)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) red[w - 1][16 * x + 4 * q + k][16 * y + c] = acc[x][y][k];
+        __syncthreads();
+        if (w > 0) return;
+#pragma unroll
+        for (int ww = 0; ww < NW - 1; ++ww)
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+#pragma unroll
+                for (int y = 0; y < 2; ++y)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) acc[x][y][k] += red[ww][16 * x + 4 * q + k][16 * y + c];
+    }
+#pragma unroll
+    for (int y = 0; y < 2; ++y) {
+        const int col = j0 + 16 * y + c;
+        const bool is_bias = a.j_bias >= 0 && col == a.j_bias;
+        if (!is_bias && col >= a.J) continue;
+        const float bias_v = is_bias ? 0.f : bias_pre[y];
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int row = i0 + 16 * x + 4 * q + k;
+                if (row >= a.I) continue;
+                const float v = acc[x][y][k];
+                if (is_bias) a.bias_grad[g * a.bgsg + row] = v;
+                else a.C[g * a.csg + (long)row * a.csi + (long)col * a.csj] = act_fwd_t<EP>(v + bias_v);
+            }
+    }
+}
+
+int launch(const GemmArgs &a, int groups_grid, hipStream_t s) {
+    const int Jt = a.J + (a.j_bias >= 0 ? 1 : 0);
+    dim3 grid((Jt + 31) / 32, (a.I + 31) / 32, groups_grid);
+    // 32-bit element offsets inside the kernel (byte offsets below BUF_BYTES)
+    const int gmax = a.groups_red > 1 ? a.groups_red : groups_grid;
+    const long span_a = (long)gmax * a.A.sg + (long)a.I * a.A.si + (long)a.R * a.A.sr;
+    const long span_b = (long)gmax * a.B.sg + (long)(a.J + 1) * a.B.si + (long)a.R * a.B.sr;
+    if (span_a >= (1L << 29) || span_b >= (1L << 29)) return EXO_ERANGE;
+    // split the reduction over more waves when the tile grid alone is small
+    const long tiles = (long)grid.x * grid.y * grid.z;
+    const long steps = (long)((a.R + 15) / 16) * a.groups_red;
+    // waves per workgroup: about one wave per SIMD of the chip (1024), at
+    // least 4 reduction steps per wave
+    int nw = 2;
+    while (nw < 8 && tiles * nw * 2 <= 1024 && steps >= 4L * nw * 2) nw *= 2;
+#define DENSE_LAUNCH(AGv, EPv, AVv, BVv)                                                                         \
+    do {                                                                                                       \
+        if (nw == 8) hipLaunchKernelGGL((dense_gemm_kernel<AGv, EPv, AVv, BVv, 8>), grid, dim3(512), 0, s, a); \
+        else if (nw == 4) hipLaunchKernelGGL((dense_gemm_kernel<AGv, EPv, AVv, BVv, 4>), grid, dim3(256), 0, s, a); \
+        else hipLaunchKernelGGL((dense_gemm_kernel<AGv, EPv, AVv, BVv, 2>), grid, dim3(128), 0, s, a);        \
+    } while (0)
+    const bool av = a.A.sr == 1, bv = a.B.sr == 1;
+    if (a.A.act < 0) { // forward: both operands contiguous along the reduction
+        if (!(av && bv)) return EXO_EINVAL;
+        switch (a.act) {
+        case ACT_RELU: DENSE_LAUNCH(-1, ACT_RELU, true, true); break;
+        case ACT_ELU: DENSE_LAUNCH(-1, ACT_ELU, true, true); break;
+        case ACT_TANH: DENSE_LAUNCH(-1, ACT_TANH, true, true); break;
+        default: DENSE_LAUNCH(-1, ACT_NONE, true, true); break;
+        }
+    } else if (av) {   // bwd-data: dY rows contiguous, W^T column walk
+        switch (a.A.act) {
+        case ACT_RELU: DENSE_LAUNCH(ACT_RELU, ACT_NONE, true, false); break;
+        case ACT_ELU: DENSE_LAUNCH(ACT_ELU, ACT_NONE, true, false); break;
+        case ACT_TANH: DENSE_LAUNCH(ACT_TANH, ACT_NONE, true, false); break;
+        default: DENSE_LAUNCH(ACT_NONE, ACT_NONE, true, false); break;
+        }
+    } else {           // bwd-weight: both operands walk rows (contiguous along i)
+        switch (a.A.act) {
+        case ACT_RELU: DENSE_LAUNCH(ACT_RELU, ACT_NONE, false, false); break;
+        case ACT_ELU: DENSE_LAUNCH(ACT_ELU, ACT_NONE, false, false); break;
+        case ACT_TANH: DENSE_LAUNCH(ACT_TANH, ACT_NONE, false, false); break;
+        default: DENSE_LAUNCH(ACT_NONE, ACT_NONE, false, false); break;
+        }
+    }
+#undef DENSE_LAUNCH
+    return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
+}
+
+Operand plain(const float *p, long sg, long si, long sr) {
+    Operand o{};
+    o.p = p;
+    o.sg = sg;
+    o.si = si;
+    o.sr = sr;
+    o.act = -1;
+    o.ones_col = -1;
+    return o;
+}
+
+} // namespace
+
+extern "C" {
+
+/* Forward of G grouped dense layers: Y[g] = act(X[g] W[g]^T + b[g]).
+ * X: [G][M][K] with group stride xsg (0 = one X shared by all groups) and row
+ * stride ldx; W: [G][N][K] contiguous; b: [G][N] or null; Y: [G][M][N] with
+ * group stride ysg and row stride ldy.  act: 0 none, 1 relu, 2 elu, 3 tanh. */
+int td7_dense_fwd(const float *x, long xsg, long ldx, const float *w, const float *b, float *y, long ysg, long ldy,
+                  int32_t groups, int32_t m, int32_t n, int32_t k, int32_t act, void *stream) {
+    if (!x || !w || !y || groups <= 0 || m < 0 || n <= 0 || k <= 0 || act < 0 || act > 3) return EXO_EINVAL;
+    if (m == 0) return EXO_OK;
+    GemmArgs a{};
+    a.A = plain(x, xsg, ldx, 1);
+    a.B = plain(w, (long)n * k, k, 1);
+    a.I = m;
+    a.J = n;
+    a.R = k;
+    a.groups_red = 1;
+    a.C = y;
+    a.csg = ysg;
+    a.csi = ldy;
+    a.csj = 1;
+    a.bias = b;
+    a.bsg = n;
+    a.act = act;
+    a.j_bias = -1;
+    return launch(a, groups, (hipStream_t)stream);
+}
+
+/* dX = sum over the reduced groups of (dY[g] * act'(Y[g])) W[g].
+ * dY, Y: [G][M][N] (group stride dysg / ysg, row strides lddy / ldy);
+ * W: [G][N][K]; dX: [M][K] per group (dxsg, lddx).  shared_input != 0: X was
+ * one tensor for all groups, dX (a single [M][K]) sums over them. */
+int td7_dense_bwd_data(const float *dy, long dysg, long lddy, const float *yv, long ysg, long ldy, const float *w,
+                       float *dx, long dxsg, long lddx, int32_t groups, int32_t shared_input, int32_t m, int32_t n,
+                       int32_t k, int32_t act, void *stream) {
+    if (!dy || !yv || !w || !dx || groups <= 0 || m < 0 || n <= 0 || k <= 0 || act < 0 || act > 3) return EXO_EINVAL;
+    if (m == 0) return EXO_OK;
+    GemmArgs a{};
+    a.A = plain(dy, dysg, lddy, 1);
+    a.A.y = yv;
+    a.A.ysg = ysg;
+    a.A.ysi = ldy;
+    a.A.ysr = 1;
+    a.A.act = act;
+    a.B = plain(w, (long)n * k, 1, k); // B(j = out col k, r = n) = W[n][k]
+    a.I = m;
+    a.J = k;
+    a.R = n;
+    a.groups_red = shared_input ? groups : 1;
+    a.C = dx;
+    a.csg = dxsg;
+    a.csi = lddx;
+    a.csj = 1;
+    a.act = ACT_NONE;
+    a.j_bias = -1;
+    return launch(a, shared_input ? 1 : groups, (hipStream_t)stream);
+}
+
+/* dW[g] = (dY[g] * act'(Y[g]))^T X[g]  ([N][K], contiguous per group) and,
+ * when db != null, db[g] = column sums of dY[g] * act'(Y[g])  ([N]). */
+int td7_dense_bwd_weight(const float *dy, long dysg, long lddy, const float *yv, long ysg, long ldy, const float *x,
+                         long xsg, long ldx, float *dw, float *db, int32_t groups, int32_t m, int32_t n, int32_t k,
+                         int32_t act, void *stream) {
+    if (!dy || !yv || !x || !dw || groups <= 0 || m < 0 || n <= 0 || k <= 0 || act < 0 || act > 3) return EXO_EINVAL;
+    GemmArgs a{};
+    a.A = plain(dy, dysg, 1, lddy); // A(i = n, r = m) = dY[m][n]
+    a.A.y = yv;
+    a.A.ysg = ysg;
+    a.A.ysi = 1;
+    a.A.ysr = ldy;
+    a.A.act = act;
+    a.B = plain(x, xsg, 1, ldx);    // B(j = k, r = m) = X[m][k]
+    a.B.ones_col = db ? k : -1;     // column K of the product is colsum(dP) = db
+    a.I = n;
+    a.J = k;
+    a.R = m;
+    a.groups_red = 1;
+    a.C = dw;
+    a.csg = (long)n * k;
+    a.csi = k;
+    a.csj = 1;
+    a.act = ACT_NONE;
+    a.bias_grad = db;
+    a.bgsg = n;
+    a.j_bias = db ? k : -1;
+    if (m == 0) return EXO_EINVAL;
+    return launch(a, groups, (hipStream_t)stream);
+}
+
+} // extern "C"

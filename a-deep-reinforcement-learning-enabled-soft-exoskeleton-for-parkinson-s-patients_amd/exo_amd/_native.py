@@ -21,6 +21,7 @@ EXO_OK = 0
 ERRORS = {-22: "EINVAL", -12: "ENOMEM", -5: "EDEVICE", -34: "ERANGE"}
 
 c_int32, c_double, c_void_p, c_uint64 = ctypes.c_int32, ctypes.c_double, ctypes.c_void_p, ctypes.c_uint64
+c_long = ctypes.c_long
 P = ctypes.POINTER
 
 
@@ -67,6 +68,14 @@ EXPORTS = {
     "td7_avgl1norm_fwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, ctypes.c_float, c_void_p]),
     "td7_avgl1norm_bwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, ctypes.c_float,
                                     c_void_p]),
+    "td7_dense_fwd": (c_int32, [c_void_p, c_long, c_long, c_void_p, c_void_p, c_void_p, c_long, c_long,
+                                c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p]),
+    "td7_dense_bwd_data": (c_int32, [c_void_p, c_long, c_long, c_void_p, c_long, c_long, c_void_p, c_void_p,
+                                     c_long, c_long, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
+                                     c_void_p]),
+    "td7_dense_bwd_weight": (c_int32, [c_void_p, c_long, c_long, c_void_p, c_long, c_long, c_void_p, c_long,
+                                       c_long, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32,
+                                       c_void_p]),
 }
 
 _lib = None

@@ -37,3 +37,100 @@ def avg_l1_norm(x, eps=1e-8):
     if x.dtype != torch.float32:
         return _AvgL1NormFn.apply(x.float(), eps).to(x.dtype)
     return _AvgL1NormFn.apply(x, eps)
+
+
+# ---------------------------------------------------------------- dense layers
+ACT_CODES = {None: 0, "none": 0, "relu": 1, "elu": 2, "tanh": 3}
+
+
+def act_code(fn):
+    """Activation function of the reference nets -> td7_dense act code (None if unsupported)."""
+    import torch.nn.functional as F
+    return {F.relu: 1, torch.relu: 1, F.elu: 2, torch.tanh: 3}.get(fn)
+
+
+def _rows(t):
+    """(tensor with unit column stride, row stride)."""
+    if t.stride(-1) != 1:
+        t = t.contiguous()
+    return t, t.stride(-2)
+
+
+class _DenseFn(torch.autograd.Function):
+    """act(x W^T + b).  Shapes: plain x [M,K], W [N,K], b [N]; grouped W
+    [G,N,K], b [G,N] with x [G,M,K] (one input per group) or x [M,K] (shared by
+    the groups) -> y [G,M,N].
+
+    Forward: hipBLASLt GEMM with its bias epilogue + the activation (faster
+    than td7_dense_fwd at these shapes, profiles/r01_dense_bench.txt) unless
+    fwd_kernel; backward: the td7_dense kernels -- act'(Y) folded into the
+    operand loads, the bias gradient as the GEMM against a ones column: two
+    launches where autograd issues the activation backward, two GEMMs, a
+    column reduction and a fill."""
+
+    fwd_kernel = False
+
+    @staticmethod
+    def forward(ctx, x, w, b, act):
+        grouped = w.dim() == 3
+        G = w.shape[0] if grouped else 1
+        N, K = w.shape[-2], w.shape[-1]
+        shared = grouped and x.dim() == 2
+        x, ldx = _rows(x)
+        M = x.shape[-2]
+        xsg = 0 if (shared or not grouped) else x.stride(0)
+        w = w.contiguous()
+        bb = b.contiguous() if b is not None else None
+        if _DenseFn.fwd_kernel:
+            y = torch.empty((G, M, N) if grouped else (M, N), dtype=torch.float32, device=x.device)
+            nat.check(nat.lib().td7_dense_fwd(nat.ptr(x), xsg, ldx, nat.ptr(w), nat.ptr(bb), nat.ptr(y),
+                                              M * N, N, G, M, N, K, act, nat.stream_ptr(x.device)), "td7_dense_fwd")
+        else:
+            y = _torch_dense(x, w, bb, act)
+        ctx.save_for_backward(x, w, y)
+        ctx.meta = (grouped, shared, G, M, N, K, act, xsg, ldx, b is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, y = ctx.saved_tensors
+        grouped, shared, G, M, N, K, act, xsg, ldx, has_b = ctx.meta
+        dy = dy.contiguous()
+        s = nat.stream_ptr(dy.device)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty((G, M, K) if (grouped and not shared) else (M, K), dtype=torch.float32, device=dy.device)
+            nat.check(nat.lib().td7_dense_bwd_data(nat.ptr(dy), M * N, N, nat.ptr(y), M * N, N, nat.ptr(w),
+                                                   nat.ptr(dx), M * K, K, G, int(shared), M, N, K, act, s),
+                      "td7_dense_bwd_data")
+        if ctx.needs_input_grad[1] or (has_b and ctx.needs_input_grad[2]):
+            dw = torch.empty_like(w)
+            db = torch.empty((G, N) if grouped else (N,), dtype=torch.float32, device=dy.device) if has_b else None
+            nat.check(nat.lib().td7_dense_bwd_weight(nat.ptr(dy), M * N, N, nat.ptr(y), M * N, N, nat.ptr(x), xsg,
+                                                     ldx, nat.ptr(dw), nat.ptr(db), G, M, N, K, act, s),
+                      "td7_dense_bwd_weight")
+        return dx, dw, db, None
+
+
+def _torch_dense(x, w, b, act):
+    if w.dim() == 3:
+        xx = x if x.dim() == 3 else x.unsqueeze(0).expand(w.shape[0], *x.shape)
+        y = torch.baddbmm(b.unsqueeze(1), xx, w.transpose(1, 2)) if b is not None else torch.bmm(xx, w.transpose(1, 2))
+    else:
+        y = torch.nn.functional.linear(x, w, b)
+    if act == 1:
+        return torch.relu_(y)
+    if act == 2:
+        return torch.nn.functional.elu_(y)
+    if act == 3:
+        return torch.tanh_(y)
+    return y
+
+
+def dense(x, w, b, act=0):
+    """Linear + activation (act code, see ACT_CODES) -- td7_dense kernels on a
+    GPU for fp32 tensors; the reference's torch expression otherwise."""
+    if x.device.type == "cuda" and x.dtype == torch.float32 and w.dtype == torch.float32 \
+            and not torch.is_autocast_enabled():
+        return _DenseFn.apply(x, w, b, act)
+    return _torch_dense(x, w, b, act)

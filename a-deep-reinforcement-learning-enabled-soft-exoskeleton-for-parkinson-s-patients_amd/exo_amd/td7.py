@@ -27,6 +27,7 @@ import torch.distributed as dist
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import ops
 from .ops import avg_l1_norm
 
 
@@ -90,11 +91,18 @@ class Actor(nn.Module):
         self.l3 = nn.Linear(hdim, action_dim)
 
     def forward(self, state, zs):
-        a = AvgL1Norm(self.l0(state))
+        act = ops.act_code(self.activ)
+        if act is None:  # an activation the fused kernels do not know: plain torch
+            a = AvgL1Norm(self.l0(state))
+            a = torch.cat([a, zs], 1)
+            a = self.activ(self.l1(a))
+            a = self.activ(self.l2(a))
+            return torch.tanh(self.l3(a))
+        a = AvgL1Norm(ops.dense(state, self.l0.weight, self.l0.bias))
         a = torch.cat([a, zs], 1)
-        a = self.activ(self.l1(a))
-        a = self.activ(self.l2(a))
-        return torch.tanh(self.l3(a))
+        a = ops.dense(a, self.l1.weight, self.l1.bias, act)
+        a = ops.dense(a, self.l2.weight, self.l2.bias, act)
+        return ops.dense(a, self.l3.weight, self.l3.bias, ops.ACT_CODES["tanh"])
 
 
 class Encoder(nn.Module):
@@ -111,14 +119,24 @@ class Encoder(nn.Module):
         self.zsa3 = nn.Linear(hdim, zs_dim)
 
     def zs(self, state):
-        zs = self.activ(self.zs1(state))
-        zs = self.activ(self.zs2(zs))
-        return AvgL1Norm(self.zs3(zs))
+        act = ops.act_code(self.activ)
+        if act is None:
+            zs = self.activ(self.zs1(state))
+            zs = self.activ(self.zs2(zs))
+            return AvgL1Norm(self.zs3(zs))
+        zs = ops.dense(state, self.zs1.weight, self.zs1.bias, act)
+        zs = ops.dense(zs, self.zs2.weight, self.zs2.bias, act)
+        return AvgL1Norm(ops.dense(zs, self.zs3.weight, self.zs3.bias))
 
     def zsa(self, zs, action):
-        zsa = self.activ(self.zsa1(torch.cat([zs, action], 1)))
-        zsa = self.activ(self.zsa2(zsa))
-        return self.zsa3(zsa)
+        act = ops.act_code(self.activ)
+        if act is None:
+            zsa = self.activ(self.zsa1(torch.cat([zs, action], 1)))
+            zsa = self.activ(self.zsa2(zsa))
+            return self.zsa3(zsa)
+        zsa = ops.dense(torch.cat([zs, action], 1), self.zsa1.weight, self.zsa1.bias, act)
+        zsa = ops.dense(zsa, self.zsa2.weight, self.zsa2.bias, act)
+        return ops.dense(zsa, self.zsa3.weight, self.zsa3.bias)
 
 
 class Critic(nn.Module):
@@ -162,6 +180,17 @@ class Critic(nn.Module):
                 sd[prefix + f"b{k}"] = torch.stack([sd.pop(prefix + n + ".bias") for n in names])
 
     def forward(self, state, action, zsa, zs):
+        act = ops.act_code(self.activ)
+        if act is not None and state.is_cuda:
+            # both heads per layer as one grouped td7_dense launch: [2, B, *]
+            B = state.shape[0]
+            sa = torch.cat([state, action], 1)
+            embeddings = torch.cat([zsa, zs], 1)
+            q = AvgL1Norm(ops.dense(sa, self.w0, self.b0))                     # shared input -> [2, B, h]
+            x = torch.cat([q, embeddings.unsqueeze(0).expand(2, B, embeddings.shape[1])], 2)
+            x = ops.dense(x, self.w1, self.b1, act)
+            x = ops.dense(x, self.w2, self.b2, act)
+            return ops.dense(x, self.w3, self.b3).squeeze(2).t()             # [B, 2]
         B, h = state.shape[0], self.hdim
         sa = torch.cat([state, action], 1)
         embeddings = torch.cat([zsa, zs], 1)

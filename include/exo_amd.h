@@ -180,6 +180,27 @@ int td7_avgl1norm_fwd(const float *x_dev, float *y_dev, float *mean_out_dev, int
 int td7_avgl1norm_bwd(const float *x_dev, const float *mean_dev, const float *gy_dev, float *gx_dev, int32_t rows,
                       int32_t cols, float eps, void *stream);
 
+/* ------------------------------------------------------------------------
+ * Fused dense layers of the TD7 nets on fp32 MFMA (csrc/td7_dense.hip).
+ * Each replaces one nn.Linear + activation of Agent/TD7_multi_agent.py:61-140
+ * (forward) and its autograd backward.  act: 0 none, 1 relu, 2 elu, 3 tanh.
+ * G groups (the critic's Q heads, :120-127) run in one launch; strides are in
+ * floats; every row has unit column stride.
+ * ---------------------------------------------------------------------- */
+/* Y[g] = act(X[g] W[g]^T + b[g]); X [G][M][K] (xsg = 0: one X for all
+ * groups), W [G][N][K] contiguous, b [G][N] or NULL, Y [G][M][N]. */
+int td7_dense_fwd(const float *x_dev, long xsg, long ldx, const float *w_dev, const float *b_dev, float *y_dev,
+                  long ysg, long ldy, int32_t groups, int32_t m, int32_t n, int32_t k, int32_t act, void *stream);
+/* dX = (dY * act'(Y)) W per group, or summed over the groups when
+ * shared_input != 0 (X was shared); act' is taken from the saved output Y. */
+int td7_dense_bwd_data(const float *dy_dev, long dysg, long lddy, const float *y_dev, long ysg, long ldy,
+                       const float *w_dev, float *dx_dev, long dxsg, long lddx, int32_t groups, int32_t shared_input,
+                       int32_t m, int32_t n, int32_t k, int32_t act, void *stream);
+/* dW[g] = (dY * act'(Y))^T X  [G][N][K]; db[g] = its column sums [G][N] (db may be NULL). */
+int td7_dense_bwd_weight(const float *dy_dev, long dysg, long lddy, const float *y_dev, long ysg, long ldy,
+                         const float *x_dev, long xsg, long ldx, float *dw_dev, float *db_dev, int32_t groups,
+                         int32_t m, int32_t n, int32_t k, int32_t act, void *stream);
+
 #ifdef __cplusplus
 }
 #endif
