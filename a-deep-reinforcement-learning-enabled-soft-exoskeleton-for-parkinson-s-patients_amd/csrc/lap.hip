@@ -143,6 +143,142 @@ __global__ void lap_totals_kernel(const float *tree, int cap, int n_strata, floa
 
 __global__ void lap_init_kernel(float *maxp) { *maxp = 1.0f; } // max_priority = 1 (:42)
 
+
+// ---------------------------------------------------------------- batched store
+// LAP.add for every env of one vectorised step (:49-63 per row): the rows of
+// stratum s go to consecutive ring slots starting at ptr[s], in env order.
+// Phase 1 (one workgroup per stratum): block scan of "row i is active and in
+// stratum s" -> slot of every row (the trash row `capacity` for inactive ones),
+// new leaves = max_priority and their ancestors, ring pointer and size.
+// Phase 2 (many workgroups): one wavefront per row copies its transition.
+constexpr int STORE_CHUNK = UPD_THREADS * 4;
+
+__global__ __launch_bounds__(UPD_THREADS) void lap_store_rank_kernel(float *tree, const float *maxp, int cap,
+                                                                     int levels, int capacity, int32_t *ring_ptr,
+                                                                     int32_t *ring_size, const int32_t *strata,
+                                                                     const uint8_t *active, int n, int32_t *row_of) {
+    const int s = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    float *T = stratum_tree(tree, s, cap);
+    __shared__ int32_t mine[STORE_CHUNK];
+    __shared__ int wsum[UPD_THREADS / 64];
+    __shared__ int chunk_total;
+    const float p = *maxp;
+    const int ptr0 = ring_ptr[s];
+    const int row0 = s * (capacity + 1);
+    int offset = 0; // rows of this stratum placed by earlier chunks
+    for (int base = 0; base < n; base += STORE_CHUNK) {
+        int f[4], cnt = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = base + 4 * t + k;
+            f[k] = (i < n && strata[i] == s && (!active || active[i])) ? 1 : 0;
+            cnt += f[k];
+        }
+        // block-wide exclusive scan of cnt
+        int incl = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += v;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        if (t == 0) {
+            int acc = 0;
+            for (int k = 0; k < UPD_THREADS / 64; ++k) {
+                const int v = wsum[k];
+                wsum[k] = acc;
+                acc += v;
+            }
+            chunk_total = acc;
+        }
+        __syncthreads();
+        int rank = offset + wsum[wv] + incl - cnt;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = base + 4 * t + k;
+            if (i < n && s == 0 && (strata[i] < 0 || strata[i] >= (int)gridDim.x)) row_of[i] = -1; // no stratum
+            if (i >= n || strata[i] != s) continue;
+            if (f[k]) {
+                const int slot = (ptr0 + rank) % capacity;
+                row_of[i] = row0 + slot;
+                T[cap + slot] = p;
+                mine[rank - offset] = slot;
+                ++rank;
+            } else {
+                row_of[i] = row0 + capacity; // inactive env: the trash row
+            }
+        }
+        const int total = chunk_total;
+        __syncthreads();
+        propagate(T, cap, levels, mine, min(total, STORE_CHUNK));
+        offset += total;
+    }
+    if (t == 0) {
+        ring_ptr[s] = (ptr0 + offset) % capacity;
+        ring_size[s] = min(ring_size[s] + offset, capacity);
+    }
+}
+
+__global__ __launch_bounds__(256) void lap_store_copy_kernel(lap_storage_desc st, const float *state,
+                                                             const float *action, const float *next_state,
+                                                             const float *reward, const uint8_t *done,
+                                                             float action_scale, int n, const int32_t *row_of) {
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (i >= n) return;
+    const long r = row_of[i];
+    if (r < 0) return;
+    const int sd = st.state_dim, ad = st.action_dim;
+    for (int k = lane; k < sd; k += 64) {
+        st.state[r * sd + k] = state[(long)i * sd + k];
+        st.next_state[r * sd + k] = next_state[(long)i * sd + k];
+    }
+    for (int k = lane; k < ad; k += 64) st.action[r * ad + k] = action[(long)i * ad + k] / action_scale;
+    if (lane == 0) {
+        st.reward[r] = reward[i];
+        st.not_done[r] = 1.0f - (done[i] ? 1.0f : 0.0f);
+    }
+}
+
+// LAP.sample (:65-111) with the gather: one wavefront per draw descends the
+// tree (every lane the same path, reads broadcast) and copies the row.
+__global__ __launch_bounds__(256) void lap_sample_gather_kernel(const float *tree, int cap, int levels, int capacity,
+                                                                const float *u, const int32_t *size, int batch,
+                                                                int total, int32_t *idx, lap_storage_desc st,
+                                                                float *o_state, float *o_action, float *o_next,
+                                                                float *o_reward, float *o_not_done) {
+    const int d = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (d >= total) return;
+    const int s = d / batch;
+    const float *T = tree + (size_t)s * 2 * cap;
+    float val = u[d] * T[1];
+    int node = 1;
+    for (int lv = 0; lv < levels; ++lv) {
+        const float left = T[2 * node], right = T[2 * node + 1];
+        if (val <= left || right <= 0.0f) {
+            node = 2 * node;
+        } else {
+            val -= left;
+            node = 2 * node + 1;
+        }
+    }
+    int i = node - cap;
+    const int sz = size[s];
+    if (i >= sz) i = sz > 0 ? sz - 1 : 0;
+    if (lane == 0) idx[d] = i;
+    const long r = (long)s * (capacity + 1) + i;
+    const int sd = st.state_dim, ad = st.action_dim;
+    for (int k = lane; k < sd; k += 64) {
+        o_state[(long)d * sd + k] = st.state[r * sd + k];
+        o_next[(long)d * sd + k] = st.next_state[r * sd + k];
+    }
+    for (int k = lane; k < ad; k += 64) o_action[(long)d * ad + k] = st.action[r * ad + k];
+    if (lane == 0) {
+        o_reward[d] = st.reward[r];
+        o_not_done[d] = st.not_done[r];
+    }
+}
+
 int rc(hipError_t e) { return e == hipSuccess ? EXO_OK : EXO_EDEVICE; }
 
 int levels_of(const lap_tree_desc *t) {
@@ -210,6 +346,36 @@ int lap_totals(const lap_tree_desc *t, float *out, void *stream) {
     if (!valid(t) || !out) return EXO_EINVAL;
     hipLaunchKernelGGL(lap_totals_kernel, dim3((t->n_strata + 63) / 64), dim3(64), 0, (hipStream_t)stream, t->tree,
                        t->cap, t->n_strata, out);
+    return rc(hipGetLastError());
+}
+
+int lap_store_batch(const lap_tree_desc *t, const lap_storage_desc *st, const float *state, const float *action,
+                    const float *next_state, const float *reward, const uint8_t *done, const int32_t *strata,
+                    const uint8_t *active, float action_scale, int32_t n, int32_t *row_ws, void *stream) {
+    if (!valid(t) || !st || !st->state || !st->action || !st->next_state || !st->reward || !st->not_done ||
+        !st->ptr || !st->size || st->state_dim <= 0 || st->action_dim <= 0 || !state || !action || !next_state ||
+        !reward || !done || !strata || !row_ws || n < 0 || action_scale == 0.0f)
+        return EXO_EINVAL;
+    if (n == 0) return EXO_OK;
+    hipLaunchKernelGGL(lap_store_rank_kernel, dim3(t->n_strata), dim3(UPD_THREADS), 0, (hipStream_t)stream, t->tree,
+                       t->max_priority, t->cap, levels_of(t), t->capacity, st->ptr, st->size, strata, active, n,
+                       row_ws);
+    if (hipGetLastError() != hipSuccess) return EXO_EDEVICE;
+    hipLaunchKernelGGL(lap_store_copy_kernel, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, *st, state,
+                       action, next_state, reward, done, action_scale, n, row_ws);
+    return rc(hipGetLastError());
+}
+
+int lap_sample_gather(const lap_tree_desc *t, const lap_storage_desc *st, const float *u, int32_t batch,
+                      int32_t *idx, float *out_state, float *out_action, float *out_next_state, float *out_reward,
+                      float *out_not_done, void *stream) {
+    if (!valid(t) || !st || !st->size || !u || !idx || batch <= 0 || !out_state || !out_action ||
+        !out_next_state || !out_reward || !out_not_done)
+        return EXO_EINVAL;
+    const int total = t->n_strata * batch;
+    hipLaunchKernelGGL(lap_sample_gather_kernel, dim3((total + 3) / 4), dim3(256), 0, (hipStream_t)stream, t->tree,
+                       t->cap, levels_of(t), t->capacity, u, st->size, batch, total, idx, *st, out_state, out_action,
+                       out_next_state, out_reward, out_not_done);
     return rc(hipGetLastError());
 }
 

@@ -30,6 +30,12 @@ class LapTreeDesc(ctypes.Structure):
                 ("cap", c_int32)]
 
 
+class LapStorageDesc(ctypes.Structure):
+    _fields_ = [("state", c_void_p), ("action", c_void_p), ("next_state", c_void_p), ("reward", c_void_p),
+                ("not_done", c_void_p), ("state_dim", c_int32), ("action_dim", c_int32), ("ptr", c_void_p),
+                ("size", c_void_p)]
+
+
 class ExoEnvConfig(ctypes.Structure):
     """exo_env_config: the constructor arguments of ExoskeletonEnv_train
     (Environment/Exoskeleton_env.py:38-48)."""
@@ -65,6 +71,10 @@ EXPORTS = {
     "lap_update": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p]),
     "lap_reset_max": (c_int32, [c_void_p, c_void_p]),
     "lap_totals": (c_int32, [c_void_p, c_void_p, c_void_p]),
+    "lap_store_batch": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                  c_void_p, ctypes.c_float, c_int32, c_void_p, c_void_p]),
+    "lap_sample_gather": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_void_p, c_void_p]),
     "td7_avgl1norm_fwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, ctypes.c_float, c_void_p]),
     "td7_avgl1norm_bwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, ctypes.c_float,
                                     c_void_p]),

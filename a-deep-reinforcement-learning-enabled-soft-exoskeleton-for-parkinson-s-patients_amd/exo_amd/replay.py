@@ -61,6 +61,13 @@ class LAP:
         self.ind = None
         self._u = torch.empty((E, self.batch_size), **f32)
         self._idx = torch.empty((E, self.batch_size), **i32)
+        self._store = nat.LapStorageDesc(self.state.data_ptr(), self.action.data_ptr(), self.next_state.data_ptr(),
+                                         self.reward.data_ptr(), self.not_done.data_ptr(), state_dim, action_dim,
+                                         self.ptr_s.data_ptr(), self.size_s.data_ptr())
+        B = E * self.batch_size  # sampled batch, written in place by lap_sample_gather (static for HIP graphs)
+        self._batch = (torch.empty((B, state_dim), **f32), torch.empty((B, action_dim), **f32),
+                       torch.empty((B, state_dim), **f32), torch.empty((B, 1), **f32), torch.empty((B, 1), **f32))
+        self._row_ws = None
         self._init_tree()
 
     def _stream(self):
@@ -104,46 +111,44 @@ class LAP:
 
     def add_batch(self, state, action, next_state, reward, done, strata, active=None):
         """One vectorised env step: row i goes to stratum strata[i] (int32 [N]) if
-        active[i] (bool [N], default all).  No host synchronisation."""
-        E, C = self.num_envs, self.max_size
+        active[i] (bool/uint8 [N], default all) -- lap_store_batch, two kernels,
+        no host synchronisation."""
         n = state.shape[0]
-        if getattr(self, "_ar_n", None) is None or self._ar_n.numel() != n:
-            self._ar_n = torch.arange(n, device=self.device)
-            self._ar_e = torch.arange(E, device=self.device)
-        strata = strata.to(torch.int64)
-        act = torch.ones((n,), dtype=torch.int64, device=self.device) if active is None else active.to(torch.int64)
-        # one-hot by comparison (F.one_hot validates its input with a host sync),
-        # stratum-major so the rank scan runs along the contiguous dimension
-        onehot = (self._ar_e[:, None] == strata[None, :]).to(torch.int32) * act[None, :].to(torch.int32)  # [E, N]
-        rank = (torch.cumsum(onehot, 1, dtype=torch.int32) - onehot)[strata, self._ar_n].to(torch.int64)
-        slot = (self.ptr_s.to(torch.int64)[strata] + rank) % C
-        slot = torch.where(act > 0, slot, torch.full_like(slot, C))              # inactive -> trash row
-        rows = self._row0[strata] + slot
-        self.state.view(-1, self.state_dim).index_copy_(0, rows, state.to(torch.float32))
-        self.action.view(-1, self.action_dim).index_copy_(0, rows, action.to(torch.float32) / self.normalize_actions)
-        self.next_state.view(-1, self.state_dim).index_copy_(0, rows, next_state.to(torch.float32))
-        self.reward.view(-1, 1).index_copy_(0, rows, reward.to(torch.float32).view(-1, 1))
-        self.not_done.view(-1, 1).index_copy_(0, rows, 1.0 - done.to(torch.float32).view(-1, 1))
-        cnt = onehot.sum(1, dtype=torch.int64)
-        lap_slot = torch.where(act > 0, slot, torch.full_like(slot, -1)).to(torch.int32)
-        st32 = strata.to(torch.int32)
-        nat.check(nat.lib().lap_add(ctypes.byref(self._desc), nat.ptr(st32), nat.ptr(lap_slot), n, self._stream()),
-                  "lap_add")
-        self.ptr_s.copy_(((self.ptr_s.to(torch.int64) + cnt) % C).to(torch.int32))
-        self.size_s.copy_(torch.clamp(self.size_s.to(torch.int64) + cnt, max=C).to(torch.int32))
+        if self._row_ws is None or self._row_ws.numel() < n:
+            self._row_ws = torch.empty((n,), dtype=torch.int32, device=self.device)
+
+        def f32(t, shape):
+            t = t.to(device=self.device, dtype=torch.float32).reshape(shape)
+            return t if t.is_contiguous() else t.contiguous()
+
+        st = f32(state, (n, self.state_dim))
+        nx = f32(next_state, (n, self.state_dim))
+        ac = f32(action, (n, self.action_dim))
+        rw = f32(reward, (n,))
+        dn = done if done.dtype == torch.uint8 else done.to(torch.uint8)
+        dn = dn.reshape(n).contiguous()
+        sr = strata if strata.dtype == torch.int32 else strata.to(torch.int32)
+        act = None
+        if active is not None:
+            act = active.view(torch.uint8) if active.dtype == torch.bool else active.to(torch.uint8)
+            act = act.contiguous()
+        nat.check(nat.lib().lap_store_batch(ctypes.byref(self._desc), ctypes.byref(self._store), nat.ptr(st),
+                                            nat.ptr(ac), nat.ptr(nx), nat.ptr(rw), nat.ptr(dn), nat.ptr(sr.contiguous()),
+                                            nat.ptr(act), float(self.normalize_actions), n, nat.ptr(self._row_ws),
+                                            self._stream()), "lap_store_batch")
 
     # ------------------------------------------------------------- sample
     def sample(self):
         """Agent/TD7_buffer_multi_agent.py:65-111: batch_size rows from every
-        stratum, stratum-major, as float32 device tensors."""
+        stratum, stratum-major, as float32 device tensors (lap_sample_gather:
+        descent + gather in one kernel; the returned tensors are reused by the
+        next call)."""
         self._u.uniform_()
-        nat.check(nat.lib().lap_sample(ctypes.byref(self._desc), nat.ptr(self._u), nat.ptr(self.size_s),
-                                       self.batch_size, nat.ptr(self._idx), self._stream()), "lap_sample")
+        nat.check(nat.lib().lap_sample_gather(ctypes.byref(self._desc), ctypes.byref(self._store), nat.ptr(self._u),
+                                              self.batch_size, nat.ptr(self._idx), *[nat.ptr(t) for t in self._batch],
+                                              self._stream()), "lap_sample_gather")
         self.ind = self._idx
-        rows = (self._row0[:, None] + self._idx.to(torch.int64)).reshape(-1)
-        return (self.state.view(-1, self.state_dim)[rows], self.action.view(-1, self.action_dim)[rows],
-                self.next_state.view(-1, self.state_dim)[rows], self.reward.view(-1, 1)[rows],
-                self.not_done.view(-1, 1)[rows])
+        return self._batch
 
     def sample_indices(self, u):
         """Indices for given uniforms u [E, batch] (parity hook)."""

@@ -170,6 +170,31 @@ int lap_reset_max(const lap_tree_desc *t, void *stream);
 /* Total priority of each stratum (root of its tree) -> out_dev[n_strata]. */
 int lap_totals(const lap_tree_desc *t, float *out_dev, void *stream);
 
+/* Transition storage of the LAP buffer: [n_strata][capacity + 1][dim] fp32
+ * (row `capacity` of every stratum is a trash row for inactive envs), and
+ * the device ring pointer / size of every stratum. */
+typedef struct {
+    float *state, *action, *next_state, *reward, *not_done;
+    int32_t state_dim, action_dim;
+    int32_t *ptr, *size;
+} lap_storage_desc;
+
+/* LAP.add (:49-63) for one vectorised env step of n envs: env i, when
+ * active[i] (NULL = all), goes to stratum strata[i] at the next ring slot
+ * (env order within a stratum), with priority max_priority; stores
+ * action/action_scale and not_done = 1 - done.  row_ws: n int32 scratch. */
+int lap_store_batch(const lap_tree_desc *t, const lap_storage_desc *st, const float *state_dev,
+                    const float *action_dev, const float *next_state_dev, const float *reward_dev,
+                    const uint8_t *done_dev, const int32_t *strata_dev, const uint8_t *active_dev, float action_scale,
+                    int32_t n, int32_t *row_ws_dev, void *stream);
+
+/* LAP.sample (:65-111): batch draws per stratum (u_dev [n_strata][batch]),
+ * indices -> idx_dev [n_strata][batch], the sampled rows gathered into
+ * out_* [n_strata * batch][dim] (stratum-major). */
+int lap_sample_gather(const lap_tree_desc *t, const lap_storage_desc *st, const float *u_dev, int32_t batch,
+                      int32_t *idx_dev, float *out_state, float *out_action, float *out_next_state,
+                      float *out_reward, float *out_not_done, void *stream);
+
 /* ------------------------------------------------------------------------
  * Fused TD7 net pieces (Agent/TD7_multi_agent.py:53-54, AvgL1Norm).
  * ---------------------------------------------------------------------- */

@@ -101,3 +101,28 @@ def test_reference_single_add_pointer_semantics():
     st = lap.state.cpu().numpy()[:, :, 0]
     assert st[0, 0] == 0 and st[1, 1] == 1 and st[2, 1] == 2 and st[0, 1] == 10 and st[1, 2] == 11
     assert lap.ptr == 2 and lap.size == 2 and lap.count == 6
+
+
+def test_sample_gathers_the_rows_of_its_indices():
+    """lap_sample_gather: the returned batch is the storage rows at lap.ind
+    (stratum-major), with action scaled and not_done = 1 - done as stored."""
+    lap = _lap(4, 64, 16)
+    n = 200
+    g = torch.Generator(device="cuda").manual_seed(1)
+    strata = torch.randint(0, 4, (n,), device="cuda", dtype=torch.int32, generator=g)
+    for step in range(3):
+        obs = torch.randn(n, 80, device="cuda", generator=g)
+        act = torch.rand(n, 7, device="cuda", generator=g) * 2 - 1
+        done = (torch.rand(n, device="cuda", generator=g) < 0.3).to(torch.uint8)
+        lap.add_batch(obs, act, obs + 1, torch.randn(n, device="cuda", generator=g), done, strata)
+    s, a, ns, r, nd = lap.sample()
+    idx = lap.ind.long()
+    rows = (torch.arange(4, device="cuda")[:, None] * 65 + idx).reshape(-1)
+    torch.testing.assert_close(s, lap.state.view(-1, 80)[rows], rtol=0, atol=0)
+    torch.testing.assert_close(a, lap.action.view(-1, 7)[rows], rtol=0, atol=0)
+    torch.testing.assert_close(ns, lap.next_state.view(-1, 80)[rows], rtol=0, atol=0)
+    torch.testing.assert_close(r, lap.reward.view(-1, 1)[rows], rtol=0, atol=0)
+    torch.testing.assert_close(nd, lap.not_done.view(-1, 1)[rows], rtol=0, atol=0)
+    assert int(idx.max()) < 64 and set(torch.unique(nd).tolist()) <= {0.0, 1.0}
+    sizes = lap.size_s.cpu().numpy()
+    assert all(int(idx[k].max()) < sizes[k] for k in range(4))
