@@ -62,6 +62,53 @@ __global__ __launch_bounds__(256) void avgl1_bwd_kernel(const float *__restrict_
     }
 }
 
+
+// Adam (torch.optim.Adam semantics, Agent/TD7_multi_agent.py:165-170 with
+// weight_decay) over one flat parameter buffer: grad += wd * p;
+// m = lerp(m, g, 1 - b1); v = b2 v + (1 - b2) g^2;  p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps).
+// The step count lives on the device: every workgroup reads it, the last one
+// to finish (ticket counter) stores step + 1 and rearms the ticket, so one
+// launch is the whole optimiser step (HIP-graph safe, no host value).
+constexpr int ADAM_THREADS = 256, ADAM_PER_THREAD = 4;
+
+__global__ __launch_bounds__(ADAM_THREADS) void adam_kernel(float *__restrict__ p, const float *__restrict__ g,
+                                                           float *__restrict__ m, float *__restrict__ v,
+                                                           float *step, uint32_t *ticket, long n, float lr, float b1,
+                                                           float b2, float eps, float wd, float gscale) {
+    __shared__ float t_sh;
+    if (threadIdx.x == 0) t_sh = *step + 1.0f;
+    __syncthreads();
+    const float t = t_sh;
+    const float bc1 = 1.0f - powf(b1, t), bc2 = 1.0f - powf(b2, t);
+    const float step_size = lr / bc1, bc2s = sqrtf(bc2);
+    const long base = ((long)blockIdx.x * ADAM_THREADS + threadIdx.x) * ADAM_PER_THREAD;
+#pragma unroll
+    for (int k = 0; k < ADAM_PER_THREAD; ++k) {
+        const long i = base + k;
+        if (i >= n) break;
+        const float pi = p[i];
+        float gi = g[i] * gscale;
+        if (wd != 0.0f) gi += wd * pi;
+        float mi = m[i];
+        mi += (1.0f - b1) * (gi - mi); // lerp_(grad, 1 - beta1)
+        const float vi = v[i] * b2 + (1.0f - b2) * gi * gi;
+        m[i] = mi;
+        v[i] = vi;
+        p[i] = pi - step_size * (mi / (sqrtf(vi) / bc2s + eps));
+    }
+    // last workgroup out advances the device step count
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        const uint32_t done = atomicAdd(ticket, 1u);
+        if (done == gridDim.x - 1) {
+            *step = t;
+            *ticket = 0u;
+            __threadfence();
+        }
+    }
+}
+
 } // namespace
 
 extern "C" {
@@ -83,6 +130,17 @@ int td7_avgl1norm_bwd(const float *x, const float *mean_in, const float *gy, flo
     if (rows == 0) return EXO_OK;
     hipLaunchKernelGGL(avgl1_bwd_kernel, dim3((rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK), dim3(256), 0,
                        (hipStream_t)stream, x, mean_in, gy, gx, rows, cols, eps);
+    return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
+}
+
+/* One Adam step over a flat fp32 buffer of n parameters (see adam_kernel). */
+int td7_adam_step(float *p, const float *g, float *m, float *v, float *step, uint32_t *ticket, int64_t n, float lr,
+                  float beta1, float beta2, float eps, float weight_decay, float grad_scale, void *stream) {
+    if (!p || !g || !m || !v || !step || !ticket || n <= 0) return EXO_EINVAL;
+    const long per_block = (long)ADAM_THREADS * ADAM_PER_THREAD;
+    const long blocks = (n + per_block - 1) / per_block;
+    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(ADAM_THREADS), 0, (hipStream_t)stream, p, g, m, v,
+                       step, ticket, (long)n, lr, beta1, beta2, eps, weight_decay, grad_scale);
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 

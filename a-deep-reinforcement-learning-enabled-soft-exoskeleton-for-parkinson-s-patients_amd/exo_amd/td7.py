@@ -27,6 +27,7 @@ import torch.distributed as dist
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import _native as nat
 from . import ops
 from .ops import avg_l1_norm
 
@@ -204,6 +205,75 @@ class Critic(nn.Module):
         return x.squeeze(2).t()
 
 
+def flatten_params(module):
+    """Re-seat every parameter of `module` as a view of one contiguous fp32
+    buffer (parameter order) and return the buffer."""
+    params = list(module.parameters())
+    flat = torch.cat([p.detach().reshape(-1) for p in params])
+    off = 0
+    for p in params:
+        n = p.numel()
+        p.data = flat[off:off + n].view_as(p)
+        off += n
+    return flat
+
+
+class FlatAdam(torch.optim.Adam):
+    """torch.optim.Adam (same hyper-parameters, same state_dict layout:
+    per-parameter step / exp_avg / exp_avg_sq) whose parameters, moments and
+    step count live in flat device buffers; step() is one gradient concat and
+    one td7_adam_step launch (csrc/td7_ops.hip) instead of PyTorch's
+    multi-tensor kernels.  step(flat_grad=g) takes an already flat (e.g.
+    all-reduced) gradient, scaled by grad_scale inside the kernel."""
+
+    def __init__(self, module, lr, weight_decay=0.0, betas=(0.9, 0.999), eps=1e-8):
+        self.flat = flatten_params(module)
+        params = list(module.parameters())
+        super().__init__(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+        self.m = torch.zeros_like(self.flat)
+        self.v = torch.zeros_like(self.flat)
+        self._step = torch.zeros((), dtype=torch.float32, device=self.flat.device)
+        self._ticket = torch.zeros((1,), dtype=torch.int32, device=self.flat.device)
+        self._bind_state()
+
+    def _params(self):
+        return self.param_groups[0]["params"]
+
+    def _bind_state(self):
+        off = 0
+        for p in self._params():
+            n = p.numel()
+            self.state[p] = {"step": self._step, "exp_avg": self.m[off:off + n].view_as(p),
+                             "exp_avg_sq": self.v[off:off + n].view_as(p)}
+            off += n
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        off, step = 0, None
+        with torch.no_grad():
+            for p in self._params():
+                n = p.numel()
+                st = self.state.get(p, {})
+                if "exp_avg" in st:
+                    self.m[off:off + n].copy_(st["exp_avg"].reshape(-1))
+                    self.v[off:off + n].copy_(st["exp_avg_sq"].reshape(-1))
+                    step = st["step"]
+                off += n
+            self._step.fill_(float(step) if step is not None else 0.0)
+        self._bind_state()
+
+    @torch.no_grad()
+    def step(self, closure=None, flat_grad=None, grad_scale=1.0):
+        g = flat_grad if flat_grad is not None else torch.cat([p.grad.reshape(-1) for p in self._params()])
+        grp = self.param_groups[0]
+        b1, b2 = grp["betas"]
+        nat.check(nat.lib().td7_adam_step(nat.ptr(self.flat), nat.ptr(g), nat.ptr(self.m), nat.ptr(self.v),
+                                          nat.ptr(self._step), nat.ptr(self._ticket), self.flat.numel(),
+                                          float(grp["lr"]), float(b1), float(b2), float(grp["eps"]),
+                                          float(grp["weight_decay"]), float(grad_scale),
+                                          nat.stream_ptr(self.flat.device)), "td7_adam_step")
+
+
 class GradSync:
     """Data-parallel gradient exchange: one flat fp32 bucket per module set,
     one all-reduce (AVG) per optimiser step (RCCL over xGMI; gloo on CPU)."""
@@ -278,12 +348,16 @@ class TD7Learner:
             self.sync.broadcast_module(m)
         if fused_adam is None:
             fused_adam = self.device.type == "cuda"
-        kw = dict(weight_decay=1e-7, fused=True) if fused_adam else dict(weight_decay=1e-7)
-        if graph_safe:
-            kw["capturable"] = True  # optimiser step counters on the device (HIP graph replay)
-        self.actor_optimizer = torch.optim.Adam(self.actor.parameters(), lr=hp.actor_lr, **kw)
-        self.critic_optimizer = torch.optim.Adam(self.critic.parameters(), lr=hp.critic_lr, **kw)
-        self.encoder_optimizer = torch.optim.Adam(self.encoder.parameters(), lr=hp.encoder_lr, **kw)
+        if fused_adam:
+            # one flat parameter buffer per net, one td7_adam_step launch per step
+            self.actor_optimizer = FlatAdam(self.actor, lr=hp.actor_lr, weight_decay=1e-7)
+            self.critic_optimizer = FlatAdam(self.critic, lr=hp.critic_lr, weight_decay=1e-7)
+            self.encoder_optimizer = FlatAdam(self.encoder, lr=hp.encoder_lr, weight_decay=1e-7)
+        else:
+            kw = dict(weight_decay=1e-7)
+            self.actor_optimizer = torch.optim.Adam(self.actor.parameters(), lr=hp.actor_lr, **kw)
+            self.critic_optimizer = torch.optim.Adam(self.critic.parameters(), lr=hp.critic_lr, **kw)
+            self.encoder_optimizer = torch.optim.Adam(self.encoder.parameters(), lr=hp.encoder_lr, **kw)
         self.actor_target = copy.deepcopy(self.actor)
         self.critic_target = copy.deepcopy(self.critic)
         self.fixed_encoder = copy.deepcopy(self.encoder)

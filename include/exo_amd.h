@@ -205,6 +205,15 @@ int td7_avgl1norm_fwd(const float *x_dev, float *y_dev, float *mean_out_dev, int
 int td7_avgl1norm_bwd(const float *x_dev, const float *mean_dev, const float *gy_dev, float *gx_dev, int32_t rows,
                       int32_t cols, float eps, void *stream);
 
+/* torch.optim.Adam step (Agent/TD7_multi_agent.py:165-170, weight_decay) over a
+ * flat buffer of n parameters: g *= grad_scale; g += wd p; m, v, p updated in
+ * place.  *step_dev (float, the optimiser's step count) is read by every
+ * workgroup and advanced by the last one (ticket_dev: one uint32, zero at
+ * the first call, left zero by every call). */
+int td7_adam_step(float *p_dev, const float *g_dev, float *m_dev, float *v_dev, float *step_dev, uint32_t *ticket_dev,
+                  int64_t n, float lr, float beta1, float beta2, float eps, float weight_decay, float grad_scale,
+                  void *stream);
+
 /* ------------------------------------------------------------------------
  * Fused dense layers of the TD7 nets on fp32 MFMA (csrc/td7_dense.hip).
  * Each replaces one nn.Linear + activation of Agent/TD7_multi_agent.py:61-140

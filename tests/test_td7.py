@@ -146,3 +146,40 @@ def test_loads_shipped_reference_checkpoint():
     assert act.shape == (4, 7) and torch.all(act.abs() <= 1)
     q = c(s, act, e.zsa(e.zs(s), act), e.zs(s))
     assert q.shape == (4, 2) and torch.isfinite(q).all()
+
+
+@pytest.mark.gpu
+def test_flat_adam_matches_torch_adam():
+    """FlatAdam (td7_adam_step) vs torch.optim.Adam on the same net and
+    gradients, over several steps; state_dict round trip keeps the moments."""
+    import copy
+
+    import torch.nn.functional as F
+    from exo_amd.td7 import Encoder, FlatAdam
+    torch.manual_seed(0)
+    net = Encoder(80, 7, 64, 96, F.elu).cuda()
+    ref = copy.deepcopy(net)
+    opt = FlatAdam(net, lr=3e-4, weight_decay=1e-7)
+    opt_ref = torch.optim.Adam(ref.parameters(), lr=3e-4, weight_decay=1e-7)
+    for it in range(5):
+        x = torch.randn(128, 80, device="cuda")
+        a = torch.randn(128, 7, device="cuda")
+        for m, o in ((net, opt), (ref, opt_ref)):
+            o.zero_grad(set_to_none=True)
+            zs = m.zs(x)
+            (m.zsa(zs, a).square().mean() + zs.abs().mean()).backward()
+        for p, q in zip(net.parameters(), ref.parameters()):
+            torch.testing.assert_close(p.grad, q.grad, rtol=1e-4, atol=1e-6)
+        opt.step()
+        opt_ref.step()
+        for p, q in zip(net.parameters(), ref.parameters()):
+            torch.testing.assert_close(p, q, rtol=1e-5, atol=1e-6)
+    assert float(opt._step) == 5.0
+    sd = opt.state_dict()
+    opt2 = FlatAdam(copy.deepcopy(net), lr=3e-4, weight_decay=1e-7)
+    opt2.load_state_dict(sd)
+    torch.testing.assert_close(opt2.m, opt.m)
+    torch.testing.assert_close(opt2.v, opt.v)
+    assert float(opt2._step) == 5.0
+    # the reference's torch Adam loads a FlatAdam state_dict
+    opt_ref.load_state_dict(sd)
