@@ -87,16 +87,16 @@ class VecTrainer:
         self._batch = ag.replay_buffer.sample()
         self._prio = ag.learner.phase_grads(*self._batch)
 
-    def _mid(self, update_actor):
+    def _mid(self, update_actor, flat_grad=None, grad_scale=1.0):
         ag = self.agent
-        ag.learner.phase_steps()
+        ag.learner.phase_steps(flat_grad, grad_scale)
         ag.replay_buffer.update_priority(self._prio)
         if update_actor:
             ag.learner.phase_actor_grads(self._batch[0], self._batch[1])
 
-    def _post(self, update_actor):
+    def _post(self, update_actor, flat_grad=None, grad_scale=1.0):
         if update_actor:
-            self.agent.learner.phase_actor_step()
+            self.agent.learner.phase_actor_step(flat_grad, grad_scale)
 
     def _eager(self, update_actor):
         L = self.agent.learner
@@ -132,15 +132,13 @@ class VecTrainer:
                     flat_c = S.pack(L.grad_params())
                 pool = g1.pool()
                 flat_a = None
+                scale = 1.0 / S.world
                 with torch.cuda.graph(g2, pool=pool, stream=s):
-                    S.unpack(flat_c, L.grad_params())
-                    self._mid(update_actor)
+                    self._mid(update_actor, flat_c, scale)   # the optimisers read the reduced bucket in place
                     if update_actor:
                         flat_a = S.pack(L.grad_params(actor=True))
                 with torch.cuda.graph(g3, pool=pool, stream=s):
-                    if update_actor:
-                        S.unpack(flat_a, L.grad_params(actor=True))
-                    self._post(update_actor)
+                    self._post(update_actor, flat_a, scale)
                 parts = [g1, g2, g3, flat_c, flat_a]
         torch.cuda.current_stream(self.device).wait_stream(s)
         self.graphs[update_actor] = parts

@@ -436,7 +436,15 @@ class TD7Learner:
         self._fixed_zs = fixed_zs
         return td_loss.detach().max(1)[0].clamp(min=hp.min_priority).pow(hp.alpha)  # :262
 
-    def phase_steps(self):
+    def phase_steps(self, flat_grad=None, grad_scale=1.0):
+        """Encoder and critic optimiser steps; flat_grad: their gradients packed
+        in grad_params() order (the data-parallel all-reduce bucket), consumed
+        in place by FlatAdam."""
+        if flat_grad is not None and isinstance(self.encoder_optimizer, FlatAdam):
+            ne = self.encoder_optimizer.flat.numel()
+            self.encoder_optimizer.step(flat_grad=flat_grad[:ne], grad_scale=grad_scale)
+            self.critic_optimizer.step(flat_grad=flat_grad[ne:], grad_scale=grad_scale)
+            return
         self.encoder_optimizer.step()
         self.critic_optimizer.step()
 
@@ -454,7 +462,10 @@ class TD7Learner:
         self.actor_optimizer.zero_grad(set_to_none=self.grads_to_none)
         actor_loss.backward()
 
-    def phase_actor_step(self):
+    def phase_actor_step(self, flat_grad=None, grad_scale=1.0):
+        if flat_grad is not None and isinstance(self.actor_optimizer, FlatAdam):
+            self.actor_optimizer.step(flat_grad=flat_grad, grad_scale=grad_scale)
+            return
         self.actor_optimizer.step()
 
     def grad_params(self, actor=False):
