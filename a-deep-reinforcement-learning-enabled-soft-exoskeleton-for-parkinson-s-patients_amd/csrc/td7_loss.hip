@@ -1,0 +1,103 @@
+// td7_loss.hip -- the scalar tail of the TD7 critic update (gfx950).
+//
+// Agent/TD7_multi_agent.py:240-262, per row b of a batch of B (<= 65536):
+//   Q_target = reward + not_done * discount * clamp(min_h Qt[b][h], min_target, max_target)
+//   running max / min of Q_target                                    (:245-246)
+//   td = |Q[b][h] - Q_target[b]|;  loss = mean_b sum_h LAP_huber(td)  (:257-259, :57-58)
+//   priority = max_h(td).clamp(min = min_priority) ** alpha          (:262)
+// PyTorch spends ~25 elementwise/reduction launches on these (and as many on
+// the loss backward); here it is one workgroup per call: q_target, and
+// critic_loss which also leaves dloss/dQ per element for the backward.
+#include <hip/hip_runtime.h>
+
+#include "exo_amd.h"
+
+namespace {
+
+constexpr int T = 1024;
+
+__device__ float block_reduce(float v, int op, float *sh) { // op 0 sum, 1 max, 2 min
+    for (int o = 32; o > 0; o >>= 1) {
+        const float u = __shfl_xor(v, o, 64);
+        v = op == 0 ? v + u : (op == 1 ? fmaxf(v, u) : fminf(v, u));
+    }
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < T / 64; ++k) v = op == 0 ? v + sh[k] : (op == 1 ? fmaxf(v, sh[k]) : fminf(v, sh[k]));
+        sh[0] = v;
+    }
+    __syncthreads();
+    return sh[0];
+}
+
+__global__ __launch_bounds__(T) void q_target_kernel(const float *qt, long qs_b, long qs_h, const float *reward,
+                                                     const float *not_done, float discount, const float *lo,
+                                                     const float *hi, float *run_max, float *run_min, float *out,
+                                                     int B) {
+    __shared__ float sh[T / 64];
+    const float l = *lo, h = *hi;
+    float mx = -INFINITY, mn = INFINITY;
+    for (int b = threadIdx.x; b < B; b += T) {
+        const float q = fminf(qt[b * qs_b], qt[b * qs_b + qs_h]);
+        const float c = fminf(fmaxf(q, l), h);                 // torch.clamp(min=l, max=h)
+        const float v = reward[b] + (not_done[b] * discount) * c;
+        out[b] = v;
+        mx = fmaxf(mx, v);
+        mn = fminf(mn, v);
+    }
+    mx = block_reduce(mx, 1, sh);
+    mn = block_reduce(mn, 2, sh);
+    if (threadIdx.x == 0) {
+        *run_max = fmaxf(*run_max, mx);
+        *run_min = fminf(*run_min, mn);
+    }
+}
+
+__global__ __launch_bounds__(T) void critic_loss_kernel(const float *q, long qs_b, long qs_h, const float *qtarget,
+                                                        float *loss, float *priority, float *dq, float alpha,
+                                                        float min_priority, int B) {
+    __shared__ float sh[T / 64];
+    float acc = 0.f;
+    const float inv_b = 1.0f / (float)B;
+    for (int b = threadIdx.x; b < B; b += T) {
+        const float t = qtarget[b];
+        float tdmax = 0.f;
+        for (int hd = 0; hd < 2; ++hd) {
+            const float d = q[b * qs_b + hd * qs_h] - t;
+            const float x = fabsf(d);
+            acc += x < 1.0f ? 0.5f * x * x : x;               // LAP_huber, min_priority = 1 (:259)
+            const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+            dq[2 * b + hd] = inv_b * (x < 1.0f ? x : 1.0f) * sg;
+            tdmax = fmaxf(tdmax, x);
+        }
+        priority[b] = powf(fmaxf(tdmax, min_priority), alpha);
+    }
+    acc = block_reduce(acc, 0, sh);
+    if (threadIdx.x == 0) *loss = acc * inv_b;
+}
+
+} // namespace
+
+extern "C" {
+
+int td7_q_target(const float *qt, long qs_b, long qs_h, const float *reward, const float *not_done, float discount,
+                 const float *min_target, const float *max_target, float *run_max, float *run_min, float *out,
+                 int32_t batch, void *stream) {
+    if (!qt || !reward || !not_done || !min_target || !max_target || !run_max || !run_min || !out || batch <= 0)
+        return EXO_EINVAL;
+    hipLaunchKernelGGL(q_target_kernel, dim3(1), dim3(T), 0, (hipStream_t)stream, qt, qs_b, qs_h, reward, not_done,
+                       discount, min_target, max_target, run_max, run_min, out, batch);
+    return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
+}
+
+int td7_critic_loss(const float *q, long qs_b, long qs_h, const float *q_target, float *loss, float *priority,
+                    float *dq, float alpha, float min_priority, int32_t batch, void *stream) {
+    if (!q || !q_target || !loss || !priority || !dq || batch <= 0) return EXO_EINVAL;
+    hipLaunchKernelGGL(critic_loss_kernel, dim3(1), dim3(T), 0, (hipStream_t)stream, q, qs_b, qs_h, q_target, loss,
+                       priority, dq, alpha, min_priority, batch);
+    return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
+}
+
+} // extern "C"

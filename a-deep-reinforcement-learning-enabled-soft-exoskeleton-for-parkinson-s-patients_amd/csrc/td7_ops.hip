@@ -75,16 +75,18 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_kernel(float *__restrict__ 
                                                            float *__restrict__ m, float *__restrict__ v,
                                                            float *step, uint32_t *ticket, long n, float lr, float b1,
                                                            float b2, float eps, float wd, float gscale) {
-    __shared__ float t_sh;
-    if (threadIdx.x == 0) t_sh = *step + 1.0f;
+    __shared__ float coef[2];
+    if (threadIdx.x == 0) { // bias corrections once per workgroup
+        const float t = *step + 1.0f;
+        coef[0] = lr / (1.0f - powf(b1, t));        // step_size
+        coef[1] = sqrtf(1.0f - powf(b2, t));        // sqrt(bias_correction2)
+    }
     __syncthreads();
-    const float t = t_sh;
-    const float bc1 = 1.0f - powf(b1, t), bc2 = 1.0f - powf(b2, t);
-    const float step_size = lr / bc1, bc2s = sqrtf(bc2);
-    const long base = ((long)blockIdx.x * ADAM_THREADS + threadIdx.x) * ADAM_PER_THREAD;
+    const float step_size = coef[0], bc2s = coef[1];
+    const long base = (long)blockIdx.x * ADAM_THREADS * ADAM_PER_THREAD + threadIdx.x;
 #pragma unroll
     for (int k = 0; k < ADAM_PER_THREAD; ++k) {
-        const long i = base + k;
+        const long i = base + (long)k * ADAM_THREADS; // coalesced: consecutive lanes, consecutive elements
         if (i >= n) break;
         const float pi = p[i];
         float gi = g[i] * gscale;
@@ -102,7 +104,7 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_kernel(float *__restrict__ 
         __threadfence();
         const uint32_t done = atomicAdd(ticket, 1u);
         if (done == gridDim.x - 1) {
-            *step = t;
+            *step = *step + 1.0f;
             *ticket = 0u;
             __threadfence();
         }

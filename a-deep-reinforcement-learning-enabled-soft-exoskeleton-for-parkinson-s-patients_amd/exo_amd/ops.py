@@ -1,6 +1,8 @@
 """Fused TD7 net ops backed by csrc/td7_ops.hip (GPU) with the reference's
 torch expression on CPU tensors (the CPU path exists for the learner's parity
 tests; on a GPU the HIP kernels are mandatory -- a missing library raises)."""
+import os
+
 import torch
 
 from . import _native as nat
@@ -68,7 +70,7 @@ class _DenseFn(torch.autograd.Function):
     launches where autograd issues the activation backward, two GEMMs, a
     column reduction and a fill."""
 
-    fwd_kernel = False
+    fwd_kernel = os.environ.get("EXO_DENSE_FWD") == "1"
 
     @staticmethod
     def forward(ctx, x, w, b, act):
@@ -134,3 +136,54 @@ def dense(x, w, b, act=0):
             and not torch.is_autocast_enabled():
         return _DenseFn.apply(x, w, b, act)
     return _torch_dense(x, w, b, act)
+
+
+# ---------------------------------------------------------------- critic tail
+def q_target(qt, reward, not_done, discount, min_target, max_target, run_max, run_min):
+    """Q_target (Agent/TD7_multi_agent.py:240-246) from the target critic's
+    two heads qt [B,2]; updates the running bounds run_max / run_min in place.
+    One td7_q_target launch on a GPU; the reference expression on a CPU."""
+    if not qt.is_cuda:
+        q = qt.min(1, keepdim=True)[0]
+        out = reward + not_done * discount * q.clamp(min_target, max_target)
+        torch.maximum(run_max, out.max(), out=run_max)
+        torch.minimum(run_min, out.min(), out=run_min)
+        return out
+    B = qt.shape[0]
+    out = torch.empty((B, 1), dtype=torch.float32, device=qt.device)
+    nat.check(nat.lib().td7_q_target(nat.ptr(qt), qt.stride(0), qt.stride(1), nat.ptr(reward.contiguous()),
+                                     nat.ptr(not_done.contiguous()), float(discount), nat.ptr(min_target),
+                                     nat.ptr(max_target), nat.ptr(run_max), nat.ptr(run_min), nat.ptr(out), B,
+                                     nat.stream_ptr(qt.device)), "td7_q_target")
+    return out
+
+
+class _CriticLossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, q_target, alpha, min_priority):
+        B = q.shape[0]
+        loss = torch.empty((), dtype=torch.float32, device=q.device)
+        prio = torch.empty((B,), dtype=torch.float32, device=q.device)
+        dq = torch.empty((B, 2), dtype=torch.float32, device=q.device)
+        nat.check(nat.lib().td7_critic_loss(nat.ptr(q), q.stride(0), q.stride(1), nat.ptr(q_target.contiguous()),
+                                            nat.ptr(loss), nat.ptr(prio), nat.ptr(dq), float(alpha),
+                                            float(min_priority), B, nat.stream_ptr(q.device)), "td7_critic_loss")
+        ctx.save_for_backward(dq)
+        ctx.mark_non_differentiable(prio)
+        return loss, prio
+
+    @staticmethod
+    def backward(ctx, gloss, gprio):
+        (dq,) = ctx.saved_tensors
+        return dq * gloss, None, None, None
+
+
+def critic_loss(q, q_target, alpha, min_priority):
+    """(LAP_huber(|q - q_target|), priority) of Agent/TD7_multi_agent.py:257-262
+    for the critic's two heads q [B,2] -- one td7_critic_loss launch forward,
+    one multiply backward on a GPU; the reference expressions on a CPU."""
+    if not q.is_cuda:
+        td = (q - q_target).abs()
+        loss = torch.where(td < 1, 0.5 * td.pow(2), 1 * td).sum(1).mean()
+        return loss, td.detach().max(1)[0].clamp(min=min_priority).pow(alpha)
+    return _CriticLossFn.apply(q, q_target, alpha, min_priority)

@@ -418,23 +418,23 @@ class TD7Learner:
                 self.target_policy_noise -= self.policy_noise_decrease
                 next_action = (self.actor_target(next_state, fixed_target_zs) + noise).clamp(-1, 1)
                 fixed_target_zsa = self.fixed_encoder_target.zsa(fixed_target_zs, next_action)
-                Q_target = self.critic_target(next_state, next_action, fixed_target_zsa,
-                                              fixed_target_zs).float().min(1, keepdim=True)[0]
-            Q_target = reward + not_done * hp.discount * Q_target.clamp(self.min_target, self.max_target)
-            # running bounds (:245-246); kept per rank, MAX-reduced when the targets refresh
-            torch.maximum(self.max, Q_target.max(), out=self.max)
-            torch.minimum(self.min, Q_target.min(), out=self.min)
+                Q_heads = self.critic_target(next_state, next_action, fixed_target_zsa, fixed_target_zs).float()
+            # Q_target and the running bounds (:240-246; bounds kept per rank,
+            # MAX-reduced when the targets refresh): one td7_q_target launch
+            Q_target = ops.q_target(Q_heads, reward, not_done, hp.discount, self.min_target, self.max_target,
+                                    self.max, self.min)
             with self._autocast():
                 fixed_zs = self.fixed_encoder.zs(state)
                 fixed_zsa = self.fixed_encoder.zsa(fixed_zs, action)
         with self._autocast():
             Q = self.critic(state, action, fixed_zsa, fixed_zs)
-        td_loss = (Q.float() - Q_target).abs()
-        critic_loss = LAP_huber(td_loss)
+        # LAP_huber critic loss and the new priorities (:257-262): one
+        # td7_critic_loss launch forward, one multiply backward
+        critic_loss, priority = ops.critic_loss(Q.float(), Q_target, hp.alpha, hp.min_priority)
         self.critic_optimizer.zero_grad(set_to_none=self.grads_to_none)
         critic_loss.backward()
         self._fixed_zs = fixed_zs
-        return td_loss.detach().max(1)[0].clamp(min=hp.min_priority).pow(hp.alpha)  # :262
+        return priority
 
     def phase_steps(self, flat_grad=None, grad_scale=1.0):
         """Encoder and critic optimiser steps; flat_grad: their gradients packed

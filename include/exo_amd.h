@@ -214,6 +214,18 @@ int td7_adam_step(float *p_dev, const float *g_dev, float *m_dev, float *v_dev, 
                   int64_t n, float lr, float beta1, float beta2, float eps, float weight_decay, float grad_scale,
                   void *stream);
 
+/* Critic target (Agent/TD7_multi_agent.py:240-246): out[b] = reward[b] +
+ * not_done[b] * discount * clamp(min(qt[b][0], qt[b][1]), *min_target,
+ * *max_target); *run_max / *run_min take the batch max / min.  qt element
+ * (b, h) at qt_dev[b*qs_b + h*qs_h]. */
+int td7_q_target(const float *qt_dev, long qs_b, long qs_h, const float *reward_dev, const float *not_done_dev,
+                 float discount, const float *min_target_dev, const float *max_target_dev, float *run_max_dev,
+                 float *run_min_dev, float *out_dev, int32_t batch, void *stream);
+/* Critic loss (:257-262): loss = mean_b sum_h LAP_huber(|q[b][h] - q_target[b]|),
+ * priority[b] = max(max_h td, min_priority)^alpha, dq [batch][2] = dloss/dq. */
+int td7_critic_loss(const float *q_dev, long qs_b, long qs_h, const float *q_target_dev, float *loss_dev,
+                    float *priority_dev, float *dq_dev, float alpha, float min_priority, int32_t batch, void *stream);
+
 /* ------------------------------------------------------------------------
  * Fused dense layers of the TD7 nets on fp32 MFMA (csrc/td7_dense.hip).
  * Each replaces one nn.Linear + activation of Agent/TD7_multi_agent.py:61-140

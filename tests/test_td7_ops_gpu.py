@@ -32,3 +32,32 @@ def test_avgl1norm_clamped_rows_and_3d():
     xb = x.clone().requires_grad_(True)
     (xb / xb.abs().mean(-1, keepdim=True).clamp(min=1e-8)).sum().backward()
     torch.testing.assert_close(xa.grad, xb.grad, rtol=1e-5, atol=1e-5)
+
+
+def test_q_target_and_critic_loss_match_reference_expressions():
+    """td7_q_target / td7_critic_loss vs the reference's torch expressions
+    (Agent/TD7_multi_agent.py:240-262) on the same inputs."""
+    from exo_amd import ops
+    torch.manual_seed(3)
+    B = 1024
+    qt = torch.randn(2, B, device="cuda").t() * 5          # [B,2] view of [2,B], like Critic.forward's output
+    reward = torch.randn(B, 1, device="cuda")
+    not_done = (torch.rand(B, 1, device="cuda") > 0.1).float()
+    lo, hi = torch.tensor(-3.0, device="cuda"), torch.tensor(4.0, device="cuda")
+    rmax, rmin = torch.tensor(-1e8, device="cuda"), torch.tensor(1e8, device="cuda")
+    out = ops.q_target(qt, reward, not_done, 0.99, lo, hi, rmax, rmin)
+    ref = reward + not_done * 0.99 * qt.min(1, keepdim=True)[0].clamp(lo, hi)
+    torch.testing.assert_close(out, ref, rtol=1e-6, atol=1e-6)
+    assert float(rmax) == float(ref.max()) and float(rmin) == float(ref.min())
+
+    q = (torch.randn(2, B, device="cuda").t() * 2).requires_grad_(True)
+    q_ref = q.detach().clone().requires_grad_(True)
+    loss, prio = ops.critic_loss(q, out, 0.4, 1.0)
+    td = (q_ref - out).abs()
+    loss_ref = torch.where(td < 1, 0.5 * td.pow(2), 1 * td).sum(1).mean()
+    prio_ref = td.detach().max(1)[0].clamp(min=1.0).pow(0.4)
+    torch.testing.assert_close(loss, loss_ref, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(prio, prio_ref, rtol=1e-6, atol=1e-6)
+    loss.backward()
+    loss_ref.backward()
+    torch.testing.assert_close(q.grad, q_ref.grad, rtol=1e-6, atol=1e-8)
