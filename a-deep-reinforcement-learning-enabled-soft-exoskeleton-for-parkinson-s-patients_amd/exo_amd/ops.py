@@ -51,6 +51,18 @@ def act_code(fn):
     return {F.relu: 1, torch.relu: 1, F.elu: 2, torch.tanh: 3}.get(fn)
 
 
+def _engine_needs(ctx, i):
+    """False when the running backward (e.g. torch.autograd.grad with explicit
+    inputs) will not use input i's gradient -- its GEMM is then skipped."""
+    fn = ctx.next_functions[i][0]
+    if fn is None:
+        return False
+    try:
+        return torch._C._will_engine_execute_node(fn)
+    except (AttributeError, RuntimeError):
+        return True
+
+
 def _rows(t):
     """(tensor with unit column stride, row stride)."""
     if t.stride(-1) != 1:
@@ -100,12 +112,13 @@ class _DenseFn(torch.autograd.Function):
         dy = dy.contiguous()
         s = nat.stream_ptr(dy.device)
         dx = dw = db = None
-        if ctx.needs_input_grad[0]:
+        need = [ctx.needs_input_grad[i] and _engine_needs(ctx, i) for i in range(3)]
+        if need[0]:
             dx = torch.empty((G, M, K) if (grouped and not shared) else (M, K), dtype=torch.float32, device=dy.device)
             nat.check(nat.lib().td7_dense_bwd_data(nat.ptr(dy), M * N, N, nat.ptr(y), M * N, N, nat.ptr(w),
                                                    nat.ptr(dx), M * K, K, G, int(shared), M, N, K, act, s),
                       "td7_dense_bwd_data")
-        if ctx.needs_input_grad[1] or (has_b and ctx.needs_input_grad[2]):
+        if need[1] or (has_b and need[2]):
             dw = torch.empty_like(w)
             db = torch.empty((G, N) if grouped else (N,), dtype=torch.float32, device=dy.device) if has_b else None
             nat.check(nat.lib().td7_dense_bwd_weight(nat.ptr(dy), M * N, N, nat.ptr(y), M * N, N, nat.ptr(x), xsg,

@@ -460,7 +460,16 @@ class TD7Learner:
             actor_loss = actor_loss + self.hp.lmbda * Q.float().abs().mean().detach() * F.mse_loss(actor.float(),
                                                                                                action)
         self.actor_optimizer.zero_grad(set_to_none=self.grads_to_none)
-        actor_loss.backward()
+        # gradients of the actor's parameters only: the reference's backward()
+        # also accumulates critic / fixed-encoder gradients that its next
+        # zero_grad() discards (:275-277) -- skipping them skips their GEMMs
+        params = list(self.actor.parameters())
+        grads = torch.autograd.grad(actor_loss, params)
+        for p, g in zip(params, grads):
+            if p.grad is None:
+                p.grad = g
+            else:
+                p.grad.add_(g)
 
     def phase_actor_step(self, flat_grad=None, grad_scale=1.0):
         if flat_grad is not None and isinstance(self.actor_optimizer, FlatAdam):
