@@ -37,7 +37,7 @@ __device__ unsigned long long *g_exo_stamps;
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                             \
         __builtin_amdgcn_sched_barrier(0);                                                                        \
         if (g_exo_stamps && (threadIdx.x & 63) == __builtin_amdgcn_readfirstlane(threadIdx.x & 63))               \
-            g_exo_stamps[(size_t)blockIdx.x * 8 + (k)] = _t;                                                      \
+            g_exo_stamps[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + (k)] = _t;                                                      \
     } while (0)
 #else
 #define STAMP(k) do {} while (0)
@@ -173,13 +173,18 @@ __device__ __forceinline__ void anchor(const Urdf &U, int link, const double *R2
     else xform(R2, p0, U.xyz[link], o);
 }
 
-__global__ __launch_bounds__(64) void exo_step_rp_kernel(Dev S, Urdf U, const float *__restrict__ act,
-                                                         float *__restrict__ obs, float *__restrict__ rew,
-                                                         uint8_t *__restrict__ done, float *__restrict__ info,
-                                                         const uint8_t *__restrict__ active) {
-    const int lane = threadIdx.x;
+// 16 envs (4 wavefronts) per workgroup: the state is SoA over envs, so one
+// 128-byte line of a double field holds 16 consecutive envs -- a 4-env
+// workgroup left each line to four workgroups on (round-robin) different XCDs
+// and HBM fetched it up to four times (PMC: 3.1x the algorithmic bytes).
+constexpr int RP_ENVS_PER_BLOCK = 16;
+
+__global__ __launch_bounds__(64 * RP_ENVS_PER_BLOCK / 4) void exo_step_rp_kernel(
+    Dev S, Urdf U, const float *__restrict__ act, float *__restrict__ obs, float *__restrict__ rew,
+    uint8_t *__restrict__ done, float *__restrict__ info, const uint8_t *__restrict__ active) {
+    const int lane = threadIdx.x & 63;
     const int sub = lane & 15, grp = sub >> 3, r = sub & 7, gbase = lane & ~7, ebase = lane & ~15;
-    const int e = blockIdx.x * 4 + (lane >> 4);
+    const int e = blockIdx.x * RP_ENVS_PER_BLOCK + (threadIdx.x >> 4);
     if (e >= S.N) return;
     const int N = S.N, c = S.counts[e], L = S.L[e];
     if ((active && !active[e]) || c >= L - 1) return; // uniform over the env's 16 lanes
@@ -392,7 +397,8 @@ extern "C" int exo_debug_set_stamps(unsigned long long *buf) {
 namespace exo {
 hipError_t launch_exo_step_rp(const Dev &S, const Urdf &U, const float *act, float *obs, float *rew, uint8_t *done,
                               float *info, const uint8_t *active, hipStream_t stream) {
-    hipLaunchKernelGGL(exo_step_rp_kernel, dim3((S.N + 3) / 4), dim3(64), 0, stream, S, U, act, obs, rew, done, info,
+    hipLaunchKernelGGL(exo_step_rp_kernel, dim3((S.N + RP_ENVS_PER_BLOCK - 1) / RP_ENVS_PER_BLOCK),
+                       dim3(64 * RP_ENVS_PER_BLOCK / 4), 0, stream, S, U, act, obs, rew, done, info,
                        active);
     return hipGetLastError();
 }

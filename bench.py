@@ -52,6 +52,36 @@ STEP_WRITE_BYTES = {
 BYTES_PER_ENV_STEP = sum(STEP_READ_BYTES.values()) + sum(STEP_WRITE_BYTES.values())
 
 
+FP32_MFMA_PEAK_TFS = 157.3  # v_mfma_f32_*_f32 dense peak (MI355X_MICROARCH.md)
+
+
+def td7_flops(agent, n_envs):
+    """Matrix flops of one training iteration: every Linear layer's 2*M*N*K,
+    x3 where it is trained (forward, input grad, weight grad), per the
+    reference's update (Agent/TD7_multi_agent.py:211-293) and select_action."""
+    L = agent.learner
+    hp = agent.hp
+    B = hp.batch_size * agent.env_num
+    def net(m, prefix=""):  # multiply-accumulates per row: sum of out*in over the weight matrices
+        macs = 0
+        for name, p in m.named_parameters():
+            if name.startswith(prefix) and p.dim() >= 2:
+                macs += p.numel()  # stacked critic heads [2, out, in] count both
+        return macs
+
+    enc_zs = net(L.encoder, "zs1") + net(L.encoder, "zs2") + net(L.encoder, "zs3")
+    enc_zsa = net(L.encoder) - enc_zs
+    actor, critic = net(L.actor), net(L.critic)
+    macs = 0
+    macs += 3 * (2 * B * enc_zs) + 3 * B * enc_zsa            # encoder: zs(s), zs(s') fwd (+bwd of zs(s)), zsa trained
+    macs += B * (enc_zs + actor + enc_zsa + critic)            # target path (no grad)
+    macs += B * (enc_zs + enc_zsa)                              # fixed embeddings
+    macs += 3 * B * critic                                      # critic trained
+    macs += 0.5 * B * (3 * actor + 2 * (enc_zsa + critic))     # actor update every policy_freq=2 steps
+    macs += n_envs * (enc_zs + actor)                           # select_action for every env
+    return 2.0 * macs
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -235,6 +265,15 @@ def main():
         }
         if agent is not None:
             res["grad_steps_per_sec"] = args.steps / elapsed
+            # TD7 on the fp32 MFMA roofline: the update's GEMM flops
+            # per grad step over the step time left after the env kernel
+            fl = td7_flops(agent, N)
+            td7_s = max(elapsed / args.steps - kern_ms * 1e-3, 1e-9)
+            res["td7_roofline"] = {"bound": "mfma", "achieved": fl / td7_s / 1e12, "peak": FP32_MFMA_PEAK_TFS,
+                                   "unit": "TFLOP/s", "frac": fl / td7_s / 1e12 / FP32_MFMA_PEAK_TFS,
+                                   "gflop_per_step": fl / 1e9,
+                                   "note": "GEMM flops of one train() step (B=1024) + batched actor inference "
+                                           "over the envs, per iteration time minus the env kernel"}
         if finite is not None:
             res["weights_finite"] = all(finite.values()) or finite
         if dp_sync is not None:

@@ -17,4 +17,5 @@ timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex exo_step --o
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex exo_step --output-format csv -d $OUT/pmc_write -o run -- \
     python3 bench.py --mode env --steps 100 --warmup 10 --no-cpu-baseline > $OUT/pmc_write.log 2>&1
 timeout -k 10 400 python3 bench.py > $OUT/bench_default.log 2>&1
+timeout -k 10 200 python3 tools/dense_bench.py > $OUT/dense_bench.txt 2>&1
 find $OUT -name "*.csv" | head -50

@@ -35,7 +35,29 @@ def pmc(d, counter, match="exo_step"):
     return dict(counter=counter, launches=int(v.size), mean_kib=float(v.mean()), median_kib=float(np.median(v)))
 
 
+def iteration_classes(stats_dir):
+    """Kernel classes of one steady-state training iteration (tools/trace_iter.py)."""
+    trace = os.path.join(stats_dir, "run_kernel_trace.csv")
+    if not os.path.exists(trace):
+        return None, []
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import trace_iter
+    rows = list(csv.DictReader(open(trace)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    starts = [i for i, r in enumerate(rows) if "exo_step" in r["Kernel_Name"]]
+    k = len(starts) // 3
+    it = rows[starts[k]:starts[k + 1]]
+    wall = (int(rows[starts[k + 1]]["Start_Timestamp"]) - int(it[0]["Start_Timestamp"])) / 1e3
+    cls = {}
+    for r in it:
+        c = trace_iter.classify(r["Kernel_Name"])
+        n, us = cls.get(c, (0, 0.0))
+        cls[c] = (n + 1, us + (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    return {"kernels": len(it), "wall_us": wall}, sorted(cls.items(), key=lambda x: -x[1][1])
+
+
 def main():
+    """usage: summarize.py ROUND TRAIN_DIR [ENV_DIR] [PMC_FETCH_DIR PMC_WRITE_DIR] [--bytes-per-launch B]"""
     args = sys.argv[1:]
     bpl = None
     if "--bytes-per-launch" in args:
@@ -43,14 +65,29 @@ def main():
         bpl = float(args[i + 1])
         del args[i:i + 2]
     rnd, stats = args[0], args[1]
+    env_dir = args[2] if len(args) in (3, 5) else None
+    pmc_dirs = args[-2:] if len(args) >= 4 else None
     here = os.path.dirname(os.path.abspath(__file__))
     ks = kernel_stats(stats)
     res = {"round": rnd, "kernels": ks[:40]}
-    lines = [f"# rocprofv3 kernel summary ({rnd})", "", "| kernel | calls | total ms | avg us | % |", "|---|---|---|---|---|"]
+    lines = [f"# rocprofv3 kernel summary ({rnd})", "", "Training bench (`bench.py`, default mode), all kernels:", "",
+             "| kernel | calls | total ms | avg us | % |", "|---|---|---|---|---|"]
     for k in ks[:25]:
         lines.append(f"| `{k['name'][:90]}` | {k['calls']} | {k['total_ms']:.2f} | {k['avg_us']:.1f} | {k['pct']:.1f} |")
-    if len(args) >= 4:
-        f, w = pmc(args[2], "FETCH_SIZE"), pmc(args[3], "WRITE_SIZE")
+    meta, cls = iteration_classes(stats)
+    if meta:
+        res["iteration"] = dict(meta, classes={c: {"kernels": n, "us": us} for c, (n, us) in cls})
+        lines += ["", f"One steady-state training iteration under the profiler: {meta['kernels']} kernels, "
+                      f"{meta['wall_us']:.0f} us wall (tracing inflates short kernels):", "",
+                  "| class | kernels | us |", "|---|---|---|"]
+        lines += [f"| {c} | {n} | {us:.1f} |" for c, (n, us) in cls]
+    if env_dir:
+        ek = [k for k in kernel_stats(env_dir) if "exo_step" in k["name"]]
+        res["env_mode_exo_step"] = ek
+        lines += ["", "Env-only bench (`bench.py --mode env`), step kernel:", ""]
+        lines += [f"- `{k['name'][:60]}`: {k['calls']} calls, avg {k['avg_us']:.2f} us" for k in ek]
+    if pmc_dirs:
+        f, w = pmc(pmc_dirs[0], "FETCH_SIZE"), pmc(pmc_dirs[1], "WRITE_SIZE")
         traffic = (2 * f["median_kib"] + w["median_kib"]) * 1024
         res["pmc_exo_step"] = dict(fetch=f, write=w, traffic_bytes_per_launch=traffic,
                                    correction="reads x2 (gfx950 FETCH_SIZE half-tally), KiB x 1024",
