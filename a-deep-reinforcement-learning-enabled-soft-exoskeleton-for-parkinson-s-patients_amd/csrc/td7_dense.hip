@@ -284,6 +284,89 @@ int launch(const GemmArgs &a, int groups_grid, hipStream_t s) {
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 
+
+// Forward Y = act(X W^T + b): one wavefront per 16x16 output tile, the whole
+// reduction loaded up front in groups of GS 16-wide steps (one 16-byte load
+// of X and one of W per lane per step) so a wave makes one or two L2 round
+// trips instead of one per step; the tail (K % 16) is a range-checked step.
+template <int EP, int GS>
+__global__ __launch_bounds__(64) void dense_fwd_kernel(GemmArgs a) {
+    const int lane = threadIdx.x, q = lane >> 4, c = lane & 15;
+    const int i0 = blockIdx.y * 16, j0 = blockIdx.x * 16, g = blockIdx.z;
+    const int row = i0 + c, col = j0 + c;
+    const __amdgpu_buffer_rsrc_t ra = rsrc(a.A.p), rb = rsrc(a.B.p);
+    const int abase = g * (int)a.A.sg + row * (int)a.A.si, bbase = g * (int)a.B.sg + col * (int)a.B.si;
+    const bool arow = row < a.I, bcol = col < a.J;
+    const float bias_v = (a.bias && bcol) ? a.bias[g * a.bsg + col] : 0.f;
+    const int nfull = a.R >> 4;
+    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    for (int s0 = 0; s0 < nfull; s0 += GS) {
+        uint32_t av[GS][4], bv[GS][4];
+#pragma unroll
+        for (int s = 0; s < GS; ++s) {
+            const int r = 16 * (s0 + s) + 4 * q;
+            const bool live = s0 + s < nfull;
+            const auto x = __builtin_amdgcn_raw_buffer_load_b128(ra, (live & arow) ? (abase + r) * 4 : BUF_OOB, 0, 0);
+            const auto y = __builtin_amdgcn_raw_buffer_load_b128(rb, (live & bcol) ? (bbase + r) * 4 : BUF_OOB, 0, 0);
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                av[s][jj] = x[jj];
+                bv[s][jj] = y[jj];
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < GS; ++s) {
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(av[s][0]), __uint_as_float(bv[s][0]), acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(av[s][1]), __uint_as_float(bv[s][1]), acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(av[s][2]), __uint_as_float(bv[s][2]), acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(av[s][3]), __uint_as_float(bv[s][3]), acc1, 0, 0, 0);
+        }
+    }
+    if (a.R & 15) { // tail step
+        const int r = 16 * nfull + 4 * q;
+        float xa[4], xb[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            xa[jj] = ldb(ra, arow & (r + jj < a.R), abase + r + jj);
+            xb[jj] = ldb(rb, bcol & (r + jj < a.R), bbase + r + jj);
+        }
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[0], xb[0], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[1], xb[1], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[2], xb[2], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[3], xb[3], acc1, 0, 0, 0);
+    }
+    const floatx4 acc = acc0 + acc1;
+    if (!bcol) return;
+    // acc[k] is C[i0 + 4q + k][col]
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int rr = i0 + 4 * q + k;
+        if (rr < a.I) a.C[g * a.csg + (long)rr * a.csi + (long)col * a.csj] = act_fwd_t<EP>(acc[k] + bias_v);
+    }
+}
+
+int launch_fwd(const GemmArgs &a, int groups_grid, hipStream_t s) {
+    dim3 grid((a.J + 15) / 16, (a.I + 15) / 16, groups_grid);
+    const long span_a = (long)groups_grid * a.A.sg + (long)a.I * a.A.si + (long)a.R;
+    const long span_b = (long)groups_grid * a.B.sg + (long)a.J * a.B.si + (long)a.R;
+    if (span_a >= (1L << 29) || span_b >= (1L << 29) || a.A.sr != 1 || a.B.sr != 1) return EXO_ERANGE;
+    const int steps = a.R >> 4;
+#define FWD_LAUNCH(EPv)                                                                                   \
+    do {                                                                                                \
+        if (steps <= 5) hipLaunchKernelGGL((dense_fwd_kernel<EPv, 5>), grid, dim3(64), 0, s, a);         \
+        else if (steps <= 10) hipLaunchKernelGGL((dense_fwd_kernel<EPv, 10>), grid, dim3(64), 0, s, a);  \
+        else hipLaunchKernelGGL((dense_fwd_kernel<EPv, 20>), grid, dim3(64), 0, s, a);                   \
+    } while (0)
+    switch (a.act) {
+    case ACT_RELU: FWD_LAUNCH(ACT_RELU); break;
+    case ACT_ELU: FWD_LAUNCH(ACT_ELU); break;
+    case ACT_TANH: FWD_LAUNCH(ACT_TANH); break;
+    default: FWD_LAUNCH(ACT_NONE); break;
+    }
+#undef FWD_LAUNCH
+    return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
+}
+
 Operand plain(const float *p, long sg, long si, long sr) {
     Operand o{};
     o.p = p;
@@ -322,7 +405,7 @@ int td7_dense_fwd(const float *x, long xsg, long ldx, const float *w, const floa
     a.bsg = n;
     a.act = act;
     a.j_bias = -1;
-    return launch(a, groups, (hipStream_t)stream);
+    return launch_fwd(a, groups, (hipStream_t)stream);
 }
 
 /* dX = sum over the reduced groups of (dY[g] * act'(Y[g])) W[g].

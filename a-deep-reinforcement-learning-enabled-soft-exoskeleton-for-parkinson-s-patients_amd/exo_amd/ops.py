@@ -75,14 +75,17 @@ class _DenseFn(torch.autograd.Function):
     [G,N,K], b [G,N] with x [G,M,K] (one input per group) or x [M,K] (shared by
     the groups) -> y [G,M,N].
 
-    Forward: hipBLASLt GEMM with its bias epilogue + the activation (faster
-    than td7_dense_fwd at these shapes, profiles/r01_dense_bench.txt) unless
-    fwd_kernel; backward: the td7_dense kernels -- act'(Y) folded into the
+    Forward: td7_dense_fwd (one launch: GEMM + bias + activation) for up to
+    fwd_kernel_max_rows rows, hipBLASLt + the activation above; backward: the
+    td7_dense kernels -- act'(Y) folded into the
     operand loads, the bias gradient as the GEMM against a ones column: two
     launches where autograd issues the activation backward, two GEMMs, a
     column reduction and a fill."""
 
-    fwd_kernel = os.environ.get("EXO_DENSE_FWD") == "1"
+    # td7_dense_fwd (fused bias + activation) up to this many rows, hipBLASLt + the
+    # activation above it (profiles/r01_dense_bench.txt: 6.7 vs 9.8 us at
+    # 1,024x300x300, 22 vs 18 us at 4,096 rows); EXO_DENSE_FWD=0/1 forces a side
+    fwd_kernel_max_rows = {"0": 0, "1": 1 << 30}.get(os.environ.get("EXO_DENSE_FWD", ""), 2048)
 
     @staticmethod
     def forward(ctx, x, w, b, act):
@@ -95,7 +98,7 @@ class _DenseFn(torch.autograd.Function):
         xsg = 0 if (shared or not grouped) else x.stride(0)
         w = w.contiguous()
         bb = b.contiguous() if b is not None else None
-        if _DenseFn.fwd_kernel:
+        if M <= _DenseFn.fwd_kernel_max_rows:
             y = torch.empty((G, M, N) if grouped else (M, N), dtype=torch.float32, device=x.device)
             nat.check(nat.lib().td7_dense_fwd(nat.ptr(x), xsg, ldx, nat.ptr(w), nat.ptr(bb), nat.ptr(y),
                                               M * N, N, G, M, N, K, act, nat.stream_ptr(x.device)), "td7_dense_fwd")

@@ -22,10 +22,10 @@ def _ref(x, w, b, act):
 @pytest.fixture(params=["torch_fwd", "kernel_fwd"])
 def fwd_mode(request):
     from exo_amd import ops
-    old = ops._DenseFn.fwd_kernel
-    ops._DenseFn.fwd_kernel = request.param == "kernel_fwd"
+    old = ops._DenseFn.fwd_kernel_max_rows
+    ops._DenseFn.fwd_kernel_max_rows = (1 << 30) if request.param == "kernel_fwd" else 0
     yield request.param
-    ops._DenseFn.fwd_kernel = old
+    ops._DenseFn.fwd_kernel_max_rows = old
 
 
 def _check(x, w, b, act, tol=2e-5):
