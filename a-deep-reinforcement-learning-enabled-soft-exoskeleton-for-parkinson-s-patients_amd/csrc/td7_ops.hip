@@ -11,6 +11,8 @@
 //             else gx_rk = gy_rk / eps            (torch.clamp passes no gradient)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "exo_amd.h"
 
 namespace {
@@ -69,8 +71,19 @@ __global__ __launch_bounds__(256) void avgl1_bwd_kernel(const float *__restrict_
 // The step count lives on the device: every workgroup reads it, the last one
 // to finish (ticket counter) stores step + 1 and rearms the ticket, so one
 // launch is the whole optimiser step (HIP-graph safe, no host value).
-constexpr int ADAM_THREADS = 256, ADAM_PER_THREAD = 4;
+constexpr int ADAM_THREADS = 256, ADAM_BLOCKS = 512;
 
+__device__ __forceinline__ void adam_one(float &p, float g, float &m, float &v, float step_size, float bc2s,
+                                         float b1, float b2, float eps, float wd, float gscale) {
+    g *= gscale;
+    if (wd != 0.0f) g += wd * p;
+    m += (1.0f - b1) * (g - m); // lerp_(grad, 1 - beta1)
+    v = v * b2 + (1.0f - b2) * g * g;
+    p -= step_size * (m / (sqrtf(v) / bc2s + eps));
+}
+
+// grid-stride over float4 groups (a fixed 512-workgroup grid: few ticket
+// atomics), scalar tail for n % 4
 __global__ __launch_bounds__(ADAM_THREADS) void adam_kernel(float *__restrict__ p, const float *__restrict__ g,
                                                            float *__restrict__ m, float *__restrict__ v,
                                                            float *step, uint32_t *ticket, long n, float lr, float b1,
@@ -83,34 +96,38 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_kernel(float *__restrict__ 
     }
     __syncthreads();
     const float step_size = coef[0], bc2s = coef[1];
-    const long base = (long)blockIdx.x * ADAM_THREADS * ADAM_PER_THREAD + threadIdx.x;
-#pragma unroll
-    for (int k = 0; k < ADAM_PER_THREAD; ++k) {
-        const long i = base + (long)k * ADAM_THREADS; // coalesced: consecutive lanes, consecutive elements
-        if (i >= n) break;
-        const float pi = p[i];
-        float gi = g[i] * gscale;
-        if (wd != 0.0f) gi += wd * pi;
-        float mi = m[i];
-        mi += (1.0f - b1) * (gi - mi); // lerp_(grad, 1 - beta1)
-        const float vi = v[i] * b2 + (1.0f - b2) * gi * gi;
-        m[i] = mi;
-        v[i] = vi;
-        p[i] = pi - step_size * (mi / (sqrtf(vi) / bc2s + eps));
+    const long n4 = n >> 2, stride = (long)gridDim.x * ADAM_THREADS;
+    const bool vec = ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) |
+                       reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v)) & 15) == 0;
+    const long start = (long)blockIdx.x * ADAM_THREADS + threadIdx.x;
+    if (vec) {
+        float4 *p4 = reinterpret_cast<float4 *>(p), *m4 = reinterpret_cast<float4 *>(m), *v4 = reinterpret_cast<float4 *>(v);
+        const float4 *g4 = reinterpret_cast<const float4 *>(g);
+        for (long i = start; i < n4; i += stride) {
+            float4 pp = p4[i], mm = m4[i], vv = v4[i];
+            const float4 gg = g4[i];
+            adam_one(pp.x, gg.x, mm.x, vv.x, step_size, bc2s, b1, b2, eps, wd, gscale);
+            adam_one(pp.y, gg.y, mm.y, vv.y, step_size, bc2s, b1, b2, eps, wd, gscale);
+            adam_one(pp.z, gg.z, mm.z, vv.z, step_size, bc2s, b1, b2, eps, wd, gscale);
+            adam_one(pp.w, gg.w, mm.w, vv.w, step_size, bc2s, b1, b2, eps, wd, gscale);
+            p4[i] = pp;
+            m4[i] = mm;
+            v4[i] = vv;
+        }
     }
-    // last workgroup out advances the device step count
+    for (long i = (vec ? 4 * n4 : 0) + start; i < n; i += stride)
+        adam_one(p[i], g[i], m[i], v[i], step_size, bc2s, b1, b2, eps, wd, gscale);
+    // the last workgroup out advances the device step count (every workgroup
+    // has read it: its read precedes its ticket in program order)
     __syncthreads();
     if (threadIdx.x == 0) {
-        __threadfence();
         const uint32_t done = atomicAdd(ticket, 1u);
         if (done == gridDim.x - 1) {
             *step = *step + 1.0f;
             *ticket = 0u;
-            __threadfence();
         }
     }
 }
-
 } // namespace
 
 extern "C" {
@@ -139,8 +156,7 @@ int td7_avgl1norm_bwd(const float *x, const float *mean_in, const float *gy, flo
 int td7_adam_step(float *p, const float *g, float *m, float *v, float *step, uint32_t *ticket, int64_t n, float lr,
                   float beta1, float beta2, float eps, float weight_decay, float grad_scale, void *stream) {
     if (!p || !g || !m || !v || !step || !ticket || n <= 0) return EXO_EINVAL;
-    const long per_block = (long)ADAM_THREADS * ADAM_PER_THREAD;
-    const long blocks = (n + per_block - 1) / per_block;
+    const long blocks = std::min<long>(ADAM_BLOCKS, (n / 4 + ADAM_THREADS - 1) / ADAM_THREADS + 1);
     hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(ADAM_THREADS), 0, (hipStream_t)stream, p, g, m, v,
                        step, ticket, (long)n, lr, beta1, beta2, eps, weight_decay, grad_scale);
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
