@@ -10,6 +10,8 @@
 // critic_loss which also leaves dloss/dQ per element for the backward.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "exo_amd.h"
 
 namespace {
@@ -78,6 +80,43 @@ __global__ __launch_bounds__(T) void critic_loss_kernel(const float *q, long qs_
     if (threadIdx.x == 0) *loss = acc * inv_b;
 }
 
+
+// Exploration / target-policy noise on an action batch (one workgroup):
+//   out = clamp(a + c(noise * sigma), -1, 1) * scale,  c = clamp(+-clip) if clip > 0
+//   sigma -= sigma_dec (after every element has used the old value)
+// select_action (TD7_multi_agent_Pink_noise.py:209-228 batched; clip 0) and the
+// critic target's smoothed next action (TD7_multi_agent.py:236-238).
+__global__ __launch_bounds__(T) void noisy_action_kernel(const float *a, const float *noise, float *sigma,
+                                                         float sigma_dec, float clip, float scale, float *out, int n) {
+    const float sg = *sigma;
+    for (int i = threadIdx.x; i < n; i += T) {
+        float e = noise[i] * sg;
+        if (clip > 0.f) e = fminf(fmaxf(e, -clip), clip);
+        out[i] = fminf(fmaxf(a[i] + e, -1.0f), 1.0f) * scale;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) *sigma = sg - sigma_dec;
+}
+
+// F.mse_loss(pred, target) forward (mean of squared differences over n) and
+// its backward d/dpred = 2 (pred - target) / n * g.
+__global__ __launch_bounds__(T) void mse_fwd_kernel(const float *x, const float *y, long n, float *loss) {
+    __shared__ float sh[T / 64];
+    float acc = 0.f;
+    for (long i = threadIdx.x; i < n; i += T) {
+        const float d = x[i] - y[i];
+        acc += d * d;
+    }
+    acc = block_reduce(acc, 0, sh);
+    if (threadIdx.x == 0) *loss = acc / (float)n;
+}
+
+__global__ __launch_bounds__(256) void mse_bwd_kernel(const float *x, const float *y, const float *g, long n,
+                                                      float *dx) {
+    const float c = 2.0f * *g / (float)n;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) dx[i] = c * (x[i] - y[i]);
+}
+
 } // namespace
 
 extern "C" {
@@ -97,6 +136,28 @@ int td7_critic_loss(const float *q, long qs_b, long qs_h, const float *q_target,
     if (!q || !q_target || !loss || !priority || !dq || batch <= 0) return EXO_EINVAL;
     hipLaunchKernelGGL(critic_loss_kernel, dim3(1), dim3(T), 0, (hipStream_t)stream, q, qs_b, qs_h, q_target, loss,
                        priority, dq, alpha, min_priority, batch);
+    return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
+}
+
+int td7_noisy_action(const float *a, const float *noise, float *sigma, float sigma_dec, float clip, float scale,
+                     float *out, int32_t n, void *stream) {
+    if (!a || !noise || !sigma || !out || n < 0) return EXO_EINVAL;
+    if (n == 0) return EXO_OK;
+    hipLaunchKernelGGL(noisy_action_kernel, dim3(1), dim3(T), 0, (hipStream_t)stream, a, noise, sigma, sigma_dec, clip,
+                       scale, out, n);
+    return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
+}
+
+int td7_mse_fwd(const float *x, const float *y, int64_t n, float *loss, void *stream) {
+    if (!x || !y || !loss || n <= 0) return EXO_EINVAL;
+    hipLaunchKernelGGL(mse_fwd_kernel, dim3(1), dim3(T), 0, (hipStream_t)stream, x, y, (long)n, loss);
+    return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
+}
+
+int td7_mse_bwd(const float *x, const float *y, const float *g, int64_t n, float *dx, void *stream) {
+    if (!x || !y || !g || !dx || n <= 0) return EXO_EINVAL;
+    const long blocks = std::min<long>(1024, (n + 255) / 256);
+    hipLaunchKernelGGL(mse_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, y, g, (long)n, dx);
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 

@@ -203,3 +203,49 @@ def critic_loss(q, q_target, alpha, min_priority):
         loss = torch.where(td < 1, 0.5 * td.pow(2), 1 * td).sum(1).mean()
         return loss, td.detach().max(1)[0].clamp(min=min_priority).pow(alpha)
     return _CriticLossFn.apply(q, q_target, alpha, min_priority)
+
+
+# ---------------------------------------------------------------- small fusions
+def noisy_action(a, noise, sigma, sigma_dec, clip=0.0, scale=1.0):
+    """clamp(a + c(noise * sigma), -1, 1) * scale with c = clamp(+-clip) when
+    clip > 0, then sigma -= sigma_dec in place (sigma: device scalar tensor).
+    One td7_noisy_action launch on a GPU; the reference expressions on a CPU."""
+    if not a.is_cuda:
+        e = noise * sigma
+        if clip > 0:
+            e = e.clamp(-clip, clip)
+        out = (a + e).clamp(-1, 1) * scale
+        sigma -= sigma_dec
+        return out
+    a = a.contiguous()
+    out = torch.empty_like(a)
+    nat.check(nat.lib().td7_noisy_action(nat.ptr(a), nat.ptr(noise.contiguous()), nat.ptr(sigma), float(sigma_dec),
+                                         float(clip), float(scale), nat.ptr(out), a.numel(),
+                                         nat.stream_ptr(a.device)), "td7_noisy_action")
+    return out
+
+
+class _MSEFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, y):
+        x, y = x.contiguous(), y.contiguous()
+        loss = torch.empty((), dtype=torch.float32, device=x.device)
+        nat.check(nat.lib().td7_mse_fwd(nat.ptr(x), nat.ptr(y), x.numel(), nat.ptr(loss), nat.stream_ptr(x.device)),
+                  "td7_mse_fwd")
+        ctx.save_for_backward(x, y)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        x, y = ctx.saved_tensors
+        dx = torch.empty_like(x)
+        nat.check(nat.lib().td7_mse_bwd(nat.ptr(x), nat.ptr(y), nat.ptr(g.contiguous()), x.numel(), nat.ptr(dx),
+                                        nat.stream_ptr(x.device)), "td7_mse_bwd")
+        return dx, None
+
+
+def mse_loss(x, y):
+    """F.mse_loss(x, y) for a target without gradient: one launch each way on a GPU."""
+    if x.is_cuda and x.dtype == torch.float32 and y.dtype == torch.float32:
+        return _MSEFn.apply(x, y.detach())
+    return torch.nn.functional.mse_loss(x, y)

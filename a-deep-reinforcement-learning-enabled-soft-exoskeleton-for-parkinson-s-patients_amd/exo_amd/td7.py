@@ -405,7 +405,7 @@ class TD7Learner:
             zs_all = self.encoder.zs(torch.cat([state, next_state], 0))
             zs, next_zs = zs_all[:B], zs_all[B:].detach()
             pred_zs = self.encoder.zsa(zs, action)
-        encoder_loss = F.mse_loss(pred_zs.float(), next_zs.float())
+        encoder_loss = ops.mse_loss(pred_zs.float(), next_zs.float())
         self.encoder_optimizer.zero_grad(set_to_none=self.grads_to_none)
         encoder_loss.backward()
         # ---- critic (:233-257)
@@ -414,9 +414,10 @@ class TD7Learner:
                 fixed_target_zs = self.fixed_encoder_target.zs(next_state)
                 if noise is None:
                     noise = torch.randn_like(action)
-                noise = (noise * self.target_policy_noise).clamp(-hp.noise_clip, hp.noise_clip)
-                self.target_policy_noise -= self.policy_noise_decrease
-                next_action = (self.actor_target(next_state, fixed_target_zs) + noise).clamp(-1, 1)
+                # (noise * sigma).clamp(+-noise_clip); sigma -= decrease; (a + noise).clamp(-1, 1)
+                next_action = ops.noisy_action(self.actor_target(next_state, fixed_target_zs).float(), noise,
+                                               self.target_policy_noise, self.policy_noise_decrease,
+                                               clip=hp.noise_clip)
                 fixed_target_zsa = self.fixed_encoder_target.zsa(fixed_target_zs, next_action)
                 Q_heads = self.critic_target(next_state, next_action, fixed_target_zsa, fixed_target_zs).float()
             # Q_target and the running bounds (:240-246; bounds kept per rank,
@@ -598,8 +599,9 @@ class Agent:
         """Device-resident batched actions for the vectorised loop (no host sync)."""
         a = self.learner.act(obs, use_checkpoint)
         if use_exploration:
-            a = a + torch.randn_like(a) * self.learner.exploration_noise_t
-            self.learner.exploration_noise_t -= self.learner.action_noise_decrease * a.shape[0]
+            L = self.learner
+            return ops.noisy_action(a, torch.randn_like(a), L.exploration_noise_t, L.action_noise_decrease * a.shape[0],
+                                    scale=self.max_action)
         return a.clamp(-1, 1) * self.max_action
 
     # ---------------------------------------------------------- training

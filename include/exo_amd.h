@@ -226,6 +226,17 @@ int td7_q_target(const float *qt_dev, long qs_b, long qs_h, const float *reward_
 int td7_critic_loss(const float *q_dev, long qs_b, long qs_h, const float *q_target_dev, float *loss_dev,
                     float *priority_dev, float *dq_dev, float alpha, float min_priority, int32_t batch, void *stream);
 
+/* out = clamp(a + c(noise * *sigma), -1, 1) * scale over n values, c = clamp to
+ * +-clip when clip > 0; then *sigma -= sigma_dec.  The exploration noise of
+ * select_action (TD7_multi_agent_Pink_noise.py:209-228, batched) and the
+ * target policy smoothing of the critic target (TD7_multi_agent.py:236-238). */
+int td7_noisy_action(const float *a_dev, const float *noise_dev, float *sigma_dev, float sigma_dec, float clip,
+                     float scale, float *out_dev, int32_t n, void *stream);
+/* F.mse_loss (encoder loss, TD7_multi_agent.py:226): *loss = mean (x - y)^2;
+ * backward dx = 2 (x - y) / n * (*g). */
+int td7_mse_fwd(const float *x_dev, const float *y_dev, int64_t n, float *loss_dev, void *stream);
+int td7_mse_bwd(const float *x_dev, const float *y_dev, const float *g_dev, int64_t n, float *dx_dev, void *stream);
+
 /* ------------------------------------------------------------------------
  * Fused dense layers of the TD7 nets on fp32 MFMA (csrc/td7_dense.hip).
  * Each replaces one nn.Linear + activation of Agent/TD7_multi_agent.py:61-140

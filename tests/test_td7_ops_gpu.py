@@ -61,3 +61,27 @@ def test_q_target_and_critic_loss_match_reference_expressions():
     loss.backward()
     loss_ref.backward()
     torch.testing.assert_close(q.grad, q_ref.grad, rtol=1e-6, atol=1e-8)
+
+
+def test_noisy_action_and_mse_match_torch():
+    from exo_amd import ops
+    torch.manual_seed(4)
+    a = torch.tanh(torch.randn(1024, 7, device="cuda") * 2)
+    noise = torch.randn(1024, 7, device="cuda")
+    for clip, scale in ((0.5, 1.0), (0.0, 2.0)):
+        sig = torch.tensor(0.3, device="cuda")
+        out = ops.noisy_action(a, noise, sig, 1e-3, clip=clip, scale=scale)
+        e = noise * 0.3
+        if clip > 0:
+            e = e.clamp(-clip, clip)
+        torch.testing.assert_close(out, (a + e).clamp(-1, 1) * scale, rtol=0, atol=1e-7)
+        assert abs(float(sig) - (0.3 - 1e-3)) < 1e-7
+    x = torch.randn(1024, 300, device="cuda", requires_grad=True)
+    y = torch.randn(1024, 300, device="cuda")
+    x2 = x.detach().clone().requires_grad_(True)
+    l1 = ops.mse_loss(x, y)
+    l2 = torch.nn.functional.mse_loss(x2, y)
+    torch.testing.assert_close(l1, l2, rtol=1e-5, atol=1e-7)
+    (3 * l1).backward()
+    (3 * l2).backward()
+    torch.testing.assert_close(x.grad, x2.grad, rtol=1e-6, atol=1e-9)
