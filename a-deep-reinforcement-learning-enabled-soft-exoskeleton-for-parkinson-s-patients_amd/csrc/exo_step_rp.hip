@@ -64,10 +64,21 @@ struct RowM {
 
 __device__ __forceinline__ double shfl_d(double x, int src) { return __shfl(x, src, 64); }
 
-__device__ __forceinline__ double group_sum(double x) { // butterfly over the 8-lane group: identical in all lanes
-    x += __shfl_xor(x, 1, 64);
-    x += __shfl_xor(x, 2, 64);
-    x += __shfl_xor(x, 4, 64);
+// DPP lane moves of a double (two dword moves, VALU only: no LDS round trip)
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double x) {
+    const long long v = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(v & 0xffffffffLL), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(v >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// sum over the 8-lane group, identical in all lanes: xor-1 and xor-2 inside
+// each quad (quad_perm), then the half-row mirror pairs the group's two quads
+__device__ __forceinline__ double group_sum(double x) {
+    x += dpp_d<0xB1>(x);  // quad_perm [1,0,3,2]
+    x += dpp_d<0x4E>(x);  // quad_perm [2,3,0,1]
+    x += dpp_d<0x141>(x); // row_half_mirror: lane i <-> 7 - i within each 8 lanes
     return x;
 }
 
