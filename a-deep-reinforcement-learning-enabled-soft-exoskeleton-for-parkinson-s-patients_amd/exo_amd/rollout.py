@@ -9,9 +9,10 @@ and done envs stay idle until the longest motion ends.
 Everything inside an iteration is device work with no host synchronisation,
 so it is captured once into HIP graphs and replayed:
   * world == 1: one graph per policy-update parity (actor updated or not);
-  * world  > 1: the gradient all-reduces (RCCL) run eagerly between graphs
-    on flat buckets the graphs pack and unpack (pre: rollout + encoder/critic
-    grads, mid: optimiser steps + priorities + actor grads, post: actor step).
+  * world  > 1: the collectives (RCCL) run eagerly between graphs: the
+    encoder/critic gradient bucket after `pre` (rollout + grads), a MAX of
+    max_priority after `mid` (optimiser steps + priorities + actor grads),
+    the actor bucket before `post` (actor step).
 Host-side bookkeeping left outside the graphs: the env reset at the end of a
 round, the target-network refresh every 250 steps (:284-293).
 """
@@ -103,6 +104,7 @@ class VecTrainer:
         self._pre()
         L.sync.allreduce_grads(L.grad_params())
         self._mid(update_actor)
+        self.agent.sync.max_(self.agent.replay_buffer._maxp)
         if update_actor:
             L.sync.allreduce_grads(L.grad_params(actor=True))
         self._post(update_actor)
@@ -155,6 +157,7 @@ class VecTrainer:
         g1.replay()
         S.allreduce_flat(flat_c)
         g2.replay()
+        S.max_(self.agent.replay_buffer._maxp)  # global max_priority after this step's updates
         if update_actor:
             S.allreduce_flat(flat_a)
         g3.replay()
@@ -178,6 +181,7 @@ class VecTrainer:
             self._replay(update_actor)
         if L.maybe_update_targets():
             ag.replay_buffer.reset_max_priority()
+            ag.sync.max_(ag.replay_buffer._maxp)
         n_active = int(self.active_counts[self.k])
         self.k += 1
         self.iters += 1

@@ -609,8 +609,10 @@ class Agent:
         state, action, next_state, reward, not_done = self.replay_buffer.sample()
         priority = self.learner.update(state, action, next_state, reward, not_done)
         self.replay_buffer.update_priority(priority)
+        self.sync.max_(self.replay_buffer._maxp)  # global max_priority (:116)
         if self.learner.maybe_update_targets():
             self.replay_buffer.reset_max_priority()
+            self.sync.max_(self.replay_buffer._maxp)  # :120 over every rank's leaves
 
     def maybe_train_and_checkpoint(self, ep_timesteps, ep_return):
         """:296-312 (the episode return is MIN-reduced over data-parallel ranks)."""

@@ -233,7 +233,8 @@ def main():
     if agent is not None and world > 1:
         # data-parallel replicas must hold bit-identical weights
         ck = torch.stack([torch.cat([p.detach().reshape(-1) for p in m.parameters()]).double().sum()
-                          for m in (agent.learner.actor, agent.learner.critic, agent.learner.encoder)])
+                          for m in (agent.learner.actor, agent.learner.critic, agent.learner.encoder)]
+                         + [agent.replay_buffer._maxp.double().reshape(())])  # and the global max_priority
         allck = [torch.zeros_like(ck) for _ in range(world)]
         dist.all_gather(allck, ck)
         dp_sync = all(torch.equal(allck[0], x) for x in allck)
