@@ -49,7 +49,7 @@ def graph_reductions_ok(device, rows=1024, cols=300, replays=3):
 
 
 class VecTrainer:
-    def __init__(self, env, agent, strata=None, use_graphs=True, warmup_eager=3):
+    def __init__(self, env, agent, strata=None, use_graphs=True, warmup_eager=3, exploration="gaussian"):
         self.env, self.agent = env, agent
         self.device = env.device
         self.n = env.n
@@ -70,13 +70,21 @@ class VecTrainer:
         self.graphs = {}
         self.dp = agent.sync.active  # tests set it to exercise the 3-graph layout at world 1
         self.last_actions = None
+        # exploration: "gaussian" (TD7_multi_agent.py select_action) or "pink"
+        # (TD7_multi_agent_Pink_noise.py: one coloured sequence per episode round)
+        if exploration not in ("gaussian", "pink"):
+            raise ValueError(f"exploration must be 'gaussian' or 'pink', not {exploration!r}")
+        self.exploration = exploration
+        self.k_dev = torch.zeros((1,), dtype=torch.int64, device=self.device)
+        if exploration == "pink":
+            agent.init_episode_noise_device(self.round_len)
         if use_graphs:
             graph_reductions_ok(self.device)
 
     # ----------------------------------------------------------- pieces
     def _rollout(self):
         ag = self.agent
-        act = ag.select_action_batch(self.obs)
+        act = ag.select_action_batch(self.obs, timestep=self.k_dev if self.exploration == "pink" else None)
         nobs, rew, done, info = self.env.step(act, active=self.active, out=self.out)
         ag.replay_buffer.add_batch(self.obs, act, nobs, rew, done, self.strata, self.active)
         self.obs.copy_(nobs)
@@ -170,7 +178,11 @@ class VecTrainer:
         if self.k == self.round_len:
             self.env.reset(obs_out=self.obs)
             self.k = 0
+            if self.exploration == "pink":
+                ag.init_episode_noise_device(self.round_len)
         self.active.copy_(self.active_table[self.k])
+        if self.exploration == "pink":
+            self.k_dev.fill_(self.k)
         L.training_steps += 1
         update_actor = L.training_steps % ag.hp.policy_freq == 0
         if not self.use_graphs or self.iters < self.warmup_eager:

@@ -583,6 +583,7 @@ class Agent:
                 if first_step or self.noise is None:
                     self.init_episode_noise()
                 a = a + self.noise[:, timestep]
+                self.learner.exploration_noise_t -= self.learner.action_noise_decrease  # once per call (:225)
             else:
                 a = a + np.random.randn(*a.shape).astype(np.float32) * self.learner.exploration_noise
                 self.learner.exploration_noise_t -= self.learner.action_noise_decrease * a.shape[0]
@@ -595,9 +596,32 @@ class Agent:
         self.noise = buf / np.max(np.abs(buf)) * self.learner.exploration_noise
 
     @torch.no_grad()
-    def select_action_batch(self, obs, use_checkpoint=False, use_exploration=True):
-        """Device-resident batched actions for the vectorised loop (no host sync)."""
+    def init_episode_noise_device(self, n_steps=None, generator=None):
+        """Device Pink-noise sequence for a new episode round (the batched
+        TD7_multi_agent_Pink_noise.py:203-207 on the GPU): [action_dim, L],
+        peak-normalised and scaled by the current exploration noise; written
+        into a persistent buffer so captured graphs keep reading it."""
+        from .pink import powerlaw_psd_gaussian_device
+        L = int(n_steps or self.ep_length)
+        buf = powerlaw_psd_gaussian_device(self.hp.beta, self.action_dim, L, self.device, generator) * self.hp.noise_scale
+        buf = buf / buf.abs().max() * self.learner.exploration_noise_t
+        if getattr(self, "noise_dev", None) is None or self.noise_dev.shape != buf.shape:
+            self.noise_dev = torch.empty_like(buf)
+        self.noise_dev.copy_(buf)
+        return self.noise_dev
+
+    @torch.no_grad()
+    def select_action_batch(self, obs, use_checkpoint=False, use_exploration=True, timestep=None):
+        """Device-resident batched actions for the vectorised loop (no host sync).
+        timestep (int64 device tensor [1]): Pink-noise exploration -- column
+        `timestep` of the episode's noise (init_episode_noise_device) is added
+        to every env's action, as the reference's batched Pink select_action
+        does (:218-226); otherwise Gaussian noise per env (TD7_multi_agent.py:205-206)."""
         a = self.learner.act(obs, use_checkpoint)
+        if use_exploration and timestep is not None:
+            col = self.noise_dev.index_select(1, timestep).t()           # [1, action_dim]
+            self.learner.exploration_noise_t -= self.learner.action_noise_decrease * a.shape[0]
+            return (a + col).clamp(-1, 1) * self.max_action
         if use_exploration:
             L = self.learner
             return ops.noisy_action(a, torch.randn_like(a), L.exploration_noise_t, L.action_noise_decrease * a.shape[0],

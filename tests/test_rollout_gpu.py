@@ -61,3 +61,19 @@ def test_graph_replay_matches_eager_numerics(layout):
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
     import graph_vs_eager
     assert graph_vs_eager.run(layout, iters=10) <= 1e-5
+
+
+def test_pink_exploration_trainer_runs_in_graphs():
+    from exo_amd import VecExoskeletonEnv
+    from exo_amd.rollout import VecTrainer
+    from exo_amd.td7 import Agent, Hyperparameters
+    torch.manual_seed(0)
+    hp = Hyperparameters(zs_dim=32, enc_hdim=32, critic_hdim=32, actor_hdim=32, batch_size=16)
+    env = VecExoskeletonEnv(64, seed=2)
+    agent = Agent(80, 7, 1, hp=hp, env_num=8, buffer_size=4096, graph_safe=True)
+    tr = VecTrainer(env, agent, exploration="pink")
+    for _ in range(8):
+        tr.step()
+    torch.cuda.synchronize()
+    assert len(tr.graphs) == 2 and int(tr.k_dev) == 7
+    assert torch.isfinite(tr.last_actions).all() and float(tr.last_actions.abs().max()) <= 1.0

@@ -183,3 +183,29 @@ def test_flat_adam_matches_torch_adam():
     assert float(opt2._step) == 5.0
     # the reference's torch Adam loads a FlatAdam state_dict
     opt_ref.load_state_dict(sd)
+
+
+@pytest.mark.gpu
+def test_device_pink_noise_matches_numpy_and_statistics():
+    """powerlaw_psd_gaussian_device: the deterministic half (masking,
+    normalisation, irfft) equals the numpy path on the same spectra; the
+    generated sequences have unit variance; the batched Pink select_action
+    adds column t of the episode noise to every env."""
+    from exo_amd.pink import irfft_reference, powerlaw_psd_gaussian_device
+    from exo_amd.td7 import Agent, Hyperparameters
+    rng = np.random.default_rng(0)
+    for n in (341, 344):
+        sr, si = rng.normal(size=(7, n // 2 + 1)), rng.normal(size=(7, n // 2 + 1))
+        dev = powerlaw_psd_gaussian_device(1.0, 7, n, "cuda", spectrum=(sr, si)).cpu().numpy()
+        np.testing.assert_allclose(dev, irfft_reference(sr, si, 1.0, n), rtol=1e-5, atol=1e-6)
+    big = powerlaw_psd_gaussian_device(1.0, 4096, 344, "cuda").cpu().numpy()
+    assert abs(big.mean()) < 0.05 and abs(big.std() - 1.0) < 0.05
+    hp = Hyperparameters(zs_dim=32, enc_hdim=32, critic_hdim=32, actor_hdim=32, batch_size=16)
+    ag = Agent(80, 7, 1, hp=hp, env_num=8, buffer_size=1024, ep_length=50)
+    noise = ag.init_episode_noise_device(50).clone()
+    assert float(noise.abs().max()) == pytest.approx(float(ag.learner.exploration_noise_t), rel=1e-6)
+    obs = torch.randn(64, 80, device="cuda")
+    t = torch.tensor([7], device="cuda")
+    a = ag.select_action_batch(obs, timestep=t)
+    ref = (ag.learner.act(obs) + noise[:, 7][None, :]).clamp(-1, 1)
+    torch.testing.assert_close(a, ref, rtol=0, atol=1e-6)
