@@ -444,6 +444,105 @@ __global__ __launch_bounds__(256) void exo_step_kernel(Dev S, Urdf U, const floa
 // ===========================================================================
 // C ABI
 // ===========================================================================
+
+// ---------------------------------------------------------------- metrics
+// Tremor-suppression statistics of the training script
+// (Simulation/Exoskeleton_agent_train.py:149-200) for every env the last step
+// advanced, from its info row, on the device.  Per env: the per-axis torque
+// and amplitude reductions (percent, nan_to_num), the end-effector amplitude
+// change from Denavit-Hartenberg FK of the IMU angles with the suppressed and
+// the unsuppressed tremor amplitudes added (Utilities/
+// calculate_arm_end_effector_points.py:18-50), and the script's counters.
+__device__ void dh_end_effector(const double th[7], double L1, double L2, double out[3]) {
+    // A_i(alpha, a = 0, d, theta): alpha = (pi/2, pi/2, -pi/2, pi/2, pi/2, pi/2, pi/2), d = (0, 0, L1, 0, L2, 0, 0)
+    const double alpha[7] = {PI / 2, PI / 2, -PI / 2, PI / 2, PI / 2, PI / 2, PI / 2};
+    const double d[7] = {0, 0, L1, 0, L2, 0, 0};
+    double T[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0}; // rows 0..2 of the running 4x4 product
+    for (int k = 0; k < 7; ++k) {
+        const double ct = cos(th[k]), st = sin(th[k]), ca = cos(alpha[k]), sa = sin(alpha[k]);
+        const double A[12] = {ct, -st * ca, st * sa, 0.0, st, ct * ca, -ct * sa, 0.0, 0.0, sa, ca, d[k]};
+        double R[12];
+        for (int i = 0; i < 3; ++i) {
+            for (int j = 0; j < 4; ++j) {
+                double v = T[i * 4 + 0] * A[0 * 4 + j] + T[i * 4 + 1] * A[1 * 4 + j] + T[i * 4 + 2] * A[2 * 4 + j];
+                if (j == 3) v += T[i * 4 + 3];
+                R[i * 4 + j] = v;
+            }
+        }
+        for (int i = 0; i < 12; ++i) T[i] = R[i];
+    }
+    out[0] = T[3];
+    out[1] = T[7];
+    out[2] = T[11];
+}
+
+__device__ __forceinline__ double pct_change(double v, double ref) { // nan_to_num((|v|-|ref|)/|ref|*100, 0, 0, 0)
+    const double x = (fabs(v) - fabs(ref)) / fabs(ref) * 100.0;
+    return isfinite(x) ? x : 0.0;
+}
+
+__global__ void tremor_metrics_kernel(Dev S, const float *__restrict__ info, const uint8_t *__restrict__ stepped,
+                                      double L1, double L2, int disregard, float *__restrict__ metrics,
+                                      float *__restrict__ counters) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= S.N || (stepped && !stepped[e])) return;
+    const float *in = info + (size_t)e * INFO;
+    double tr[7], ta[7];
+    for (int j = 0; j < 7; ++j) {
+        tr[j] = pct_change(in[7 + j], in[21 + j]);   // torque_val vs tremor_torque_val
+        ta[j] = pct_change(in[14 + j], in[28 + j]);  // ampl_val vs tremor_ampl_val
+    }
+    // return_original_joint_angles at the post-step count: x, y, z, elbow y, elbow z, 0, 0 (degrees)
+    const int cnt = S.counts[e];
+    const double *imu = S.imu + (size_t)S.motion[e] * 5 * S.Lmax;
+    const int col[5] = {2, 3, 4, 0, 1};
+    double q0[7], q1[7], q2[7];
+    for (int j = 0; j < 7; ++j) {
+        const double o = j < 5 ? imu[col[j] * S.Lmax + cnt] * (PI / 180) : 0.0;
+        q0[j] = o;
+        q1[j] = (double)in[14 + j] * (PI / 180) + o;
+        q2[j] = (double)in[28 + j] * (PI / 180) + o;
+    }
+    double p0[3], p1[3], p2[3];
+    dh_end_effector(q0, L1, L2, p0);
+    dh_end_effector(q1, L1, L2, p1);
+    dh_end_effector(q2, L1, L2, p2);
+    const double ds = sqrt((p1[0] - p0[0]) * (p1[0] - p0[0]) + (p1[1] - p0[1]) * (p1[1] - p0[1]) +
+                           (p1[2] - p0[2]) * (p1[2] - p0[2]));
+    const double du = sqrt((p2[0] - p0[0]) * (p2[0] - p0[0]) + (p2[1] - p0[1]) * (p2[1] - p0[1]) +
+                           (p2[2] - p0[2]) * (p2[2] - p0[2]));
+    double total = (ds - du) / du * 100.0;
+    // counters (before the disregard clamp, :172-184)
+    float *cn = counters + (size_t)e * 6;
+    int nonneg = 0, neg = 0;
+    for (int j = 0; j < 4; ++j) (tr[j] >= 0 ? nonneg : neg) += 1;
+    cn[0] += nonneg;
+    cn[1] += neg;
+    if (neg > 0) cn[2] += 1;
+    if (total < 0) {
+        cn[4] += 1;
+        cn[5] = (float)total;
+    } else {
+        cn[3] += 1;
+    }
+    if (disregard) { // :186-191
+        for (int j = 0; j < 7; ++j) {
+            if (tr[j] > 0) tr[j] = 0;
+            if (ta[j] > 0) ta[j] = 0;
+        }
+        if (total > 0) total = 0;
+    }
+    float *m = metrics + (size_t)e * 16;
+    bool nz = false;
+    for (int j = 0; j < 7; ++j) {
+        m[j] = (float)tr[j];
+        m[7 + j] = (float)ta[j];
+        nz |= tr[j] != 0.0;
+    }
+    m[14] = (float)total;
+    m[15] = nz ? 1.f : 0.f;
+}
+
 struct exo_ctx {
     int device = 0;
     int N = 0, n_motions = 0, Lmax = 0;
@@ -760,6 +859,17 @@ int exo_set_seed(exo_ctx *c, uint64_t seed) {
     if (!c) return EXO_EINVAL;
     c->seed = seed;
     return EXO_OK;
+}
+
+int exo_tremor_metrics(exo_ctx *c, const float *info_dev, const uint8_t *stepped_dev, double humerus_length,
+                       double forearm_length, double hand_length, int32_t disregard, float *metrics_dev,
+                       float *counters_dev, void *stream) {
+    (void)hand_length; // the reference's DH table ends at the wrist (a = d = 0 for joints 6, 7)
+    if (!c || !info_dev || !metrics_dev || !counters_dev) return EXO_EINVAL;
+    DeviceGuard g(c->device);
+    hipLaunchKernelGGL(tremor_metrics_kernel, dim3((c->N + 255) / 256), dim3(256), 0, (hipStream_t)stream, c->S,
+                       info_dev, stepped_dev, humerus_length, forearm_length, disregard, metrics_dev, counters_dev);
+    return check(c, hipGetLastError(), "exo_tremor_metrics");
 }
 
 const char *exo_last_error(const exo_ctx *c) { return c ? c->err.c_str() : "null context"; }

@@ -64,6 +64,8 @@ EXPORTS = {
     "exo_set_step_variant": (c_int32, [c_void_p, c_int32]),
     "exo_last_error": (ctypes.c_char_p, [c_void_p]),
     "exo_destroy": (None, [c_void_p]),
+    "exo_tremor_metrics": (c_int32, [c_void_p, c_void_p, c_void_p, c_double, c_double, c_double, c_int32, c_void_p,
+                                     c_void_p, c_void_p]),
     "lap_tree_floats": (c_int32, [c_int32, c_int32]),
     "lap_init": (c_int32, [c_void_p, c_void_p]),
     "lap_add": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p]),

@@ -150,6 +150,32 @@ class VecExoskeletonEnv:
         if tuple(t.shape) != shape or t.dtype != dtype or not t.is_contiguous():
             raise ValueError(f"output buffer must be contiguous {dtype} {shape}")
 
+    METRIC_SLICES = {"tremor_reduction": slice(0, 7), "tremor_reduction_ampl": slice(7, 14),
+                     "tremor_reduction_ampl_total": 14, "any_reduction": 15}
+    COUNTER_NAMES = ("tremor_when_reduction_nonneg", "tremor_when_reduction_neg", "tremor_reduction_in_episode",
+                     "tremor_when_ampl_reduction_nonneg", "tremor_when_ampl_reduction_neg",
+                     "tremor_ampl_total_reduction_ep")
+
+    def tremor_metrics(self, info, stepped=None, counters=None, humerus_length=0.4, forearm_length=0.4,
+                       hand_length=0.05, disregard=True, out=None):
+        """The training script's per-step tremor-suppression statistics
+        (Simulation/Exoskeleton_agent_train.py:149-200) for the envs the last
+        step advanced, on the device.  info: that step's [N, 40] output;
+        stepped: bool/uint8 [N] (the `active` mask passed to step(), before the
+        step's done flags); counters [N, 6] float32 accumulate (COUNTER_NAMES).
+        Returns (metrics [N, 16] per METRIC_SLICES, counters)."""
+        if counters is None:
+            counters = torch.zeros((self.n, 6), dtype=torch.float32, device=self.device)
+        m = out if out is not None else torch.zeros((self.n, 16), dtype=torch.float32, device=self.device)
+        st = None
+        if stepped is not None:
+            st = (stepped.view(torch.uint8) if stepped.dtype == torch.bool else stepped.to(torch.uint8)).contiguous()
+        nat.check(nat.lib().exo_tremor_metrics(self._ctx, nat.ptr(info.contiguous()), nat.ptr(st),
+                                               float(humerus_length), float(forearm_length), float(hand_length),
+                                               int(bool(disregard)), nat.ptr(m), nat.ptr(counters), self._stream()),
+                  "exo_tremor_metrics", self._ctx)
+        return m, counters
+
     STEP_VARIANTS = {"auto": 0, "lanes": 1, "rows": 2}
 
     def set_step_variant(self, name):

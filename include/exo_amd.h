@@ -125,6 +125,22 @@ int exo_set_seed(exo_ctx *ctx, uint64_t seed);
 const char *exo_last_error(const exo_ctx *ctx);
 void exo_destroy(exo_ctx *ctx);
 
+/* Tremor-suppression statistics of Simulation/Exoskeleton_agent_train.py:149-200
+ * for every env the last exo_step advanced (stepped_dev[i] != 0; NULL = all),
+ * read from that step's info rows (info_dev [N][40]):
+ *   metrics_dev [N][16] (written): torque reduction per axis (7, percent,
+ *     nan_to_num), amplitude reduction per axis (7), end-effector amplitude
+ *     change (1; DH FK of Utilities/calculate_arm_end_effector_points.py:18-50
+ *     on the IMU angles with the suppressed / unsuppressed tremor amplitudes),
+ *     any-nonzero flag (1); with disregard != 0 positive values are zeroed
+ *     (:186-191);
+ *   counters_dev [N][6] (accumulated): tremor_when_reduction[0..1],
+ *     tremor_reduction_in_episode, tremor_when_ampl_reduction[0..1],
+ *     tremor_ampl_total_reduction_ep (last negative value). */
+int exo_tremor_metrics(exo_ctx *c, const float *info_dev, const uint8_t *stepped_dev, double humerus_length,
+                       double forearm_length, double hand_length, int32_t disregard, float *metrics_dev,
+                       float *counters_dev, void *stream);
+
 /* ------------------------------------------------------------------------
  * LAP prioritised replay (Agent/TD7_buffer_multi_agent.py:5-120), one
  * sum tree per stratum (the reference keeps one priority row per env,
