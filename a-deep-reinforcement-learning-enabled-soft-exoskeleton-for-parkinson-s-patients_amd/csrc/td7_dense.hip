@@ -19,6 +19,8 @@
 // inside the kernel.  fp32 in, fp32 accumulate: exact f32 fma chains.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "exo_amd.h"
 
 namespace {
@@ -120,11 +122,25 @@ __device__ __forceinline__ void load_step(__amdgpu_buffer_rsrc_t rp, int base_g,
     }
 }
 
+// Workgroups are dealt round-robin to the 8 XCDs (each with its own L2): the
+// linear workgroup id is remapped so that XCD k works a contiguous run of
+// (row-major) tiles -- one L2 sees 1/8 of the X rows and all of W instead of
+// all of both.  Returns the tile's (x, y, z).
+__device__ __forceinline__ int3 xcd_tile() {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int T = gx * gy * gridDim.z;
+    const int id = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int q8 = T >> 3, r8 = T & 7, x = id & 7, loc = id >> 3;
+    const int t = x < r8 ? x * (q8 + 1) + loc : r8 * (q8 + 1) + (x - r8) * q8 + loc;
+    return make_int3(t % gx, (t / gx) % gy, t / (gx * gy));
+}
+
 template <int AG, int EP, bool AV, bool BV, int NW>
 __global__ __launch_bounds__(64 * NW) void dense_gemm_kernel(GemmArgs a) {
     __shared__ __attribute__((aligned(16))) float red[NW > 1 ? NW - 1 : 1][32][33];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, q = lane >> 4, c = lane & 15;
-    const int i0 = blockIdx.y * 32, j0 = blockIdx.x * 32, g = blockIdx.z;
+    const int3 tile = xcd_tile();
+    const int i0 = tile.y * 32, j0 = tile.x * 32, g = tile.z;
     const __amdgpu_buffer_rsrc_t ra = rsrc(a.A.p), rb = rsrc(a.B.p);
     const __amdgpu_buffer_rsrc_t ry = rsrc(AG >= 0 ? a.A.y : a.A.p);
     const int nsteps_g = (a.R + 15) >> 4;            // 16-wide steps per reduction group
@@ -289,10 +305,13 @@ int launch(const GemmArgs &a, int groups_grid, hipStream_t s) {
 // reduction loaded up front in groups of GS 16-wide steps (one 16-byte load
 // of X and one of W per lane per step) so a wave makes one or two L2 round
 // trips instead of one per step; the tail (K % 16) is a range-checked step.
+// (2x2 waves per workgroup sharing X / W rows through L1 measured slower than
+// one wave per workgroup with this remap.)
 template <int EP, int GS>
 __global__ __launch_bounds__(64) void dense_fwd_kernel(GemmArgs a) {
     const int lane = threadIdx.x, q = lane >> 4, c = lane & 15;
-    const int i0 = blockIdx.y * 16, j0 = blockIdx.x * 16, g = blockIdx.z;
+    const int3 tile = xcd_tile();
+    const int i0 = tile.y * 16, j0 = tile.x * 16, g = tile.z;
     const int row = i0 + c, col = j0 + c;
     const __amdgpu_buffer_rsrc_t ra = rsrc(a.A.p), rb = rsrc(a.B.p);
     const int abase = g * (int)a.A.sg + row * (int)a.A.si, bbase = g * (int)a.B.sg + col * (int)a.B.si;
@@ -300,8 +319,9 @@ __global__ __launch_bounds__(64) void dense_fwd_kernel(GemmArgs a) {
     const float bias_v = (a.bias && bcol) ? a.bias[g * a.bsg + col] : 0.f;
     const int nfull = a.R >> 4;
     floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-    for (int s0 = 0; s0 < nfull; s0 += GS) {
-        uint32_t av[GS][4], bv[GS][4];
+    // groups of GS 16-wide steps, two register buffers: group k+1's loads are
+    // in flight while group k's MFMAs run
+    auto load = [&](int s0, uint32_t (&av)[GS][4], uint32_t (&bv)[GS][4]) {
 #pragma unroll
         for (int s = 0; s < GS; ++s) {
             const int r = 16 * (s0 + s) + 4 * q;
@@ -314,12 +334,30 @@ __global__ __launch_bounds__(64) void dense_fwd_kernel(GemmArgs a) {
                 bv[s][jj] = y[jj];
             }
         }
+    };
+    auto mma = [&](const uint32_t (&av)[GS][4], const uint32_t (&bv)[GS][4]) {
 #pragma unroll
         for (int s = 0; s < GS; ++s) {
             acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(av[s][0]), __uint_as_float(bv[s][0]), acc0, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(av[s][1]), __uint_as_float(bv[s][1]), acc1, 0, 0, 0);
             acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(av[s][2]), __uint_as_float(bv[s][2]), acc0, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(av[s][3]), __uint_as_float(bv[s][3]), acc1, 0, 0, 0);
+        }
+    };
+    if constexpr (GS >= 20) { // the launcher picks GS = 20 only for R < 336: one group
+        uint32_t a0[GS][4], b0[GS][4];
+        load(0, a0, b0);
+        __builtin_amdgcn_sched_barrier(0); // all loads in flight before the first MFMA
+        mma(a0, b0);
+    } else {
+        uint32_t a0[GS][4], b0[GS][4], a1[GS][4], b1[GS][4];
+        if (nfull > 0) load(0, a0, b0);
+        for (int s0 = 0; s0 < nfull; s0 += 2 * GS) {
+            if (s0 + GS < nfull) load(s0 + GS, a1, b1);
+            mma(a0, b0);
+            if (s0 + GS >= nfull) break;
+            if (s0 + 2 * GS < nfull) load(s0 + 2 * GS, a0, b0);
+            mma(a1, b1);
         }
     }
     if (a.R & 15) { // tail step
@@ -345,6 +383,202 @@ __global__ __launch_bounds__(64) void dense_fwd_kernel(GemmArgs a) {
     }
 }
 
+// ---- bwd-weight on the output-contiguous layout ------------------------------
+// dW[g][i][j] = sum_m dP[m][i] X[m][j], dP = dY * act'(Y), db[g][i] = sum_m dP[m][i].
+// Both operands are contiguous along the OUTPUT dimensions (i resp. j) and
+// strided along the reduction m, so the k-permutation of the forward kernel
+// is applied to the output dimensions instead: in a 4-row step (rows m0..m0+3)
+// lane (c, q) loads VA consecutive i of row m0+q (one b32/b64/b128) and 4
+// consecutive j of that row (one b128).  MFMA (s, t) of the step multiplies A
+// row r <-> i = i0 + VA*r + s with B column c <-> j = j0 + 4c + t: VA*4 MFMAs
+// per 2-3 vector loads, a (16 VA) x 64 tile per workgroup.  The NW waves of a
+// workgroup take the steps round-robin and are summed through LDS.
+//
+// Lanes past the edge load the last VA (4) in-range elements of the row and
+// shift them into place; what they deliver for rows i >= I / columns j >= J
+// only reaches accumulator elements that are never stored.  Rows m >= M load 0.
+struct WgradArgs {
+    const float *dy, *y, *x;
+    int dysg, lddy, ysg, ldy, xsg, ldx;
+    float *dw, *db;
+    int I, J, M;
+};
+
+template <int VA>
+__device__ __forceinline__ void ld_vec(__amdgpu_buffer_rsrc_t r, int byte_off, float (&v)[VA]) {
+    if (VA == 4) {
+        const auto x = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = __uint_as_float(x[e]);
+    } else if (VA == 2) {
+        const auto x = __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, 0);
+        v[0] = __uint_as_float(x[0]);
+        v[VA - 1] = __uint_as_float(x[1]);
+    } else {
+        v[0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
+    }
+}
+
+// out[e] = v[min(e + sh, VA - 1)]  (sh > 0 only on the edge lanes)
+// (written as a select on sh with constant indices: a compare against e + sh
+// lets the compiler fold the chain into a dynamic index -> scratch)
+template <int VA>
+__device__ __forceinline__ float shifted(const float (&v)[VA], int sh, int e) {
+    float o = v[VA - 1];
+#pragma unroll
+    for (int d = VA - 2; d >= 0; --d) o = (sh == d) ? v[e + d < VA ? e + d : VA - 1] : o;
+    return o;
+}
+
+template <int AG, int VA, int NW>
+__global__ __launch_bounds__(64 * NW) void dense_wgrad_kernel(WgradArgs a) {
+    constexpr int KS = VA == 1 ? 8 : 4; // 4-row steps per prefetch group (two groups in flight)
+    constexpr int NACC = VA * 4;
+    __shared__ float red[NW > 1 ? NW / 2 : 1][NACC * 4 + VA][64];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, q = lane >> 4, c = lane & 15;
+    const int3 tile = xcd_tile();
+    const int i0 = tile.y * 16 * VA, j0 = tile.x * 64, g = tile.z;
+    const int ia = i0 + VA * c, ib = min(ia, a.I - VA), shi = ia - ib;
+    const int ja = j0 + 4 * c, jb = min(ja, a.J - 4), shj = ja - jb;
+    const __amdgpu_buffer_rsrc_t rdy = rsrc(a.dy), ry = rsrc(AG > 0 ? a.y : a.dy), rx = rsrc(a.x);
+    const int dyb = g * a.dysg + ib, yb = g * a.ysg + ib, xb = g * a.xsg + jb;
+    const int nks = (a.M + 3) >> 2;
+    const int my = nks > w ? (nks - w + NW - 1) / NW : 0;
+    const int ngrp = (my + KS - 1) / KS;
+
+    struct Buf {
+        float a[KS][VA], y[KS][VA], b[KS][4];
+    };
+    floatx4 acc[VA][4];
+    float bsum[VA];
+#pragma unroll
+    for (int s = 0; s < VA; ++s) {
+        bsum[s] = 0.f;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[s][u] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    auto load = [&](int grp, Buf &f) {
+#pragma unroll
+        for (int sp = 0; sp < KS; ++sp) {
+            const int k = grp * KS + sp;
+            const int m = 4 * (w + k * NW) + q;
+            const bool live = (k < my) & (m < a.M);
+            ld_vec<VA>(rdy, live ? (dyb + m * a.lddy) * 4 : BUF_OOB, f.a[sp]);
+            if (AG > 0) ld_vec<VA>(ry, live ? (yb + m * a.ldy) * 4 : BUF_OOB, f.y[sp]);
+            ld_vec<4>(rx, live ? (xb + m * a.ldx) * 4 : BUF_OOB, f.b[sp]);
+        }
+    };
+    auto mma = [&](const Buf &f) {
+#pragma unroll
+        for (int sp = 0; sp < KS; ++sp) {
+            float fa[VA], fb[4];
+#pragma unroll
+            for (int s = 0; s < VA; ++s) {
+                fa[s] = shifted<VA>(f.a[sp], shi, s);
+                if (AG > 0) fa[s] *= act_grad_t<AG>(shifted<VA>(f.y[sp], shi, s));
+                bsum[s] += fa[s];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) fb[u] = shifted<4>(f.b[sp], shj, u);
+#pragma unroll
+            for (int s = 0; s < VA; ++s)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) acc[s][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[s], fb[u], acc[s][u], 0, 0, 0);
+        }
+    };
+    Buf b0, b1;
+    if (ngrp > 0) load(0, b0);
+    for (int grp = 0; grp < ngrp; grp += 2) {
+        if (grp + 1 < ngrp) load(grp + 1, b1);
+        mma(b0);
+        if (grp + 1 >= ngrp) break;
+        if (grp + 2 < ngrp) load(grp + 2, b0);
+        mma(b1);
+    }
+    // tree-sum the NW partial tiles through LDS (lane-major: conflict free)
+#pragma unroll
+    for (int half = NW / 2; half >= 1; half >>= 1) {
+        if (w >= half && w < 2 * half) {
+#pragma unroll
+            for (int s = 0; s < VA; ++s) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) red[w - half][(s * 4 + u) * 4 + k][lane] = acc[s][u][k];
+                red[w - half][NACC * 4 + s][lane] = bsum[s];
+            }
+        }
+        __syncthreads();
+        if (w < half) {
+#pragma unroll
+            for (int s = 0; s < VA; ++s) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) acc[s][u][k] += red[w][(s * 4 + u) * 4 + k][lane];
+                bsum[s] += red[w][NACC * 4 + s][lane];
+            }
+        }
+        __syncthreads();
+    }
+    if (w > 0) return;
+    // acc[s][u][k] is dW[i0 + VA*(4q + k) + s][j0 + 4c + u]
+    float *dwg = a.dw + (long)g * a.I * a.J;
+#pragma unroll
+    for (int s = 0; s < VA; ++s)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = i0 + VA * (4 * q + k) + s;
+            if (i >= a.I) continue;
+            float *row = dwg + (long)i * a.J;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (ja + u < a.J) row[ja + u] = acc[s][u][k];
+        }
+    if (a.db && tile.x == 0) {
+#pragma unroll
+        for (int s = 0; s < VA; ++s) {
+            float v = bsum[s];
+            v += __shfl_xor(v, 16);
+            v += __shfl_xor(v, 32);
+            if (q == 0 && ia + s < a.I) a.db[(long)g * a.I + ia + s] = v;
+        }
+    }
+}
+
+int launch_wgrad(const WgradArgs &a, int groups, int act, hipStream_t s) {
+    const int jt = (a.J + 63) / 64;
+    auto tiles = [&](int va) { return (long)jt * ((a.I + 16 * va - 1) / (16 * va)) * groups; };
+    // the widest i-vector that still yields ~1k waves at NW = 8
+    int va = 4;
+    while (va > 1 && (tiles(va) * 8 < 768 || a.I < va)) va >>= 1;
+    const long nks = (a.M + 3) / 4;
+    int nw = 2;
+    while (nw < 8 && nks >= 8L * nw * 2 && tiles(va) * nw * 2 <= 2048) nw *= 2;
+    dim3 grid(jt, (a.I + 16 * va - 1) / (16 * va), groups);
+#define WG_NW(AGv, VAv)                                                                              \
+    do {                                                                                           \
+        if (nw == 8) hipLaunchKernelGGL((dense_wgrad_kernel<AGv, VAv, 8>), grid, dim3(512), 0, s, a); \
+        else if (nw == 4) hipLaunchKernelGGL((dense_wgrad_kernel<AGv, VAv, 4>), grid, dim3(256), 0, s, a); \
+        else hipLaunchKernelGGL((dense_wgrad_kernel<AGv, VAv, 2>), grid, dim3(128), 0, s, a);       \
+    } while (0)
+#define WG_VA(AGv)                      \
+    do {                              \
+        if (va == 4) WG_NW(AGv, 4);   \
+        else if (va == 2) WG_NW(AGv, 2); \
+        else WG_NW(AGv, 1);           \
+    } while (0)
+    switch (act) {
+    case ACT_RELU: WG_VA(ACT_RELU); break;
+    case ACT_ELU: WG_VA(ACT_ELU); break;
+    case ACT_TANH: WG_VA(ACT_TANH); break;
+    default: WG_VA(ACT_NONE); break;
+    }
+#undef WG_VA
+#undef WG_NW
+    return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
+}
+
 int launch_fwd(const GemmArgs &a, int groups_grid, hipStream_t s) {
     dim3 grid((a.J + 15) / 16, (a.I + 15) / 16, groups_grid);
     const long span_a = (long)groups_grid * a.A.sg + (long)a.I * a.A.si + (long)a.R;
@@ -355,7 +589,8 @@ int launch_fwd(const GemmArgs &a, int groups_grid, hipStream_t s) {
     do {                                                                                                \
         if (steps <= 5) hipLaunchKernelGGL((dense_fwd_kernel<EPv, 5>), grid, dim3(64), 0, s, a);         \
         else if (steps <= 10) hipLaunchKernelGGL((dense_fwd_kernel<EPv, 10>), grid, dim3(64), 0, s, a);  \
-        else hipLaunchKernelGGL((dense_fwd_kernel<EPv, 20>), grid, dim3(64), 0, s, a);                   \
+        else if (steps <= 20) hipLaunchKernelGGL((dense_fwd_kernel<EPv, 20>), grid, dim3(64), 0, s, a);  \
+        else hipLaunchKernelGGL((dense_fwd_kernel<EPv, 10>), grid, dim3(64), 0, s, a);                   \
     } while (0)
     switch (a.act) {
     case ACT_RELU: FWD_LAUNCH(ACT_RELU); break;
@@ -466,6 +701,15 @@ int td7_dense_bwd_weight(const float *dy, long dysg, long lddy, const float *yv,
     a.bgsg = n;
     a.j_bias = db ? k : -1;
     if (m == 0) return EXO_EINVAL;
+    if (n >= 4 && k >= 4 && std::getenv("EXO_WGRAD_V3") == nullptr) {
+        // output-contiguous wgrad kernel: 32-bit element offsets
+        const long span = (long)groups * (dysg > ysg ? (dysg > xsg ? dysg : xsg) : (ysg > xsg ? ysg : xsg)) +
+                          (long)m * (lddy > ldy ? (lddy > ldx ? lddy : ldx) : (ldy > ldx ? ldy : ldx)) + n + k;
+        if (span < (1L << 29)) {
+            WgradArgs w{dy, yv, x, (int)dysg, (int)lddy, (int)ysg, (int)ldy, (int)xsg, (int)ldx, dw, db, n, k, m};
+            return launch_wgrad(w, groups, act, (hipStream_t)stream);
+        }
+    }
     return launch(a, groups, (hipStream_t)stream);
 }
 

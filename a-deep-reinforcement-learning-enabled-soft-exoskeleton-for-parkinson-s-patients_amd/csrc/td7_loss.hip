@@ -100,15 +100,46 @@ __global__ __launch_bounds__(T) void noisy_action_kernel(const float *a, const f
 
 // F.mse_loss(pred, target) forward (mean of squared differences over n) and
 // its backward d/dpred = 2 (pred - target) / n * g.
-__global__ __launch_bounds__(T) void mse_fwd_kernel(const float *x, const float *y, long n, float *loss) {
-    __shared__ float sh[T / 64];
+constexpr int MSE_BLOCKS = 256; // == TD7_MSE_WS - 1
+__global__ __launch_bounds__(256) void mse_fwd_kernel(const float *x, const float *y, long n, float *loss, float *ws) {
+    __shared__ float sh[256 / 64];
+    __shared__ bool last;
     float acc = 0.f;
-    for (long i = threadIdx.x; i < n; i += T) {
-        const float d = x[i] - y[i];
-        acc += d * d;
+    const long stride = (long)gridDim.x * 256;
+    if ((n & 3) == 0 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0) {
+        const float4 *x4 = reinterpret_cast<const float4 *>(x), *y4 = reinterpret_cast<const float4 *>(y);
+        for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n / 4; i += stride) {
+            const float4 a = x4[i], b = y4[i];
+            const float d0 = a.x - b.x, d1 = a.y - b.y, d2 = a.z - b.z, d3 = a.w - b.w;
+            acc += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+        }
+    } else {
+        for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+            const float d = x[i] - y[i];
+            acc += d * d;
+        }
     }
-    acc = block_reduce(acc, 0, sh);
-    if (threadIdx.x == 0) *loss = acc / (float)n;
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    // block partials -> ws[b]; the last block to finish sums them in block
+    // order (deterministic) and re-arms the ticket (ws[MSE_BLOCKS]) to zero
+    unsigned *ticket = reinterpret_cast<unsigned *>(ws + MSE_BLOCKS);
+    if (threadIdx.x == 0) {
+        ws[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
+        __threadfence();
+        last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last || threadIdx.x >= 64) return;
+    __threadfence();
+    float v = 0.f;
+    for (unsigned b = threadIdx.x; b < gridDim.x; b += 64) v += __builtin_nontemporal_load(ws + b);
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (threadIdx.x == 0) {
+        *loss = v / (float)n;
+        *ticket = 0u;
+    }
 }
 
 __global__ __launch_bounds__(256) void mse_bwd_kernel(const float *x, const float *y, const float *g, long n,
@@ -148,9 +179,11 @@ int td7_noisy_action(const float *a, const float *noise, float *sigma, float sig
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 
-int td7_mse_fwd(const float *x, const float *y, int64_t n, float *loss, void *stream) {
-    if (!x || !y || !loss || n <= 0) return EXO_EINVAL;
-    hipLaunchKernelGGL(mse_fwd_kernel, dim3(1), dim3(T), 0, (hipStream_t)stream, x, y, (long)n, loss);
+int td7_mse_fwd(const float *x, const float *y, int64_t n, float *loss, float *ws, void *stream) {
+    if (!x || !y || !loss || !ws || n <= 0) return EXO_EINVAL;
+    const long blocks = std::min<long>(MSE_BLOCKS, (n / 4 + 255) / 256 + 1);
+    hipLaunchKernelGGL(mse_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, y, (long)n, loss,
+                       ws);
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 

@@ -86,7 +86,7 @@ EXPORTS = {
                                   ctypes.c_float, c_int32, c_void_p]),
     "td7_noisy_action": (c_int32, [c_void_p, c_void_p, c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                    c_void_p, c_int32, c_void_p]),
-    "td7_mse_fwd": (c_int32, [c_void_p, c_void_p, ctypes.c_int64, c_void_p, c_void_p]),
+    "td7_mse_fwd": (c_int32, [c_void_p, c_void_p, ctypes.c_int64, c_void_p, c_void_p, c_void_p]),
     "td7_mse_bwd": (c_int32, [c_void_p, c_void_p, c_void_p, ctypes.c_int64, c_void_p, c_void_p]),
     "td7_avgl1norm_fwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, ctypes.c_float, c_void_p]),
     "td7_avgl1norm_bwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, ctypes.c_float,

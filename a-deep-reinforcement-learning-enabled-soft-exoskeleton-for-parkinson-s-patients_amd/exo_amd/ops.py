@@ -225,12 +225,29 @@ def noisy_action(a, noise, sigma, sigma_dec, clip=0.0, scale=1.0):
     return out
 
 
+TD7_MSE_WS = 257  # include/exo_amd.h
+_mse_ws = {}
+
+
+def _mse_workspace(device):
+    """Zeroed block-partials + ticket buffer of td7_mse_fwd, one per device (the
+    encoder loss never runs on two streams at once)."""
+    key = torch.device(device)
+    ws = _mse_ws.get(key)
+    if ws is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("mse_loss: run once eagerly on this stream before graph capture")
+        ws = _mse_ws[key] = torch.zeros(TD7_MSE_WS, dtype=torch.float32, device=device)
+    return ws
+
+
 class _MSEFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, y):
         x, y = x.contiguous(), y.contiguous()
         loss = torch.empty((), dtype=torch.float32, device=x.device)
-        nat.check(nat.lib().td7_mse_fwd(nat.ptr(x), nat.ptr(y), x.numel(), nat.ptr(loss), nat.stream_ptr(x.device)),
+        nat.check(nat.lib().td7_mse_fwd(nat.ptr(x), nat.ptr(y), x.numel(), nat.ptr(loss),
+                                        nat.ptr(_mse_workspace(x.device)), nat.stream_ptr(x.device)),
                   "td7_mse_fwd")
         ctx.save_for_backward(x, y)
         return loss

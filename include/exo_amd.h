@@ -249,8 +249,11 @@ int td7_critic_loss(const float *q_dev, long qs_b, long qs_h, const float *q_tar
 int td7_noisy_action(const float *a_dev, const float *noise_dev, float *sigma_dev, float sigma_dec, float clip,
                      float scale, float *out_dev, int32_t n, void *stream);
 /* F.mse_loss (encoder loss, TD7_multi_agent.py:226): *loss = mean (x - y)^2;
- * backward dx = 2 (x - y) / n * (*g). */
-int td7_mse_fwd(const float *x_dev, const float *y_dev, int64_t n, float *loss_dev, void *stream);
+ * backward dx = 2 (x - y) / n * (*g).  ws_dev: TD7_MSE_WS floats, zeroed once
+ * by the caller (block partials + a ticket the kernel leaves at zero); one
+ * workspace per stream. */
+#define TD7_MSE_WS 257
+int td7_mse_fwd(const float *x_dev, const float *y_dev, int64_t n, float *loss_dev, float *ws_dev, void *stream);
 int td7_mse_bwd(const float *x_dev, const float *y_dev, const float *g_dev, int64_t n, float *dx_dev, void *stream);
 
 /* ------------------------------------------------------------------------

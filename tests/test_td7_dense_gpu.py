@@ -45,7 +45,8 @@ def _check(x, w, b, act, tol=2e-5):
 
 
 @pytest.mark.parametrize("act", [0, 1, 2, 3])
-@pytest.mark.parametrize("m,n,k", [(1024, 300, 80), (1000, 300, 307), (1024, 7, 300), (37, 300, 87), (4096, 300, 300)])
+@pytest.mark.parametrize("m,n,k", [(1024, 300, 80), (1000, 300, 307), (1024, 7, 300), (37, 300, 87), (4096, 300, 300),
+                                   (3, 5, 4), (130, 6, 9), (1023, 65, 130)])
 def test_dense_plain(act, m, n, k, fwd_mode):
     torch.manual_seed(m + n + k + act)
     x = torch.randn(m, k, device="cuda")

@@ -70,6 +70,24 @@ def main():
                                                     m, n, k, 2, nat.stream_ptr(dev)))
         tf = timeit(lambda: torch.nn.functional.elu(torch.nn.functional.linear(x, w, b)))
         print(f"{m:5d} {n:4d} {k:4d} | {f:7.2f} {bd:7.2f} {bw:7.2f} | {tf:9.2f} | {2 * m * n * k / f / 1e3:8.0f}")
+    # the critic's two Q heads: groups = 2, separate inputs (TD7 critic q2/q3 layers)
+    for (m, n, k) in [(1024, 320, 920), (1024, 320, 320)]:
+        x = torch.randn(2, m, k, device="cuda")
+        w = torch.randn(2, n, k, device="cuda")
+        b = torch.randn(2, n, device="cuda")
+        y = torch.empty(2, m, n, device="cuda")
+        dy = torch.randn(2, m, n, device="cuda")
+        dx = torch.empty(2, m, k, device="cuda")
+        dw = torch.empty(2, n, k, device="cuda")
+        db = torch.empty(2, n, device="cuda")
+        P = nat.ptr
+        f = timeit(lambda: L.td7_dense_fwd(P(x), m * k, k, P(w), P(b), P(y), m * n, n, 2, m, n, k, 2, nat.stream_ptr(dev)))
+        bd = timeit(lambda: L.td7_dense_bwd_data(P(dy), m * n, n, P(y), m * n, n, P(w), P(dx), m * k, k, 2, 0,
+                                                  m, n, k, 2, nat.stream_ptr(dev)))
+        bw = timeit(lambda: L.td7_dense_bwd_weight(P(dy), m * n, n, P(y), m * n, n, P(x), m * k, k, P(dw), P(db), 2,
+                                                    m, n, k, 2, nat.stream_ptr(dev)))
+        tf = timeit(lambda: torch.nn.functional.elu(torch.baddbmm(b.unsqueeze(1), x, w.transpose(1, 2))))
+        print(f"2x{m:4d} {n:4d} {k:4d} | {f:7.2f} {bd:7.2f} {bw:7.2f} | {tf:9.2f} | {4 * m * n * k / f / 1e3:8.0f}")
 
 
 if __name__ == "__main__":

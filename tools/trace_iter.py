@@ -7,6 +7,8 @@ from collections import defaultdict
 
 
 def classify(n):
+    if "dense_" in n.split("(")[0] or "(anonymous namespace)::dense" in n:
+        return "td7_dense (HIP)"
     if "exo_step" in n:
         return "env step (HIP)"
     if n.startswith("lap_") or "lap_" in n.split("(")[0]:
