@@ -307,52 +307,96 @@ int launch(const GemmArgs &a, int groups_grid, hipStream_t s) {
 // trips instead of one per step; the tail (K % 16) is a range-checked step.
 // (2x2 waves per workgroup sharing X / W rows through L1 measured slower than
 // one wave per workgroup with this remap.)
-template <int EP, int GS>
-__global__ __launch_bounds__(64) void dense_fwd_kernel(GemmArgs a) {
-    const int lane = threadIdx.x, q = lane >> 4, c = lane & 15;
+template <int EP, int GS, int TM, int TN, int KW>
+__global__ __launch_bounds__(64 * KW) void dense_fwd_kernel(GemmArgs a) {
+    // a (16 TM) x (16 TN) tile per workgroup; per 16-wide step TM + TN b128
+    // loads feed 4 TM TN MFMAs.  KW waves split the reduction (halves, summed
+    // through LDS at the end).
+    constexpr bool SPLIT = TM * TN == 1; // 1x1: two accumulators break the MFMA dependency chain
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
     const int3 tile = xcd_tile();
-    const int i0 = tile.y * 16, j0 = tile.x * 16, g = tile.z;
-    const int row = i0 + c, col = j0 + c;
+    const int i0 = tile.y * 16 * TM, j0 = tile.x * 16 * TN, g = tile.z;
     const __amdgpu_buffer_rsrc_t ra = rsrc(a.A.p), rb = rsrc(a.B.p);
-    const int abase = g * (int)a.A.sg + row * (int)a.A.si, bbase = g * (int)a.B.sg + col * (int)a.B.si;
-    const bool arow = row < a.I, bcol = col < a.J;
-    const float bias_v = (a.bias && bcol) ? a.bias[g * a.bsg + col] : 0.f;
-    const int nfull = a.R >> 4;
-    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    int abase[TM], bbase[TN];
+    bool arow[TM], bcol[TN];
+#pragma unroll
+    for (int x = 0; x < TM; ++x) {
+        const int row = i0 + 16 * x + c;
+        abase[x] = g * (int)a.A.sg + row * (int)a.A.si;
+        arow[x] = row < a.I;
+    }
+    float bias_v[TN];
+#pragma unroll
+    for (int y = 0; y < TN; ++y) {
+        const int col = j0 + 16 * y + c;
+        bbase[y] = g * (int)a.B.sg + col * (int)a.B.si;
+        bcol[y] = col < a.J;
+        bias_v[y] = (a.bias && bcol[y]) ? a.bias[g * a.bsg + col] : 0.f;
+    }
+    const int nall = a.R >> 4, per = (nall + KW - 1) / KW;
+    const int sbeg = w * per, nfull = min(nall, sbeg + per); // this wave's steps [sbeg, nfull)
+    floatx4 acc[TM][TN][SPLIT ? 2 : 1];
+#pragma unroll
+    for (int x = 0; x < TM; ++x)
+#pragma unroll
+        for (int y = 0; y < TN; ++y)
+#pragma unroll
+            for (int h = 0; h < (SPLIT ? 2 : 1); ++h) acc[x][y][h] = floatx4{0.f, 0.f, 0.f, 0.f};
     // groups of GS 16-wide steps, two register buffers: group k+1's loads are
     // in flight while group k's MFMAs run
-    auto load = [&](int s0, uint32_t (&av)[GS][4], uint32_t (&bv)[GS][4]) {
+    auto load = [&](int s0, uint32_t (&av)[GS][TM][4], uint32_t (&bv)[GS][TN][4]) {
 #pragma unroll
         for (int s = 0; s < GS; ++s) {
             const int r = 16 * (s0 + s) + 4 * q;
             const bool live = s0 + s < nfull;
-            const auto x = __builtin_amdgcn_raw_buffer_load_b128(ra, (live & arow) ? (abase + r) * 4 : BUF_OOB, 0, 0);
-            const auto y = __builtin_amdgcn_raw_buffer_load_b128(rb, (live & bcol) ? (bbase + r) * 4 : BUF_OOB, 0, 0);
 #pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-                av[s][jj] = x[jj];
-                bv[s][jj] = y[jj];
+            for (int x = 0; x < TM; ++x) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(ra, (live & arow[x]) ? (abase[x] + r) * 4 : BUF_OOB, 0, 0);
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) av[s][x][jj] = v[jj];
+            }
+#pragma unroll
+            for (int y = 0; y < TN; ++y) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(rb, (live & bcol[y]) ? (bbase[y] + r) * 4 : BUF_OOB, 0, 0);
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) bv[s][y][jj] = v[jj];
             }
         }
     };
-    auto mma = [&](const uint32_t (&av)[GS][4], const uint32_t (&bv)[GS][4]) {
+    auto step = [&](const float (&xa)[TM][4], const float (&xb)[TN][4]) {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+            for (int x = 0; x < TM; ++x)
+#pragma unroll
+                for (int y = 0; y < TN; ++y) {
+                    floatx4 &d = acc[x][y][SPLIT ? (jj & 1) : 0];
+                    d = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[x][jj], xb[y][jj], d, 0, 0, 0);
+                }
+    };
+    auto mma = [&](const uint32_t (&av)[GS][TM][4], const uint32_t (&bv)[GS][TN][4]) {
 #pragma unroll
         for (int s = 0; s < GS; ++s) {
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(av[s][0]), __uint_as_float(bv[s][0]), acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(av[s][1]), __uint_as_float(bv[s][1]), acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(av[s][2]), __uint_as_float(bv[s][2]), acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(av[s][3]), __uint_as_float(bv[s][3]), acc1, 0, 0, 0);
+            float xa[TM][4], xb[TN][4];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+#pragma unroll
+                for (int x = 0; x < TM; ++x) xa[x][jj] = __uint_as_float(av[s][x][jj]);
+#pragma unroll
+                for (int y = 0; y < TN; ++y) xb[y][jj] = __uint_as_float(bv[s][y][jj]);
+            }
+            step(xa, xb);
         }
     };
     if constexpr (GS >= 20) { // the launcher picks GS = 20 only for R < 336: one group
-        uint32_t a0[GS][4], b0[GS][4];
-        load(0, a0, b0);
+        uint32_t a0[GS][TM][4], b0[GS][TN][4];
+        load(sbeg, a0, b0);
         __builtin_amdgcn_sched_barrier(0); // all loads in flight before the first MFMA
         mma(a0, b0);
     } else {
-        uint32_t a0[GS][4], b0[GS][4], a1[GS][4], b1[GS][4];
-        if (nfull > 0) load(0, a0, b0);
-        for (int s0 = 0; s0 < nfull; s0 += 2 * GS) {
+        uint32_t a0[GS][TM][4], b0[GS][TN][4], a1[GS][TM][4], b1[GS][TN][4];
+        if (nfull > sbeg) load(sbeg, a0, b0);
+        for (int s0 = sbeg; s0 < nfull; s0 += 2 * GS) {
             if (s0 + GS < nfull) load(s0 + GS, a1, b1);
             mma(a0, b0);
             if (s0 + GS >= nfull) break;
@@ -360,26 +404,56 @@ __global__ __launch_bounds__(64) void dense_fwd_kernel(GemmArgs a) {
             mma(a1, b1);
         }
     }
-    if (a.R & 15) { // tail step
-        const int r = 16 * nfull + 4 * q;
-        float xa[4], xb[4];
+    if ((a.R & 15) && w == KW - 1) { // tail step
+        const int r = 16 * nall + 4 * q;
+        float xa[TM][4], xb[TN][4];
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
-            xa[jj] = ldb(ra, arow & (r + jj < a.R), abase + r + jj);
-            xb[jj] = ldb(rb, bcol & (r + jj < a.R), bbase + r + jj);
-        }
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[0], xb[0], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[1], xb[1], acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[2], xb[2], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[3], xb[3], acc1, 0, 0, 0);
-    }
-    const floatx4 acc = acc0 + acc1;
-    if (!bcol) return;
-    // acc[k] is C[i0 + 4q + k][col]
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int rr = i0 + 4 * q + k;
-        if (rr < a.I) a.C[g * a.csg + (long)rr * a.csi + (long)col * a.csj] = act_fwd_t<EP>(acc[k] + bias_v);
+            for (int x = 0; x < TM; ++x) xa[x][jj] = ldb(ra, arow[x] & (r + jj < a.R), abase[x] + r + jj);
+#pragma unroll
+            for (int y = 0; y < TN; ++y) xb[y][jj] = ldb(rb, bcol[y] & (r + jj < a.R), bbase[y] + r + jj);
+        }
+        step(xa, xb);
+    }
+    if constexpr (SPLIT)
+#pragma unroll
+        for (int x = 0; x < TM; ++x)
+#pragma unroll
+            for (int y = 0; y < TN; ++y) {
+                acc[x][y][0] += acc[x][y][SPLIT ? 1 : 0];
+                acc[x][y][SPLIT ? 1 : 0] = floatx4{0.f, 0.f, 0.f, 0.f};
+            }
+    if constexpr (KW > 1) {
+        __shared__ floatx4 red[KW - 1][TM * TN][64];
+        if (w > 0)
+#pragma unroll
+            for (int x = 0; x < TM; ++x)
+#pragma unroll
+                for (int y = 0; y < TN; ++y) red[w - 1][x * TN + y][lane] = acc[x][y][0];
+        __syncthreads();
+        if (w > 0) return;
+#pragma unroll
+        for (int ww = 0; ww < KW - 1; ++ww)
+#pragma unroll
+            for (int x = 0; x < TM; ++x)
+#pragma unroll
+                for (int y = 0; y < TN; ++y) acc[x][y][0] += red[ww][x * TN + y][lane];
+    }
+    // acc[x][y][.][k] is C[i0 + 16x + 4q + k][j0 + 16y + c]
+#pragma unroll
+    for (int y = 0; y < TN; ++y) {
+        if (!bcol[y]) continue;
+        const int col = j0 + 16 * y + c;
+#pragma unroll
+        for (int x = 0; x < TM; ++x) {
+            const floatx4 v = SPLIT ? acc[x][y][0] + acc[x][y][SPLIT ? 1 : 0] : acc[x][y][0];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int rr = i0 + 16 * x + 4 * q + k;
+                if (rr < a.I) a.C[g * a.csg + (long)rr * a.csi + (long)col * a.csj] = act_fwd_t<EP>(v[k] + bias_v[y]);
+            }
+        }
     }
 }
 
@@ -580,17 +654,45 @@ int launch_wgrad(const WgradArgs &a, int groups, int act, hipStream_t s) {
 }
 
 int launch_fwd(const GemmArgs &a, int groups_grid, hipStream_t s) {
-    dim3 grid((a.J + 15) / 16, (a.I + 15) / 16, groups_grid);
     const long span_a = (long)groups_grid * a.A.sg + (long)a.I * a.A.si + (long)a.R;
     const long span_b = (long)groups_grid * a.B.sg + (long)a.J * a.B.si + (long)a.R;
     if (span_a >= (1L << 29) || span_b >= (1L << 29) || a.A.sr != 1 || a.B.sr != 1) return EXO_ERANGE;
     const int steps = a.R >> 4;
-#define FWD_LAUNCH(EPv)                                                                                   \
-    do {                                                                                                \
-        if (steps <= 5) hipLaunchKernelGGL((dense_fwd_kernel<EPv, 5>), grid, dim3(64), 0, s, a);         \
-        else if (steps <= 10) hipLaunchKernelGGL((dense_fwd_kernel<EPv, 10>), grid, dim3(64), 0, s, a);  \
-        else if (steps <= 20) hipLaunchKernelGGL((dense_fwd_kernel<EPv, 20>), grid, dim3(64), 0, s, a);  \
-        else hipLaunchKernelGGL((dense_fwd_kernel<EPv, 10>), grid, dim3(64), 0, s, a);                   \
+    static const int force = [] {
+        const char *e = std::getenv("EXO_FWD_TILE");
+        return e ? std::atoi(e) : 0;
+    }();
+    // 16x16 tiles (one wave each) while they number < ~2 per SIMD; beyond
+    // that 32x32 tiles (half the L2 traffic per MFMA).  (Splitting the
+    // reduction over 2 waves, EXO_FWD_TILE=xx2, measured slower at every TD7
+    // shape.)
+    const long t16 = (long)((a.I + 15) / 16) * ((a.J + 15) / 16) * groups_grid;
+    int tm = 1, tn = 1, kw = 1;
+    if (force) {
+        tm = force / 100;
+        tn = force / 10 % 10;
+        kw = force % 10;
+    } else if (t16 >= 2048) {
+        tm = tn = 2;
+    }
+    dim3 grid((a.J + 16 * tn - 1) / (16 * tn), (a.I + 16 * tm - 1) / (16 * tm), groups_grid);
+    const int wsteps = (steps + kw - 1) / kw;
+#define FWD_GS(EPv, TMv, TNv, KWv)                                                                              \
+    do {                                                                                                      \
+        const dim3 blk(64 * KWv);                                                                             \
+        if (wsteps <= 5) hipLaunchKernelGGL((dense_fwd_kernel<EPv, 5, TMv, TNv, KWv>), grid, blk, 0, s, a);    \
+        else if (TMv * TNv == 1 && wsteps <= 20)                                                              \
+            hipLaunchKernelGGL((dense_fwd_kernel<EPv, 20, TMv, TNv, KWv>), grid, blk, 0, s, a);               \
+        else if (TMv * TNv == 1)                                                                              \
+            hipLaunchKernelGGL((dense_fwd_kernel<EPv, 10, TMv, TNv, KWv>), grid, blk, 0, s, a);               \
+        else hipLaunchKernelGGL((dense_fwd_kernel<EPv, 5, TMv, TNv, KWv>), grid, blk, 0, s, a);                \
+    } while (0)
+#define FWD_LAUNCH(EPv)                                            \
+    do {                                                           \
+        if (tm == 2 && tn == 2 && kw == 2) FWD_GS(EPv, 2, 2, 2);   \
+        else if (tm == 2 && tn == 2) FWD_GS(EPv, 2, 2, 1);         \
+        else if (kw == 2) FWD_GS(EPv, 1, 1, 2);                    \
+        else FWD_GS(EPv, 1, 1, 1);                                 \
     } while (0)
     switch (a.act) {
     case ACT_RELU: FWD_LAUNCH(ACT_RELU); break;
@@ -599,6 +701,7 @@ int launch_fwd(const GemmArgs &a, int groups_grid, hipStream_t s) {
     default: FWD_LAUNCH(ACT_NONE); break;
     }
 #undef FWD_LAUNCH
+#undef FWD_GS
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 
