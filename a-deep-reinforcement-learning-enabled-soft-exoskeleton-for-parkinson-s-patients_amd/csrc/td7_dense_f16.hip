@@ -1,0 +1,8 @@
+// PREC_F16 instantiation of the TD7 dense-layer launchers (td7_dense_kernels.h).
+#include "td7_dense_kernels.h"
+
+namespace td7dense {
+template void launch_gemm_p<PREC_F16>(const GemmArgs &, dim3, int, hipStream_t);
+template void launch_wgrad_p<PREC_F16>(const WgradArgs &, dim3, int, int, int, hipStream_t);
+template void launch_fwd_p<PREC_F16>(const GemmArgs &, dim3, int, int, int, int, hipStream_t);
+} // namespace td7dense

@@ -1,0 +1,714 @@
+// td7_dense_kernels.h -- the TD7 dense-layer kernels and their per-precision
+// launchers (see td7_dense.hip for the design notes).  Each precision's
+// launchers are instantiated in their own translation unit
+// (td7_dense_{f32,bf16,f16}.hip) so the three compile in parallel.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdlib>
+
+#include "exo_amd.h"
+
+namespace td7dense {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef short shortx4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 halfx4 __attribute__((ext_vector_type(4)));
+
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_ELU = 2, ACT_TANH = 3 };
+
+// MFMA operand precision.  F32: v_mfma_f32_16x16x4_f32, four per 16-wide
+// reduction step (exact f32 fma chains).  BF16 / F16: the same fp32 operands
+// rounded to nearest even as they are loaded, one v_mfma_f32_16x16x16_{bf16,f16}
+// per step with the step's 4 values per lane as the instruction's 4 k-slots,
+// fp32 accumulate; memory, epilogues and bias gradients stay fp32.
+enum Prec : int { PREC_F32 = 0, PREC_BF16 = 1, PREC_F16 = 2 };
+
+template <int P>
+__device__ __forceinline__ floatx4 mfma_k16(const float (&a)[4], const float (&b)[4], floatx4 c) {
+    if constexpr (P == PREC_F16) {
+        const halfx4 ha = {(_Float16)a[0], (_Float16)a[1], (_Float16)a[2], (_Float16)a[3]};
+        const halfx4 hb = {(_Float16)b[0], (_Float16)b[1], (_Float16)b[2], (_Float16)b[3]};
+        return __builtin_amdgcn_mfma_f32_16x16x16f16(ha, hb, c, 0, 0, 0);
+    } else {
+        const bf16x4 ba = {(__bf16)a[0], (__bf16)a[1], (__bf16)a[2], (__bf16)a[3]};
+        const bf16x4 bb = {(__bf16)b[0], (__bf16)b[1], (__bf16)b[2], (__bf16)b[3]};
+        return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(shortx4, ba),
+                                                         __builtin_bit_cast(shortx4, bb), c, 0, 0, 0);
+    }
+}
+
+// derivative of the activation expressed through its output y
+template <int ACT>
+__device__ __forceinline__ float act_grad_t(float y) {
+    if (ACT == ACT_RELU) return y > 0.f ? 1.f : 0.f;
+    if (ACT == ACT_ELU) return y > 0.f ? 1.f : y + 1.f;
+    if (ACT == ACT_TANH) return 1.f - y * y;
+    return 1.f;
+}
+template <int ACT>
+__device__ __forceinline__ float act_fwd_t(float x) {
+    if (ACT == ACT_RELU) return x > 0.f ? x : 0.f;
+    if (ACT == ACT_ELU) return x > 0.f ? x : expm1f(x);
+    if (ACT == ACT_TANH) return tanhf(x);
+    return x;
+}
+
+// An operand element (i, r) of group g lives at p[g*sg + i*si + r*sr].  When
+// act >= 0 the operand is dY and is multiplied by act'(Y) read at the same
+// (g, i, r) from y (strides ysg/ysi/ysr).
+struct Operand {
+    const float *p;
+    long sg, si, sr;
+    const float *y;
+    long ysg, ysi, ysr;
+    int act; // -1: plain operand
+    int ones_col; // >= 0: index i == ones_col reads 1.0 (bias column of bwd-weight)
+};
+
+struct GemmArgs {
+    Operand A, B;
+    int I, J, R;      // C is I x J, reduction length R
+    int groups_red;   // > 1: also reduce over this many groups (bwd-data of a shared input)
+    // epilogue
+    float *C;
+    long csg, csi, csj;
+    const float *bias; // forward: + bias[g*bsg + j]
+    long bsg;
+    int act;           // forward activation
+    float *bias_grad;  // bwd-weight: column j == J_bias goes to bias_grad[g*bgsg + i]
+    long bgsg;
+    int j_bias;        // -1: none
+};
+
+// Workgroup tile 32x32 (2x2 v_mfma_f32_16x16x4_f32 tiles per wave, four
+// independent accumulators); the NW waves of a workgroup split the reduction
+// dimension in 16-wide steps (step s goes to wave s % NW) and their partial
+// tiles are summed through LDS at the end.  Operands are loaded straight
+// from global memory (L2) into registers -- no LDS staging, no barrier in
+// the loop: each wave streams its steps with the next step group's loads in
+// flight under the current group's MFMAs.  A lane (c, q) feeds MFMA jj of a
+// step with A(i, r0+4q+jj) and B(j, r0+4q+jj) (the same permutation of the
+// step's r on both operands).  Per 16-wide step a wave loads 2 A and 2 B
+// fragments for 16 MFMAs, half the L2 traffic per MFMA of one 16x16 tile
+// per wave, and NW x (I/32)(J/32) waves keep the whole chip busy on these
+// small GEMMs (M <= 4096, N, K <= 921).
+constexpr int BUF_BYTES = 0x7FFFFF00, BUF_OOB = 0x7FFFFF00; // offset past the records -> the load returns 0
+constexpr int SPG = 2;                                      // 16-wide steps per prefetch group
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float *p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(p), 0, BUF_BYTES, 0x00020000);
+}
+
+__device__ __forceinline__ float ldb(__amdgpu_buffer_rsrc_t r, bool ok, int off) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, ok ? off * 4 : BUF_OOB, 0, 0));
+}
+
+// one operand's fragments for SPG steps: [step][tile 0/1][jj]
+struct Frag {
+    float v[SPG][2][4];
+};
+
+// element (i, r) with i = i0 + 16*tile + c, r = r0 + 4q + jj.  VEC (contiguous
+// along r, the step fully inside R): one 16-byte load; else 4 checked dwords.
+template <bool VEC>
+__device__ __forceinline__ void load_step(__amdgpu_buffer_rsrc_t rp, int base_g, int si, int sr, int i0, int c, int I,
+                                          int r0, int R, int q, float (&f)[2][4], bool full) {
+#pragma unroll
+    for (int tl = 0; tl < 2; ++tl) {
+        const int i = i0 + 16 * tl + c;
+        const int r = r0 + 4 * q;
+        if (VEC && full) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rp, i < I ? (base_g + i * si + r) * 4 : BUF_OOB, 0, 0);
+            f[tl][0] = __uint_as_float(v[0]);
+            f[tl][1] = __uint_as_float(v[1]);
+            f[tl][2] = __uint_as_float(v[2]);
+            f[tl][3] = __uint_as_float(v[3]);
+        } else {
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) f[tl][jj] = ldb(rp, (i < I) & (r + jj < R), base_g + i * si + (r + jj) * sr);
+        }
+    }
+}
+
+// Workgroups are dealt round-robin to the 8 XCDs (each with its own L2): the
+// linear workgroup id is remapped so that XCD k works a contiguous run of
+// (row-major) tiles -- one L2 sees 1/8 of the X rows and all of W instead of
+// all of both.  Returns the tile's (x, y, z).
+__device__ __forceinline__ int3 xcd_tile() {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int T = gx * gy * gridDim.z;
+    const int id = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int q8 = T >> 3, r8 = T & 7, x = id & 7, loc = id >> 3;
+    const int t = x < r8 ? x * (q8 + 1) + loc : r8 * (q8 + 1) + (x - r8) * q8 + loc;
+    return make_int3(t % gx, (t / gx) % gy, t / (gx * gy));
+}
+
+template <int AG, int EP, bool AV, bool BV, int NW, int P>
+__global__ __launch_bounds__(64 * NW) void dense_gemm_kernel(GemmArgs a) {
+    __shared__ __attribute__((aligned(16))) float red[NW > 1 ? NW - 1 : 1][32][33];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, q = lane >> 4, c = lane & 15;
+    const int3 tile = xcd_tile();
+    const int i0 = tile.y * 32, j0 = tile.x * 32, g = tile.z;
+    const __amdgpu_buffer_rsrc_t ra = rsrc(a.A.p), rb = rsrc(a.B.p);
+    const __amdgpu_buffer_rsrc_t ry = rsrc(AG >= 0 ? a.A.y : a.A.p);
+    const int nsteps_g = (a.R + 15) >> 4;            // 16-wide steps per reduction group
+    const int nsteps = nsteps_g * a.groups_red;
+    const int full_steps = a.R >> 4;                  // steps entirely inside R
+    // this wave's steps: w, w + NW, ...; processed SPG at a time
+    const int my = nsteps > w ? (nsteps - w + NW - 1) / NW : 0;
+    const int ngrp = (my + SPG - 1) / SPG;
+
+    // epilogue bias fetched up front (its latency hides under the main loop)
+    float bias_pre[2];
+#pragma unroll
+    for (int y = 0; y < 2; ++y) {
+        const int col = j0 + 16 * y + c;
+        bias_pre[y] = (a.bias && col < a.J) ? a.bias[g * a.bsg + col] : 0.f;
+    }
+    floatx4 acc[2][2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) acc[x][y] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    auto load = [&](int grp, Frag &fa, Frag &fy, Frag &fb) {
+#pragma unroll
+        for (int sp = 0; sp < SPG; ++sp) {
+            const int k = grp * SPG + sp;           // k-th step of this wave
+            const int st = w + k * NW;              // global step index
+            const bool live = k < my;
+            const int gg = a.groups_red > 1 ? st / nsteps_g : g;
+            const int sl = live ? st % nsteps_g : 0;
+            const int r0 = live ? sl * 16 : a.R;    // a dead step loads zeros (r >= R)
+            const bool full = live && sl < full_steps;
+            load_step<AV>(ra, gg * (int)a.A.sg, (int)a.A.si, (int)a.A.sr, i0, c, a.I, r0, a.R, q, fa.v[sp], full);
+            if (AG >= 0)
+                load_step<AV>(ry, gg * (int)a.A.ysg, (int)a.A.ysi, (int)a.A.ysr, i0, c, a.I, r0, a.R, q, fy.v[sp], full);
+            load_step<BV>(rb, gg * (int)a.B.sg, (int)a.B.si, (int)a.B.sr, j0, c, a.J, r0, a.R, q, fb.v[sp], full);
+            if (a.B.ones_col >= 0) { // bwd-weight: column ones_col of B is all ones (-> bias gradient)
+#pragma unroll
+                for (int tl = 0; tl < 2; ++tl)
+                    if (j0 + 16 * tl + c == a.B.ones_col)
+#pragma unroll
+                        for (int jj = 0; jj < 4; ++jj) fb.v[sp][tl][jj] = (r0 + 4 * q + jj < a.R) ? 1.f : 0.f;
+            }
+        }
+    };
+    auto mma = [&](const Frag &fa, const Frag &fy, const Frag &fb) {
+        if constexpr (P != PREC_F32) {
+#pragma unroll
+            for (int sp = 0; sp < SPG; ++sp) {
+                float av[2][4];
+#pragma unroll
+                for (int tl = 0; tl < 2; ++tl)
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj)
+                        av[tl][jj] = AG >= 0 ? fa.v[sp][tl][jj] * act_grad_t<AG>(fy.v[sp][tl][jj]) : fa.v[sp][tl][jj];
+#pragma unroll
+                for (int x = 0; x < 2; ++x)
+#pragma unroll
+                    for (int y = 0; y < 2; ++y) acc[x][y] = mfma_k16<P>(av[x], fb.v[sp][y], acc[x][y]);
+            }
+            return;
+        }
+#pragma unroll
+        for (int sp = 0; sp < SPG; ++sp)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                float av[2];
+#pragma unroll
+                for (int tl = 0; tl < 2; ++tl)
+                    av[tl] = AG >= 0 ? fa.v[sp][tl][jj] * act_grad_t<AG>(fy.v[sp][tl][jj]) : fa.v[sp][tl][jj];
+#pragma unroll
+                for (int x = 0; x < 2; ++x)
+#pragma unroll
+                    for (int y = 0; y < 2; ++y)
+                        acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[x], fb.v[sp][y][jj], acc[x][y], 0, 0, 0);
+            }
+    };
+    Frag a0, y0, b0, a1, y1, b1;
+    if (ngrp > 0) load(0, a0, y0, b0);
+    for (int grp = 0; grp < ngrp; grp += 2) {
+        if (grp + 1 < ngrp) load(grp + 1, a1, y1, b1);
+        mma(a0, y0, b0);
+        if (grp + 1 >= ngrp) break;
+        if (grp + 2 < ngrp) load(grp + 2, a0, y0, b0);
+        mma(a1, y1, b1);
+    }
+    // sum the NW partial tiles: waves 1.. park theirs in LDS, wave 0 adds them
+    // acc[x][y][k] is C[i0 + 16x + 4q + k][j0 + 16y + c]
+    if (NW > 1) {
+        if (w > 0)
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+#pragma unroll
+                for (int y = 0; y < 2; ++y)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) red[w - 1][16 * x + 4 * q + k][16 * y + c] = acc[x][y][k];
+        __syncthreads();
+        if (w > 0) return;
+#pragma unroll
+        for (int ww = 0; ww < NW - 1; ++ww)
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+#pragma unroll
+                for (int y = 0; y < 2; ++y)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) acc[x][y][k] += red[ww][16 * x + 4 * q + k][16 * y + c];
+    }
+#pragma unroll
+    for (int y = 0; y < 2; ++y) {
+        const int col = j0 + 16 * y + c;
+        const bool is_bias = a.j_bias >= 0 && col == a.j_bias;
+        if (!is_bias && col >= a.J) continue;
+        const float bias_v = is_bias ? 0.f : bias_pre[y];
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int row = i0 + 16 * x + 4 * q + k;
+                if (row >= a.I) continue;
+                const float v = acc[x][y][k];
+                if (is_bias) a.bias_grad[g * a.bgsg + row] = v;
+                else a.C[g * a.csg + (long)row * a.csi + (long)col * a.csj] = act_fwd_t<EP>(v + bias_v);
+            }
+    }
+}
+
+template <int P>
+void launch_gemm_p(const GemmArgs &a, dim3 grid, int nw, hipStream_t s) {
+#define DENSE_LAUNCH(AGv, EPv, AVv, BVv)                                                                            \
+    do {                                                                                                          \
+        if (nw == 8) hipLaunchKernelGGL((dense_gemm_kernel<AGv, EPv, AVv, BVv, 8, P>), grid, dim3(512), 0, s, a);    \
+        else if (nw == 4) hipLaunchKernelGGL((dense_gemm_kernel<AGv, EPv, AVv, BVv, 4, P>), grid, dim3(256), 0, s, a); \
+        else hipLaunchKernelGGL((dense_gemm_kernel<AGv, EPv, AVv, BVv, 2, P>), grid, dim3(128), 0, s, a);           \
+    } while (0)
+    if (a.A.sr == 1) { // bwd-data: dY rows contiguous, W^T column walk
+        switch (a.A.act) {
+        case ACT_RELU: DENSE_LAUNCH(ACT_RELU, ACT_NONE, true, false); break;
+        case ACT_ELU: DENSE_LAUNCH(ACT_ELU, ACT_NONE, true, false); break;
+        case ACT_TANH: DENSE_LAUNCH(ACT_TANH, ACT_NONE, true, false); break;
+        default: DENSE_LAUNCH(ACT_NONE, ACT_NONE, true, false); break;
+        }
+    } else {           // bwd-weight (generic layout): both operands walk rows (contiguous along i)
+        switch (a.A.act) {
+        case ACT_RELU: DENSE_LAUNCH(ACT_RELU, ACT_NONE, false, false); break;
+        case ACT_ELU: DENSE_LAUNCH(ACT_ELU, ACT_NONE, false, false); break;
+        case ACT_TANH: DENSE_LAUNCH(ACT_TANH, ACT_NONE, false, false); break;
+        default: DENSE_LAUNCH(ACT_NONE, ACT_NONE, false, false); break;
+        }
+    }
+#undef DENSE_LAUNCH
+}
+
+// Forward Y = act(X W^T + b): one wavefront per 16x16 output tile, the whole
+// reduction loaded up front in groups of GS 16-wide steps (one 16-byte load
+// of X and one of W per lane per step) so a wave makes one or two L2 round
+// trips instead of one per step; the tail (K % 16) is a range-checked step.
+// (2x2 waves per workgroup sharing X / W rows through L1 measured slower than
+// one wave per workgroup with this remap.)
+template <int EP, int GS, int TM, int TN, int KW, int P>
+__global__ __launch_bounds__(64 * KW) void dense_fwd_kernel(GemmArgs a) {
+    // a (16 TM) x (16 TN) tile per workgroup; per 16-wide step TM + TN b128
+    // loads feed 4 TM TN MFMAs.  KW waves split the reduction (halves, summed
+    // through LDS at the end).
+    constexpr bool SPLIT = TM * TN == 1; // 1x1: two accumulators break the MFMA dependency chain
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
+    const int3 tile = xcd_tile();
+    const int i0 = tile.y * 16 * TM, j0 = tile.x * 16 * TN, g = tile.z;
+    const __amdgpu_buffer_rsrc_t ra = rsrc(a.A.p), rb = rsrc(a.B.p);
+    int abase[TM], bbase[TN];
+    bool arow[TM], bcol[TN];
+#pragma unroll
+    for (int x = 0; x < TM; ++x) {
+        const int row = i0 + 16 * x + c;
+        abase[x] = g * (int)a.A.sg + row * (int)a.A.si;
+        arow[x] = row < a.I;
+    }
+    float bias_v[TN];
+#pragma unroll
+    for (int y = 0; y < TN; ++y) {
+        const int col = j0 + 16 * y + c;
+        bbase[y] = g * (int)a.B.sg + col * (int)a.B.si;
+        bcol[y] = col < a.J;
+        bias_v[y] = (a.bias && bcol[y]) ? a.bias[g * a.bsg + col] : 0.f;
+    }
+    const int nall = a.R >> 4, per = (nall + KW - 1) / KW;
+    const int sbeg = w * per, nfull = min(nall, sbeg + per); // this wave's steps [sbeg, nfull)
+    floatx4 acc[TM][TN][SPLIT ? 2 : 1];
+#pragma unroll
+    for (int x = 0; x < TM; ++x)
+#pragma unroll
+        for (int y = 0; y < TN; ++y)
+#pragma unroll
+            for (int h = 0; h < (SPLIT ? 2 : 1); ++h) acc[x][y][h] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // groups of GS 16-wide steps, two register buffers: group k+1's loads are
+    // in flight while group k's MFMAs run
+    auto load = [&](int s0, uint32_t (&av)[GS][TM][4], uint32_t (&bv)[GS][TN][4]) {
+#pragma unroll
+        for (int s = 0; s < GS; ++s) {
+            const int r = 16 * (s0 + s) + 4 * q;
+            const bool live = s0 + s < nfull;
+#pragma unroll
+            for (int x = 0; x < TM; ++x) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(ra, (live & arow[x]) ? (abase[x] + r) * 4 : BUF_OOB, 0, 0);
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) av[s][x][jj] = v[jj];
+            }
+#pragma unroll
+            for (int y = 0; y < TN; ++y) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(rb, (live & bcol[y]) ? (bbase[y] + r) * 4 : BUF_OOB, 0, 0);
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) bv[s][y][jj] = v[jj];
+            }
+        }
+    };
+    auto step = [&](const float (&xa)[TM][4], const float (&xb)[TN][4], int h) {
+        if constexpr (P != PREC_F32) {
+#pragma unroll
+            for (int x = 0; x < TM; ++x)
+#pragma unroll
+                for (int y = 0; y < TN; ++y) {
+                    floatx4 &d = acc[x][y][SPLIT ? (h & 1) : 0];
+                    d = mfma_k16<P>(xa[x], xb[y], d);
+                }
+            return;
+        }
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+            for (int x = 0; x < TM; ++x)
+#pragma unroll
+                for (int y = 0; y < TN; ++y) {
+                    floatx4 &d = acc[x][y][SPLIT ? (jj & 1) : 0];
+                    d = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[x][jj], xb[y][jj], d, 0, 0, 0);
+                }
+    };
+    auto mma = [&](const uint32_t (&av)[GS][TM][4], const uint32_t (&bv)[GS][TN][4]) {
+#pragma unroll
+        for (int s = 0; s < GS; ++s) {
+            float xa[TM][4], xb[TN][4];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+#pragma unroll
+                for (int x = 0; x < TM; ++x) xa[x][jj] = __uint_as_float(av[s][x][jj]);
+#pragma unroll
+                for (int y = 0; y < TN; ++y) xb[y][jj] = __uint_as_float(bv[s][y][jj]);
+            }
+            step(xa, xb, s);
+        }
+    };
+    if constexpr (GS >= 20) { // the launcher picks GS = 20 only for R < 336: one group
+        uint32_t a0[GS][TM][4], b0[GS][TN][4];
+        load(sbeg, a0, b0);
+        __builtin_amdgcn_sched_barrier(0); // all loads in flight before the first MFMA
+        mma(a0, b0);
+    } else {
+        uint32_t a0[GS][TM][4], b0[GS][TN][4], a1[GS][TM][4], b1[GS][TN][4];
+        if (nfull > sbeg) load(sbeg, a0, b0);
+        for (int s0 = sbeg; s0 < nfull; s0 += 2 * GS) {
+            if (s0 + GS < nfull) load(s0 + GS, a1, b1);
+            mma(a0, b0);
+            if (s0 + GS >= nfull) break;
+            if (s0 + 2 * GS < nfull) load(s0 + 2 * GS, a0, b0);
+            mma(a1, b1);
+        }
+    }
+    if ((a.R & 15) && w == KW - 1) { // tail step
+        const int r = 16 * nall + 4 * q;
+        float xa[TM][4], xb[TN][4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+#pragma unroll
+            for (int x = 0; x < TM; ++x) xa[x][jj] = ldb(ra, arow[x] & (r + jj < a.R), abase[x] + r + jj);
+#pragma unroll
+            for (int y = 0; y < TN; ++y) xb[y][jj] = ldb(rb, bcol[y] & (r + jj < a.R), bbase[y] + r + jj);
+        }
+        step(xa, xb, 0);
+    }
+    if constexpr (SPLIT)
+#pragma unroll
+        for (int x = 0; x < TM; ++x)
+#pragma unroll
+            for (int y = 0; y < TN; ++y) {
+                acc[x][y][0] += acc[x][y][SPLIT ? 1 : 0];
+                acc[x][y][SPLIT ? 1 : 0] = floatx4{0.f, 0.f, 0.f, 0.f};
+            }
+    if constexpr (KW > 1) {
+        __shared__ floatx4 red[KW - 1][TM * TN][64];
+        if (w > 0)
+#pragma unroll
+            for (int x = 0; x < TM; ++x)
+#pragma unroll
+                for (int y = 0; y < TN; ++y) red[w - 1][x * TN + y][lane] = acc[x][y][0];
+        __syncthreads();
+        if (w > 0) return;
+#pragma unroll
+        for (int ww = 0; ww < KW - 1; ++ww)
+#pragma unroll
+            for (int x = 0; x < TM; ++x)
+#pragma unroll
+                for (int y = 0; y < TN; ++y) acc[x][y][0] += red[ww][x * TN + y][lane];
+    }
+    // acc[x][y][.][k] is C[i0 + 16x + 4q + k][j0 + 16y + c]
+#pragma unroll
+    for (int y = 0; y < TN; ++y) {
+        if (!bcol[y]) continue;
+        const int col = j0 + 16 * y + c;
+#pragma unroll
+        for (int x = 0; x < TM; ++x) {
+            const floatx4 v = SPLIT ? acc[x][y][0] + acc[x][y][SPLIT ? 1 : 0] : acc[x][y][0];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int rr = i0 + 16 * x + 4 * q + k;
+                if (rr < a.I) a.C[g * a.csg + (long)rr * a.csi + (long)col * a.csj] = act_fwd_t<EP>(v[k] + bias_v[y]);
+            }
+        }
+    }
+}
+
+// ---- bwd-weight on the output-contiguous layout ------------------------------
+// dW[g][i][j] = sum_m dP[m][i] X[m][j], dP = dY * act'(Y), db[g][i] = sum_m dP[m][i].
+// Both operands are contiguous along the OUTPUT dimensions (i resp. j) and
+// strided along the reduction m, so the k-permutation of the forward kernel
+// is applied to the output dimensions instead: in a 4-row step (rows m0..m0+3)
+// lane (c, q) loads VA consecutive i of row m0+q (one b32/b64/b128) and 4
+// consecutive j of that row (one b128).  MFMA (s, t) of the step multiplies A
+// row r <-> i = i0 + VA*r + s with B column c <-> j = j0 + 4c + t: VA*4 MFMAs
+// per 2-3 vector loads, a (16 VA) x 64 tile per workgroup.  The NW waves of a
+// workgroup take the steps round-robin and are summed through LDS.
+//
+// Lanes past the edge load the last VA (4) in-range elements of the row and
+// shift them into place; what they deliver for rows i >= I / columns j >= J
+// only reaches accumulator elements that are never stored.  Rows m >= M load 0.
+struct WgradArgs {
+    const float *dy, *y, *x;
+    int dysg, lddy, ysg, ldy, xsg, ldx;
+    float *dw, *db;
+    int I, J, M;
+};
+
+template <int VA>
+__device__ __forceinline__ void ld_vec(__amdgpu_buffer_rsrc_t r, int byte_off, float (&v)[VA]) {
+    if (VA == 4) {
+        const auto x = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = __uint_as_float(x[e]);
+    } else if (VA == 2) {
+        const auto x = __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, 0);
+        v[0] = __uint_as_float(x[0]);
+        v[VA - 1] = __uint_as_float(x[1]);
+    } else {
+        v[0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
+    }
+}
+
+// out[e] = v[min(e + sh, VA - 1)]  (sh > 0 only on the edge lanes)
+// (written as a select on sh with constant indices: a compare against e + sh
+// lets the compiler fold the chain into a dynamic index -> scratch)
+template <int VA>
+__device__ __forceinline__ float shifted(const float (&v)[VA], int sh, int e) {
+    float o = v[VA - 1];
+#pragma unroll
+    for (int d = VA - 2; d >= 0; --d) o = (sh == d) ? v[e + d < VA ? e + d : VA - 1] : o;
+    return o;
+}
+
+template <int AG, int VA, int NW, int P>
+__global__ __launch_bounds__(64 * NW) void dense_wgrad_kernel(WgradArgs a) {
+    constexpr int KS = VA == 1 ? 8 : 4; // 4-row steps per prefetch group (two groups in flight)
+    constexpr int NACC = VA * 4;
+    __shared__ float red[NW > 1 ? NW / 2 : 1][NACC * 4 + VA][64];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, q = lane >> 4, c = lane & 15;
+    const int3 tile = xcd_tile();
+    const int i0 = tile.y * 16 * VA, j0 = tile.x * 64, g = tile.z;
+    const int ia = i0 + VA * c, ib = min(ia, a.I - VA), shi = ia - ib;
+    const int ja = j0 + 4 * c, jb = min(ja, a.J - 4), shj = ja - jb;
+    const __amdgpu_buffer_rsrc_t rdy = rsrc(a.dy), ry = rsrc(AG > 0 ? a.y : a.dy), rx = rsrc(a.x);
+    const int dyb = g * a.dysg + ib, yb = g * a.ysg + ib, xb = g * a.xsg + jb;
+    const int nks = (a.M + 3) >> 2;
+    const int my = nks > w ? (nks - w + NW - 1) / NW : 0;
+    const int ngrp = (my + KS - 1) / KS;
+
+    struct Buf {
+        float a[KS][VA], y[KS][VA], b[KS][4];
+    };
+    floatx4 acc[VA][4];
+    float bsum[VA];
+#pragma unroll
+    for (int s = 0; s < VA; ++s) {
+        bsum[s] = 0.f;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[s][u] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    auto load = [&](int grp, Buf &f) {
+#pragma unroll
+        for (int sp = 0; sp < KS; ++sp) {
+            const int k = grp * KS + sp;
+            const int m = 4 * (w + k * NW) + q;
+            const bool live = (k < my) & (m < a.M);
+            ld_vec<VA>(rdy, live ? (dyb + m * a.lddy) * 4 : BUF_OOB, f.a[sp]);
+            if (AG > 0) ld_vec<VA>(ry, live ? (yb + m * a.ldy) * 4 : BUF_OOB, f.y[sp]);
+            ld_vec<4>(rx, live ? (xb + m * a.ldx) * 4 : BUF_OOB, f.b[sp]);
+        }
+    };
+    auto mma = [&](const Buf &f) {
+        if constexpr (P != PREC_F32) {
+            // four 4-row steps form one 16-deep MFMA: k-slot 4q + e of lane
+            // (c, q) is row m of step e (the same m on both operands)
+#pragma unroll
+            for (int s4 = 0; s4 < KS; s4 += 4) {
+                float fa[VA][4], fb[4][4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+#pragma unroll
+                    for (int s = 0; s < VA; ++s) {
+                        float v = shifted<VA>(f.a[s4 + e], shi, s);
+                        if (AG > 0) v *= act_grad_t<AG>(shifted<VA>(f.y[s4 + e], shi, s));
+                        bsum[s] += v;
+                        fa[s][e] = v;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) fb[u][e] = shifted<4>(f.b[s4 + e], shj, u);
+                }
+#pragma unroll
+                for (int s = 0; s < VA; ++s)
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) acc[s][u] = mfma_k16<P>(fa[s], fb[u], acc[s][u]);
+            }
+            return;
+        }
+#pragma unroll
+        for (int sp = 0; sp < KS; ++sp) {
+            float fa[VA], fb[4];
+#pragma unroll
+            for (int s = 0; s < VA; ++s) {
+                fa[s] = shifted<VA>(f.a[sp], shi, s);
+                if (AG > 0) fa[s] *= act_grad_t<AG>(shifted<VA>(f.y[sp], shi, s));
+                bsum[s] += fa[s];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) fb[u] = shifted<4>(f.b[sp], shj, u);
+#pragma unroll
+            for (int s = 0; s < VA; ++s)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) acc[s][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[s], fb[u], acc[s][u], 0, 0, 0);
+        }
+    };
+    Buf b0, b1;
+    if (ngrp > 0) load(0, b0);
+    for (int grp = 0; grp < ngrp; grp += 2) {
+        if (grp + 1 < ngrp) load(grp + 1, b1);
+        mma(b0);
+        if (grp + 1 >= ngrp) break;
+        if (grp + 2 < ngrp) load(grp + 2, b0);
+        mma(b1);
+    }
+    // tree-sum the NW partial tiles through LDS (lane-major: conflict free)
+#pragma unroll
+    for (int half = NW / 2; half >= 1; half >>= 1) {
+        if (w >= half && w < 2 * half) {
+#pragma unroll
+            for (int s = 0; s < VA; ++s) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) red[w - half][(s * 4 + u) * 4 + k][lane] = acc[s][u][k];
+                red[w - half][NACC * 4 + s][lane] = bsum[s];
+            }
+        }
+        __syncthreads();
+        if (w < half) {
+#pragma unroll
+            for (int s = 0; s < VA; ++s) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) acc[s][u][k] += red[w][(s * 4 + u) * 4 + k][lane];
+                bsum[s] += red[w][NACC * 4 + s][lane];
+            }
+        }
+        __syncthreads();
+    }
+    if (w > 0) return;
+    // acc[s][u][k] is dW[i0 + VA*(4q + k) + s][j0 + 4c + u]
+    float *dwg = a.dw + (long)g * a.I * a.J;
+#pragma unroll
+    for (int s = 0; s < VA; ++s)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = i0 + VA * (4 * q + k) + s;
+            if (i >= a.I) continue;
+            float *row = dwg + (long)i * a.J;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (ja + u < a.J) row[ja + u] = acc[s][u][k];
+        }
+    if (a.db && tile.x == 0) {
+#pragma unroll
+        for (int s = 0; s < VA; ++s) {
+            float v = bsum[s];
+            v += __shfl_xor(v, 16);
+            v += __shfl_xor(v, 32);
+            if (q == 0 && ia + s < a.I) a.db[(long)g * a.I + ia + s] = v;
+        }
+    }
+}
+
+template <int P>
+void launch_wgrad_p(const WgradArgs &a, dim3 grid, int va, int nw, int act, hipStream_t s) {
+#define WG_NW(AGv, VAv)                                                                              \
+    do {                                                                                           \
+        if (nw == 8) hipLaunchKernelGGL((dense_wgrad_kernel<AGv, VAv, 8, P>), grid, dim3(512), 0, s, a); \
+        else if (nw == 4) hipLaunchKernelGGL((dense_wgrad_kernel<AGv, VAv, 4, P>), grid, dim3(256), 0, s, a); \
+        else hipLaunchKernelGGL((dense_wgrad_kernel<AGv, VAv, 2, P>), grid, dim3(128), 0, s, a);       \
+    } while (0)
+#define WG_VA(AGv)                      \
+    do {                              \
+        if (va == 4) WG_NW(AGv, 4);   \
+        else if (va == 2) WG_NW(AGv, 2); \
+        else WG_NW(AGv, 1);           \
+    } while (0)
+    switch (act) {
+    case ACT_RELU: WG_VA(ACT_RELU); break;
+    case ACT_ELU: WG_VA(ACT_ELU); break;
+    case ACT_TANH: WG_VA(ACT_TANH); break;
+    default: WG_VA(ACT_NONE); break;
+    }
+#undef WG_VA
+#undef WG_NW
+}
+
+template <int P>
+void launch_fwd_p(const GemmArgs &a, dim3 grid, int tm, int tn, int kw, int wsteps, hipStream_t s) {
+#define FWD_GS(EPv, TMv, TNv, KWv)                                                                              \
+    do {                                                                                                      \
+        const dim3 blk(64 * KWv);                                                                             \
+        if (wsteps <= 5) hipLaunchKernelGGL((dense_fwd_kernel<EPv, 5, TMv, TNv, KWv, P>), grid, blk, 0, s, a); \
+        else if (TMv * TNv == 1 && wsteps <= 20)                                                              \
+            hipLaunchKernelGGL((dense_fwd_kernel<EPv, 20, TMv, TNv, KWv, P>), grid, blk, 0, s, a);            \
+        else if (TMv * TNv == 1)                                                                              \
+            hipLaunchKernelGGL((dense_fwd_kernel<EPv, 10, TMv, TNv, KWv, P>), grid, blk, 0, s, a);            \
+        else hipLaunchKernelGGL((dense_fwd_kernel<EPv, 5, TMv, TNv, KWv, P>), grid, blk, 0, s, a);             \
+    } while (0)
+#define FWD_LAUNCH(EPv)                                                                 \
+    do {                                                                                \
+        if (tm == 2 && tn == 2) FWD_GS(EPv, 2, 2, 1);                                   \
+        else if (kw == 2) FWD_GS(EPv, 1, 1, 2);                                         \
+        else FWD_GS(EPv, 1, 1, 1);                                                      \
+    } while (0)
+    switch (a.act) {
+    case ACT_RELU: FWD_LAUNCH(ACT_RELU); break;
+    case ACT_ELU: FWD_LAUNCH(ACT_ELU); break;
+    case ACT_TANH: FWD_LAUNCH(ACT_TANH); break;
+    default: FWD_LAUNCH(ACT_NONE); break;
+    }
+#undef FWD_LAUNCH
+#undef FWD_GS
+}
+
+
+} // namespace td7dense

@@ -1,6 +1,7 @@
 """Fused TD7 net ops backed by csrc/td7_ops.hip (GPU) with the reference's
 torch expression on CPU tensors (the CPU path exists for the learner's parity
 tests; on a GPU the HIP kernels are mandatory -- a missing library raises)."""
+import contextlib
 import os
 
 import torch
@@ -43,6 +44,25 @@ def avg_l1_norm(x, eps=1e-8):
 
 # ---------------------------------------------------------------- dense layers
 ACT_CODES = {None: 0, "none": 0, "relu": 1, "elu": 2, "tanh": 3}
+
+# MFMA operand precision of the td7_dense kernels (csrc/td7_dense_kernels.h
+# Prec; bits 8-15 of the act argument): "fp32" exact f32 MFMA; "bf16" / "fp16"
+# round the fp32 operands to nearest even as they are loaded (fp32 memory,
+# accumulation, epilogues and bias gradients).
+PRECISIONS = {"fp32": 0, "bf16": 1, "fp16": 2}
+_matrix_prec = 0
+
+
+@contextlib.contextmanager
+def matrix_precision(name):
+    """Dense layers created inside the block run their GEMMs (forward and the
+    matching backward) with `name` MFMA operands."""
+    global _matrix_prec
+    old, _matrix_prec = _matrix_prec, PRECISIONS[name]
+    try:
+        yield
+    finally:
+        _matrix_prec = old
 
 
 def act_code(fn):
@@ -98,14 +118,16 @@ class _DenseFn(torch.autograd.Function):
         xsg = 0 if (shared or not grouped) else x.stride(0)
         w = w.contiguous()
         bb = b.contiguous() if b is not None else None
-        if M <= _DenseFn.fwd_kernel_max_rows:
+        prec = _matrix_prec
+        if prec or M <= _DenseFn.fwd_kernel_max_rows:
             y = torch.empty((G, M, N) if grouped else (M, N), dtype=torch.float32, device=x.device)
             nat.check(nat.lib().td7_dense_fwd(nat.ptr(x), xsg, ldx, nat.ptr(w), nat.ptr(bb), nat.ptr(y),
-                                              M * N, N, G, M, N, K, act, nat.stream_ptr(x.device)), "td7_dense_fwd")
+                                              M * N, N, G, M, N, K, act | prec << 8, nat.stream_ptr(x.device)),
+                      "td7_dense_fwd")
         else:
             y = _torch_dense(x, w, bb, act)
         ctx.save_for_backward(x, w, y)
-        ctx.meta = (grouped, shared, G, M, N, K, act, xsg, ldx, b is not None)
+        ctx.meta = (grouped, shared, G, M, N, K, act | prec << 8, xsg, ldx, b is not None)
         return y
 
     @staticmethod

@@ -7,8 +7,9 @@ save/load suffixes) with three MI355X-first changes:
   (:245-246) and max_priority live in device tensors, the target policy noise
   scale is a device scalar, and LAP sampling/priority updates are HIP sum-tree
   kernels (exo_amd.replay.LAP, csrc/lap.hip);
-* optional bf16 autocast of the MLPs (BASELINE.json configs[1]: "TD7 bf16");
-  losses, optimiser state and master weights stay fp32;
+* optional bf16 / fp16 MFMA operands in the dense layers (BASELINE.json
+  configs[1] "TD7 bf16", configs[4] "fp16 MFMA"); activations, losses,
+  optimiser state and master weights stay fp32;
 * data-parallel training: gradients of encoder/critic/actor are flattened into
   one bucket per update and all-reduced over RCCL; the scalar bounds are
   MAX-reduced.
@@ -385,9 +386,12 @@ class TD7Learner:
         return float(self.exploration_noise_t)
 
     def _autocast(self):
-        if self.precision == "bf16":
-            return torch.autocast(device_type=self.device.type, dtype=torch.bfloat16)
-        return torch.autocast(device_type=self.device.type, enabled=False)
+        """fp32 (default): exact f32 MFMA.  bf16 / fp16: the dense layers'
+        GEMMs take MFMA operands rounded to bf16 / fp16 (fp32 storage,
+        accumulation, activations, norms, losses and optimiser state)."""
+        if self.precision not in ops.PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(ops.PRECISIONS)}, not {self.precision!r}")
+        return ops.matrix_precision(self.precision)
 
     # One TD7 update (:211-293) is split into phases so a data-parallel step
     # needs only two collectives and every phase can be captured in a HIP

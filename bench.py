@@ -89,7 +89,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--mode", choices=["train", "env"], default="train")
-    ap.add_argument("--precision", choices=["bf16", "fp32"], default="fp32")
+    ap.add_argument("--precision", choices=["bf16", "fp16", "fp32"], default="fp32")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no HIP graph capture of the training iteration")

@@ -209,3 +209,27 @@ def test_device_pink_noise_matches_numpy_and_statistics():
     a = ag.select_action_batch(obs, timestep=t)
     ref = (ag.learner.act(obs) + noise[:, 7][None, :]).clamp(-1, 1)
     torch.testing.assert_close(a, ref, rtol=0, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["bf16", "fp16"])
+def test_reduced_precision_train_steps_track_fp32(precision):
+    """BASELINE configs[1] ("TD7 bf16") / configs[4] ("fp16 MFMA"): the golden
+    steps with bf16 / fp16 MFMA operands stay within the rounding error of the
+    fp32 reference (priorities 2e-2, parameters 1e-3 after two Adam steps)."""
+    g = _golden()
+    L = _learner(g, "cpu")
+    L2 = TD7Learner(80, 7, L.hp, learning_steps=int(g["learning_steps"]), device="cuda", precision=precision)
+    for name in ("actor", "critic", "encoder", "actor_target", "critic_target", "fixed_encoder",
+                 "fixed_encoder_target"):
+        getattr(L2, name).load_state_dict(getattr(L, name).state_dict())
+    for step in range(2):
+        b = [torch.tensor(g[f"batch{step}_{k}"], device="cuda") for k in
+             ("state", "action", "next_state", "reward", "not_done")]
+        prio = L2.update(*b, noise=torch.tensor(g[f"batch{step}_noise"], device="cuda"))
+        np.testing.assert_allclose(prio.cpu().numpy(), g[f"priority{step}"], rtol=2e-2, atol=2e-2)
+        for name in ("actor", "critic", "encoder"):
+            ref = _sd(g, f"step{step}_{name}")
+            for k, v in getattr(L2, name).state_dict().items():
+                np.testing.assert_allclose(v.cpu().numpy(), ref[k].numpy(), rtol=0, atol=1e-3,
+                                           err_msg=f"step {step} {name}.{k}")

@@ -109,3 +109,55 @@ def test_nets_fused_match_torch_layers():
     torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-4, atol=1e-5)
     for g0, g1 in zip(outs[0][2], outs[1][2]):
         torch.testing.assert_close(g0, g1, rtol=1e-3, atol=1e-6)
+
+
+# ------------------------------------------------------------ bf16 / fp16 MFMA
+_ROUND = {"bf16": torch.bfloat16, "fp16": torch.float16}
+_GRAD = {0: lambda y: torch.ones_like(y), 1: lambda y: (y > 0).to(y.dtype), 2: lambda y: torch.where(y > 0, 1.0, y + 1),
+         3: lambda y: 1 - y * y}
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+@pytest.mark.parametrize("act", [0, 2, 3])
+@pytest.mark.parametrize("m,n,k,g,shared", [(1024, 300, 80, 0, False), (1000, 300, 307, 0, False),
+                                            (4096, 300, 300, 0, False), (37, 7, 87, 0, False),
+                                            (1024, 320, 920, 2, False), (1024, 320, 87, 2, True),
+                                            (1024, 1, 320, 2, False)])
+def test_dense_reduced_precision_is_the_gemm_of_rounded_operands(prec, act, m, n, k, g, shared):
+    """bf16 / fp16 operand mode: each GEMM equals the fp64 GEMM of the
+    operands rounded to nearest even (dP = dY * act'(Y) rounded as loaded);
+    the bias gradient is the fp32 column sum of the unrounded dP."""
+    from exo_amd import ops
+    torch.manual_seed(m + n + k + act)
+    rd = lambda t: t.to(_ROUND[prec]).double()  # noqa: E731
+    x = torch.randn(m, k, device="cuda") if (g == 0 or shared) else torch.randn(g, m, k, device="cuda")
+    w = (torch.randn(n, k, device="cuda") if g == 0 else torch.randn(g, n, k, device="cuda")) / k ** 0.5
+    b = torch.randn(n, device="cuda") if g == 0 else torch.randn(g, n, device="cuda")
+    xr, wr, br = (t.clone().requires_grad_(True) for t in (x, w, b))
+    with ops.matrix_precision(prec):
+        y = ops._DenseFn.apply(xr, wr, br, act)
+    xx = rd(x) if (g == 0 or not shared) else rd(x).unsqueeze(0).expand(g, m, k)
+    pre = (xx @ rd(w).transpose(-1, -2)) + b.double().unsqueeze(-2)
+    ref = ACTS[act](pre)
+    torch.testing.assert_close(y.double(), ref, rtol=1e-5, atol=1e-5)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    dp32 = dy * _GRAD[act](y.detach())
+    dp = rd(dp32)
+    dx = dp @ rd(w)
+    if g and shared:
+        dx = dx.sum(0)
+    dw = dp.transpose(-1, -2) @ xx
+    db = dp32.double().sum(-2)
+    for got, r, name in ((xr.grad, dx, "dx"), (wr.grad, dw, "dW"), (br.grad, db, "db")):
+        scale = max(1.0, float(r.abs().max()))
+        torch.testing.assert_close(got.double(), r, rtol=2e-3, atol=2e-3 * scale, msg=name)
+
+
+def test_reduced_precision_rejects_bad_codes():
+    from exo_amd import _native as nat
+    x = torch.randn(4, 4, device="cuda")
+    y = torch.empty(4, 4, device="cuda")
+    rc = nat.lib().td7_dense_fwd(nat.ptr(x), 0, 4, nat.ptr(x), None, nat.ptr(y), 16, 4, 1, 4, 4, 4, 3 << 8,
+                                 nat.stream_ptr(x.device))
+    assert rc == -22

@@ -8,6 +8,10 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 import torch  # noqa: E402
 from exo_amd import _native as nat  # noqa: E402
 
+# MFMA operand precision (DB_PREC=fp32|bf16|fp16): bits 8-15 of the act code
+PREC = {"fp32": 0, "bf16": 1, "fp16": 2}[os.environ.get("DB_PREC", "fp32")]
+ACT = 2 | PREC << 8  # ELU
+
 
 def timeit(fn, reps=20, replays=10):
     """GPU time per launch: `reps` launches captured in a HIP graph, replayed
@@ -47,6 +51,7 @@ def floor():
 
 def main():
     floor()
+    print("MFMA operands:", os.environ.get("DB_PREC", "fp32"))
     L = nat.lib()
     dev = torch.device("cuda")
     print(f"{'M':>5} {'N':>4} {'K':>4} | {'fwd':>7} {'bwd_d':>7} {'bwd_w':>7} | {'torch fwd':>9} | GF/s fwd")
@@ -63,11 +68,11 @@ def main():
         dw = torch.empty(n, k, device="cuda")
         db = torch.empty(n, device="cuda")
         P = nat.ptr
-        f = timeit(lambda: L.td7_dense_fwd(P(x), 0, k, P(w), P(b), P(y), m * n, n, 1, m, n, k, 2, nat.stream_ptr(dev)))
+        f = timeit(lambda: L.td7_dense_fwd(P(x), 0, k, P(w), P(b), P(y), m * n, n, 1, m, n, k, ACT, nat.stream_ptr(dev)))
         bd = timeit(lambda: L.td7_dense_bwd_data(P(dy), m * n, n, P(y), m * n, n, P(w), P(dx), m * k, k, 1, 0,
-                                                  m, n, k, 2, nat.stream_ptr(dev)))
+                                                  m, n, k, ACT, nat.stream_ptr(dev)))
         bw = timeit(lambda: L.td7_dense_bwd_weight(P(dy), m * n, n, P(y), m * n, n, P(x), 0, k, P(dw), P(db), 1,
-                                                    m, n, k, 2, nat.stream_ptr(dev)))
+                                                    m, n, k, ACT, nat.stream_ptr(dev)))
         tf = timeit(lambda: torch.nn.functional.elu(torch.nn.functional.linear(x, w, b)))
         print(f"{m:5d} {n:4d} {k:4d} | {f:7.2f} {bd:7.2f} {bw:7.2f} | {tf:9.2f} | {2 * m * n * k / f / 1e3:8.0f}")
     # the critic's two Q heads: groups = 2, separate inputs (TD7 critic q2/q3 layers)
@@ -81,11 +86,11 @@ def main():
         dw = torch.empty(2, n, k, device="cuda")
         db = torch.empty(2, n, device="cuda")
         P = nat.ptr
-        f = timeit(lambda: L.td7_dense_fwd(P(x), m * k, k, P(w), P(b), P(y), m * n, n, 2, m, n, k, 2, nat.stream_ptr(dev)))
+        f = timeit(lambda: L.td7_dense_fwd(P(x), m * k, k, P(w), P(b), P(y), m * n, n, 2, m, n, k, ACT, nat.stream_ptr(dev)))
         bd = timeit(lambda: L.td7_dense_bwd_data(P(dy), m * n, n, P(y), m * n, n, P(w), P(dx), m * k, k, 2, 0,
-                                                  m, n, k, 2, nat.stream_ptr(dev)))
+                                                  m, n, k, ACT, nat.stream_ptr(dev)))
         bw = timeit(lambda: L.td7_dense_bwd_weight(P(dy), m * n, n, P(y), m * n, n, P(x), m * k, k, P(dw), P(db), 2,
-                                                    m, n, k, 2, nat.stream_ptr(dev)))
+                                                    m, n, k, ACT, nat.stream_ptr(dev)))
         tf = timeit(lambda: torch.nn.functional.elu(torch.baddbmm(b.unsqueeze(1), x, w.transpose(1, 2))))
         print(f"2x{m:4d} {n:4d} {k:4d} | {f:7.2f} {bd:7.2f} {bw:7.2f} | {tf:9.2f} | {4 * m * n * k / f / 1e3:8.0f}")
 
