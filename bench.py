@@ -53,6 +53,16 @@ BYTES_PER_ENV_STEP = sum(STEP_READ_BYTES.values()) + sum(STEP_WRITE_BYTES.values
 
 
 FP32_MFMA_PEAK_TFS = 157.3  # v_mfma_f32_*_f32 dense peak (MI355X_MICROARCH.md)
+BF16_MFMA_PEAK_TFS = 2500.0  # bf16 / fp16 dense MFMA peak (MI355X_MICROARCH.md, no sparsity)
+MFMA_PEAK_TFS = {"fp32": FP32_MFMA_PEAK_TFS, "bf16": BF16_MFMA_PEAK_TFS, "fp16": BF16_MFMA_PEAK_TFS}
+
+# BASELINE.json configs: configs[1] is the bench line; configs[3] / configs[4]
+# run with --workload (their own lines, not the driver's bench line)
+WORKLOADS = {
+    "configs1": "configs[1]: 4096 vectorised exo envs per MI355X",
+    "dr_sweep": "configs[3]: domain-randomised tremor/DR sweep, per-env draws",
+    "wide": "configs[4]: wide TD7 (1024-wide MLPs, reference layer count), fp16 MFMA",
+}
 
 
 def td7_flops(agent, n_envs):
@@ -87,15 +97,24 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--envs", type=int, default=None, help="envs per GPU (workload default: 4096 / 16384 / 65536)")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="configs1")
     ap.add_argument("--mode", choices=["train", "env"], default="train")
-    ap.add_argument("--precision", choices=["bf16", "fp16", "fp32"], default="fp32")
+    ap.add_argument("--precision", choices=["bf16", "fp16", "fp32"], default=None,
+                    help="TD7 MFMA operands (workload default: bf16 per configs[1], fp16 for wide)")
+    ap.add_argument("--batch", type=int, default=None, help="TD7 rows per stratum (default 128)")
+    ap.add_argument("--cpu-threads", type=int, default=None, help="threads of the multi-core CPU baseline")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no HIP graph capture of the training iteration")
     ap.add_argument("--kernel-timing-steps", type=int, default=100,
                     help="env-only launches timed with HIP events for the roofline line")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.envs is None:
+        a.envs = {"configs1": 4096, "dr_sweep": 16384, "wide": 65536}[a.workload]
+    if a.precision is None:
+        a.precision = "fp16" if a.workload == "wide" else "bf16"
+    return a
 
 
 def pmc_traffic(bytes_per_launch):
@@ -111,22 +130,78 @@ def pmc_traffic(bytes_per_launch):
     return None, None
 
 
-def cpu_baseline(seconds):
-    """The oracle (plain C, fp64, one core) stepping 8 envs, one per motion, with
-    random actions -- the 'port' CPU baseline.  Bounded by `seconds`."""
+def cpu_baseline(seconds, threads=None):
+    """The oracle (plain C, fp64) stepping 8 envs each, one per motion, with
+    random actions -- the 'port' CPU baseline: one core for ~1/3 of the
+    budget, then one stepping loop per host core (ctypes drops the GIL) for
+    the rest.  `value` is the all-core rate."""
+    import threading
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
     from exo_amd import motions
     angles, lengths = motions.load()
     O.bench(8, angles, lengths, 2000)  # warm
-    steps, t0 = 0, time.perf_counter()
     chunk = 20000
-    while time.perf_counter() - t0 < seconds:
-        steps += O.bench(8, angles, lengths, chunk, seed=steps + 1)
+
+    def run(budget, seed0, out, i):
+        steps, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < budget:
+            steps += O.bench(8, angles, lengths, chunk, seed=seed0 + steps + 1)
+        out[i] = (steps, time.perf_counter() - t0)
+
+    one = [None]
+    run(seconds / 3, 0, one, 0)
+    s1, d1 = one[0]
+    if threads is None:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    threads = max(1, min(threads, len(os.sched_getaffinity(0))))
+    res = [None] * threads
+    ts = [threading.Thread(target=run, args=(seconds * 2 / 3, 10 ** 9 * (i + 1), res, i)) for i in range(threads)]
+    t0 = time.perf_counter()
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
     dt = time.perf_counter() - t0
-    return {"value": steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/exo_oracle.c env.step, 8 envs (one per motion), {steps} env-steps in {dt:.1f} s, "
-                      f"random actions, episode-synchronous resets"}
+    steps = sum(r[0] for r in res)
+    return {"value": steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "single_core_value": s1 / d1,
+            "sample": f"oracle/exo_oracle.c env.step (fp64, the reference's algorithm incl. scipy-RK45 control), "
+                      f"8 envs (one per motion) per thread, random actions, episode-synchronous resets: "
+                      f"{steps} env-steps in {dt:.1f} s on {threads} threads; 1 core: {s1} in {d1:.1f} s"}
+
+
+def critic_gemm_timing(agent, reps=20, replays=10):
+    """The critic's largest GEMM (both Q heads of Linear(2 zs + h -> h) + ELU,
+    Agent/TD7_multi_agent.py:121-126) alone: td7_dense_fwd launches captured in
+    a HIP graph, HIP events around the replays.  Returns (us per launch, flop)."""
+    from exo_amd import ops
+    L = agent.learner
+    c = L.critic
+    B = agent.hp.batch_size * agent.env_num
+    dev = c.w1.device
+    x = torch.randn(2, B, c.w1.shape[2], device=dev)
+    fn = lambda: ops.dense(x, c.w1, c.b1, ops.ACT_CODES["elu"])  # noqa: E731
+    with torch.no_grad(), ops.matrix_precision(L.precision):
+        fn()
+        st = torch.cuda.Stream(device=dev)
+        st.wait_stream(torch.cuda.current_stream(dev))
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(st):
+            with torch.cuda.graph(g, stream=st):
+                for _ in range(reps):
+                    fn()
+        torch.cuda.current_stream(dev).wait_stream(st)
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(replays):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / (reps * replays) * 1e3
+    return us, 2.0 * 2 * B * c.w1.shape[1] * c.w1.shape[2]
 
 
 def main():
@@ -148,7 +223,12 @@ def main():
     from exo_amd import VecExoskeletonEnv
 
     N = args.envs
-    env = VecExoskeletonEnv(N, seed=1000 + rank, device=dev)
+    env_kw = {}
+    if args.workload == "dr_sweep":  # per-env DR draws
+        rng = np.random.default_rng(1000 + rank)
+        env_kw = dict(matrix_noise_fraction=rng.uniform(0.05, 0.25, N), dr_actuator_range=rng.uniform(0.0, 0.1, N),
+                      dr_actuator_end_pos_shift=rng.uniform(0.0, 0.04, N), tremor_amplitude_range=(0.1, 1.0))
+    env = VecExoskeletonEnv(N, seed=1000 + rank, device=dev, **env_kw)
     Ls = env.lengths_host
     round_len = int(Ls.max()) - 3
     active_per_k = np.array([(Ls - 3 > k).sum() for k in range(round_len)])
@@ -157,6 +237,10 @@ def main():
         from exo_amd.rollout import VecTrainer
         from exo_amd.td7 import Agent, Hyperparameters
         hp = Hyperparameters()
+        if args.workload == "wide":  # 1024-wide encoder / critic / actor
+            hp = Hyperparameters(zs_dim=1024, enc_hdim=1024, critic_hdim=1024, actor_hdim=1024)
+        if args.batch:
+            hp.batch_size = args.batch
         agent = Agent(80, 7, 1, env_num=8, hp=hp, device=dev, precision=args.precision, n_envs=N,
                       process_group=dist.group.WORLD if world > 1 else None, graph_safe=not args.eager)
         trainer = VecTrainer(env, agent, use_graphs=not args.eager)
@@ -252,9 +336,9 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f64" if agent is None else f"f64 sim + {args.precision} TD7",
             "data": "synthetic: reference motions 0-7 (env i -> motion i mod 8), Philox tremor/DR draws, "
-                    + ("random actions" if agent is None else "random-init TD7 (reference widths 300/320)"),
-            "config": {"workload": "configs[1]: 4096 vectorised exo envs per MI355X"
-                                   + (", TD7 batch 8x128" if agent else ", env only"),
+                    + ("random actions" if agent is None else (f"random-init TD7 (widths {agent.hp.zs_dim}/{agent.hp.critic_hdim})")),
+            "config": {"workload": WORKLOADS[args.workload]
+                                   + (f", TD7 batch 8x{agent.hp.batch_size}" if agent else ", env only"),
                        "envs_per_gpu": N, "mode": args.mode, "parallelism": f"env-shard x{world}"
                        + (" + TD7 DP all-reduce" if agent and world > 1 else "")},
             "roofline": {"kernel": "exo_step_rp_kernel" if N <= 16384 else "exo_step_kernel", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
@@ -270,11 +354,22 @@ def main():
             # per grad step over the step time left after the env kernel
             fl = td7_flops(agent, N)
             td7_s = max(elapsed / args.steps - kern_ms * 1e-3, 1e-9)
-            res["td7_roofline"] = {"bound": "mfma", "achieved": fl / td7_s / 1e12, "peak": FP32_MFMA_PEAK_TFS,
-                                   "unit": "TFLOP/s", "frac": fl / td7_s / 1e12 / FP32_MFMA_PEAK_TFS,
-                                   "gflop_per_step": fl / 1e9,
-                                   "note": "GEMM flops of one train() step (B=1024) + batched actor inference "
+            peak = MFMA_PEAK_TFS[args.precision]
+            res["td7_roofline"] = {"bound": "mfma", "achieved": fl / td7_s / 1e12, "peak": peak,
+                                   "unit": "TFLOP/s", "frac": fl / td7_s / 1e12 / peak,
+                                   "gflop_per_step": fl / 1e9, "mfma_operands": args.precision,
+                                   "formula": "sum over Linear layers of 2*M*N*K: x3 (fwd, dX, dW) where trained, "
+                                              "x1 no-grad; actor update x0.5 (policy_freq 2); + select_action "
+                                              "over all envs (bench.td7_flops)",
+                                   "note": "GEMM flops of one train() step (B=8x128) + batched actor inference "
                                            "over the envs, per iteration time minus the env kernel"}
+            us, cfl = critic_gemm_timing(agent)
+            res["critic_gemm_roofline"] = {
+                "kernel": "td7_dense_fwd, critic Linear(2*zs+h -> h) + ELU, both Q heads", "bound": "mfma",
+                "shape": [2, agent.hp.batch_size * agent.env_num, agent.learner.critic.w1.shape[1],
+                          agent.learner.critic.w1.shape[2]],
+                "achieved": cfl / (us * 1e-6) / 1e12, "peak": peak, "unit": "TFLOP/s",
+                "frac": cfl / (us * 1e-6) / 1e12 / peak, "avg_kernel_us": us}
         if finite is not None:
             res["weights_finite"] = all(finite.values()) or finite
         if dp_sync is not None:
@@ -282,7 +377,7 @@ def main():
             if not dp_sync:
                 res["dp_weight_checksums"] = dp_ck
         if not args.no_cpu_baseline and world == 1:
-            res["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds)
+            res["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, args.cpu_threads)
         print(json.dumps(res))
     if world > 1:
         dist.destroy_process_group()

@@ -224,3 +224,50 @@ def test_kernel_variants_agree():
         np.testing.assert_allclose(o0[2], o1[2], rtol=1e-5, atol=1e-7)
     for i in (0, 513, 1029):
         np.testing.assert_allclose(envs[0].get_state(i), envs[1].get_state(i), rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_domain_randomisation_sweep_matches_oracle(variant):
+    """BASELINE configs[3]: 16,384 envs with per-env DR draws
+    (matrix_noise_fraction ~ U(0.05, 0.25), dr_actuator_range ~ U(0, 0.1),
+    dr_actuator_end_pos_shift ~ U(0, 0.04), tremor magnitude range [0.1, 1.0]
+    -- Exoskeleton_env.py:70's range); a sample of envs replayed on the oracle
+    with each env's own parameters and draw streams."""
+    from exo_amd import VecExoskeletonEnv, motions
+    N, seed = 16384, 2024
+    rng = np.random.default_rng(3)
+    mat_f = rng.uniform(0.05, 0.25, N)
+    act_r = rng.uniform(0.0, 0.1, N)
+    shift_r = rng.uniform(0.0, 0.04, N)
+    env = VecExoskeletonEnv(N, seed=seed, matrix_noise_fraction=mat_f, dr_actuator_range=act_r,
+                            dr_actuator_end_pos_shift=shift_r, tremor_amplitude_range=(0.1, 1.0))
+    env.set_step_variant(variant)
+    obs0 = env.reset().cpu().numpy()
+    angles, lengths = motions.load()
+    lib = model_host()
+    acts = rng.uniform(-1, 1, (6, N, 7)).astype(np.float32)
+    outs = []
+    o = env.new_outputs(True)
+    for k in range(6):
+        ob, r, dn, inf = env.step(torch.as_tensor(acts[k], device=env.device), out=o)
+        outs.append((ob.cpu().numpy().copy(), r.cpu().numpy().copy(), inf.cpu().numpy().copy()))
+    cfg = env_kwargs_default()
+    for e in [0, 5, 4097, 9999, 16383]:
+        m = e % 8
+        L = int(lengths[m])
+        oe = O.OracleEnv(angles[m][:, :L], cfg["seq"], np.array([0.1, 1.0]), cfg["h1"], cfg["h2"], 40.0, 20.0,
+                         shift_r[e], act_r[e], mat_f[e])
+        oe.reset(philox_draws(L, seed, e, 0, lib))
+        ob = oe.reset(philox_draws(L, seed, e, 1, lib))
+        _close_obs(obs0[e], ob)
+        _, D, S, sh, mx = oe.episode()
+        Dg, Sg, _, shg, mxg = env.episode(e)   # per-env DR draws: bit-exact
+        np.testing.assert_array_equal(Dg, D)
+        np.testing.assert_array_equal(Sg, S)
+        np.testing.assert_array_equal(shg, sh)
+        np.testing.assert_array_equal(mxg, mx)
+        for k in range(6):
+            ob, r, dn, info, _ = oe.step(acts[k][e].astype(np.float64))
+            _close_obs(outs[k][0][e], ob)
+            np.testing.assert_allclose(outs[k][1][e], r, rtol=2e-6, atol=1e-7)
+            np.testing.assert_allclose(outs[k][2][e], info, rtol=1e-5, atol=1e-6)
