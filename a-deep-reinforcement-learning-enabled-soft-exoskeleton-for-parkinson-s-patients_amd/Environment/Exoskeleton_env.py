@@ -10,7 +10,9 @@ step/reset run as HIP kernels on the GPU.  Differences, all deliberate:
   ``np.random`` state at construction (so ``set_seeds`` keeps runs repeatable);
   the reference draws from ``np.random`` directly.
 * PyBullet is replaced by URDF forward kinematics plus the idealised position
-  motor model of SURVEY.md A.2 (Bullet parity is unpinned).
+  motor model of SURVEY.md A.2 (default), or with ``physics="multibody"`` by
+  Featherstone dynamics of the URDF tree with a joint-space impulse solve of
+  the motors and limits (Bullet parity is unpinned).
 * ``check_movement_boundaries`` counts violations instead of printing them.
 """
 import numpy as np
@@ -40,7 +42,7 @@ class ExoskeletonEnv_train:
     def __init__(self, reference_motion_file_num: str, tremor_sequence, tremor_amplitude_range=(0.95, 1.05),
                  first_harmonics_interval=(4, 6), second_harmonics_interval=(8, 10), max_force_shoulder: float = 40,
                  max_force_elbow: float = 20, dr_actuator_end_pos_shift: float = 0.02, dr_actuator_range: float = 0.1,
-                 matrix_noise_fraction: float = 0.1, seed=None, device=None):
+                 matrix_noise_fraction: float = 0.1, seed=None, device=None, physics="ideal"):
         self.file_num = str(reference_motion_file_num)
         self.dt = 1 / 40
         self.tremor_input_sequence = np.asarray(tremor_sequence)
@@ -63,7 +65,7 @@ class ExoskeletonEnv_train:
                                       max_force_shoulder=max_force_shoulder, max_force_elbow=max_force_elbow,
                                       dr_actuator_end_pos_shift=dr_actuator_end_pos_shift,
                                       dr_actuator_range=dr_actuator_range,
-                                      matrix_noise_fraction=matrix_noise_fraction)
+                                      matrix_noise_fraction=matrix_noise_fraction, physics=physics)
         self.device = self._vec.device
         self.max_count = int(self._vec.lengths_host[0])
         self.action_space = Box(-1.0, 1.0, shape=(7,), dtype=np.float32)  # :74

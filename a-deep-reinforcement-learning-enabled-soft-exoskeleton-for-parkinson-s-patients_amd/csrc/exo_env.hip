@@ -12,6 +12,8 @@
 //                      the actuated joint ODE, lane 1 the tremor-only ODE
 //                      (:409-414), then lane 0 finishes the step (targets,
 //                      motor update, reward, observation; :417-471).
+//   exo_multibody_kernel (csrc/exo_multibody.hip): the multibody stepSimulation
+//                      that follows the step kernel in EXO_PHYS_MULTIBODY mode.
 //
 // C ABI: include/exo_amd.h.
 #include <hip/hip_runtime.h>
@@ -282,7 +284,14 @@ __global__ __launch_bounds__(256) void exo_step_kernel(Dev S, Urdf U, const floa
         for (int j = 0; j < 5; ++j) q[j] = S.phys_q[(size_t)j * N + e];
 #pragma unroll
         for (int j = 0; j < 6; ++j) refo[j] = S.ref[(size_t)j * N + e];
-        link_coms(U, q, ak, refn);
+        if (S.mb_q) { // multibody mode: the k-links sit at their prismatic joint positions
+            double qp[14];
+#pragma unroll
+            for (int j = 0; j < 14; ++j) qp[j] = S.mb_q[(size_t)(5 + j) * N + e];
+            link_coms(U, q, ak, refn, qp);
+        } else {
+            link_coms(U, q, ak, refn);
+        }
 #pragma unroll
         for (int k = 0; k < 14; ++k)
 #pragma unroll
@@ -431,6 +440,12 @@ __global__ __launch_bounds__(256) void exo_step_kernel(Dev S, Urdf U, const floa
     if (!(-80 < ang[0] && ang[0] < 80) || !(-40 < ang[1] && ang[1] < 160.5) || !(-151.5 < ang[2] && ang[2] < 33.5) ||
         !(-10 < ang[3] && ang[3] < 150))
         S.viol[e] += 1;
+    if (S.mb_tgt) { // multibody mode: exo_multibody_kernel runs stepSimulation next
+#pragma unroll
+        for (int j = 0; j < 5; ++j) S.mb_tgt[(size_t)j * N + e] = tgt[j];
+        S.mb_flag[e] = 1;
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
         const double q0 = S.phys_q[(size_t)j * N + e];
@@ -554,6 +569,10 @@ struct exo_ctx {
     std::vector<void *> allocs;
     float *obs_scratch = nullptr;
     int step_variant = EXO_STEP_AUTO;
+    int physics = EXO_PHYS_IDEAL;
+    MbModel mb{};
+    double *mb_q = nullptr, *mb_qd = nullptr, *mb_tgt = nullptr;
+    uint8_t *mb_flag = nullptr;
     std::string err;
 };
 
@@ -730,13 +749,105 @@ int exo_step(exo_ctx *c, const float *act_dev, float *obs_dev, float *rew_dev, u
     if (!c || !act_dev || !obs_dev || !rew_dev || !done_dev) return EXO_EINVAL;
     DeviceGuard g(c->device);
     const bool rows = c->step_variant == EXO_STEP_ROWS || (c->step_variant == EXO_STEP_AUTO && c->N <= 16384);
-    if (rows)
-        return check(c, launch_exo_step_rp(c->S, c->U, act_dev, obs_dev, rew_dev, done_dev, info_dev, active_dev,
-                                           (hipStream_t)stream), "exo_step");
-    const int threads = 256, lanes = 2 * c->N;
-    hipLaunchKernelGGL(exo_step_kernel, dim3((lanes + threads - 1) / threads), dim3(threads), 0, (hipStream_t)stream,
-                       c->S, c->U, act_dev, obs_dev, rew_dev, done_dev, info_dev, active_dev);
-    return check(c, hipGetLastError(), "exo_step");
+    hipError_t e;
+    if (rows) {
+        e = launch_exo_step_rp(c->S, c->U, act_dev, obs_dev, rew_dev, done_dev, info_dev, active_dev,
+                               (hipStream_t)stream);
+    } else {
+        const int threads = 256, lanes = 2 * c->N;
+        hipLaunchKernelGGL(exo_step_kernel, dim3((lanes + threads - 1) / threads), dim3(threads), 0,
+                           (hipStream_t)stream, c->S, c->U, act_dev, obs_dev, rew_dev, done_dev, info_dev, active_dev);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess && c->physics == EXO_PHYS_MULTIBODY) // stepSimulation (:433) of the envs just stepped
+        e = launch_exo_multibody(c->S, c->U, c->mb, c->S.mb_tgt, c->S.mb_flag, 1, (hipStream_t)stream);
+    return check(c, e, "exo_step");
+}
+
+void exo_multibody_default_params(exo_mb_params *p) {
+    if (!p) return;
+    p->gravity = 9.81;               // Exoskeleton_env.py:116
+    p->kp = 0.1;                     // setJointMotorControlArray defaults (sim:115-117)
+    p->kd = 1.0;
+    p->motor_impulse = 1e5 * DT;     // default force 1e5, x timestep
+    p->passive_impulse = 1.0;        // pybullet's default joint velocity motors
+    p->limit_impulse = 100.0;        // btMultiBodyConstraint default
+    p->erp = 0.2;                    // btContactSolverInfo default
+    p->lin_damp = 0.04;              // btMultiBody defaults
+    p->ang_damp = 0.04;
+    p->max_vel = 100.0;
+    p->iters = 50;                   // pybullet default numSolverIterations
+}
+
+int exo_set_physics(exo_ctx *c, int32_t mode, const exo_mb_params *params) {
+    if (!c || (mode != EXO_PHYS_IDEAL && mode != EXO_PHYS_MULTIBODY)) return EXO_EINVAL;
+    exo_mb_params p;
+    exo_multibody_default_params(&p);
+    if (params) p = *params;
+    if (p.iters < 0 || p.iters > 100000 || !(p.motor_impulse >= 0) || !(p.passive_impulse >= 0) ||
+        !(p.limit_impulse >= 0) || !(p.max_vel > 0))
+        return fail(c, EXO_EINVAL, "exo_set_physics: invalid multibody parameters");
+    DeviceGuard g(c->device);
+    const size_t N = c->N;
+    int rc = check(c, hipDeviceSynchronize(), "exo_set_physics");
+    if (rc) return rc;
+    if (mode == EXO_PHYS_IDEAL) {
+        c->physics = mode;
+        c->S.mb_q = c->S.mb_qd = c->S.mb_tgt = nullptr;
+        c->S.mb_flag = nullptr;
+        return EXO_OK;
+    }
+    if (!c->mb_q) {
+        c->mb_q = dalloc<double>(c, NJ * N);
+        c->mb_qd = dalloc<double>(c, NJ * N);
+        c->mb_tgt = dalloc<double>(c, 5 * N);
+        c->mb_flag = dalloc<uint8_t>(c, N);
+        if (!c->mb_q || !c->mb_qd || !c->mb_tgt || !c->mb_flag) return fail(c, EXO_ENOMEM, "exo_set_physics: out of memory");
+    }
+    if (c->physics != EXO_PHYS_MULTIBODY) {
+        // continue from the current arm pose at rest, k-links at their load position 0
+        hipError_t e = hipMemset(c->mb_q, 0, NJ * N * sizeof(double));
+        if (e == hipSuccess) e = hipMemset(c->mb_qd, 0, NJ * N * sizeof(double));
+        if (e == hipSuccess) e = hipMemset(c->mb_flag, 0, N);
+        if (e == hipSuccess) e = hipMemcpy(c->mb_q, c->S.phys_q, 5 * N * sizeof(double), hipMemcpyDeviceToDevice);
+        if ((rc = check(c, e, "exo_set_physics"))) return rc;
+    }
+    build_mb_model(c->mb);
+    c->mb.g = p.gravity; c->mb.kp = p.kp; c->mb.kd = p.kd; c->mb.motor_imp = p.motor_impulse;
+    c->mb.passive_imp = p.passive_impulse; c->mb.limit_imp = p.limit_impulse; c->mb.erp = p.erp;
+    c->mb.lin_damp = p.lin_damp; c->mb.ang_damp = p.ang_damp; c->mb.max_vel = p.max_vel; c->mb.iters = p.iters;
+    c->S.mb_q = c->mb_q; c->S.mb_qd = c->mb_qd; c->S.mb_tgt = c->mb_tgt; c->S.mb_flag = c->mb_flag;
+    c->physics = mode;
+    return EXO_OK;
+}
+
+int exo_multibody_advance(exo_ctx *c, const double *targets_dev, const uint8_t *mask_dev, void *stream) {
+    if (!c || !targets_dev) return EXO_EINVAL;
+    if (c->physics != EXO_PHYS_MULTIBODY) return fail(c, EXO_EINVAL, "exo_multibody_advance: physics is not multibody");
+    DeviceGuard g(c->device);
+    return check(c, launch_exo_multibody(c->S, c->U, c->mb, targets_dev, const_cast<uint8_t *>(mask_dev), 0,
+                                         (hipStream_t)stream), "exo_multibody_advance");
+}
+
+int exo_get_multibody_state_host(exo_ctx *c, int32_t env, double *q19, double *qd19) {
+    if (!c || env < 0 || env >= c->N || !q19 || !qd19) return EXO_EINVAL;
+    if (c->physics != EXO_PHYS_MULTIBODY) return fail(c, EXO_EINVAL, "physics is not multibody");
+    DeviceGuard g(c->device);
+    int rc = check(c, hipDeviceSynchronize(), "sync");
+    for (int j = 0; j < NJ && !rc; ++j) rc = read1(c, (const double *)c->mb_q, (size_t)j * c->N + env, &q19[j]);
+    for (int j = 0; j < NJ && !rc; ++j) rc = read1(c, (const double *)c->mb_qd, (size_t)j * c->N + env, &qd19[j]);
+    return rc;
+}
+
+int exo_set_multibody_state_host(exo_ctx *c, int32_t env, const double *q19, const double *qd19) {
+    if (!c || env < 0 || env >= c->N || !q19 || !qd19) return EXO_EINVAL;
+    if (c->physics != EXO_PHYS_MULTIBODY) return fail(c, EXO_EINVAL, "physics is not multibody");
+    DeviceGuard g(c->device);
+    int rc = check(c, hipDeviceSynchronize(), "sync");
+    for (int j = 0; j < NJ && !rc; ++j) rc = write1(c, c->mb_q, (size_t)j * c->N + env, q19[j]);
+    for (int j = 0; j < NJ && !rc; ++j) rc = write1(c, c->mb_qd, (size_t)j * c->N + env, qd19[j]);
+    for (int j = 0; j < 5 && !rc; ++j) rc = write1(c, c->S.phys_q, (size_t)j * c->N + env, q19[j]);
+    return rc;
 }
 
 int32_t exo_num_envs(const exo_ctx *c) { return c ? c->N : 0; }

@@ -87,6 +87,16 @@ struct Urdf {           // filled on the host (exo_create) and passed by value
     double kbase[5][3]; // world positions of the base-fixed k-links (joints 14..18)
     double com3[3];     // auxlink3 CoM in its frame (exo_v3.urdf:84)
     double lo[5], hi[5];// revolute limits (exo_v3.urdf:17,37,57,77,97)
+    double kz[14][3];   // prismatic joints 5..18: axis (0 0 1) of the joint frame in the parent frame
+};
+
+// Multibody physics mode (csrc/exo_multibody.hip): <inertial> data of the arm
+// links (exo_v3.urdf:23-27, 43-47, 63-67, 83-87, 103-107; the k-links have mass
+// 1 and unit inertia) and the solver constants (include/exo_amd.h exo_mb_params).
+struct MbModel {
+    double m[5], com[5][3], Rin[5][9], Id[5][3];
+    double g, kp, kd, motor_imp, passive_imp, limit_imp, erp, lin_damp, ang_damp, max_vel;
+    int iters;
 };
 
 // ---------------------------------------------------------------------------
@@ -113,6 +123,10 @@ struct Dev {
     double *prev_a, *prev2_a;        // [7][N]
     int32_t *err;                    // [1] sticky error bits
     int32_t *viol;                   // [N] steps with a joint-range violation
+    // multibody physics mode only (nullptr in the idealised mode):
+    double *mb_q, *mb_qd;            // [19][N] joint positions / velocities (rows 0..4 mirror phys_q)
+    double *mb_tgt;                  // [5][N] POSITION_CONTROL targets written by the step kernel (rad)
+    uint8_t *mb_flag;                // [N] 1 = the step kernel stepped the env, the physics kernel follows
 };
 
 __host__ __device__ inline void matmul3(const double *A, const double *B, double *C) {
@@ -138,11 +152,27 @@ __host__ __device__ inline void xform(const double *R, const double *p, const do
     for (int a = 0; a < 3; ++a) o[a] = p[a] + R[a * 3] * v[0] + R[a * 3 + 1] * v[1] + R[a * 3 + 2] * v[2];
 }
 
+// Multibody mode: a k-link (joint 5..18) slides qk along its joint axis,
+// which is kz in the parent frame R (R4 for k12/k22, R2 for the humerus
+// k-links, the world for the base k-links).
+__host__ __device__ __forceinline__ void slide(const Urdf &U, int link, const double *R2, const double *R4, double qk,
+                                               double *o) {
+    const double *z = U.kz[link - 5];
+    const double *R = (link == 5 || link == 6) ? R4 : R2;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const double ax = link >= 14 ? z[a] : R[a * 3] * z[0] + R[a * 3 + 1] * z[1] + R[a * 3 + 2] * z[2];
+        o[a] += qk * ax;
+    }
+}
+
 // Forward kinematics of the link CoMs that getLinkState(...)[0] returns
 // (Exoskeleton_sim_pybullet.py:129-142, 194-195, 348-349) for revolute
-// positions q[5]; prismatic actuator anchors are held at 0.
+// positions q[5]; prismatic actuator anchors are held at 0
+// unless qp (positions of joints 5..18, multibody mode) is given.
 // act[k] = CoM of link K_LINK[k] (without the dummy shift); ref = links 0, 3.
-__host__ __device__ inline void link_coms(const Urdf &U, const double *q, double act[14][3], double ref[6]) {
+__host__ __device__ inline void link_coms(const Urdf &U, const double *q, double act[14][3], double ref[6],
+                                          const double *qp = nullptr) {
     double Rt[9], R0[9], R1[9], R2[9], R3[9], R4[9];
     double p0[3] = {U.xyz[0][0], U.xyz[0][1], U.xyz[0][2] + 0.1}; // base at [0,0,0.1] (sim:18)
     double s, c;
@@ -161,6 +191,7 @@ __host__ __device__ inline void link_coms(const Urdf &U, const double *q, double
         if (j == 5 || j == 6) xform(R4, p3, U.xyz[j], act[k]);             // k12, k22 on the forearm
         else if (j >= 14) { act[k][0] = U.kbase[j - 14][0]; act[k][1] = U.kbase[j - 14][1]; act[k][2] = U.kbase[j - 14][2]; }
         else xform(R2, p0, U.xyz[j], act[k]);                               // k11..k72 on the humerus
+        if (qp) slide(U, j, R2, R4, qp[j - 5], act[k]);
     }
 }
 
@@ -372,6 +403,11 @@ __host__ __device__ inline double philox_u01(uint64_t seed, uint32_t env, uint32
 // row-parallel step (csrc/exo_step_rp.hip): 16 lanes per env, for small env counts
 hipError_t launch_exo_step_rp(const Dev &S, const Urdf &U, const float *act, float *obs, float *rew, uint8_t *done,
                               float *info, const uint8_t *active, hipStream_t stream);
+// multibody stepSimulation (csrc/exo_multibody.hip) of the envs with flag[e] != 0
+// (flag NULL = all); tgt [5][N]; clear_flag: zero the flags afterwards
+struct MbModel;
+hipError_t launch_exo_multibody(const Dev &S, const Urdf &U, const MbModel &M, const double *tgt, uint8_t *flag,
+                                int clear_flag, hipStream_t stream);
 #endif
 
 // URDF numbers, Simulation/exo_v3.urdf (kept literally: 3.141593 is not pi)
@@ -387,15 +423,49 @@ constexpr double J_RPY[5][3] = {{-3.141593, 3.141593, -3.141593}, {-1.570796, 3.
                                 {1.570796, 3.141593, 1.570796}, {1.570796, -1.570796, 0.000000},
                                 {1.570796, 3.141593, -3.141593}};
 
+// origin rpy of the prismatic joints 5..18 (exo_v3.urdf:120, 139, 158, ...)
+constexpr double J_RPY_K[3][3] = {{3.141593, 3.089233, 3.141593},   // k12, k22 (on alkar)
+                                  {-0.000000, 4.590216, -0.000000}, // k52 .. k62 (on the humerus)
+                                  {-3.141593, 3.141593, -3.141593}};// k51 .. k61 (on the base)
+inline int rpy_k_row(int joint) { return joint <= 6 ? 0 : (joint <= 13 ? 1 : 2); }
+
+// <inertial> of the arm links 0..4 (exo_v3.urdf:23-27, 43-47, 63-67, 83-87, 103-107)
+constexpr double L_MASS[5] = {0.20000000298023, 0.20000000298023, 2.0, 0.11219999939203, 1.1219999790192};
+constexpr double L_COM[5][3] = {{0, 0, 0}, {0, 0, 0}, {0.230000, 0, 0}, {0, 0.500000, -0.000000},
+                                {0.005234, 0, -0.245137}};
+constexpr double L_IRPY[5][3] = {{-3.141593, 3.141593, -3.141593}, {1.570796, 3.141593, -3.141593},
+                                 {-0.000000, -1.570796, 0.000000}, {1.570796, 3.141593, -3.141593},
+                                 {-3.141593, 3.141593, -3.141593}};
+constexpr double L_IDIAG[5][3] = {{0.00058960002794266, 0.00058960002794266, 0.0001124999968335},
+                                  {0.00058960002794266, 0.00058960002794266, 0.0001124999968335},
+                                  {0.05895833298564, 0.05895833298564, 0.011250000447035},
+                                  {0.00039539280435958, 0.00039539280435958, 3.5410318407441e-05},
+                                  {0.039536823770183, 0.039536823770183, 0.0035406111384836}};
+
+// URDF rpy -> rotation Rz(yaw) Ry(pitch) Rx(roll)
+inline void rpy_to_R(const double *r, double *R) {
+    const double cr = cos(r[0]), sr = sin(r[0]), cp = cos(r[1]), sp = sin(r[1]), cy = cos(r[2]), sy = sin(r[2]);
+    R[0] = cy * cp; R[1] = cy * sp * sr - sy * cr; R[2] = cy * sp * cr + sy * sr;
+    R[3] = sy * cp; R[4] = sy * sp * sr + cy * cr; R[5] = sy * sp * cr - cy * sr;
+    R[6] = -sp;     R[7] = cp * sr;                R[8] = cp * cr;
+}
+
+// Host-side precomputation of the multibody model's constant part.
+inline void build_mb_model(MbModel &M) {
+    for (int i = 0; i < 5; ++i) {
+        M.m[i] = L_MASS[i];
+        rpy_to_R(L_IRPY[i], M.Rin[i]);
+        for (int a = 0; a < 3; ++a) { M.com[i][a] = L_COM[i][a]; M.Id[i][a] = L_IDIAG[i][a]; }
+    }
+}
+
 // Host-side precomputation of the constant part of the kinematic tree.
 inline void build_urdf(Urdf &U) {
-    for (int j = 0; j < 5; ++j) {
-        const double *r = J_RPY[j];
-        const double cr = cos(r[0]), sr = sin(r[0]), cp = cos(r[1]), sp = sin(r[1]), cy = cos(r[2]), sy = sin(r[2]);
-        double *R = U.Ro[j]; // Rz(yaw) Ry(pitch) Rx(roll)
-        R[0] = cy * cp; R[1] = cy * sp * sr - sy * cr; R[2] = cy * sp * cr + sy * sr;
-        R[3] = sy * cp; R[4] = sy * sp * sr + cy * cr; R[5] = sy * sp * cr - cy * sr;
-        R[6] = -sp;     R[7] = cp * sr;                R[8] = cp * cr;
+    for (int j = 0; j < 5; ++j) rpy_to_R(J_RPY[j], U.Ro[j]);
+    for (int j = 5; j < NJ; ++j) {
+        double R[9];
+        rpy_to_R(J_RPY_K[rpy_k_row(j)], R);
+        U.kz[j - 5][0] = R[2]; U.kz[j - 5][1] = R[5]; U.kz[j - 5][2] = R[8];
     }
     for (int j = 0; j < NJ; ++j)
         for (int a = 0; a < 3; ++a) U.xyz[j][a] = J_XYZ[j][a];

@@ -235,6 +235,10 @@ __global__ __launch_bounds__(64 * RP_ENVS_PER_BLOCK / 4) void exo_step_rp_kernel
     {
         anchor(U, K_LINK[2 * j], R2, p0, R4, p3, k1);
         anchor(U, K_LINK[2 * j + 1], R2, p0, R4, p3, k2);
+        if (S.mb_q) { // multibody mode: the k-links sit at their prismatic joint positions
+            slide(U, K_LINK[2 * j], R2, R4, S.mb_q[(size_t)K_LINK[2 * j] * N + e], k1);
+            slide(U, K_LINK[2 * j + 1], R2, R4, S.mb_q[(size_t)K_LINK[2 * j + 1] * N + e], k2);
+        }
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
             k1[d] += S.shift[(size_t)((2 * j) * 3 + d) * N + e];
@@ -386,9 +390,14 @@ __global__ __launch_bounds__(64 * RP_ENVS_PER_BLOCK / 4) void exo_step_rp_kernel
     const double ang = imu[col * S.Lmax + c] + (joint < 4 ? qdeg : 0.0);
     bool viol = false;
     if (r < 5) {
-        const double q0 = S.phys_q[(size_t)joint * N + e];
-        const double nq = q0 + 0.1 * (ang * (PI / 180) - q0);
-        S.phys_q[(size_t)joint * N + e] = fmin(fmax(nq, U.lo[joint]), U.hi[joint]);
+        if (S.mb_tgt) { // multibody mode: exo_multibody_kernel runs stepSimulation next
+            S.mb_tgt[(size_t)joint * N + e] = ang * (PI / 180);
+            if (r == 0) S.mb_flag[e] = 1;
+        } else {
+            const double q0 = S.phys_q[(size_t)joint * N + e];
+            const double nq = q0 + 0.1 * (ang * (PI / 180) - q0);
+            S.phys_q[(size_t)joint * N + e] = fmin(fmax(nq, U.lo[joint]), U.hi[joint]);
+        }
         const double lo[4] = {-80, -40, -151.5, -10}, hi[4] = {80, 160.5, 33.5, 150};
         if (joint < 4) viol = !(lo[joint] < ang && ang < hi[joint]); // check_movement_boundaries (:594-605)
     }

@@ -46,6 +46,12 @@ class ExoEnvConfig(ctypes.Structure):
                 ("dr_actuator_range", c_double), ("matrix_noise_fraction", c_double)]
 
 
+class ExoMbParams(ctypes.Structure):
+    """exo_mb_params: constants of the multibody stepSimulation (include/exo_amd.h)."""
+    _fields_ = [(n, c_double) for n in ("gravity", "kp", "kd", "motor_impulse", "passive_impulse", "limit_impulse",
+                                        "erp", "lin_damp", "ang_damp", "max_vel")] + [("iters", c_int32)]
+
+
 EXPORTS = {
     "exo_create": (c_int32, [P(ExoEnvConfig), c_int32, P(c_double), P(c_int32), c_int32, c_int32, c_uint64, c_int32,
                              P(c_void_p)]),
@@ -62,6 +68,11 @@ EXPORTS = {
     "exo_set_state_host": (c_int32, [c_void_p, c_int32, P(c_double)]),
     "exo_set_seed": (c_int32, [c_void_p, c_uint64]),
     "exo_set_step_variant": (c_int32, [c_void_p, c_int32]),
+    "exo_multibody_default_params": (None, [P(ExoMbParams)]),
+    "exo_set_physics": (c_int32, [c_void_p, c_int32, P(ExoMbParams)]),
+    "exo_multibody_advance": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "exo_get_multibody_state_host": (c_int32, [c_void_p, c_int32, P(c_double), P(c_double)]),
+    "exo_set_multibody_state_host": (c_int32, [c_void_p, c_int32, P(c_double), P(c_double)]),
     "exo_last_error": (ctypes.c_char_p, [c_void_p]),
     "exo_destroy": (None, [c_void_p]),
     "exo_tremor_metrics": (c_int32, [c_void_p, c_void_p, c_void_p, c_double, c_double, c_double, c_int32, c_void_p,

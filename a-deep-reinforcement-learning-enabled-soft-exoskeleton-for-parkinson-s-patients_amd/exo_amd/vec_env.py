@@ -51,7 +51,9 @@ class VecExoskeletonEnv:
 
     observation_dim, action_dim = OBS_DIM, ACT_DIM
 
-    def __init__(self, n_envs, motions=None, seed=0, device=None, **kwargs):
+    PHYSICS = {"ideal": 0, "multibody": 1}
+
+    def __init__(self, n_envs, motions=None, seed=0, device=None, physics="ideal", multibody_params=None, **kwargs):
         self.device = nat.require_gpu(device)
         self.n = int(n_envs)
         unknown = set(kwargs) - set(DEFAULTS)
@@ -97,6 +99,9 @@ class VecExoskeletonEnv:
         self.lengths = torch.as_tensor(self.lengths_host, device=self.device)
         n_axes = self.tremor_sequence.sum(1)
         self.max_reward = n_axes * 0.5 + 0.9 + 0.05 + 0.05 + 0.5  # Exoskeleton_env.py:167-169
+        self.physics = "ideal"
+        if physics != "ideal" or multibody_params is not None:
+            self.set_physics(physics, multibody_params)
 
     # ------------------------------------------------------------------ core
     def _stream(self):
@@ -183,6 +188,57 @@ class VecExoskeletonEnv:
         env), 'auto' (rows for N <= 16384)."""
         nat.check(nat.lib().exo_set_step_variant(self._ctx, self.STEP_VARIANTS[name]), "exo_set_step_variant",
                   self._ctx)
+
+    # ----------------------------------------------------- physics model
+    @staticmethod
+    def multibody_params(**overrides):
+        """Default exo_mb_params (Bullet's defaults, include/exo_amd.h) with overrides."""
+        p = nat.ExoMbParams()
+        nat.lib().exo_multibody_default_params(ctypes.byref(p))
+        for k, val in overrides.items():
+            if not hasattr(p, k):
+                raise TypeError(f"unknown multibody parameter {k!r}")
+            setattr(p, k, val)
+        return p
+
+    def set_physics(self, physics, params=None):
+        """stepSimulation model (Exoskeleton_env.py:433): 'ideal' -- the idealised
+        position motors of SURVEY.md A.2 (default) -- or 'multibody' -- Featherstone
+        dynamics of the 19-joint URDF tree with a joint-space impulse solve of the
+        motors and joint limits (csrc/exo_multibody.hip).  params: a
+        multibody_params() struct or a dict of overrides."""
+        if physics not in self.PHYSICS:
+            raise ValueError(f"physics must be one of {sorted(self.PHYSICS)}")
+        if isinstance(params, dict):
+            params = self.multibody_params(**params)
+        nat.check(nat.lib().exo_set_physics(self._ctx, self.PHYSICS[physics],
+                                            ctypes.byref(params) if params is not None else None),
+                  "exo_set_physics", self._ctx)
+        self.physics = physics
+
+    def multibody_advance(self, targets, mask=None):
+        """One multibody stepSimulation alone: targets float64 [5, N] device (rad)."""
+        t = targets.to(device=self.device, dtype=torch.float64).contiguous()
+        assert t.shape == (5, self.n), t.shape
+        m = None if mask is None else mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        nat.check(nat.lib().exo_multibody_advance(self._ctx, nat.ptr(t), nat.ptr(m), self._stream()),
+                  "exo_multibody_advance", self._ctx)
+
+    def multibody_state(self, env):
+        """(q[19], qd[19]) of one env's URDF joints (pybullet link order)."""
+        q, qd = np.zeros(19), np.zeros(19)
+        dp = lambda a: a.ctypes.data_as(nat.P(ctypes.c_double))  # noqa: E731
+        nat.check(nat.lib().exo_get_multibody_state_host(self._ctx, env, dp(q), dp(qd)),
+                  "exo_get_multibody_state_host", self._ctx)
+        return q, qd
+
+    def set_multibody_state(self, env, q, qd):
+        q = np.ascontiguousarray(q, dtype=np.float64)
+        qd = np.ascontiguousarray(qd, dtype=np.float64)
+        assert q.shape == (19,) and qd.shape == (19,)
+        dp = lambda a: a.ctypes.data_as(nat.P(ctypes.c_double))  # noqa: E731
+        nat.check(nat.lib().exo_set_multibody_state_host(self._ctx, env, dp(q), dp(qd)),
+                  "exo_set_multibody_state_host", self._ctx)
 
     # ------------------------------------------------------- parity / debug
     def reset_from_draws(self, env_ids, draws, obs_out=None):

@@ -119,6 +119,42 @@ int exo_set_state_host(exo_ctx *ctx, int32_t env, const double *in);
 #define EXO_STEP_ROWS 2
 int exo_set_step_variant(exo_ctx *ctx, int32_t variant);
 
+/* ------------------------------------------------------------------------
+ * Physics of stepSimulation (Exoskeleton_env.py:433, Bullet 3.2.5 -- absent
+ * here).  EXO_PHYS_IDEAL (default): the idealised position motors of
+ * SURVEY.md A.2 (each revolute joint moves 10 % of the way to its target,
+ * clamped to the URDF limits; prismatic anchors stay at 0).
+ * EXO_PHYS_MULTIBODY: the btMultiBody pipeline on the 19-joint URDF tree --
+ * Featherstone forward dynamics (gravity, link damping, gyroscopic terms), the
+ * joint motors and violated joint limits as rows of a joint-space projected
+ * Gauss-Seidel impulse solve, semi-implicit Euler (csrc/exo_multibody.hip,
+ * oracle/multibody.c).  The constants are Bullet
+ * defaults from its documentation, not measured against pybullet.
+ * ---------------------------------------------------------------------- */
+#define EXO_PHYS_IDEAL 0
+#define EXO_PHYS_MULTIBODY 1
+typedef struct {
+    double gravity;         /* m/s^2 along -z (setGravity, :116) */
+    double kp, kd;          /* POSITION_CONTROL gains of the revolute motors (sim:115-117 defaults 0.1, 1) */
+    double motor_impulse;   /* max impulse of the revolute motors (force 1e5 x dt) */
+    double passive_impulse; /* max impulse of the prismatic joints' default velocity motors (1) */
+    double limit_impulse;   /* max impulse of a joint-limit row (100) */
+    double erp;             /* limit error reduction (0.2) */
+    double lin_damp, ang_damp; /* btMultiBody link damping (0.04, 0.04) */
+    double max_vel;         /* max joint velocity (100) */
+    int32_t iters;          /* solver sweeps (numSolverIterations, 50) */
+} exo_mb_params;
+void exo_multibody_default_params(exo_mb_params *out);
+/* Select the physics (params NULL = defaults).  Switching to MULTIBODY starts
+ * from the current arm pose at rest with the k-links at 0. */
+int exo_set_physics(exo_ctx *ctx, int32_t mode, const exo_mb_params *params);
+/* One multibody stepSimulation alone for the envs with mask byte != 0 (NULL =
+ * all), POSITION_CONTROL targets targets_dev [5][N] (rad, joints 0..4). */
+int exo_multibody_advance(exo_ctx *ctx, const double *targets_dev, const uint8_t *mask_dev, void *stream);
+/* Joint positions / velocities of the 19 URDF joints (pybullet link order). */
+int exo_get_multibody_state_host(exo_ctx *ctx, int32_t env, double *q19, double *qd19);
+int exo_set_multibody_state_host(exo_ctx *ctx, int32_t env, const double *q19, const double *qd19);
+
 /* Re-key the Philox draw streams of later resets (ExoskeletonEnv_train.seed, :189-191). */
 int exo_set_seed(exo_ctx *ctx, uint64_t seed);
 

@@ -24,6 +24,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "multibody.h"
+
 #define DT (1.0 / 40.0) /* Environment/Exoskeleton_env.py:59 */
 
 /* ------------------------------------------------------------------------ */
@@ -294,6 +296,10 @@ typedef struct {
     double com[NJ * 3];     /* link CoMs cached at the last stepSimulation */
     double max_reward;
     int n_axes;
+    /* stepSimulation model: 0 idealised motors, 1 multibody (multibody.c) */
+    int physics;
+    mb_params mb;
+    double mb_q[NJ], mb_qd[NJ], mb_stats[4];
 } oracle_env;
 
 oracle_env *oracle_env_create(int L, const double *imu, const int *seq, const double *amp, const double *h1,
@@ -310,6 +316,7 @@ oracle_env *oracle_env_create(int L, const double *imu, const int *seq, const do
     e->max_reward = e->n_axes * 0.5 + 0.9 + 0.05 + 0.05 + 0.5;
     double z[5] = {0};
     oracle_link_coms(z, e->com); /* loadURDF at q = 0 (sim:18) */
+    oracle_mb_default_params(&e->mb);
     return e;
 }
 
@@ -487,12 +494,19 @@ int oracle_env_step(oracle_env *e, const double *a, float *obs, double *reward, 
            ey = e->imu[0 * L + c] + qa[3];
     double tgt[5] = {sz * d2r, sy * d2r, sx * d2r, ey * d2r, e->imu[1 * L + c] * d2r};
     if (targets_out) memcpy(targets_out, tgt, sizeof tgt);
-    /* stepSimulation: idealised position motors, limits clamp */
-    for (int j = 0; j < 5; ++j) {
-        double q = e->phys_q[j] + 0.1 * (tgt[j] - e->phys_q[j]);
-        e->phys_q[j] = fmin(fmax(q, J_LO[j]), J_HI[j]);
+    if (e->physics == 1) {
+        /* stepSimulation: multibody dynamics + joint-space impulse solve (multibody.c) */
+        if (oracle_mb_step(e->mb_q, e->mb_qd, tgt, &e->mb, e->mb_stats)) return -3;
+        for (int j = 0; j < 5; ++j) e->phys_q[j] = e->mb_q[j];
+        oracle_mb_link_coms(e->mb_q, e->com);
+    } else {
+        /* stepSimulation: idealised position motors, limits clamp */
+        for (int j = 0; j < 5; ++j) {
+            double q = e->phys_q[j] + 0.1 * (tgt[j] - e->phys_q[j]);
+            e->phys_q[j] = fmin(fmax(q, J_LO[j]), J_HI[j]);
+        }
+        oracle_link_coms(e->phys_q, e->com);
     }
-    oracle_link_coms(e->phys_q, e->com);
     /* get_reward :341-366 */
     const double eps = 1e-10;
     double M = e->maxE + e->maxS;
@@ -540,6 +554,22 @@ void oracle_env_episode(const oracle_env *e, double *I, double *D, double *S, do
 }
 void oracle_env_phys(const oracle_env *e, double *q5) { memcpy(q5, e->phys_q, sizeof e->phys_q); }
 int oracle_env_counts(const oracle_env *e) { return e->counts; }
+/* multibody mode: select it (with optional parameters) and read / write the 19-joint state */
+void oracle_env_set_physics(oracle_env *e, int mode, const mb_params *p) {
+    e->physics = mode;
+    if (p) e->mb = *p;
+}
+void oracle_env_mb_state(const oracle_env *e, double *q19, double *qd19, double *stats4) {
+    if (q19) memcpy(q19, e->mb_q, sizeof e->mb_q);
+    if (qd19) memcpy(qd19, e->mb_qd, sizeof e->mb_qd);
+    if (stats4) memcpy(stats4, e->mb_stats, sizeof e->mb_stats);
+}
+void oracle_env_set_mb_state(oracle_env *e, const double *q19, const double *qd19) {
+    memcpy(e->mb_q, q19, sizeof e->mb_q);
+    memcpy(e->mb_qd, qd19, sizeof e->mb_qd);
+    for (int j = 0; j < 5; ++j) e->phys_q[j] = q19[j];
+    oracle_mb_link_coms(e->mb_q, e->com);
+}
 
 /* ------------------------------------------------------------------------ */
 /* CPU baseline driver: n_envs envs stepped sequentially on one core with     */

@@ -18,6 +18,13 @@ _f = ctypes.POINTER(ctypes.c_float)
 _i = ctypes.POINTER(ctypes.c_int)
 
 
+class MBParams(ctypes.Structure):
+    """mb_params of multibody.h (Bullet-equivalent step constants)."""
+    _fields_ = [(n, ctypes.c_double) for n in ("dt", "gravity", "kp", "kd", "motor_impulse", "passive_impulse",
+                                               "limit_impulse", "erp", "lin_damp", "ang_damp", "max_vel")] + \
+               [("iters", ctypes.c_int)]
+
+
 def build():
     subprocess.run(["make", "-s", "-C", HERE], check=True)
 
@@ -40,6 +47,15 @@ def lib():
         L.oracle_env_episode.argtypes = [ctypes.c_void_p, _d, _d, _d, _d, _d]
         L.oracle_env_phys.argtypes = [ctypes.c_void_p, _d]
         L.oracle_env_counts.argtypes = [ctypes.c_void_p]
+        L.oracle_env_set_physics.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(MBParams)]
+        L.oracle_env_mb_state.argtypes = [ctypes.c_void_p, _d, _d, _d]
+        L.oracle_env_set_mb_state.argtypes = [ctypes.c_void_p, _d, _d]
+        L.oracle_mb_default_params.argtypes = [ctypes.POINTER(MBParams)]
+        L.oracle_mb_aba.argtypes = [_d, _d, _d, ctypes.POINTER(MBParams), _d]
+        L.oracle_mb_rnea.argtypes = [_d, _d, _d, ctypes.POINTER(MBParams), _d]
+        L.oracle_mb_mass.argtypes = [_d, _d]
+        L.oracle_mb_link_coms.argtypes = [_d, _d]
+        L.oracle_mb_step.argtypes = [_d, _d, _d, ctypes.POINTER(MBParams), _d]
         L.oracle_bench.restype = ctypes.c_long
         L.oracle_bench.argtypes = [ctypes.c_int, _d, _i, ctypes.c_int, ctypes.c_long, ctypes.c_uint64]
         _lib = L
@@ -65,6 +81,62 @@ def link_coms(q5):
     out = np.zeros((19, 3))
     lib().oracle_link_coms(_p(q5), _p(out))
     return out
+
+
+# ---------------------------------------------------------------- multibody
+def mb_params(**overrides):
+    p = MBParams()
+    lib().oracle_mb_default_params(ctypes.byref(p))
+    for k, v in overrides.items():
+        setattr(p, k, v)
+    return p
+
+
+def _vec(x, n=19):
+    a = np.ascontiguousarray(x, dtype=np.float64)
+    assert a.shape == (n,), a.shape
+    return a
+
+
+def mb_aba(q, qd, tau=None, params=None):
+    """Articulated-Body Algorithm: joint accelerations (19)."""
+    p = params or mb_params()
+    out = np.zeros(19)
+    t = None if tau is None else _p(_vec(tau))
+    lib().oracle_mb_aba(_p(_vec(q)), _p(_vec(qd)), t, ctypes.byref(p), _p(out))
+    return out
+
+
+def mb_rnea(q, qd, qdd, params=None):
+    """Recursive Newton-Euler: joint forces (19)."""
+    p = params or mb_params()
+    out = np.zeros(19)
+    lib().oracle_mb_rnea(_p(_vec(q)), _p(_vec(qd)), _p(_vec(qdd)), ctypes.byref(p), _p(out))
+    return out
+
+
+def mb_mass(q):
+    """Composite-Rigid-Body Algorithm: joint-space inertia (19 x 19)."""
+    out = np.zeros((19, 19))
+    lib().oracle_mb_mass(_p(_vec(q)), _p(out))
+    return out
+
+
+def mb_link_coms(q):
+    out = np.zeros((19, 3))
+    lib().oracle_mb_link_coms(_p(_vec(q)), _p(out))
+    return out
+
+
+def mb_step(q, qd, targets, params=None):
+    """One multibody stepSimulation: returns (q', qd', stats[4])."""
+    p = params or mb_params()
+    q, qd = _vec(q).copy(), _vec(qd).copy()
+    st = np.zeros(4)
+    rc = lib().oracle_mb_step(_p(q), _p(qd), _p(_vec(targets, 5)), ctypes.byref(p), _p(st))
+    if rc:
+        raise RuntimeError("singular joint-space inertia")
+    return q, qd, st
 
 
 class OracleEnv:
@@ -115,6 +187,19 @@ class OracleEnv:
         q = np.zeros(5)
         lib().oracle_env_phys(self.h, _p(q))
         return q
+
+    def set_physics(self, mode, params=None):
+        """mode 'ideal'  or 'multibody' (multibody.c)."""
+        m = {"ideal": 0, "multibody": 1}[mode]
+        lib().oracle_env_set_physics(self.h, m, ctypes.byref(params) if params is not None else None)
+
+    def mb_state(self):
+        q, qd, st = np.zeros(19), np.zeros(19), np.zeros(4)
+        lib().oracle_env_mb_state(self.h, _p(q), _p(qd), _p(st))
+        return q, qd, st
+
+    def set_mb_state(self, q, qd):
+        lib().oracle_env_set_mb_state(self.h, _p(_vec(q)), _p(_vec(qd)))
 
     @property
     def counts(self):

@@ -1,0 +1,137 @@
+"""GPU parity of the multibody stepSimulation (csrc/exo_multibody.hip) against
+the CPU oracle (oracle/multibody.c).  SURVEY.md 8(f) row 2.
+
+The kernel and the oracle compute the same model in fp64 with different
+factorisations (kernel: Composite-Rigid-Body M, Newton-Euler bias and the
+Schur complement of the arrow-shaped M; oracle: Articulated-Body Algorithm and
+a dense Gauss-Jordan inverse of M), so they agree to rounding: joint positions
+to 1e-9 rad (m), velocities to 1e-7 rad/s, observations to the float32 tolerance
+of tests/test_env_gpu.py.  Bullet parity is unpinned (tests/test_multibody_oracle.py).
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from helpers import env_kwargs, episode_steps, golden_env
+
+pytestmark = pytest.mark.gpu
+
+LO = np.array([-1.3962633609772, -0.69813168048859, -2.6441738605499, -0.034906584769487, -1.5184364318848])
+HI = np.array([1.3962633609772, 2.8187066316605, 0.78539800643921, 2.6179938726127, 1.3962633609772])
+
+
+def _states(n, seed):
+    rng = np.random.default_rng(seed)
+    q = np.zeros((n, 19))
+    qd = rng.uniform(-2.0, 2.0, (n, 19))
+    q[:, :5] = rng.uniform(LO, HI)
+    q[:, 5:] = rng.uniform(-0.05, 0.05, (n, 14))
+    # a few envs beyond a joint limit (limit rows) and with saturating targets
+    for i in range(0, n, 5):
+        j = i % 5
+        q[i, j] = HI[j] + 0.05 if i % 2 else LO[j] - 0.05
+    for i in range(2, n, 7):
+        q[i, 5 + i % 14] = 0.55 if i % 2 else -0.55
+    tgt = q[:, :5] + rng.uniform(-0.5, 0.5, (n, 5))
+    return q, qd, tgt
+
+
+@pytest.mark.parametrize("params", [{}, {"iters": 7, "lin_damp": 0.3, "ang_damp": 0.1},
+                                    {"motor_impulse": 0.05, "passive_impulse": 0.02}])
+def test_advance_matches_oracle_on_random_states(params):
+    from exo_amd import VecExoskeletonEnv
+    n = 40
+    env = VecExoskeletonEnv(n, seed=11, physics="multibody", multibody_params=params or None)
+    q, qd, tgt = _states(n, 3)
+    for i in range(n):
+        env.set_multibody_state(i, q[i], qd[i])
+    mask = torch.ones(n, dtype=torch.uint8, device=env.device)
+    mask[3] = 0  # an idle env keeps its state
+    env.multibody_advance(torch.as_tensor(tgt.T.copy(), device=env.device), mask=mask)
+    torch.cuda.synchronize()
+    p = O.mb_params(**params)
+    for i in range(n):
+        gq, gqd = env.multibody_state(i)
+        if i == 3:
+            np.testing.assert_array_equal(gq, q[i])
+            np.testing.assert_array_equal(gqd, qd[i])
+            continue
+        oq, oqd, _ = O.mb_step(q[i], qd[i], tgt[i], p)
+        np.testing.assert_allclose(gq, oq, rtol=0, atol=1e-9, err_msg=f"env {i}")
+        np.testing.assert_allclose(gqd, oqd, rtol=1e-8, atol=1e-7, err_msg=f"env {i}")
+        np.testing.assert_allclose(env.get_state(i)[1:6], oq[:5], rtol=0, atol=1e-9)
+
+
+@pytest.mark.parametrize("variant", ["rows", "lanes"])
+def test_env_episodes_match_oracle_in_multibody_mode(variant):
+    """The 8 reference motions with their golden draws and actions, stepped with
+    the multibody physics on the GPU and in the oracle."""
+    from exo_amd import VecExoskeletonEnv
+    from exo_amd import motions
+    gold = [golden_env(m) for m in range(8)]
+    per = [env_kwargs(d) for d in gold]
+    kw = {k: np.stack([np.asarray(p[k], dtype=np.float64) for p in per]) for k in per[0]}
+    env = VecExoskeletonEnv(8, motions=list(range(8)), seed=5, **kw)
+    env.set_step_variant(variant)
+    for m in range(8):  # fresh-load link cache, as tests/test_env_gpu.py
+        st = env.get_state(m)
+        st[6:12] = 0.0
+        st[49] = 0
+        env.set_state(m, st)
+    env.set_physics("multibody")
+    angles, _ = motions.load()
+    orc = []
+    for m, d in enumerate(gold):
+        L = int(d["L"])
+        e = O.OracleEnv(angles[m][:, :L], d["tremor_seq"], d["amp_range"], d["harm1"], d["harm2"], d["max_force"][0],
+                        d["max_force"][1], d["dr"][0], d["dr"][1], d["dr"][2])
+        e.set_physics("multibody")
+        e.reset(d["ep0_draws"])
+        orc.append(e)
+    env.reset_from_draws(list(range(8)), [d["ep0_draws"] for d in gold])
+    out = env.new_outputs(True)
+    for ep in (1,):
+        obs0 = env.reset_from_draws(list(range(8)), [d[f"ep{ep}_draws"] for d in gold]).cpu().numpy()
+        for m in range(8):
+            np.testing.assert_allclose(obs0[m], orc[m].reset(gold[m][f"ep{ep}_draws"]), rtol=2e-6, atol=2e-6)
+        idx = [episode_steps(d, ep) for d in gold]
+        for k in range(max(i.size for i in idx)):
+            act = np.zeros((8, 7), dtype=np.float32)
+            active = np.array([k < idx[m].size for m in range(8)])
+            for m in np.nonzero(active)[0]:
+                act[m] = gold[m]["step_action"][idx[m][k]]
+            obs, rew, done, info = env.step(torch.as_tensor(act, device=env.device),
+                                            active=torch.as_tensor(active, device=env.device), out=out)
+            obs, rew = obs.cpu().numpy(), rew.cpu().numpy()
+            for m in np.nonzero(active)[0]:
+                o_obs, o_r, o_done, o_info, _ = orc[m].step(act[m].astype(np.float64))
+                np.testing.assert_allclose(obs[m], o_obs, rtol=2e-6, atol=2e-6, err_msg=f"motion {m} step {k}")
+                np.testing.assert_allclose(rew[m], o_r, rtol=2e-6, atol=1e-7)
+                if k % 23 == 0 or k == idx[m].size - 1:
+                    gq, gqd = env.multibody_state(int(m))
+                    oq, oqd, _ = orc[m].mb_state()
+                    np.testing.assert_allclose(gq, oq, rtol=0, atol=1e-9, err_msg=f"motion {m} step {k}")
+                    np.testing.assert_allclose(gqd, oqd, rtol=1e-7, atol=1e-7, err_msg=f"motion {m} step {k}")
+
+
+def test_switching_physics_keeps_the_pose_and_ideal_mode_is_unchanged():
+    from exo_amd import VecExoskeletonEnv
+    n = 16
+    a = VecExoskeletonEnv(n, seed=21)
+    b = VecExoskeletonEnv(n, seed=21)
+    a.reset()
+    b.reset()
+    act = torch.rand((n, 7), device=a.device) * 2 - 1
+    for _ in range(5):
+        a.step(act)
+        b.step(act)
+    b.set_physics("multibody")
+    for i in range(n):
+        q, qd = b.multibody_state(i)
+        np.testing.assert_array_equal(q[:5], a.get_state(i)[1:6])
+        assert not q[5:].any() and not qd.any()
+    b.set_physics("ideal")
+    oa = a.step(act)[0].cpu().numpy()
+    ob = b.step(act)[0].cpu().numpy()
+    np.testing.assert_array_equal(oa, ob)
