@@ -100,6 +100,8 @@ def parse():
     ap.add_argument("--envs", type=int, default=None, help="envs per GPU (workload default: 4096 / 16384 / 65536)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="configs1")
     ap.add_argument("--mode", choices=["train", "env"], default="train")
+    ap.add_argument("--physics", choices=["ideal", "multibody"], default="ideal",
+                    help="stepSimulation model: idealised motors (default, SURVEY.md A.2) or the multibody solve")
     ap.add_argument("--precision", choices=["bf16", "fp16", "fp32"], default=None,
                     help="TD7 MFMA operands (workload default: bf16 per configs[1], fp16 for wide)")
     ap.add_argument("--batch", type=int, default=None, help="TD7 rows per stratum (default 128)")
@@ -228,7 +230,7 @@ def main():
         rng = np.random.default_rng(1000 + rank)
         env_kw = dict(matrix_noise_fraction=rng.uniform(0.05, 0.25, N), dr_actuator_range=rng.uniform(0.0, 0.1, N),
                       dr_actuator_end_pos_shift=rng.uniform(0.0, 0.04, N), tremor_amplitude_range=(0.1, 1.0))
-    env = VecExoskeletonEnv(N, seed=1000 + rank, device=dev, **env_kw)
+    env = VecExoskeletonEnv(N, seed=1000 + rank, device=dev, physics=args.physics, **env_kw)
     Ls = env.lengths_host
     round_len = int(Ls.max()) - 3
     active_per_k = np.array([(Ls - 3 > k).sum() for k in range(round_len)])
@@ -266,6 +268,19 @@ def main():
             ev.append((e0, e1))
         state["k"] = k + 1
         return int(active_per_k[k])
+
+    def multibody_timing(n=50):
+        """exo_multibody_kernel alone (multibody physics): HIP events around
+        exo_multibody_advance launches over all envs, on the launch stream."""
+        tgt = torch.zeros((5, N), dtype=torch.float64, device=dev)
+        env.multibody_advance(tgt)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(n):
+            env.multibody_advance(tgt)
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / n
 
     def kernel_timing(n):
         """exo_step_kernel alone, HIP events on the launch stream, all envs active."""
@@ -339,15 +354,23 @@ def main():
                     + ("random actions" if agent is None else (f"random-init TD7 (widths {agent.hp.zs_dim}/{agent.hp.critic_hdim})")),
             "config": {"workload": WORKLOADS[args.workload]
                                    + (f", TD7 batch 8x{agent.hp.batch_size}" if agent else ", env only"),
-                       "envs_per_gpu": N, "mode": args.mode, "parallelism": f"env-shard x{world}"
+                       "envs_per_gpu": N, "mode": args.mode, "physics": args.physics,
+                       "parallelism": f"env-shard x{world}"
                        + (" + TD7 DP all-reduce" if agent and world > 1 else "")},
-            "roofline": {"kernel": "exo_step_rp_kernel" if N <= 16384 else "exo_step_kernel", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+            "roofline": {"kernel": ("exo_step_rp_kernel" if N <= 16384 else "exo_step_kernel")
+                                   + (" + exo_multibody_kernel" if args.physics == "multibody" else ""), "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_unit": "bytes per launch", "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": BYTES_PER_ENV_STEP * active_avg,
                          "bytes_per_env_step": BYTES_PER_ENV_STEP, "avg_kernel_ms": kern_ms,
                          "active_envs_per_launch": active_avg},
         }
+        if args.physics == "multibody":
+            # q, qd of 19 joints read + written (f64), 5 targets, 1 flag byte read + cleared
+            mb_ms = multibody_timing()
+            res["multibody_kernel"] = {"kernel": "exo_multibody_kernel", "avg_kernel_ms": mb_ms,
+                                       "bytes_per_env_step": 19 * 8 * 4 + 5 * 8 + 2, "envs_per_launch": N,
+                                       "note": "included in ms_per_step; the roofline object above is the step kernel"}
         if agent is not None:
             res["grad_steps_per_sec"] = args.steps / elapsed
             # TD7 on the fp32 MFMA roofline: the update's GEMM flops
