@@ -363,6 +363,7 @@ class TD7Learner:
         self.critic_target = copy.deepcopy(self.critic)
         self.fixed_encoder = copy.deepcopy(self.encoder)
         self.fixed_encoder_target = copy.deepcopy(self.encoder)
+        self.pair_fixed_encoders()
         self.checkpoint_actor = copy.deepcopy(self.actor)
         self.checkpoint_encoder = copy.deepcopy(self.encoder)
         self.offline = offline
@@ -380,6 +381,49 @@ class TD7Learner:
         self.policy_noise_decrease = hp.target_policy_noise / learning_steps
         self.action_noise_decrease = hp.exploration_noise / learning_steps
         self.exploration_noise_t = torch.tensor(float(hp.exploration_noise), **f32)
+
+    ENC_LAYERS = ("zs1", "zs2", "zs3", "zsa1", "zsa2", "zsa3")
+
+    def pair_fixed_encoders(self):
+        """Store the fixed encoder's and the fixed target encoder's weights as
+        one stacked [2, out, in] tensor per layer (the two modules' parameters
+        become views of slices 0 / 1, so loads, target refreshes and
+        checkpoints are unchanged).  Their passes in the critic update -- zs of
+        the state (fixed) and of the next state (target), then zsa -- are
+        independent and equal in shape, so on the GPU each layer of both runs
+        as ONE grouped td7_dense launch (Agent/TD7_multi_agent.py:236-251)."""
+        self._pair = {}
+        with torch.no_grad():
+            for name in self.ENC_LAYERS:
+                fa, fb = getattr(self.fixed_encoder, name), getattr(self.fixed_encoder_target, name)
+                W = torch.stack([fa.weight.data, fb.weight.data])
+                B = torch.stack([fa.bias.data, fb.bias.data])
+                fa.weight.data, fb.weight.data = W[0], W[1]
+                fa.bias.data, fb.bias.data = B[0], B[1]
+                self._pair[name] = (W, B)
+
+    def _paired(self):
+        return (self.device.type == "cuda" and getattr(self, "_pair", None) is not None
+                and ops.act_code(self.fixed_encoder.activ) is not None
+                and self._pair["zs1"][0].data_ptr() == self.fixed_encoder.zs1.weight.data_ptr())
+
+    def _pair_dense(self, x, name, act):
+        W, B = self._pair[name]
+        return ops.dense(x, W, B, act)
+
+    def _pair_zs(self, state, next_state):
+        """[fixed_encoder.zs(state), fixed_encoder_target.zs(next_state)] as [2, B, zs_dim]."""
+        act = ops.act_code(self.fixed_encoder.activ)
+        x = torch.stack([state, next_state])
+        x = self._pair_dense(x, "zs1", act)
+        x = self._pair_dense(x, "zs2", act)
+        return AvgL1Norm(self._pair_dense(x, "zs3", 0))
+
+    def _pair_zsa(self, zs2, actions2):
+        act = ops.act_code(self.fixed_encoder.activ)
+        x = self._pair_dense(torch.cat([zs2, actions2], 2), "zsa1", act)
+        x = self._pair_dense(x, "zsa2", act)
+        return self._pair_dense(x, "zsa3", 0)
 
     @property
     def exploration_noise(self):
@@ -415,22 +459,32 @@ class TD7Learner:
         # ---- critic (:233-257)
         with torch.no_grad():
             with self._autocast():
-                fixed_target_zs = self.fixed_encoder_target.zs(next_state)
+                paired = self._paired()
+                if paired:  # fixed (state) and fixed target (next state) encoders, one launch per layer
+                    zs2 = self._pair_zs(state, next_state)
+                    fixed_zs, fixed_target_zs = zs2[0], zs2[1]
+                else:
+                    fixed_target_zs = self.fixed_encoder_target.zs(next_state)
                 if noise is None:
                     noise = torch.randn_like(action)
                 # (noise * sigma).clamp(+-noise_clip); sigma -= decrease; (a + noise).clamp(-1, 1)
                 next_action = ops.noisy_action(self.actor_target(next_state, fixed_target_zs).float(), noise,
                                                self.target_policy_noise, self.policy_noise_decrease,
                                                clip=hp.noise_clip)
-                fixed_target_zsa = self.fixed_encoder_target.zsa(fixed_target_zs, next_action)
+                if paired:
+                    zsa2 = self._pair_zsa(zs2, torch.stack([action, next_action]))
+                    fixed_zsa, fixed_target_zsa = zsa2[0], zsa2[1]
+                else:
+                    fixed_target_zsa = self.fixed_encoder_target.zsa(fixed_target_zs, next_action)
                 Q_heads = self.critic_target(next_state, next_action, fixed_target_zsa, fixed_target_zs).float()
             # Q_target and the running bounds (:240-246; bounds kept per rank,
             # MAX-reduced when the targets refresh): one td7_q_target launch
             Q_target = ops.q_target(Q_heads, reward, not_done, hp.discount, self.min_target, self.max_target,
                                     self.max, self.min)
-            with self._autocast():
-                fixed_zs = self.fixed_encoder.zs(state)
-                fixed_zsa = self.fixed_encoder.zsa(fixed_zs, action)
+            if not paired:
+                with self._autocast():
+                    fixed_zs = self.fixed_encoder.zs(state)
+                    fixed_zsa = self.fixed_encoder.zsa(fixed_zs, action)
         with self._autocast():
             Q = self.critic(state, action, fixed_zsa, fixed_zs)
         # LAP_huber critic loss and the new priorities (:257-262): one
@@ -708,6 +762,7 @@ class Agent:
         L.actor_target = copy.deepcopy(L.actor)
         L.fixed_encoder = copy.deepcopy(L.encoder)
         L.fixed_encoder_target = copy.deepcopy(L.encoder)
+        L.pair_fixed_encoders()
         L.checkpoint_actor.load_state_dict(ld("_checkpoint_actor"))
         L.checkpoint_encoder.load_state_dict(ld("_checkpoint_encoder"))
 

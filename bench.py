@@ -132,11 +132,41 @@ def pmc_traffic(bytes_per_launch):
     return None, None
 
 
-def cpu_baseline(seconds, threads=None):
+def cpu_td7_update_seconds(hp, batch_rows, threads, budget=6.0):
+    """Seconds per TD7 update on the host cores: the build's TD7Learner (the
+    reference's update math, Agent/TD7_multi_agent.py:211-293) on torch-CPU
+    fp32 with `threads` intra-op threads, a bounded sample of updates on a
+    synthetic batch of the bench's size."""
+    from exo_amd.td7 import TD7Learner
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        torch.manual_seed(0)
+        L = TD7Learner(80, 7, hp, device="cpu", fused_adam=False)
+        g = torch.Generator().manual_seed(0)
+        s = torch.randn(batch_rows, 80, generator=g)
+        a = torch.rand(batch_rows, 7, generator=g) * 2 - 1
+        ns = torch.randn(batch_rows, 80, generator=g)
+        r = torch.rand(batch_rows, 1, generator=g)
+        nd = torch.ones(batch_rows, 1)
+        L.update(s, a, ns, r, nd)  # warm
+        n, t0 = 0, time.perf_counter()
+        while n < 2 or (time.perf_counter() - t0 < budget and n < 50):
+            L.update(s, a, ns, r, nd)
+            n += 1
+        return (time.perf_counter() - t0) / n, n
+    finally:
+        torch.set_num_threads(prev)
+
+
+def cpu_baseline(seconds, threads=None, td7=None):
     """The oracle (plain C, fp64) stepping 8 envs each, one per motion, with
     random actions -- the 'port' CPU baseline: one core for ~1/3 of the
     budget, then one stepping loop per host core (ctypes drops the GIL) for
-    the rest.  `value` is the all-core rate."""
+    the rest.  With td7=(hp, batch_rows, env_steps_per_iteration) the same
+    training loop as the GPU bench is priced on the host: per iteration the
+    env-steps at the all-core env rate plus one TD7 update on all cores, and
+    `value` is that loop's env-steps/s; otherwise `value` is the env rate."""
     import threading
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
@@ -166,11 +196,22 @@ def cpu_baseline(seconds, threads=None):
         t.join()
     dt = time.perf_counter() - t0
     steps = sum(r[0] for r in res)
-    return {"value": steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "single_core_value": s1 / d1,
-            "sample": f"oracle/exo_oracle.c env.step (fp64, the reference's algorithm incl. scipy-RK45 control), "
-                      f"8 envs (one per motion) per thread, random actions, episode-synchronous resets: "
-                      f"{steps} env-steps in {dt:.1f} s on {threads} threads; 1 core: {s1} in {d1:.1f} s"}
+    env_rate = steps / dt
+    out = {"value": env_rate, "unit": "env-steps/s", "cores": threads, "kind": "port",
+           "env_only_value": env_rate, "single_core_value": s1 / d1,
+           "sample": f"oracle/exo_oracle.c env.step (fp64, the reference's algorithm incl. scipy-RK45 control), "
+                     f"8 envs (one per motion) per thread, random actions, episode-synchronous resets: "
+                     f"{steps} env-steps in {dt:.1f} s on {threads} threads; 1 core: {s1} in {d1:.1f} s"}
+    if td7 is not None:
+        hp, rows, per_it = td7
+        upd, n = cpu_td7_update_seconds(hp, rows, threads)
+        it_s = per_it / env_rate + upd
+        out["value"] = per_it / it_s
+        out["td7_update_ms"] = upd * 1e3
+        out["sample"] += (f"; + TD7 update (build's TD7Learner, torch-CPU fp32, {threads} threads, batch {rows}): "
+                          f"{upd * 1e3:.1f} ms per update over {n} updates; value = the bench loop priced on the "
+                          f"host: {per_it:.0f} active env-steps + 1 update per iteration")
+    return out
 
 
 def critic_gemm_timing(agent, reps=20, replays=10):
@@ -357,6 +398,7 @@ def main():
                        "envs_per_gpu": N, "mode": args.mode, "physics": args.physics,
                        "parallelism": f"env-shard x{world}"
                        + (" + TD7 DP all-reduce" if agent and world > 1 else "")},
+            "env_kernel_env_steps_per_sec": active_avg / (kern_ms * 1e-3),
             "roofline": {"kernel": ("exo_step_rp_kernel" if N <= 16384 else "exo_step_kernel")
                                    + (" + exo_multibody_kernel" if args.physics == "multibody" else ""), "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -400,7 +442,10 @@ def main():
             if not dp_sync:
                 res["dp_weight_checksums"] = dp_ck
         if not args.no_cpu_baseline and world == 1:
-            res["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, args.cpu_threads)
+            td7 = None
+            if agent is not None:
+                td7 = (agent.hp, agent.hp.batch_size * agent.env_num, total_env_steps / args.steps)
+            res["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, args.cpu_threads, td7)
         print(json.dumps(res))
     if world > 1:
         dist.destroy_process_group()
