@@ -19,6 +19,7 @@ CPU parity tests run it against the reference's golden train() steps); Agent
 adds the replay buffer, the checkpoint policy and data parallelism.
 """
 import copy
+import os
 from dataclasses import dataclass, field
 from typing import Callable
 
@@ -443,9 +444,21 @@ class TD7Learner:
     # sees fixed_encoder / fixed_encoder_target, :233-251), so both are
     # computed before either optimiser steps -- the same arithmetic as the
     # reference's encoder-then-critic order.
-    def phase_grads(self, state, action, next_state, reward, not_done, noise=None):
-        hp = self.hp
-        # ---- encoder (:219-228)
+    # The encoder's loss and gradients (:219-228) depend on nothing the critic
+    # computes and the critic never reads the live encoder (only the fixed
+    # encoders), so on the GPU they run on a side stream -- a parallel branch
+    # of the captured iteration graph -- concurrently with the critic's
+    # target / fixed-embedding passes and its loss and gradients; the branch
+    # joins before the optimiser steps (and the data-parallel all-reduce).
+    # The small GEMMs of each branch fill a fraction of the 256 CUs, so the
+    # two overlap: 0.965 vs 1.095 ms per bench iteration
+    # (profiles/r01b_raw/overlap_ab.txt; also measured there and not kept:
+    # the encoder's Adam step on the branch -- no gain -- and LAP.update_priority
+    # on a third branch -- slower).  EXO_TD7_OVERLAP=0 serialises.
+    overlap = os.environ.get("EXO_TD7_OVERLAP", "1") == "1"
+
+    def _encoder_grads(self, state, action, next_state):
+        """:219-228 -- loss and gradients of the live encoder."""
         with self._autocast():
             # zs(state) and zs(next_state) of the live encoder as one pass; the
             # next-state half is detached (it is computed under no_grad at :220)
@@ -456,6 +469,21 @@ class TD7Learner:
         encoder_loss = ops.mse_loss(pred_zs.float(), next_zs.float())
         self.encoder_optimizer.zero_grad(set_to_none=self.grads_to_none)
         encoder_loss.backward()
+
+    def phase_grads(self, state, action, next_state, reward, not_done, noise=None):
+        hp = self.hp
+        # ---- encoder (:219-228)
+        side = None
+        if self.overlap and self.device.type == "cuda":
+            cur = torch.cuda.current_stream(self.device)
+            if getattr(self, "_side", None) is None:
+                self._side = torch.cuda.Stream(device=self.device)
+            side = self._side
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                self._encoder_grads(state, action, next_state)
+        else:
+            self._encoder_grads(state, action, next_state)
         # ---- critic (:233-257)
         with torch.no_grad():
             with self._autocast():
@@ -492,8 +520,16 @@ class TD7Learner:
         critic_loss, priority = ops.critic_loss(Q.float(), Q_target, hp.alpha, hp.min_priority)
         self.critic_optimizer.zero_grad(set_to_none=self.grads_to_none)
         critic_loss.backward()
+        if side is not None:
+            self.join_side()
         self._fixed_zs = fixed_zs
         return priority
+
+    def join_side(self):
+        """Order the current stream after the encoder branch (end of an update)."""
+        side = getattr(self, "_side", None)
+        if side is not None and self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).wait_stream(side)
 
     def phase_steps(self, flat_grad=None, grad_scale=1.0):
         """Encoder and critic optimiser steps; flat_grad: their gradients packed
