@@ -16,6 +16,8 @@ so it is captured once into HIP graphs and replayed:
 Host-side bookkeeping left outside the graphs: the env reset at the end of a
 round, the target-network refresh every 250 steps (:284-293).
 """
+import os
+
 import numpy as np
 import torch
 
@@ -90,11 +92,36 @@ class VecTrainer:
         self.obs.copy_(nobs)
         self.last_actions = act
 
+    # The update samples its batch BEFORE this iteration's transitions are
+    # stored (from iteration 1 on), which frees the rollout (batched actor
+    # inference -> exo_step -> replay insert) to run on a side stream -- a
+    # parallel branch of the captured graph -- concurrently with the TD7
+    # gradients.  The branch joins before the priority update and the
+    # optimiser steps, so the replay insert still precedes update_priority and
+    # select_action still reads the weights of the previous update, as in the
+    # serial order; the only change is the one-step lag between a transition's
+    # insert and its first chance to be sampled (the reference trains in
+    # bursts after each episode round anyway, Exoskeleton_agent_train.py:208).
+    # EXO_ROLLOUT_OVERLAP=0 keeps the serial insert-then-sample order.
+    overlap_rollout = os.environ.get("EXO_ROLLOUT_OVERLAP", "1") == "1"
+
     def _pre(self):
-        self._rollout()
         ag = self.agent
+        if self.iters == 0 or not self.overlap_rollout:
+            self._rollout()
+            self._batch = ag.replay_buffer.sample()
+            self._prio = ag.learner.phase_grads(*self._batch)
+            return
         self._batch = ag.replay_buffer.sample()
+        cur = torch.cuda.current_stream(self.device)
+        if getattr(self, "_rollout_stream", None) is None:
+            self._rollout_stream = torch.cuda.Stream(device=self.device)
+        br = self._rollout_stream
+        br.wait_stream(cur)
+        with torch.cuda.stream(br):
+            self._rollout()
         self._prio = ag.learner.phase_grads(*self._batch)
+        cur.wait_stream(br)
 
     def _mid(self, update_actor, flat_grad=None, grad_scale=1.0):
         ag = self.agent
