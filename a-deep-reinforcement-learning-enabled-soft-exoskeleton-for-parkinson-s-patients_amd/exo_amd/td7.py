@@ -485,6 +485,9 @@ class TD7Learner:
         else:
             self._encoder_grads(state, action, next_state)
         # ---- critic (:233-257)
+        if noise is None:
+            noise = torch.randn_like(action)
+        split = side is not None and os.environ.get("EXO_TD7_TARGET_BRANCH", "1") == "1"
         with torch.no_grad():
             with self._autocast():
                 paired = self._paired()
@@ -493,28 +496,33 @@ class TD7Learner:
                     fixed_zs, fixed_target_zs = zs2[0], zs2[1]
                 else:
                     fixed_target_zs = self.fixed_encoder_target.zs(next_state)
-                if noise is None:
-                    noise = torch.randn_like(action)
-                # (noise * sigma).clamp(+-noise_clip); sigma -= decrease; (a + noise).clamp(-1, 1)
-                next_action = ops.noisy_action(self.actor_target(next_state, fixed_target_zs).float(), noise,
-                                               self.target_policy_noise, self.policy_noise_decrease,
-                                               clip=hp.noise_clip)
-                if paired:
-                    zsa2 = self._pair_zsa(zs2, torch.stack([action, next_action]))
-                    fixed_zsa, fixed_target_zsa = zsa2[0], zsa2[1]
-                else:
-                    fixed_target_zsa = self.fixed_encoder_target.zsa(fixed_target_zs, next_action)
-                Q_heads = self.critic_target(next_state, next_action, fixed_target_zsa, fixed_target_zs).float()
-            # Q_target and the running bounds (:240-246; bounds kept per rank,
-            # MAX-reduced when the targets refresh): one td7_q_target launch
-            Q_target = ops.q_target(Q_heads, reward, not_done, hp.discount, self.min_target, self.max_target,
-                                    self.max, self.min)
-            if not paired:
-                with self._autocast():
                     fixed_zs = self.fixed_encoder.zs(state)
+        if split:
+            # the target chain (actor_target -> zsa -> critic_target -> Q_target,
+            # :236-246) as a third branch, concurrent with the online critic's
+            # forward on the current stream; they meet at the loss
+            cur = torch.cuda.current_stream(self.device)
+            if getattr(self, "_tside", None) is None:
+                self._tside = torch.cuda.Stream(device=self.device)
+            self._tside.wait_stream(cur)
+            with torch.cuda.stream(self._tside):
+                Q_target = self._target_chain(next_state, reward, not_done, noise, fixed_target_zs, None)
+            with torch.no_grad(), self._autocast():
+                fixed_zsa = self.fixed_encoder.zsa(fixed_zs, action)
+            with self._autocast():
+                Q = self.critic(state, action, fixed_zsa, fixed_zs)
+            cur.wait_stream(self._tside)
+        else:
+            fixed_zsa = None
+            if paired:
+                Q_target, fixed_zsa = self._target_chain(next_state, reward, not_done, noise, fixed_target_zs,
+                                                         (zs2, action))
+            else:
+                Q_target = self._target_chain(next_state, reward, not_done, noise, fixed_target_zs, None)
+                with torch.no_grad(), self._autocast():
                     fixed_zsa = self.fixed_encoder.zsa(fixed_zs, action)
-        with self._autocast():
-            Q = self.critic(state, action, fixed_zsa, fixed_zs)
+            with self._autocast():
+                Q = self.critic(state, action, fixed_zsa, fixed_zs)
         # LAP_huber critic loss and the new priorities (:257-262): one
         # td7_critic_loss launch forward, one multiply backward
         critic_loss, priority = ops.critic_loss(Q.float(), Q_target, hp.alpha, hp.min_priority)
@@ -524,6 +532,31 @@ class TD7Learner:
             self.join_side()
         self._fixed_zs = fixed_zs
         return priority
+
+    @torch.no_grad()
+    def _target_chain(self, next_state, reward, not_done, noise, fixed_target_zs, pair):
+        """:236-246: target action with clipped noise, the target critic's heads
+        and Q_target with the running bounds.  pair = (zs2, action): the fixed
+        encoder's zsa rides along in the grouped zsa launches and is returned."""
+        hp = self.hp
+        with self._autocast():
+            # (noise * sigma).clamp(+-noise_clip); sigma -= decrease; (a + noise).clamp(-1, 1)
+            next_action = ops.noisy_action(self.actor_target(next_state, fixed_target_zs).float(), noise,
+                                           self.target_policy_noise, self.policy_noise_decrease,
+                                           clip=hp.noise_clip)
+            fixed_zsa = None
+            if pair is not None:
+                zs2, action = pair
+                zsa2 = self._pair_zsa(zs2, torch.stack([action, next_action]))
+                fixed_zsa, fixed_target_zsa = zsa2[0], zsa2[1]
+            else:
+                fixed_target_zsa = self.fixed_encoder_target.zsa(fixed_target_zs, next_action)
+            Q_heads = self.critic_target(next_state, next_action, fixed_target_zsa, fixed_target_zs).float()
+        # Q_target and the running bounds (:240-246; bounds kept per rank,
+        # MAX-reduced when the targets refresh): one td7_q_target launch
+        Q_target = ops.q_target(Q_heads, reward, not_done, hp.discount, self.min_target, self.max_target,
+                                self.max, self.min)
+        return Q_target if pair is None else (Q_target, fixed_zsa)
 
     def join_side(self):
         """Order the current stream after the encoder branch (end of an update)."""
