@@ -52,6 +52,7 @@ STEP_WRITE_BYTES = {
 BYTES_PER_ENV_STEP = sum(STEP_READ_BYTES.values()) + sum(STEP_WRITE_BYTES.values())
 
 
+FP64_VALU_PEAK_TFS = 78.6   # MI355X fp64 vector peak (AMD spec)
 FP32_MFMA_PEAK_TFS = 157.3  # v_mfma_f32_*_f32 dense peak (MI355X_MICROARCH.md)
 BF16_MFMA_PEAK_TFS = 2500.0  # bf16 / fp16 dense MFMA peak (MI355X_MICROARCH.md, no sparsity)
 MFMA_PEAK_TFS = {"fp32": FP32_MFMA_PEAK_TFS, "bf16": BF16_MFMA_PEAK_TFS, "fp16": BF16_MFMA_PEAK_TFS}
@@ -129,6 +130,17 @@ def pmc_traffic(bytes_per_launch):
         d = json.load(open(f)).get("pmc_exo_step")
         if d and d.get("algorithmic_bytes_per_launch") == bytes_per_launch:
             return d["traffic_bytes_per_launch"], os.path.relpath(f, REPO)
+    return None, None
+
+
+def pmc_valu_flops(envs_per_launch):
+    """fp64 VALU flops per exo_step launch from the newest committed PMC pass
+    (profiles/r*_valu_exo_step.json, tools/env_valu_pmc.sh) on this env count."""
+    import glob
+    for f in reversed(sorted(glob.glob(os.path.join(REPO, "profiles", "r*_valu_exo_step.json")))):
+        d = json.load(open(f))
+        if d.get("envs_per_launch") == envs_per_launch:
+            return d["fp64_flops_per_launch"], os.path.relpath(f, REPO)
     return None, None
 
 
@@ -407,6 +419,14 @@ def main():
                          "bytes_per_env_step": BYTES_PER_ENV_STEP, "avg_kernel_ms": kern_ms,
                          "active_envs_per_launch": active_avg},
         }
+        vfl, vsrc = pmc_valu_flops(N) if args.physics == "ideal" and N <= 16384 else (None, None)
+        if vfl and kern_active == N:
+            # the env kernel is fp64-VALU/latency bound -- its
+            # compute fraction next to the HBM one (flops: PMC, issued lanes)
+            res["valu_roofline"] = {"kernel": res["roofline"]["kernel"], "bound": "valu",
+                                    "achieved": vfl / (kern_ms * 1e-3) / 1e12, "peak": FP64_VALU_PEAK_TFS,
+                                    "unit": "TFLOP/s (fp64)", "frac": vfl / (kern_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFS,
+                                    "flops_per_launch": vfl, "flops_source": vsrc}
         if args.physics == "multibody":
             # q, qd of 19 joints read + written (f64), 5 targets, 1 flag byte read + cleared
             mb_ms = multibody_timing()
