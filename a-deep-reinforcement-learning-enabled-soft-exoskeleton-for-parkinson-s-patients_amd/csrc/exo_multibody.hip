@@ -356,27 +356,41 @@ __global__ __launch_bounds__(MB_G *MB_ENVS) void exo_multibody_kernel(Dev S, Urd
     double lam_l = 0.0, lam_m = 0.0;
     const bool any_lim = __ballot(has_lim) != 0ull; // wave uniform
 
-    // ---- projected Gauss-Seidel sweeps (rows in Bullet's creation order)
+    // ---- projected Gauss-Seidel sweeps (rows in Bullet's creation order).
+    // The 5 base k-links' rows touch only their own velocity (their rows and
+    // columns of M^-1 are zero elsewhere), so their sweeps run on their own
+    // lanes first; the joint-coupled rows 0..13 then sweep with broadcasts.
+    // Row j's impulse change is computed on every lane from its own row and
+    // read from lane j (v_readlane); only lane j keeps its new impulse.
+    const double sl_eff = has_lim ? sl : 0.0; // lanes without a violated limit broadcast 0
+    if (own && d >= NC) {
+        for (int it = 0; it < P.iters; ++it) {
+            if (has_lim) {
+                const double nl = fmin(fmax(lam_l + (wl - sl * vs) * dinv, 0.0), P.limit_imp);
+                vs += diag * ((nl - lam_l) * sl);
+                lam_l = nl;
+            }
+            const double nl = fmin(fmax(lam_m + (wm - vs) * dinv, -imp), imp);
+            vs += diag * (nl - lam_m);
+            lam_m = nl;
+        }
+    }
     for (int it = 0; it < P.iters; ++it) {
         if (any_lim) {
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                const bool mine = has_lim && d == j;
+            for (int j = 0; j < NC; ++j) {
                 const double nl = fmin(fmax(lam_l + (wl - sl * vs) * dinv, 0.0), P.limit_imp);
-                const double dl = mine ? (nl - lam_l) * sl : 0.0;
-                lam_l = mine ? nl : lam_l;
-                if (j < NC) vs += row[j < NC ? j : 0] * group_bcast(dl, j, upper);
-                else vs = (d == j) ? vs + diag * dl : vs;
+                const double dl = (nl - lam_l) * sl_eff;
+                lam_l = d == j ? nl : lam_l;
+                vs += row[j] * group_bcast(dl, j, upper);
             }
         }
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const bool mine = d == j;
+        for (int j = 0; j < NC; ++j) {
             const double nl = fmin(fmax(lam_m + (wm - vs) * dinv, -imp), imp);
-            const double dl = mine ? nl - lam_m : 0.0;
-            lam_m = mine ? nl : lam_m;
-            if (j < NC) vs += row[j < NC ? j : 0] * group_bcast(dl, j, upper);
-            else vs = mine ? vs + diag * dl : vs;
+            const double dl = nl - lam_m;
+            lam_m = d == j ? nl : lam_m;
+            vs += row[j] * group_bcast(dl, j, upper);
         }
     }
 
