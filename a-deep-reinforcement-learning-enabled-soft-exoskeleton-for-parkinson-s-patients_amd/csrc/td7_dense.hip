@@ -157,7 +157,18 @@ int td7_dense_fwd(const float *x, long xsg, long ldx, const float *w, const floa
 int td7_dense_bwd_data(const float *dy, long dysg, long lddy, const float *yv, long ysg, long ldy, const float *w,
                        float *dx, long dxsg, long lddx, int32_t groups, int32_t shared_input, int32_t m, int32_t n,
                        int32_t k, int32_t act, void *stream) {
+    return td7_dense_bwd_data_cols(dy, dysg, lddy, yv, ysg, ldy, w, dx, dxsg, lddx, groups, shared_input, m, n, k, 0,
+                                   k, act, stream);
+}
+
+/* td7_dense_bwd_data for the input columns [c0, c1) only: the gradient w.r.t.
+ * the slice of a concatenated input that requires it (the rest of dX is left
+ * untouched). */
+int td7_dense_bwd_data_cols(const float *dy, long dysg, long lddy, const float *yv, long ysg, long ldy,
+                            const float *w, float *dx, long dxsg, long lddx, int32_t groups, int32_t shared_input,
+                            int32_t m, int32_t n, int32_t k, int32_t c0, int32_t c1, int32_t act, void *stream) {
     if (!dy || !yv || !w || !dx || groups <= 0 || m < 0 || n <= 0 || k <= 0) return EXO_EINVAL;
+    if (c0 < 0 || c1 > k || c0 >= c1) return EXO_EINVAL;
     const int prec = act >> 8;
     act &= 0xFF;
     if (act > 3 || prec > PREC_F16) return EXO_EINVAL;
@@ -169,12 +180,12 @@ int td7_dense_bwd_data(const float *dy, long dysg, long lddy, const float *yv, l
     a.A.ysi = ldy;
     a.A.ysr = 1;
     a.A.act = act;
-    a.B = plain(w, (long)n * k, 1, k); // B(j = out col k, r = n) = W[n][k]
+    a.B = plain(w + c0, (long)n * k, 1, k); // B(j = out col c0 + j, r = n) = W[n][c0 + j]
     a.I = m;
-    a.J = k;
+    a.J = c1 - c0;
     a.R = n;
     a.groups_red = shared_input ? groups : 1;
-    a.C = dx;
+    a.C = dx + c0;
     a.csg = dxsg;
     a.csi = lddx;
     a.csj = 1;

@@ -108,7 +108,7 @@ class _DenseFn(torch.autograd.Function):
     fwd_kernel_max_rows = {"0": 0, "1": 1 << 30}.get(os.environ.get("EXO_DENSE_FWD", ""), 2048)
 
     @staticmethod
-    def forward(ctx, x, w, b, act):
+    def forward(ctx, x, w, b, act, dx_cols=None):
         grouped = w.dim() == 3
         G = w.shape[0] if grouped else 1
         N, K = w.shape[-2], w.shape[-1]
@@ -128,6 +128,7 @@ class _DenseFn(torch.autograd.Function):
             y = _torch_dense(x, w, bb, act)
         ctx.save_for_backward(x, w, y)
         ctx.meta = (grouped, shared, G, M, N, K, act | prec << 8, xsg, ldx, b is not None)
+        ctx.dx_cols = dx_cols
         return y
 
     @staticmethod
@@ -140,16 +141,19 @@ class _DenseFn(torch.autograd.Function):
         need = [ctx.needs_input_grad[i] and _engine_needs(ctx, i) for i in range(3)]
         if need[0]:
             dx = torch.empty((G, M, K) if (grouped and not shared) else (M, K), dtype=torch.float32, device=dy.device)
-            nat.check(nat.lib().td7_dense_bwd_data(nat.ptr(dy), M * N, N, nat.ptr(y), M * N, N, nat.ptr(w),
-                                                   nat.ptr(dx), M * K, K, G, int(shared), M, N, K, act, s),
-                      "td7_dense_bwd_data")
+            c0, c1 = ctx.dx_cols if ctx.dx_cols is not None else (0, K)
+            # columns outside [c0, c1) belong to concatenated inputs that need no
+            # gradient: left unwritten, never read
+            nat.check(nat.lib().td7_dense_bwd_data_cols(nat.ptr(dy), M * N, N, nat.ptr(y), M * N, N, nat.ptr(w),
+                                                        nat.ptr(dx), M * K, K, G, int(shared), M, N, K, c0, c1, act,
+                                                        s), "td7_dense_bwd_data")
         if need[1] or (has_b and need[2]):
             dw = torch.empty_like(w)
             db = torch.empty((G, N) if grouped else (N,), dtype=torch.float32, device=dy.device) if has_b else None
             nat.check(nat.lib().td7_dense_bwd_weight(nat.ptr(dy), M * N, N, nat.ptr(y), M * N, N, nat.ptr(x), xsg,
                                                      ldx, nat.ptr(dw), nat.ptr(db), G, M, N, K, act, s),
                       "td7_dense_bwd_weight")
-        return dx, dw, db, None
+        return dx, dw, db, None, None
 
 
 def _torch_dense(x, w, b, act):
@@ -167,12 +171,14 @@ def _torch_dense(x, w, b, act):
     return y
 
 
-def dense(x, w, b, act=0):
+def dense(x, w, b, act=0, dx_cols=None):
     """Linear + activation (act code, see ACT_CODES) -- td7_dense kernels on a
-    GPU for fp32 tensors; the reference's torch expression otherwise."""
+    GPU for fp32 tensors; the reference's torch expression otherwise.
+    dx_cols = (c0, c1): only input columns [c0, c1) need a gradient (x is a
+    concatenation whose other parts do not require one)."""
     if x.device.type == "cuda" and x.dtype == torch.float32 and w.dtype == torch.float32 \
             and not torch.is_autocast_enabled():
-        return _DenseFn.apply(x, w, b, act)
+        return _DenseFn.apply(x, w, b, act, dx_cols)
     return _torch_dense(x, w, b, act)
 
 
@@ -288,3 +294,24 @@ def mse_loss(x, y):
     if x.is_cuda and x.dtype == torch.float32 and y.dtype == torch.float32:
         return _MSEFn.apply(x, y.detach())
     return torch.nn.functional.mse_loss(x, y)
+
+
+_DX_COLS = os.environ.get("EXO_TD7_DX_COLS", "1") != "0"
+
+
+def concat_grad_cols(parts):
+    """dx_cols hint for a dense layer whose input is torch.cat(parts, -1): the
+    contiguous column range of the parts that require a gradient, or None
+    (all columns) when they are not contiguous."""
+    if not _DX_COLS:
+        return None
+    widths = [p.shape[-1] for p in parts]
+    need = [p.requires_grad for p in parts]
+    if not any(need):
+        return None
+    first = need.index(True)
+    last = len(need) - 1 - need[::-1].index(True)
+    if not all(need[first:last + 1]):
+        return None
+    c0 = sum(widths[:first])
+    return (c0, c0 + sum(widths[first:last + 1]))

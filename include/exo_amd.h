@@ -308,6 +308,13 @@ int td7_dense_fwd(const float *x_dev, long xsg, long ldx, const float *w_dev, co
 int td7_dense_bwd_data(const float *dy_dev, long dysg, long lddy, const float *y_dev, long ysg, long ldy,
                        const float *w_dev, float *dx_dev, long dxsg, long lddx, int32_t groups, int32_t shared_input,
                        int32_t m, int32_t n, int32_t k, int32_t act, void *stream);
+/* The same for the input columns [c0, c1) only (the slice of a concatenated
+ * input that requires a gradient, e.g. the critic's q part, :123-126); the
+ * other columns of dX are not written. */
+int td7_dense_bwd_data_cols(const float *dy_dev, long dysg, long lddy, const float *y_dev, long ysg, long ldy,
+                            const float *w_dev, float *dx_dev, long dxsg, long lddx, int32_t groups,
+                            int32_t shared_input, int32_t m, int32_t n, int32_t k, int32_t c0, int32_t c1, int32_t act,
+                            void *stream);
 /* dW[g] = (dY * act'(Y))^T X  [G][N][K]; db[g] = its column sums [G][N] (db may be NULL). */
 int td7_dense_bwd_weight(const float *dy_dev, long dysg, long lddy, const float *y_dev, long ysg, long ldy,
                          const float *x_dev, long xsg, long ldx, float *dw_dev, float *db_dev, int32_t groups,

@@ -111,6 +111,64 @@ def test_nets_fused_match_torch_layers():
         torch.testing.assert_close(g0, g1, rtol=1e-3, atol=1e-6)
 
 
+@pytest.mark.parametrize("c0,c1,shared", [(0, 320, False), (0, 620, False), (320, 620, False), (80, 87, True),
+                                         (1, 919, False)])
+def test_dense_bwd_data_column_window(c0, c1, shared):
+    """td7_dense_bwd_data_cols writes exactly the input columns [c0, c1) of dX,
+    equal to the full input gradient there."""
+    from exo_amd import _native as nat
+    torch.manual_seed(c0 + c1)
+    m, n, k = 1000, 320, 87 if shared else 920
+    c1 = min(c1, k)
+    dy = torch.randn(2, m, n, device="cuda")
+    y = torch.randn(2, m, n, device="cuda")
+    w = torch.randn(2, n, k, device="cuda") / k ** 0.5
+    shape = (m, k) if shared else (2, m, k)
+    full = torch.zeros(shape, device="cuda")
+    win = torch.full(shape, 7.0, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    for out, (a, b) in ((full, (0, k)), (win, (c0, c1))):
+        nat.check(nat.lib().td7_dense_bwd_data_cols(nat.ptr(dy), m * n, n, nat.ptr(y), m * n, n, nat.ptr(w),
+                                                    nat.ptr(out), m * k, k, 2, int(shared), m, n, k, a, b, 2, s),
+                  "td7_dense_bwd_data_cols")
+    torch.cuda.synchronize()
+    torch.testing.assert_close(win[..., c0:c1], full[..., c0:c1], rtol=0, atol=0)
+    assert (win[..., :c0] == 7.0).all() and (win[..., c1:] == 7.0).all()
+    bad = nat.lib().td7_dense_bwd_data_cols(nat.ptr(dy), m * n, n, nat.ptr(y), m * n, n, nat.ptr(w), nat.ptr(full),
+                                            m * k, k, 2, int(shared), m, n, k, 5, 5, 2, s)
+    assert bad != 0
+
+
+def test_critic_actor_update_gradients_with_partial_inputs():
+    """The actor-update pattern: the critic's zs and the encoder's zs are
+    constants, only the action path needs input gradients (column windows)."""
+    import copy
+
+    import torch.nn.functional as F
+    from exo_amd.td7 import Actor, Critic, Encoder
+    torch.manual_seed(1)
+    B = 300
+    state = torch.randn(B, 80, device="cuda")
+    enc = Encoder(80, 7, 300, 300, F.elu).cuda()
+    actor = Actor(80, 7, 300, 320, F.relu).cuda()
+    critic = Critic(80, 7, 300, 320, F.elu).cuda()
+    with torch.no_grad():
+        zs = enc.zs(state)
+    outs = []
+    for fused in (True, False):
+        e, a, c = copy.deepcopy(enc), copy.deepcopy(actor), copy.deepcopy(critic)
+        if not fused:
+            e.activ = lambda t: F.elu(t)
+            a.activ = lambda t: F.relu(t)
+            c.activ = lambda t: F.elu(t)
+        pi = a(state, zs)
+        q = c(state, pi, e.zsa(zs, pi), zs)
+        (-q.mean()).backward()
+        outs.append([p.grad.clone() for p in a.parameters()])
+    for g0, g1 in zip(*outs):
+        torch.testing.assert_close(g0, g1, rtol=1e-3, atol=1e-6)
+
+
 # ------------------------------------------------------------ bf16 / fp16 MFMA
 _ROUND = {"bf16": torch.bfloat16, "fp16": torch.float16}
 _GRAD = {0: lambda y: torch.ones_like(y), 1: lambda y: (y > 0).to(y.dtype), 2: lambda y: torch.where(y > 0, 1.0, y + 1),
