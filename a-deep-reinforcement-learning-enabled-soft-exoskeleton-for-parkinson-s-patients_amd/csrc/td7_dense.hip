@@ -18,6 +18,8 @@
 // shared by the groups (stride 0) has its bwd-data reduced over the groups
 // inside the kernel.  fp32 in memory, fp32 accumulate; the MFMA operands are
 // exact f32 (default) or rounded to bf16 / f16 (Prec, bits 8-15 of act).
+#include <climits>
+
 #include "td7_dense_kernels.h"
 
 namespace td7dense {
@@ -25,8 +27,10 @@ namespace td7dense {
 // instantiated in td7_dense_{f32,bf16,f16}.hip
 #define TD7_EXTERN(P)                                                                                 \
     extern template void launch_gemm_p<P>(const GemmArgs &, dim3, int, hipStream_t);                  \
-    extern template void launch_wgrad_p<P>(const WgradArgs &, dim3, int, int, int, hipStream_t);      \
-    extern template void launch_fwd_p<P>(const GemmArgs &, dim3, int, int, int, int, hipStream_t);
+    extern template void launch_wgrad_p<P, false>(const WgradArgs &, dim3, int, int, int, hipStream_t); \
+    extern template void launch_wgrad_p<P, true>(const WgradArgs &, dim3, int, int, int, hipStream_t);  \
+    extern template void launch_fwd_p<P, false>(const GemmArgs &, dim3, int, int, int, int, hipStream_t); \
+    extern template void launch_fwd_p<P, true>(const GemmArgs &, dim3, int, int, int, int, hipStream_t);
 TD7_EXTERN(PREC_F32)
 TD7_EXTERN(PREC_BF16)
 TD7_EXTERN(PREC_F16)
@@ -57,7 +61,7 @@ int launch(const GemmArgs &a, int groups_grid, int prec, hipStream_t s) {
 }
 
 
-int launch_wgrad(const WgradArgs &a, int groups, int act, int prec, hipStream_t s) {
+int launch_wgrad(const WgradArgs &a, int groups, int act, int prec, hipStream_t s, bool cat = false) {
     const int jt = (a.J + 63) / 64;
     auto tiles = [&](int va) { return (long)jt * ((a.I + 16 * va - 1) / (16 * va)) * groups; };
     // the widest i-vector that still yields ~1k waves at NW = 8
@@ -67,14 +71,20 @@ int launch_wgrad(const WgradArgs &a, int groups, int act, int prec, hipStream_t 
     int nw = 2;
     while (nw < 8 && nks >= 8L * nw * 2 && tiles(va) * nw * 2 <= 2048) nw *= 2;
     dim3 grid(jt, (a.I + 16 * va - 1) / (16 * va), groups);
-    if (prec == PREC_BF16) launch_wgrad_p<PREC_BF16>(a, grid, va, nw, act, s);
-    else if (prec == PREC_F16) launch_wgrad_p<PREC_F16>(a, grid, va, nw, act, s);
-    else launch_wgrad_p<PREC_F32>(a, grid, va, nw, act, s);
+    if (cat) {
+        if (prec == PREC_BF16) launch_wgrad_p<PREC_BF16, true>(a, grid, va, nw, act, s);
+        else if (prec == PREC_F16) launch_wgrad_p<PREC_F16, true>(a, grid, va, nw, act, s);
+        else launch_wgrad_p<PREC_F32, true>(a, grid, va, nw, act, s);
+    } else {
+        if (prec == PREC_BF16) launch_wgrad_p<PREC_BF16, false>(a, grid, va, nw, act, s);
+        else if (prec == PREC_F16) launch_wgrad_p<PREC_F16, false>(a, grid, va, nw, act, s);
+        else launch_wgrad_p<PREC_F32, false>(a, grid, va, nw, act, s);
+    }
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 
-int launch_fwd(const GemmArgs &a, int groups_grid, int prec, hipStream_t s) {
-    const long span_a = (long)groups_grid * a.A.sg + (long)a.I * a.A.si + (long)a.R;
+int launch_fwd(const GemmArgs &a, int groups_grid, int prec, hipStream_t s, bool cat = false) {
+    const long span_a = cat ? 0 : (long)groups_grid * a.A.sg + (long)a.I * a.A.si + (long)a.R;
     const long span_b = (long)groups_grid * a.B.sg + (long)a.J * a.B.si + (long)a.R;
     if (span_a >= (1L << 29) || span_b >= (1L << 29) || a.A.sr != 1 || a.B.sr != 1) return EXO_ERANGE;
     const int steps = a.R >> 4;
@@ -97,10 +107,37 @@ int launch_fwd(const GemmArgs &a, int groups_grid, int prec, hipStream_t s) {
     }
     dim3 grid((a.J + 16 * tn - 1) / (16 * tn), (a.I + 16 * tm - 1) / (16 * tm), groups_grid);
     const int wsteps = (steps + kw - 1) / kw;
-    if (prec == PREC_BF16) launch_fwd_p<PREC_BF16>(a, grid, tm, tn, kw, wsteps, s);
-    else if (prec == PREC_F16) launch_fwd_p<PREC_F16>(a, grid, tm, tn, kw, wsteps, s);
-    else launch_fwd_p<PREC_F32>(a, grid, tm, tn, kw, wsteps, s);
+    if (cat) {
+        if (prec == PREC_BF16) launch_fwd_p<PREC_BF16, true>(a, grid, tm, tn, kw, wsteps, s);
+        else if (prec == PREC_F16) launch_fwd_p<PREC_F16, true>(a, grid, tm, tn, kw, wsteps, s);
+        else launch_fwd_p<PREC_F32, true>(a, grid, tm, tn, kw, wsteps, s);
+    } else {
+        if (prec == PREC_BF16) launch_fwd_p<PREC_BF16, false>(a, grid, tm, tn, kw, wsteps, s);
+        else if (prec == PREC_F16) launch_fwd_p<PREC_F16, false>(a, grid, tm, tn, kw, wsteps, s);
+        else launch_fwd_p<PREC_F32, false>(a, grid, tm, tn, kw, wsteps, s);
+    }
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
+}
+
+// segments of a concatenated input -> CatSeg; the total width, or < 0 when the
+// layout breaks the kernels' 4-column chunk rule
+static int make_cat(CatSeg &c, int nseg, const float *const *xs, const long *xsg, const long *ldx, const int32_t *widths) {
+    if (nseg < 1 || nseg > CAT_MAX || !xs || !xsg || !ldx || !widths) return -1;
+    int k = 0;
+    for (int s = 0; s < CAT_MAX; ++s) {
+        c.p[s] = s < nseg ? xs[s] : xs[0];
+        c.sg[s] = s < nseg ? xsg[s] : 0;
+        c.ld[s] = s < nseg ? (int)ldx[s] : 0;
+        c.kb[s] = s < nseg ? k : INT_MAX;
+        if (s < nseg) {
+            if (!xs[s] || widths[s] <= 0 || xsg[s] < 0 || ldx[s] < widths[s] || ldx[s] >= (1L << 30)) return -1;
+            if (s < nseg - 1 && widths[s] % 4) return -1;
+            if (s == nseg - 1 && widths[s] < 4) return -1;
+            k += widths[s];
+        }
+    }
+    c.kb[CAT_MAX] = INT_MAX;
+    return k;
 }
 
 Operand plain(const float *p, long sg, long si, long sr) {
@@ -148,6 +185,68 @@ int td7_dense_fwd(const float *x, long xsg, long ldx, const float *w, const floa
     a.act = act;
     a.j_bias = -1;
     return launch_fwd(a, groups, prec, (hipStream_t)stream);
+}
+
+/* td7_dense_fwd of a concatenated input X = [X_0 | ... | X_{nseg-1}] (the
+ * reference's Linear(torch.cat(...))) read in place: segment s is
+ * xs[s] [G][M][widths[s]] with group stride xsg[s] (0 = shared by the groups)
+ * and row stride ldx[s]; K = sum of widths.  nseg <= 4, interior widths
+ * multiples of 4, the last >= 4 (else EXO_EINVAL: concatenate instead). */
+int td7_dense_fwd_cat(int32_t nseg, const float *const *xs, const long *xsg, const long *ldx, const int32_t *widths,
+                      const float *w, const float *b, float *y, long ysg, long ldy, int32_t groups, int32_t m, int32_t n,
+                      int32_t act, void *stream) {
+    if (!w || !y || groups <= 0 || m < 0 || n <= 0) return EXO_EINVAL;
+    const int prec = act >> 8;
+    act &= 0xFF;
+    if (act > 3 || prec > PREC_F16) return EXO_EINVAL;
+    GemmArgs a{};
+    const int k = make_cat(a.cat, nseg, xs, xsg, ldx, widths);
+    if (k <= 0) return EXO_EINVAL;
+    if (m == 0) return EXO_OK;
+    a.A = plain(xs[0], 0, 0, 1);
+    a.B = plain(w, (long)n * k, k, 1);
+    a.I = m;
+    a.J = n;
+    a.R = k;
+    a.groups_red = 1;
+    a.C = y;
+    a.csg = ysg;
+    a.csi = ldy;
+    a.csj = 1;
+    a.bias = b;
+    a.bsg = n;
+    a.act = act;
+    a.j_bias = -1;
+    return launch_fwd(a, groups, prec, (hipStream_t)stream, true);
+}
+
+/* td7_dense_bwd_weight of a layer whose input was given by segments
+ * (td7_dense_fwd_cat's layout); N >= 4. */
+int td7_dense_bwd_weight_cat(const float *dy, long dysg, long lddy, const float *yv, long ysg, long ldy, int32_t nseg,
+                             const float *const *xs, const long *xsg, const long *ldx, const int32_t *widths, float *dw,
+                             float *db, int32_t groups, int32_t m, int32_t n, int32_t act, void *stream) {
+    if (!dy || !yv || !dw || groups <= 0 || m <= 0 || n < 4) return EXO_EINVAL;
+    const int prec = act >> 8;
+    act &= 0xFF;
+    if (act > 3 || prec > PREC_F16) return EXO_EINVAL;
+    WgradArgs w{};
+    const int k = make_cat(w.cat, nseg, xs, xsg, ldx, widths);
+    if (k <= 0) return EXO_EINVAL;
+    const long span = (long)groups * (dysg > ysg ? dysg : ysg) + (long)m * (lddy > ldy ? lddy : ldy) + n;
+    if (span >= (1L << 29)) return EXO_ERANGE;
+    w.dy = dy;
+    w.y = yv;
+    w.x = xs[0];
+    w.dysg = (int)dysg;
+    w.lddy = (int)lddy;
+    w.ysg = (int)ysg;
+    w.ldy = (int)ldy;
+    w.dw = dw;
+    w.db = db;
+    w.I = n;
+    w.J = k;
+    w.M = m;
+    return launch_wgrad(w, groups, act, prec, (hipStream_t)stream, true);
 }
 
 /* dX = sum over the reduced groups of (dY[g] * act'(Y[g])) W[g].
@@ -230,7 +329,7 @@ int td7_dense_bwd_weight(const float *dy, long dysg, long lddy, const float *yv,
         const long span = (long)groups * (dysg > ysg ? (dysg > xsg ? dysg : xsg) : (ysg > xsg ? ysg : xsg)) +
                           (long)m * (lddy > ldy ? (lddy > ldx ? lddy : ldx) : (ldy > ldx ? ldy : ldx)) + n + k;
         if (span < (1L << 29)) {
-            WgradArgs w{dy, yv, x, (int)dysg, (int)lddy, (int)ysg, (int)ldy, (int)xsg, (int)ldx, dw, db, n, k, m};
+            WgradArgs w{{}, dy, yv, x, (int)dysg, (int)lddy, (int)ysg, (int)ldy, (int)xsg, (int)ldx, dw, db, n, k, m};
             return launch_wgrad(w, groups, act, prec, (hipStream_t)stream);
         }
     }

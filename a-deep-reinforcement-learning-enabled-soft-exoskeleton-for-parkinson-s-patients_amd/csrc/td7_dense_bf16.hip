@@ -3,6 +3,8 @@
 
 namespace td7dense {
 template void launch_gemm_p<PREC_BF16>(const GemmArgs &, dim3, int, hipStream_t);
-template void launch_wgrad_p<PREC_BF16>(const WgradArgs &, dim3, int, int, int, hipStream_t);
-template void launch_fwd_p<PREC_BF16>(const GemmArgs &, dim3, int, int, int, int, hipStream_t);
+template void launch_wgrad_p<PREC_BF16, false>(const WgradArgs &, dim3, int, int, int, hipStream_t);
+template void launch_fwd_p<PREC_BF16, false>(const GemmArgs &, dim3, int, int, int, int, hipStream_t);
+template void launch_wgrad_p<PREC_BF16, true>(const WgradArgs &, dim3, int, int, int, hipStream_t);
+template void launch_fwd_p<PREC_BF16, true>(const GemmArgs &, dim3, int, int, int, int, hipStream_t);
 } // namespace td7dense

@@ -3,6 +3,8 @@
 
 namespace td7dense {
 template void launch_gemm_p<PREC_F32>(const GemmArgs &, dim3, int, hipStream_t);
-template void launch_wgrad_p<PREC_F32>(const WgradArgs &, dim3, int, int, int, hipStream_t);
-template void launch_fwd_p<PREC_F32>(const GemmArgs &, dim3, int, int, int, int, hipStream_t);
+template void launch_wgrad_p<PREC_F32, false>(const WgradArgs &, dim3, int, int, int, hipStream_t);
+template void launch_fwd_p<PREC_F32, false>(const GemmArgs &, dim3, int, int, int, int, hipStream_t);
+template void launch_wgrad_p<PREC_F32, true>(const WgradArgs &, dim3, int, int, int, hipStream_t);
+template void launch_fwd_p<PREC_F32, true>(const GemmArgs &, dim3, int, int, int, int, hipStream_t);
 } // namespace td7dense

@@ -16,6 +16,15 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef short shortx4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 halfx4 __attribute__((ext_vector_type(4)));
+typedef uint32_t uint32_t4 __attribute__((ext_vector_type(4), aligned(4))); // 16-byte global load, dword aligned
+typedef const __attribute__((address_space(1))) uint32_t4 *gptr4;
+
+// 16-byte global (not flat) load; lanes with !ok read a valid fallback address
+// and return zeros (no exec-mask branch around the load)
+__device__ __forceinline__ uint32_t4 gload4(const float *p, const float *fallback, bool ok) {
+    const uint32_t4 v = *(gptr4)(ok ? p : fallback);
+    return ok ? v : uint32_t4{0u, 0u, 0u, 0u};
+}
 
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_ELU = 2, ACT_TANH = 3 };
 
@@ -68,7 +77,27 @@ struct Operand {
     int ones_col; // >= 0: index i == ones_col reads 1.0 (bias column of bwd-weight)
 };
 
+// A concatenated operand X = [X_0 | X_1 | ... ] along its columns (the
+// inputs of the TD7 layers that read torch.cat(...) in the reference): segment
+// s holds columns [kb[s], kb[s+1]) at p[s] + g*sg[s] + row*ld[s] + (col - kb[s]);
+// sg[s] = 0 for a segment shared by the groups.  Interior boundaries are
+// multiples of 4 and the last segment is >= 4 wide, so every 4-column chunk a
+// lane loads lies in one segment.  Unused entries: kb = INT_MAX.
+constexpr int CAT_MAX = 4;
+struct CatSeg {
+    const float *p[CAT_MAX];
+    long sg[CAT_MAX];
+    int ld[CAT_MAX];
+    int kb[CAT_MAX + 1];
+};
+
+// segment of column r (r < total width)
+__device__ __forceinline__ int cat_seg(const CatSeg &c, int r) {
+    return (r >= c.kb[1]) + (r >= c.kb[2]) + (r >= c.kb[3]);
+}
+
 struct GemmArgs {
+    CatSeg cat; // forward with CAT: the A operand (X) by segments
     Operand A, B;
     int I, J, R;      // C is I x J, reduction length R
     int groups_red;   // > 1: also reduce over this many groups (bwd-data of a shared input)
@@ -310,7 +339,7 @@ void launch_gemm_p(const GemmArgs &a, dim3 grid, int nw, hipStream_t s) {
 // trips instead of one per step; the tail (K % 16) is a range-checked step.
 // (2x2 waves per workgroup sharing X / W rows through L1 measured slower than
 // one wave per workgroup with this remap.)
-template <int EP, int GS, int TM, int TN, int KW, int P>
+template <int EP, int GS, int TM, int TN, int KW, int P, bool CAT>
 __global__ __launch_bounds__(64 * KW) void dense_fwd_kernel(GemmArgs a) {
     // a (16 TM) x (16 TN) tile per workgroup; per 16-wide step TM + TN b128
     // loads feed 4 TM TN MFMAs.  KW waves split the reduction (halves, summed
@@ -322,12 +351,31 @@ __global__ __launch_bounds__(64 * KW) void dense_fwd_kernel(GemmArgs a) {
     const __amdgpu_buffer_rsrc_t ra = rsrc(a.A.p), rb = rsrc(a.B.p);
     int abase[TM], bbase[TN];
     bool arow[TM], bcol[TN];
+    int arowi[TM];
 #pragma unroll
     for (int x = 0; x < TM; ++x) {
         const int row = i0 + 16 * x + c;
         abase[x] = g * (int)a.A.sg + row * (int)a.A.si;
         arow[x] = row < a.I;
+        arowi[x] = arow[x] ? row : 0;
     }
+    // CAT: segment bases (wave-uniform: group offset and -kb folded in)
+    const float *cb0 = a.cat.p[0] + g * a.cat.sg[0], *cb1 = a.cat.p[1] + g * a.cat.sg[1] - a.cat.kb[1],
+                *cb2 = a.cat.p[2] + g * a.cat.sg[2] - a.cat.kb[2], *cb3 = a.cat.p[3] + g * a.cat.sg[3] - a.cat.kb[3];
+    // pointer to X(row, r) for a chunk r .. r+3 (one segment)
+    const int kb1 = a.cat.kb[1], kb2 = a.cat.kb[2], kb3 = a.cat.kb[3];
+    const int cl0 = a.cat.ld[0], dl1 = a.cat.ld[1] - cl0, dl2 = a.cat.ld[2] - a.cat.ld[1], dl3 = a.cat.ld[3] - a.cat.ld[2];
+    const long e1 = cb1 - cb0, e2 = cb2 - cb1, e3 = cb3 - cb2; // element distances between segment bases
+    // (the segment picked by arithmetic on the monotone flags s1 >= s2 >= s3: a
+    // select chain over the bases is turned into an LDS lookup table)
+    auto cat_ptr = [=](int row, int r) {
+        const int s1 = r >= kb1, s2 = r >= kb2, s3 = r >= kb3;
+        const long off = s1 * e1 + s2 * e2 + s3 * e3;
+        const int ld = cl0 + s1 * dl1 + s2 * dl2 + s3 * dl3;
+        return cb0 + off + (long)row * ld + r;
+    };
+    // CAT: the 4 A values (r .. r+3) of row tile x as one 16-byte global load
+    auto ld_cat = [&](int x, int r, bool ok) { return gload4(cat_ptr(arowi[x], ok ? r : 0), cb0, ok); };
     float bias_v[TN];
 #pragma unroll
     for (int y = 0; y < TN; ++y) {
@@ -354,9 +402,15 @@ __global__ __launch_bounds__(64 * KW) void dense_fwd_kernel(GemmArgs a) {
             const bool live = s0 + s < nfull;
 #pragma unroll
             for (int x = 0; x < TM; ++x) {
-                const auto v = __builtin_amdgcn_raw_buffer_load_b128(ra, (live & arow[x]) ? (abase[x] + r) * 4 : BUF_OOB, 0, 0);
+                if constexpr (CAT) {
+                    const auto v = ld_cat(x, r, live & arow[x]);
 #pragma unroll
-                for (int jj = 0; jj < 4; ++jj) av[s][x][jj] = v[jj];
+                    for (int jj = 0; jj < 4; ++jj) av[s][x][jj] = v[jj];
+                } else {
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b128(ra, (live & arow[x]) ? (abase[x] + r) * 4 : BUF_OOB, 0, 0);
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj) av[s][x][jj] = v[jj];
+                }
             }
 #pragma unroll
             for (int y = 0; y < TN; ++y) {
@@ -423,7 +477,13 @@ __global__ __launch_bounds__(64 * KW) void dense_fwd_kernel(GemmArgs a) {
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
 #pragma unroll
-            for (int x = 0; x < TM; ++x) xa[x][jj] = ldb(ra, arow[x] & (r + jj < a.R), abase[x] + r + jj);
+            for (int x = 0; x < TM; ++x) {
+                if constexpr (CAT) { // the chunk r .. r+3 lies in one segment
+                    xa[x][jj] = (arow[x] & (r + jj < a.R)) ? cat_ptr(arowi[x], r)[jj] : 0.f;
+                } else {
+                    xa[x][jj] = ldb(ra, arow[x] & (r + jj < a.R), abase[x] + r + jj);
+                }
+            }
 #pragma unroll
             for (int y = 0; y < TN; ++y) xb[y][jj] = ldb(rb, bcol[y] & (r + jj < a.R), bbase[y] + r + jj);
         }
@@ -485,6 +545,7 @@ __global__ __launch_bounds__(64 * KW) void dense_fwd_kernel(GemmArgs a) {
 // shift them into place; what they deliver for rows i >= I / columns j >= J
 // only reaches accumulator elements that are never stored.  Rows m >= M load 0.
 struct WgradArgs {
+    CatSeg cat; // CAT: X by segments (along j)
     const float *dy, *y, *x;
     int dysg, lddy, ysg, ldy, xsg, ldx;
     float *dw, *db;
@@ -517,7 +578,7 @@ __device__ __forceinline__ float shifted(const float (&v)[VA], int sh, int e) {
     return o;
 }
 
-template <int AG, int VA, int NW, int P>
+template <int AG, int VA, int NW, int P, bool CAT>
 __global__ __launch_bounds__(64 * NW) void dense_wgrad_kernel(WgradArgs a) {
     constexpr int KS = VA == 1 ? 8 : 4; // 4-row steps per prefetch group (two groups in flight)
     constexpr int NACC = VA * 4;
@@ -529,6 +590,19 @@ __global__ __launch_bounds__(64 * NW) void dense_wgrad_kernel(WgradArgs a) {
     const int ja = j0 + 4 * c, jb = min(ja, a.J - 4), shj = ja - jb;
     const __amdgpu_buffer_rsrc_t rdy = rsrc(a.dy), ry = rsrc(AG > 0 ? a.y : a.dy), rx = rsrc(a.x);
     const int dyb = g * a.dysg + ib, yb = g * a.ysg + ib, xb = g * a.xsg + jb;
+    const float *xcat = nullptr; // CAT: this lane's 4 columns jb .. jb+3 (one segment)
+    int xld = 0;
+    if constexpr (CAT) {
+        const int sg = cat_seg(a.cat, jb);
+        const float *p = a.cat.p[0];
+        long gs = a.cat.sg[0];
+        int ld = a.cat.ld[0], kb = a.cat.kb[0];
+#pragma unroll
+        for (int k = 1; k < CAT_MAX; ++k)
+            if (sg == k) p = a.cat.p[k], gs = a.cat.sg[k], ld = a.cat.ld[k], kb = a.cat.kb[k];
+        xcat = p + g * gs + (jb - kb);
+        xld = ld;
+    }
     const int nks = (a.M + 3) >> 2;
     const int my = nks > w ? (nks - w + NW - 1) / NW : 0;
     const int ngrp = (my + KS - 1) / KS;
@@ -552,7 +626,13 @@ __global__ __launch_bounds__(64 * NW) void dense_wgrad_kernel(WgradArgs a) {
             const bool live = (k < my) & (m < a.M);
             ld_vec<VA>(rdy, live ? (dyb + m * a.lddy) * 4 : BUF_OOB, f.a[sp]);
             if (AG > 0) ld_vec<VA>(ry, live ? (yb + m * a.ldy) * 4 : BUF_OOB, f.y[sp]);
-            ld_vec<4>(rx, live ? (xb + m * a.ldx) * 4 : BUF_OOB, f.b[sp]);
+            if constexpr (CAT) {
+                const uint32_t4 v = gload4(xcat + (long)m * xld, xcat, live);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) f.b[sp][e] = __uint_as_float(v[e]);
+            } else {
+                ld_vec<4>(rx, live ? (xb + m * a.ldx) * 4 : BUF_OOB, f.b[sp]);
+            }
         }
     };
     auto mma = [&](const Buf &f) {
@@ -658,13 +738,13 @@ __global__ __launch_bounds__(64 * NW) void dense_wgrad_kernel(WgradArgs a) {
     }
 }
 
-template <int P>
+template <int P, bool CAT>
 void launch_wgrad_p(const WgradArgs &a, dim3 grid, int va, int nw, int act, hipStream_t s) {
 #define WG_NW(AGv, VAv)                                                                              \
     do {                                                                                           \
-        if (nw == 8) hipLaunchKernelGGL((dense_wgrad_kernel<AGv, VAv, 8, P>), grid, dim3(512), 0, s, a); \
-        else if (nw == 4) hipLaunchKernelGGL((dense_wgrad_kernel<AGv, VAv, 4, P>), grid, dim3(256), 0, s, a); \
-        else hipLaunchKernelGGL((dense_wgrad_kernel<AGv, VAv, 2, P>), grid, dim3(128), 0, s, a);       \
+        if (nw == 8) hipLaunchKernelGGL((dense_wgrad_kernel<AGv, VAv, 8, P, CAT>), grid, dim3(512), 0, s, a); \
+        else if (nw == 4) hipLaunchKernelGGL((dense_wgrad_kernel<AGv, VAv, 4, P, CAT>), grid, dim3(256), 0, s, a); \
+        else hipLaunchKernelGGL((dense_wgrad_kernel<AGv, VAv, 2, P, CAT>), grid, dim3(128), 0, s, a);       \
     } while (0)
 #define WG_VA(AGv)                      \
     do {                              \
@@ -682,17 +762,17 @@ void launch_wgrad_p(const WgradArgs &a, dim3 grid, int va, int nw, int act, hipS
 #undef WG_NW
 }
 
-template <int P>
+template <int P, bool CAT>
 void launch_fwd_p(const GemmArgs &a, dim3 grid, int tm, int tn, int kw, int wsteps, hipStream_t s) {
 #define FWD_GS(EPv, TMv, TNv, KWv)                                                                              \
     do {                                                                                                      \
         const dim3 blk(64 * KWv);                                                                             \
-        if (wsteps <= 5) hipLaunchKernelGGL((dense_fwd_kernel<EPv, 5, TMv, TNv, KWv, P>), grid, blk, 0, s, a); \
+        if (wsteps <= 5) hipLaunchKernelGGL((dense_fwd_kernel<EPv, 5, TMv, TNv, KWv, P, CAT>), grid, blk, 0, s, a); \
         else if (TMv * TNv == 1 && wsteps <= 20)                                                              \
-            hipLaunchKernelGGL((dense_fwd_kernel<EPv, 20, TMv, TNv, KWv, P>), grid, blk, 0, s, a);            \
+            hipLaunchKernelGGL((dense_fwd_kernel<EPv, 20, TMv, TNv, KWv, P, CAT>), grid, blk, 0, s, a);            \
         else if (TMv * TNv == 1)                                                                              \
-            hipLaunchKernelGGL((dense_fwd_kernel<EPv, 10, TMv, TNv, KWv, P>), grid, blk, 0, s, a);            \
-        else hipLaunchKernelGGL((dense_fwd_kernel<EPv, 5, TMv, TNv, KWv, P>), grid, blk, 0, s, a);             \
+            hipLaunchKernelGGL((dense_fwd_kernel<EPv, 10, TMv, TNv, KWv, P, CAT>), grid, blk, 0, s, a);            \
+        else hipLaunchKernelGGL((dense_fwd_kernel<EPv, 5, TMv, TNv, KWv, P, CAT>), grid, blk, 0, s, a);             \
     } while (0)
 #define FWD_LAUNCH(EPv)                                                                 \
     do {                                                                                \

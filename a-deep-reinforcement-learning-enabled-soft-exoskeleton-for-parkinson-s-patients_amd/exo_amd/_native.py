@@ -110,6 +110,11 @@ EXPORTS = {
     "td7_dense_bwd_data_cols": (c_int32, [c_void_p, c_long, c_long, c_void_p, c_long, c_long, c_void_p, c_void_p,
                                           c_long, c_long, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
                                           c_int32, c_void_p]),
+    "td7_dense_fwd_cat": (c_int32, [c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                    c_long, c_long, c_int32, c_int32, c_int32, c_int32, c_void_p]),
+    "td7_dense_bwd_weight_cat": (c_int32, [c_void_p, c_long, c_long, c_void_p, c_long, c_long, c_int32, c_void_p,
+                                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32,
+                                           c_int32, c_void_p]),
     "td7_dense_bwd_weight": (c_int32, [c_void_p, c_long, c_long, c_void_p, c_long, c_long, c_void_p, c_long,
                                        c_long, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32,
                                        c_void_p]),

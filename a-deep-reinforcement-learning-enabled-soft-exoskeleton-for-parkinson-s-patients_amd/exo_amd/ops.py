@@ -2,6 +2,7 @@
 torch expression on CPU tensors (the CPU path exists for the learner's parity
 tests; on a GPU the HIP kernels are mandatory -- a missing library raises)."""
 import contextlib
+import ctypes
 import os
 
 import torch
@@ -154,6 +155,109 @@ class _DenseFn(torch.autograd.Function):
                                                      ldx, nat.ptr(dw), nat.ptr(db), G, M, N, K, act, s),
                       "td7_dense_bwd_weight")
         return dx, dw, db, None, None
+
+
+class _DenseCatFn(torch.autograd.Function):
+    """act(torch.cat(parts, -1) W^T + b) without materialising the
+    concatenation: td7_dense_fwd_cat / td7_dense_bwd_weight_cat read the parts
+    in place, and each part that needs a gradient gets its own td7_dense_bwd_data
+    launch over its column window, written straight into its gradient tensor.
+    With grouped W [G,N,K] a part is [G,M,k] (one per group) or [M,k] (shared
+    by the groups: its gradient sums over them)."""
+
+    @staticmethod
+    def forward(ctx, w, b, act, *parts):
+        grouped = w.dim() == 3
+        G = w.shape[0] if grouped else 1
+        N, K = w.shape[-2], w.shape[-1]
+        parts = [_rows(p)[0] for p in parts]
+        M = parts[0].shape[-2]
+        n = len(parts)
+        widths = [p.shape[-1] for p in parts]
+        sgs = [p.stride(0) if (grouped and p.dim() == 3) else 0 for p in parts]
+        lds = [p.stride(-2) for p in parts]
+        w = w.contiguous()
+        bb = b.contiguous() if b is not None else None
+        prec = _matrix_prec
+        seg = ((ctypes.c_void_p * n)(*[p.data_ptr() for p in parts]), (ctypes.c_long * n)(*sgs),
+               (ctypes.c_long * n)(*lds), (ctypes.c_int32 * n)(*widths))
+        y = torch.empty((G, M, N) if grouped else (M, N), dtype=torch.float32, device=w.device)
+        nat.check(nat.lib().td7_dense_fwd_cat(n, *seg, nat.ptr(w), nat.ptr(bb), nat.ptr(y), M * N, N, G, M, N,
+                                              act | prec << 8, nat.stream_ptr(w.device)), "td7_dense_fwd_cat")
+        ctx.save_for_backward(w, y, *parts)
+        ctx.meta = (grouped, G, M, N, K, act | prec << 8, b is not None, widths, sgs, lds)
+        # ctx.next_functions has one entry per TENSOR input: argument index -> entry
+        args = (w, b, act, *parts)
+        ctx.edge = {i: sum(isinstance(t, torch.Tensor) for t in args[:i]) for i in range(len(args))}
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        w, y, *parts = ctx.saved_tensors
+        grouped, G, M, N, K, act, has_b, widths, sgs, lds = ctx.meta
+        dy = dy.contiguous()
+        s = nat.stream_ptr(dy.device)
+        n = len(parts)
+        dw = db = None
+        if (ctx.needs_input_grad[0] and _engine_needs(ctx, ctx.edge[0])) or \
+                (has_b and ctx.needs_input_grad[1] and _engine_needs(ctx, ctx.edge[1])):
+            dw = torch.empty_like(w)
+            db = torch.empty((G, N) if grouped else (N,), dtype=torch.float32, device=dy.device) if has_b else None
+            seg = ((ctypes.c_void_p * n)(*[p.data_ptr() for p in parts]), (ctypes.c_long * n)(*sgs),
+                   (ctypes.c_long * n)(*lds), (ctypes.c_int32 * n)(*widths))
+            nat.check(nat.lib().td7_dense_bwd_weight_cat(nat.ptr(dy), M * N, N, nat.ptr(y), M * N, N, n, *seg,
+                                                         nat.ptr(dw), nat.ptr(db), G, M, N, act, s),
+                      "td7_dense_bwd_weight_cat")
+        grads = []
+        c0 = 0
+        for i, p in enumerate(parts):
+            k = widths[i]
+            g = None
+            if ctx.needs_input_grad[3 + i] and _engine_needs(ctx, ctx.edge[3 + i]):
+                shared = grouped and p.dim() == 2
+                g = torch.empty(p.shape, dtype=torch.float32, device=dy.device)
+                # C = dx + c0 is the part's own gradient buffer (row stride k)
+                nat.check(nat.lib().td7_dense_bwd_data_cols(nat.ptr(dy), M * N, N, nat.ptr(y), M * N, N, nat.ptr(w),
+                                                            g.data_ptr() - 4 * c0, M * k, k, G, int(shared), M, N, K,
+                                                            c0, c0 + k, act, s), "td7_dense_bwd_data")
+            grads.append(g)
+            c0 += k
+        return (dw, db, None, *grads)
+
+
+def _cat_ok(parts, w):
+    """The concatenated-input kernels apply: <= 4 parts, interior widths
+    multiples of 4, the last >= 4 wide, N >= 4, fp32 on the GPU."""
+    if not (1 < len(parts) <= 4) or w.shape[-2] < 4:
+        return False
+    widths = [p.shape[-1] for p in parts]
+    if any(k % 4 for k in widths[:-1]) or widths[-1] < 4:
+        return False
+    grouped = w.dim() == 3
+    rows = parts[0].shape[-2]
+    for p in parts:
+        if p.dtype != torch.float32 or not p.is_cuda or p.shape[-2] != rows:
+            return False
+        if p.dim() == 3 and not (grouped and p.shape[0] == w.shape[0]):
+            return False
+    return True
+
+
+def dense_cat(parts, w, b, act=0):
+    """dense(torch.cat(parts, -1), w, b, act) reading the parts in place (parts
+    of a grouped layer may be [G,M,k] or shared [M,k]).  Falls back to the
+    concatenation where the fused kernels do not apply."""
+    if _CAT and w.is_cuda and w.dtype == torch.float32 and not torch.is_autocast_enabled() and _cat_ok(parts, w) \
+            and (_matrix_prec or parts[0].shape[-2] <= _DenseFn.fwd_kernel_max_rows):
+        return _DenseCatFn.apply(w, b, act, *parts)
+    grouped = w.dim() == 3
+    if grouped and any(p.dim() == 3 for p in parts):
+        G = w.shape[0]
+        parts = [p if p.dim() == 3 else p.unsqueeze(0).expand(G, *p.shape) for p in parts]
+    return dense(torch.cat(parts, -1), w, b, act, concat_grad_cols(parts))
+
+
+_CAT = os.environ.get("EXO_TD7_CAT", "1") != "0"
 
 
 def _torch_dense(x, w, b, act):

@@ -102,8 +102,7 @@ class Actor(nn.Module):
             a = self.activ(self.l2(a))
             return torch.tanh(self.l3(a))
         a = AvgL1Norm(ops.dense(state, self.l0.weight, self.l0.bias))
-        cols = ops.concat_grad_cols([a, zs])
-        a = ops.dense(torch.cat([a, zs], 1), self.l1.weight, self.l1.bias, act, cols)
+        a = ops.dense_cat([a, zs], self.l1.weight, self.l1.bias, act)
         a = ops.dense(a, self.l2.weight, self.l2.bias, act)
         return ops.dense(a, self.l3.weight, self.l3.bias, ops.ACT_CODES["tanh"])
 
@@ -137,8 +136,7 @@ class Encoder(nn.Module):
             zsa = self.activ(self.zsa1(torch.cat([zs, action], 1)))
             zsa = self.activ(self.zsa2(zsa))
             return self.zsa3(zsa)
-        zsa = ops.dense(torch.cat([zs, action], 1), self.zsa1.weight, self.zsa1.bias, act,
-                        ops.concat_grad_cols([zs, action]))
+        zsa = ops.dense_cat([zs, action], self.zsa1.weight, self.zsa1.bias, act)
         zsa = ops.dense(zsa, self.zsa2.weight, self.zsa2.bias, act)
         return ops.dense(zsa, self.zsa3.weight, self.zsa3.bias)
 
@@ -187,14 +185,10 @@ class Critic(nn.Module):
         act = ops.act_code(self.activ)
         if act is not None and state.is_cuda:
             # both heads per layer as one grouped td7_dense launch: [2, B, *]
-            B = state.shape[0]
-            sa = torch.cat([state, action], 1)
-            embeddings = torch.cat([zsa, zs], 1)
-            q = AvgL1Norm(ops.dense(sa, self.w0, self.b0, 0, ops.concat_grad_cols([state, action])))  # -> [2, B, h]
-            # input gradient only for the parts that need one (q; zsa in the actor update)
-            cols = ops.concat_grad_cols([q, zsa, zs])
-            x = torch.cat([q, embeddings.unsqueeze(0).expand(2, B, embeddings.shape[1])], 2)
-            x = ops.dense(x, self.w1, self.b1, act, cols)
+            # the concatenations [state, action] and [q, zsa, zs] are read in
+            # place by the kernels (zsa, zs shared by the two heads)
+            q = AvgL1Norm(ops.dense_cat([state, action], self.w0, self.b0, 0))  # -> [2, B, h]
+            x = ops.dense_cat([q, zsa, zs], self.w1, self.b1, act)
             x = ops.dense(x, self.w2, self.b2, act)
             return ops.dense(x, self.w3, self.b3).squeeze(2).t()             # [B, 2]
         B, h = state.shape[0], self.hdim
@@ -425,7 +419,8 @@ class TD7Learner:
 
     def _pair_zsa(self, zs2, actions2):
         act = ops.act_code(self.fixed_encoder.activ)
-        x = self._pair_dense(torch.cat([zs2, actions2], 2), "zsa1", act)
+        W, B = self._pair["zsa1"]
+        x = ops.dense_cat([zs2, actions2], W, B, act)
         x = self._pair_dense(x, "zsa2", act)
         return self._pair_dense(x, "zsa3", 0)
 

@@ -308,6 +308,22 @@ int td7_dense_fwd(const float *x_dev, long xsg, long ldx, const float *w_dev, co
 int td7_dense_bwd_data(const float *dy_dev, long dysg, long lddy, const float *y_dev, long ysg, long ldy,
                        const float *w_dev, float *dx_dev, long dxsg, long lddx, int32_t groups, int32_t shared_input,
                        int32_t m, int32_t n, int32_t k, int32_t act, void *stream);
+/* td7_dense_fwd of a concatenated input X = [X_0 | ... | X_{nseg-1}] read in
+ * place (the reference's Linear(torch.cat([...], 1)), Agent/TD7_multi_agent.py:
+ * 70, 104, 126-129): segment s is xs[s], [G][M][widths[s]] with group stride
+ * xsg[s] (0 = shared by the groups) and row stride ldx[s]; K = sum of widths.
+ * nseg <= 4, interior widths multiples of 4, the last >= 4 (else EXO_EINVAL). */
+int td7_dense_fwd_cat(int32_t nseg, const float *const *xs_dev, const long *xsg, const long *ldx,
+                      const int32_t *widths, const float *w_dev, const float *b_dev, float *y_dev, long ysg, long ldy,
+                      int32_t groups, int32_t m, int32_t n, int32_t act, void *stream);
+
+/* td7_dense_bwd_weight of a layer whose input is given by segments (the
+ * layout of td7_dense_fwd_cat); N >= 4. */
+int td7_dense_bwd_weight_cat(const float *dy_dev, long dysg, long lddy, const float *y_dev, long ysg, long ldy,
+                             int32_t nseg, const float *const *xs_dev, const long *xsg, const long *ldx,
+                             const int32_t *widths, float *dw_dev, float *db_dev, int32_t groups, int32_t m, int32_t n,
+                             int32_t act, void *stream);
+
 /* The same for the input columns [c0, c1) only (the slice of a concatenated
  * input that requires a gradient, e.g. the critic's q part, :123-126); the
  * other columns of dX are not written. */

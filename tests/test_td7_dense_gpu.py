@@ -139,6 +139,69 @@ def test_dense_bwd_data_column_window(c0, c1, shared):
     assert bad != 0
 
 
+@pytest.mark.parametrize("case", ["plain2", "grouped3", "grouped_shared2", "pairs"])
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_dense_cat_matches_concatenation(case, prec):
+    """td7_dense_fwd_cat / bwd_weight_cat / per-part bwd_data against the same
+    layer on torch.cat of the parts: forward, every part's gradient (only for
+    parts that require one), dW and db."""
+    from exo_amd import ops
+    torch.manual_seed(hash(case) % 1000)
+    M = 777
+    mk = lambda *s: torch.randn(*s, device="cuda")
+    if case == "plain2":      # Encoder.zsa1: [zs | action]
+        parts, w, b, need = [mk(M, 300), mk(M, 7)], mk(300, 307) / 17, mk(300), [True, True]
+    elif case == "grouped3":  # critic layer 1: [q (per head) | zsa | zs (shared)]
+        parts, w, b, need = [mk(2, M, 320), mk(M, 300), mk(M, 300)], mk(2, 320, 920) / 30, mk(2, 320), [True, True, False]
+    elif case == "grouped_shared2":  # critic layer 0: [state | action], both shared
+        parts, w, b, need = [mk(M, 80), mk(M, 7)], mk(2, 320, 87) / 9, mk(2, 320), [False, True]
+    else:                     # paired fixed encoders' zsa1: [zs2 | actions2] per group
+        parts, w, b, need = [mk(2, M, 300), mk(2, M, 7)], mk(2, 300, 307) / 17, mk(2, 300), [True, False]
+    outs = []
+    for fused in (True, False):
+        ps = [p.clone().requires_grad_(r) for p, r in zip(parts, need)]
+        ww, bb = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+        with ops.matrix_precision(prec):
+            if fused:
+                y = ops.dense_cat(ps, ww, bb, 2)
+            else:
+                if w.dim() == 3 and any(p.dim() == 3 for p in ps):
+                    full = torch.cat([p if p.dim() == 3 else p.unsqueeze(0).expand(w.shape[0], *p.shape)
+                                      for p in ps], -1)
+                else:
+                    full = torch.cat(ps, -1)
+                y = ops.dense(full, ww, bb, 2)
+        torch.manual_seed(7)  # the same output gradient for both
+        y.backward(torch.randn_like(y))
+        outs.append((y.detach(), ww.grad, bb.grad, [p.grad for p in ps]))
+    tol = 1e-5 if prec == "fp32" else 2e-3
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=tol, atol=tol)
+    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=tol, atol=tol * 30)
+    torch.testing.assert_close(outs[0][2], outs[1][2], rtol=tol, atol=tol * 30)
+    for a, r, n in zip(outs[0][3], outs[1][3], need):
+        if n:
+            torch.testing.assert_close(a, r, rtol=tol, atol=tol * 10)
+        else:
+            assert a is None and r is None
+
+
+def test_dense_cat_rejects_bad_layouts():
+    from exo_amd import _native as nat
+    import ctypes
+    x = torch.zeros(8, 6, device="cuda")
+    w = torch.zeros(4, 12, device="cuda")
+    y = torch.zeros(8, 4, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    P = (ctypes.c_void_p * 2)(x.data_ptr(), x.data_ptr())
+    sg, ld = (ctypes.c_long * 2)(0, 0), (ctypes.c_long * 2)(6, 6)
+    assert nat.lib().td7_dense_fwd_cat(2, P, sg, ld, (ctypes.c_int32 * 2)(6, 6), nat.ptr(w), None, nat.ptr(y), 32, 4,
+                                       1, 8, 4, 0, s) != 0  # interior width 6 not a multiple of 4
+    assert nat.lib().td7_dense_fwd_cat(2, P, sg, ld, (ctypes.c_int32 * 2)(8, 2), nat.ptr(w), None, nat.ptr(y), 32, 4,
+                                       1, 8, 4, 0, s) != 0  # last part narrower than 4
+    assert nat.lib().td7_dense_fwd_cat(5, P, sg, ld, (ctypes.c_int32 * 2)(4, 4), nat.ptr(w), None, nat.ptr(y), 32, 4,
+                                       1, 8, 4, 0, s) != 0  # too many parts
+
+
 def test_critic_actor_update_gradients_with_partial_inputs():
     """The actor-update pattern: the critic's zs and the encoder's zs are
     constants, only the action path needs input gradients (column windows)."""
