@@ -58,8 +58,8 @@ __global__ __launch_bounds__(T) void q_target_kernel(const float *qt, long qs_b,
 }
 
 __global__ __launch_bounds__(T) void critic_loss_kernel(const float *q, long qs_b, long qs_h, const float *qtarget,
-                                                        float *loss, float *priority, float *dq, float alpha,
-                                                        float min_priority, int B) {
+                                                        float *loss, float *priority, float *dq, long dqs_b,
+                                                        long dqs_h, float alpha, float min_priority, int B) {
     __shared__ float sh[T / 64];
     float acc = 0.f;
     const float inv_b = 1.0f / (float)B;
@@ -71,7 +71,7 @@ __global__ __launch_bounds__(T) void critic_loss_kernel(const float *q, long qs_
             const float x = fabsf(d);
             acc += x < 1.0f ? 0.5f * x * x : x;               // LAP_huber, min_priority = 1 (:259)
             const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
-            dq[2 * b + hd] = inv_b * (x < 1.0f ? x : 1.0f) * sg;
+            dq[b * dqs_b + hd * dqs_h] = inv_b * (x < 1.0f ? x : 1.0f) * sg;
             tdmax = fmaxf(tdmax, x);
         }
         priority[b] = powf(fmaxf(tdmax, min_priority), alpha);
@@ -164,9 +164,16 @@ int td7_q_target(const float *qt, long qs_b, long qs_h, const float *reward, con
 
 int td7_critic_loss(const float *q, long qs_b, long qs_h, const float *q_target, float *loss, float *priority,
                     float *dq, float alpha, float min_priority, int32_t batch, void *stream) {
+    return td7_critic_loss_strided(q, qs_b, qs_h, q_target, loss, priority, dq, 2, 1, alpha, min_priority, batch,
+                                   stream);
+}
+
+int td7_critic_loss_strided(const float *q, long qs_b, long qs_h, const float *q_target, float *loss,
+                            float *priority, float *dq, long dqs_b, long dqs_h, float alpha, float min_priority,
+                            int32_t batch, void *stream) {
     if (!q || !q_target || !loss || !priority || !dq || batch <= 0) return EXO_EINVAL;
     hipLaunchKernelGGL(critic_loss_kernel, dim3(1), dim3(T), 0, (hipStream_t)stream, q, qs_b, qs_h, q_target, loss,
-                       priority, dq, alpha, min_priority, batch);
+                       priority, dq, dqs_b, dqs_h, alpha, min_priority, batch);
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 

@@ -128,6 +128,69 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_kernel(float *__restrict__ 
         }
     }
 }
+
+// Several FlatAdam steps in one launch, the gradients read where autograd left
+// them (one tensor per parameter: no concatenation into a flat buffer).
+struct AdamOpt {
+    float *p, *m, *v, *step;
+    float lr, b1, b2, eps, wd;
+};
+struct AdamSeg {
+    const float *g;
+    long off; // into the optimiser's flat p / m / v
+    int n, opt;
+};
+struct AdamMulti {
+    AdamOpt o[TD7_ADAM_MAX_OPT];
+    AdamSeg s[TD7_ADAM_MAX_SEG];
+    int nopt, nseg;
+    uint32_t *ticket;
+};
+
+__global__ __launch_bounds__(ADAM_THREADS) void adam_multi_kernel(AdamMulti a) {
+    __shared__ float coef[TD7_ADAM_MAX_OPT][2];
+    if (threadIdx.x < a.nopt) {
+        const AdamOpt &o = a.o[threadIdx.x];
+        const float t = *o.step + 1.0f;
+        coef[threadIdx.x][0] = o.lr / (1.0f - powf(o.b1, t));
+        coef[threadIdx.x][1] = sqrtf(1.0f - powf(o.b2, t));
+    }
+    __syncthreads();
+    const long stride = (long)gridDim.x * ADAM_THREADS;
+    const long start = (long)blockIdx.x * ADAM_THREADS + threadIdx.x;
+    for (int k = 0; k < a.nseg; ++k) {
+        const AdamSeg sg = a.s[k];
+        const AdamOpt &o = a.o[sg.opt];
+        const float step_size = coef[sg.opt][0], bc2s = coef[sg.opt][1];
+        float *p = o.p + sg.off, *m = o.m + sg.off, *v = o.v + sg.off;
+        const float *g = sg.g;
+        const bool vec = ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) |
+                           reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v)) & 15) == 0;
+        const long n4 = vec ? sg.n >> 2 : 0;
+        for (long i = start; i < n4; i += stride) {
+            float4 pp = reinterpret_cast<float4 *>(p)[i], mm = reinterpret_cast<float4 *>(m)[i],
+                   vv = reinterpret_cast<float4 *>(v)[i];
+            const float4 gg = reinterpret_cast<const float4 *>(g)[i];
+            adam_one(pp.x, gg.x, mm.x, vv.x, step_size, bc2s, o.b1, o.b2, o.eps, o.wd, 1.0f);
+            adam_one(pp.y, gg.y, mm.y, vv.y, step_size, bc2s, o.b1, o.b2, o.eps, o.wd, 1.0f);
+            adam_one(pp.z, gg.z, mm.z, vv.z, step_size, bc2s, o.b1, o.b2, o.eps, o.wd, 1.0f);
+            adam_one(pp.w, gg.w, mm.w, vv.w, step_size, bc2s, o.b1, o.b2, o.eps, o.wd, 1.0f);
+            reinterpret_cast<float4 *>(p)[i] = pp;
+            reinterpret_cast<float4 *>(m)[i] = mm;
+            reinterpret_cast<float4 *>(v)[i] = vv;
+        }
+        for (long i = 4 * n4 + start; i < sg.n; i += stride)
+            adam_one(p[i], g[i], m[i], v[i], step_size, bc2s, o.b1, o.b2, o.eps, o.wd, 1.0f);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t done = atomicAdd(a.ticket, 1u);
+        if (done == gridDim.x - 1) {
+            for (int k = 0; k < a.nopt; ++k) *a.o[k].step = *a.o[k].step + 1.0f;
+            *a.ticket = 0u;
+        }
+    }
+}
 } // namespace
 
 extern "C" {
@@ -149,6 +212,31 @@ int td7_avgl1norm_bwd(const float *x, const float *mean_in, const float *gy, flo
     if (rows == 0) return EXO_OK;
     hipLaunchKernelGGL(avgl1_bwd_kernel, dim3((rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK), dim3(256), 0,
                        (hipStream_t)stream, x, mean_in, gy, gx, rows, cols, eps);
+    return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
+}
+
+/* nopt FlatAdam steps in one launch (see include/exo_amd.h). */
+int td7_adam_step_multi(int32_t nopt, float *const *p, float *const *m, float *const *v, float *const *step,
+                        const float *lr, const float *beta1, const float *beta2, const float *eps,
+                        const float *weight_decay, int32_t nseg, const float *const *g, const int64_t *off,
+                        const int32_t *n, const int32_t *opt, uint32_t *ticket, void *stream) {
+    if (nopt <= 0 || nopt > TD7_ADAM_MAX_OPT || nseg <= 0 || nseg > TD7_ADAM_MAX_SEG || !ticket) return EXO_EINVAL;
+    AdamMulti a{};
+    a.nopt = nopt;
+    a.nseg = nseg;
+    a.ticket = ticket;
+    for (int k = 0; k < nopt; ++k) {
+        if (!p[k] || !m[k] || !v[k] || !step[k]) return EXO_EINVAL;
+        a.o[k] = AdamOpt{p[k], m[k], v[k], step[k], lr[k], beta1[k], beta2[k], eps[k], weight_decay[k]};
+    }
+    long total = 0;
+    for (int k = 0; k < nseg; ++k) {
+        if (!g[k] || n[k] <= 0 || off[k] < 0 || opt[k] < 0 || opt[k] >= nopt) return EXO_EINVAL;
+        a.s[k] = AdamSeg{g[k], (long)off[k], n[k], opt[k]};
+        total = std::max<long>(total, n[k]);
+    }
+    const long blocks = std::min<long>(ADAM_BLOCKS, (total / 4 + ADAM_THREADS - 1) / ADAM_THREADS + 1);
+    hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)blocks), dim3(ADAM_THREADS), 0, (hipStream_t)stream, a);
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 

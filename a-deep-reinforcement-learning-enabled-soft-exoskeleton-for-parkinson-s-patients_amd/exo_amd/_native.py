@@ -95,6 +95,8 @@ EXPORTS = {
                                c_void_p, c_void_p, c_void_p, c_int32, c_void_p]),
     "td7_critic_loss": (c_int32, [c_void_p, c_long, c_long, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float,
                                   ctypes.c_float, c_int32, c_void_p]),
+    "td7_critic_loss_strided": (c_int32, [c_void_p, c_long, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_long,
+                                          c_long, ctypes.c_float, ctypes.c_float, c_int32, c_void_p]),
     "td7_noisy_action": (c_int32, [c_void_p, c_void_p, c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                    c_void_p, c_int32, c_void_p]),
     "td7_mse_fwd": (c_int32, [c_void_p, c_void_p, ctypes.c_int64, c_void_p, c_void_p, c_void_p]),
@@ -115,6 +117,9 @@ EXPORTS = {
     "td7_dense_bwd_weight_cat": (c_int32, [c_void_p, c_long, c_long, c_void_p, c_long, c_long, c_int32, c_void_p,
                                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32,
                                            c_int32, c_void_p]),
+    "td7_adam_step_multi": (c_int32, [c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_void_p]),
     "td7_dense_bwd_weight": (c_int32, [c_void_p, c_long, c_long, c_void_p, c_long, c_long, c_void_p, c_long,
                                        c_long, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32,
                                        c_void_p]),

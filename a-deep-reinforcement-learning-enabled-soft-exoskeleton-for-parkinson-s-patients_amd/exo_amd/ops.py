@@ -337,6 +337,23 @@ def critic_loss(q, q_target, alpha, min_priority):
     return _CriticLossFn.apply(q, q_target, alpha, min_priority)
 
 
+def critic_loss_and_grad(q, q_target, alpha, min_priority):
+    """GPU: (loss, priority, dloss/dq) in one td7_critic_loss launch with dq in
+    q's own strides -- the caller back-propagates dq from q directly
+    (torch.autograd.backward(q, dq)): no ones-seed fill, no dq * dloss
+    multiply, and for the critic's [2,B] head layout viewed as [B,2] no copy
+    before the last layer's backward."""
+    B = q.shape[0]
+    loss = torch.empty((), dtype=torch.float32, device=q.device)
+    prio = torch.empty((B,), dtype=torch.float32, device=q.device)
+    dq = torch.empty_strided(q.shape, q.stride(), dtype=torch.float32, device=q.device)
+    nat.check(nat.lib().td7_critic_loss_strided(nat.ptr(q), q.stride(0), q.stride(1), nat.ptr(q_target.contiguous()),
+                                                nat.ptr(loss), nat.ptr(prio), nat.ptr(dq), dq.stride(0), dq.stride(1),
+                                                float(alpha), float(min_priority), B, nat.stream_ptr(q.device)),
+              "td7_critic_loss")
+    return loss, prio, dq
+
+
 # ---------------------------------------------------------------- small fusions
 def noisy_action(a, noise, sigma, sigma_dec, clip=0.0, scale=1.0):
     """clamp(a + c(noise * sigma), -1, 1) * scale with c = clamp(+-clip) when

@@ -19,6 +19,7 @@ CPU parity tests run it against the reference's golden train() steps); Agent
 adds the replay buffer, the checkpoint policy and data parallelism.
 """
 import copy
+import ctypes
 import os
 from dataclasses import dataclass, field
 from typing import Callable
@@ -273,6 +274,49 @@ class FlatAdam(torch.optim.Adam):
                                           nat.stream_ptr(self.flat.device)), "td7_adam_step")
 
 
+    MAX_OPT, MAX_SEG = 3, 40  # include/exo_amd.h TD7_ADAM_MAX_*
+    _multi_ticket = {}
+
+    @staticmethod
+    @torch.no_grad()
+    def step_many(opts):
+        """The steps of several FlatAdams (GPU, grad_scale 1) as ONE
+        td7_adam_step_multi launch reading each parameter's gradient where
+        autograd left it -- no concatenation into a flat gradient buffer.
+        Parameters without a gradient are skipped (torch.optim.Adam)."""
+        segs = []
+        for k, o in enumerate(opts):
+            off = 0
+            for p in o._params():
+                if p.grad is not None:
+                    segs.append((p.grad.contiguous(), off, p.numel(), k))
+                off += p.numel()
+        if not segs:
+            return
+        if len(opts) > FlatAdam.MAX_OPT or len(segs) > FlatAdam.MAX_SEG:
+            for o in opts:
+                o.step()
+            return
+        dev = opts[0].flat.device
+        ticket = FlatAdam._multi_ticket.get(dev)
+        if ticket is None:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("FlatAdam.step_many: run once eagerly before graph capture")
+            ticket = FlatAdam._multi_ticket[dev] = torch.zeros((1,), dtype=torch.int32, device=dev)
+        n = len(opts)
+        P = lambda ts: (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])  # noqa: E731
+        F32 = lambda vs: (ctypes.c_float * n)(*[float(v) for v in vs])  # noqa: E731
+        grps = [o.param_groups[0] for o in opts]
+        ns = len(segs)
+        nat.check(nat.lib().td7_adam_step_multi(
+            n, P([o.flat for o in opts]), P([o.m for o in opts]), P([o.v for o in opts]), P([o._step for o in opts]),
+            F32([g["lr"] for g in grps]), F32([g["betas"][0] for g in grps]), F32([g["betas"][1] for g in grps]),
+            F32([g["eps"] for g in grps]), F32([g["weight_decay"] for g in grps]), ns,
+            (ctypes.c_void_p * ns)(*[sg[0].data_ptr() for sg in segs]), (ctypes.c_int64 * ns)(*[sg[1] for sg in segs]),
+            (ctypes.c_int32 * ns)(*[sg[2] for sg in segs]), (ctypes.c_int32 * ns)(*[sg[3] for sg in segs]),
+            nat.ptr(ticket), nat.stream_ptr(dev)), "td7_adam_step_multi")
+
+
 class GradSync:
     """Data-parallel gradient exchange: one flat fp32 bucket per module set,
     one all-reduce (AVG) per optimiser step (RCCL over xGMI; gloo on CPU)."""
@@ -523,9 +567,14 @@ class TD7Learner:
                 Q = self.critic(state, action, fixed_zsa, fixed_zs)
         # LAP_huber critic loss and the new priorities (:257-262): one
         # td7_critic_loss launch forward, one multiply backward
-        critic_loss, priority = ops.critic_loss(Q.float(), Q_target, hp.alpha, hp.min_priority)
         self.critic_optimizer.zero_grad(set_to_none=self.grads_to_none)
-        critic_loss.backward()
+        if Q.is_cuda and Q.dtype == torch.float32:
+            # dloss/dQ from the loss kernel, back-propagated from Q directly
+            critic_loss, priority, dQ = ops.critic_loss_and_grad(Q, Q_target, hp.alpha, hp.min_priority)
+            torch.autograd.backward(Q, dQ)
+        else:
+            critic_loss, priority = ops.critic_loss(Q.float(), Q_target, hp.alpha, hp.min_priority)
+            critic_loss.backward()
         if side is not None:
             self.join_side()
         self._fixed_zs = fixed_zs
@@ -571,6 +620,9 @@ class TD7Learner:
             self.encoder_optimizer.step(flat_grad=flat_grad[:ne], grad_scale=grad_scale)
             self.critic_optimizer.step(flat_grad=flat_grad[ne:], grad_scale=grad_scale)
             return
+        if isinstance(self.encoder_optimizer, FlatAdam) and self.device.type == "cuda":
+            FlatAdam.step_many([self.encoder_optimizer, self.critic_optimizer])
+            return
         self.encoder_optimizer.step()
         self.critic_optimizer.step()
 
@@ -581,25 +633,44 @@ class TD7Learner:
             actor = self.actor(state, fixed_zs)
             fixed_zsa = self.fixed_encoder.zsa(fixed_zs, actor)
             Q = self.critic(state, actor, fixed_zsa, fixed_zs)
-        actor_loss = -Q.float().mean()
-        if self.offline:
-            actor_loss = actor_loss + self.hp.lmbda * Q.float().abs().mean().detach() * F.mse_loss(actor.float(),
-                                                                                               action)
         self.actor_optimizer.zero_grad(set_to_none=self.grads_to_none)
         # gradients of the actor's parameters only: the reference's backward()
         # also accumulates critic / fixed-encoder gradients that its next
         # zero_grad() discards (:275-277) -- skipping them skips their GEMMs
         params = list(self.actor.parameters())
-        grads = torch.autograd.grad(actor_loss, params)
+        if Q.is_cuda and Q.dtype == torch.float32 and not self.offline:
+            # d(-Q.mean())/dQ is the constant -1/Q.numel(): back-propagated from
+            # Q directly (a cached tensor in Q's strides, no loss kernels)
+            grads = torch.autograd.grad(Q, params, grad_outputs=self._neg_mean_grad(Q))
+        else:
+            actor_loss = -Q.float().mean()
+            if self.offline:
+                actor_loss = actor_loss + self.hp.lmbda * Q.float().abs().mean().detach() * F.mse_loss(actor.float(),
+                                                                                                   action)
+            grads = torch.autograd.grad(actor_loss, params)
         for p, g in zip(params, grads):
             if p.grad is None:
                 p.grad = g
             else:
                 p.grad.add_(g)
 
+    def _neg_mean_grad(self, Q):
+        key = (tuple(Q.shape), Q.stride(), Q.device)
+        cache = getattr(self, "_nmg", None)
+        if cache is None or cache[0] != key:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("actor update: run once eagerly before graph capture")
+            g = torch.empty_strided(Q.shape, Q.stride(), dtype=torch.float32, device=Q.device)
+            g.fill_(-1.0 / Q.numel())
+            self._nmg = cache = (key, g)
+        return cache[1]
+
     def phase_actor_step(self, flat_grad=None, grad_scale=1.0):
         if flat_grad is not None and isinstance(self.actor_optimizer, FlatAdam):
             self.actor_optimizer.step(flat_grad=flat_grad, grad_scale=grad_scale)
+            return
+        if isinstance(self.actor_optimizer, FlatAdam) and self.device.type == "cuda":
+            FlatAdam.step_many([self.actor_optimizer])
             return
         self.actor_optimizer.step()
 

@@ -266,6 +266,19 @@ int td7_adam_step(float *p_dev, const float *g_dev, float *m_dev, float *v_dev, 
                   int64_t n, float lr, float beta1, float beta2, float eps, float weight_decay, float grad_scale,
                   void *stream);
 
+/* nopt FlatAdam steps (each: flat p / m / v buffers, device step count,
+ * hyper-parameters) in ONE launch, the gradients read from nseg separate
+ * tensors: segment k is g[k][0 .. n[k]) for the parameters at flat offset
+ * off[k] of optimiser opt[k] (a parameter without gradient has no segment and
+ * is skipped, as torch.optim.Adam skips it).  grad_scale 1.  The steps of all
+ * optimisers advance by one; ticket_dev as td7_adam_step (its own, one uint32). */
+#define TD7_ADAM_MAX_OPT 3
+#define TD7_ADAM_MAX_SEG 40
+int td7_adam_step_multi(int32_t nopt, float *const *p_dev, float *const *m_dev, float *const *v_dev,
+                        float *const *step_dev, const float *lr, const float *beta1, const float *beta2,
+                        const float *eps, const float *weight_decay, int32_t nseg, const float *const *g_dev,
+                        const int64_t *off, const int32_t *n, const int32_t *opt, uint32_t *ticket_dev, void *stream);
+
 /* Critic target (Agent/TD7_multi_agent.py:240-246): out[b] = reward[b] +
  * not_done[b] * discount * clamp(min(qt[b][0], qt[b][1]), *min_target,
  * *max_target); *run_max / *run_min take the batch max / min.  qt element
@@ -277,6 +290,11 @@ int td7_q_target(const float *qt_dev, long qs_b, long qs_h, const float *reward_
  * priority[b] = max(max_h td, min_priority)^alpha, dq [batch][2] = dloss/dq. */
 int td7_critic_loss(const float *q_dev, long qs_b, long qs_h, const float *q_target_dev, float *loss_dev,
                     float *priority_dev, float *dq_dev, float alpha, float min_priority, int32_t batch, void *stream);
+/* td7_critic_loss with dloss/dQ written at dq[b*dqs_b + head*dqs_h] (the
+ * layout of the critic's output view, so the backward needs no copy). */
+int td7_critic_loss_strided(const float *q_dev, long qs_b, long qs_h, const float *q_target_dev, float *loss_dev,
+                            float *priority_dev, float *dq_dev, long dqs_b, long dqs_h, float alpha,
+                            float min_priority, int32_t batch, void *stream);
 
 /* out = clamp(a + c(noise * *sigma), -1, 1) * scale over n values, c = clamp to
  * +-clip when clip > 0; then *sigma -= sigma_dec.  The exploration noise of

@@ -85,3 +85,62 @@ def test_noisy_action_and_mse_match_torch():
     (3 * l1).backward()
     (3 * l2).backward()
     torch.testing.assert_close(x.grad, x2.grad, rtol=1e-6, atol=1e-9)
+
+
+def test_critic_loss_and_grad_writes_dq_in_q_strides():
+    """ops.critic_loss_and_grad: the same loss / priorities / dq as the
+    autograd path, dq laid out like q (the [B,2] view of the heads' [2,B])."""
+    from exo_amd import ops
+    torch.manual_seed(4)
+    B = 1000
+    target = torch.randn(B, 1, device="cuda")
+    q = torch.randn(2, B, device="cuda").t() * 2
+    loss, prio, dq = ops.critic_loss_and_grad(q, target, 0.4, 1.0)
+    assert dq.stride() == q.stride()
+    qr = q.clone().requires_grad_(True)
+    loss_r, prio_r = ops.critic_loss(qr, target, 0.4, 1.0)
+    loss_r.backward()
+    torch.testing.assert_close(loss, loss_r, rtol=0, atol=0)
+    torch.testing.assert_close(prio, prio_r, rtol=0, atol=0)
+    torch.testing.assert_close(dq, qr.grad, rtol=0, atol=0)
+
+
+def test_flat_adam_step_many_matches_separate_steps():
+    """FlatAdam.step_many (one td7_adam_step_multi launch over per-parameter
+    gradients of several optimisers) == each optimiser's own step; a
+    parameter without gradient is left alone."""
+    import copy
+
+    import torch.nn.functional as F
+    from exo_amd.td7 import Critic, Encoder, FlatAdam
+    torch.manual_seed(5)
+    nets = [Encoder(80, 7, 300, 300, F.elu).cuda(), Critic(80, 7, 300, 320, F.elu).cuda()]
+    twins = [copy.deepcopy(n) for n in nets]
+    opts = [FlatAdam(nets[0], lr=3e-4, weight_decay=1e-7), FlatAdam(nets[1], lr=1e-3, weight_decay=1e-7)]
+    refs = [FlatAdam(twins[0], lr=3e-4, weight_decay=1e-7), FlatAdam(twins[1], lr=1e-3, weight_decay=1e-7)]
+    for it in range(3):
+        for a, b in zip(nets, twins):
+            for i, (p, q) in enumerate(zip(a.parameters(), b.parameters())):
+                g = torch.randn_like(p)
+                p.grad, q.grad = g.clone(), g.clone()
+        skip = list(nets[0].parameters())[1]
+        skip_before = skip.detach().clone()
+        skip.grad = None
+        FlatAdam.step_many(opts)
+        # reference: the same update with the skipped parameter's gradient zero
+        # and its value / moments restored afterwards
+        rskip = list(twins[0].parameters())[1]
+        keep = (rskip.detach().clone(), refs[0].state[rskip]["exp_avg"].clone(), refs[0].state[rskip]["exp_avg_sq"].clone())
+        rskip.grad = torch.zeros_like(rskip)
+        for o in refs:
+            o.step()
+        with torch.no_grad():
+            rskip.copy_(keep[0])
+            refs[0].state[rskip]["exp_avg"].copy_(keep[1])
+            refs[0].state[rskip]["exp_avg_sq"].copy_(keep[2])
+        torch.testing.assert_close(skip.detach(), skip_before, rtol=0, atol=0)
+        for a, b in zip(nets, twins):
+            for p, q in zip(a.parameters(), b.parameters()):
+                torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-6, atol=1e-7)
+        for o, r in zip(opts, refs):
+            assert float(o._step) == float(r._step) == it + 1
