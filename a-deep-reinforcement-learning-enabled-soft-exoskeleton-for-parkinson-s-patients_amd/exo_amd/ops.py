@@ -260,6 +260,95 @@ def dense_cat(parts, w, b, act=0):
 _CAT = os.environ.get("EXO_TD7_CAT", "1") != "0"
 
 
+def pair_rows(a, b):
+    """torch.stack([a, b]) for two equally shaped row-major tensors -- a view
+    without a copy when b directly follows a in memory (the replay batch's
+    state / next_state, exo_amd/replay.py); else the stack."""
+    if (a.dim() == 2 and a.shape == b.shape and a.dtype == b.dtype and a.device == b.device and a.is_contiguous()
+            and b.is_contiguous() and b.data_ptr() == a.data_ptr() + a.numel() * a.element_size()
+            and not (a.requires_grad or b.requires_grad)):
+        return a.as_strided((2, *a.shape), (a.numel(), *a.stride()))
+    return torch.stack([a, b])
+
+
+def _dense_raw(x, w, b, act):
+    """Forward of one fused layer outside autograd -> y (x [M,K] row-major)."""
+    x, ldx = _rows(x)
+    M, N, K = x.shape[0], w.shape[0], w.shape[1]
+    y = torch.empty((M, N), dtype=torch.float32, device=x.device)
+    nat.check(nat.lib().td7_dense_fwd(nat.ptr(x), 0, ldx, nat.ptr(w), nat.ptr(b), nat.ptr(y), M * N, N, 1, M, N, K,
+                                      act | _matrix_prec << 8, nat.stream_ptr(x.device)), "td7_dense_fwd")
+    return y
+
+
+class _ZsHalfGradFn(torch.autograd.Function):
+    """The encoder's zs = AvgL1Norm(L3(act(L2(act(L1(x)))))) over 2B rows whose
+    first B rows need gradients and the last B do not (Agent/TD7_multi_agent.py:
+    220-223: zs(state) trained, zs(next_state) under no_grad): one launch per
+    layer forward over all 2B rows, the backward over the first B rows only --
+    no zero-padded gradient for the detached half (autograd's slice backward
+    would fill and copy one)."""
+
+    @staticmethod
+    def forward(ctx, x, B, act, w1, b1, w2, b2, w3, b3):
+        prec = _matrix_prec
+        w1, w2, w3 = w1.contiguous(), w2.contiguous(), w3.contiguous()
+        h1 = _dense_raw(x, w1, b1, act)
+        h2 = _dense_raw(h1, w2, b2, act)
+        h3 = _dense_raw(h2, w3, b3, 0)
+        zs = torch.empty_like(h3)
+        mean = torch.empty((h3.shape[0],), dtype=torch.float32, device=h3.device)
+        nat.check(nat.lib().td7_avgl1norm_fwd(nat.ptr(h3), nat.ptr(zs), nat.ptr(mean), h3.shape[0], h3.shape[1],
+                                              1e-8, nat.stream_ptr(h3.device)), "td7_avgl1norm_fwd")
+        ctx.save_for_backward(x, h1, h2, h3, mean, w1, w2, w3)
+        ctx.meta = (B, act, prec)
+        nxt = zs[B:]
+        ctx.mark_non_differentiable(nxt)
+        return zs[:B], nxt
+
+    @staticmethod
+    def backward(ctx, gzs, _gnext):
+        x, h1, h2, h3, mean, w1, w2, w3 = ctx.saved_tensors
+        B, act, prec = ctx.meta
+        s = nat.stream_ptr(gzs.device)
+        L = nat.lib()
+        gzs = gzs.contiguous()
+        g3 = torch.empty((B, h3.shape[1]), dtype=torch.float32, device=gzs.device)
+        nat.check(L.td7_avgl1norm_bwd(nat.ptr(h3), nat.ptr(mean), nat.ptr(gzs), nat.ptr(g3), B, h3.shape[1], 1e-8, s),
+                  "td7_avgl1norm_bwd")
+        grads = []
+        x1, ldx1 = _rows(x)
+        # (dY, Y, act, W, X, row stride of X, need dX) per layer, last first
+        layers = ((h3, 0, w3, h2, h2.shape[1], True), (h2, act, w2, h1, h1.shape[1], True),
+                  (h1, act, w1, x1, ldx1, False))
+        dy = g3
+        for y, a, w, xin, ldx, need_dx in layers:
+            N, K = w.shape
+            code = a | prec << 8
+            dw = torch.empty_like(w)
+            db = torch.empty((N,), dtype=torch.float32, device=w.device)
+            nat.check(L.td7_dense_bwd_weight(nat.ptr(dy), B * N, N, nat.ptr(y), B * N, N, nat.ptr(xin), 0, ldx,
+                                             nat.ptr(dw), nat.ptr(db), 1, B, N, K, code, s), "td7_dense_bwd_weight")
+            dx = None
+            if need_dx:
+                dx = torch.empty((B, K), dtype=torch.float32, device=w.device)
+                nat.check(L.td7_dense_bwd_data(nat.ptr(dy), B * N, N, nat.ptr(y), B * N, N, nat.ptr(w), nat.ptr(dx),
+                                               B * K, K, 1, 0, B, N, K, code, s), "td7_dense_bwd_data")
+            grads.append((dw, db))
+            dy = dx
+        (dw3, db3), (dw2, db2), (dw1, db1) = grads
+        return None, None, None, dw1, db1, dw2, db2, dw3, db3
+
+
+def encoder_zs_half_grad(x, B, act, layers):
+    """(zs(x[:B]) with gradients, zs(x[B:]) without) -- see _ZsHalfGradFn.
+    layers: the three (weight, bias) pairs."""
+    if x.requires_grad:
+        raise ValueError("encoder_zs_half_grad: the input rows take no gradient")
+    (w1, b1), (w2, b2), (w3, b3) = layers
+    return _ZsHalfGradFn.apply(x, B, act, w1, b1, w2, b2, w3, b3)
+
+
 def _torch_dense(x, w, b, act):
     if w.dim() == 3:
         xx = x if x.dim() == 3 else x.unsqueeze(0).expand(w.shape[0], *x.shape)

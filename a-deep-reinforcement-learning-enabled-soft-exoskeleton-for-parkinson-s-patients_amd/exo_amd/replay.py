@@ -65,8 +65,11 @@ class LAP:
                                          self.reward.data_ptr(), self.not_done.data_ptr(), state_dim, action_dim,
                                          self.ptr_s.data_ptr(), self.size_s.data_ptr())
         B = E * self.batch_size  # sampled batch, written in place by lap_sample_gather (static for HIP graphs)
-        self._batch = (torch.empty((B, state_dim), **f32), torch.empty((B, action_dim), **f32),
-                       torch.empty((B, state_dim), **f32), torch.empty((B, 1), **f32), torch.empty((B, 1), **f32))
+        # state and next_state adjacent in one [2, B, dim] buffer: the learner's
+        # paired passes over both read it as one tensor (ops.pair_rows), no stack / cat
+        sn = torch.empty((2, B, state_dim), **f32)
+        self._batch = (sn[0], torch.empty((B, action_dim), **f32), sn[1], torch.empty((B, 1), **f32),
+                       torch.empty((B, 1), **f32))
         self._row_ws = None
         self._init_tree()
 

@@ -456,7 +456,7 @@ class TD7Learner:
     def _pair_zs(self, state, next_state):
         """[fixed_encoder.zs(state), fixed_encoder_target.zs(next_state)] as [2, B, zs_dim]."""
         act = ops.act_code(self.fixed_encoder.activ)
-        x = torch.stack([state, next_state])
+        x = ops.pair_rows(state, next_state)
         x = self._pair_dense(x, "zs1", act)
         x = self._pair_dense(x, "zs2", act)
         return AvgL1Norm(self._pair_dense(x, "zs3", 0))
@@ -505,8 +505,15 @@ class TD7Learner:
             # zs(state) and zs(next_state) of the live encoder as one pass; the
             # next-state half is detached (it is computed under no_grad at :220)
             B = state.shape[0]
-            zs_all = self.encoder.zs(torch.cat([state, next_state], 0))
-            zs, next_zs = zs_all[:B], zs_all[B:].detach()
+            enc = self.encoder
+            act = ops.act_code(enc.activ)
+            if state.is_cuda and act is not None and state.dtype == torch.float32 and not state.requires_grad:
+                # one launch per layer over both halves, backward over the first only
+                zs, next_zs = ops.encoder_zs_half_grad(ops.pair_rows(state, next_state).view(2 * B, -1), B, act,
+                                                       [(l.weight, l.bias) for l in (enc.zs1, enc.zs2, enc.zs3)])
+            else:
+                zs_all = enc.zs(torch.cat([state, next_state], 0))
+                zs, next_zs = zs_all[:B], zs_all[B:].detach()
             pred_zs = self.encoder.zsa(zs, action)
         encoder_loss = ops.mse_loss(pred_zs.float(), next_zs.float())
         self.encoder_optimizer.zero_grad(set_to_none=self.grads_to_none)

@@ -282,3 +282,34 @@ def test_reduced_precision_rejects_bad_codes():
     rc = nat.lib().td7_dense_fwd(nat.ptr(x), 0, 4, nat.ptr(x), None, nat.ptr(y), 16, 4, 1, 4, 4, 4, 3 << 8,
                                  nat.stream_ptr(x.device))
     assert rc == -22
+
+
+def test_encoder_zs_half_grad_matches_autograd_slices():
+    """ops.encoder_zs_half_grad (forward over 2B rows, backward over the first
+    B) == the reference expression zs(cat)[:B] / [B:].detach() under autograd."""
+    import copy
+
+    import torch.nn.functional as F
+    from exo_amd import ops
+    from exo_amd.td7 import Encoder
+    torch.manual_seed(9)
+    B = 300
+    sn = torch.randn(2, B, 80, device="cuda")
+    enc = Encoder(80, 7, 300, 300, F.elu).cuda()
+    ref = copy.deepcopy(enc)
+    x = ops.pair_rows(sn[0], sn[1])
+    assert x.data_ptr() == sn.data_ptr()
+    zs, nxt = ops.encoder_zs_half_grad(x.view(2 * B, 80), B, 2, [(l.weight, l.bias) for l in (enc.zs1, enc.zs2, enc.zs3)])
+    allr = ref.zs(torch.cat([sn[0], sn[1]], 0))
+    zr, nr = allr[:B], allr[B:].detach()
+    torch.testing.assert_close(zs, zr, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(nxt, nr, rtol=1e-5, atol=1e-5)
+    assert not nxt.requires_grad
+    g = torch.randn_like(zs)
+    zs.backward(g)
+    zr.backward(g)
+    for p, q in zip(enc.parameters(), ref.parameters()):
+        if p.grad is None:
+            assert q.grad is None or not q.grad.any()
+            continue
+        torch.testing.assert_close(p.grad, q.grad, rtol=1e-4, atol=1e-6)
