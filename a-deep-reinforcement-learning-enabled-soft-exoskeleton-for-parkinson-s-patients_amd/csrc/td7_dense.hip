@@ -30,7 +30,9 @@ namespace td7dense {
     extern template void launch_wgrad_p<P, false>(const WgradArgs &, dim3, int, int, int, hipStream_t); \
     extern template void launch_wgrad_p<P, true>(const WgradArgs &, dim3, int, int, int, hipStream_t);  \
     extern template void launch_fwd_p<P, false>(const GemmArgs &, dim3, int, int, int, int, hipStream_t); \
-    extern template void launch_fwd_p<P, true>(const GemmArgs &, dim3, int, int, int, int, hipStream_t);
+    extern template void launch_fwd_p<P, true>(const GemmArgs &, dim3, int, int, int, int, hipStream_t); \
+    extern template void launch_fwd_norm_p<P, false>(const GemmArgs &, dim3, float *, float *, float, hipStream_t); \
+    extern template void launch_fwd_norm_p<P, true>(const GemmArgs &, dim3, float *, float *, float, hipStream_t);
 TD7_EXTERN(PREC_F32)
 TD7_EXTERN(PREC_BF16)
 TD7_EXTERN(PREC_F16)
@@ -140,6 +142,24 @@ static int make_cat(CatSeg &c, int nseg, const float *const *xs, const long *xsg
     return k;
 }
 
+static int launch_fwd_norm(const GemmArgs &a, int groups, int prec, float *h, float *mean, float eps, hipStream_t s, bool cat) {
+    if (a.J > 320) return EXO_EINVAL; // 4 waves x 5 column tiles per workgroup
+    const long span_a = cat ? 0 : (long)groups * a.A.sg + (long)a.I * a.A.si + (long)a.R;
+    const long span_b = (long)groups * a.B.sg + (long)a.J * a.B.si + (long)a.R;
+    if (span_a >= (1L << 29) || span_b >= (1L << 29)) return EXO_ERANGE;
+    const dim3 grid((a.I + 15) / 16, groups);
+    if (cat) {
+        if (prec == PREC_BF16) launch_fwd_norm_p<PREC_BF16, true>(a, grid, h, mean, eps, s);
+        else if (prec == PREC_F16) launch_fwd_norm_p<PREC_F16, true>(a, grid, h, mean, eps, s);
+        else launch_fwd_norm_p<PREC_F32, true>(a, grid, h, mean, eps, s);
+    } else {
+        if (prec == PREC_BF16) launch_fwd_norm_p<PREC_BF16, false>(a, grid, h, mean, eps, s);
+        else if (prec == PREC_F16) launch_fwd_norm_p<PREC_F16, false>(a, grid, h, mean, eps, s);
+        else launch_fwd_norm_p<PREC_F32, false>(a, grid, h, mean, eps, s);
+    }
+    return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
+}
+
 Operand plain(const float *p, long sg, long si, long sr) {
     Operand o{};
     o.p = p;
@@ -218,6 +238,62 @@ int td7_dense_fwd_cat(int32_t nseg, const float *const *xs, const long *xsg, con
     a.act = act;
     a.j_bias = -1;
     return launch_fwd(a, groups, prec, (hipStream_t)stream, true);
+}
+
+/* y = AvgL1Norm(X W^T + b) per output row (no activation), N <= 320: one
+ * launch for td7_dense_fwd + td7_avgl1norm_fwd.  Layout as td7_dense_fwd (y:
+ * [G][M][N] with group stride ysg, row stride ldy); h (pre-norm, same layout)
+ * and mean ([G][M], the raw mean |h|) are written when non-null.  prec: the
+ * MFMA operand precision (Prec). */
+int td7_dense_fwd_norm(const float *x, long xsg, long ldx, const float *w, const float *b, float *y, float *h,
+                       float *mean, long ysg, long ldy, int32_t groups, int32_t m, int32_t n, int32_t k, int32_t prec,
+                       float eps, void *stream) {
+    if (!x || !w || !y || groups <= 0 || m < 0 || n <= 0 || n > 320 || k <= 0 || prec < 0 || prec > PREC_F16)
+        return EXO_EINVAL;
+    if (m == 0) return EXO_OK;
+    GemmArgs a{};
+    a.A = plain(x, xsg, ldx, 1);
+    a.B = plain(w, (long)n * k, k, 1);
+    a.I = m;
+    a.J = n;
+    a.R = k;
+    a.groups_red = 1;
+    a.C = y;
+    a.csg = ysg;
+    a.csi = ldy;
+    a.csj = 1;
+    a.bias = b;
+    a.bsg = n;
+    a.act = ACT_NONE;
+    a.j_bias = -1;
+    return launch_fwd_norm(a, groups, prec, h, mean, eps, (hipStream_t)stream, false);
+}
+
+/* td7_dense_fwd_norm of a concatenated input (td7_dense_fwd_cat's segments). */
+int td7_dense_fwd_norm_cat(int32_t nseg, const float *const *xs, const long *xsg, const long *ldx,
+                           const int32_t *widths, const float *w, const float *b, float *y, float *h, float *mean,
+                           long ysg, long ldy, int32_t groups, int32_t m, int32_t n, int32_t prec, float eps,
+                           void *stream) {
+    if (!w || !y || groups <= 0 || m < 0 || n <= 0 || n > 320 || prec < 0 || prec > PREC_F16) return EXO_EINVAL;
+    GemmArgs a{};
+    const int k = make_cat(a.cat, nseg, xs, xsg, ldx, widths);
+    if (k <= 0) return EXO_EINVAL;
+    if (m == 0) return EXO_OK;
+    a.A = plain(xs[0], 0, 0, 1);
+    a.B = plain(w, (long)n * k, k, 1);
+    a.I = m;
+    a.J = n;
+    a.R = k;
+    a.groups_red = 1;
+    a.C = y;
+    a.csg = ysg;
+    a.csi = ldy;
+    a.csj = 1;
+    a.bias = b;
+    a.bsg = n;
+    a.act = ACT_NONE;
+    a.j_bias = -1;
+    return launch_fwd_norm(a, groups, prec, h, mean, eps, (hipStream_t)stream, true);
 }
 
 /* td7_dense_bwd_weight of a layer whose input was given by segments

@@ -530,6 +530,177 @@ __global__ __launch_bounds__(64 * KW) void dense_fwd_kernel(GemmArgs a) {
     }
 }
 
+// ---- forward + AvgL1Norm ----------------------------------------------------
+// y = h / max(mean_j |h_j|, eps) with h = X W^T + b (no activation): the TD7
+// layers followed by AvgL1Norm (Agent/TD7_multi_agent.py:53-54 after :61, :103,
+// :126).  One workgroup owns 16 rows and ALL N <= 320 output columns (4 waves x
+// NT = 5 16-wide column tiles), so the row mean is a workgroup reduction and
+// the separate AvgL1Norm launch disappears.  h and the raw mean are stored when
+// hout / mean_out are given (the backward of a trained layer needs them).
+// Per 16-wide reduction step a lane loads one A (b128, shared by the 4 waves
+// through L1) and NT B fragments; GS steps per prefetch group, two groups in
+// flight.
+struct CatRows { // segment bases of a CAT A operand for one group (see CatSeg)
+    const float *cb0;
+    long e1, e2, e3;
+    int kb1, kb2, kb3, cl0, dl1, dl2, dl3;
+    __device__ __forceinline__ CatRows(const CatSeg &c, int g) {
+        const float *b0 = c.p[0] + g * c.sg[0], *b1 = c.p[1] + g * c.sg[1] - c.kb[1],
+                    *b2 = c.p[2] + g * c.sg[2] - c.kb[2], *b3 = c.p[3] + g * c.sg[3] - c.kb[3];
+        cb0 = b0;
+        e1 = b1 - b0;
+        e2 = b2 - b1;
+        e3 = b3 - b2;
+        kb1 = c.kb[1];
+        kb2 = c.kb[2];
+        kb3 = c.kb[3];
+        cl0 = c.ld[0];
+        dl1 = c.ld[1] - c.ld[0];
+        dl2 = c.ld[2] - c.ld[1];
+        dl3 = c.ld[3] - c.ld[2];
+    }
+    __device__ __forceinline__ const float *ptr(int row, int r) const {
+        const int s1 = r >= kb1, s2 = r >= kb2, s3 = r >= kb3;
+        return cb0 + (s1 * e1 + s2 * e2 + s3 * e3) + (long)row * (cl0 + s1 * dl1 + s2 * dl2 + s3 * dl3) + r;
+    }
+};
+
+template <int P, bool CAT>
+__global__ __launch_bounds__(256) void dense_fwd_norm_kernel(GemmArgs a, float *hout, float *mean_out, float eps) {
+    constexpr int NT = 5, GS = 2;
+    __shared__ float red[4][16];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
+    const int i0 = blockIdx.x * 16, g = blockIdx.y, j0 = w * 16 * NT;
+    const __amdgpu_buffer_rsrc_t ra = rsrc(a.A.p), rb = rsrc(a.B.p);
+    const int row = i0 + c;
+    const bool arow = row < a.I;
+    const int abase = g * (int)a.A.sg + row * (int)a.A.si;
+    const CatRows cr(a.cat, CAT ? g : 0);
+    int bbase[NT];
+    bool bcol[NT];
+#pragma unroll
+    for (int y = 0; y < NT; ++y) {
+        const int col = j0 + 16 * y + c;
+        bbase[y] = g * (int)a.B.sg + col * (int)a.B.si;
+        bcol[y] = col < a.J;
+    }
+    floatx4 acc[NT];
+#pragma unroll
+    for (int y = 0; y < NT; ++y) acc[y] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const int nall = a.R >> 4;
+    auto load = [&](int s0, uint32_t (&av)[GS][4], uint32_t (&bv)[GS][NT][4]) {
+#pragma unroll
+        for (int s = 0; s < GS; ++s) {
+            const int r = 16 * (s0 + s) + 4 * q;
+            const bool live = s0 + s < nall;
+            if constexpr (CAT) {
+                const auto v = gload4(cr.ptr(arow ? row : 0, live ? r : 0), cr.cb0, live & arow);
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) av[s][jj] = v[jj];
+            } else {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(ra, (live & arow) ? (abase + r) * 4 : BUF_OOB, 0, 0);
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) av[s][jj] = v[jj];
+            }
+#pragma unroll
+            for (int y = 0; y < NT; ++y) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(rb, (live & bcol[y]) ? (bbase[y] + r) * 4 : BUF_OOB, 0, 0);
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) bv[s][y][jj] = v[jj];
+            }
+        }
+    };
+    auto step = [&](const float (&xa)[4], const float (&xb)[NT][4]) {
+        if constexpr (P != PREC_F32) {
+#pragma unroll
+            for (int y = 0; y < NT; ++y) acc[y] = mfma_k16<P>(xa, xb[y], acc[y]);
+        } else {
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+                for (int y = 0; y < NT; ++y) acc[y] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[jj], xb[y][jj], acc[y], 0, 0, 0);
+        }
+    };
+    auto mma = [&](const uint32_t (&av)[GS][4], const uint32_t (&bv)[GS][NT][4]) {
+#pragma unroll
+        for (int s = 0; s < GS; ++s) {
+            float xa[4], xb[NT][4];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                xa[jj] = __uint_as_float(av[s][jj]);
+#pragma unroll
+                for (int y = 0; y < NT; ++y) xb[y][jj] = __uint_as_float(bv[s][y][jj]);
+            }
+            step(xa, xb);
+        }
+    };
+    {
+        uint32_t a0[GS][4], b0[GS][NT][4], a1[GS][4], b1[GS][NT][4];
+        if (nall > 0) load(0, a0, b0);
+        for (int s0 = 0; s0 < nall; s0 += 2 * GS) {
+            if (s0 + GS < nall) load(s0 + GS, a1, b1);
+            mma(a0, b0);
+            if (s0 + GS >= nall) break;
+            if (s0 + 2 * GS < nall) load(s0 + 2 * GS, a0, b0);
+            mma(a1, b1);
+        }
+    }
+    if (a.R & 15) { // tail step
+        const int r = 16 * nall + 4 * q;
+        float xa[4], xb[NT][4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            if constexpr (CAT)
+                xa[jj] = (arow & (r + jj < a.R)) ? cr.ptr(row, r)[jj] : 0.f;
+            else
+                xa[jj] = ldb(ra, arow & (r + jj < a.R), abase + r + jj);
+#pragma unroll
+            for (int y = 0; y < NT; ++y) xb[y][jj] = ldb(rb, bcol[y] & (r + jj < a.R), bbase[y] + r + jj);
+        }
+        step(xa, xb);
+    }
+    // acc[y][k] is h[i0 + 4q + k][j0 + 16y + c] (before the bias)
+    float part[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int y = 0; y < NT; ++y) {
+        const float bv = (a.bias && bcol[y]) ? a.bias[g * a.bsg + j0 + 16 * y + c] : 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            acc[y][k] = bcol[y] ? acc[y][k] + bv : 0.f;
+            part[k] += fabsf(acc[y][k]);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) part[k] += __shfl_xor(part[k], o, 64);
+    if (c == 0)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) red[w][4 * q + k] = part[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int rr = i0 + 4 * q + k;
+        // the same summation order for every lane of the row
+        const float m = (red[0][4 * q + k] + red[1][4 * q + k] + red[2][4 * q + k] + red[3][4 * q + k]) / a.J;
+        const float sc = fmaxf(m, eps);
+        if (rr >= a.I) continue;
+        if (mean_out && w == 0 && c == 0) mean_out[(long)g * a.I + rr] = m;
+#pragma unroll
+        for (int y = 0; y < NT; ++y) {
+            if (!bcol[y]) continue;
+            const long o = g * a.csg + (long)rr * a.csi + (j0 + 16 * y + c);
+            a.C[o] = acc[y][k] / sc;
+            if (hout) hout[o] = acc[y][k];
+        }
+    }
+}
+
+template <int P, bool CAT>
+void launch_fwd_norm_p(const GemmArgs &a, dim3 grid, float *hout, float *mean_out, float eps, hipStream_t s) {
+    hipLaunchKernelGGL((dense_fwd_norm_kernel<P, CAT>), grid, dim3(256), 0, s, a, hout, mean_out, eps);
+}
+
 // ---- bwd-weight on the output-contiguous layout ------------------------------
 // dW[g][i][j] = sum_m dP[m][i] X[m][j], dP = dY * act'(Y), db[g][i] = sum_m dP[m][i].
 // Both operands are contiguous along the OUTPUT dimensions (i resp. j) and

@@ -120,6 +120,12 @@ EXPORTS = {
     "td7_adam_step_multi": (c_int32, [c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                       c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                       c_void_p]),
+    "td7_dense_fwd_norm": (c_int32, [c_void_p, c_long, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                     c_long, c_long, c_int32, c_int32, c_int32, c_int32, c_int32, ctypes.c_float,
+                                     c_void_p]),
+    "td7_dense_fwd_norm_cat": (c_int32, [c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                         c_void_p, c_void_p, c_long, c_long, c_int32, c_int32, c_int32, c_int32,
+                                         ctypes.c_float, c_void_p]),
     "td7_dense_bwd_weight": (c_int32, [c_void_p, c_long, c_long, c_void_p, c_long, c_long, c_void_p, c_long,
                                        c_long, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32,
                                        c_void_p]),

@@ -194,35 +194,125 @@ class _DenseCatFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         w, y, *parts = ctx.saved_tensors
-        grouped, G, M, N, K, act, has_b, widths, sgs, lds = ctx.meta
-        dy = dy.contiguous()
-        s = nat.stream_ptr(dy.device)
-        n = len(parts)
-        dw = db = None
-        if (ctx.needs_input_grad[0] and _engine_needs(ctx, ctx.edge[0])) or \
-                (has_b and ctx.needs_input_grad[1] and _engine_needs(ctx, ctx.edge[1])):
-            dw = torch.empty_like(w)
-            db = torch.empty((G, N) if grouped else (N,), dtype=torch.float32, device=dy.device) if has_b else None
-            seg = ((ctypes.c_void_p * n)(*[p.data_ptr() for p in parts]), (ctypes.c_long * n)(*sgs),
-                   (ctypes.c_long * n)(*lds), (ctypes.c_int32 * n)(*widths))
-            nat.check(nat.lib().td7_dense_bwd_weight_cat(nat.ptr(dy), M * N, N, nat.ptr(y), M * N, N, n, *seg,
-                                                         nat.ptr(dw), nat.ptr(db), G, M, N, act, s),
-                      "td7_dense_bwd_weight_cat")
-        grads = []
-        c0 = 0
-        for i, p in enumerate(parts):
-            k = widths[i]
-            g = None
-            if ctx.needs_input_grad[3 + i] and _engine_needs(ctx, ctx.edge[3 + i]):
-                shared = grouped and p.dim() == 2
-                g = torch.empty(p.shape, dtype=torch.float32, device=dy.device)
-                # C = dx + c0 is the part's own gradient buffer (row stride k)
-                nat.check(nat.lib().td7_dense_bwd_data_cols(nat.ptr(dy), M * N, N, nat.ptr(y), M * N, N, nat.ptr(w),
-                                                            g.data_ptr() - 4 * c0, M * k, k, G, int(shared), M, N, K,
-                                                            c0, c0 + k, act, s), "td7_dense_bwd_data")
-            grads.append(g)
-            c0 += k
-        return (dw, db, None, *grads)
+        return _parts_backward(ctx, dy, w, y, parts, ctx.meta)
+
+
+def _seg_arrays(parts, sgs, lds, widths):
+    n = len(parts)
+    return ((ctypes.c_void_p * n)(*[p.data_ptr() for p in parts]), (ctypes.c_long * n)(*sgs),
+            (ctypes.c_long * n)(*lds), (ctypes.c_int32 * n)(*widths))
+
+
+def _parts_backward(ctx, dy, w, y, parts, meta):
+    """Backward of act(cat(parts) W^T + b) (y: the layer's output, for act'):
+    (dW, db, None, grad of each part) -- see _DenseCatFn."""
+    grouped, G, M, N, K, act, has_b, widths, sgs, lds = meta
+    dy = dy.contiguous()
+    s = nat.stream_ptr(dy.device)
+    n = len(parts)
+    dw = db = None
+    if (ctx.needs_input_grad[0] and _engine_needs(ctx, ctx.edge[0])) or \
+            (has_b and ctx.needs_input_grad[1] and _engine_needs(ctx, ctx.edge[1])):
+        dw = torch.empty_like(w)
+        db = torch.empty((G, N) if grouped else (N,), dtype=torch.float32, device=dy.device) if has_b else None
+        nat.check(nat.lib().td7_dense_bwd_weight_cat(nat.ptr(dy), M * N, N, nat.ptr(y), M * N, N, n,
+                                                     *_seg_arrays(parts, sgs, lds, widths), nat.ptr(dw), nat.ptr(db),
+                                                     G, M, N, act, s), "td7_dense_bwd_weight_cat")
+    grads = []
+    c0 = 0
+    for i, p in enumerate(parts):
+        k = widths[i]
+        g = None
+        if ctx.needs_input_grad[3 + i] and _engine_needs(ctx, ctx.edge[3 + i]):
+            shared = grouped and p.dim() == 2
+            g = torch.empty(p.shape, dtype=torch.float32, device=dy.device)
+            # C = dx + c0 is the part's own gradient buffer (row stride k)
+            nat.check(nat.lib().td7_dense_bwd_data_cols(nat.ptr(dy), M * N, N, nat.ptr(y), M * N, N, nat.ptr(w),
+                                                        g.data_ptr() - 4 * c0, M * k, k, G, int(shared), M, N, K,
+                                                        c0, c0 + k, act, s), "td7_dense_bwd_data")
+        grads.append(g)
+        c0 += k
+    return (dw, db, None, *grads)
+
+
+def _parts_meta(w, parts):
+    grouped = w.dim() == 3
+    widths = [p.shape[-1] for p in parts]
+    sgs = [p.stride(0) if (grouped and p.dim() == 3) else 0 for p in parts]
+    lds = [p.stride(-2) for p in parts]
+    return grouped, widths, sgs, lds
+
+
+class _DenseNormFn(torch.autograd.Function):
+    """AvgL1Norm(cat(parts) W^T + b) (no activation) as ONE td7_dense_fwd_norm
+    launch (the row mean reduced inside the GEMM's workgroup); the backward is
+    td7_avgl1norm_bwd from the saved pre-norm h and mean, then the layer's
+    backward as _DenseCatFn.  N <= 320."""
+
+    @staticmethod
+    def forward(ctx, w, b, train, *parts):
+        parts = [_rows(p)[0] for p in parts]
+        grouped, widths, sgs, lds = _parts_meta(w, parts)
+        G = w.shape[0] if grouped else 1
+        N, K = w.shape[-2], w.shape[-1]
+        M = parts[0].shape[-2]
+        w = w.contiguous()
+        bb = b.contiguous() if b is not None else None
+        prec = _matrix_prec
+        shape = (G, M, N) if grouped else (M, N)
+        y = torch.empty(shape, dtype=torch.float32, device=w.device)
+        h = torch.empty(shape, dtype=torch.float32, device=w.device) if train else None
+        mean = torch.empty((G * M,), dtype=torch.float32, device=w.device) if train else None
+        st = nat.stream_ptr(w.device)
+        if len(parts) == 1:
+            nat.check(nat.lib().td7_dense_fwd_norm(nat.ptr(parts[0]), sgs[0], lds[0], nat.ptr(w), nat.ptr(bb),
+                                                   nat.ptr(y), nat.ptr(h), nat.ptr(mean), M * N, N, G, M, N, K, prec,
+                                                   1e-8, st), "td7_dense_fwd_norm")
+        else:
+            nat.check(nat.lib().td7_dense_fwd_norm_cat(len(parts), *_seg_arrays(parts, sgs, lds, widths), nat.ptr(w),
+                                                       nat.ptr(bb), nat.ptr(y), nat.ptr(h), nat.ptr(mean), M * N, N,
+                                                       G, M, N, prec, 1e-8, st), "td7_dense_fwd_norm_cat")
+        if train:
+            ctx.save_for_backward(w, h, mean, *parts)
+        ctx.meta = (grouped, G, M, N, K, prec << 8, b is not None, widths, sgs, lds)
+        args = (w, b, train, *parts)
+        ctx.edge = {i: sum(isinstance(t, torch.Tensor) for t in args[:i]) for i in range(len(args))}
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        w, h, mean, *parts = ctx.saved_tensors
+        meta = ctx.meta
+        G, M, N = meta[1], meta[2], meta[3]
+        gy = gy.contiguous()
+        gh = torch.empty_like(h)
+        nat.check(nat.lib().td7_avgl1norm_bwd(nat.ptr(h), nat.ptr(mean), nat.ptr(gy), nat.ptr(gh), G * M, N, 1e-8,
+                                              nat.stream_ptr(gy.device)), "td7_avgl1norm_bwd")
+        return _parts_backward(ctx, gh, w, h, parts, meta)
+
+
+_NORM = os.environ.get("EXO_TD7_NORM_FUSED", "1") != "0"
+
+
+def dense_norm(parts, w, b):
+    """AvgL1Norm(dense(torch.cat(parts, -1), w, b)) -- one fused launch on the
+    GPU where it applies (N <= 320, the concatenated-input rules of
+    dense_cat); the two ops otherwise."""
+    ok = (_NORM and w.is_cuda and w.dtype == torch.float32 and not torch.is_autocast_enabled()
+          and w.shape[-2] <= 320 and (_matrix_prec or parts[0].shape[-2] <= _DenseFn.fwd_kernel_max_rows))
+    if ok and len(parts) > 1:
+        ok = _CAT and _cat_ok(parts, w)
+    elif ok:
+        p = parts[0]
+        ok = (p.is_cuda and p.dtype == torch.float32 and p.shape[-1] >= 4
+              and (p.dim() == 2 or (w.dim() == 3 and p.shape[0] == w.shape[0])))
+    if ok:
+        # h and the mean are kept only when this call records a backward
+        train = torch.is_grad_enabled() and (w.requires_grad or (b is not None and b.requires_grad)
+                                             or any(p.requires_grad for p in parts))
+        return _DenseNormFn.apply(w, b, train, *parts)
+    y = dense_cat(parts, w, b, 0) if len(parts) > 1 else dense(parts[0], w, b, 0)
+    return avg_l1_norm(y)
 
 
 def _cat_ok(parts, w):
@@ -295,11 +385,20 @@ class _ZsHalfGradFn(torch.autograd.Function):
         w1, w2, w3 = w1.contiguous(), w2.contiguous(), w3.contiguous()
         h1 = _dense_raw(x, w1, b1, act)
         h2 = _dense_raw(h1, w2, b2, act)
-        h3 = _dense_raw(h2, w3, b3, 0)
-        zs = torch.empty_like(h3)
-        mean = torch.empty((h3.shape[0],), dtype=torch.float32, device=h3.device)
-        nat.check(nat.lib().td7_avgl1norm_fwd(nat.ptr(h3), nat.ptr(zs), nat.ptr(mean), h3.shape[0], h3.shape[1],
-                                              1e-8, nat.stream_ptr(h3.device)), "td7_avgl1norm_fwd")
+        M2, N3, K3 = h2.shape[0], w3.shape[0], w3.shape[1]
+        mean = torch.empty((M2,), dtype=torch.float32, device=h2.device)
+        st = nat.stream_ptr(h2.device)
+        if _NORM and N3 <= 320:  # last layer + AvgL1Norm in one launch
+            h3 = torch.empty((M2, N3), dtype=torch.float32, device=h2.device)
+            zs = torch.empty_like(h3)
+            nat.check(nat.lib().td7_dense_fwd_norm(nat.ptr(h2), 0, K3, nat.ptr(w3), nat.ptr(b3), nat.ptr(zs),
+                                                   nat.ptr(h3), nat.ptr(mean), M2 * N3, N3, 1, M2, N3, K3, prec, 1e-8,
+                                                   st), "td7_dense_fwd_norm")
+        else:
+            h3 = _dense_raw(h2, w3, b3, 0)
+            zs = torch.empty_like(h3)
+            nat.check(nat.lib().td7_avgl1norm_fwd(nat.ptr(h3), nat.ptr(zs), nat.ptr(mean), M2, N3, 1e-8, st),
+                      "td7_avgl1norm_fwd")
         ctx.save_for_backward(x, h1, h2, h3, mean, w1, w2, w3)
         ctx.meta = (B, act, prec)
         nxt = zs[B:]

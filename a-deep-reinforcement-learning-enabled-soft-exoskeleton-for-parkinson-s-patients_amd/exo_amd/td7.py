@@ -102,7 +102,7 @@ class Actor(nn.Module):
             a = self.activ(self.l1(a))
             a = self.activ(self.l2(a))
             return torch.tanh(self.l3(a))
-        a = AvgL1Norm(ops.dense(state, self.l0.weight, self.l0.bias))
+        a = ops.dense_norm([state], self.l0.weight, self.l0.bias)
         a = ops.dense_cat([a, zs], self.l1.weight, self.l1.bias, act)
         a = ops.dense(a, self.l2.weight, self.l2.bias, act)
         return ops.dense(a, self.l3.weight, self.l3.bias, ops.ACT_CODES["tanh"])
@@ -129,7 +129,7 @@ class Encoder(nn.Module):
             return AvgL1Norm(self.zs3(zs))
         zs = ops.dense(state, self.zs1.weight, self.zs1.bias, act)
         zs = ops.dense(zs, self.zs2.weight, self.zs2.bias, act)
-        return AvgL1Norm(ops.dense(zs, self.zs3.weight, self.zs3.bias))
+        return ops.dense_norm([zs], self.zs3.weight, self.zs3.bias)
 
     def zsa(self, zs, action):
         act = ops.act_code(self.activ)
@@ -188,7 +188,7 @@ class Critic(nn.Module):
             # both heads per layer as one grouped td7_dense launch: [2, B, *]
             # the concatenations [state, action] and [q, zsa, zs] are read in
             # place by the kernels (zsa, zs shared by the two heads)
-            q = AvgL1Norm(ops.dense_cat([state, action], self.w0, self.b0, 0))  # -> [2, B, h]
+            q = ops.dense_norm([state, action], self.w0, self.b0)  # -> [2, B, h]
             x = ops.dense_cat([q, zsa, zs], self.w1, self.b1, act)
             x = ops.dense(x, self.w2, self.b2, act)
             return ops.dense(x, self.w3, self.b3).squeeze(2).t()             # [B, 2]
@@ -459,7 +459,8 @@ class TD7Learner:
         x = ops.pair_rows(state, next_state)
         x = self._pair_dense(x, "zs1", act)
         x = self._pair_dense(x, "zs2", act)
-        return AvgL1Norm(self._pair_dense(x, "zs3", 0))
+        W, B = self._pair["zs3"]
+        return ops.dense_norm([x], W, B)
 
     def _pair_zsa(self, zs2, actions2):
         act = ops.act_code(self.fixed_encoder.activ)

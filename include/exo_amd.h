@@ -335,6 +335,21 @@ int td7_dense_fwd_cat(int32_t nseg, const float *const *xs_dev, const long *xsg,
                       const int32_t *widths, const float *w_dev, const float *b_dev, float *y_dev, long ysg, long ldy,
                       int32_t groups, int32_t m, int32_t n, int32_t act, void *stream);
 
+/* y = AvgL1Norm(X W^T + b) per output row (Agent/TD7_multi_agent.py:53-54
+ * after a Linear without activation, :61 / :103 / :126), N <= 320: one launch
+ * for td7_dense_fwd + td7_avgl1norm_fwd.  Layout as td7_dense_fwd; h_dev
+ * (pre-norm, y's layout) and mean_dev ([G][M], the raw mean |h| of
+ * td7_avgl1norm_fwd) are written when non-null.  prec: MFMA operand precision
+ * (0 fp32, 1 bf16, 2 fp16). */
+int td7_dense_fwd_norm(const float *x_dev, long xsg, long ldx, const float *w_dev, const float *b_dev, float *y_dev,
+                       float *h_dev, float *mean_dev, long ysg, long ldy, int32_t groups, int32_t m, int32_t n,
+                       int32_t k, int32_t prec, float eps, void *stream);
+/* td7_dense_fwd_norm of a concatenated input (td7_dense_fwd_cat's segments). */
+int td7_dense_fwd_norm_cat(int32_t nseg, const float *const *xs_dev, const long *xsg, const long *ldx,
+                           const int32_t *widths, const float *w_dev, const float *b_dev, float *y_dev, float *h_dev,
+                           float *mean_dev, long ysg, long ldy, int32_t groups, int32_t m, int32_t n, int32_t prec,
+                           float eps, void *stream);
+
 /* td7_dense_bwd_weight of a layer whose input is given by segments (the
  * layout of td7_dense_fwd_cat); N >= 4. */
 int td7_dense_bwd_weight_cat(const float *dy_dev, long dysg, long lddy, const float *y_dev, long ysg, long ldy,

@@ -313,3 +313,39 @@ def test_encoder_zs_half_grad_matches_autograd_slices():
             assert q.grad is None or not q.grad.any()
             continue
         torch.testing.assert_close(p.grad, q.grad, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("case", ["plain", "pair3d", "critic_cat", "ragged"])
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_dense_norm_matches_separate_ops(case, prec):
+    """ops.dense_norm (td7_dense_fwd_norm[_cat]: GEMM + bias + AvgL1Norm in one
+    launch) == AvgL1Norm(dense(...)) forward and backward."""
+    from exo_amd import ops
+    torch.manual_seed(len(case))
+    mk = lambda *s: torch.randn(*s, device="cuda")
+    if case == "plain":        # Actor.l0 / Encoder.zs3
+        parts, w, b = [mk(1024, 80)], mk(320, 80) / 9, mk(320)
+    elif case == "pair3d":     # paired fixed encoders' zs3
+        parts, w, b = [mk(2, 1024, 300)], mk(2, 300, 300) / 17, mk(2, 300)
+    elif case == "critic_cat":  # critic q = AvgL1Norm(Linear([state | action])), both heads
+        parts, w, b = [mk(1024, 80), mk(1024, 7)], mk(2, 320, 87) / 9, mk(2, 320)
+    else:                      # ragged rows and columns
+        parts, w, b = [mk(37, 19)], mk(45, 19) / 4, mk(45)
+    outs = []
+    for fused in (True, False):
+        ps = [p.clone().requires_grad_(True) for p in parts]
+        ww, bb = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+        with ops.matrix_precision(prec):
+            if fused:
+                y = ops.dense_norm(ps, ww, bb)
+            else:
+                y = ops.avg_l1_norm(ops.dense_cat(ps, ww, bb, 0) if len(ps) > 1 else ops.dense(ps[0], ww, bb, 0))
+        torch.manual_seed(3)
+        y.backward(torch.randn_like(y))
+        outs.append((y.detach(), ww.grad, bb.grad, [p.grad for p in ps]))
+    tol = 2e-5 if prec == "fp32" else 2e-3
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=tol, atol=tol)
+    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=tol, atol=tol * 20)
+    torch.testing.assert_close(outs[0][2], outs[1][2], rtol=tol, atol=tol * 20)
+    for a, r in zip(outs[0][3], outs[1][3]):
+        torch.testing.assert_close(a, r, rtol=tol, atol=tol * 20)
