@@ -11,6 +11,7 @@
 #else
 #include <hip/hip_runtime.h>
 #endif
+#include "philox.h"
 #include <math.h>
 #include <stdint.h>
 
@@ -379,17 +380,6 @@ __host__ __device__ inline bool rk45_solve(const OdeM &M, const double *T, doubl
 // ---------------------------------------------------------------------------
 // Philox4x32-10 counter-based draws for the reset path.
 // ---------------------------------------------------------------------------
-__host__ __device__ inline void philox4x32(uint32_t c[4], uint32_t k0, uint32_t k1) {
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
-        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
-        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
-        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
-        c[0] = n0; c[1] = (uint32_t)p1; c[2] = n2; c[3] = (uint32_t)p0;
-        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
-    }
-}
 
 // Unit uniform number p of the draw stream of (env, episode): 53-bit, [0, 1).
 __host__ __device__ inline double philox_u01(uint64_t seed, uint32_t env, uint32_t episode, uint32_t p) {

@@ -19,6 +19,7 @@
 
 #include <string>
 
+#include "philox.h"
 #include "exo_amd.h"
 
 namespace {
@@ -242,16 +243,13 @@ __global__ __launch_bounds__(256) void lap_store_copy_kernel(lap_storage_desc st
 
 // LAP.sample (:65-111) with the gather: one wavefront per draw descends the
 // tree (every lane the same path, reads broadcast) and copies the row.
-__global__ __launch_bounds__(256) void lap_sample_gather_kernel(const float *tree, int cap, int levels, int capacity,
-                                                                const float *u, const int32_t *size, int batch,
-                                                                int total, int32_t *idx, lap_storage_desc st,
-                                                                float *o_state, float *o_action, float *o_next,
-                                                                float *o_reward, float *o_not_done) {
-    const int d = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (d >= total) return;
+__device__ __forceinline__ void sample_descend(const float *tree, int cap, int levels, int capacity, float ud,
+                                               const int32_t *size, int batch, int d, int lane, int32_t *idx,
+                                               const lap_storage_desc &st, float *o_state, float *o_action,
+                                               float *o_next, float *o_reward, float *o_not_done) {
     const int s = d / batch;
     const float *T = tree + (size_t)s * 2 * cap;
-    float val = u[d] * T[1];
+    float val = ud * T[1];
     int node = 1;
     for (int lv = 0; lv < levels; ++lv) {
         const float left = T[2 * node], right = T[2 * node + 1];
@@ -278,6 +276,45 @@ __global__ __launch_bounds__(256) void lap_sample_gather_kernel(const float *tre
         o_not_done[d] = st.not_done[r];
     }
 }
+
+// rng != nullptr: u[d] is drawn in the kernel (Philox block d of this call,
+// word 0 -> [0, 1)); the device call counter advances once per launch (the
+// last workgroup out, as td7_adam_step's step count).
+struct SampleRng {
+    uint64_t seed;
+    uint32_t tag;
+    unsigned long long *counter;
+    uint32_t *ticket;
+};
+
+__global__ __launch_bounds__(256) void lap_sample_gather_kernel(const float *tree, int cap, int levels, int capacity,
+                                                                const float *u, const int32_t *size, int batch,
+                                                                int total, int32_t *idx, lap_storage_desc st,
+                                                                float *o_state, float *o_action, float *o_next,
+                                                                float *o_reward, float *o_not_done, SampleRng rng) {
+    const int d = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (rng.counter) {
+        const unsigned long long call = *rng.counter;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence();
+            if (atomicAdd(rng.ticket, 1u) == gridDim.x - 1) {
+                *rng.counter = call + 1ull;
+                *rng.ticket = 0u;
+            }
+        }
+        if (d >= total) return;
+        uint32_t r[4];
+        philox_block(rng.seed, rng.tag, call, (uint32_t)d, r);
+        sample_descend(tree, cap, levels, capacity, u01_open_hi(r[0]), size, batch, d, lane, idx, st, o_state,
+                       o_action, o_next, o_reward, o_not_done);
+        return;
+    }
+    if (d >= total) return;
+    sample_descend(tree, cap, levels, capacity, u[d], size, batch, d, lane, idx, st, o_state, o_action, o_next,
+                   o_reward, o_not_done);
+}
+
 
 int rc(hipError_t e) { return e == hipSuccess ? EXO_OK : EXO_EDEVICE; }
 
@@ -375,7 +412,21 @@ int lap_sample_gather(const lap_tree_desc *t, const lap_storage_desc *st, const 
     const int total = t->n_strata * batch;
     hipLaunchKernelGGL(lap_sample_gather_kernel, dim3((total + 3) / 4), dim3(256), 0, (hipStream_t)stream, t->tree,
                        t->cap, levels_of(t), t->capacity, u, st->size, batch, total, idx, *st, out_state, out_action,
-                       out_next_state, out_reward, out_not_done);
+                       out_next_state, out_reward, out_not_done, SampleRng{0, 0, nullptr, nullptr});
+    return rc(hipGetLastError());
+}
+
+int lap_sample_gather_rng(const lap_tree_desc *t, const lap_storage_desc *st, uint64_t seed, uint32_t tag,
+                          unsigned long long *counter, uint32_t *ticket, int32_t batch, int32_t *idx,
+                          float *out_state, float *out_action, float *out_next_state, float *out_reward,
+                          float *out_not_done, void *stream) {
+    if (!valid(t) || !st || !st->size || !counter || !ticket || !idx || batch <= 0 || !out_state || !out_action ||
+        !out_next_state || !out_reward || !out_not_done)
+        return EXO_EINVAL;
+    const int total = t->n_strata * batch;
+    hipLaunchKernelGGL(lap_sample_gather_kernel, dim3((total + 3) / 4), dim3(256), 0, (hipStream_t)stream, t->tree,
+                       t->cap, levels_of(t), t->capacity, nullptr, st->size, batch, total, idx, *st, out_state,
+                       out_action, out_next_state, out_reward, out_not_done, SampleRng{seed, tag, counter, ticket});
     return rc(hipGetLastError());
 }
 

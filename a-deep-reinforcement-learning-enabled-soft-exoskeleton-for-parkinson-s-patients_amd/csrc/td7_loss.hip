@@ -12,6 +12,7 @@
 
 #include <algorithm>
 
+#include "philox.h"
 #include "exo_amd.h"
 
 namespace {
@@ -96,6 +97,36 @@ __global__ __launch_bounds__(T) void noisy_action_kernel(const float *a, const f
     }
     __syncthreads();
     if (threadIdx.x == 0) *sigma = sg - sigma_dec;
+}
+
+// noisy_action_kernel with the noise drawn in the kernel: element 2j+t is
+// normal t of Philox block j of this call (Box-Muller); the device call
+// counter advances by one per launch (no host value: graph-replay safe).
+__global__ __launch_bounds__(T) void noisy_action_rng_kernel(const float *a, uint64_t seed, uint32_t tag,
+                                                             unsigned long long *counter, float *sigma,
+                                                             float sigma_dec, float clip, float scale, float *out,
+                                                             int n) {
+    const float sg = *sigma;
+    const unsigned long long call = *counter;
+    for (int j = threadIdx.x; 2 * j < n; j += T) {
+        uint32_t r[4];
+        philox_block(seed, tag, call, (uint32_t)j, r);
+        float z[2];
+        box_muller(r, z[0], z[1]);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int i = 2 * j + t;
+            if (i >= n) break;
+            float e = z[t] * sg;
+            if (clip > 0.f) e = fminf(fmaxf(e, -clip), clip);
+            out[i] = fminf(fmaxf(a[i] + e, -1.0f), 1.0f) * scale;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        *sigma = sg - sigma_dec;
+        *counter = call + 1ull;
+    }
 }
 
 // F.mse_loss(pred, target) forward (mean of squared differences over n) and
@@ -183,6 +214,14 @@ int td7_noisy_action(const float *a, const float *noise, float *sigma, float sig
     if (n == 0) return EXO_OK;
     hipLaunchKernelGGL(noisy_action_kernel, dim3(1), dim3(T), 0, (hipStream_t)stream, a, noise, sigma, sigma_dec, clip,
                        scale, out, n);
+    return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
+}
+
+int td7_noisy_action_rng(const float *a, uint64_t seed, uint32_t tag, unsigned long long *counter, float *sigma,
+                         float sigma_dec, float clip, float scale, float *out, int32_t n, void *stream) {
+    if (!a || !counter || !sigma || !out || n < 0) return EXO_EINVAL;
+    hipLaunchKernelGGL(noisy_action_rng_kernel, dim3(1), dim3(T), 0, (hipStream_t)stream, a, seed, tag, counter, sigma,
+                       sigma_dec, clip, scale, out, n);
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 

@@ -543,10 +543,48 @@ def critic_loss_and_grad(q, q_target, alpha, min_priority):
 
 
 # ---------------------------------------------------------------- small fusions
-def noisy_action(a, noise, sigma, sigma_dec, clip=0.0, scale=1.0):
+class DeviceRNG:
+    """A counter-based (Philox4x32-10) random stream consumed INSIDE the kernels
+    that need random numbers (td7_noisy_action_rng, lap_sample_gather_rng):
+    key = seed, counter = (draw index, call number, tag).  The call number lives
+    on the device and each launch advances it, so a captured HIP graph draws
+    fresh numbers on every replay with no generator kernel and no host value.
+    The seed follows torch.initial_seed(), so torch.manual_seed reproduces runs;
+    each consumer (tag) has its own stream (concurrent graph branches never
+    share a counter)."""
+
+    def __init__(self, device, tag):
+        self.tag = int(tag) & 0xFFFFFFFF
+        self.seed = (torch.initial_seed() * 0x9E3779B97F4A7C15 + (self.tag + 1) * 0xD1B54A32D192ED03) & (2 ** 64 - 1)
+        # [call number, ticket (uint32 in the low half)]
+        self.state = torch.zeros((2,), dtype=torch.int64, device=device)
+
+    @property
+    def counter_ptr(self):
+        return self.state.data_ptr()
+
+    @property
+    def ticket_ptr(self):
+        return self.state.data_ptr() + 8
+
+
+def noisy_action(a, noise, sigma, sigma_dec, clip=0.0, scale=1.0, rng=None):
     """clamp(a + c(noise * sigma), -1, 1) * scale with c = clamp(+-clip) when
     clip > 0, then sigma -= sigma_dec in place (sigma: device scalar tensor).
-    One td7_noisy_action launch on a GPU; the reference expressions on a CPU."""
+    One td7_noisy_action launch on a GPU; the reference expressions on a CPU.
+    noise=None: standard normal noise -- drawn inside the kernel from `rng`
+    (a DeviceRNG) on a GPU, torch.randn_like on a CPU."""
+    if noise is None and a.is_cuda:
+        if rng is None:
+            raise ValueError("noisy_action: noise=None needs a DeviceRNG on the GPU")
+        a = a.contiguous()
+        out = torch.empty_like(a)
+        nat.check(nat.lib().td7_noisy_action_rng(nat.ptr(a), rng.seed, rng.tag, rng.counter_ptr, nat.ptr(sigma),
+                                                 float(sigma_dec), float(clip), float(scale), nat.ptr(out), a.numel(),
+                                                 nat.stream_ptr(a.device)), "td7_noisy_action_rng")
+        return out
+    if noise is None:
+        noise = torch.randn_like(a)
     if not a.is_cuda:
         e = noise * sigma
         if clip > 0:

@@ -15,6 +15,7 @@ Two insert paths:
                     active env-step (documented divergence).
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -60,6 +61,10 @@ class LAP:
         self._row0 = (torch.arange(E, device=self.device, dtype=torch.int64) * (C + 1))
         self.ind = None
         self._u = torch.empty((E, self.batch_size), **f32)
+        # sample() draws its uniforms in the kernel (EXO_DEVICE_RNG=0: torch.rand + lap_sample_gather)
+        from .ops import DeviceRNG
+        self.device_rng = os.environ.get("EXO_DEVICE_RNG", "1") != "0"
+        self._rng = DeviceRNG(self.device, 3)
         self._idx = torch.empty((E, self.batch_size), **i32)
         self._store = nat.LapStorageDesc(self.state.data_ptr(), self.action.data_ptr(), self.next_state.data_ptr(),
                                          self.reward.data_ptr(), self.not_done.data_ptr(), state_dim, action_dim,
@@ -146,10 +151,19 @@ class LAP:
         stratum, stratum-major, as float32 device tensors (lap_sample_gather:
         descent + gather in one kernel; the returned tensors are reused by the
         next call)."""
-        self._u.uniform_()
-        nat.check(nat.lib().lap_sample_gather(ctypes.byref(self._desc), ctypes.byref(self._store), nat.ptr(self._u),
-                                              self.batch_size, nat.ptr(self._idx), *[nat.ptr(t) for t in self._batch],
-                                              self._stream()), "lap_sample_gather")
+        if self.device_rng:
+            # the uniforms drawn inside the kernel (ops.DeviceRNG): no generator launch
+            r = self._rng
+            nat.check(nat.lib().lap_sample_gather_rng(ctypes.byref(self._desc), ctypes.byref(self._store), r.seed,
+                                                      r.tag, r.counter_ptr, r.ticket_ptr, self.batch_size,
+                                                      nat.ptr(self._idx), *[nat.ptr(t) for t in self._batch],
+                                                      self._stream()), "lap_sample_gather_rng")
+        else:
+            self._u.uniform_()
+            nat.check(nat.lib().lap_sample_gather(ctypes.byref(self._desc), ctypes.byref(self._store),
+                                                  nat.ptr(self._u), self.batch_size, nat.ptr(self._idx),
+                                                  *[nat.ptr(t) for t in self._batch], self._stream()),
+                      "lap_sample_gather")
         self.ind = self._idx
         return self._batch
 

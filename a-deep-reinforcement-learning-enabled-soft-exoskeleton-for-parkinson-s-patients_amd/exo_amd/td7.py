@@ -423,6 +423,11 @@ class TD7Learner:
         self.policy_noise_decrease = hp.target_policy_noise / learning_steps
         self.action_noise_decrease = hp.exploration_noise / learning_steps
         self.exploration_noise_t = torch.tensor(float(hp.exploration_noise), **f32)
+        # target-policy and exploration noise drawn inside their kernels on the
+        # GPU (ops.DeviceRNG); EXO_DEVICE_RNG=0: torch.randn_like
+        self._device_rng = os.environ.get("EXO_DEVICE_RNG", "1") != "0"
+        self._noise_rng = ops.DeviceRNG(self.device, 1) if self.device.type == "cuda" else None
+        self._explore_rng = ops.DeviceRNG(self.device, 2) if self.device.type == "cuda" else None
 
     ENC_LAYERS = ("zs1", "zs2", "zs3", "zsa1", "zsa2", "zsa3")
 
@@ -535,8 +540,8 @@ class TD7Learner:
         else:
             self._encoder_grads(state, action, next_state)
         # ---- critic (:233-257)
-        if noise is None:
-            noise = torch.randn_like(action)
+        if noise is None and not (action.is_cuda and self._device_rng):
+            noise = torch.randn_like(action)  # on the GPU: drawn inside the noisy-action kernel
         split = side is not None and os.environ.get("EXO_TD7_TARGET_BRANCH", "1") == "1"
         with torch.no_grad():
             with self._autocast():
@@ -598,7 +603,7 @@ class TD7Learner:
             # (noise * sigma).clamp(+-noise_clip); sigma -= decrease; (a + noise).clamp(-1, 1)
             next_action = ops.noisy_action(self.actor_target(next_state, fixed_target_zs).float(), noise,
                                            self.target_policy_noise, self.policy_noise_decrease,
-                                           clip=hp.noise_clip)
+                                           clip=hp.noise_clip, rng=self._noise_rng)
             fixed_zsa = None
             if pair is not None:
                 zs2, action = pair
@@ -828,8 +833,9 @@ class Agent:
             return (a + col).clamp(-1, 1) * self.max_action
         if use_exploration:
             L = self.learner
-            return ops.noisy_action(a, torch.randn_like(a), L.exploration_noise_t, L.action_noise_decrease * a.shape[0],
-                                    scale=self.max_action)
+            noise = None if (a.is_cuda and L._device_rng) else torch.randn_like(a)
+            return ops.noisy_action(a, noise, L.exploration_noise_t, L.action_noise_decrease * a.shape[0],
+                                    scale=self.max_action, rng=L._explore_rng)
         return a.clamp(-1, 1) * self.max_action
 
     # ---------------------------------------------------------- training

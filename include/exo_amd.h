@@ -246,6 +246,14 @@ int lap_store_batch(const lap_tree_desc *t, const lap_storage_desc *st, const fl
 int lap_sample_gather(const lap_tree_desc *t, const lap_storage_desc *st, const float *u_dev, int32_t batch,
                       int32_t *idx_dev, float *out_state, float *out_action, float *out_next_state,
                       float *out_reward, float *out_not_done, void *stream);
+/* lap_sample_gather with the uniforms drawn inside the kernel (Philox4x32-10,
+ * key seed, counter words (draw index, call, tag)); *counter_dev (the call
+ * number) advances by one per launch, ticket_dev: one uint32, zero at the first
+ * call, left zero.  Graph-replay safe: no host value changes between calls. */
+int lap_sample_gather_rng(const lap_tree_desc *t, const lap_storage_desc *st, uint64_t seed, uint32_t tag,
+                          unsigned long long *counter_dev, uint32_t *ticket_dev, int32_t batch, int32_t *idx_dev,
+                          float *out_state, float *out_action, float *out_next_state, float *out_reward,
+                          float *out_not_done, void *stream);
 
 /* ------------------------------------------------------------------------
  * Fused TD7 net pieces (Agent/TD7_multi_agent.py:53-54, AvgL1Norm).
@@ -302,6 +310,12 @@ int td7_critic_loss_strided(const float *q_dev, long qs_b, long qs_h, const floa
  * target policy smoothing of the critic target (TD7_multi_agent.py:236-238). */
 int td7_noisy_action(const float *a_dev, const float *noise_dev, float *sigma_dev, float sigma_dec, float clip,
                      float scale, float *out_dev, int32_t n, void *stream);
+/* td7_noisy_action with the noise drawn in the kernel: element 2j+t is normal t
+ * (Box-Muller) of Philox4x32-10 block (j, call, tag) under key seed, call =
+ * *counter_dev, which advances by one per launch (graph-replay safe). */
+int td7_noisy_action_rng(const float *a_dev, uint64_t seed, uint32_t tag, unsigned long long *counter_dev,
+                         float *sigma_dev, float sigma_dec, float clip, float scale, float *out_dev, int32_t n,
+                         void *stream);
 /* F.mse_loss (encoder loss, TD7_multi_agent.py:226): *loss = mean (x - y)^2;
  * backward dx = 2 (x - y) / n * (*g).  ws_dev: TD7_MSE_WS floats, zeroed once
  * by the caller (block partials + a ticket the kernel leaves at zero); one

@@ -6,7 +6,7 @@ set -o pipefail
 VAR=${1:?switch variable}
 mkdir -p gpurun_out
 rm -f gpurun_out/ab_*.json
-timeout -k 10 300 python -u -m pytest tests/test_td7_dense_gpu.py tests/test_td7_ops_gpu.py tests/test_graph_order_gpu.py tests/test_rollout_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/ab_tests.log 2>&1 || exit $?
+timeout -k 10 300 python -u -m pytest tests/test_device_rng_gpu.py tests/test_td7_dense_gpu.py tests/test_td7_ops_gpu.py tests/test_graph_order_gpu.py tests/test_rollout_gpu.py tests/test_lap_gpu.py tests/test_td7.py -x -q --timeout 120 --timeout-method thread > gpurun_out/ab_tests.log 2>&1 || exit $?
 for i in 1 2 3; do
   for v in 0 1; do
     env $VAR=$v timeout -k 10 200 python bench.py --steps 300 --warmup 50 --no-cpu-baseline > gpurun_out/ab_${v}_$i.json 2>gpurun_out/ab_err.log || exit $?
