@@ -403,12 +403,15 @@ class _ZsHalfGradFn(torch.autograd.Function):
         ctx.meta = (B, act, prec)
         nxt = zs[B:]
         ctx.mark_non_differentiable(nxt)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the detached half
         return zs[:B], nxt
 
     @staticmethod
     def backward(ctx, gzs, _gnext):
         x, h1, h2, h3, mean, w1, w2, w3 = ctx.saved_tensors
         B, act, prec = ctx.meta
+        if gzs is None:
+            return (None,) * 9
         s = nat.stream_ptr(gzs.device)
         L = nat.lib()
         gzs = gzs.contiguous()
@@ -634,6 +637,25 @@ class _MSEFn(torch.autograd.Function):
         nat.check(nat.lib().td7_mse_bwd(nat.ptr(x), nat.ptr(y), nat.ptr(g.contiguous()), x.numel(), nat.ptr(dx),
                                         nat.stream_ptr(x.device)), "td7_mse_bwd")
         return dx, None
+
+
+_ones = {}
+
+
+def mse_grad(x, y):
+    """d F.mse_loss(x, y) / dx = 2 (x - y) / n as one td7_mse_bwd launch (the
+    caller back-propagates it from x directly: no loss value, no seed fill)."""
+    key = torch.device(x.device)
+    one = _ones.get(key)
+    if one is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("mse_grad: run once eagerly on this device before graph capture")
+        one = _ones[key] = torch.ones((), dtype=torch.float32, device=x.device)
+    x, y = x.contiguous(), y.contiguous()
+    dx = torch.empty_like(x)
+    nat.check(nat.lib().td7_mse_bwd(nat.ptr(x), nat.ptr(y), nat.ptr(one), x.numel(), nat.ptr(dx),
+                                    nat.stream_ptr(x.device)), "td7_mse_bwd")
+    return dx
 
 
 def mse_loss(x, y):

@@ -133,7 +133,8 @@ class LAP:
         nx = f32(next_state, (n, self.state_dim))
         ac = f32(action, (n, self.action_dim))
         rw = f32(reward, (n,))
-        dn = done if done.dtype == torch.uint8 else done.to(torch.uint8)
+        dn = done if done.dtype == torch.uint8 else (done.view(torch.uint8) if done.dtype == torch.bool
+                                                     else done.to(torch.uint8))
         dn = dn.reshape(n).contiguous()
         sr = strata if strata.dtype == torch.int32 else strata.to(torch.int32)
         act = None

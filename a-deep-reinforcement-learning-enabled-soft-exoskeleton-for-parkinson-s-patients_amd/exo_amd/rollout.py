@@ -62,8 +62,16 @@ class VecTrainer:
         self.active_counts = self.active_table.sum(1).cpu().numpy()
         self.strata = (torch.as_tensor(env.motions % agent.env_num, dtype=torch.int32, device=self.device)
                        if strata is None else strata)
-        self.obs = env.reset()
-        self.out = env.new_outputs(True)
+        # two observation buffers used in alternation (iteration i reads obs[c]
+        # and the env writes its next observation into obs[1 - c]): no copy of
+        # the next observation per step.  The two HIP graphs (policy-update
+        # parities) alternate in lockstep with c, so each graph always sees the
+        # same pair.
+        o0 = env.reset()
+        self._obs = [o0, torch.empty_like(o0)]
+        outs = [env.new_outputs(True), env.new_outputs(True)]
+        self._outs = [(self._obs[1], *outs[0][1:]), (self._obs[0], *outs[1][1:])]
+        self._cur = 0
         self.active = self.active_table[0].clone()
         self.k = 0
         self.use_graphs = use_graphs
@@ -86,11 +94,21 @@ class VecTrainer:
     # ----------------------------------------------------------- pieces
     def _rollout(self):
         ag = self.agent
-        act = ag.select_action_batch(self.obs, timestep=self.k_dev if self.exploration == "pink" else None)
-        nobs, rew, done, info = self.env.step(act, active=self.active, out=self.out)
-        ag.replay_buffer.add_batch(self.obs, act, nobs, rew, done, self.strata, self.active)
-        self.obs.copy_(nobs)
+        obs = self.obs
+        act = ag.select_action_batch(obs, timestep=self.k_dev if self.exploration == "pink" else None)
+        nobs, rew, done, info = self.env.step(act, active=self.active, out=self._outs[self._cur])
+        ag.replay_buffer.add_batch(obs, act, nobs, rew, done, self.strata, self.active)
         self.last_actions = act
+
+    @property
+    def obs(self):
+        """The current observation buffer."""
+        return self._obs[self._cur]
+
+    @property
+    def out(self):
+        """The env output buffers (obs, reward, done, info) of the current step."""
+        return self._outs[self._cur]
 
     # The update samples its batch BEFORE this iteration's transitions are
     # stored (from iteration 1 on), which frees the rollout (batched actor
@@ -224,4 +242,5 @@ class VecTrainer:
         n_active = int(self.active_counts[self.k])
         self.k += 1
         self.iters += 1
+        self._cur ^= 1  # the next observation is in the other buffer
         return n_active

@@ -521,9 +521,14 @@ class TD7Learner:
                 zs_all = enc.zs(torch.cat([state, next_state], 0))
                 zs, next_zs = zs_all[:B], zs_all[B:].detach()
             pred_zs = self.encoder.zsa(zs, action)
-        encoder_loss = ops.mse_loss(pred_zs.float(), next_zs.float())
         self.encoder_optimizer.zero_grad(set_to_none=self.grads_to_none)
-        encoder_loss.backward()
+        if pred_zs.is_cuda and pred_zs.dtype == torch.float32:
+            # d mse / d pred_zs from one kernel, back-propagated from pred_zs
+            # (the loss value itself is not used by the update)
+            torch.autograd.backward(pred_zs, ops.mse_grad(pred_zs, next_zs.detach()))
+        else:
+            encoder_loss = ops.mse_loss(pred_zs.float(), next_zs.float())
+            encoder_loss.backward()
 
     def phase_grads(self, state, action, next_state, reward, not_done, noise=None):
         hp = self.hp

@@ -137,7 +137,10 @@ class VecExoskeletonEnv:
         obs, rew, done, info = out
         act = None
         if active is not None:
-            act = active.to(device=self.device, dtype=torch.uint8).contiguous()
+            if active.dtype == torch.bool and active.device == self.device and active.is_contiguous():
+                act = active.view(torch.uint8)  # same bytes, no conversion kernel
+            else:
+                act = active.to(device=self.device, dtype=torch.uint8).contiguous()
         rc = nat.lib().exo_step(self._ctx, nat.ptr(a), nat.ptr(obs), nat.ptr(rew), nat.ptr(done),
                                 nat.ptr(info) if with_info else None, nat.ptr(act), self._stream())
         nat.check(rc, "exo_step", self._ctx)
