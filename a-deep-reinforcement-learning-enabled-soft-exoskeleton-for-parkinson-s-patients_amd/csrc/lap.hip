@@ -28,15 +28,38 @@ constexpr int UPD_THREADS = 1024;
 
 __device__ __forceinline__ float *stratum_tree(float *tree, int s, int cap) { return tree + (size_t)s * 2 * cap; }
 
-// Recompute the ancestors of the n leaves slot[0..n) of one stratum, bottom-up.
+// Recompute the ancestors of the n leaves slot[0..n) of one stratum, bottom-up,
+// one level per barrier.  The lower levels work in global memory; once every
+// parent of a level is below TOPN/2 the top of the tree (nodes [1, TOPN), the
+// parents and their children) is staged in LDS and the remaining levels (12 of
+// the 18 of a 250k-slot stratum) run there -- one L2 round trip per level
+// fewer -- and the recomputed nodes [1, TOPN/2) are written back.  The same
+// additions in the same order: the sums are bit-identical.
+constexpr int TOPN = 8192;
 __device__ void propagate(float *T, int cap, int levels, const int32_t *slot, int n) {
-    for (int lv = 1; lv <= levels; ++lv) {
+    __shared__ float top[TOPN];
+    int lv = 1;
+    for (; lv <= levels && ((2 * cap) >> lv) > TOPN / 2; ++lv) {
         __syncthreads();
         for (int k = threadIdx.x; k < n; k += blockDim.x) {
             const int node = (cap + slot[k]) >> lv;
             T[node] = T[2 * node] + T[2 * node + 1];
         }
     }
+    __syncthreads();
+    if (lv > levels) return;
+    const int lim = min(TOPN, 2 * cap);
+    for (int i = threadIdx.x; i < lim; i += blockDim.x) top[i] = T[i];
+    for (; lv <= levels; ++lv) {
+        __syncthreads();
+        for (int k = threadIdx.x; k < n; k += blockDim.x) {
+            const int node = (cap + slot[k]) >> lv;
+            top[node] = top[2 * node] + top[2 * node + 1];
+        }
+    }
+    __syncthreads();
+    const int wb = min(TOPN / 2, cap);
+    for (int i = 1 + threadIdx.x; i < wb; i += blockDim.x) T[i] = top[i];
     __syncthreads();
 }
 
@@ -101,12 +124,22 @@ __global__ __launch_bounds__(UPD_THREADS) void lap_update_kernel(float *tree, fl
     const int32_t *I = idx + (size_t)s * batch;
     const float *P = prio + (size_t)s * batch;
     __shared__ float red[UPD_THREADS / 64];
+    __shared__ int32_t li[UPD_THREADS];
     float mx = 0.0f;
-    for (int b = threadIdx.x; b < batch; b += blockDim.x) {
-        bool last = true; // a later duplicate overwrites this one
-        for (int b2 = b + 1; b2 < batch; ++b2) last &= (I[b2] != I[b]);
-        if (last) T[cap + I[b]] = P[b];
-        mx = fmaxf(mx, P[b]);
+    for (int b0 = 0; b0 < batch; b0 += UPD_THREADS) { // the batch's indices staged in LDS
+        const int nb = min(UPD_THREADS, batch - b0);
+        __syncthreads();
+        if ((int)threadIdx.x < nb) li[threadIdx.x] = I[b0 + threadIdx.x];
+        __syncthreads();
+        const int b = b0 + threadIdx.x;
+        if (b < batch) {
+            const int me = li[threadIdx.x];
+            bool last = true; // a later duplicate overwrites this one
+            for (int k = threadIdx.x + 1; k < nb; ++k) last &= (li[k] != me);
+            for (int b2 = b0 + nb; b2 < batch; ++b2) last &= (I[b2] != me);
+            if (last) T[cap + me] = P[b];
+            mx = fmaxf(mx, P[b]);
+        }
     }
     for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;

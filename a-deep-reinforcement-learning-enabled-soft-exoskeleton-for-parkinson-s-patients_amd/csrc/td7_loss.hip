@@ -103,12 +103,12 @@ __global__ __launch_bounds__(T) void noisy_action_kernel(const float *a, const f
 // normal t of Philox block j of this call (Box-Muller); the device call
 // counter advances by one per launch (no host value: graph-replay safe).
 __global__ __launch_bounds__(T) void noisy_action_rng_kernel(const float *a, uint64_t seed, uint32_t tag,
-                                                             unsigned long long *counter, float *sigma,
-                                                             float sigma_dec, float clip, float scale, float *out,
-                                                             int n) {
+                                                             unsigned long long *counter, uint32_t *ticket,
+                                                             float *sigma, float sigma_dec, float clip, float scale,
+                                                             float *out, int n) {
     const float sg = *sigma;
     const unsigned long long call = *counter;
-    for (int j = threadIdx.x; 2 * j < n; j += T) {
+    for (int j = blockIdx.x * T + threadIdx.x; 2 * j < n; j += gridDim.x * T) {
         uint32_t r[4];
         philox_block(seed, tag, call, (uint32_t)j, r);
         float z[2];
@@ -122,10 +122,16 @@ __global__ __launch_bounds__(T) void noisy_action_rng_kernel(const float *a, uin
             out[i] = fminf(fmaxf(a[i] + e, -1.0f), 1.0f) * scale;
         }
     }
+    // every workgroup has read sigma and the call number: the last one out
+    // advances both
     __syncthreads();
     if (threadIdx.x == 0) {
-        *sigma = sg - sigma_dec;
-        *counter = call + 1ull;
+        __threadfence();
+        if (atomicAdd(ticket, 1u) == gridDim.x - 1) {
+            *sigma = sg - sigma_dec;
+            *counter = call + 1ull;
+            *ticket = 0u;
+        }
     }
 }
 
@@ -217,11 +223,13 @@ int td7_noisy_action(const float *a, const float *noise, float *sigma, float sig
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 
-int td7_noisy_action_rng(const float *a, uint64_t seed, uint32_t tag, unsigned long long *counter, float *sigma,
-                         float sigma_dec, float clip, float scale, float *out, int32_t n, void *stream) {
-    if (!a || !counter || !sigma || !out || n < 0) return EXO_EINVAL;
-    hipLaunchKernelGGL(noisy_action_rng_kernel, dim3(1), dim3(T), 0, (hipStream_t)stream, a, seed, tag, counter, sigma,
-                       sigma_dec, clip, scale, out, n);
+int td7_noisy_action_rng(const float *a, uint64_t seed, uint32_t tag, unsigned long long *counter,
+                         uint32_t *ticket, float *sigma, float sigma_dec, float clip, float scale, float *out,
+                         int32_t n, void *stream) {
+    if (!a || !counter || !ticket || !sigma || !out || n < 0) return EXO_EINVAL;
+    const int blocks = std::max(1, std::min(256, (n / 2 + T - 1) / T));
+    hipLaunchKernelGGL(noisy_action_rng_kernel, dim3(blocks), dim3(T), 0, (hipStream_t)stream, a, seed, tag, counter,
+                       ticket, sigma, sigma_dec, clip, scale, out, n);
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 

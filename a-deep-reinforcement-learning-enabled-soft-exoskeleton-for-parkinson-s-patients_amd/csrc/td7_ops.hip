@@ -143,10 +143,13 @@ struct AdamSeg {
 struct AdamMulti {
     AdamOpt o[TD7_ADAM_MAX_OPT];
     AdamSeg s[TD7_ADAM_MAX_SEG];
+    int q0[TD7_ADAM_MAX_SEG + 1]; // segment k owns the 4-element groups [q0[k], q0[k+1])
     int nopt, nseg;
     uint32_t *ticket;
 };
 
+// One thread per 4-element group of the concatenated segments (every segment
+// padded to whole groups), so all segments are updated in one parallel pass.
 __global__ __launch_bounds__(ADAM_THREADS) void adam_multi_kernel(AdamMulti a) {
     __shared__ float coef[TD7_ADAM_MAX_OPT][2];
     if (threadIdx.x < a.nopt) {
@@ -156,31 +159,33 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_multi_kernel(AdamMulti a) {
         coef[threadIdx.x][1] = sqrtf(1.0f - powf(o.b2, t));
     }
     __syncthreads();
-    const long stride = (long)gridDim.x * ADAM_THREADS;
-    const long start = (long)blockIdx.x * ADAM_THREADS + threadIdx.x;
-    for (int k = 0; k < a.nseg; ++k) {
+    const int gi = blockIdx.x * ADAM_THREADS + threadIdx.x;
+    if (gi < a.q0[a.nseg]) {
+        int k = 0;
+        for (int s = 1; s < a.nseg; ++s) k += gi >= a.q0[s];
         const AdamSeg sg = a.s[k];
-        const AdamOpt &o = a.o[sg.opt];
+        const AdamOpt o = a.o[sg.opt];
         const float step_size = coef[sg.opt][0], bc2s = coef[sg.opt][1];
-        float *p = o.p + sg.off, *m = o.m + sg.off, *v = o.v + sg.off;
-        const float *g = sg.g;
-        const bool vec = ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) |
-                           reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v)) & 15) == 0;
-        const long n4 = vec ? sg.n >> 2 : 0;
-        for (long i = start; i < n4; i += stride) {
-            float4 pp = reinterpret_cast<float4 *>(p)[i], mm = reinterpret_cast<float4 *>(m)[i],
-                   vv = reinterpret_cast<float4 *>(v)[i];
-            const float4 gg = reinterpret_cast<const float4 *>(g)[i];
+        const long e0 = 4L * (gi - a.q0[k]);
+        float *p = o.p + sg.off + e0, *m = o.m + sg.off + e0, *v = o.v + sg.off + e0;
+        const float *g = sg.g + e0;
+        const bool vec = e0 + 4 <= sg.n && ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) |
+                                              reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v)) & 15) == 0;
+        if (vec) {
+            float4 pp = *reinterpret_cast<float4 *>(p), mm = *reinterpret_cast<float4 *>(m),
+                   vv = *reinterpret_cast<float4 *>(v);
+            const float4 gg = *reinterpret_cast<const float4 *>(g);
             adam_one(pp.x, gg.x, mm.x, vv.x, step_size, bc2s, o.b1, o.b2, o.eps, o.wd, 1.0f);
             adam_one(pp.y, gg.y, mm.y, vv.y, step_size, bc2s, o.b1, o.b2, o.eps, o.wd, 1.0f);
             adam_one(pp.z, gg.z, mm.z, vv.z, step_size, bc2s, o.b1, o.b2, o.eps, o.wd, 1.0f);
             adam_one(pp.w, gg.w, mm.w, vv.w, step_size, bc2s, o.b1, o.b2, o.eps, o.wd, 1.0f);
-            reinterpret_cast<float4 *>(p)[i] = pp;
-            reinterpret_cast<float4 *>(m)[i] = mm;
-            reinterpret_cast<float4 *>(v)[i] = vv;
+            *reinterpret_cast<float4 *>(p) = pp;
+            *reinterpret_cast<float4 *>(m) = mm;
+            *reinterpret_cast<float4 *>(v) = vv;
+        } else {
+            const int ne = (int)min(4L, (long)sg.n - e0);
+            for (int e = 0; e < ne; ++e) adam_one(p[e], g[e], m[e], v[e], step_size, bc2s, o.b1, o.b2, o.eps, o.wd, 1.0f);
         }
-        for (long i = 4 * n4 + start; i < sg.n; i += stride)
-            adam_one(p[i], g[i], m[i], v[i], step_size, bc2s, o.b1, o.b2, o.eps, o.wd, 1.0f);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -229,13 +234,16 @@ int td7_adam_step_multi(int32_t nopt, float *const *p, float *const *m, float *c
         if (!p[k] || !m[k] || !v[k] || !step[k]) return EXO_EINVAL;
         a.o[k] = AdamOpt{p[k], m[k], v[k], step[k], lr[k], beta1[k], beta2[k], eps[k], weight_decay[k]};
     }
-    long total = 0;
+    long groups = 0;
     for (int k = 0; k < nseg; ++k) {
         if (!g[k] || n[k] <= 0 || off[k] < 0 || opt[k] < 0 || opt[k] >= nopt) return EXO_EINVAL;
         a.s[k] = AdamSeg{g[k], (long)off[k], n[k], opt[k]};
-        total = std::max<long>(total, n[k]);
+        a.q0[k] = (int)groups;
+        groups += (n[k] + 3) / 4;
     }
-    const long blocks = std::min<long>(ADAM_BLOCKS, (total / 4 + ADAM_THREADS - 1) / ADAM_THREADS + 1);
+    if (groups >= (1L << 30)) return EXO_ERANGE;
+    a.q0[nseg] = (int)groups;
+    const long blocks = (groups + ADAM_THREADS - 1) / ADAM_THREADS;
     hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)blocks), dim3(ADAM_THREADS), 0, (hipStream_t)stream, a);
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }

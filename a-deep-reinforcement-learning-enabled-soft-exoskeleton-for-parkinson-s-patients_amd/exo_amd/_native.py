@@ -129,8 +129,8 @@ EXPORTS = {
     "td7_dense_fwd_norm_cat": (c_int32, [c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                          c_void_p, c_void_p, c_long, c_long, c_int32, c_int32, c_int32, c_int32,
                                          ctypes.c_float, c_void_p]),
-    "td7_noisy_action_rng": (c_int32, [c_void_p, ctypes.c_uint64, ctypes.c_uint32, c_void_p, c_void_p, ctypes.c_float,
-                                       ctypes.c_float, ctypes.c_float, c_void_p, c_int32, c_void_p]),
+    "td7_noisy_action_rng": (c_int32, [c_void_p, ctypes.c_uint64, ctypes.c_uint32, c_void_p, c_void_p, c_void_p,
+                                       ctypes.c_float, ctypes.c_float, ctypes.c_float, c_void_p, c_int32, c_void_p]),
     "td7_dense_bwd_weight": (c_int32, [c_void_p, c_long, c_long, c_void_p, c_long, c_long, c_void_p, c_long,
                                        c_long, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32,
                                        c_void_p]),

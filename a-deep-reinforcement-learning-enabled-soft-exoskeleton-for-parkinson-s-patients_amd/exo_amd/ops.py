@@ -582,7 +582,8 @@ def noisy_action(a, noise, sigma, sigma_dec, clip=0.0, scale=1.0, rng=None):
             raise ValueError("noisy_action: noise=None needs a DeviceRNG on the GPU")
         a = a.contiguous()
         out = torch.empty_like(a)
-        nat.check(nat.lib().td7_noisy_action_rng(nat.ptr(a), rng.seed, rng.tag, rng.counter_ptr, nat.ptr(sigma),
+        nat.check(nat.lib().td7_noisy_action_rng(nat.ptr(a), rng.seed, rng.tag, rng.counter_ptr, rng.ticket_ptr,
+                                                 nat.ptr(sigma),
                                                  float(sigma_dec), float(clip), float(scale), nat.ptr(out), a.numel(),
                                                  nat.stream_ptr(a.device)), "td7_noisy_action_rng")
         return out

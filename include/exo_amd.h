@@ -312,10 +312,11 @@ int td7_noisy_action(const float *a_dev, const float *noise_dev, float *sigma_de
                      float scale, float *out_dev, int32_t n, void *stream);
 /* td7_noisy_action with the noise drawn in the kernel: element 2j+t is normal t
  * (Box-Muller) of Philox4x32-10 block (j, call, tag) under key seed, call =
- * *counter_dev, which advances by one per launch (graph-replay safe). */
+ * *counter_dev, which advances by one per launch (graph-replay safe);
+ * ticket_dev: one uint32, zero at the first call, left zero. */
 int td7_noisy_action_rng(const float *a_dev, uint64_t seed, uint32_t tag, unsigned long long *counter_dev,
-                         float *sigma_dev, float sigma_dec, float clip, float scale, float *out_dev, int32_t n,
-                         void *stream);
+                         uint32_t *ticket_dev, float *sigma_dev, float sigma_dec, float clip, float scale,
+                         float *out_dev, int32_t n, void *stream);
 /* F.mse_loss (encoder loss, TD7_multi_agent.py:226): *loss = mean (x - y)^2;
  * backward dx = 2 (x - y) / n * (*g).  ws_dev: TD7_MSE_WS floats, zeroed once
  * by the caller (block partials + a ticket the kernel leaves at zero); one

@@ -36,7 +36,7 @@ def test_noisy_action_rng_draws_box_muller_normals_of_philox():
     sigma = torch.tensor(0.1, device="cuda")
     outs = [ops.noisy_action(a, None, sigma, 0.0, rng=rng) for _ in range(2)]
     torch.cuda.synchronize()
-    assert int(rng.state[0]) == 2
+    assert int(rng.state[0]) == 2 and int(rng.state[1]) == 0
     for call, out in enumerate(outs):
         r = philox(np.arange((n + 1) // 2), call, 7, rng.seed).astype(np.float64)
         u1 = (np.floor(r[:, 0] / 256) + 1) * 2.0 ** -24
