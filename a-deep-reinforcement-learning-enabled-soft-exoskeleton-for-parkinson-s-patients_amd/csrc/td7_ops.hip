@@ -71,7 +71,7 @@ __global__ __launch_bounds__(256) void avgl1_bwd_kernel(const float *__restrict_
 // The step count lives on the device: every workgroup reads it, the last one
 // to finish (ticket counter) stores step + 1 and rearms the ticket, so one
 // launch is the whole optimiser step (HIP-graph safe, no host value).
-constexpr int ADAM_THREADS = 256, ADAM_BLOCKS = 512;
+constexpr int ADAM_THREADS = 256, ADAM_BLOCKS = 256, ADAM_MULTI_BLOCKS = 256;
 
 __device__ __forceinline__ void adam_one(float &p, float g, float &m, float &v, float step_size, float bc2s,
                                          float b1, float b2, float eps, float wd, float gscale) {
@@ -148,23 +148,30 @@ struct AdamMulti {
     uint32_t *ticket;
 };
 
-// One thread per 4-element group of the concatenated segments (every segment
-// padded to whole groups), so all segments are updated in one parallel pass.
+// Threads stride over the 4-element groups of the concatenated segments (every
+// segment padded to whole groups), so all segments are updated in one pass.
 __global__ __launch_bounds__(ADAM_THREADS) void adam_multi_kernel(AdamMulti a) {
     __shared__ float coef[TD7_ADAM_MAX_OPT][2];
+    __shared__ AdamSeg segs[TD7_ADAM_MAX_SEG];
+    __shared__ AdamOpt opts[TD7_ADAM_MAX_OPT];
+    // the descriptors staged in LDS (per-lane indexed reads of the kernel
+    // arguments would be dependent global loads ahead of the data loads)
+    if (threadIdx.x < a.nseg) segs[threadIdx.x] = a.s[threadIdx.x];
     if (threadIdx.x < a.nopt) {
-        const AdamOpt &o = a.o[threadIdx.x];
+        const AdamOpt o = a.o[threadIdx.x];
+        opts[threadIdx.x] = o;
         const float t = *o.step + 1.0f;
         coef[threadIdx.x][0] = o.lr / (1.0f - powf(o.b1, t));
         coef[threadIdx.x][1] = sqrtf(1.0f - powf(o.b2, t));
     }
     __syncthreads();
-    const int gi = blockIdx.x * ADAM_THREADS + threadIdx.x;
-    if (gi < a.q0[a.nseg]) {
+    // grid-stride over the groups: a bounded grid keeps the ticket atomics
+    // (one per workgroup, serialised on one address) few
+    for (int gi = blockIdx.x * ADAM_THREADS + threadIdx.x; gi < a.q0[a.nseg]; gi += gridDim.x * ADAM_THREADS) {
         int k = 0;
         for (int s = 1; s < a.nseg; ++s) k += gi >= a.q0[s];
-        const AdamSeg sg = a.s[k];
-        const AdamOpt o = a.o[sg.opt];
+        const AdamSeg sg = segs[k];
+        const AdamOpt o = opts[sg.opt];
         const float step_size = coef[sg.opt][0], bc2s = coef[sg.opt][1];
         const long e0 = 4L * (gi - a.q0[k]);
         float *p = o.p + sg.off + e0, *m = o.m + sg.off + e0, *v = o.v + sg.off + e0;
@@ -243,7 +250,7 @@ int td7_adam_step_multi(int32_t nopt, float *const *p, float *const *m, float *c
     }
     if (groups >= (1L << 30)) return EXO_ERANGE;
     a.q0[nseg] = (int)groups;
-    const long blocks = (groups + ADAM_THREADS - 1) / ADAM_THREADS;
+    const long blocks = std::min<long>(ADAM_MULTI_BLOCKS, (groups + ADAM_THREADS - 1) / ADAM_THREADS);
     hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)blocks), dim3(ADAM_THREADS), 0, (hipStream_t)stream, a);
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
