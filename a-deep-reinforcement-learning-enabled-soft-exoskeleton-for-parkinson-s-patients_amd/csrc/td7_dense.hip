@@ -33,6 +33,10 @@ namespace td7dense {
     extern template void launch_fwd_p<P, true>(const GemmArgs &, dim3, int, int, int, int, hipStream_t); \
     extern template void launch_fwd_norm_p<P, false>(const GemmArgs &, dim3, float *, float *, float, hipStream_t); \
     extern template void launch_fwd_norm_p<P, true>(const GemmArgs &, dim3, float *, float *, float, hipStream_t);
+extern template void launch_fwd_lds_p<PREC_BF16, false>(const GemmArgs &, dim3, int, hipStream_t);
+extern template void launch_fwd_lds_p<PREC_F16, false>(const GemmArgs &, dim3, int, hipStream_t);
+extern template void launch_fwd_lds_p<PREC_BF16, true>(const GemmArgs &, dim3, int, hipStream_t);
+extern template void launch_fwd_lds_p<PREC_F16, true>(const GemmArgs &, dim3, int, hipStream_t);
 TD7_EXTERN(PREC_F32)
 TD7_EXTERN(PREC_BF16)
 TD7_EXTERN(PREC_F16)
@@ -90,6 +94,30 @@ int launch_fwd(const GemmArgs &a, int groups_grid, int prec, hipStream_t s, bool
     const long span_b = (long)groups_grid * a.B.sg + (long)a.J * a.B.si + (long)a.R;
     if (span_a >= (1L << 29) || span_b >= (1L << 29) || a.A.sr != 1 || a.B.sr != 1) return EXO_ERANGE;
     const int steps = a.R >> 4;
+    // large layers with 16-bit operands: the LDS-tiled kernel when its 64 x 64
+    // tiles number >= 256 (one per CU) and K >= 256 (profiles/r01e_raw/
+    // lds_fwd.txt: 1.3-1.6x at 4,096 rows, 2.8x on the wide critic's
+    // 2 x 1,024 x 1,024 x 3,072, 4.7-5.7x at 65,536 rows; with fewer tiles it
+    // loses to the register-streaming kernel, cat_bench_lds1024.txt).
+    // EXO_FWD_LDS=0 disables it.
+    static const bool lds_on = [] {
+        const char *e = std::getenv("EXO_FWD_LDS");
+        return !(e && e[0] == '0');
+    }();
+    const long t64 = (long)((a.I + 63) / 64) * ((a.J + 63) / 64) * groups_grid;
+    if (prec != PREC_F32 && lds_on && t64 >= 256 && a.J >= 64 && a.R >= 256) {
+        const long t128 = (long)((a.I + 127) / 128) * ((a.J + 127) / 128) * groups_grid;
+        const int bm = t128 >= 256 ? 128 : 64;
+        dim3 grid((a.J + bm - 1) / bm, (a.I + bm - 1) / bm, groups_grid);
+        if (cat) {
+            if (prec == PREC_BF16) launch_fwd_lds_p<PREC_BF16, true>(a, grid, bm, s);
+            else launch_fwd_lds_p<PREC_F16, true>(a, grid, bm, s);
+        } else {
+            if (prec == PREC_BF16) launch_fwd_lds_p<PREC_BF16, false>(a, grid, bm, s);
+            else launch_fwd_lds_p<PREC_F16, false>(a, grid, bm, s);
+        }
+        return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
+    }
     static const int force = [] {
         const char *e = std::getenv("EXO_FWD_TILE");
         return e ? std::atoi(e) : 0;

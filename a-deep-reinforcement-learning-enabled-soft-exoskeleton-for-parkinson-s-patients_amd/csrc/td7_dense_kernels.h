@@ -701,6 +701,170 @@ void launch_fwd_norm_p(const GemmArgs &a, dim3 grid, float *hout, float *mean_ou
     hipLaunchKernelGGL((dense_fwd_norm_kernel<P, CAT>), grid, dim3(256), 0, s, a, hout, mean_out, eps);
 }
 
+// ---- forward of the large layers: LDS-tiled ---------------------------------
+// Y = act(X W^T + b) for the big GEMMs (the batched policy over thousands of
+// envs, the 1024-wide configuration), bf16 / fp16 operands only.  A workgroup
+// (4 waves as 2 x 2) owns a BM x BN output tile; per 32-deep K slice every
+// thread loads (BM + BN) x 32 / 256 fp32 values with 16-byte buffer loads,
+// rounds them to 16-bit and stores them to LDS (double-buffered, rows padded
+// to 40 halves against bank conflicts); each wave then runs (BM/32) x (BN/32)
+// 16x16x16 MFMAs per 16-deep step from LDS fragments.  The next slice's global
+// loads are in flight while the current one is multiplied.  Compared with the
+// register-streaming kernel above, each global byte feeds BM/16 (resp. BN/16)
+// MFMA tiles instead of 1-2.
+template <int P>
+__device__ __forceinline__ uint16_t to_half_bits(float v) {
+    if constexpr (P == PREC_F16) return __builtin_bit_cast(uint16_t, (_Float16)v);
+    else return __builtin_bit_cast(uint16_t, (__bf16)v);
+}
+
+template <int EP, int P, int BM, int BN, bool CAT>
+__global__ __launch_bounds__(256) void dense_fwd_lds_kernel(GemmArgs a) {
+    constexpr int BK = 32, LDK = 40;                 // halves per LDS row (32 + 8 pad)
+    constexpr int AL = BM * BK / 256 / 4, BL = BN * BK / 256 / 4;  // 16-byte loads per thread per slice
+    constexpr int TM = BM / 32, TN = BN / 32;        // 16x16 MFMA tiles per wave
+    __shared__ __attribute__((aligned(16))) uint16_t As[2][BM][LDK];
+    __shared__ __attribute__((aligned(16))) uint16_t Bs[2][BN][LDK];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, q = lane >> 4, c = lane & 15;
+    const int wm = w >> 1, wn = w & 1;
+    const int3 tile = xcd_tile();
+    const int i0 = tile.y * BM, j0 = tile.x * BN, g = tile.z;
+    const __amdgpu_buffer_rsrc_t ra = rsrc(a.A.p), rb = rsrc(a.B.p);
+    const int K = a.R, nk = (K + BK - 1) / BK;
+    // this thread's load slots: row (t >> 3) + 32 l, k chunk 4 (t & 7)
+    const int lr = t >> 3, lk = 4 * (t & 7);
+    const CatRows cr(a.cat, CAT ? g : 0);
+    float ra_v[AL][4], rb_v[BL][4];
+    auto gload = [&](int kt) {
+        const int k = kt * BK + lk;
+        const bool full = k + 4 <= K;
+#pragma unroll
+        for (int l = 0; l < AL; ++l) {
+            const int row = i0 + lr + 32 * l;
+            const bool ok = row < a.I;
+            if constexpr (CAT) { // the chunk k .. k+3 lies in one segment
+                const float *p = cr.ptr(ok ? row : 0, (k < K) ? k : 0);
+                if (full) {
+                    const auto v = gload4(p, cr.cb0, ok);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) ra_v[l][e] = __uint_as_float(v[e]);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) ra_v[l][e] = (ok & (k + e < K)) ? p[e] : 0.f;
+                }
+                continue;
+            }
+            const int base = g * (int)a.A.sg + row * (int)a.A.si + k;
+            if (full) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(ra, ok ? base * 4 : BUF_OOB, 0, 0);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) ra_v[l][e] = __uint_as_float(v[e]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) ra_v[l][e] = ldb(ra, ok & (k + e < K), base + e);
+            }
+        }
+#pragma unroll
+        for (int l = 0; l < BL; ++l) {
+            const int col = j0 + lr + 32 * l;
+            const bool ok = col < a.J;
+            const int base = g * (int)a.B.sg + col * (int)a.B.si + k;
+            if (full) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(rb, ok ? base * 4 : BUF_OOB, 0, 0);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) rb_v[l][e] = __uint_as_float(v[e]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) rb_v[l][e] = ldb(rb, ok & (k + e < K), base + e);
+            }
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int l = 0; l < AL; ++l) {
+            uint16_t h[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) h[e] = to_half_bits<P>(ra_v[l][e]);
+            *reinterpret_cast<uint2 *>(&As[buf][lr + 32 * l][lk]) = __builtin_bit_cast(uint2, h);
+        }
+#pragma unroll
+        for (int l = 0; l < BL; ++l) {
+            uint16_t h[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) h[e] = to_half_bits<P>(rb_v[l][e]);
+            *reinterpret_cast<uint2 *>(&Bs[buf][lr + 32 * l][lk]) = __builtin_bit_cast(uint2, h);
+        }
+    };
+    floatx4 acc[TM][TN];
+#pragma unroll
+    for (int x = 0; x < TM; ++x)
+#pragma unroll
+        for (int y = 0; y < TN; ++y) acc[x][y] = floatx4{0.f, 0.f, 0.f, 0.f};
+    auto compute = [&](int buf) {
+#pragma unroll
+        for (int ks = 0; ks < BK; ks += 16) {
+            shortx4 af[TM], bf[TN];
+#pragma unroll
+            for (int x = 0; x < TM; ++x)
+                af[x] = *reinterpret_cast<const shortx4 *>(&As[buf][wm * (BM / 2) + 16 * x + c][ks + 4 * q]);
+#pragma unroll
+            for (int y = 0; y < TN; ++y)
+                bf[y] = *reinterpret_cast<const shortx4 *>(&Bs[buf][wn * (BN / 2) + 16 * y + c][ks + 4 * q]);
+#pragma unroll
+            for (int x = 0; x < TM; ++x)
+#pragma unroll
+                for (int y = 0; y < TN; ++y) {
+                    if constexpr (P == PREC_F16)
+                        acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(halfx4, af[x]),
+                                                                          __builtin_bit_cast(halfx4, bf[y]), acc[x][y],
+                                                                          0, 0, 0);
+                    else
+                        acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(af[x], bf[y], acc[x][y], 0, 0, 0);
+                }
+        }
+    };
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nk) gload(kt + 1);
+        compute(buf);
+        if (kt + 1 < nk) lstore(buf ^ 1);
+        __syncthreads();
+    }
+    // acc[x][y][k] is C[i0 + wm BM/2 + 16x + 4q + k][j0 + wn BN/2 + 16y + c]
+#pragma unroll
+    for (int y = 0; y < TN; ++y) {
+        const int col = j0 + wn * (BN / 2) + 16 * y + c;
+        if (col >= a.J) continue;
+        const float bv = a.bias ? a.bias[g * a.bsg + col] : 0.f;
+#pragma unroll
+        for (int x = 0; x < TM; ++x)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int row = i0 + wm * (BM / 2) + 16 * x + 4 * q + k;
+                if (row < a.I) a.C[g * a.csg + (long)row * a.csi + (long)col * a.csj] = act_fwd_t<EP>(acc[x][y][k] + bv);
+            }
+    }
+}
+
+template <int P, bool CAT>
+void launch_fwd_lds_p(const GemmArgs &a, dim3 grid, int bm, hipStream_t s) {
+#define FWD_LDS(EPv)                                                                                    \
+    do {                                                                                              \
+        if (bm == 128) hipLaunchKernelGGL((dense_fwd_lds_kernel<EPv, P, 128, 128, CAT>), grid, dim3(256), 0, s, a); \
+        else hipLaunchKernelGGL((dense_fwd_lds_kernel<EPv, P, 64, 64, CAT>), grid, dim3(256), 0, s, a);          \
+    } while (0)
+    switch (a.act) {
+    case ACT_RELU: FWD_LDS(ACT_RELU); break;
+    case ACT_ELU: FWD_LDS(ACT_ELU); break;
+    case ACT_TANH: FWD_LDS(ACT_TANH); break;
+    default: FWD_LDS(ACT_NONE); break;
+    }
+#undef FWD_LDS
+}
+
 // ---- bwd-weight on the output-contiguous layout ------------------------------
 // dW[g][i][j] = sum_m dP[m][i] X[m][j], dP = dY * act'(Y), db[g][i] = sum_m dP[m][i].
 // Both operands are contiguous along the OUTPUT dimensions (i resp. j) and

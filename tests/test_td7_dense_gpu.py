@@ -349,3 +349,29 @@ def test_dense_norm_matches_separate_ops(case, prec):
     torch.testing.assert_close(outs[0][2], outs[1][2], rtol=tol, atol=tol * 20)
     for a, r in zip(outs[0][3], outs[1][3]):
         torch.testing.assert_close(a, r, rtol=tol, atol=tol * 20)
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+@pytest.mark.parametrize("g,m,n,k,cat", [(1, 1100, 130, 333, False), (2, 1024, 320, 920, True), (1, 4096, 300, 300, False),
+                                         (1, 1031, 70, 259, True), (2, 2048, 1024, 1027, False)])
+def test_lds_forward_kernel_is_the_gemm_of_rounded_operands(prec, g, m, n, k, cat):
+    """The LDS-tiled forward (td7_dense_fwd / _fwd_cat with 16-bit operands at
+    >= 1,024 rows and K >= 256): ragged edges, groups, concatenated inputs."""
+    from exo_amd import ops
+    torch.manual_seed(m + n + k)
+    dt = _ROUND[prec]
+    w = torch.randn(g, n, k, device="cuda") / k ** 0.5 if g > 1 else torch.randn(n, k, device="cuda") / k ** 0.5
+    b = torch.randn(g, n, device="cuda") if g > 1 else torch.randn(n, device="cuda")
+    if cat:  # [q (per group) | e (shared)] with a 4-aligned boundary
+        k0 = (k // 3) // 4 * 4
+        parts = [torch.randn(g, m, k0, device="cuda") if g > 1 else torch.randn(m, k0, device="cuda"),
+                 torch.randn(m, k - k0, device="cuda")]
+        with ops.matrix_precision(prec):
+            y = ops.dense_cat(parts, w, b, 2)
+        x = torch.cat([parts[0], parts[1].expand(g, m, k - k0) if g > 1 else parts[1]], -1)
+    else:
+        x = torch.randn(g, m, k, device="cuda") if g > 1 else torch.randn(m, k, device="cuda")
+        with ops.matrix_precision(prec):
+            y = ops.dense(x, w, b, 2)
+    ref = torch.nn.functional.elu(x.to(dt).float() @ w.to(dt).float().transpose(-1, -2) + b.unsqueeze(-2))
+    torch.testing.assert_close(y, ref.reshape(y.shape), rtol=1e-4, atol=1e-4)
