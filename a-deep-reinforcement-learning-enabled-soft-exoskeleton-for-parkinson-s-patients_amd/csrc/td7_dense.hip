@@ -95,7 +95,8 @@ int launch_fwd(const GemmArgs &a, int groups_grid, int prec, hipStream_t s, bool
     if (span_a >= (1L << 29) || span_b >= (1L << 29) || a.A.sr != 1 || a.B.sr != 1) return EXO_ERANGE;
     const int steps = a.R >> 4;
     // large layers with 16-bit operands: the LDS-tiled kernel when its 64 x 64
-    // tiles number >= 256 (one per CU) and K >= 256 (profiles/r01e_raw/
+    // tiles number >= 256 (one per CU) and K >= 256, or >= 2,048 tiles and K >= 64
+    // (profiles/r01e_raw/
     // lds_fwd.txt: 1.3-1.6x at 4,096 rows, 2.8x on the wide critic's
     // 2 x 1,024 x 1,024 x 3,072, 4.7-5.7x at 65,536 rows; with fewer tiles it
     // loses to the register-streaming kernel, cat_bench_lds1024.txt).
@@ -105,7 +106,7 @@ int launch_fwd(const GemmArgs &a, int groups_grid, int prec, hipStream_t s, bool
         return !(e && e[0] == '0');
     }();
     const long t64 = (long)((a.I + 63) / 64) * ((a.J + 63) / 64) * groups_grid;
-    if (prec != PREC_F32 && lds_on && t64 >= 256 && a.J >= 64 && a.R >= 256) {
+    if (prec != PREC_F32 && lds_on && a.J >= 64 && ((t64 >= 256 && a.R >= 256) || (t64 >= 2048 && a.R >= 64))) {
         const long t128 = (long)((a.I + 127) / 128) * ((a.J + 127) / 128) * groups_grid;
         const int bm = t128 >= 256 ? 128 : 64;
         dim3 grid((a.J + bm - 1) / bm, (a.I + bm - 1) / bm, groups_grid);
