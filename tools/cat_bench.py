@@ -17,12 +17,14 @@ def main():
     L = nat.lib()
     dev = torch.device("cuda")
     s = nat.stream_ptr(dev)
-    M = 1024
+    M = int(os.environ.get("CB_ROWS", "1024"))
     cases = {"critic1 [q(2)|zsa|zs] 920": ([(2, 320), (1, 300), (1, 300)], 2, 320),
              "critic0 [state|action] 87": ([(1, 80), (1, 7)], 2, 320),
              "zsa1 [zs|action] 307": ([(1, 300), (1, 7)], 1, 300),
              "actor1 [a|zs] 620": ([(1, 320), (1, 300)], 1, 320),
-             "aligned [a|b] 640": ([(1, 320), (1, 320)], 1, 320)}
+             "aligned [a|b] 640": ([(1, 320), (1, 320)], 1, 320),
+             "wide critic1 [q(2)|zsa|zs] 3072": ([(2, 1024), (1, 1024), (1, 1024)], 2, 1024),
+             "wide actor1 [a|zs] 2048": ([(1, 1024), (1, 1024)], 1, 1024)}
     for name, (segs, G, N) in cases.items():
         parts = [torch.randn(M, k, device=dev) if g == 1 else torch.randn(g, M, k, device=dev) for g, k in segs]
         K = sum(k for _, k in segs)
@@ -44,7 +46,7 @@ def main():
         t_copy = timeit(lambda: torch.cat(parts if G == 1 or not any(p.dim() == 3 for p in parts) else
                                           [p if p.dim() == 3 else p.unsqueeze(0).expand(G, M, p.shape[-1])
                                            for p in parts], -1))
-        print(f"{name:30s} cat-kernel {t_cat:7.2f} us | plain kernel {t_plain:7.2f} us + torch.cat {t_copy:6.2f} us")
+        print(f"M={M} {name:34s} cat-kernel {t_cat:7.2f} us | plain kernel {t_plain:7.2f} us + torch.cat {t_copy:6.2f} us")
 
 
 if __name__ == "__main__":
