@@ -96,6 +96,34 @@ __device__ __forceinline__ int cat_seg(const CatSeg &c, int r) {
     return (r >= c.kb[1]) + (r >= c.kb[2]) + (r >= c.kb[3]);
 }
 
+// The b128 chunk X(row, r .. r+3) of a CAT operand from segment sg (wave-
+// uniform): one buffer load whose lanes outside the segment (or !ok) read past
+// the records, i.e. 0.  Returned unconsumed, so the load stays in flight.
+// (uniform branches with constant indices: a dynamic index into the kernel
+// arguments would put them in scratch)
+__device__ __forceinline__ uint32_t4 cat_load_seg(const CatSeg &c, int sg, int g, int row, int r, bool ok) {
+    uint32_t4 v = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < CAT_MAX; ++k) {
+        if (sg != k) continue;
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(c.p[k] + g * c.sg[k]), 0, 0x7FFFFF00, 0x00020000);
+        const bool in = ok & (r >= c.kb[k]) & (r < c.kb[k + 1]);
+        v = __builtin_amdgcn_raw_buffer_load_b128(rs, in ? (row * c.ld[k] + (r - c.kb[k])) * 4 : 0x7FFFFF00, 0, 0);
+    }
+    return v;
+}
+
+// ... for a wave-uniform reduction window [w0, w1] (the columns a load
+// instruction covers): one load when the window lies in one segment (the
+// common case); a window across a boundary ORs its segments' loads.
+__device__ __forceinline__ uint32_t4 cat_load(const CatSeg &c, int g, int row, int r, bool ok, int w0, int w1) {
+    const int sa = cat_seg(c, w0), sb = cat_seg(c, w1);
+    uint32_t4 v = cat_load_seg(c, sa, g, row, r, ok);
+    for (int sg = sa + 1; sg <= sb; ++sg) v |= cat_load_seg(c, sg, g, row, r, ok);
+    return v;
+}
+
 struct GemmArgs {
     CatSeg cat; // forward with CAT: the A operand (X) by segments
     Operand A, B;
@@ -403,6 +431,8 @@ __global__ __launch_bounds__(64 * KW) void dense_fwd_kernel(GemmArgs a) {
 #pragma unroll
             for (int x = 0; x < TM; ++x) {
                 if constexpr (CAT) {
+                    // (16-byte global loads: per-segment buffer loads behind
+                    // uniform branches measured slower in this kernel)
                     const auto v = ld_cat(x, r, live & arow[x]);
 #pragma unroll
                     for (int jj = 0; jj < 4; ++jj) av[s][x][jj] = v[jj];
@@ -743,12 +773,13 @@ __global__ __launch_bounds__(256) void dense_fwd_lds_kernel(GemmArgs a) {
             const int row = i0 + lr + 32 * l;
             const bool ok = row < a.I;
             if constexpr (CAT) { // the chunk k .. k+3 lies in one segment
-                const float *p = cr.ptr(ok ? row : 0, (k < K) ? k : 0);
                 if (full) {
-                    const auto v = gload4(p, cr.cb0, ok);
+                    const int w0 = kt * BK;
+                    const auto v = cat_load(a.cat, g, ok ? row : 0, k, ok, w0, min(w0 + BK - 1, K - 1));
 #pragma unroll
                     for (int e = 0; e < 4; ++e) ra_v[l][e] = __uint_as_float(v[e]);
                 } else {
+                    const float *p = cr.ptr(ok ? row : 0, (k < K) ? k : 0);
 #pragma unroll
                     for (int e = 0; e < 4; ++e) ra_v[l][e] = (ok & (k + e < K)) ? p[e] : 0.f;
                 }
@@ -944,6 +975,7 @@ __global__ __launch_bounds__(64 * NW) void dense_wgrad_kernel(WgradArgs a) {
 
     struct Buf {
         float a[KS][VA], y[KS][VA], b[KS][4];
+        bool lv[CAT ? KS : 1]; // CAT: row m in range (the X load is masked where consumed)
     };
     floatx4 acc[VA][4];
     float bsum[VA];
@@ -962,7 +994,9 @@ __global__ __launch_bounds__(64 * NW) void dense_wgrad_kernel(WgradArgs a) {
             ld_vec<VA>(rdy, live ? (dyb + m * a.lddy) * 4 : BUF_OOB, f.a[sp]);
             if (AG > 0) ld_vec<VA>(ry, live ? (yb + m * a.ldy) * 4 : BUF_OOB, f.y[sp]);
             if constexpr (CAT) {
-                const uint32_t4 v = gload4(xcat + (long)m * xld, xcat, live);
+                // a valid address for dead rows, zeroed at the MFMA (no wait here)
+                const uint32_t4 v = *(gptr4)(live ? xcat + (long)m * xld : xcat);
+                f.lv[CAT ? sp : 0] = live;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) f.b[sp][e] = __uint_as_float(v[e]);
             } else {
@@ -987,7 +1021,10 @@ __global__ __launch_bounds__(64 * NW) void dense_wgrad_kernel(WgradArgs a) {
                         fa[s][e] = v;
                     }
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) fb[u][e] = shifted<4>(f.b[s4 + e], shj, u);
+                    for (int u = 0; u < 4; ++u) {
+                        fb[u][e] = shifted<4>(f.b[s4 + e], shj, u);
+                        if constexpr (CAT) fb[u][e] = f.lv[CAT ? s4 + e : 0] ? fb[u][e] : 0.f;
+                    }
                 }
 #pragma unroll
                 for (int s = 0; s < VA; ++s)
@@ -1006,7 +1043,10 @@ __global__ __launch_bounds__(64 * NW) void dense_wgrad_kernel(WgradArgs a) {
                 bsum[s] += fa[s];
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) fb[u] = shifted<4>(f.b[sp], shj, u);
+            for (int u = 0; u < 4; ++u) {
+                fb[u] = shifted<4>(f.b[sp], shj, u);
+                if constexpr (CAT) fb[u] = f.lv[CAT ? sp : 0] ? fb[u] : 0.f;
+            }
 #pragma unroll
             for (int s = 0; s < VA; ++s)
 #pragma unroll
