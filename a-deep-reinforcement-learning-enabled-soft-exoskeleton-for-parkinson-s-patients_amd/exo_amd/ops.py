@@ -292,6 +292,8 @@ class _DenseNormFn(torch.autograd.Function):
 
 
 _NORM = os.environ.get("EXO_TD7_NORM_FUSED", "1") != "0"
+# fuse below 2,048 rows too (A/B switch)
+_NORM_SMALL = os.environ.get("EXO_TD7_NORM_SMALL", "1") != "0"
 
 
 def dense_norm(parts, w, b):
@@ -299,7 +301,8 @@ def dense_norm(parts, w, b):
     GPU where it applies (N <= 320, the concatenated-input rules of
     dense_cat); the two ops otherwise."""
     ok = (_NORM and w.is_cuda and w.dtype == torch.float32 and not torch.is_autocast_enabled()
-          and w.shape[-2] <= 320 and (_matrix_prec or parts[0].shape[-2] <= _DenseFn.fwd_kernel_max_rows))
+          and w.shape[-2] <= 320 and (_matrix_prec or parts[0].shape[-2] <= _DenseFn.fwd_kernel_max_rows)
+          and (_NORM_SMALL or parts[0].shape[-2] >= 2048))
     if ok and len(parts) > 1:
         ok = _CAT and _cat_ok(parts, w)
     elif ok:
