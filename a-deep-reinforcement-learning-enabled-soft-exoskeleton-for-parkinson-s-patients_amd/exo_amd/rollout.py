@@ -230,6 +230,7 @@ class VecTrainer:
             self.k_dev.fill_(self.k)
         L.training_steps += 1
         update_actor = L.training_steps % ag.hp.policy_freq == 0
+        L.prefetch_actor = update_actor  # phase_grads may start the actor forward early
         if not self.use_graphs or self.iters < self.warmup_eager:
             self._eager(update_actor)
         elif update_actor not in self.graphs:

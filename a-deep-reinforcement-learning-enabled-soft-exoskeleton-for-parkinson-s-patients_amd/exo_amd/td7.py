@@ -504,6 +504,10 @@ class TD7Learner:
     # the encoder's Adam step on the branch -- no gain -- and LAP.update_priority
     # on a third branch -- slower).  EXO_TD7_OVERLAP=0 serialises.
     overlap = os.environ.get("EXO_TD7_OVERLAP", "1") == "1"
+    # the actor forward of an actor-update iteration on its own branch during the
+    # critic update (set per iteration by the trainer through prefetch_actor)
+    actor_branch = os.environ.get("EXO_TD7_ACTOR_BRANCH", "1") == "1"
+    prefetch_actor = False
 
     def _encoder_grads(self, state, action, next_state):
         """:219-228 -- loss and gradients of the live encoder."""
@@ -557,6 +561,19 @@ class TD7Learner:
                 else:
                     fixed_target_zs = self.fixed_encoder_target.zs(next_state)
                     fixed_zs = self.fixed_encoder.zs(state)
+        if split and self.prefetch_actor and self.actor_branch:
+            # this iteration also updates the actor (:268-277): its forward and
+            # the fixed encoder's zsa of its actions read no weight the critic /
+            # encoder steps change, so they run now on a fourth branch, under
+            # the critic's backward; only the critic pass of the actor loss
+            # waits for the new critic weights (phase_actor_grads)
+            cur = torch.cuda.current_stream(self.device)
+            if getattr(self, "_aside", None) is None:
+                self._aside = torch.cuda.Stream(device=self.device)
+            self._aside.wait_stream(cur)
+            with torch.cuda.stream(self._aside), self._autocast():
+                actor = self.actor(state, fixed_zs)
+                self._actor_pre = (actor, self.fixed_encoder.zsa(fixed_zs, actor))
         if split:
             # the target chain (actor_target -> zsa -> critic_target -> Q_target,
             # :236-246) as a third branch, concurrent with the online critic's
@@ -595,6 +612,8 @@ class TD7Learner:
             critic_loss.backward()
         if side is not None:
             self.join_side()
+        if getattr(self, "_actor_pre", None) is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._aside)
         self._fixed_zs = fixed_zs
         return priority
 
@@ -647,9 +666,13 @@ class TD7Learner:
     def phase_actor_grads(self, state, action):
         """:268-277 with the just-updated critic."""
         fixed_zs = self._fixed_zs
+        pre, self._actor_pre = getattr(self, "_actor_pre", None), None
         with self._autocast():
-            actor = self.actor(state, fixed_zs)
-            fixed_zsa = self.fixed_encoder.zsa(fixed_zs, actor)
+            if pre is not None:  # computed on the actor branch of phase_grads
+                actor, fixed_zsa = pre
+            else:
+                actor = self.actor(state, fixed_zs)
+                fixed_zsa = self.fixed_encoder.zsa(fixed_zs, actor)
             Q = self.critic(state, actor, fixed_zsa, fixed_zs)
         self.actor_optimizer.zero_grad(set_to_none=self.grads_to_none)
         # gradients of the actor's parameters only: the reference's backward()
