@@ -375,3 +375,34 @@ def test_lds_forward_kernel_is_the_gemm_of_rounded_operands(prec, g, m, n, k, ca
             y = ops.dense(x, w, b, 2)
     ref = torch.nn.functional.elu(x.to(dt).float() @ w.to(dt).float().transpose(-1, -2) + b.unsqueeze(-2))
     torch.testing.assert_close(y, ref.reshape(y.shape), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+@pytest.mark.parametrize("case", ["plain", "cat", "shared"])
+def test_large_weight_gradient_as_lds_gemm(prec, case, monkeypatch):
+    """Weight and bias gradients of the wide layers through the LDS-tiled GEMM on
+    transposed operands (ops._wgrad_lds) == the output-contiguous wgrad kernel."""
+    from exo_amd import ops
+    torch.manual_seed(len(case))
+    M, N = 1024, 1024
+    if case == "plain":
+        parts, w = [torch.randn(M, 1024, device="cuda")], torch.randn(N, 1024, device="cuda") / 32
+        b = torch.randn(N, device="cuda")
+    elif case == "cat":      # the wide critic's [q | zsa | zs]
+        parts = [torch.randn(2, M, 1024, device="cuda"), torch.randn(M, 1024, device="cuda"),
+                 torch.randn(M, 1024, device="cuda")]
+        w, b = torch.randn(2, N, 3072, device="cuda") / 55, torch.randn(2, N, device="cuda")
+    else:                    # one input shared by the two heads
+        parts, w = [torch.randn(M, 1024, device="cuda")], torch.randn(2, N, 1024, device="cuda") / 32
+        b = torch.randn(2, N, device="cuda")
+    outs = []
+    for on in (True, False):
+        monkeypatch.setattr(ops, "_WGRAD_GEMM", on)
+        ww, bb = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+        with ops.matrix_precision(prec):
+            y = ops.dense_cat(parts, ww, bb, 2) if len(parts) > 1 else ops.dense(parts[0], ww, bb, 2)
+        torch.manual_seed(3)
+        y.backward(torch.randn_like(y))
+        outs.append((ww.grad, bb.grad))
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=2e-3, atol=2e-3)
+    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-4, atol=1e-3)
