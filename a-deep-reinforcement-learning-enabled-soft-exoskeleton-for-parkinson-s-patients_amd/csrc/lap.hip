@@ -91,6 +91,26 @@ __global__ __launch_bounds__(UPD_THREADS) void lap_add_kernel(float *tree, const
     }
 }
 
+// Sum of the leaves [0, sz) of one stratum's tree: the reference samples
+// against cumsum(priority[i, :size]) (:76-77), and with its single-add pointer
+// quirk (:59-61) strata 1..E-1 hold their newest transition at slot == size,
+// outside that prefix -- so the draw is scaled by the prefix total, not the
+// root.  One root-to-leaf walk towards leaf sz adding every left sibling.
+__device__ __forceinline__ float prefix_total(const float *T, int cap, int levels, int sz) {
+    if (sz >= cap) return T[1];
+    float acc = 0.0f;
+    int node = 1;
+    for (int lv = levels - 1; lv >= 0; --lv) {
+        if ((sz >> lv) & 1) {
+            acc += T[2 * node];
+            node = 2 * node + 1;
+        } else {
+            node = 2 * node;
+        }
+    }
+    return acc;
+}
+
 // LAP.sample (:75-78): idx = searchsorted_left(cumsum(p[:size]), u * total)
 __global__ void lap_sample_kernel(const float *tree, int cap, int levels, const float *u, const int32_t *size,
                                   int batch, int32_t *idx) {
@@ -98,7 +118,8 @@ __global__ void lap_sample_kernel(const float *tree, int cap, int levels, const 
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= batch) return;
     const float *T = tree + (size_t)s * 2 * cap;
-    float val = u[(size_t)s * batch + b] * T[1];
+    const int sz = size[s];
+    float val = u[(size_t)s * batch + b] * prefix_total(T, cap, levels, sz);
     int node = 1;
     for (int lv = 0; lv < levels; ++lv) {
         const float left = T[2 * node], right = T[2 * node + 1];
@@ -110,7 +131,6 @@ __global__ void lap_sample_kernel(const float *tree, int cap, int levels, const 
         }
     }
     int i = node - cap;
-    const int sz = size[s];
     if (i >= sz) i = sz > 0 ? sz - 1 : 0;
     idx[(size_t)s * batch + b] = i;
 }
@@ -282,7 +302,8 @@ __device__ __forceinline__ void sample_descend(const float *tree, int cap, int l
                                                float *o_next, float *o_reward, float *o_not_done) {
     const int s = d / batch;
     const float *T = tree + (size_t)s * 2 * cap;
-    float val = ud * T[1];
+    const int sz = size[s];
+    float val = ud * prefix_total(T, cap, levels, sz);
     int node = 1;
     for (int lv = 0; lv < levels; ++lv) {
         const float left = T[2 * node], right = T[2 * node + 1];
@@ -294,7 +315,6 @@ __device__ __forceinline__ void sample_descend(const float *tree, int cap, int l
         }
     }
     int i = node - cap;
-    const int sz = size[s];
     if (i >= sz) i = sz > 0 ? sz - 1 : 0;
     if (lane == 0) idx[d] = i;
     const long r = (long)s * (capacity + 1) + i;

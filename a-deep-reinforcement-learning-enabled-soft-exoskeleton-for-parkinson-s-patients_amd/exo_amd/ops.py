@@ -148,9 +148,7 @@ class _DenseFn(torch.autograd.Function):
             nat.check(nat.lib().td7_dense_bwd_data_cols(nat.ptr(dy), M * N, N, nat.ptr(y), M * N, N, nat.ptr(w),
                                                         nat.ptr(dx), M * K, K, G, int(shared), M, N, K, c0, c1, act,
                                                         s), "td7_dense_bwd_data")
-        if (need[1] or (has_b and need[2])) and _wgrad_as_gemm(G, M, N, K, act):
-            dw, db = _wgrad_lds(dy, y, [x], w, G, M, N, K, act, has_b, grouped)
-        elif need[1] or (has_b and need[2]):
+        if need[1] or (has_b and need[2]):
             dw = torch.empty_like(w)
             db = torch.empty((G, N) if grouped else (N,), dtype=torch.float32, device=dy.device) if has_b else None
             nat.check(nat.lib().td7_dense_bwd_weight(nat.ptr(dy), M * N, N, nat.ptr(y), M * N, N, nat.ptr(x), xsg,
@@ -215,14 +213,11 @@ def _parts_backward(ctx, dy, w, y, parts, meta):
     dw = db = None
     if (ctx.needs_input_grad[0] and _engine_needs(ctx, ctx.edge[0])) or \
             (has_b and ctx.needs_input_grad[1] and _engine_needs(ctx, ctx.edge[1])):
-        if _wgrad_as_gemm(G, M, N, K, act):
-            dw, db = _wgrad_lds(dy, y, parts, w, G, M, N, K, act, has_b, grouped)
-        else:
-            dw = torch.empty_like(w)
-            db = torch.empty((G, N) if grouped else (N,), dtype=torch.float32, device=dy.device) if has_b else None
-            nat.check(nat.lib().td7_dense_bwd_weight_cat(nat.ptr(dy), M * N, N, nat.ptr(y), M * N, N, n,
-                                                         *_seg_arrays(parts, sgs, lds, widths), nat.ptr(dw),
-                                                         nat.ptr(db), G, M, N, act, s), "td7_dense_bwd_weight_cat")
+        dw = torch.empty_like(w)
+        db = torch.empty((G, N) if grouped else (N,), dtype=torch.float32, device=dy.device) if has_b else None
+        nat.check(nat.lib().td7_dense_bwd_weight_cat(nat.ptr(dy), M * N, N, nat.ptr(y), M * N, N, n,
+                                                     *_seg_arrays(parts, sgs, lds, widths), nat.ptr(dw),
+                                                     nat.ptr(db), G, M, N, act, s), "td7_dense_bwd_weight_cat")
     grads = []
     c0 = 0
     for i, p in enumerate(parts):
@@ -238,40 +233,6 @@ def _parts_backward(ctx, dy, w, y, parts, meta):
         grads.append(g)
         c0 += k
     return (dw, db, None, *grads)
-
-
-_WGRAD_GEMM = os.environ.get("EXO_TD7_WGRAD_GEMM", "0") == "1"  # measured neutral, off
-_ACT_GRAD = {1: lambda y: (y > 0).to(y.dtype), 2: lambda y: torch.where(y > 0, 1.0, y + 1.0),
-             3: lambda y: 1.0 - y * y}
-
-
-def _wgrad_as_gemm(G, M, N, K, act):
-    """Large 16-bit weight gradients (the 1024-wide configuration) go through
-    the LDS-tiled forward GEMM on transposed operands (_wgrad_lds); the
-    output-contiguous wgrad kernel stays for the TD7 default widths."""
-    return _WGRAD_GEMM and (act >> 8) != 0 and N >= 256 and K >= 256 and M >= 256 and G * N * K >= (1 << 21)
-
-
-def _wgrad_lds(dy, y, parts, w, G, M, N, K, act, has_b, grouped):
-    """dW = dP^T X and db = colsum(dP), dP = dY * act'(Y): the transposes
-    dP^T [G,N,M] and X^T [G,K,M] are materialised so the reduction over the
-    batch rows is contiguous, then one td7_dense_fwd (LDS-tiled, the layer's
-    operand precision) computes dW[g] = dP^T[g] (X^T[g])^T.  A shared part is
-    broadcast to the groups in X^T."""
-    a, prec = act & 0xFF, act >> 8
-    dp = dy * _ACT_GRAD[a](y) if a else dy
-    dp = dp.reshape(G, M, N)
-    dpt = dp.transpose(1, 2).contiguous()                                         # [G, N, M]
-    xs = [(p if p.dim() == 3 else p.unsqueeze(0).expand(G, M, p.shape[-1])) for p in parts]
-    xt = torch.cat([x.transpose(1, 2) for x in xs], 1).contiguous()              # [G, K, M]
-    dw = torch.empty((G, N, K), dtype=torch.float32, device=dy.device)
-    nat.check(nat.lib().td7_dense_fwd(nat.ptr(dpt), N * M, M, nat.ptr(xt), None, nat.ptr(dw), N * K, K, G, N, K, M,
-                                      prec << 8, nat.stream_ptr(dy.device)), "td7_dense_fwd")
-    db = dp.sum(1) if has_b else None
-    if not grouped:
-        dw = dw[0]
-        db = db[0] if db is not None else None
-    return dw, db
 
 
 def _parts_meta(w, parts):

@@ -64,9 +64,11 @@ class VecTrainer:
                        if strata is None else strata)
         # two observation buffers used in alternation (iteration i reads obs[c]
         # and the env writes its next observation into obs[1 - c]): no copy of
-        # the next observation per step.  The two HIP graphs (policy-update
-        # parities) alternate in lockstep with c, so each graph always sees the
-        # same pair.
+        # the next observation per step.  A captured graph bakes in the pair it
+        # was captured with, so graphs are keyed by (policy-update parity, c):
+        # with policy_freq 2 and training_steps advanced only here the two
+        # alternate in lockstep and 2 graphs are captured; otherwise (policy_freq
+        # 1/3/4, or train() called in between) up to 4.
         o0 = env.reset()
         self._obs = [o0, torch.empty_like(o0)]
         outs = [env.new_outputs(True), env.new_outputs(True)]
@@ -77,6 +79,7 @@ class VecTrainer:
         self.use_graphs = use_graphs
         self.warmup_eager = warmup_eager
         self.iters = 0
+        self.resets = 0  # episode-round resets done by step()
         self.graphs = {}
         self.dp = agent.sync.active  # tests set it to exercise the 3-graph layout at world 1
         self.last_actions = None
@@ -192,16 +195,19 @@ class VecTrainer:
                     self._mid(update_actor, flat_c, scale)   # the optimisers read the reduced bucket in place
                     if update_actor:
                         flat_a = S.pack(L.grad_params(actor=True))
-                with torch.cuda.graph(g3, pool=pool, stream=s):
-                    self._post(update_actor, flat_a, scale)
+                if update_actor:  # no actor step at this parity: nothing to capture
+                    with torch.cuda.graph(g3, pool=pool, stream=s):
+                        self._post(update_actor, flat_a, scale)
+                else:
+                    g3 = None
                 parts = [g1, g2, g3, flat_c, flat_a]
         torch.cuda.current_stream(self.device).wait_stream(s)
-        self.graphs[update_actor] = parts
+        self.graphs[(update_actor, self._cur)] = parts
         # capture records but does not execute: run the iteration now
         self._replay(update_actor)
 
     def _replay(self, update_actor):
-        parts = self.graphs[update_actor]
+        parts = self.graphs[(update_actor, self._cur)]
         if not self.dp:
             parts[0].replay()
             return
@@ -213,7 +219,7 @@ class VecTrainer:
         S.max_(self.agent.replay_buffer._maxp)  # global max_priority after this step's updates
         if update_actor:
             S.allreduce_flat(flat_a)
-        g3.replay()
+            g3.replay()
 
     # ------------------------------------------------------------- step
     def step(self):
@@ -223,6 +229,7 @@ class VecTrainer:
         if self.k == self.round_len:
             self.env.reset(obs_out=self.obs)
             self.k = 0
+            self.resets += 1
             if self.exploration == "pink":
                 ag.init_episode_noise_device(self.round_len)
         self.active.copy_(self.active_table[self.k])
@@ -233,7 +240,7 @@ class VecTrainer:
         L.prefetch_actor = update_actor  # phase_grads may start the actor forward early
         if not self.use_graphs or self.iters < self.warmup_eager:
             self._eager(update_actor)
-        elif update_actor not in self.graphs:
+        elif (update_actor, self._cur) not in self.graphs:
             self._capture(update_actor)
         else:
             self._replay(update_actor)

@@ -182,6 +182,14 @@ class Critic(nn.Module):
                 sd[prefix + f"w{k}"] = torch.stack([sd.pop(prefix + n + ".weight") for n in names])
                 sd[prefix + f"b{k}"] = torch.stack([sd.pop(prefix + n + ".bias") for n in names])
 
+    @staticmethod
+    def optimizer_layout():
+        """Where each stacked parameter (w0, b0, ..., w3, b3) sits in the
+        reference Critic's parameter order (q01.weight, q01.bias, q1.weight, ...,
+        q3.bias, q02.weight, ..., q6.bias; :109-121): for parameter j, head h is
+        reference parameter h * 8 + j."""
+        return [[(h * 8 + j, h) for h in range(2)] for j in range(8)]
+
     def forward(self, state, action, zsa, zs):
         act = ops.act_code(self.activ)
         if act is not None and state.is_cuda:
@@ -226,9 +234,13 @@ class FlatAdam(torch.optim.Adam):
     multi-tensor kernels.  step(flat_grad=g) takes an already flat (e.g.
     all-reduced) gradient, scaled by grad_scale inside the kernel."""
 
-    def __init__(self, module, lr, weight_decay=0.0, betas=(0.9, 0.999), eps=1e-8):
+    def __init__(self, module, lr, weight_decay=0.0, betas=(0.9, 0.999), eps=1e-8, layout=None):
         self.flat = flatten_params(module)
         params = list(module.parameters())
+        # layout (Critic.optimizer_layout): the reference module's parameters
+        # are slices of ours; state_dict() writes, load_state_dict() reads the
+        # reference's per-parameter layout so optimizer checkpoints interchange
+        self.layout = layout
         super().__init__(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         self.m = torch.zeros_like(self.flat)
         self.v = torch.zeros_like(self.flat)
@@ -247,7 +259,39 @@ class FlatAdam(torch.optim.Adam):
                              "exp_avg_sq": self.v[off:off + n].view_as(p)}
             off += n
 
+    def state_dict(self):
+        sd = super().state_dict()
+        if self.layout is None:
+            return sd
+        n_ref = sum(len(parts) for parts in self.layout)
+        state = {}
+        for j, parts in enumerate(self.layout):
+            st = sd["state"].get(j)
+            if st is None:
+                continue
+            for ref, sl in parts:
+                state[ref] = {"step": st["step"].clone() if torch.is_tensor(st["step"]) else st["step"],
+                              "exp_avg": st["exp_avg"][sl].clone(), "exp_avg_sq": st["exp_avg_sq"][sl].clone()}
+        groups = [dict(g, params=list(range(n_ref))) for g in sd["param_groups"]]
+        return {"state": state, "param_groups": groups}
+
+    def _from_reference_layout(self, sd):
+        n_ref = sum(len(parts) for parts in self.layout)
+        if len(sd["param_groups"][0]["params"]) != n_ref:
+            return sd  # already in this module's own layout
+        state = {}
+        for j, parts in enumerate(self.layout):
+            refs = [sd["state"].get(ref) for ref, _ in parts]
+            if any(r is None for r in refs):
+                continue
+            state[j] = {"step": refs[0]["step"], "exp_avg": torch.stack([r["exp_avg"] for r in refs]),
+                        "exp_avg_sq": torch.stack([r["exp_avg_sq"] for r in refs])}
+        groups = [dict(g, params=list(range(len(self.layout)))) for g in sd["param_groups"]]
+        return {"state": state, "param_groups": groups}
+
     def load_state_dict(self, state_dict):
+        if self.layout is not None:
+            state_dict = self._from_reference_layout(state_dict)
         super().load_state_dict(state_dict)
         off, step = 0, None
         with torch.no_grad():
@@ -394,7 +438,8 @@ class TD7Learner:
         if fused_adam:
             # one flat parameter buffer per net, one td7_adam_step launch per step
             self.actor_optimizer = FlatAdam(self.actor, lr=hp.actor_lr, weight_decay=1e-7)
-            self.critic_optimizer = FlatAdam(self.critic, lr=hp.critic_lr, weight_decay=1e-7)
+            self.critic_optimizer = FlatAdam(self.critic, lr=hp.critic_lr, weight_decay=1e-7,
+                                             layout=Critic.optimizer_layout())
             self.encoder_optimizer = FlatAdam(self.encoder, lr=hp.encoder_lr, weight_decay=1e-7)
         else:
             kw = dict(weight_decay=1e-7)
@@ -790,13 +835,16 @@ class Agent:
                                  normalize_actions=True, prioritized=True)
         self.max_action = max_action
         self.offline = offline
-        # checkpointing (:175-180)
+        self._init_checkpointing()
+        self.noise = None
+
+    def _init_checkpointing(self):
+        """Checkpointing tracked values (:175-180)."""
         self.eps_since_update = 0
         self.timesteps_since_update = 0
         self.max_eps_before_update = 1
         self.min_return = 1e8
         self.best_min_return = -1e8
-        self.noise = None
 
     # the reference exposes the nets and counters on the agent itself
     def __getattr__(self, name):
@@ -806,6 +854,14 @@ class Agent:
         raise AttributeError(name)
 
     # ----------------------------------------------------------- acting
+    # Exploration-noise schedule: every select_action call decrements
+    # exploration_noise once, as both reference variants do
+    # (TD7_multi_agent.py:207, TD7_multi_agent_Pink_noise.py:225) -- the
+    # training script calls it once per env with a 1-D state, the Pink
+    # evaluation once per step with the batch.  select_action_batch stands in
+    # for the training script's per-env calls of one vectorised step, so its
+    # Gaussian branch decrements once per env; its Pink branch is the batched
+    # Pink select_action and decrements once per call.
     def select_action(self, state, timestep=None, first_step=True, use_checkpoint=False, use_exploration=True):
         """Accepts one state (80,) or a batch (N, 80) as numpy; returns numpy."""
         s = np.asarray(state, dtype=np.float32)
@@ -815,32 +871,40 @@ class Agent:
         a = a.cpu().numpy()
         if use_exploration:
             if timestep is not None:
-                # Pink-noise variant (TD7_multi_agent_Pink_noise.py:203-228): one coloured
+                # Pink-noise variant (TD7_multi_agent_Pink_noise.py:218-226): one coloured
                 # noise sequence per episode, scaled by exploration_noise
                 if first_step or self.noise is None:
                     self.init_episode_noise()
                 a = a + self.noise[:, timestep]
-                self.learner.exploration_noise_t -= self.learner.action_noise_decrease  # once per call (:225)
             else:
                 a = a + np.random.randn(*a.shape).astype(np.float32) * self.learner.exploration_noise
-                self.learner.exploration_noise_t -= self.learner.action_noise_decrease * a.shape[0]
+            self.learner.exploration_noise_t -= self.learner.action_noise_decrease
         a = np.clip(a, -1, 1) * self.max_action
         return a[0] if single else a
 
+    # source of the per-episode coloured-noise generator (the reference's
+    # ColoredNoiseProcess creates np.random.default_rng() per episode,
+    # Agent/Pink_noise.py:57 -> colorednoise.py:104); tests inject seeded ones
+    noise_rng_factory = staticmethod(np.random.default_rng)
+
     def init_episode_noise(self):
+        """TD7_multi_agent_Pink_noise.py:203-206: a fresh [action_dim, ep_length]
+        power-law sequence, peak-normalised, times the current exploration noise."""
         from .pink import powerlaw_psd_gaussian
-        buf = powerlaw_psd_gaussian(self.hp.beta, (self.action_dim, self.ep_length)) * self.hp.noise_scale
+        buf = powerlaw_psd_gaussian(self.hp.beta, (self.action_dim, self.ep_length), rng=self.noise_rng_factory())
         self.noise = buf / np.max(np.abs(buf)) * self.learner.exploration_noise
 
     @torch.no_grad()
-    def init_episode_noise_device(self, n_steps=None, generator=None):
+    def init_episode_noise_device(self, n_steps=None, generator=None, spectrum=None):
         """Device Pink-noise sequence for a new episode round (the batched
         TD7_multi_agent_Pink_noise.py:203-207 on the GPU): [action_dim, L],
         peak-normalised and scaled by the current exploration noise; written
-        into a persistent buffer so captured graphs keep reading it."""
+        into a persistent buffer so captured graphs keep reading it.
+        spectrum = (sr, si): given scaled Gaussian spectra instead of device
+        draws (parity tests)."""
         from .pink import powerlaw_psd_gaussian_device
         L = int(n_steps or self.ep_length)
-        buf = powerlaw_psd_gaussian_device(self.hp.beta, self.action_dim, L, self.device, generator) * self.hp.noise_scale
+        buf = powerlaw_psd_gaussian_device(self.hp.beta, self.action_dim, L, self.device, generator, spectrum)
         buf = buf / buf.abs().max() * self.learner.exploration_noise_t
         if getattr(self, "noise_dev", None) is None or self.noise_dev.shape != buf.shape:
             self.noise_dev = torch.empty_like(buf)
@@ -853,11 +917,13 @@ class Agent:
         timestep (int64 device tensor [1]): Pink-noise exploration -- column
         `timestep` of the episode's noise (init_episode_noise_device) is added
         to every env's action, as the reference's batched Pink select_action
-        does (:218-226); otherwise Gaussian noise per env (TD7_multi_agent.py:205-206)."""
+        does (:218-226), and exploration_noise decreases once per call (:225);
+        otherwise Gaussian noise per env (TD7_multi_agent.py:205-207), one
+        decrement per env (the training script's per-env calls)."""
         a = self.learner.act(obs, use_checkpoint)
         if use_exploration and timestep is not None:
             col = self.noise_dev.index_select(1, timestep).t()           # [1, action_dim]
-            self.learner.exploration_noise_t -= self.learner.action_noise_decrease * a.shape[0]
+            self.learner.exploration_noise_t -= self.learner.action_noise_decrease
             return (a + col).clamp(-1, 1) * self.max_action
         if use_exploration:
             L = self.learner

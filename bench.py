@@ -112,6 +112,8 @@ def parse():
     ap.add_argument("--eager", action="store_true", help="no HIP graph capture of the training iteration")
     ap.add_argument("--kernel-timing-steps", type=int, default=100,
                     help="env-only launches timed with HIP events for the roofline line")
+    ap.add_argument("--no-td7-variants", action="store_true",
+                    help="skip the fp32-TD7 and 256-wide-alias sub-lines (configs[1] train mode)")
     a = ap.parse_args()
     if a.envs is None:
         a.envs = {"configs1": 4096, "dr_sweep": 16384, "wide": 65536}[a.workload]
@@ -259,6 +261,39 @@ def critic_gemm_timing(agent, reps=20, replays=10):
     return us, 2.0 * 2 * B * c.w1.shape[1] * c.w1.shape[2]
 
 
+# the reference's update-to-data ratio: per episode round of its 8 envs
+# (Σ(L-3) = 2,257 active env-steps) it trains round(mean(ep_len)) = 283 steps
+# (Simulation/Exoskeleton_agent_train.py:115,145,208 -> TD7_multi_agent.py:315-325)
+REFERENCE_ENV_STEPS_PER_UPDATE = 2257 / 283
+
+
+def td7_variants(env, dev, args, iters=60, warmup=8):
+    """Sub-lines next to the bf16 headline (configs[1]): the same training
+    iteration with exact fp32 TD7 (the reference's precision) and with the
+    256-wide alias of BASELINE configs[1]'s "256-wide MLPs" wording, each on a
+    fresh graph-replayed trainer over the same envs: ms per iteration."""
+    from exo_amd.rollout import VecTrainer
+    from exo_amd.td7 import Agent, Hyperparameters
+    out = {}
+    for name, hp, prec in (("fp32_300_320", Hyperparameters(), "fp32"),
+                           ("bf16_alias256", Hyperparameters(zs_dim=256, enc_hdim=256, critic_hdim=256,
+                                                             actor_hdim=256), "bf16")):
+        torch.manual_seed(1)
+        ag = Agent(80, 7, 1, env_num=8, hp=hp, device=dev, precision=prec, n_envs=env.n, graph_safe=True)
+        tr = VecTrainer(env, ag, use_graphs=True)
+        for _ in range(warmup):
+            tr.step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            tr.step()
+        torch.cuda.synchronize()
+        out[name] = {"ms_per_iteration": (time.perf_counter() - t0) / iters * 1e3, "precision": prec,
+                     "widths": [hp.zs_dim, hp.enc_hdim, hp.critic_hdim, hp.actor_hdim], "iterations": iters}
+        del tr, ag
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -309,6 +344,7 @@ def main():
         k = state["k"]
         if k == round_len:
             state["obs"] = env.reset()
+            state["resets"] = state.get("resets", 0) + 1
             k = 0
         act = torch.rand((N, 7), device=dev) * 2 - 1
         e0 = e1 = None
@@ -335,6 +371,18 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / n
 
+    def reset_timing(n=5):
+        """One episode-round reset (exo_reset_kernel over all envs), HIP events
+        on the launch stream; after the timed loop (the trainer is done)."""
+        env.reset()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(n):
+            env.reset()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / n
+
     def kernel_timing(n):
         """exo_step_kernel alone, HIP events on the launch stream, all envs active."""
         env.reset()
@@ -355,6 +403,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    resets0 = trainer.resets if trainer is not None else state.get("resets", 0)
     t0 = time.perf_counter()
     env_steps = 0
     for _ in range(args.steps):
@@ -364,18 +413,31 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    resets_in_window = (trainer.resets if trainer is not None else state.get("resets", 0)) - resets0
+    reset_ms = reset_timing()
     if ev:  # env mode: the timed launches themselves
         kern_ms, kern_active = float(np.mean([a.elapsed_time(b) for a, b in ev])), env_steps / args.steps
     else:   # train mode: the env kernel is inside graph replays; time it separately afterwards
         kern_ms, kern_active = kernel_timing(min(args.kernel_timing_steps, int(Ls.min()) - 3))
-    t = torch.tensor([elapsed, float(env_steps)], device=dev, dtype=torch.float64)
+    # Whole-round rate, independent of where the K-iteration window falls in
+    # the 344-step episode round: one round = round_len iterations (active
+    # env-steps A_round = sum over k of the envs still running) + one reset.
+    # t_iter = the window's time per iteration with any resets it contained
+    # taken out; value = A_round / (round_len * t_iter + t_reset), summed over
+    # ranks (max of the ranks' times).
+    t = torch.tensor([elapsed, float(env_steps), (elapsed - resets_in_window * reset_ms * 1e-3) / args.steps,
+                      reset_ms * 1e-3], device=dev, dtype=torch.float64)
     if world > 1:
         tmax, tsum = t.clone(), t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
         elapsed, total_env_steps = float(tmax[0]), float(tsum[1])
+        t_iter, t_reset = float(tmax[2]), float(tmax[3])
     else:
         total_env_steps = float(env_steps)
+        t_iter, t_reset = float(t[2]), float(t[3])
+    A_round = float(active_per_k.sum())
+    round_value = world * A_round / (round_len * t_iter + t_reset)
     finite = None
     if agent is not None:
         finite = {n: bool(torch.isfinite(torch.cat([p.detach().reshape(-1) for p in m.parameters()])).all())
@@ -397,7 +459,7 @@ def main():
         traffic, traffic_src = pmc_traffic(float(BYTES_PER_ENV_STEP * active_avg))
         res = {
             "metric": "env steps/sec (batched exo sim) + TD7 grad-steps/sec at 1/2/4/8 MI355X",
-            "value": total_env_steps / elapsed,
+            "value": round_value,
             "unit": "env-steps/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
@@ -410,6 +472,11 @@ def main():
                        "envs_per_gpu": N, "mode": args.mode, "physics": args.physics,
                        "parallelism": f"env-shard x{world}"
                        + (" + TD7 DP all-reduce" if agent and world > 1 else "")},
+            "value_formula": "whole episode rounds: world * A_round / (round_len * t_iter + t_reset); A_round = "
+                             f"{A_round:.0f} active env-steps per {round_len}-iteration round and rank, t_iter = "
+                             f"{t_iter * 1e3:.4f} ms (window time minus {resets_in_window} reset(s), per iteration), "
+                             f"t_reset = {t_reset * 1e3:.4f} ms (exo_reset_kernel, HIP events)",
+            "window_value": total_env_steps / elapsed,
             "env_kernel_env_steps_per_sec": active_avg / (kern_ms * 1e-3),
             "roofline": {"kernel": ("exo_step_rp_kernel" if N <= 16384 else "exo_step_kernel")
                                    + (" + exo_multibody_kernel" if args.physics == "multibody" else ""), "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
@@ -434,7 +501,18 @@ def main():
                                        "bytes_per_env_step": 19 * 8 * 4 + 5 * 8 + 2, "envs_per_launch": N,
                                        "note": "included in ms_per_step; the roofline object above is the step kernel"}
         if agent is not None:
-            res["grad_steps_per_sec"] = args.steps / elapsed
+            gs = args.steps / elapsed  # data-parallel ranks share one update: a grad step is per iteration
+            res["grad_steps_per_sec"] = gs
+            per_update = A_round / round_len
+            ref_ratio = REFERENCE_ENV_STEPS_PER_UPDATE
+            res["update_to_data"] = {
+                "env_steps_per_grad_step": world * per_update,
+                "reference_env_steps_per_grad_step": ref_ratio,
+                "env_steps_per_sec_at_reference_ratio": gs * ref_ratio,
+                "note": "this loop trains one grad step per vectorised env step (the reference script's ratio per "
+                        "vectorised step of its 8 envs, Exoskeleton_agent_train.py:208); at the reference's ratio "
+                        f"per env-step ({ref_ratio:.2f} = 2,257 active env-steps / 283 updates per round) the loop "
+                        "is update bound: grad_steps_per_sec x that ratio"}
             # TD7 on the fp32 MFMA roofline: the update's GEMM flops
             # per grad step over the step time left after the env kernel
             fl = td7_flops(agent, N)
@@ -455,6 +533,8 @@ def main():
                           agent.learner.critic.w1.shape[2]],
                 "achieved": cfl / (us * 1e-6) / 1e12, "peak": peak, "unit": "TFLOP/s",
                 "frac": cfl / (us * 1e-6) / 1e12 / peak, "avg_kernel_us": us}
+        if agent is not None and args.workload == "configs1" and world == 1 and not args.no_td7_variants:
+            res["td7_variants"] = td7_variants(env, dev, args)
         if finite is not None:
             res["weights_finite"] = all(finite.values()) or finite
         if dp_sync is not None:

@@ -28,8 +28,19 @@ numbers it produces are written here):
 * ``td7_small.npz``     - nets + two ``Agent.train()`` steps of
   ``Agent/TD7_multi_agent.py`` at reduced widths, with the sampled batch and
   the target-policy noise injected.
+* ``td7_full.npz``      - three ``Agent.train()`` steps at the bench's shape
+  (300/320 wide, 8 x 128 rows): sampled gradients, parameters, priorities
+  (``python tests/golden/make_golden.py --only td7_full``); ``td7_wide.npz``
+  the same at configs[4]'s 1,024 widths (``--only td7_wide``).
 * ``lap_cases.npz``     - ``Agent/TD7_buffer_multi_agent.LAP.sample`` indices for
   integer-valued priorities and injected uniforms.
+* ``lap_full.npz``      - ``LAP.sample`` at max_size 2.5e5 (18 tree levels),
+  180,000 filled rows, a nonzero leaf at slot == size (``--only lap_full``).
+* ``pink.npz``          - ``Agent/colorednoise.powerlaw_psd_gaussian`` with seeded
+  generators, and the Pink agent's exploring ``select_action`` over two
+  episodes (``--only pink``).
+* ``checkpoint_policy.npz`` - ``maybe_train_and_checkpoint`` decisions over 40
+  recorded episodes, train() stubbed (``--only checkpoint_policy``).
 * ``select_action.npz`` - batched ``select_action`` of
   ``Agent/TD7_multi_agent_Pink_noise.py:209`` with exploration off.
 """
@@ -389,6 +400,82 @@ def make_td7(rng):
     return out
 
 
+def make_td7_full(name="td7_full"):
+    """Three Agent.train() steps of Agent/TD7_multi_agent.py:211-293 at the
+    bench's own shape (zs/enc 300, critic/actor 320, 8 x 128 rows; step 2
+    updates the actor).  The batches come from tests/helpers.td7_full_batch
+    (seeded PCG64, sums stored); LAP.sample / update_priority and
+    torch.randn_like (the target-policy noise) are injected.  Stored per step:
+    the gradients each optimiser step consumed and the updated parameters,
+    sampled at fixed indices (helpers.td7_full_sample_index) with their
+    float64 sums / L2 norms, the priorities, the running Q bounds."""
+    import torch
+    import Agent.TD7_multi_agent as td
+    sys.path.insert(0, os.path.dirname(HERE))
+    from helpers import (TD7_FULL_ENVS, TD7_FULL_LEARNING_STEPS, TD7_FULL_QBOUNDS, TD7_GOLDENS, td7_full_batch,
+                         td7_full_sample_index)
+    HP, STEPS = TD7_GOLDENS[name]
+    torch.manual_seed(0)
+    hp = td.Hyperparameters(buffer_size=16, **HP)
+    agent = td.Agent(80, 7, 1, learning_steps=TD7_FULL_LEARNING_STEPS, hp=hp, env_num=TD7_FULL_ENVS)
+    agent.min_target, agent.max_target = TD7_FULL_QBOUNDS
+    out = {}
+
+    def put(prefix, name, t):
+        v = t.detach().cpu().numpy().astype(np.float32).reshape(-1)
+        idx = td7_full_sample_index(name, v.size)
+        out[f"{prefix}.{name}"] = v[idx]
+        out[f"{prefix}.{name}.sum"] = np.float64(v.astype(np.float64).sum())
+        out[f"{prefix}.{name}.norm"] = np.float64(np.sqrt((v.astype(np.float64) ** 2).sum()))
+
+    def dump(prefix, mod, mname):
+        for k, v in mod.state_dict().items():
+            put(prefix, f"{mname}.{k}", v)
+
+    for name in ["actor", "critic", "encoder"]:
+        dump("init", getattr(agent, name), name)
+    grads = {}
+    for mname in ["actor", "critic", "encoder"]:
+        opt = getattr(agent, mname + "_optimizer")
+        mod = getattr(agent, mname)
+        names = [k for k, _ in mod.named_parameters()]
+        orig = opt.step
+
+        def step(*a, _orig=orig, _mod=mod, _names=names, _m=mname, **k):
+            for n, p in zip(_names, _mod.parameters()):
+                grads[f"{_m}.{n}"] = p.grad.detach().clone()
+            return _orig(*a, **k)
+        opt.step = step
+    prios = []
+    for it in range(STEPS):
+        s, a, s2, r, nd, nz = td7_full_batch(it)
+        out[f"batch{it}_sum"] = np.array([x.astype(np.float64).sum() for x in (s, a, s2, r, nd, nz)])
+        agent.replay_buffer.sample = lambda b=(s, a, s2, r, nd): tuple(torch.tensor(x) for x in b)
+        agent.replay_buffer.update_priority = lambda p: prios.append(p.detach().cpu().numpy().copy())
+        orig = torch.randn_like
+        torch.randn_like = lambda x, nz=nz: torch.tensor(nz)
+        grads.clear()
+        try:
+            agent.train()
+        finally:
+            torch.randn_like = orig
+        for k, g in grads.items():
+            put(f"step{it}_grad", k, g)
+        for name in ["actor", "critic", "encoder"]:
+            dump(f"step{it}", getattr(agent, name), name)
+        out[f"step{it}_updated"] = np.array(sorted({k.split(".")[0] for k in grads}))
+        out[f"priority{it}"] = prios[it].reshape(-1).astype(np.float32)
+        out[f"step{it}_max"] = np.float64(agent.max)
+        out[f"step{it}_min"] = np.float64(agent.min)
+        out[f"step{it}_target_policy_noise"] = np.float64(agent.hp.target_policy_noise)
+    return out
+
+
+def make_td7_wide():
+    """make_td7_full at configs[4]'s widths (every MLP and zs 1,024), 2 steps."""
+    return make_td7_full("td7_wide")
+
+
 def make_lap(rng):
     import torch
     from Agent.TD7_buffer_multi_agent import LAP
@@ -412,6 +499,117 @@ def make_lap(rng):
     return dict(priority=prio, size=np.int32(size), u=us, index=idx)
 
 
+def make_lap_full():
+    """Agent/TD7_buffer_multi_agent.LAP.sample (:65-85) at the bench's depth:
+    max_size 2.5e5 (an 18-level sum tree), 180,000 filled rows per stratum,
+    integer priorities (exact float32 cumsums), batch 128.  Strata 1 and 2 hold
+    a nonzero priority at slot == size, as the reference's single-add pointer
+    quirk leaves them (:59-61): cumsum(priority[:size]) must exclude it."""
+    import torch
+    from Agent.TD7_buffer_multi_agent import LAP
+    E, C, size, batch = 3, int(2.5e5), 180000, 128
+    rng = np.random.Generator(np.random.PCG64(4321))
+    lap = LAP(80, 7, torch.device("cpu"), E, max_size=C, batch_size=batch, max_action=1)
+    lap.size = size
+    prio = rng.integers(0, 6, (E, C)).astype(np.uint8)
+    prio[:, size + 1:] = 0
+    prio[0, size] = 0
+    prio[1:, size] = 5
+    prio[2, :5000] = 0
+    lap.priority = torch.tensor(prio.astype(np.float32))
+    us = rng.uniform(0, 1, (E, batch)).astype(np.float32)
+    us[0, 0] = 0.0
+    it = iter(us)
+    orig = torch.rand
+    torch.rand = lambda size=None, device=None: torch.tensor(next(it))
+    try:
+        lap.sample()
+    finally:
+        torch.rand = orig
+    return dict(priority=prio, size=np.int32(size), u=us, index=np.array(lap.priority_indexes, dtype=np.int64))
+
+
+PINK_CASES = [(1.0, (7, 344), 0.0, 11), (1.0, (7, 229), 0.0, 12), (1.0, (7, 341), 0.0, 13), (2.0, (3, 100), 0.0, 14),
+              (0.5, (7, 64), 0.0, 15), (1.0, (2, 50), 0.1, 16), (1.0, 33, 0.0, 17)]
+
+
+def make_pink():
+    """Agent/colorednoise.powerlaw_psd_gaussian (:9-124) with a seeded
+    np.random.Generator on several shapes / exponents / cut-offs, and the Pink
+    agent's select_action (Agent/TD7_multi_agent_Pink_noise.py:203-228) over
+    two episodes with exploration on: the per-episode noise buffer
+    (ColoredActionNoise, Agent/Pink_noise.py:100-143, its generator seeded by
+    patching np.random.default_rng: seed 77 for episode 0, 78 for episode 1),
+    the actions and hp.exploration_noise after every call."""
+    import torch
+    import Agent.colorednoise as cn
+    import Agent.TD7_multi_agent_Pink_noise as tp
+    out = {}
+    for k, (beta, size, fmin, seed) in enumerate(PINK_CASES):
+        out[f"case{k}"] = cn.powerlaw_psd_gaussian(beta, size, fmin=fmin, rng=np.random.default_rng(seed))
+    torch.manual_seed(2)
+    hp = tp.Hyperparameters(zs_dim=16, enc_hdim=24, critic_hdim=20, actor_hdim=18)
+    L = 60
+    agent = tp.Agent(80, 7, 1, learning_steps=1000, hp=hp, env_num=2, ep_length=L)
+    for name in ["actor", "fixed_encoder"]:
+        for k, v in getattr(agent, name).state_dict().items():
+            out[f"{name}.{k}"] = v.numpy().copy()
+    rng = np.random.default_rng(5)
+    seeds = iter([77, 78])
+    orig = np.random.default_rng
+    plan = [(0, t) for t in range(5)] + [(1, t) for t in range(3)]
+    states = rng.normal(0, 1, (len(plan), 6, 80)).astype(np.float32)
+    acts, expl, noises = [], [], []
+    np.random.default_rng = lambda *a, **k: orig(next(seeds))
+    try:
+        for j, (ep, t) in enumerate(plan):
+            acts.append(agent.select_action(states[j], timestep=t, first_step=(t == 0)))
+            expl.append(agent.hp.exploration_noise)
+            if t == 0:
+                noises.append(np.array(agent.noise))
+    finally:
+        np.random.default_rng = orig
+    out.update(states=states, plan=np.array(plan, dtype=np.int32), actions=np.array(acts), exploration=np.array(expl),
+               noise=np.array(noises), noise_seeds=np.array([77, 78]), ep_length=np.int32(L),
+               learning_steps=np.int64(1000))
+    return out
+
+
+def make_checkpoint_policy():
+    """Agent.maybe_train_and_checkpoint / train_and_reset
+    (Agent/TD7_multi_agent.py:296-325) driven by recorded episode lengths and
+    returns, train() stubbed to its step counter: after every call the
+    checkpointing state, the number of train() calls so far, and which actor /
+    encoder the checkpoint holds (a marker written into a bias before each
+    call).  steps_before_checkpointing = 60 and max_eps_when_checkpointing = 3
+    so the 750k-step switch and reset_weight happen within 40 episodes."""
+    import torch
+    import Agent.TD7_multi_agent as td
+    torch.manual_seed(3)
+    hp = td.Hyperparameters(zs_dim=8, enc_hdim=8, critic_hdim=8, actor_hdim=8, batch_size=4, buffer_size=16,
+                            steps_before_checkpointing=60, max_eps_when_checkpointing=3, reset_weight=0.9)
+    agent = td.Agent(80, 7, 1, learning_steps=1000, hp=hp, env_num=2)
+
+    def stub_train():
+        agent.training_steps += 1
+    agent.train = stub_train
+    rng = np.random.default_rng(8)
+    n = 40
+    ep_len = rng.integers(3, 12, n)
+    ret = np.cumsum(rng.normal(0.3, 1.0, n)) + rng.normal(0, 0.5, n)
+    rows = []
+    for j in range(n):
+        with torch.no_grad():
+            agent.actor.l3.bias[0] = float(j)
+            agent.fixed_encoder.zs1.bias[0] = float(j)
+        agent.maybe_train_and_checkpoint(int(ep_len[j]), float(ret[j]))
+        rows.append([agent.eps_since_update, agent.timesteps_since_update, agent.max_eps_before_update,
+                     agent.min_return, agent.best_min_return, agent.training_steps,
+                     float(agent.checkpoint_actor.l3.bias[0]), float(agent.checkpoint_encoder.zs1.bias[0])])
+    return dict(ep_len=ep_len.astype(np.int64), ret=ret, trace=np.array(rows, dtype=np.float64),
+                hp=np.array([60, 3, 0.9]))
+
+
 def make_select_action(rng):
     import torch
     import Agent.TD7_multi_agent_Pink_noise as tp
@@ -430,6 +628,17 @@ def make_select_action(rng):
 
 
 def main():
+    if "--only" in sys.argv:  # regenerate single fixtures: --only td7_full
+        which = sys.argv[sys.argv.index("--only") + 1].split(",")
+        sys.path.insert(0, REF)
+        cwd = os.getcwd()
+        os.chdir(os.path.join(REF, "Simulation"))
+        try:
+            for w in which:
+                np.savez_compressed(os.path.join(HERE, f"{w}.npz"), **globals()[f"make_{w}"]())
+        finally:
+            os.chdir(cwd)
+        return
     install_stubs()
     sys.path.insert(0, REF)
     cwd = os.getcwd()

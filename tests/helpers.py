@@ -69,3 +69,43 @@ def philox_draws(L, seed, env, episode, lib=None):
     lib = lib or model_host()
     n = 208 + 8 * int(L)
     return np.array([lib.mh_philox_u01(seed, env, episode, p) for p in range(n)])
+
+
+# ----------------------------------------------------------------------------
+# td7_full.npz: the TD7 update at the bench's own shape (configs[1]: zs/enc 300,
+# critic/actor 320, 8 strata x 128 rows).  The batches are regenerated from a
+# seeded PCG64 stream (their float64 sums are stored in the fixture and
+# checked), so the fixture holds only the reference's outputs.
+TD7_FULL_HP = dict(zs_dim=300, enc_hdim=300, critic_hdim=320, actor_hdim=320, batch_size=128)
+TD7_FULL_ENVS = 8
+TD7_FULL_STEPS = 3
+# td7_wide.npz: configs[4]'s wide TD7 (every MLP 1,024 wide, zs 1,024), same batches
+TD7_WIDE_HP = dict(zs_dim=1024, enc_hdim=1024, critic_hdim=1024, actor_hdim=1024, batch_size=128)
+TD7_WIDE_STEPS = 2
+TD7_GOLDENS = {"td7_full": (TD7_FULL_HP, TD7_FULL_STEPS), "td7_wide": (TD7_WIDE_HP, TD7_WIDE_STEPS)}
+TD7_FULL_LEARNING_STEPS = 500000
+TD7_FULL_SAMPLES = 512
+# running Q-target clamp bounds injected before the first step (:243; 0/0 until
+# the first target refresh otherwise, which would hide the clamp)
+TD7_FULL_QBOUNDS = (-1.5, 2.0)
+
+
+def td7_full_batch(step):
+    """(state, action, next_state, reward, not_done, noise) of golden step `step` (float32 numpy)."""
+    B = TD7_FULL_ENVS * TD7_FULL_HP["batch_size"]
+    rng = np.random.Generator(np.random.PCG64(9000 + step))
+    s = rng.normal(0, 1, (B, 80)).astype(np.float32)
+    a = rng.uniform(-1, 1, (B, 7)).astype(np.float32)
+    s2 = (s + 0.1 * rng.normal(0, 1, (B, 80))).astype(np.float32)
+    r = rng.uniform(-2, 3, (B, 1)).astype(np.float32)
+    nd = (rng.uniform(0, 1, (B, 1)) > 0.02).astype(np.float32)
+    nz = rng.normal(0, 1, (B, 7)).astype(np.float32)
+    return s, a, s2, r, nd, nz
+
+
+def td7_full_sample_index(name, numel):
+    """Fixed flat indices at which a parameter / gradient tensor is sampled."""
+    if numel <= TD7_FULL_SAMPLES:
+        return np.arange(numel, dtype=np.int64)
+    seed = sum(ord(c) * (i + 1) for i, c in enumerate(name))
+    return np.sort(np.random.Generator(np.random.PCG64(seed)).choice(numel, TD7_FULL_SAMPLES, replace=False))

@@ -126,3 +126,54 @@ def test_sample_gathers_the_rows_of_its_indices():
     assert int(idx.max()) < 64 and set(torch.unique(nd).tolist()) <= {0.0, 1.0}
     sizes = lap.size_s.cpu().numpy()
     assert all(int(idx[k].max()) < sizes[k] for k in range(4))
+
+
+def test_sample_matches_reference_at_full_depth():
+    """tests/golden/lap_full.npz: the reference's LAP.sample at max_size 2.5e5
+    (all 18 tree levels active, 180,000 filled rows) with a nonzero leaf at
+    slot == size in strata 1-2 (the single-add pointer quirk, :59-61): the
+    descent is scaled by the prefix total over [0, size), so the indices match
+    searchsorted_left(cumsum(priority[:size]), u * total) exactly."""
+    g = np.load(f"{GOLDEN}/lap_full.npz", allow_pickle=False)
+    prio, size, u, ref = g["priority"].astype(np.float32), int(g["size"]), g["u"], g["index"]
+    E, C = prio.shape
+    lap = _lap(E, C, u.shape[1])
+    assert lap._cap == 1 << 18
+    _set_priorities(lap, prio)
+    lap.size_s.fill_(size)
+    np.testing.assert_array_equal(lap.totals.cpu().numpy(), prio.sum(1))  # root includes slot == size
+    idx = lap.sample_indices(torch.as_tensor(u)).cpu().numpy()
+    np.testing.assert_array_equal(idx, ref)
+    assert idx.max() < size
+    # the fused sample + gather kernel descends identically: tag every stored
+    # row with its slot and check the gathered rows
+    slots = torch.arange(C + 1, device="cuda", dtype=torch.float32)
+    lap.reward[:, :, 0] = slots
+    lap.state[:, :, 0] = slots
+    lap.next_state[:, :, 1] = -slots
+    lap.device_rng = False
+    lap._u.copy_(torch.as_tensor(u))
+    lap._u.uniform_ = lambda: lap._u  # keep the injected uniforms
+    s, a, s2, r, nd = lap.sample()
+    got = lap.ind.cpu().numpy()
+    np.testing.assert_array_equal(got, ref)
+    np.testing.assert_array_equal(r.cpu().numpy().reshape(E, -1), ref.astype(np.float32))
+    np.testing.assert_array_equal(s[:, 0].cpu().numpy().reshape(E, -1), ref.astype(np.float32))
+    np.testing.assert_array_equal(s2[:, 1].cpu().numpy().reshape(E, -1), -ref.astype(np.float32))
+
+
+def test_sample_never_returns_the_slot_at_size():
+    """Single-add pointer quirk: the newest transition of strata 1.. sits at
+    slot == size and carries max_priority; the reference never samples it
+    until size grows past it."""
+    lap = _lap(3, 64, 256)
+    for step in range(5):
+        for e in range(3):
+            lap.add(np.zeros(80), np.zeros(7), np.zeros(80), 0.0, False, tremor_num=e)
+    assert lap.size == 5
+    p = lap.priority.cpu().numpy()
+    assert p[1, 5] == 1.0 and p[2, 5] == 1.0 and p[0, 5] == 0.0  # written past size
+    idx = lap.sample_indices(torch.rand(3, 256, device="cuda")).cpu().numpy()
+    assert idx.max() <= 4
+    # with uniform priorities every slot < size is drawn
+    assert all(len(np.unique(idx[s])) == 5 for s in range(3))

@@ -6,12 +6,13 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _make(use_graphs, seed=0):
+def _make(use_graphs, seed=0, policy_freq=2):
     from exo_amd import VecExoskeletonEnv
     from exo_amd.rollout import VecTrainer
     from exo_amd.td7 import Agent, Hyperparameters
     torch.manual_seed(seed)
-    hp = Hyperparameters(zs_dim=32, enc_hdim=32, critic_hdim=32, actor_hdim=32, batch_size=16, target_update_rate=5)
+    hp = Hyperparameters(zs_dim=32, enc_hdim=32, critic_hdim=32, actor_hdim=32, batch_size=16, target_update_rate=5,
+                         policy_freq=policy_freq)
     env = VecExoskeletonEnv(64, seed=seed)
     agent = Agent(80, 7, 1, hp=hp, env_num=8, buffer_size=4096, graph_safe=use_graphs)
     return VecTrainer(env, agent, use_graphs=use_graphs), env, agent
@@ -23,7 +24,7 @@ def test_graph_replay_matches_eager_bookkeeping():
     for _ in range(12):
         assert te.step() == tg.step()
     torch.cuda.synchronize()
-    assert len(tg.graphs) == 2  # one graph per policy-update parity
+    assert len(tg.graphs) == 2  # policy_freq 2: parity and observation buffer alternate in lockstep
     np.testing.assert_array_equal(ag_e.replay_buffer.size_s.cpu().numpy(), ag_g.replay_buffer.size_s.cpu().numpy())
     np.testing.assert_array_equal(ag_e.replay_buffer.ptr_s.cpu().numpy(), ag_g.replay_buffer.ptr_s.cpu().numpy())
     assert ag_g.learner.training_steps == 12
@@ -61,6 +62,22 @@ def test_graph_replay_matches_eager_numerics(layout):
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
     import graph_vs_eager
     assert graph_vs_eager.run(layout, iters=10) <= 1e-5
+
+
+def test_graph_replay_matches_eager_with_policy_freq_3():
+    """policy_freq 3: the policy-update parity no longer flips with the
+    observation buffer, so graphs are keyed by (parity, buffer) -- 4 captures
+    -- and every replay reads the observation buffer of its own iteration
+    (keyed by parity alone a replay read a stale buffer)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import graph_vs_eager
+    assert graph_vs_eager.run("single", iters=12, policy_freq=3) <= 1e-5
+    tg, _, _ = _make(True, policy_freq=3)
+    for _ in range(12):
+        tg.step()
+    assert sorted(tg.graphs) == [(False, 0), (False, 1), (True, 0), (True, 1)]
 
 
 def test_pink_exploration_trainer_runs_in_graphs():

@@ -233,3 +233,47 @@ def test_reduced_precision_train_steps_track_fp32(precision):
             for k, v in getattr(L2, name).state_dict().items():
                 np.testing.assert_allclose(v.cpu().numpy(), ref[k].numpy(), rtol=0, atol=1e-3,
                                            err_msg=f"step {step} {name}.{k}")
+
+
+def test_critic_optimizer_state_interchanges_with_reference_layout():
+    """The critic's FlatAdam state_dict uses the reference Critic's 16
+    per-head parameters (q01 ... q3, q02 ... q6, Agent/TD7_multi_agent.py:109-121),
+    so a reference-saved _critic_optimizer loads here and ours loads into the
+    reference's torch.optim.Adam (the stacked heads had 8)."""
+    import torch.nn as nn
+    from exo_amd.td7 import Critic, FlatAdam
+
+    class RefCritic(nn.Module):  # the reference's parameter layout (names and order)
+        def __init__(self, s, a, zs, h):
+            super().__init__()
+            self.q01, self.q1, self.q2, self.q3 = (nn.Linear(s + a, h), nn.Linear(2 * zs + h, h), nn.Linear(h, h),
+                                                   nn.Linear(h, 1))
+            self.q02, self.q4, self.q5, self.q6 = (nn.Linear(s + a, h), nn.Linear(2 * zs + h, h), nn.Linear(h, h),
+                                                   nn.Linear(h, 1))
+
+    torch.manual_seed(0)
+    c = Critic(80, 7, 16, 20)
+    ref = RefCritic(80, 7, 16, 20)
+    ref.load_state_dict(c.state_dict())
+    opt_ref = torch.optim.Adam(ref.parameters(), lr=3e-4, weight_decay=1e-7)
+    for _ in range(3):
+        opt_ref.zero_grad()
+        sum((p * torch.randn_like(p)).sum() for p in ref.parameters()).backward()
+        opt_ref.step()
+    ours = FlatAdam(c, lr=3e-4, weight_decay=1e-7, layout=Critic.optimizer_layout())
+    ours.load_state_dict(opt_ref.state_dict())
+    ref_params = list(ref.parameters())
+    ref_state = opt_ref.state_dict()["state"]
+    for j, p in enumerate(c.parameters()):
+        for ref_i, h in Critic.optimizer_layout()[j]:
+            assert ref_params[ref_i].shape == p[h].shape
+            torch.testing.assert_close(ours.state[p]["exp_avg"][h], ref_state[ref_i]["exp_avg"], rtol=0, atol=0)
+            torch.testing.assert_close(ours.state[p]["exp_avg_sq"][h], ref_state[ref_i]["exp_avg_sq"], rtol=0, atol=0)
+    assert float(ours._step) == 3.0
+    # and back: our state_dict loads into the reference's Adam unchanged
+    sd = ours.state_dict()
+    assert sorted(sd["state"]) == list(range(16)) and sd["param_groups"][0]["params"] == list(range(16))
+    opt_ref2 = torch.optim.Adam(RefCritic(80, 7, 16, 20).parameters(), lr=3e-4, weight_decay=1e-7)
+    opt_ref2.load_state_dict(sd)
+    for i in range(16):
+        torch.testing.assert_close(opt_ref2.state_dict()["state"][i]["exp_avg"], ref_state[i]["exp_avg"])

@@ -243,11 +243,18 @@ _GRAD = {0: lambda y: torch.ones_like(y), 1: lambda y: (y > 0).to(y.dtype), 2: l
 @pytest.mark.parametrize("m,n,k,g,shared", [(1024, 300, 80, 0, False), (1000, 300, 307, 0, False),
                                             (4096, 300, 300, 0, False), (37, 7, 87, 0, False),
                                             (1024, 320, 920, 2, False), (1024, 320, 87, 2, True),
-                                            (1024, 1, 320, 2, False)])
+                                            (1024, 1, 320, 2, False),
+                                            # configs[4] (wide TD7, 1,024 x 4): hidden layers, the critic's
+                                            # [q|zsa|zs] layer, the shared first layer, 8 x 1,024 rows
+                                            (1024, 1024, 1024, 0, False), (1024, 1024, 3072, 2, False),
+                                            (1024, 1024, 87, 2, True), (8192, 1024, 1024, 0, False),
+                                            (8192, 1024, 3072, 2, False)])
 def test_dense_reduced_precision_is_the_gemm_of_rounded_operands(prec, act, m, n, k, g, shared):
     """bf16 / fp16 operand mode: each GEMM equals the fp64 GEMM of the
     operands rounded to nearest even (dP = dY * act'(Y) rounded as loaded);
-    the bias gradient is the fp32 column sum of the unrounded dP."""
+    the bias gradient is the fp32 column sum of the unrounded dP.  Covers the
+    TD7 default widths and the wide configuration (forward, bwd-data and
+    wgrad at 1,024 / 3,072)."""
     from exo_amd import ops
     torch.manual_seed(m + n + k + act)
     rd = lambda t: t.to(_ROUND[prec]).double()  # noqa: E731
@@ -377,32 +384,34 @@ def test_lds_forward_kernel_is_the_gemm_of_rounded_operands(prec, g, m, n, k, ca
     torch.testing.assert_close(y, ref.reshape(y.shape), rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.parametrize("prec", ["bf16", "fp16"])
-@pytest.mark.parametrize("case", ["plain", "cat", "shared"])
-def test_large_weight_gradient_as_lds_gemm(prec, case, monkeypatch):
-    """Weight and bias gradients of the wide layers through the LDS-tiled GEMM on
-    transposed operands (ops._wgrad_lds) == the output-contiguous wgrad kernel."""
+@pytest.mark.parametrize("m", [1024, 8192])
+def test_wide_critic_concat_layer_fp16(m):
+    """configs[4]'s critic layer 1 as the model runs it: [q | zsa | zs] read in
+    place (q per head [2,M,1024], zsa and zs shared), W [2, 1024, 3072], fp16
+    operands: forward, every part's gradient and dW / db against the fp64 GEMM
+    of the rounded operands."""
     from exo_amd import ops
-    torch.manual_seed(len(case))
-    M, N = 1024, 1024
-    if case == "plain":
-        parts, w = [torch.randn(M, 1024, device="cuda")], torch.randn(N, 1024, device="cuda") / 32
-        b = torch.randn(N, device="cuda")
-    elif case == "cat":      # the wide critic's [q | zsa | zs]
-        parts = [torch.randn(2, M, 1024, device="cuda"), torch.randn(M, 1024, device="cuda"),
-                 torch.randn(M, 1024, device="cuda")]
-        w, b = torch.randn(2, N, 3072, device="cuda") / 55, torch.randn(2, N, device="cuda")
-    else:                    # one input shared by the two heads
-        parts, w = [torch.randn(M, 1024, device="cuda")], torch.randn(2, N, 1024, device="cuda") / 32
-        b = torch.randn(2, N, device="cuda")
-    outs = []
-    for on in (True, False):
-        monkeypatch.setattr(ops, "_WGRAD_GEMM", on)
-        ww, bb = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
-        with ops.matrix_precision(prec):
-            y = ops.dense_cat(parts, ww, bb, 2) if len(parts) > 1 else ops.dense(parts[0], ww, bb, 2)
-        torch.manual_seed(3)
-        y.backward(torch.randn_like(y))
-        outs.append((ww.grad, bb.grad))
-    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=2e-3, atol=2e-3)
-    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-4, atol=1e-3)
+    torch.manual_seed(m)
+    rd = lambda t: t.to(torch.float16).double()  # noqa: E731
+    q = torch.randn(2, m, 1024, device="cuda")
+    zsa, zs = torch.randn(m, 1024, device="cuda"), torch.randn(m, 1024, device="cuda")
+    w = torch.randn(2, 1024, 3072, device="cuda") / 3072 ** 0.5
+    b = torch.randn(2, 1024, device="cuda")
+    parts = [t.clone().requires_grad_(True) for t in (q, zsa, zs)]
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    with ops.matrix_precision("fp16"):
+        y = ops.dense_cat(parts, wr, br, 2)
+    x = torch.cat([rd(q), rd(zsa).unsqueeze(0).expand(2, m, 1024), rd(zs).unsqueeze(0).expand(2, m, 1024)], -1)
+    ref = torch.nn.functional.elu(x @ rd(w).transpose(-1, -2) + b.double().unsqueeze(-2))
+    torch.testing.assert_close(y.double(), ref, rtol=1e-5, atol=1e-5)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    dp32 = dy * _GRAD[2](y.detach())
+    dp = rd(dp32)
+    dx = dp @ rd(w)                                       # [2, M, 3072]
+    want = {"q": dx[..., :1024], "zsa": dx[..., 1024:2048].sum(0), "zs": dx[..., 2048:].sum(0),
+            "dW": dp.transpose(-1, -2) @ x, "db": dp32.double().sum(-2)}
+    got = {"q": parts[0].grad, "zsa": parts[1].grad, "zs": parts[2].grad, "dW": wr.grad, "db": br.grad}
+    for name, r in want.items():
+        scale = max(1.0, float(r.abs().max()))
+        torch.testing.assert_close(got[name].double(), r, rtol=2e-3, atol=2e-3 * scale, msg=name)

@@ -65,7 +65,7 @@ def trainer_graph_check(iters=12):
     bad = 0
     for it in range(iters):
         par = it % 2 == 0
-        g1, g2, g3, flat_c, flat_a = tr.graphs[par]
+        g1, g2, g3, flat_c, flat_a = next(v for k, v in tr.graphs.items() if k[0] == par)
         host = torch.empty(flat_c.numel(), pin_memory=True)
         g1.replay()
         ev = torch.cuda.Event()

@@ -30,8 +30,12 @@ def _make_full(use_graphs, seed=0):
     return VecTrainer(env, agent, use_graphs=use_graphs), env, agent
 
 
-def run(layout, iters=10, full=False, seed=7, quiet=False):
-    mk = _make_full if full else _make
+def run(layout, iters=10, full=False, seed=7, quiet=False, policy_freq=2):
+    if full:
+        mk = _make_full
+    else:
+        def mk(use_graphs, seed):
+            return _make(use_graphs, seed=seed, policy_freq=policy_freq)
     # one trainer at a time: both draw from the global torch RNG
     ref = []
     if os.environ.get("GVE_SKIP_EAGER") != "1":

@@ -31,7 +31,7 @@ def main(K=200):
     t2 = time.perf_counter()
     print(f"host issue {1e3 * (t1 - t0) / K:.3f} ms/iter, wall {1e3 * (t2 - t0) / K:.3f} ms/iter")
     # the two parities' graphs alternately, nothing else
-    gs = [tr.graphs[False][0], tr.graphs[True][0]]
+    gs = [tr.graphs[k][0] for k in sorted(tr.graphs)]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(K):
@@ -52,7 +52,7 @@ def main(K=200):
     torch.cuda.synchronize()
     print(f"active copy {1e3 * (t1 - t0) / K:.3f} ms, maybe_update_targets {1e3 * (t2 - t1) / K:.3f} ms")
     # replay alone (no per-step host work besides the launch)
-    g = tr.graphs[False][0]
+    g = next(v for k, v in tr.graphs.items() if not k[0])[0]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(K):
