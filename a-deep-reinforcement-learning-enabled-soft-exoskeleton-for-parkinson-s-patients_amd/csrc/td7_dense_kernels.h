@@ -35,6 +35,16 @@ enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_ELU = 2, ACT_TANH = 3 };
 // fp32 accumulate; memory, epilogues and bias gradients stay fp32.
 enum Prec : int { PREC_F32 = 0, PREC_BF16 = 1, PREC_F16 = 2 };
 
+// fp16 operands of the backward: the gradient operand dP = dY act'(Y) is
+// multiplied by 2^10 before it is rounded and the fp32 accumulators by 2^-10
+// after (exact: a power of two).  The TD7 gradients are small -- the wide
+// encoder's d mse / d pred is 2 (pred - target) / (B zs_dim) ~ 1e-6, the
+// critic's dloss/dQ <= 1/B -- and below fp16's 6.1e-5 they would be rounded as
+// subnormals (1e-6: ~6 % quantum); scaled, they stay normal down to 6e-8 and
+// keep 11 bits, with overflow only above 64.  bf16 has fp32's exponent range.
+template <int P>
+__device__ __forceinline__ constexpr float grad_scale() { return P == PREC_F16 ? 1024.f : 1.f; }
+
 template <int P>
 __device__ __forceinline__ floatx4 mfma_k16(const float (&a)[4], const float (&b)[4], floatx4 c) {
     if constexpr (P == PREC_F16) {
@@ -230,6 +240,12 @@ __global__ __launch_bounds__(64 * NW) void dense_gemm_kernel(GemmArgs a) {
     for (int x = 0; x < 2; ++x)
 #pragma unroll
         for (int y = 0; y < 2; ++y) acc[x][y] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // bwd-weight with 16-bit operands: the bias gradient (the ones column) is
+    // summed from the UNROUNDED dP in fp32 here, as the wgrad kernel does, not
+    // taken from the rounded MFMA column; bsum[tl] = this lane's part of row
+    // i0 + 16 tl + c
+    const bool bias_tile = P != PREC_F32 && a.B.ones_col >= j0 && a.B.ones_col < j0 + 32;
+    float bsum[2] = {0.f, 0.f};
 
     auto load = [&](int grp, Frag &fa, Frag &fy, Frag &fb) {
 #pragma unroll
@@ -262,8 +278,11 @@ __global__ __launch_bounds__(64 * NW) void dense_gemm_kernel(GemmArgs a) {
 #pragma unroll
                 for (int tl = 0; tl < 2; ++tl)
 #pragma unroll
-                    for (int jj = 0; jj < 4; ++jj)
-                        av[tl][jj] = AG >= 0 ? fa.v[sp][tl][jj] * act_grad_t<AG>(fy.v[sp][tl][jj]) : fa.v[sp][tl][jj];
+                    for (int jj = 0; jj < 4; ++jj) {
+                        const float dp = AG >= 0 ? fa.v[sp][tl][jj] * act_grad_t<AG>(fy.v[sp][tl][jj]) : fa.v[sp][tl][jj];
+                        if (bias_tile) bsum[tl] += dp;
+                        av[tl][jj] = AG >= 0 ? dp * grad_scale<P>() : dp;
+                    }
 #pragma unroll
                 for (int x = 0; x < 2; ++x)
 #pragma unroll
@@ -295,27 +314,48 @@ __global__ __launch_bounds__(64 * NW) void dense_gemm_kernel(GemmArgs a) {
         if (grp + 2 < ngrp) load(grp + 2, a0, y0, b0);
         mma(a1, y1, b1);
     }
+    if (bias_tile)
+#pragma unroll
+        for (int tl = 0; tl < 2; ++tl) {
+            bsum[tl] += __shfl_xor(bsum[tl], 16);
+            bsum[tl] += __shfl_xor(bsum[tl], 32);
+        }
     // sum the NW partial tiles: waves 1.. park theirs in LDS, wave 0 adds them
-    // acc[x][y][k] is C[i0 + 16x + 4q + k][j0 + 16y + c]
+    // acc[x][y][k] is C[i0 + 16x + 4q + k][j0 + 16y + c]; the bias partials go
+    // to the padding column 32
     if (NW > 1) {
-        if (w > 0)
+        if (w > 0) {
 #pragma unroll
             for (int x = 0; x < 2; ++x)
 #pragma unroll
                 for (int y = 0; y < 2; ++y)
 #pragma unroll
                     for (int k = 0; k < 4; ++k) red[w - 1][16 * x + 4 * q + k][16 * y + c] = acc[x][y][k];
+            if (bias_tile && q == 0)
+#pragma unroll
+                for (int tl = 0; tl < 2; ++tl) red[w - 1][16 * tl + c][32] = bsum[tl];
+        }
         __syncthreads();
         if (w > 0) return;
 #pragma unroll
-        for (int ww = 0; ww < NW - 1; ++ww)
+        for (int ww = 0; ww < NW - 1; ++ww) {
 #pragma unroll
             for (int x = 0; x < 2; ++x)
 #pragma unroll
                 for (int y = 0; y < 2; ++y)
 #pragma unroll
                     for (int k = 0; k < 4; ++k) acc[x][y][k] += red[ww][16 * x + 4 * q + k][16 * y + c];
+            if (bias_tile)
+#pragma unroll
+                for (int tl = 0; tl < 2; ++tl) bsum[tl] += red[ww][16 * tl + c][32];
+        }
     }
+    // the bias of row i0 + 16x + 4q + k sits in lane c = 4q + k
+    float bias_row[2][4];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) bias_row[x][k] = bias_tile ? __shfl(bsum[x], 4 * q + k) : 0.f;
 #pragma unroll
     for (int y = 0; y < 2; ++y) {
         const int col = j0 + 16 * y + c;
@@ -328,7 +368,8 @@ __global__ __launch_bounds__(64 * NW) void dense_gemm_kernel(GemmArgs a) {
             for (int k = 0; k < 4; ++k) {
                 const int row = i0 + 16 * x + 4 * q + k;
                 if (row >= a.I) continue;
-                const float v = acc[x][y][k];
+                const float v = (is_bias && bias_tile) ? bias_row[x][k]
+                                : AG >= 0 ? acc[x][y][k] * (1.f / grad_scale<P>()) : acc[x][y][k];
                 if (is_bias) a.bias_grad[g * a.bgsg + row] = v;
                 else a.C[g * a.csg + (long)row * a.csi + (long)col * a.csj] = act_fwd_t<EP>(v + bias_v);
             }
@@ -1018,7 +1059,7 @@ __global__ __launch_bounds__(64 * NW) void dense_wgrad_kernel(WgradArgs a) {
                         float v = shifted<VA>(f.a[s4 + e], shi, s);
                         if (AG > 0) v *= act_grad_t<AG>(shifted<VA>(f.y[s4 + e], shi, s));
                         bsum[s] += v;
-                        fa[s][e] = v;
+                        fa[s][e] = v * grad_scale<P>();
                     }
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
@@ -1100,7 +1141,7 @@ __global__ __launch_bounds__(64 * NW) void dense_wgrad_kernel(WgradArgs a) {
             float *row = dwg + (long)i * a.J;
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-                if (ja + u < a.J) row[ja + u] = acc[s][u][k];
+                if (ja + u < a.J) row[ja + u] = acc[s][u][k] * (1.f / grad_scale<P>());
         }
     if (a.db && tile.x == 0) {
 #pragma unroll

@@ -359,6 +359,7 @@ def pair_rows(a, b):
     state / next_state, exo_amd/replay.py); else the stack."""
     if (a.dim() == 2 and a.shape == b.shape and a.dtype == b.dtype and a.device == b.device and a.is_contiguous()
             and b.is_contiguous() and b.data_ptr() == a.data_ptr() + a.numel() * a.element_size()
+            and a.untyped_storage().data_ptr() == b.untyped_storage().data_ptr()  # adjacent in ONE allocation
             and not (a.requires_grad or b.requires_grad)):
         return a.as_strided((2, *a.shape), (a.numel(), *a.stride()))
     return torch.stack([a, b])

@@ -234,6 +234,14 @@ def test_critic_actor_update_gradients_with_partial_inputs():
 
 # ------------------------------------------------------------ bf16 / fp16 MFMA
 _ROUND = {"bf16": torch.bfloat16, "fp16": torch.float16}
+# the backward's gradient operand dP is rounded after scaling by 2^10 in fp16
+# (csrc/td7_dense_kernels.h grad_scale: keeps small gradients out of fp16's
+# subnormal range); exact power of two, so this is the rounding model
+_GSCALE = {"bf16": 1.0, "fp16": 1024.0}
+
+
+def _rd_grad(t, prec):
+    return (t * _GSCALE[prec]).to(_ROUND[prec]).double() / _GSCALE[prec]
 _GRAD = {0: lambda y: torch.ones_like(y), 1: lambda y: (y > 0).to(y.dtype), 2: lambda y: torch.where(y > 0, 1.0, y + 1),
          3: lambda y: 1 - y * y}
 
@@ -271,15 +279,19 @@ def test_dense_reduced_precision_is_the_gemm_of_rounded_operands(prec, act, m, n
     dy = torch.randn_like(y)
     y.backward(dy)
     dp32 = dy * _GRAD[act](y.detach())
-    dp = rd(dp32)
+    dp = _rd_grad(dp32, prec)
     dx = dp @ rd(w)
     if g and shared:
         dx = dx.sum(0)
     dw = dp.transpose(-1, -2) @ xx
     db = dp32.double().sum(-2)
-    for got, r, name in ((xr.grad, dx, "dx"), (wr.grad, dw, "dW"), (br.grad, db, "db")):
+    # tanh: the kernel forms 1 - y*y with one fused multiply-add, torch with two
+    # roundings; near |y| = 1 that ulp-level difference flips the rounding of
+    # some dP elements to 16 bits
+    tg = 1e-3 if act == 3 else 1e-4
+    for got, r, name, tol in ((xr.grad, dx, "dx", tg), (wr.grad, dw, "dW", tg), (br.grad, db, "db", 1e-5)):
         scale = max(1.0, float(r.abs().max()))
-        torch.testing.assert_close(got.double(), r, rtol=2e-3, atol=2e-3 * scale, msg=name)
+        torch.testing.assert_close(got.double(), r, rtol=tol, atol=tol * scale, msg=name)
 
 
 def test_reduced_precision_rejects_bad_codes():
@@ -407,11 +419,12 @@ def test_wide_critic_concat_layer_fp16(m):
     dy = torch.randn_like(y)
     y.backward(dy)
     dp32 = dy * _GRAD[2](y.detach())
-    dp = rd(dp32)
+    dp = _rd_grad(dp32, "fp16")
     dx = dp @ rd(w)                                       # [2, M, 3072]
     want = {"q": dx[..., :1024], "zsa": dx[..., 1024:2048].sum(0), "zs": dx[..., 2048:].sum(0),
             "dW": dp.transpose(-1, -2) @ x, "db": dp32.double().sum(-2)}
     got = {"q": parts[0].grad, "zsa": parts[1].grad, "zs": parts[2].grad, "dW": wr.grad, "db": br.grad}
     for name, r in want.items():
         scale = max(1.0, float(r.abs().max()))
-        torch.testing.assert_close(got[name].double(), r, rtol=2e-3, atol=2e-3 * scale, msg=name)
+        tol = 1e-5 if name == "db" else 1e-4
+        torch.testing.assert_close(got[name].double(), r, rtol=tol, atol=tol * scale, msg=name)

@@ -78,7 +78,8 @@ def trainer_graph_check(iters=12):
         ref = flat_c.cpu()
         bad += int(not torch.equal(host, ref))
         g2.replay()
-        g3.replay()
+        if g3 is not None:  # captured only at the actor-update parity
+            g3.replay()
         torch.cuda.synchronize()
     print(f"trainer 'pre' graph: stale/racy bucket reads {bad}/{iters}")
     return bad
