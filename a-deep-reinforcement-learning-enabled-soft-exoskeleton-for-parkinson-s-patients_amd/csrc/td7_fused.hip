@@ -1,0 +1,399 @@
+// td7_fused.hip -- row-tile-fused TD7 networks (see td7_fused.h): weight
+// packing and the forward passes of the TD7 update and of select_action.
+//
+//   td7f_select : Agent.select_action over the vectorised envs (Agent/TD7_multi_agent.py:192-209,
+//                 batched; the fixed encoder's zs, the actor, Gaussian exploration noise)
+//   td7f_target : the critic target chain (:233-241) -- kernel A: fixed_target_zs(s'),
+//                 actor_target + clipped noise, fixed_target_zsa; kernel B: both heads of
+//                 critic_target, one workgroup per (16 rows, head)
+//   td7f_fixed  : fixed_zs / fixed_zsa of the critic update (:248-249)
+//
+// Every Linear is the gemm of td7_fused.h (16-bit operands from LDS x packed
+// weights streamed from L2, fp32 accumulate) with its bias/activation/norm
+// fused; one launch per network pass instead of one (or more) per layer.
+#include "td7_fused.h"
+
+#include <algorithm>
+
+#include "philox.h"
+
+namespace td7f {
+
+// ---------------------------------------------------------------- packing
+struct PackJob {
+    const float *w;
+    long ld;
+    int N, K;
+    u32x4 *wf, *wb;
+    int ksf, ntf, ksb, ntb;
+};
+struct PackArgs {
+    int njobs;
+    long start[TD7F_MAX_PACK + 1];  // prefix sums of the jobs' 16-byte items
+    PackJob j[TD7F_MAX_PACK];
+};
+
+template <int P>
+__global__ __launch_bounds__(256) void pack_kernel(PackArgs a) {
+    const long total = a.start[a.njobs];
+    for (long it = (long)blockIdx.x * 256 + threadIdx.x; it < total; it += (long)gridDim.x * 256) {
+        int q = 0;
+        while (it >= a.start[q + 1]) ++q;
+        const PackJob &J = a.j[q];
+        long k = it - a.start[q];
+        const long nf = (long)J.ntf * J.ksf * 64;
+        const int l = (int)(k & 63);
+        uint32_t v[4];
+        if (k < nf) {  // forward: W[16t + (l&15)][32s + 8(l>>4) + j]
+            const long blk = k >> 6;
+            const int t = (int)(blk / J.ksf), s = (int)(blk % J.ksf);
+            const int n = 16 * t + (l & 15), k0 = 32 * s + 8 * (l >> 4);
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                const int c = k0 + 2 * jj;
+                const float x0 = (n < J.N && c < J.K) ? J.w[(long)n * J.ld + c] : 0.f;
+                const float x1 = (n < J.N && c + 1 < J.K) ? J.w[(long)n * J.ld + c + 1] : 0.f;
+                v[jj] = (uint32_t)Ty<P>::bits(x0) | ((uint32_t)Ty<P>::bits(x1) << 16);
+            }
+            J.wf[k] = u32x4{v[0], v[1], v[2], v[3]};
+        } else {  // dX: W[32s + 8(l>>4) + j][16t + (l&15)]
+            k -= nf;
+            const long blk = k >> 6;
+            const int t = (int)(blk / J.ksb), s = (int)(blk % J.ksb);
+            const int c = 16 * t + (l & 15), n0 = 32 * s + 8 * (l >> 4);
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                const int n = n0 + 2 * jj;
+                const float x0 = (n < J.N && c < J.K) ? J.w[(long)n * J.ld + c] : 0.f;
+                const float x1 = (n + 1 < J.N && c < J.K) ? J.w[(long)(n + 1) * J.ld + c] : 0.f;
+                v[jj] = (uint32_t)Ty<P>::bits(x0) | ((uint32_t)Ty<P>::bits(x1) << 16);
+            }
+            J.wb[k] = u32x4{v[0], v[1], v[2], v[3]};
+        }
+    }
+}
+
+// ---------------------------------------------------------------- select_action
+// rows per workgroup = 16 SELECT_RT: 1 puts a workgroup on every CU at 4,096 envs
+// (the weight stream per CU, not the MFMA work, bounds these passes)
+constexpr int SELECT_RT = 1;
+struct SelectArgs {
+    Lin zs[3], ac[4];
+    int act_enc, act_actor;
+    const float *obs;
+    int n, S, A, Z, Ha;
+    float *out;
+    Noise nz;
+    R16 X, H1, H2, CAT;
+    R32 F;
+    int lds_bytes;
+};
+
+#define RING_START(first)      \
+    u32x4 R[PD][TH];           \
+    ring_fill(R, GDesc{(first).wf, (first).ksf, 0})
+
+template <int P, int TH>
+__global__ __launch_bounds__(NTH) void select_kernel(SelectArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    constexpr int RT = SELECT_RT, rows = RT * TR;
+    const int row0 = blockIdx.x * rows;
+    int si = 0;
+    FSTAMP(si);
+    zero_lds(lds, a.lds_bytes);
+    __syncthreads();
+    load_rows<P>(lds, a.X, 0, a.obs, a.S, a.S, rows, row0, a.n);
+    RING_START(a.zs[0]);
+    __syncthreads();
+    // zs = fixed_encoder.zs(obs) (:93-97) -> CAT[:, Ha:Ha+Z]
+    layer_fwd<P, RT, TH>(lds, R, a.X, a.zs[0], &a.zs[1], a.act_enc, a.H1, 0, NO32, nullptr, 0, row0, a.n, si);
+    layer_fwd<P, RT, TH>(lds, R, a.H1, a.zs[1], &a.zs[2], a.act_enc, a.H2, 0, NO32, nullptr, 0, row0, a.n, si);
+    layer_fwd<P, RT, TH>(lds, R, a.H2, a.zs[2], &a.ac[0], ACT_NONE, NO16, 0, a.F, nullptr, 0, row0, a.n, si);
+    norm_fwd<P>(lds, a.F, a.Z, rows, 1e-8f, a.CAT, a.Ha, NO16, 0, NO32, nullptr, 0, nullptr, nullptr, row0, a.n);
+    __syncthreads();
+    // actor (:72-77): AvgL1Norm(l0(s)) | zs -> l1 -> l2 -> tanh(l3)
+    layer_fwd<P, RT, TH>(lds, R, a.X, a.ac[0], &a.ac[1], ACT_NONE, NO16, 0, a.F, nullptr, 0, row0, a.n, si);
+    norm_fwd<P>(lds, a.F, a.Ha, rows, 1e-8f, a.CAT, 0, NO16, 0, NO32, nullptr, 0, nullptr, nullptr, row0, a.n);
+    __syncthreads();
+    layer_fwd<P, RT, TH>(lds, R, a.CAT, a.ac[1], &a.ac[2], a.act_actor, a.H1, 0, NO32, nullptr, 0, row0, a.n, si);
+    layer_fwd<P, RT, TH>(lds, R, a.H1, a.ac[2], (const Lin *)nullptr, a.act_actor, a.H2, 0, NO32, nullptr, 0, row0, a.n, si);
+    layer_thin_fwd<P>(lds, a.H2, a.ac[3], ACT_TANH, a.F, rows, nullptr, 0, row0, a.n, si);
+    noise_rows<P>(lds, a.F, a.A, rows, row0, a.n, a.nz, a.out, NO16, 0, NO16, 0);
+}
+
+// ---------------------------------------------------------------- critic target chain
+struct TargetArgs {
+    Lin enc[6], ac[4], cr[8];
+    int act_enc, act_actor, act_critic;
+    const float *ns;  // next_state [B][S]
+    int B, S, A, Z, Ha, Hc;
+    Noise nz;
+    uint16_t *img;  // [B][2Z + A]: zsa | zs | next_action
+    float *qt;      // [B][2]
+    R16 X, H1, H2, CATA, CATZ, OUT, CAT;
+    R32 F;
+    int lds_a, lds_b;
+};
+
+template <int P, int TH>
+__global__ __launch_bounds__(NTH) void target_a_kernel(TargetArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    constexpr int RT = 1, rows = TR;
+    const int row0 = blockIdx.x * rows, B = a.B, Z = a.Z;
+    int si = 0;
+    FSTAMP(si);
+    zero_lds(lds, a.lds_a);
+    __syncthreads();
+    load_rows<P>(lds, a.X, 0, a.ns, a.S, a.S, rows, row0, B);
+    RING_START(a.enc[0]);
+    __syncthreads();
+    // fixed_target_zs = fixed_encoder_target.zs(next_state) (:234)
+    layer_fwd<P, RT, TH>(lds, R, a.X, a.enc[0], &a.enc[1], a.act_enc, a.H1, 0, NO32, nullptr, 0, row0, B, si);
+    layer_fwd<P, RT, TH>(lds, R, a.H1, a.enc[1], &a.enc[2], a.act_enc, a.H2, 0, NO32, nullptr, 0, row0, B, si);
+    layer_fwd<P, RT, TH>(lds, R, a.H2, a.enc[2], &a.ac[0], ACT_NONE, NO16, 0, a.F, nullptr, 0, row0, B, si);
+    norm_fwd<P>(lds, a.F, Z, rows, 1e-8f, a.CATA, a.Ha, a.CATZ, 0, NO32, nullptr, 0, nullptr, nullptr, row0, B);
+    __syncthreads();
+    // next_action = (actor_target(s', zs) + clip(noise * sigma)).clamp(-1, 1) (:236-238)
+    layer_fwd<P, RT, TH>(lds, R, a.X, a.ac[0], &a.ac[1], ACT_NONE, NO16, 0, a.F, nullptr, 0, row0, B, si);
+    norm_fwd<P>(lds, a.F, a.Ha, rows, 1e-8f, a.CATA, 0, NO16, 0, NO32, nullptr, 0, nullptr, nullptr, row0, B);
+    __syncthreads();
+    layer_fwd<P, RT, TH>(lds, R, a.CATA, a.ac[1], &a.ac[2], a.act_actor, a.H1, 0, NO32, nullptr, 0, row0, B, si);
+    layer_fwd<P, RT, TH>(lds, R, a.H1, a.ac[2], &a.enc[3], a.act_actor, a.H2, 0, NO32, nullptr, 0, row0, B, si);
+    layer_thin_fwd<P>(lds, a.H2, a.ac[3], ACT_TANH, a.F, rows, nullptr, 0, row0, B, si);
+    noise_rows<P>(lds, a.F, a.A, rows, row0, B, a.nz, nullptr, a.CATZ, Z, a.OUT, 2 * Z);
+    __syncthreads();
+    // fixed_target_zsa = fixed_encoder_target.zsa(zs, next_action) (:240) -> OUT[:, 0:Z]
+    layer_fwd<P, RT, TH>(lds, R, a.CATZ, a.enc[3], &a.enc[4], a.act_enc, a.H1, 0, NO32, nullptr, 0, row0, B, si);
+    layer_fwd<P, RT, TH>(lds, R, a.H1, a.enc[4], &a.enc[5], a.act_enc, a.H2, 0, NO32, nullptr, 0, row0, B, si);
+    layer_fwd<P, RT, TH>(lds, R, a.H2, a.enc[5], (const Lin *)nullptr, ACT_NONE, a.OUT, 0, NO32, nullptr, 0, row0, B, si);
+    // zs into OUT[:, Z:2Z] (from CATZ[:, 0:Z])
+    for (int k = threadIdx.x; k < rows * Z; k += NTH) {
+        const int row = k / Z, c = k - row * Z;
+        *p16(lds, a.OUT, row, Z + c) = *p16(lds, a.CATZ, row, c);
+    }
+    __syncthreads();
+    store_rows16(lds, a.OUT, 0, a.img, (2 * Z + a.A + 7) / 8 * 8, (2 * Z + a.A + 7) / 8 * 8, rows, row0, B);
+}
+
+template <int P, int TH>
+__global__ __launch_bounds__(NTH) void target_b_kernel(TargetArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    constexpr int RT = 1, rows = TR;
+    const int row0 = blockIdx.x * rows, B = a.B, Z = a.Z, h = blockIdx.y;
+    const long ild = (2 * Z + a.A + 7) / 8 * 8;
+    const Lin *cr = a.cr + h;  // layer l of head h: cr[2 l]
+    int si = 0;
+    FSTAMP(si);
+    zero_lds(lds, a.lds_b);
+    __syncthreads();
+    load_rows<P>(lds, a.X, 0, a.ns, a.S, a.S, rows, row0, B);
+    load_rows16(lds, a.X, a.S, a.img + 2 * Z, ild, a.A, rows, row0, B);
+    load_rows16(lds, a.CAT, a.Hc, a.img, ild, 2 * Z, rows, row0, B);
+    RING_START(cr[0]);
+    __syncthreads();
+    // critic_target(s', a', zsa, zs) head h (:109-140): AvgL1Norm(q0(sa)) | zsa | zs -> q1 -> q2 -> q3
+    layer_fwd<P, RT, TH>(lds, R, a.X, cr[0], &cr[2], ACT_NONE, NO16, 0, a.F, nullptr, 0, row0, B, si);
+    norm_fwd<P>(lds, a.F, a.Hc, rows, 1e-8f, a.CAT, 0, NO16, 0, NO32, nullptr, 0, nullptr, nullptr, row0, B);
+    __syncthreads();
+    layer_fwd<P, RT, TH>(lds, R, a.CAT, cr[2], &cr[4], a.act_critic, a.H1, 0, NO32, nullptr, 0, row0, B, si);
+    layer_fwd<P, RT, TH>(lds, R, a.H1, cr[4], (const Lin *)nullptr, a.act_critic, a.H2, 0, NO32, nullptr, 0, row0, B, si);
+    layer_thin_fwd<P>(lds, a.H2, cr[6], ACT_NONE, a.F, rows, a.qt + h, 2, row0, B, si);
+}
+
+// ---------------------------------------------------------------- fixed embeddings
+struct FixedArgs {
+    Lin enc[6];
+    int act_enc;
+    const float *s, *act;
+    int B, S, A, Z;
+    float *zs, *zsa;
+    R16 X, H1, H2, CATZ;
+    R32 F;
+    int lds_bytes;
+};
+
+template <int P, int TH>
+__global__ __launch_bounds__(NTH) void fixed_kernel(FixedArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    constexpr int RT = 1, rows = TR;
+    const int row0 = blockIdx.x * rows, B = a.B, Z = a.Z;
+    int si = 0;
+    FSTAMP(si);
+    zero_lds(lds, a.lds_bytes);
+    __syncthreads();
+    load_rows<P>(lds, a.X, 0, a.s, a.S, a.S, rows, row0, B);
+    load_rows<P>(lds, a.CATZ, Z, a.act, a.A, a.A, rows, row0, B);
+    RING_START(a.enc[0]);
+    __syncthreads();
+    layer_fwd<P, RT, TH>(lds, R, a.X, a.enc[0], &a.enc[1], a.act_enc, a.H1, 0, NO32, nullptr, 0, row0, B, si);
+    layer_fwd<P, RT, TH>(lds, R, a.H1, a.enc[1], &a.enc[2], a.act_enc, a.H2, 0, NO32, nullptr, 0, row0, B, si);
+    layer_fwd<P, RT, TH>(lds, R, a.H2, a.enc[2], &a.enc[3], ACT_NONE, NO16, 0, a.F, nullptr, 0, row0, B, si);
+    norm_fwd<P>(lds, a.F, Z, rows, 1e-8f, a.CATZ, 0, NO16, 0, NO32, a.zs, Z, nullptr, nullptr, row0, B);
+    __syncthreads();
+    layer_fwd<P, RT, TH>(lds, R, a.CATZ, a.enc[3], &a.enc[4], a.act_enc, a.H1, 0, NO32, nullptr, 0, row0, B, si);
+    layer_fwd<P, RT, TH>(lds, R, a.H1, a.enc[4], &a.enc[5], a.act_enc, a.H2, 0, NO32, nullptr, 0, row0, B, si);
+    layer_fwd<P, RT, TH>(lds, R, a.H2, a.enc[5], (const Lin *)nullptr, ACT_NONE, NO16, 0, NO32, a.zsa, Z, row0, B, si);
+}
+
+// ---------------------------------------------------------------- host side
+}  // namespace td7f
+
+using namespace td7f;
+
+extern "C" {
+
+#ifdef EXO_STAMPS
+int td7f_debug_set_stamps(unsigned long long *buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_td7f_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -5;
+}
+#endif
+
+int td7f_pack(int32_t prec, int32_t njobs, const td7f_pack_job *jobs, void *stream) {
+    if ((prec != PREC_BF16 && prec != PREC_F16) || njobs <= 0 || njobs > TD7F_MAX_PACK || !jobs) return EXO_EINVAL;
+    PackArgs a{};
+    a.njobs = njobs;
+    a.start[0] = 0;
+    for (int q = 0; q < njobs; ++q) {
+        const td7f_pack_job &J = jobs[q];
+        if (!J.w || !J.wf || J.n_out <= 0 || J.n_in <= 0 || J.ld < J.n_in || J.ksf * 32 < J.n_in ||
+            J.ntf * 16 < J.n_out || (J.wb && (J.ksb * 32 < J.n_out || J.ntb * 16 < J.n_in)))
+            return EXO_EINVAL;
+        a.j[q] = PackJob{J.w, (long)J.ld, J.n_out, J.n_in, (u32x4 *)J.wf, (u32x4 *)J.wb, J.ksf, J.ntf,
+                         J.wb ? J.ksb : 0, J.wb ? J.ntb : 0};
+        a.start[q + 1] = a.start[q] + (long)J.ntf * J.ksf * 64 + (J.wb ? (long)J.ntb * J.ksb * 64 : 0);
+    }
+    const long total = a.start[njobs];
+    const int blocks = (int)std::min<long>(2048, (total + 255) / 256);
+    if (prec == PREC_BF16)
+        hipLaunchKernelGGL(pack_kernel<PREC_BF16>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
+    else
+        hipLaunchKernelGGL(pack_kernel<PREC_F16>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
+    return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
+}
+
+int td7f_select(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7f_lin *actor, const float *obs,
+                int32_t n, const td7f_noise *noise, float *out, void *stream) {
+    if ((prec != PREC_BF16 && prec != PREC_F16) || !act || !enc || !actor || !obs || !noise || !out || n <= 0)
+        return EXO_EINVAL;
+    td7f_lin all[7] = {enc[0], enc[1], enc[2], actor[0], actor[1], actor[2], actor[3]};
+    const int th = th_of(all, 7);
+    if (th != 4 && th != 5) return EXO_EINVAL;
+    SelectArgs a{};
+    for (int i = 0; i < 3; ++i) a.zs[i] = lin_of(enc[i]);
+    for (int i = 0; i < 4; ++i) a.ac[i] = lin_of(actor[i]);
+    a.act_enc = act[0];
+    a.act_actor = act[1];
+    a.obs = obs;
+    a.n = n;
+    a.S = enc[0].n_in;
+    a.A = actor[3].n_out;
+    a.Z = enc[2].n_out;
+    a.Ha = actor[0].n_out;
+    if (actor[0].n_in != a.S || actor[1].n_in != a.Ha + a.Z || a.A > 16) return EXO_EINVAL;
+    a.out = out;
+    a.nz = noise_of(*noise);
+    const int rows = SELECT_RT * TR, hmax = std::max(enc[0].n_out, std::max(enc[1].n_out, std::max(a.Ha, actor[1].n_out)));
+    Bump b(rows / TR);
+    a.X = b.r16(rows, ld16(a.S));
+    a.H1 = b.r16(rows, ld16(hmax));
+    a.H2 = b.r16(rows, ld16(hmax));
+    a.CAT = b.r16(rows, ld16(a.Ha + a.Z));
+    a.F = b.r32(rows, std::max(std::max(a.Z, a.Ha), 16));
+    a.lds_bytes = b.off;
+    return DISPATCH(prec, th, select_kernel, dim3((n + rows - 1) / rows), b.off, a, (hipStream_t)stream);
+}
+
+int td7f_target(int32_t prec, const int32_t *act, const td7f_lin *tenc, const td7f_lin *tactor,
+                const td7f_lin *tcritic, const float *ns, int32_t B, const td7f_noise *noise, uint16_t *img,
+                float *qt, void *stream) {
+    if ((prec != PREC_BF16 && prec != PREC_F16) || !act || !tenc || !tactor || !tcritic || !ns || !noise || !img ||
+        !qt || B <= 0)
+        return EXO_EINVAL;
+    td7f_lin all[18];
+    for (int i = 0; i < 6; ++i) all[i] = tenc[i];
+    for (int i = 0; i < 4; ++i) all[6 + i] = tactor[i];
+    for (int i = 0; i < 8; ++i) all[10 + i] = tcritic[i];
+    const int th = th_of(all, 18);
+    if (th != 4 && th != 5) return EXO_EINVAL;
+    TargetArgs a{};
+    for (int i = 0; i < 6; ++i) a.enc[i] = lin_of(tenc[i]);
+    for (int i = 0; i < 4; ++i) a.ac[i] = lin_of(tactor[i]);
+    for (int i = 0; i < 8; ++i) a.cr[i] = lin_of(tcritic[i]);
+    a.act_enc = act[0];
+    a.act_actor = act[1];
+    a.act_critic = act[2];
+    a.ns = ns;
+    a.B = B;
+    a.S = tenc[0].n_in;
+    a.A = tactor[3].n_out;
+    a.Z = tenc[2].n_out;
+    a.Ha = tactor[0].n_out;
+    a.Hc = tcritic[0].n_out;
+    // tcritic is [layer][head]: layer l of head h at 2l + h
+    if (tcritic[0].n_in != a.S + a.A || tcritic[2].n_in != a.Hc + 2 * a.Z || tcritic[4].n_in != a.Hc ||
+        tenc[3].n_in != a.Z + a.A || a.A > 16)
+        return EXO_EINVAL;
+    a.nz = noise_of(*noise);
+    a.img = img;
+    a.qt = qt;
+    const int rows = TR;
+    int hmax = 0;
+    for (int i = 0; i < 18; ++i) hmax = std::max(hmax, all[i].n_out);
+    Bump ba(1);
+    a.X = ba.r16(rows, ld16(a.S + a.A));
+    a.H1 = ba.r16(rows, ld16(hmax));
+    a.H2 = ba.r16(rows, ld16(hmax));
+    a.CATA = ba.r16(rows, ld16(a.Ha + a.Z));
+    a.CATZ = ba.r16(rows, ld16(a.Z + a.A));
+    a.OUT = ba.r16(rows, round_up(2 * a.Z + a.A, 8));  // == the image row (16-byte stores)
+    a.F = ba.r32(rows, std::max(hmax, 16));
+    a.lds_a = ba.off;
+    Bump bb(1);
+    const R16 Xb = bb.r16(rows, ld16(a.S + a.A)), H1b = bb.r16(rows, ld16(hmax)), H2b = bb.r16(rows, ld16(hmax));
+    const R16 CATb = bb.r16(rows, ld16(a.Hc + 2 * a.Z));
+    const R32 Fb = bb.r32(rows, std::max(hmax, 16));
+    a.lds_b = bb.off;
+    const hipStream_t st = (hipStream_t)stream;
+    int rc = DISPATCH(prec, th, target_a_kernel, dim3((B + rows - 1) / rows), ba.off, a, st);
+    if (rc != EXO_OK) return rc;
+    TargetArgs b2 = a;
+    b2.X = Xb;
+    b2.H1 = H1b;
+    b2.H2 = H2b;
+    b2.CAT = CATb;
+    b2.F = Fb;
+    return DISPATCH(prec, th, target_b_kernel, dim3((B + rows - 1) / rows, 2), bb.off, b2, st);
+}
+
+int td7f_fixed(int32_t prec, const int32_t *act, const td7f_lin *fenc, const float *s, const float *action,
+               int32_t B, float *zs, float *zsa, void *stream) {
+    if ((prec != PREC_BF16 && prec != PREC_F16) || !act || !fenc || !s || !action || !zs || !zsa || B <= 0)
+        return EXO_EINVAL;
+    const int th = th_of(fenc, 6);
+    if (th != 4 && th != 5) return EXO_EINVAL;
+    FixedArgs a{};
+    for (int i = 0; i < 6; ++i) a.enc[i] = lin_of(fenc[i]);
+    a.act_enc = act[0];
+    a.s = s;
+    a.act = action;
+    a.B = B;
+    a.S = fenc[0].n_in;
+    a.Z = fenc[2].n_out;
+    a.A = fenc[3].n_in - a.Z;
+    if (a.A <= 0 || a.A > 16) return EXO_EINVAL;
+    a.zs = zs;
+    a.zsa = zsa;
+    const int rows = TR;
+    int hmax = 0;
+    for (int i = 0; i < 6; ++i) hmax = std::max(hmax, fenc[i].n_out);
+    Bump b(1);
+    a.X = b.r16(rows, ld16(a.S));
+    a.H1 = b.r16(rows, ld16(hmax));
+    a.H2 = b.r16(rows, ld16(hmax));
+    a.CATZ = b.r16(rows, ld16(a.Z + a.A));
+    a.F = b.r32(rows, std::max(hmax, 16));
+    a.lds_bytes = b.off;
+    return DISPATCH(prec, th, fixed_kernel, dim3((B + rows - 1) / rows), b.off, a, (hipStream_t)stream);
+}
+
+}  // extern "C"

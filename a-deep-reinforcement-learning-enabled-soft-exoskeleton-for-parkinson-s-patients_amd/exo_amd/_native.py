@@ -52,6 +52,43 @@ class ExoMbParams(ctypes.Structure):
                                         "erp", "lin_damp", "ang_damp", "max_vel")] + [("iters", c_int32)]
 
 
+class TD7FLin(ctypes.Structure):
+    """td7f_lin (include/exo_amd.h)."""
+    _fields_ = [("wf", c_void_p), ("wb", c_void_p), ("b", c_void_p), ("n_out", c_int32), ("n_in", c_int32),
+                ("ksf", c_int32), ("ksb", c_int32), ("w", c_void_p), ("ldw", ctypes.c_int64)]
+
+
+class TD7FPackJob(ctypes.Structure):
+    """td7f_pack_job (include/exo_amd.h)."""
+    _fields_ = [("w", c_void_p), ("ld", ctypes.c_int64), ("n_out", c_int32), ("n_in", c_int32), ("wf", c_void_p),
+                ("wb", c_void_p), ("ksf", c_int32), ("ntf", c_int32), ("ksb", c_int32), ("ntb", c_int32)]
+
+
+class TD7FNoise(ctypes.Structure):
+    """td7f_noise (include/exo_amd.h)."""
+    _fields_ = [("seed", c_uint64), ("tag", ctypes.c_uint32), ("pad0", ctypes.c_uint32), ("counter", c_void_p),
+                ("ticket", c_void_p), ("sigma", c_void_p), ("sigma_dec", ctypes.c_float), ("clip", ctypes.c_float),
+                ("scale", ctypes.c_float), ("pad1", c_int32), ("z", c_void_p)]
+
+
+class TD7FXT(ctypes.Structure):
+    """td7f_xt (include/exo_amd.h)."""
+    _fields_ = [("x", c_void_p), ("dp", c_void_p), ("part", c_void_p)]
+
+
+class TD7FActorBufs(ctypes.Structure):
+    """td7f_actor_bufs (include/exo_amd.h)."""
+    _fields_ = [("act_out", c_void_p), ("zsa_out", c_void_p), ("h0", c_void_p), ("mean0", c_void_p),
+                ("ya", c_void_p * 2), ("yz", c_void_p * 2), ("yc", c_void_p * 2), ("da", c_void_p),
+                ("dzsa", c_void_p)]
+
+
+class TD7FWgJob(ctypes.Structure):
+    """td7f_wg_job (include/exo_amd.h)."""
+    _fields_ = [("dp", c_void_p), ("x", c_void_p), ("part", c_void_p), ("dw", c_void_p), ("db", c_void_p),
+                ("n", c_int32), ("k", c_int32), ("row_tiles", c_int32)]
+
+
 EXPORTS = {
     "exo_create": (c_int32, [P(ExoEnvConfig), c_int32, P(c_double), P(c_int32), c_int32, c_int32, c_uint64, c_int32,
                              P(c_void_p)]),
@@ -134,6 +171,21 @@ EXPORTS = {
     "td7_dense_bwd_weight": (c_int32, [c_void_p, c_long, c_long, c_void_p, c_long, c_long, c_void_p, c_long,
                                        c_long, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32,
                                        c_void_p]),
+    "td7f_pack": (c_int32, [c_int32, c_int32, P(TD7FPackJob), c_void_p]),
+    "td7f_select": (c_int32, [c_int32, P(c_int32), P(TD7FLin), P(TD7FLin), c_void_p, c_int32, P(TD7FNoise), c_void_p,
+                              c_void_p]),
+    "td7f_target": (c_int32, [c_int32, P(c_int32), P(TD7FLin), P(TD7FLin), P(TD7FLin), c_void_p, c_int32,
+                              P(TD7FNoise), c_void_p, c_void_p, c_void_p]),
+    "td7f_fixed": (c_int32, [c_int32, P(c_int32), P(TD7FLin), c_void_p, c_void_p, c_int32, c_void_p, c_void_p,
+                             c_void_p]),
+    "td7f_critic": (c_int32, [c_int32, P(c_int32), P(TD7FLin)] + [c_void_p] * 7 + [ctypes.c_float]
+                    + [c_void_p] * 4 + [c_int32] * 3 + [c_void_p] * 4 + [P(TD7FXT), ctypes.c_int64, c_void_p]),
+    "td7f_encoder": (c_int32, [c_int32, P(c_int32), P(TD7FLin), c_void_p, c_void_p, c_void_p, c_int32, P(c_void_p),
+                               P(TD7FXT), ctypes.c_int64, c_void_p]),
+    "td7f_actor": (c_int32, [c_int32, c_int32, P(c_int32), P(TD7FLin), P(TD7FLin), P(TD7FLin), c_void_p, c_void_p,
+                             c_int32, P(TD7FActorBufs), P(TD7FXT), ctypes.c_int64, c_void_p]),
+    "td7f_wgrad": (c_int32, [c_int32, c_int32, P(TD7FWgJob), ctypes.c_int64, c_int32, c_void_p, c_void_p, c_int32,
+                             ctypes.c_float, ctypes.c_float, c_void_p]),
 }
 
 _lib = None

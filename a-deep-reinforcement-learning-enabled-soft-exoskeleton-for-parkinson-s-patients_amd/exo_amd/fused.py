@@ -1,0 +1,374 @@
+"""Row-tile-fused TD7 networks on the GPU (csrc/td7_fused.hip): the host side.
+
+With bf16 / fp16 MFMA operands the TD7 nets of Agent/TD7_multi_agent.py:61-140
+run as whole-network launches (one workgroup per 16 rows, activations in LDS)
+instead of one launch per Linear.  Their weights are read from packed 16-bit
+copies in MFMA-fragment order (PackedLinear), refreshed by td7f_pack after every
+change of the fp32 master weights (optimiser steps, target refreshes, loads).
+
+FusedNets owns the packed copies of every net the update reads and the
+launch wrappers; TD7Learner routes its passes here when `fused` is on.
+"""
+import ctypes
+
+import torch
+
+from . import _native as nat
+from . import ops
+
+PD = 5  # include/exo_amd.h TD7F_PD
+NW = 4  # waves per fused workgroup (csrc/td7_fused.h)
+MAX_PACK = 32
+PREC = {"bf16": 1, "fp16": 2}
+
+
+TD7FLin, TD7FPackJob, TD7FNoise = nat.TD7FLin, nat.TD7FPackJob, nat.TD7FNoise
+
+
+def _ks(k):
+    """k-steps of a packed operand: ceil(k / 32) rounded up to TD7F_PD."""
+    return -(-(-(-k // 32)) // PD) * PD
+
+
+def _tiles(n):
+    """16-wide tiles of a packed operand: exact up to NW, else a multiple of NW."""
+    t = -(-n // 16)
+    return t if t <= NW else -(-t // NW) * NW
+
+
+class PackedLinear:
+    """The 16-bit packed operands of one Linear W [N, K] (a view of the fp32
+    master weight; one head of a stacked critic layer is a slice): the forward
+    operand and, with bwd=True, the dX operand."""
+
+    def __init__(self, weight, bias, bwd):
+        N, K = weight.shape
+        dev = weight.device
+        self.weight, self.bias = weight, bias
+        self.N, self.K = N, K
+        self.ksf, self.ntf = _ks(K), _tiles(N)
+        self.wf = torch.zeros(self.ntf * self.ksf * 64 * 8, dtype=torch.int16, device=dev)
+        self.ksb = _ks(N) if bwd else 0
+        self.ntb = -(-(-(-K // 16)) // NW) * NW if bwd else 0
+        self.wb = torch.zeros(self.ntb * self.ksb * 64 * 8, dtype=torch.int16, device=dev) if bwd else None
+        assert weight.stride(1) == 1
+        self.lin = TD7FLin(self.wf.data_ptr(), self.wb.data_ptr() if bwd else None, bias.data_ptr(), N, K, self.ksf,
+                           self.ksb, weight.data_ptr(), weight.stride(0))
+
+    def job(self):
+        w = self.weight
+        assert w.stride(1) == 1
+        return TD7FPackJob(w.data_ptr(), w.stride(0), self.N, self.K, self.wf.data_ptr(),
+                           self.wb.data_ptr() if self.wb is not None else None, self.ksf, self.ntf, self.ksb, self.ntb)
+
+
+def _lin_array(lins):
+    return (TD7FLin * len(lins))(*[pl.lin for pl in lins])
+
+
+class PackedNet:
+    """Packed copies of a set of Linears, refreshed together by one td7f_pack launch."""
+
+    def __init__(self, layers, prec, bwd=False):
+        self.layers = [PackedLinear(w, b, bwd) for w, b in layers]
+        self.prec = prec
+        self.array = _lin_array(self.layers)
+
+    def pack(self, stream=None):
+        jobs = [pl.job() for pl in self.layers]
+        dev = self.layers[0].wf.device
+        st = stream if stream is not None else nat.stream_ptr(dev)
+        for i in range(0, len(jobs), MAX_PACK):
+            part = jobs[i:i + MAX_PACK]
+            nat.check(nat.lib().td7f_pack(self.prec, len(part), (TD7FPackJob * len(part))(*part), st), "td7f_pack")
+        self._ver = self._versions()
+
+    def _versions(self):
+        return tuple(t._version for pl in self.layers for t in (pl.weight, pl.bias))
+
+    def refresh(self):
+        """Repack when a master weight changed through torch since the last
+        pack (load_state_dict, copy_: their version counters moved); the HIP
+        optimiser steps write the masters in place, and their callers repack
+        explicitly (TD7Learner.phase_actor_step, maybe_update_targets)."""
+        if self._versions() != self._ver:
+            self.pack()
+
+
+def encoder_layers(enc):
+    return [(getattr(enc, n).weight, getattr(enc, n).bias) for n in ("zs1", "zs2", "zs3", "zsa1", "zsa2", "zsa3")]
+
+
+def actor_layers(actor):
+    return [(getattr(actor, n).weight, getattr(actor, n).bias) for n in ("l0", "l1", "l2", "l3")]
+
+
+def critic_layers(critic):
+    """[layer][head] order: w_k[h] of the stacked critic (the reference's q01/q02, q1/q4, q2/q5, q3/q6)."""
+    out = []
+    for k in range(4):
+        w, b = getattr(critic, f"w{k}"), getattr(critic, f"b{k}")
+        for h in range(2):
+            out.append((w[h], b[h]))
+    return out
+
+
+def supported(learner):
+    """The fused path applies: GPU, bf16/fp16 operands, the reference's
+    activations, every hidden width 49..320 (packed tiles per wave 4 or 5),
+    critic / actor / encoder of the reference shapes."""
+    hp = learner.hp
+    if learner.device.type != "cuda" or learner.precision not in PREC:
+        return False
+    acts = [ops.act_code(f) for f in (hp.enc_activ, hp.actor_activ, hp.critic_activ)]
+    if any(a is None or a == ops.ACT_CODES["tanh"] for a in acts):
+        return False
+    widths = (hp.zs_dim, hp.enc_hdim, hp.critic_hdim, hp.actor_hdim)
+    th = {_tiles(w) // NW for w in widths}
+    return all(49 <= w <= 320 and w % 4 == 0 for w in widths) and len(th) == 1 and th <= {4, 5}
+
+
+class FusedNets:
+    """Packed copies of every TD7 net plus the fused launches of one learner."""
+
+    def __init__(self, learner):
+        L = learner
+        self.L = L
+        self.prec = PREC[L.precision]
+        self.dev = L.device
+        hp = L.hp
+        self.act = (ctypes.c_int32 * 3)(ops.act_code(hp.enc_activ), ops.act_code(hp.actor_activ),
+                                        ops.act_code(hp.critic_activ))
+        self._build()
+
+    def _build(self):
+        L, p = self.L, self.prec
+        self.nets = {
+            "fixed_encoder": PackedNet(encoder_layers(L.fixed_encoder), p, bwd=True),
+            "fixed_encoder_target": PackedNet(encoder_layers(L.fixed_encoder_target), p),
+            "actor": PackedNet(actor_layers(L.actor), p, bwd=True),
+            "actor_target": PackedNet(actor_layers(L.actor_target), p),
+            "critic_target": PackedNet(critic_layers(L.critic_target), p),
+            "encoder": PackedNet(encoder_layers(L.encoder), p, bwd=True),
+            "critic": PackedNet(critic_layers(L.critic), p, bwd=True),
+        }
+        self.pack_all()
+        self._train = {}
+
+    def train(self, B):
+        """The gradient passes for batches of B rows (buffers made on first use)."""
+        t = self._train.get(B)
+        if t is None:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("FusedNets.train: run once eagerly before graph capture")
+            t = self._train[B] = FusedTrain(self, B)
+        return t
+
+    def rebuild(self):
+        """After the learner re-created nets (Agent.load): new views, repacked."""
+        self._build()
+
+    def pack(self, *names):
+        for n in names:
+            self.nets[n].pack()
+
+    def pack_all(self):
+        self.pack(*self.nets)
+
+    def refresh(self, *names):
+        for n in names:
+            self.nets[n].refresh()
+
+    # ------------------------------------------------------------- noise
+    def _noise(self, rng, sigma, dec, clip, scale, z=None):
+        return TD7FNoise(rng.seed, rng.tag, 0, rng.counter_ptr, rng.ticket_ptr, sigma.data_ptr(), float(dec),
+                         float(clip), float(scale), 0, z.data_ptr() if z is not None else None)
+
+    # ------------------------------------------------------------- passes
+    @torch.no_grad()
+    def select(self, obs, scale=1.0):
+        """select_action_batch with Gaussian exploration (one launch): actor(obs,
+        fixed_encoder.zs(obs)) + N(0, exploration_noise) per element, clamped,
+        times max_action; exploration_noise decreases once per env."""
+        L = self.L
+        self.refresh("fixed_encoder", "actor")
+        obs = obs.contiguous()
+        n = obs.shape[0]
+        out = torch.empty((n, L.actor.l3.out_features), dtype=torch.float32, device=obs.device)
+        nz = self._noise(L._explore_rng, L.exploration_noise_t, L.action_noise_decrease * n, 0.0, scale)
+        fe, ac = self.nets["fixed_encoder"].layers, self.nets["actor"].layers
+        nat.check(nat.lib().td7f_select(self.prec, self.act, _lin_array(fe[:3]), self.nets["actor"].array,
+                                        nat.ptr(obs), n, ctypes.byref(nz), nat.ptr(out), nat.stream_ptr(obs.device)),
+                  "td7f_select")
+        return out
+
+    def _img(self, B):
+        Z = self.L.hp.zs_dim
+        A = self.L.actor.l3.out_features
+        buf = getattr(self, "_tgt_img", None)
+        if buf is None or buf.shape[0] < B:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("FusedNets.target: run once eagerly before graph capture")
+            buf = self._tgt_img = torch.empty((B, -(-(2 * Z + A) // 8) * 8), dtype=torch.int16, device=self.dev)
+        return buf
+
+    @torch.no_grad()
+    def target_heads(self, next_state, noise=None):
+        """Both heads of critic_target(s', a'(s'), zsa', zs') [B, 2] with a' the
+        noisy target action (:233-241); two launches.  noise: given standard
+        normals [B, A] (parity tests) instead of the device stream."""
+        L = self.L
+        self.refresh("fixed_encoder_target", "actor_target", "critic_target")
+        ns = next_state.contiguous()
+        B = ns.shape[0]
+        qt = torch.empty((B, 2), dtype=torch.float32, device=ns.device)
+        z = noise.to(device=ns.device, dtype=torch.float32).contiguous() if noise is not None else None
+        nz = self._noise(L._noise_rng, L.target_policy_noise, L.policy_noise_decrease, L.hp.noise_clip, 1.0, z)
+        nat.check(nat.lib().td7f_target(self.prec, self.act, self.nets["fixed_encoder_target"].array,
+                                        self.nets["actor_target"].array, self.nets["critic_target"].array,
+                                        nat.ptr(ns), B, ctypes.byref(nz), nat.ptr(self._img(B)), nat.ptr(qt),
+                                        nat.stream_ptr(ns.device)), "td7f_target")
+        return qt
+
+    @torch.no_grad()
+    def fixed(self, state, action):
+        """(fixed_encoder.zs(state), fixed_encoder.zsa(zs, action)), one launch (:248-249)."""
+        self.refresh("fixed_encoder")
+        s, a = state.contiguous(), action.contiguous()
+        B = s.shape[0]
+        Z = self.L.hp.zs_dim
+        zs = torch.empty((B, Z), dtype=torch.float32, device=s.device)
+        zsa = torch.empty((B, Z), dtype=torch.float32, device=s.device)
+        nat.check(nat.lib().td7f_fixed(self.prec, self.act, self.nets["fixed_encoder"].array, nat.ptr(s), nat.ptr(a),
+                                       B, nat.ptr(zs), nat.ptr(zsa), nat.stream_ptr(s.device)), "td7f_fixed")
+        return zs, zsa
+
+
+class XTBuffers:
+    """The transposed 16-bit weight-gradient operands of one Linear (include/exo_amd.h td7f_xt)."""
+
+    def __init__(self, N, K, B, ld, dev):
+        r64 = lambda n: -(-n // 64) * 64  # noqa: E731
+        self.N, self.K = N, K
+        self.x = torch.zeros((r64(K), ld), dtype=torch.int16, device=dev)
+        self.dp = torch.zeros((r64(N), ld), dtype=torch.int16, device=dev)
+        self.part = torch.zeros((-(-B // 16), N), dtype=torch.float32, device=dev)
+        self.c = nat.TD7FXT(self.x.data_ptr(), self.dp.data_ptr(), self.part.data_ptr())
+
+
+def _grad_views(opt):
+    """Persistent gradient tensors of a FlatAdam's parameters: views of one flat
+    buffer in parameter order (the fused weight-gradient launch writes them;
+    the optimiser step and the data-parallel all-reduce read them)."""
+    g = torch.zeros_like(opt.flat)
+    off = 0
+    for p in opt._params():
+        n = p.numel()
+        p.grad = g[off:off + n].view_as(p)
+        off += n
+    return g
+
+
+class FusedTrain:
+    """The gradient passes of one TD7 update as fused launches (csrc/td7_fused_train.hip)
+    for a batch of B rows: buffers are allocated on the first call (outside graph capture)."""
+
+    def __init__(self, nets, B):
+        self.nets, self.L, self.B = nets, nets.L, B
+        L, dev = self.L, nets.dev
+        hp = L.hp
+        self.ld = -(-B // 32) * 32
+        Z, He, Hc, Ha = hp.zs_dim, hp.enc_hdim, hp.critic_hdim, hp.actor_hdim
+        A = L.actor.l3.out_features
+        S = L.actor.l0.in_features
+        self.S, self.A = S, A
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.xt_enc = [XTBuffers(pl.N, pl.K, B, self.ld, dev) for pl in nets.nets["encoder"].layers]
+        self.xt_critic = [XTBuffers(pl.N, pl.K, B, self.ld, dev) for pl in nets.nets["critic"].layers]
+        self.xt_actor = [XTBuffers(pl.N, pl.K, B, self.ld, dev) for pl in nets.nets["actor"].layers]
+        self.y_enc = [torch.empty((B, He), **f32) for _ in range(4)]
+        self.y_critic = [torch.empty((2, B, Hc), **f32) for _ in range(2)]
+        self.td = torch.zeros((B, 2), **f32)
+        self.q = torch.zeros((B, 2), **f32)
+        self.prio = torch.zeros((B,), **f32)
+        self.act_out = torch.zeros((B, A), **f32)
+        self.zsa_out = torch.zeros((B, Z), **f32)
+        self.h0 = torch.zeros((B, Ha), **f32)
+        self.mean0 = torch.zeros((B,), **f32)
+        self.ya = [torch.zeros((B, Ha), **f32) for _ in range(2)]
+        self.yz = [torch.zeros((B, He), **f32) for _ in range(2)]
+        self.yc = [torch.zeros((2, B, Hc), **f32) for _ in range(2)]
+        self.da = torch.zeros((2, B, A), **f32)
+        self.dzsa = torch.zeros((2, B, Z), **f32)
+        P = ctypes.c_void_p
+        self.actor_bufs = nat.TD7FActorBufs(self.act_out.data_ptr(), self.zsa_out.data_ptr(), self.h0.data_ptr(),
+                                            self.mean0.data_ptr(), (P * 2)(*[t.data_ptr() for t in self.ya]),
+                                            (P * 2)(*[t.data_ptr() for t in self.yz]),
+                                            (P * 2)(*[t.data_ptr() for t in self.yc]), self.da.data_ptr(),
+                                            self.dzsa.data_ptr())
+        self.enc_grad = _grad_views(L.encoder_optimizer)
+        self.critic_grad = _grad_views(L.critic_optimizer)
+        self.actor_grad = _grad_views(L.actor_optimizer)
+        # weight-gradient jobs: [layer] (encoder), [layer][head] (critic), [layer] (actor)
+        rt = -(-B // 16)
+        enc_p = list(L.encoder.parameters())
+        jobs = []
+        for i, xb in enumerate(self.xt_enc):
+            jobs.append(self._job(xb, enc_p[2 * i].grad, enc_p[2 * i + 1].grad, rt))
+        for k in range(4):
+            gw, gb = getattr(L.critic, f"w{k}").grad, getattr(L.critic, f"b{k}").grad
+            for h in range(2):
+                jobs.append(self._job(self.xt_critic[2 * k + h], gw[h], gb[h], rt))
+        self.jobs_ec = (nat.TD7FWgJob * len(jobs))(*jobs)
+        act_p = list(L.actor.parameters())
+        ajobs = [self._job(xb, act_p[2 * i].grad, act_p[2 * i + 1].grad, rt) for i, xb in enumerate(self.xt_actor)]
+        self.jobs_a = (nat.TD7FWgJob * len(ajobs))(*ajobs)
+        self.ptrs_y_enc = (P * 4)(*[t.data_ptr() for t in self.y_enc])
+
+    @staticmethod
+    def _job(xb, gw, gb, rt):
+        assert gw.is_contiguous() and gb.is_contiguous()
+        return nat.TD7FWgJob(xb.dp.data_ptr(), xb.x.data_ptr(), xb.part.data_ptr(), gw.data_ptr(), gb.data_ptr(),
+                             xb.N, xb.K, rt)
+
+    @staticmethod
+    def _xts(bufs):
+        return (nat.TD7FXT * len(bufs))(*[b.c for b in bufs])
+
+    def encoder(self, state, action, next_state):
+        fz = self.nets
+        fz.refresh("encoder")
+        nat.check(nat.lib().td7f_encoder(fz.prec, fz.act, fz.nets["encoder"].array, nat.ptr(state), nat.ptr(action),
+                                         nat.ptr(next_state), self.B, self.ptrs_y_enc, self._xts(self.xt_enc), self.ld,
+                                         nat.stream_ptr(state.device)), "td7f_encoder")
+
+    def critic(self, state, action, zs, zsa, qt, reward, not_done):
+        fz, L = self.nets, self.L
+        fz.refresh("critic")
+        nat.check(nat.lib().td7f_critic(
+            fz.prec, fz.act, fz.nets["critic"].array, nat.ptr(state), nat.ptr(action), nat.ptr(zs), nat.ptr(zsa),
+            nat.ptr(qt), nat.ptr(reward), nat.ptr(not_done), float(L.hp.discount), nat.ptr(L.min_target),
+            nat.ptr(L.max_target), nat.ptr(L.max), nat.ptr(L.min), self.B, self.S, self.A, nat.ptr(self.td),
+            nat.ptr(self.q), nat.ptr(self.y_critic[0]), nat.ptr(self.y_critic[1]), self._xts(self.xt_critic), self.ld,
+            nat.stream_ptr(state.device)), "td7f_critic")
+
+    def wgrad_encoder_critic(self):
+        """Every encoder and critic weight/bias gradient (one launch) and the LAP priorities."""
+        fz, hp = self.nets, self.L.hp
+        nat.check(nat.lib().td7f_wgrad(fz.prec, len(self.jobs_ec), self.jobs_ec, self.ld, self.ld, nat.ptr(self.td),
+                                       nat.ptr(self.prio), self.B, float(hp.alpha), float(hp.min_priority),
+                                       nat.stream_ptr(fz.dev)), "td7f_wgrad")
+        return self.prio
+
+    def actor(self, phase, state, zs):
+        fz = self.nets
+        fz.refresh("actor", "fixed_encoder", "critic")
+        nat.check(nat.lib().td7f_actor(fz.prec, phase, fz.act, fz.nets["actor"].array, fz.nets["fixed_encoder"].array,
+                                       fz.nets["critic"].array, nat.ptr(state), nat.ptr(zs), self.B,
+                                       ctypes.byref(self.actor_bufs), self._xts(self.xt_actor), self.ld,
+                                       nat.stream_ptr(state.device)), f"td7f_actor[{phase}]")
+
+    def wgrad_actor(self):
+        fz = self.nets
+        nat.check(nat.lib().td7f_wgrad(fz.prec, len(self.jobs_a), self.jobs_a, self.ld, self.ld, None, None, 0, 0.0,
+                                       0.0, nat.stream_ptr(fz.dev)), "td7f_wgrad")

@@ -473,6 +473,14 @@ class TD7Learner:
         self._device_rng = os.environ.get("EXO_DEVICE_RNG", "1") != "0"
         self._noise_rng = ops.DeviceRNG(self.device, 1) if self.device.type == "cuda" else None
         self._explore_rng = ops.DeviceRNG(self.device, 2) if self.device.type == "cuda" else None
+        # bf16/fp16 on the GPU: whole-network fused launches (exo_amd/fused.py,
+        # csrc/td7_fused.hip) over packed 16-bit weight copies; EXO_TD7_FUSED=0
+        # keeps the per-layer kernels
+        self.fused = None
+        if os.environ.get("EXO_TD7_FUSED", "1") != "0" and self._device_rng:
+            from . import fused as _fused
+            if _fused.supported(self):
+                self.fused = _fused.FusedNets(self)
 
     ENC_LAYERS = ("zs1", "zs2", "zs3", "zsa1", "zsa2", "zsa3")
 
@@ -580,6 +588,8 @@ class TD7Learner:
             encoder_loss.backward()
 
     def phase_grads(self, state, action, next_state, reward, not_done, noise=None):
+        if self.fused is not None and state.is_cuda:
+            return self._phase_grads_fused(state, action, next_state, reward, not_done, noise)
         hp = self.hp
         # ---- encoder (:219-228)
         side = None
@@ -662,6 +672,58 @@ class TD7Learner:
         self._fixed_zs = fixed_zs
         return priority
 
+    def _phase_grads_fused(self, state, action, next_state, reward, not_done, noise=None):
+        """phase_grads as fused launches (exo_amd/fused.py, csrc/td7_fused*.hip):
+        the encoder update (one launch) on a side branch, the critic target
+        chain (two launches) on a second, fixed_zs / fixed_zsa (one) and -- in
+        an actor-update iteration -- the actor's forward (one) on a third; the
+        critic's forward, loss and backward as one launch once the target heads
+        are in, then every encoder and critic weight gradient plus the LAP
+        priorities as one grouped launch.  The gradients land in the
+        optimisers' flat gradient buffers (the parameters' .grad are views)."""
+        hp, fz = self.hp, self.fused
+        B = state.shape[0]
+        tr = fz.train(B)
+        state, action, next_state = state.contiguous(), action.contiguous(), next_state.contiguous()
+        reward, not_done = reward.contiguous(), not_done.contiguous()
+        cur = torch.cuda.current_stream(self.device)
+        branch = self.overlap
+
+        def stream(name):
+            st = getattr(self, name, None)
+            if st is None:
+                st = torch.cuda.Stream(device=self.device)
+                setattr(self, name, st)
+            st.wait_stream(cur)
+            return st
+
+        if branch:
+            side, tside = stream("_side"), stream("_tside")
+            with torch.cuda.stream(side):
+                tr.encoder(state, action, next_state)
+            with torch.cuda.stream(tside):
+                qt = fz.target_heads(next_state, noise)
+        else:
+            tr.encoder(state, action, next_state)
+            qt = fz.target_heads(next_state, noise)
+        zs, zsa = fz.fixed(state, action)
+        self._actor_fused_pre = False
+        if branch and self.prefetch_actor and self.actor_branch:
+            aside = stream("_aside")
+            with torch.cuda.stream(aside):
+                tr.actor(0, state, zs)
+            self._actor_fused_pre = True
+        if branch:
+            cur.wait_stream(tside)
+        tr.critic(state, action, zs, zsa, qt, reward, not_done)
+        if branch:
+            cur.wait_stream(side)
+        priority = tr.wgrad_encoder_critic()
+        if self._actor_fused_pre:
+            cur.wait_stream(self._aside)
+        self._fixed_zs = zs
+        return priority
+
     @torch.no_grad()
     def _target_chain(self, next_state, reward, not_done, noise, fixed_target_zs, pair):
         """:236-246: target action with clipped noise, the target critic's heads
@@ -701,15 +763,32 @@ class TD7Learner:
             ne = self.encoder_optimizer.flat.numel()
             self.encoder_optimizer.step(flat_grad=flat_grad[:ne], grad_scale=grad_scale)
             self.critic_optimizer.step(flat_grad=flat_grad[ne:], grad_scale=grad_scale)
+            if self.fused is not None:
+                self.fused.pack("encoder", "critic")
             return
         if isinstance(self.encoder_optimizer, FlatAdam) and self.device.type == "cuda":
             FlatAdam.step_many([self.encoder_optimizer, self.critic_optimizer])
+            if self.fused is not None:
+                self.fused.pack("encoder", "critic")
             return
         self.encoder_optimizer.step()
         self.critic_optimizer.step()
 
     def phase_actor_grads(self, state, action):
         """:268-277 with the just-updated critic."""
+        if self.fused is not None and state.is_cuda and not self.offline:
+            # fused: actor forward (unless prefetched on its branch), the critic
+            # heads back to the action / zsa inputs, the zsa and actor backward,
+            # then the actor's weight gradients (one grouped launch)
+            tr = self.fused.train(state.shape[0])
+            st = state.contiguous()
+            if not getattr(self, "_actor_fused_pre", False):
+                tr.actor(0, st, self._fixed_zs)
+            self._actor_fused_pre = False
+            tr.actor(1, st, self._fixed_zs)
+            tr.actor(2, st, self._fixed_zs)
+            tr.wgrad_actor()
+            return
         fixed_zs = self._fixed_zs
         pre, self._actor_pre = getattr(self, "_actor_pre", None), None
         with self._autocast():
@@ -754,11 +833,12 @@ class TD7Learner:
     def phase_actor_step(self, flat_grad=None, grad_scale=1.0):
         if flat_grad is not None and isinstance(self.actor_optimizer, FlatAdam):
             self.actor_optimizer.step(flat_grad=flat_grad, grad_scale=grad_scale)
-            return
-        if isinstance(self.actor_optimizer, FlatAdam) and self.device.type == "cuda":
+        elif isinstance(self.actor_optimizer, FlatAdam) and self.device.type == "cuda":
             FlatAdam.step_many([self.actor_optimizer])
-            return
-        self.actor_optimizer.step()
+        else:
+            self.actor_optimizer.step()
+        if self.fused is not None:
+            self.fused.pack("actor")  # select_action reads the packed actor
 
     def grad_params(self, actor=False):
         if actor:
@@ -796,6 +876,8 @@ class TD7Learner:
                          (self.fixed_encoder_target, self.fixed_encoder), (self.fixed_encoder, self.encoder)):
             with torch.no_grad():
                 torch._foreach_copy_(list(dst.parameters()), list(src.parameters()))
+        if self.fused is not None:
+            self.fused.pack("actor_target", "critic_target", "fixed_encoder_target", "fixed_encoder")
         self.sync_bounds()
         self.max_target.copy_(self.max)
         self.min_target.copy_(self.min)
@@ -920,6 +1002,9 @@ class Agent:
         does (:218-226), and exploration_noise decreases once per call (:225);
         otherwise Gaussian noise per env (TD7_multi_agent.py:205-207), one
         decrement per env (the training script's per-env calls)."""
+        fz = self.learner.fused
+        if fz is not None and use_exploration and timestep is None and not use_checkpoint and obs.is_cuda:
+            return fz.select(obs, scale=self.max_action)  # zs, actor and the noise in one launch
         a = self.learner.act(obs, use_checkpoint)
         if use_exploration and timestep is not None:
             col = self.noise_dev.index_select(1, timestep).t()           # [1, action_dim]
@@ -1009,6 +1094,8 @@ class Agent:
         L.fixed_encoder = copy.deepcopy(L.encoder)
         L.fixed_encoder_target = copy.deepcopy(L.encoder)
         L.pair_fixed_encoders()
+        if L.fused is not None:
+            L.fused.rebuild()
         L.checkpoint_actor.load_state_dict(ld("_checkpoint_actor"))
         L.checkpoint_encoder.load_state_dict(ld("_checkpoint_encoder"))
 

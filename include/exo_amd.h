@@ -384,6 +384,137 @@ int td7_dense_bwd_weight(const float *dy_dev, long dysg, long lddy, const float 
                          const float *x_dev, long xsg, long ldx, float *dw_dev, float *db_dev, int32_t groups,
                          int32_t m, int32_t n, int32_t k, int32_t act, void *stream);
 
+/* ---------------------------------------------------------------------------
+ * Row-tile-fused TD7 networks (csrc/td7_fused.hip), bf16 / fp16 MFMA operands
+ * (prec 1 / 2).  One workgroup owns 16 (select: 32) rows and runs a whole
+ * network pass of Agent/TD7_multi_agent.py on them with the activations in
+ * LDS; weights are read from packed 16-bit copies (td7f_pack, refreshed after
+ * every optimiser step / target copy).  Widths: hidden <= 320, inputs <= 1,008. */
+#define TD7F_PD 5          /* k-steps of weight loads in flight; packed k-steps are multiples of it */
+#define TD7F_MAX_PACK 32
+
+/* One nn.Linear: packed operands + fp32 bias.  ksf = k-steps of the forward
+ * operand (ceil(n_in/32) rounded up to TD7F_PD), ksb = k-steps of the dX
+ * operand (ceil(n_out/32) rounded up to TD7F_PD). */
+typedef struct {
+    const void *wf;
+    const void *wb;
+    const float *b;
+    int32_t n_out, n_in, ksf, ksb;
+    const float *w; /* fp32 master weight [n_out][n_in] (row stride ldw): the thin (<= 16 wide) products */
+    int64_t ldw;
+} td7f_lin;
+
+/* Pack one fp32 weight [n_out][n_in] (row stride ld floats) into the forward
+ * operand wf (ntf tiles x ksf k-steps x 64 lanes x 16 B) and, when wb is not
+ * NULL, the dX operand wb (ntb tiles x ksb k-steps x 64 x 16 B); zero padded. */
+typedef struct {
+    const float *w;
+    int64_t ld;
+    int32_t n_out, n_in;
+    void *wf;
+    void *wb;
+    int32_t ksf, ntf, ksb, ntb;
+} td7f_pack_job;
+
+/* In-kernel Gaussian noise of td7_noisy_action_rng (same stream, same element
+ * order): out = clamp(a + c(z * sigma), -1, 1) * scale, then sigma -= sigma_dec
+ * and the call counter advances (last workgroup out, ticket).  z non-NULL:
+ * the standard normals are given (z[row * A + c], td7_noisy_action) and the
+ * counter is left alone. */
+typedef struct {
+    uint64_t seed;
+    uint32_t tag, pad0;
+    unsigned long long *counter;
+    uint32_t *ticket;
+    float *sigma;
+    float sigma_dec, clip, scale;
+    int32_t pad1;
+    const float *z;
+} td7f_noise;
+
+/* Activation codes of the three nets: act[0] encoder, act[1] actor, act[2] critic (1 relu, 2 elu). */
+int td7f_pack(int32_t prec, int32_t njobs, const td7f_pack_job *jobs, void *stream);
+/* Agent.select_action_batch (TD7_multi_agent.py:192-209 batched): actor(obs,
+ * fixed_encoder.zs(obs)) + Gaussian exploration noise -> act_out [n][A].
+ * enc: zs1..zs3, actor: l0..l3. */
+int td7f_select(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7f_lin *actor, const float *obs_dev,
+                int32_t n, const td7f_noise *noise, float *act_out_dev, void *stream);
+/* The critic target chain (TD7_multi_agent.py:233-241): fixed_target_zs(s'),
+ * next_action = actor_target(s', zs) + clipped noise, fixed_target_zsa and both
+ * heads of critic_target -> qt_dev [B][2].  tenc: zs1..zs3, zsa1..zsa3;
+ * tcritic: [layer][head] (8).  tgt_img_dev: [B][round_up(2 zs_dim + A, 8)]
+ * 16-bit scratch ([zsa | zs | next_action] per row). */
+int td7f_target(int32_t prec, const int32_t *act, const td7f_lin *tenc, const td7f_lin *tactor,
+                const td7f_lin *tcritic, const float *next_state_dev, int32_t B, const td7f_noise *noise,
+                uint16_t *tgt_img_dev, float *qt_dev, void *stream);
+/* fixed_zs = fixed_encoder.zs(state), fixed_zsa = fixed_encoder.zsa(fixed_zs,
+ * action) (TD7_multi_agent.py:248-249) -> fp32 [B][zs_dim] each. */
+int td7f_fixed(int32_t prec, const int32_t *act, const td7f_lin *fenc, const float *state_dev,
+               const float *action_dev, int32_t B, float *zs_dev, float *zsa_dev, void *stream);
+
+/* The gradient passes (csrc/td7_fused_train.hip).  Each leaves, per trained
+ * layer, the transposed 16-bit operands of its weight gradient -- the layer
+ * input X^T [round_up(n_in, 64)][ld] and dP^T = (dY act'(Y))^T [round_up(n_out,
+ * 64)][ld] (x 1024 at fp16), ld = the batch padded to 32, rows past the valid
+ * ones zero -- and fp32 column sums of dP per 16-row tile (part
+ * [ceil(B/16)][n_out]); td7f_wgrad turns them into dW and db. */
+typedef struct {
+    void *x;
+    void *dp;
+    float *part;
+} td7f_xt;
+/* Critic update (TD7_multi_agent.py:241-262): Q_target from the target heads
+ * qt_dev [B][2] (clamp to [*lo, *hi], running bounds *run_max / *run_min
+ * updated), both heads of the critic on [s, a] and [q | zsa | zs], |Q - Q_target|
+ * -> td_dev [B][2] (the LAP priorities), the LAP-Huber gradient and the dX
+ * chain of every layer.  critic: [layer][head] (8), with dX operands.  q_dev
+ * (may be NULL): the Q values; y1/y2: [2][B][hdim] fp32 scratch.  xt: [layer][head]. */
+int td7f_critic(int32_t prec, const int32_t *act, const td7f_lin *critic, const float *s_dev, const float *a_dev,
+                const float *zs_dev, const float *zsa_dev, const float *qt_dev, const float *reward_dev,
+                const float *not_done_dev, float discount, const float *lo_dev, const float *hi_dev,
+                float *run_max_dev, float *run_min_dev, int32_t B, int32_t state_dim, int32_t action_dim,
+                float *td_dev, float *q_dev, float *y1_dev, float *y2_dev, const td7f_xt *xt, int64_t ld,
+                void *stream);
+/* Encoder update (TD7_multi_agent.py:219-228): zs(s') (no grad), zs(s),
+ * zsa(zs, a), d mse / d pred and the dX chain of all six layers.  y: four
+ * [B][enc_hdim] fp32 scratch buffers (zs1, zs2, zsa1, zsa2 activations). */
+int td7f_encoder(int32_t prec, const int32_t *act, const td7f_lin *enc, const float *s_dev, const float *a_dev,
+                 const float *ns_dev, int32_t B, float *const *y, const td7f_xt *xt, int64_t ld, void *stream);
+/* Actor update (TD7_multi_agent.py:266-277) in three launches: phase 0 actor(s,
+ * fixed_zs) and fixed_encoder.zsa of it; phase 1 the (updated) critic on them and
+ * d(-mean Q) back to the action and zsa inputs per head; phase 2 the fixed zsa
+ * backward to the action, tanh' and the actor's dX chain (xt: the 4 actor layers). */
+typedef struct {
+    float *act_out;  /* [B][A] */
+    float *zsa_out;  /* [B][zs_dim] */
+    float *h0;       /* [B][actor_hdim] pre-norm l0 output */
+    float *mean0;    /* [B] */
+    float *ya[2];    /* actor l1 / l2 activations [B][actor_hdim] */
+    float *yz[2];    /* fixed zsa1 / zsa2 activations [B][enc_hdim] */
+    float *yc[2];    /* critic l1 / l2 activations [2][B][critic_hdim] */
+    float *da;       /* [2][B][A] */
+    float *dzsa;     /* [2][B][zs_dim] */
+} td7f_actor_bufs;
+int td7f_actor(int32_t prec, int32_t phase, const int32_t *act, const td7f_lin *actor, const td7f_lin *fenc,
+               const td7f_lin *critic, const float *s_dev, const float *zs_dev, int32_t B,
+               const td7f_actor_bufs *bufs, const td7f_xt *xt, int64_t ld, void *stream);
+/* dW = dP^T X / gs -> dw [n][k] (fp32, row stride k) and db = the column
+ * partials summed over row_tiles (when db is not NULL), for njobs layers in one
+ * launch; rows = the reduction length (multiple of 32).  prio_dev not NULL:
+ * also the LAP priorities max(td0, td1, min_priority)^alpha (TD7_multi_agent.py:262). */
+#define TD7F_MAX_WG 16
+typedef struct {
+    const void *dp;
+    const void *x;
+    const float *part;
+    float *dw;
+    float *db;
+    int32_t n, k, row_tiles;
+} td7f_wg_job;
+int td7f_wgrad(int32_t prec, int32_t njobs, const td7f_wg_job *jobs, int64_t ld, int32_t rows, const float *td_dev,
+               float *prio_dev, int32_t B, float alpha, float min_priority, void *stream);
+
 #ifdef __cplusplus
 }
 #endif
