@@ -29,6 +29,19 @@ typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
+// Global-memory accesses through address-space-1 pointers: pointers read from
+// the argument structs are generic, and a generic access compiles to a FLAT
+// instruction, which counts against the LDS counter too -- every LDS wait would
+// then also wait for every weight load in flight.
+template <typename T>
+__device__ __forceinline__ T ldg(const T *p) {
+    return *(const __attribute__((address_space(1))) T *)p;
+}
+template <typename T>
+__device__ __forceinline__ void stg(T *p, T v) {
+    *(__attribute__((address_space(1))) T *)p = v;
+}
+
 constexpr int NW = 4;            // waves of one k-group: output tile t goes to wave t % NW
 constexpr int NKG = 2;           // k-groups: each gemm's k-steps are split over NKG sets of NW waves
 constexpr int NTH = 64 * NW * NKG;  // threads per workgroup (2 waves per SIMD)
@@ -62,9 +75,12 @@ template <> struct Ty<PREC_F16> {
     static constexpr float gs = 1024.f;
 };
 
+// ELU's negative branch as exp(x) - 1 (v_exp_f32): within ~1e-7 of expm1f,
+// four orders below the 16-bit rounding every activation then takes; the
+// per-element epilogue cost matters here (every layer's epilogue runs it)
 __device__ __forceinline__ float act_fwd(int act, float x) {
     if (act == ACT_RELU) return x > 0.f ? x : 0.f;
-    if (act == ACT_ELU) return x > 0.f ? x : expm1f(x);
+    if (act == ACT_ELU) return x > 0.f ? x : __expf(x) - 1.0f;
     if (act == ACT_TANH) return tanhf(x);
     return x;
 }
@@ -135,7 +151,7 @@ __device__ __forceinline__ void ring_fill(u32x4 (&R)[PD][TH], const GDesc &g) {
         for (int p = 0; p < PD; ++p)
 #pragma unroll
             for (int i = 0; i < TH; ++i) {
-                R[p][i] = g.wp[((size_t)(g.t0 + w + NW * i) * g.ks + kb + p) * 64 + lane];
+                R[p][i] = ldg(g.wp + ((size_t)(g.t0 + w + NW * i) * g.ks + kb + p) * 64 + lane);
                 __builtin_amdgcn_sched_barrier(0);
             }
     }
@@ -164,7 +180,7 @@ __device__ __forceinline__ void epi_prefetch(const EpiSrc &e, int t0, floatx4 (&
         for (int r = 0; r < RT; ++r) {
             const int row = (threadIdx.x & 15) + TR * r;
             const bool ok = e.p && mine && col >= 0 && col < e.ncols && (e.ld == 0 || e.row0 + row < e.nrows);
-            ep[r][i] = ok ? *(const floatx4 *)(e.p + (e.ld ? (long)(e.row0 + row) * e.ld : 0) + col)
+            ep[r][i] = ok ? ldg((const floatx4 *)(e.p + (e.ld ? (long)(e.row0 + row) * e.ld : 0) + col))
                           : floatx4{0.f, 0.f, 0.f, 0.f};
         }
     }
@@ -211,7 +227,7 @@ __device__ __forceinline__ void gemm(char *lds, int a_off, int lda, const GDesc 
                 }
 #pragma unroll
                 for (int i = 0; i < TH; ++i) {
-                    R[p][i] = bp[i][(s + PD) * 64];
+                    R[p][i] = ldg(bp[i] + (s + PD) * 64);
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
@@ -238,7 +254,7 @@ __device__ __forceinline__ void gemm(char *lds, int a_off, int lda, const GDesc 
             if (ne > nb) {
 #pragma unroll
                 for (int i = 0; i < TH; ++i) {
-                    R[p][i] = np[i][p * 64];
+                    R[p][i] = ldg(np[i] + p * 64);
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
@@ -318,7 +334,7 @@ __device__ __forceinline__ void epi_fwd(char *lds, const floatx4 (&acc)[RT][TH],
             for (int e = 0; e < 4; ++e) v[e] = act_fwd(act, acc[r][i][e] + b[e]);
             if (o16.off >= 0) *(u32x2 *)p16(lds, o16, row, col0 + n) = pack4<P>(v);
             if (o32.off >= 0) *(floatx4 *)p32(lds, o32, row, n) = floatx4{v[0], v[1], v[2], v[3]};
-            if (g && row0 + row < nrows) *(floatx4 *)(g + (long)(row0 + row) * gld + n) = floatx4{v[0], v[1], v[2], v[3]};
+            if (g && row0 + row < nrows) stg((floatx4 *)(g + (long)(row0 + row) * gld + n), floatx4{v[0], v[1], v[2], v[3]});
         }
     }
 }
@@ -361,7 +377,7 @@ __device__ __forceinline__ void epi_bwd(char *lds, const floatx4 (&acc)[RT][TH],
                     float s[4] = {v[0] * Ty<P>::gs, v[1] * Ty<P>::gs, v[2] * Ty<P>::gs, v[3] * Ty<P>::gs};
                     *(u32x2 *)p16(lds, o16, row, m) = pack4<P>(s);
                 }
-                if (g && row0 + row < nrows) *(floatx4 *)(g + (long)(row0 + row) * gld + m) = floatx4{v[0], v[1], v[2], v[3]};
+                if (g && row0 + row < nrows) stg((floatx4 *)(g + (long)(row0 + row) * gld + m), floatx4{v[0], v[1], v[2], v[3]});
             }
         }
         if (part) {
@@ -369,40 +385,51 @@ __device__ __forceinline__ void epi_bwd(char *lds, const floatx4 (&acc)[RT][TH],
             for (int e = 0; e < 4; ++e)
 #pragma unroll
                 for (int o = 1; o < 16; o <<= 1) cs[e] += __shfl_xor(cs[e], o, 64);
-            if (in && (threadIdx.x & 15) == 0) *(floatx4 *)(part + m) = floatx4{cs[0], cs[1], cs[2], cs[3]};
+            if (in && (threadIdx.x & 15) == 0) stg((floatx4 *)(part + m), floatx4{cs[0], cs[1], cs[2], cs[3]});
         }
     }
 }
 
 // Thin GEMMs on the VALU (an output width or a reduction too narrow for a
 // 16-wide MFMA tile: the N = 1 / 7 heads, the 7-wide action windows of the
-// backward): out[row][j] = sum_{k < K} X[row][k] w(j, k) for j < ncols, with
-// X the 16-bit image `in` (columns xc0 + k) and w(j, k) = W[(j0 + j) * ldw + k]
-// (trans = false) or W[k * ldw + j0 + j] (trans = true) from the fp32 master
-// weights rounded to the MFMA operand type -- the operands the per-layer
-// kernels use.  Raw sums to the fp32 LDS region out (columns 0..ncols).
-// Each (row, j) sums over kl lanes (a power of two <= 32) and reduces by shuffles.
+// backward).  stage_thin copies the ncols x K weight slice w(j, k) =
+// W[(j0 + j) * ldw + k] (trans = false) or W[k * ldw + j0 + j] (trans = true)
+// of the fp32 master weights into the LDS region wl [ncols][K], rounded to the
+// MFMA operand type (the operands the per-layer kernels use) -- at kernel start,
+// off the critical path (no barrier: the kernel's first one covers it).
 template <int P>
-__device__ __forceinline__ void thin(char *lds, R16 in, int xc0, int K, const float *W, long ldw, int j0, bool trans,
-                                     int ncols, int rows, R32 out, float scale) {
-    int kl = 1;
-    while (kl < 32 && kl < K) kl <<= 1;
-    const int items = rows * ncols;
-    for (int base = 0; base < items * kl; base += NTH) {
-        const int it = (base + (int)threadIdx.x) / kl, sl = (base + (int)threadIdx.x) % kl;
-        float acc = 0.f;
-        if (it < items) {
-            const int row = it / ncols, j = it - row * ncols;
-            for (int k = sl; k < K; k += kl) {
-                const float wv = trans ? W[(long)k * ldw + j0 + j] : W[(long)(j0 + j) * ldw + k];
-                acc += Ty<P>::val(*p16(lds, in, row, xc0 + k)) * Ty<P>::val(Ty<P>::bits(wv));
-            }
-        }
-        for (int o = kl / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-        if (it < items && sl == 0) {
-            const int row = it / ncols, j = it - row * ncols;
-            *p32(lds, out, row, j) = acc * scale;
-        }
+__device__ __forceinline__ void stage_thin(char *lds, R32 wl, const float *W, long ldw, int j0, bool trans, int ncols,
+                                           int K) {
+#pragma unroll 4
+    for (int idx = threadIdx.x; idx < ncols * K; idx += NTH) {
+        const int j = idx / K, k = idx - j * K;
+        const float w = ldg(trans ? W + (long)k * ldw + j0 + j : W + (long)(j0 + j) * ldw + k);
+        *p32(lds, wl, j, k) = Ty<P>::val(Ty<P>::bits(w));
+    }
+}
+// out[row][j] = scale * sum_{k < K} X[row][xc0 + k] wl[j][k] for j < ncols <= 16
+// (raw sums to the fp32 LDS region out), 16 rows: one pass, a thread per
+// (row, k-slice of NTH / 16), every output of the row accumulated in registers,
+// then reduced over the slices by shuffles.
+template <int P>
+__device__ __forceinline__ void thin(char *lds, R16 in, int xc0, int K, R32 wl, int ncols, R32 out, float scale) {
+    constexpr int KS = NTH / TR;
+    const int row = threadIdx.x / KS, sl = threadIdx.x % KS;
+    float acc[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+    for (int k = sl; k < K; k += KS) {
+        const float x = Ty<P>::val(*p16(lds, in, row, xc0 + k));
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+            if (j < ncols) acc[j] += x * *p32(lds, wl, j, k);
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        if (j >= ncols) break;
+#pragma unroll
+        for (int o = KS / 2; o > 0; o >>= 1) acc[j] += __shfl_xor(acc[j], o, 64);
+        if (sl == 0) *p32(lds, out, row, j) = acc[j] * scale;
     }
 }
 
@@ -418,12 +445,12 @@ __device__ __forceinline__ void make_dp(char *lds, R32 dy, int N, int act, const
         for (int r = 0; r < TR; ++r) {
             float v = *p32(lds, dy, r, n);
             if (row0 + r >= nrows) v = 0.f;
-            else if (act != ACT_NONE) v *= act_grad(act, y[(long)(row0 + r) * yld + n]);
+            else if (act != ACT_NONE) v *= act_grad(act, ldg(y + (long)(row0 + r) * yld + n));
             *p32(lds, dy, r, n) = v;
             *p16(lds, o16, r, n) = Ty<P>::bits(v * Ty<P>::gs);
             cs += v;
         }
-        if (part) part[n] = cs;
+        if (part) stg(part + n, cs);
     }
 }
 
@@ -434,9 +461,10 @@ __device__ __forceinline__ void load_rows(char *lds, R16 dst, int col0, const fl
                                           int rows, int row0, int nrows) {
     if (ncols % 4 == 0 && sld % 4 == 0 && col0 % 4 == 0) {  // 16-byte loads, 8-byte LDS stores
         const int nq = ncols / 4;
+#pragma unroll 4
         for (int k = threadIdx.x; k < rows * nq; k += NTH) {
             const int row = k / nq, c = 4 * (k - row * nq);
-            const floatx4 v = (row0 + row < nrows) ? *(const floatx4 *)(src + (long)(row0 + row) * sld + c)
+            const floatx4 v = (row0 + row < nrows) ? ldg((const floatx4 *)(src + (long)(row0 + row) * sld + c))
                                                     : floatx4{0.f, 0.f, 0.f, 0.f};
             const float f[4] = {v[0], v[1], v[2], v[3]};
             *(u32x2 *)p16(lds, dst, row, col0 + c) = pack4<P>(f);
@@ -445,7 +473,7 @@ __device__ __forceinline__ void load_rows(char *lds, R16 dst, int col0, const fl
     }
     for (int k = threadIdx.x; k < rows * ncols; k += NTH) {
         const int row = k / ncols, c = k - row * ncols;
-        const float v = (row0 + row < nrows) ? src[(long)(row0 + row) * sld + c] : 0.f;
+        const float v = (row0 + row < nrows) ? ldg(src + (long)(row0 + row) * sld + c) : 0.f;
         *p16(lds, dst, row, col0 + c) = Ty<P>::bits(v);
     }
 }
@@ -456,21 +484,21 @@ __device__ __forceinline__ void load_rows16(char *lds, R16 dst, int col0, const 
         for (int k = threadIdx.x; k < rows * nq; k += NTH) {
             const int row = k / nq, c = 8 * (k - row * nq);
             *(u32x4 *)p16(lds, dst, row, col0 + c) = (row0 + row < nrows)
-                                                          ? *(const u32x4 *)(src + (long)(row0 + row) * sld + c)
+                                                          ? ldg((const u32x4 *)(src + (long)(row0 + row) * sld + c))
                                                           : u32x4{0u, 0u, 0u, 0u};
         }
         return;
     }
     for (int k = threadIdx.x; k < rows * ncols; k += NTH) {
         const int row = k / ncols, c = k - row * ncols;
-        *p16(lds, dst, row, col0 + c) = (row0 + row < nrows) ? src[(long)(row0 + row) * sld + c] : (uint16_t)0;
+        *p16(lds, dst, row, col0 + c) = (row0 + row < nrows) ? ldg(src + (long)(row0 + row) * sld + c) : (uint16_t)0;
     }
 }
 __device__ __forceinline__ void load_rows32(char *lds, R32 dst, const float *src, long sld, int ncols, int rows,
                                             int row0, int nrows) {
     for (int k = threadIdx.x; k < rows * ncols; k += NTH) {
         const int row = k / ncols, c = k - row * ncols;
-        *p32(lds, dst, row, c) = (row0 + row < nrows) ? src[(long)(row0 + row) * sld + c] : 0.f;
+        *p32(lds, dst, row, c) = (row0 + row < nrows) ? ldg(src + (long)(row0 + row) * sld + c) : 0.f;
     }
 }
 // 16-bit LDS image rows -> global [row0+row][c] (same element type)
@@ -480,20 +508,51 @@ __device__ __forceinline__ void store_rows16(char *lds, R16 src, int col0, uint1
         const int nq = ncols / 8;
         for (int k = threadIdx.x; k < rows * nq; k += NTH) {
             const int row = k / nq, c = 8 * (k - row * nq);
-            if (row0 + row < nrows) *(u32x4 *)(dst + (long)(row0 + row) * dld + c) = *(const u32x4 *)p16(lds, src, row, col0 + c);
+            if (row0 + row < nrows) stg((u32x4 *)(dst + (long)(row0 + row) * dld + c), *(const u32x4 *)p16(lds, src, row, col0 + c));
         }
         return;
     }
     for (int k = threadIdx.x; k < rows * ncols; k += NTH) {
         const int row = k / ncols, c = k - row * ncols;
-        if (row0 + row < nrows) dst[(long)(row0 + row) * dld + c] = *p16(lds, src, row, col0 + c);
+        if (row0 + row < nrows) stg(dst + (long)(row0 + row) * dld + c, *p16(lds, src, row, col0 + c));
     }
 }
 
-// The transposed layer input for the weight gradient: X^T[c][row0 + row] (16-bit)
-// for c < ncols from the LDS image (columns col0 + c), 16 rows per thread-column.
+// The weight-gradient operands (layer inputs X^T, gradient operands dP^T) are
+// stored in MFMA-fragment blocks: operand row c (an input column of X or an
+// output column of dP), batch row r lives at
+//   ((c / 16) * (ld / 32) + r / 32) * 512 + ((c % 16) + 16 ((r % 32) / 8)) * 8 + r % 8
+// (16-bit units, ld = padded batch), so that td7f_wgrad's 16 x 32 fragment of a
+// k-step is one contiguous 1 KiB block (one full-line 16-byte load per lane).
+// blk8 -> the 8 batch rows r..r+7 (r % 8 == 0) of operand row c.
+__device__ __forceinline__ uint16_t *blk8(uint16_t *base, long ld, int c, int r) {
+    return base + ((long)(c >> 4) * (ld >> 5) + (r >> 5)) * 512 + ((c & 15) + 16 * ((r & 31) >> 3)) * 8;
+}
+
+// The layer input for the weight gradient from the LDS image (columns col0 + c,
+// c < ncols), 16 rows per call (row0 % 16 == 0), in the blocked layout above.
 __device__ __forceinline__ void save_xt(char *lds, R16 src, int col0, int ncols, uint16_t *xt, long ld, int rows,
                                         int row0) {
+    if (col0 % 2 == 0 && src.ld % 2 == 0) {  // column pairs: 32-bit LDS reads
+        for (int k = threadIdx.x; k < ((ncols + 1) / 2) * (rows / TR); k += NTH) {
+            const int c = 2 * (k % ((ncols + 1) / 2)), rb = (k / ((ncols + 1) / 2)) * TR;
+            uint32_t lo[8], hi[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t r0 = *(const uint32_t *)p16(lds, src, rb + 2 * j, col0 + c);
+                const uint32_t r1 = *(const uint32_t *)p16(lds, src, rb + 2 * j + 1, col0 + c);
+                lo[j] = (r0 & 0xffffu) | (r1 << 16);
+                hi[j] = (r0 >> 16) | (r1 & 0xffff0000u);
+            }
+            stg((u32x4 *)blk8(xt, ld, c, row0 + rb), u32x4{lo[0], lo[1], lo[2], lo[3]});
+            stg((u32x4 *)blk8(xt, ld, c, row0 + rb + 8), u32x4{lo[4], lo[5], lo[6], lo[7]});
+            if (c + 1 < ncols) {
+                stg((u32x4 *)blk8(xt, ld, c + 1, row0 + rb), u32x4{hi[0], hi[1], hi[2], hi[3]});
+                stg((u32x4 *)blk8(xt, ld, c + 1, row0 + rb + 8), u32x4{hi[4], hi[5], hi[6], hi[7]});
+            }
+        }
+        return;
+    }
     for (int k = threadIdx.x; k < ncols * (rows / TR); k += NTH) {
         const int c = k % ncols, rb = (k / ncols) * TR;
         uint32_t v[8];
@@ -501,9 +560,8 @@ __device__ __forceinline__ void save_xt(char *lds, R16 src, int col0, int ncols,
         for (int j = 0; j < 8; ++j)
             v[j] = (uint32_t)*p16(lds, src, rb + 2 * j, col0 + c) |
                    ((uint32_t)*p16(lds, src, rb + 2 * j + 1, col0 + c) << 16);
-        u32x4 *d = (u32x4 *)(xt + (long)c * ld + row0 + rb);
-        d[0] = u32x4{v[0], v[1], v[2], v[3]};
-        d[1] = u32x4{v[4], v[5], v[6], v[7]};
+        stg((u32x4 *)blk8(xt, ld, c, row0 + rb), u32x4{v[0], v[1], v[2], v[3]});
+        stg((u32x4 *)blk8(xt, ld, c, row0 + rb + 8), u32x4{v[4], v[5], v[6], v[7]});
     }
 }
 
@@ -528,11 +586,11 @@ __device__ __forceinline__ void norm_fwd(char *lds, R32 h, int N, int rows, floa
         if (o16.off >= 0) *p16(lds, o16, row, col0 + n) = b;
         if (o16b.off >= 0) *p16(lds, o16b, row, col0b + n) = b;
         if (o32.off >= 0) *p32(lds, o32, row, n) = v;
-        if (g && row0 + row < nrows) g[(long)(row0 + row) * gld + n] = v;
+        if (g && row0 + row < nrows) stg(g + (long)(row0 + row) * gld + n, v);
     }
     if (j0 == 0) {
         if (mean_lds) mean_lds[row] = m;
-        if (gmean && row0 + row < nrows) gmean[row0 + row] = m;
+        if (gmean && row0 + row < nrows) stg(gmean + row0 + row, m);
     }
 }
 
@@ -575,11 +633,10 @@ __device__ __forceinline__ void norm_bwd(char *lds, R32 dy, R32 h, const float *
             else v[r >> 1] = hb;
         }
         if (dpt) {
-            u32x4 *d = (u32x4 *)(dpt + (long)n * dpt_ld + row0);
-            d[0] = u32x4{v[0], v[1], v[2], v[3]};
-            d[1] = u32x4{v[4], v[5], v[6], v[7]};
+            stg((u32x4 *)blk8(dpt, dpt_ld, n, row0), u32x4{v[0], v[1], v[2], v[3]});
+            stg((u32x4 *)blk8(dpt, dpt_ld, n, row0 + 8), u32x4{v[4], v[5], v[6], v[7]});
         }
-        if (part) part[n] = csum;
+        if (part) stg(part + n, csum);
     }
 }
 
@@ -612,7 +669,7 @@ static __device__ unsigned long long *g_td7f_stamps;  // per translation unit
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                \
         __builtin_amdgcn_sched_barrier(0);                                                         \
         if (g_td7f_stamps && threadIdx.x == 0 && (si) < 64)                                        \
-            g_td7f_stamps[(size_t)(blockIdx.x + blockIdx.y * gridDim.x) * 64 + (si)] = _t;         \
+            stg(g_td7f_stamps + (size_t)(blockIdx.x + blockIdx.y * gridDim.x) * 64 + (si), _t);    \
         ++(si);                                                                                    \
     } while (0)
 #else
@@ -650,16 +707,16 @@ __device__ __forceinline__ void layer_fwd(char *lds, u32x4 (&R)[PD][TH], R16 a, 
 // A thin forward Linear (N <= 16) on the VALU: out[row][n] = act(x W^T + b) in
 // the fp32 region `out` (and global g when not null).  Ends with a barrier.
 template <int P>
-__device__ __forceinline__ void layer_thin_fwd(char *lds, R16 a, const Lin &L, int act, R32 out, int rows, float *g,
-                                               long gld, int row0, int nrows, int &si) {
+__device__ __forceinline__ void layer_thin_fwd(char *lds, R16 a, const Lin &L, R32 wl, int act, R32 out, int rows,
+                                               float *g, long gld, int row0, int nrows, int &si) {
     FSTAMP(si);
-    thin<P>(lds, a, 0, L.K, L.w, L.ldw, 0, false, L.N, rows, out, 1.f);
+    thin<P>(lds, a, 0, L.K, wl, L.N, out, 1.f);
     __syncthreads();
     for (int k = threadIdx.x; k < rows * L.N; k += NTH) {
         const int row = k / L.N, n = k - row * L.N;
-        const float v = act_fwd(act, *p32(lds, out, row, n) + L.b[n]);
+        const float v = act_fwd(act, *p32(lds, out, row, n) + ldg(L.b + n));
         *p32(lds, out, row, n) = v;
-        if (g && row0 + row < nrows) g[(long)(row0 + row) * gld + n] = v;
+        if (g && row0 + row < nrows) stg(g + (long)(row0 + row) * gld + n, v);
     }
     __syncthreads();
 }
@@ -675,8 +732,8 @@ __device__ __forceinline__ void zero_lds(char *lds, int bytes) {
 template <int P>
 __device__ __forceinline__ void noise_rows(char *lds, R32 a, int A, int rows, int row0, int nrows, const Noise &nz,
                                            float *out, R16 o1, int c1, R16 o2, int c2) {
-    const float sg = *nz.sigma;
-    const unsigned long long call = *nz.counter;
+    const float sg = ldg(nz.sigma);
+    const unsigned long long call = ldg(nz.counter);
     for (int k = threadIdx.x; k < rows * A; k += NTH) {
         const int row = k / A, c = k - row * A;
         float v = 0.f;
@@ -684,7 +741,7 @@ __device__ __forceinline__ void noise_rows(char *lds, R32 a, int A, int rows, in
             const uint32_t i = (uint32_t)((row0 + row) * A + c);
             float z;
             if (nz.z) {
-                z = nz.z[i];
+                z = ldg(nz.z + i);
             } else {
                 uint32_t r[4];
                 philox_block(nz.seed, nz.tag, call, i >> 1, r);
@@ -695,7 +752,7 @@ __device__ __forceinline__ void noise_rows(char *lds, R32 a, int A, int rows, in
             float e = z * sg;
             if (nz.clip > 0.f) e = fminf(fmaxf(e, -nz.clip), nz.clip);
             v = fminf(fmaxf(*p32(lds, a, row, c) + e, -1.0f), 1.0f) * nz.scale;
-            if (out) out[i] = v;
+            if (out) stg(out + i, v);
         }
         const uint16_t b = Ty<P>::bits(v);
         if (o1.off >= 0) *p16(lds, o1, row, c1 + c) = b;

@@ -85,7 +85,7 @@ struct SelectArgs {
     float *out;
     Noise nz;
     R16 X, H1, H2, CAT;
-    R32 F;
+    R32 F, TW;
     int lds_bytes;
 };
 
@@ -103,6 +103,7 @@ __global__ __launch_bounds__(NTH) void select_kernel(SelectArgs a) {
     zero_lds(lds, a.lds_bytes);
     __syncthreads();
     load_rows<P>(lds, a.X, 0, a.obs, a.S, a.S, rows, row0, a.n);
+    stage_thin<P>(lds, a.TW, a.ac[3].w, a.ac[3].ldw, 0, false, a.A, a.ac[3].K);
     RING_START(a.zs[0]);
     __syncthreads();
     // zs = fixed_encoder.zs(obs) (:93-97) -> CAT[:, Ha:Ha+Z]
@@ -117,7 +118,7 @@ __global__ __launch_bounds__(NTH) void select_kernel(SelectArgs a) {
     __syncthreads();
     layer_fwd<P, RT, TH>(lds, R, a.CAT, a.ac[1], &a.ac[2], a.act_actor, a.H1, 0, NO32, nullptr, 0, row0, a.n, si);
     layer_fwd<P, RT, TH>(lds, R, a.H1, a.ac[2], (const Lin *)nullptr, a.act_actor, a.H2, 0, NO32, nullptr, 0, row0, a.n, si);
-    layer_thin_fwd<P>(lds, a.H2, a.ac[3], ACT_TANH, a.F, rows, nullptr, 0, row0, a.n, si);
+    layer_thin_fwd<P>(lds, a.H2, a.ac[3], a.TW, ACT_TANH, a.F, rows, nullptr, 0, row0, a.n, si);
     noise_rows<P>(lds, a.F, a.A, rows, row0, a.n, a.nz, a.out, NO16, 0, NO16, 0);
 }
 
@@ -131,7 +132,7 @@ struct TargetArgs {
     uint16_t *img;  // [B][2Z + A]: zsa | zs | next_action
     float *qt;      // [B][2]
     R16 X, H1, H2, CATA, CATZ, OUT, CAT;
-    R32 F;
+    R32 F, TW;
     int lds_a, lds_b;
 };
 
@@ -145,6 +146,7 @@ __global__ __launch_bounds__(NTH) void target_a_kernel(TargetArgs a) {
     zero_lds(lds, a.lds_a);
     __syncthreads();
     load_rows<P>(lds, a.X, 0, a.ns, a.S, a.S, rows, row0, B);
+    stage_thin<P>(lds, a.TW, a.ac[3].w, a.ac[3].ldw, 0, false, a.A, a.ac[3].K);
     RING_START(a.enc[0]);
     __syncthreads();
     // fixed_target_zs = fixed_encoder_target.zs(next_state) (:234)
@@ -159,7 +161,7 @@ __global__ __launch_bounds__(NTH) void target_a_kernel(TargetArgs a) {
     __syncthreads();
     layer_fwd<P, RT, TH>(lds, R, a.CATA, a.ac[1], &a.ac[2], a.act_actor, a.H1, 0, NO32, nullptr, 0, row0, B, si);
     layer_fwd<P, RT, TH>(lds, R, a.H1, a.ac[2], &a.enc[3], a.act_actor, a.H2, 0, NO32, nullptr, 0, row0, B, si);
-    layer_thin_fwd<P>(lds, a.H2, a.ac[3], ACT_TANH, a.F, rows, nullptr, 0, row0, B, si);
+    layer_thin_fwd<P>(lds, a.H2, a.ac[3], a.TW, ACT_TANH, a.F, rows, nullptr, 0, row0, B, si);
     noise_rows<P>(lds, a.F, a.A, rows, row0, B, a.nz, nullptr, a.CATZ, Z, a.OUT, 2 * Z);
     __syncthreads();
     // fixed_target_zsa = fixed_encoder_target.zsa(zs, next_action) (:240) -> OUT[:, 0:Z]
@@ -189,6 +191,7 @@ __global__ __launch_bounds__(NTH) void target_b_kernel(TargetArgs a) {
     load_rows<P>(lds, a.X, 0, a.ns, a.S, a.S, rows, row0, B);
     load_rows16(lds, a.X, a.S, a.img + 2 * Z, ild, a.A, rows, row0, B);
     load_rows16(lds, a.CAT, a.Hc, a.img, ild, 2 * Z, rows, row0, B);
+    stage_thin<P>(lds, a.TW, cr[6].w, cr[6].ldw, 0, false, 1, cr[6].K);
     RING_START(cr[0]);
     __syncthreads();
     // critic_target(s', a', zsa, zs) head h (:109-140): AvgL1Norm(q0(sa)) | zsa | zs -> q1 -> q2 -> q3
@@ -197,7 +200,7 @@ __global__ __launch_bounds__(NTH) void target_b_kernel(TargetArgs a) {
     __syncthreads();
     layer_fwd<P, RT, TH>(lds, R, a.CAT, cr[2], &cr[4], a.act_critic, a.H1, 0, NO32, nullptr, 0, row0, B, si);
     layer_fwd<P, RT, TH>(lds, R, a.H1, cr[4], (const Lin *)nullptr, a.act_critic, a.H2, 0, NO32, nullptr, 0, row0, B, si);
-    layer_thin_fwd<P>(lds, a.H2, cr[6], ACT_NONE, a.F, rows, a.qt + h, 2, row0, B, si);
+    layer_thin_fwd<P>(lds, a.H2, cr[6], a.TW, ACT_NONE, a.F, rows, a.qt + h, 2, row0, B, si);
 }
 
 // ---------------------------------------------------------------- fixed embeddings
@@ -299,6 +302,7 @@ int td7f_select(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7
     a.H2 = b.r16(rows, ld16(hmax));
     a.CAT = b.r16(rows, ld16(a.Ha + a.Z));
     a.F = b.r32(rows, std::max(std::max(a.Z, a.Ha), 16));
+    a.TW = b.r32(a.A, actor[3].n_in);
     a.lds_bytes = b.off;
     return DISPATCH(prec, th, select_kernel, dim3((n + rows - 1) / rows), b.off, a, (hipStream_t)stream);
 }
@@ -347,11 +351,13 @@ int td7f_target(int32_t prec, const int32_t *act, const td7f_lin *tenc, const td
     a.CATZ = ba.r16(rows, ld16(a.Z + a.A));
     a.OUT = ba.r16(rows, round_up(2 * a.Z + a.A, 8));  // == the image row (16-byte stores)
     a.F = ba.r32(rows, std::max(hmax, 16));
+    a.TW = ba.r32(a.A, tactor[3].n_in);
     a.lds_a = ba.off;
     Bump bb(1);
     const R16 Xb = bb.r16(rows, ld16(a.S + a.A)), H1b = bb.r16(rows, ld16(hmax)), H2b = bb.r16(rows, ld16(hmax));
     const R16 CATb = bb.r16(rows, ld16(a.Hc + 2 * a.Z));
     const R32 Fb = bb.r32(rows, std::max(hmax, 16));
+    const R32 TWb = bb.r32(1, tcritic[6].n_in);
     a.lds_b = bb.off;
     const hipStream_t st = (hipStream_t)stream;
     int rc = DISPATCH(prec, th, target_a_kernel, dim3((B + rows - 1) / rows), ba.off, a, st);
@@ -362,6 +368,7 @@ int td7f_target(int32_t prec, const int32_t *act, const td7f_lin *tenc, const td
     b2.H2 = H2b;
     b2.CAT = CATb;
     b2.F = Fb;
+    b2.TW = TWb;
     return DISPATCH(prec, th, target_b_kernel, dim3((B + rows - 1) / rows, 2), bb.off, b2, st);
 }
 

@@ -76,7 +76,7 @@ struct CriticArgs {
     XT xt[8];          // [layer][head]
     long ld;           // row stride of the transposed operands
     R16 X, CAT, H1, H2, DP0, DP1;
-    R32 H0, DY, F;
+    R32 H0, DY, F, TW;
     int small_off;     // 2 x 16 floats: row means, row dots
     int lds_bytes;
 };
@@ -97,6 +97,7 @@ __global__ __launch_bounds__(NTH) void critic_kernel(CriticArgs a) {
     load_rows<P>(lds, a.X, a.S, a.a, a.A, a.A, TR, row0, B);
     load_rows<P>(lds, a.CAT, Hc, a.zsa, Z, Z, TR, row0, B);
     load_rows<P>(lds, a.CAT, Hc + Z, a.zs, Z, Z, TR, row0, B);
+    stage_thin<P>(lds, a.TW, cr[6].w, cr[6].ldw, 0, false, 1, cr[6].K);
     u32x4 R[PD][TH];
     ring_fill(R, fwd_of(cr[0]));
     __syncthreads();
@@ -111,16 +112,16 @@ __global__ __launch_bounds__(NTH) void critic_kernel(CriticArgs a) {
     layer_fwd<P, 1, TH>(lds, R, a.H1, cr[4], &b3, a.act, a.H2, 0, NO32, y2, Hc, row0, B, si);
     save_xt(lds, a.H1, 0, Hc, xt[4].x, a.ld, TR, row0);
     save_xt(lds, a.H2, 0, Hc, xt[6].x, a.ld, TR, row0);
-    layer_thin_fwd<P>(lds, a.H2, cr[6], ACT_NONE, a.F, TR, nullptr, 0, row0, B, si);
+    layer_thin_fwd<P>(lds, a.H2, cr[6], a.TW, ACT_NONE, a.F, TR, nullptr, 0, row0, B, si);
     // Q_target (:241-246) and the LAP-Huber gradient (:257-259) of this head
     if (threadIdx.x < TR) {
         const int r = threadIdx.x, b = row0 + r;
         float dq = 0.f;
         if (b < B) {
             const float qv = *p32(lds, a.F, r, 0);
-            const float qm = fminf(a.qt[2 * b], a.qt[2 * b + 1]);
-            const float c = fminf(fmaxf(qm, *a.lo), *a.hi);
-            const float t = a.reward[b] + (a.not_done[b] * a.discount) * c;
+            const float qm = fminf(ldg(a.qt + 2 * b), ldg(a.qt + 2 * b + 1));
+            const float c = fminf(fmaxf(qm, ldg(a.lo)), ldg(a.hi));
+            const float t = ldg(a.reward + b) + (ldg(a.not_done + b) * a.discount) * c;
             if (h == 0) {
                 atomic_max_f(a.run_max, t);
                 atomic_min_f(a.run_min, t);
@@ -128,8 +129,8 @@ __global__ __launch_bounds__(NTH) void critic_kernel(CriticArgs a) {
             const float d = qv - t, x = fabsf(d);
             const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
             dq = a.inv_b * (x < 1.0f ? x : 1.0f) * sg;
-            a.td[2 * b + h] = x;
-            if (a.q) a.q[2 * b + h] = qv;
+            stg(a.td + 2 * b + h, x);
+            if (a.q) stg(a.q + 2 * b + h, qv);
         }
         *p32(lds, a.F, r, 0) = dq;
     }
@@ -257,7 +258,7 @@ struct ActorArgs {
     XT xt[4];                  // actor layers
     long ld;
     R16 X, CATA, CATZ, CAT, H1, H2, DP0, DP1;
-    R32 H0, DY, F;
+    R32 H0, DY, F, TW, TW2;
     int small_off;
     int lds;
 };
@@ -273,6 +274,7 @@ __global__ __launch_bounds__(NTH) void actor_a_kernel(ActorArgs a) {
     load_rows<P>(lds, a.X, 0, a.s, a.S, a.S, TR, row0, B);
     load_rows<P>(lds, a.CATA, Ha, a.zs, Z, Z, TR, row0, B);
     load_rows<P>(lds, a.CATZ, 0, a.zs, Z, Z, TR, row0, B);
+    stage_thin<P>(lds, a.TW, a.ac[3].w, a.ac[3].ldw, 0, false, a.A, a.ac[3].K);
     u32x4 R[PD][TH];
     ring_fill(R, fwd_of(a.ac[0]));
     __syncthreads();
@@ -286,7 +288,7 @@ __global__ __launch_bounds__(NTH) void actor_a_kernel(ActorArgs a) {
     layer_fwd<P, 1, TH>(lds, R, a.H1, a.ac[2], &a.fe[3], a.act_actor, a.H2, 0, NO32, a.ya[1], Ha, row0, B, si);
     save_xt(lds, a.H1, 0, Ha, a.xt[2].x, ld, TR, row0);
     save_xt(lds, a.H2, 0, Ha, a.xt[3].x, ld, TR, row0);
-    layer_thin_fwd<P>(lds, a.H2, a.ac[3], ACT_TANH, a.F, TR, a.act_out, a.A, row0, B, si);
+    layer_thin_fwd<P>(lds, a.H2, a.ac[3], a.TW, ACT_TANH, a.F, TR, a.act_out, a.A, row0, B, si);
     for (int k = threadIdx.x; k < TR * a.A; k += NTH) {
         const int r = k / a.A, c = k - r * a.A;
         *p16(lds, a.CATZ, r, Z + c) = Ty<P>::bits(*p32(lds, a.F, r, c));
@@ -306,12 +308,14 @@ __global__ __launch_bounds__(NTH) void actor_b_kernel(ActorArgs a) {
     float *mean = (float *)(lds + a.small_off), *dot = mean + TR;
     float *y1 = a.yc[0] + (long)h * B * Hc, *y2 = a.yc[1] + (long)h * B * Hc;
     int si = 0;
+    FSTAMP(si);
     zero_lds(lds, a.lds);
     __syncthreads();
     load_rows<P>(lds, a.X, 0, a.s, a.S, a.S, TR, row0, B);
     load_rows<P>(lds, a.X, a.S, a.act_out, a.A, a.A, TR, row0, B);
     load_rows<P>(lds, a.CAT, Hc, a.zsa_out, Z, Z, TR, row0, B);
     load_rows<P>(lds, a.CAT, Hc + Z, a.zs, Z, Z, TR, row0, B);
+    stage_thin<P>(lds, a.TW, cr[0].w, cr[0].ldw, a.S, true, a.A, Hc);
     u32x4 R[PD][TH];
     ring_fill(R, fwd_of(cr[0]));
     __syncthreads();
@@ -340,13 +344,16 @@ __global__ __launch_bounds__(NTH) void actor_b_kernel(ActorArgs a) {
     // the q columns -> AvgL1Norm backward -> q0's dP -> its action columns (thin)
     layer_bwd<P, TH>(lds, R, a.DP1, cr[2], 0, Hc, nullptr, ACT_NONE, nullptr, 0, a.DY, nullptr, 0, NO16, nullptr,
                      row0, B, si);
+    FSTAMP(si);
     norm_bwd<P>(lds, a.DY, a.H0, mean, Hc, 1e-8f, dot, a.DP0, nullptr, 0, nullptr, row0, B);
     __syncthreads();
-    thin<P>(lds, a.DP0, 0, Hc, cr[0].w, cr[0].ldw, a.S, true, a.A, TR, a.F, 1.f / Ty<P>::gs);
+    FSTAMP(si);
+    thin<P>(lds, a.DP0, 0, Hc, a.TW, a.A, a.F, 1.f / Ty<P>::gs);
     __syncthreads();
+    FSTAMP(si);
     for (int k = threadIdx.x; k < TR * a.A; k += NTH) {
         const int r = k / a.A, c = k - r * a.A;
-        if (row0 + r < B) a.da[((long)h * B + row0 + r) * a.A + c] = *p32(lds, a.F, r, c);
+        if (row0 + r < B) stg(a.da + ((long)h * B + row0 + r) * a.A + c, *p32(lds, a.F, r, c));
     }
 }
 
@@ -357,16 +364,19 @@ __global__ __launch_bounds__(NTH) void actor_c_kernel(ActorArgs a) {
     const long ld = a.ld;
     float *mean = (float *)(lds + a.small_off), *dot = mean + TR;
     int si = 0;
+    FSTAMP(si);
     zero_lds(lds, a.lds);
     __syncthreads();
     // d zsa = sum over the heads -> the fixed encoder's zsa3 dP (no activation)
+#pragma unroll 4
     for (int k = threadIdx.x; k < TR * Z; k += NTH) {
         const int r = k / Z, c = k - r * Z, b = row0 + r;
-        const float v = b < B ? a.dzsa[(long)b * Z + c] + a.dzsa[((long)B + b) * Z + c] : 0.f;
+        const float v = b < B ? ldg(a.dzsa + (long)b * Z + c) + ldg(a.dzsa + ((long)B + b) * Z + c) : 0.f;
         *p16(lds, a.DP0, r, c) = Ty<P>::bits(v * Ty<P>::gs);
     }
-    if (threadIdx.x < TR) mean[threadIdx.x] = row0 + (int)threadIdx.x < B ? a.mean0[row0 + threadIdx.x] : 0.f;
+    if (threadIdx.x < TR) mean[threadIdx.x] = row0 + (int)threadIdx.x < B ? ldg(a.mean0 + row0 + threadIdx.x) : 0.f;
     load_rows32(lds, a.H0, a.h0, Ha, Ha, TR, row0, B);
+    stage_thin<P>(lds, a.TW, a.fe[3].w, a.fe[3].ldw, Z, true, A, He);
     u32x4 R[PD][TH];
     ring_fill(R, bwd_of(a.fe[5], 0));
     __syncthreads();
@@ -377,14 +387,16 @@ __global__ __launch_bounds__(NTH) void actor_c_kernel(ActorArgs a) {
     layer_bwd<P, TH>(lds, R, a.DP1, a.fe[4], 0, He, &nx11, a.act_enc, a.yz[0], He, NO32, nullptr, 0, a.DP0, nullptr,
                      row0, B, si);
     // the action columns of zsa1's input (thin), + both critic heads' d action, x tanh'
-    thin<P>(lds, a.DP0, 0, He, a.fe[3].w, a.fe[3].ldw, Z, true, A, TR, a.F, 1.f / Ty<P>::gs);
+    FSTAMP(si);
+    thin<P>(lds, a.DP0, 0, He, a.TW, A, a.F, 1.f / Ty<P>::gs);
     __syncthreads();
+    FSTAMP(si);
     for (int k = threadIdx.x; k < TR * A; k += NTH) {
         const int r = k / A, c = k - r * A, b = row0 + r;
         float v = 0.f;
         if (b < B) {
-            const float y = a.act_out[(long)b * A + c];
-            v = (*p32(lds, a.F, r, c) + a.da[(long)b * A + c] + a.da[((long)B + b) * A + c]) * (1.f - y * y);
+            const float y = ldg(a.act_out + (long)b * A + c);
+            v = (*p32(lds, a.F, r, c) + ldg(a.da + (long)b * A + c) + ldg(a.da + ((long)B + b) * A + c)) * (1.f - y * y);
         }
         *p32(lds, a.F, r, c) = v;
     }
@@ -402,8 +414,11 @@ __global__ __launch_bounds__(NTH) void actor_c_kernel(ActorArgs a) {
     save_xt(lds, a.DP1, 0, Ha, a.xt[1].dp, ld, TR, row0);
     layer_bwd<P, TH>(lds, R, a.DP1, a.ac[1], 0, Ha, nullptr, ACT_NONE, nullptr, 0, a.DY, nullptr, 0, NO16, nullptr,
                      row0, B, si);
+    FSTAMP(si);
     norm_bwd<P>(lds, a.DY, a.H0, mean, Ha, 1e-8f, dot, a.DP0, a.xt[0].dp, ld, a.xt[0].part + (long)tile * Ha, row0,
                 B);
+    __syncthreads();
+    FSTAMP(si);
 }
 
 // ---------------------------------------------------------------- weight gradients
@@ -432,13 +447,13 @@ struct WgArgs {
     WgJob j[TD7F_MAX_WG];
 };
 
-constexpr int PD2 = 4;
+constexpr int PD2 = 8;  // k-steps (32 rows) in flight; the reduction length is a multiple of 32 PD2
 
 template <int P>
 __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs a) {
     if ((int)blockIdx.x == a.total) {
         for (int b = threadIdx.x; b < a.B; b += 256)
-            a.prio[b] = powf(fmaxf(fmaxf(a.td[2 * b], a.td[2 * b + 1]), a.minp), a.alpha);
+            stg(a.prio + b, powf(fmaxf(fmaxf(ldg(a.td + 2 * b), ldg(a.td + 2 * b + 1)), a.minp), a.alpha));
         return;
     }
     int q = 0;
@@ -449,47 +464,56 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs a) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wn = n0 + 32 * (w >> 1), wk = k0 + 32 * (w & 1);
     const long ld = a.ld;
-    // fragment rows (n for A, k for B) of the 2 sub-tiles; the operands are
-    // padded to multiples of 64 rows (zeros), so every load is in range
+    // the operands are in fragment blocks (td7_fused.h blk8): the 16 x 32
+    // fragment of operand rows g*16.. and k-step s is the 1 KiB block g * (ld/32) + s;
+    // they are padded to multiples of 64 rows (zeros), so every load is in range
     const uint16_t *ap[2], *bp[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-        ap[u] = J.dp + (long)(wn + 16 * u + (lane & 15)) * ld + 8 * (lane >> 4);
-        bp[u] = J.x + (long)(wk + 16 * u + (lane & 15)) * ld + 8 * (lane >> 4);
+        ap[u] = J.dp + (long)((wn + 16 * u) >> 4) * (ld >> 5) * 512 + lane * 8;
+        bp[u] = J.x + (long)((wk + 16 * u) >> 4) * (ld >> 5) * 512 + lane * 8;
     }
     floatx4 acc[2][2];
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int v = 0; v < 2; ++v) acc[u][v] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // rows is a multiple of 32 PD2 (the host pads the operands with zero columns):
+    // PD2 k-steps of loads in flight, issue order pinned as in gemm
     const int ns = a.rows / 32;
     u32x4 fa[PD2][2], fb[PD2][2];
 #pragma unroll
     for (int p = 0; p < PD2; ++p)
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            fa[p][u] = p < ns ? *(const u32x4 *)(ap[u] + 32 * p) : u32x4{0u, 0u, 0u, 0u};
-            fb[p][u] = p < ns ? *(const u32x4 *)(bp[u] + 32 * p) : u32x4{0u, 0u, 0u, 0u};
+            fa[p][u] = ldg((const u32x4 *)(ap[u] + 512 * p));
+            fb[p][u] = ldg((const u32x4 *)(bp[u] + 512 * p));
+            __builtin_amdgcn_sched_barrier(0);
         }
-    for (int s0 = 0; s0 < ns; s0 += PD2) {
+    int s0 = 0;
+    for (; s0 + PD2 < ns; s0 += PD2) {
 #pragma unroll
         for (int p = 0; p < PD2; ++p) {
             const int s = s0 + p;
-            if (s < ns) {
 #pragma unroll
-                for (int u = 0; u < 2; ++u)
+            for (int u = 0; u < 2; ++u)
 #pragma unroll
-                    for (int v = 0; v < 2; ++v) acc[u][v] = Ty<P>::mfma(fa[p][u], fb[p][v], acc[u][v]);
-                if (s + PD2 < ns) {
+                for (int v = 0; v < 2; ++v) acc[u][v] = Ty<P>::mfma(fa[p][u], fb[p][v], acc[u][v]);
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                    for (int u = 0; u < 2; ++u) {
-                        fa[p][u] = *(const u32x4 *)(ap[u] + 32 * (s + PD2));
-                        fb[p][u] = *(const u32x4 *)(bp[u] + 32 * (s + PD2));
-                    }
-                }
+            for (int u = 0; u < 2; ++u) {
+                fa[p][u] = ldg((const u32x4 *)(ap[u] + 512 * (s + PD2)));
+                fb[p][u] = ldg((const u32x4 *)(bp[u] + 512 * (s + PD2)));
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
     }
+#pragma unroll
+    for (int p = 0; p < PD2; ++p)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int v = 0; v < 2; ++v) acc[u][v] = Ty<P>::mfma(fa[p][u], fb[p][v], acc[u][v]);
     // C[n][k]: lane holds n = 16u + 4(lane >> 4) + e, k = 16v + (lane & 15)
 #pragma unroll
     for (int u = 0; u < 2; ++u)
@@ -499,16 +523,22 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs a) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int n = wn + 16 * u + 4 * (lane >> 4) + e;
-                if (n < J.N && k < J.K) J.dw[(long)n * J.K + k] = acc[u][v][e] * (1.f / Ty<P>::gs);
+                if (n < J.N && k < J.K) stg(J.dw + (long)n * J.K + k, acc[u][v][e] * (1.f / Ty<P>::gs));
             }
         }
-    if (k0 == 0 && J.db && threadIdx.x < 64) {
-        const int n = n0 + threadIdx.x;
+    if (k0 == 0 && J.db) {
+        // db[n] = sum of the row-tile partials: the 4 waves take every 4th
+        // tile (independent loads in flight), then one LDS reduction
+        __shared__ float red[4][64];
+        const int n = n0 + lane;
+        float sacc = 0.f;
         if (n < J.N) {
-            float sacc = 0.f;
-            for (int r = 0; r < J.ntiles_rows; ++r) sacc += J.part[(long)r * J.N + n];
-            J.db[n] = sacc;
+#pragma unroll 8
+            for (int r = w; r < J.ntiles_rows; r += 4) sacc += ldg(J.part + (long)r * J.N + n);
         }
+        red[w][lane] = sacc;
+        __syncthreads();
+        if (w == 0 && n < J.N) stg(J.db + n, ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]);
     }
 }
 
@@ -531,6 +561,12 @@ static bool wb_ok(const td7f_lin *l, int n) {
 }
 
 extern "C" {
+
+#ifdef EXO_STAMPS
+int td7f_train_debug_set_stamps(unsigned long long *buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_td7f_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -5;
+}
+#endif
 
 int td7f_critic(int32_t prec, const int32_t *act, const td7f_lin *critic, const float *s, const float *a,
                 const float *zs, const float *zsa, const float *qt, const float *reward, const float *not_done,
@@ -569,6 +605,7 @@ int td7f_critic(int32_t prec, const int32_t *act, const td7f_lin *critic, const 
     g.H0 = b.r32(TR, g.Hc);
     g.DY = b.r32(TR, g.Hc);
     g.F = b.r32(TR, 16);
+    g.TW = b.r32(1, g.Hc);
     const R32 sm = b.r32(1, 2 * TR);
     g.small_off = sm.off;
     g.lds_bytes = b.off;
@@ -673,6 +710,7 @@ int td7f_actor(int32_t prec, int32_t phase, const int32_t *act, const td7f_lin *
         g.H2 = b.r16(TR, ld16(hmax));
         g.H0 = b.r32(TR, g.Ha);
         g.F = b.r32(TR, 16);
+        g.TW = b.r32(g.A, g.Ha);
     } else if (phase == 1) {
         g.X = b.r16(TR, ld16(g.S + g.A));
         g.CAT = b.r16(TR, ld16(g.Hc + 2 * g.Z));
@@ -683,12 +721,14 @@ int td7f_actor(int32_t prec, int32_t phase, const int32_t *act, const td7f_lin *
         g.H0 = b.r32(TR, g.Hc);
         g.DY = b.r32(TR, g.Hc);
         g.F = b.r32(TR, 16);
+        g.TW = b.r32(g.A, g.Hc);
     } else {
         g.DP0 = b.r16(TR, ld16(std::max(hmax, g.Z)));
         g.DP1 = b.r16(TR, ld16(std::max(hmax, g.Z)));
         g.H0 = b.r32(TR, g.Ha);
         g.DY = b.r32(TR, g.Ha);
         g.F = b.r32(TR, 16);
+        g.TW = b.r32(g.A, g.He);
     }
     const R32 sm = b.r32(1, 2 * TR);
     g.small_off = sm.off;
@@ -702,8 +742,8 @@ int td7f_actor(int32_t prec, int32_t phase, const int32_t *act, const td7f_lin *
 
 int td7f_wgrad(int32_t prec, int32_t njobs, const td7f_wg_job *jobs, int64_t ld, int32_t rows, const float *td,
                float *prio, int32_t B, float alpha, float min_priority, void *stream) {
-    if (!prec_ok(prec) || njobs <= 0 || njobs > TD7F_MAX_WG || !jobs || rows <= 0 || rows % 32 || ld < rows ||
-        ld % 32 || (prio && (!td || B <= 0)))
+    if (!prec_ok(prec) || njobs <= 0 || njobs > TD7F_MAX_WG || !jobs || rows <= 0 || rows % (32 * PD2) ||
+        ld < rows || ld % 32 || (prio && (!td || B <= 0)))
         return EXO_EINVAL;
     WgArgs g{};
     g.njobs = njobs;

@@ -169,8 +169,16 @@ class FusedNets:
         self._build()
 
     def pack(self, *names):
-        for n in names:
-            self.nets[n].pack()
+        """Repack the named nets in as few td7f_pack launches as their layers fit
+        (TD7F_MAX_PACK jobs each)."""
+        nets = [self.nets[n] for n in names]
+        jobs = [pl.job() for net in nets for pl in net.layers]
+        st = nat.stream_ptr(self.dev)
+        for i in range(0, len(jobs), MAX_PACK):
+            part = jobs[i:i + MAX_PACK]
+            nat.check(nat.lib().td7f_pack(self.prec, len(part), (TD7FPackJob * len(part))(*part), st), "td7f_pack")
+        for net in nets:
+            net._ver = net._versions()
 
     def pack_all(self):
         self.pack(*self.nets)
@@ -277,7 +285,9 @@ class FusedTrain:
         self.nets, self.L, self.B = nets, nets.L, B
         L, dev = self.L, nets.dev
         hp = L.hp
-        self.ld = -(-B // 32) * 32
+        # row stride of the transposed operands = the weight-gradient reduction
+        # length: the batch padded to 256 rows (zero columns; td7f_wgrad's k-loop)
+        self.ld = -(-B // 256) * 256
         Z, He, Hc, Ha = hp.zs_dim, hp.enc_hdim, hp.critic_hdim, hp.actor_hdim
         A = L.actor.l3.out_features
         S = L.actor.l0.in_features

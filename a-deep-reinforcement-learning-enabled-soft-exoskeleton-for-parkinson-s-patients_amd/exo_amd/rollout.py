@@ -144,12 +144,36 @@ class VecTrainer:
         self._prio = ag.learner.phase_grads(*self._batch)
         cur.wait_stream(br)
 
+    # LAP.update_priority reads only the sampled indices and the new priorities
+    # and writes only the sum trees, which nothing else in the iteration reads
+    # after the sample: on one GPU it runs as its own graph branch beside the
+    # optimiser steps and the actor update, joined at the end of the iteration
+    # (before the next sample).  Data-parallel runs keep it in place (the MAX
+    # all-reduce of max_priority follows it).  EXO_PRIO_BRANCH=0 serialises.
+    prio_branch = os.environ.get("EXO_PRIO_BRANCH", "1") == "1"
+
     def _mid(self, update_actor, flat_grad=None, grad_scale=1.0):
         ag = self.agent
-        ag.learner.phase_steps(flat_grad, grad_scale)
-        ag.replay_buffer.update_priority(self._prio)
+        self._pside = None
+        if self.prio_branch and not self.dp:
+            cur = torch.cuda.current_stream(self.device)
+            if getattr(self, "_prio_stream", None) is None:
+                self._prio_stream = torch.cuda.Stream(device=self.device)
+            self._pside = self._prio_stream
+            self._pside.wait_stream(cur)
+            with torch.cuda.stream(self._pside):
+                ag.replay_buffer.update_priority(self._prio)
+            ag.learner.phase_steps(flat_grad, grad_scale)
+        else:
+            ag.learner.phase_steps(flat_grad, grad_scale)
+            ag.replay_buffer.update_priority(self._prio)
         if update_actor:
             ag.learner.phase_actor_grads(self._batch[0], self._batch[1])
+
+    def _join_prio(self):
+        if getattr(self, "_pside", None) is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._pside)
+            self._pside = None
 
     def _post(self, update_actor, flat_grad=None, grad_scale=1.0):
         if update_actor:
@@ -164,6 +188,7 @@ class VecTrainer:
         if update_actor:
             L.sync.allreduce_grads(L.grad_params(actor=True))
         self._post(update_actor)
+        self._join_prio()
 
     def _capture(self, update_actor):
         """Capture this parity's iteration; the capture itself performs one real iteration."""
@@ -178,6 +203,7 @@ class VecTrainer:
                     self._pre()
                     self._mid(update_actor)
                     self._post(update_actor)
+                    self._join_prio()
                 parts = [g]
             else:
                 # Each parity's graphs own their gradient buffers (set_to_none

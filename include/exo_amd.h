@@ -456,8 +456,9 @@ int td7f_fixed(int32_t prec, const int32_t *act, const td7f_lin *fenc, const flo
 /* The gradient passes (csrc/td7_fused_train.hip).  Each leaves, per trained
  * layer, the transposed 16-bit operands of its weight gradient -- the layer
  * input X^T [round_up(n_in, 64)][ld] and dP^T = (dY act'(Y))^T [round_up(n_out,
- * 64)][ld] (x 1024 at fp16), ld = the batch padded to 32, rows past the valid
- * ones zero -- and fp32 column sums of dP per 16-row tile (part
+ * 64)][ld] (x 1024 at fp16), ld = the batch padded to 256, stored in 1 KiB
+ * MFMA-fragment blocks of 16 operand rows x 32 batch rows (csrc/td7_fused.h
+ * blk8), padding zero -- and fp32 column sums of dP per 16-row tile (part
  * [ceil(B/16)][n_out]); td7f_wgrad turns them into dW and db. */
 typedef struct {
     void *x;
