@@ -146,15 +146,17 @@ __device__ __forceinline__ void ring_fill(u32x4 (&R)[PD][TH], const GDesc &g) {
     const int wv = threadIdx.x >> 6, w = wv % NW, kg = wv / NW, lane = threadIdx.x & 63;
     int kb, ke;
     kgroup_range(g.ks, kg, kb, ke);
-    if (ke > kb) {
+    // a k-group with no k-steps of g reloads the first fragment instead of
+    // skipping: the loads stay unconditional, so s_waitcnt counts stay exact for
+    // the loads issued before the ring (kernel-start staging)
+    const bool live = ke > kb;
 #pragma unroll
-        for (int p = 0; p < PD; ++p)
+    for (int p = 0; p < PD; ++p)
 #pragma unroll
-            for (int i = 0; i < TH; ++i) {
-                R[p][i] = ldg(g.wp + ((size_t)(g.t0 + w + NW * i) * g.ks + kb + p) * 64 + lane);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-    }
+        for (int i = 0; i < TH; ++i) {
+            R[p][i] = ldg(g.wp + (live ? ((size_t)(g.t0 + w + NW * i) * g.ks + kb + p) * 64 : 0) + lane);
+            __builtin_amdgcn_sched_barrier(0);
+        }
 }
 
 // acc[r][i] (tile t0 + w + NW i) over the rows 16r..16r+15 of the image at a_off.
@@ -397,41 +399,47 @@ __device__ __forceinline__ void epi_bwd(char *lds, const floatx4 (&acc)[RT][TH],
 // of the fp32 master weights into the LDS region wl [ncols][K], rounded to the
 // MFMA operand type (the operands the per-layer kernels use) -- at kernel start,
 // off the critical path (no barrier: the kernel's first one covers it).
+// rows j >= ncols of the region (up to nc_pad) are zero-filled (thin's NC).
 template <int P>
 __device__ __forceinline__ void stage_thin(char *lds, R32 wl, const float *W, long ldw, int j0, bool trans, int ncols,
-                                           int K) {
+                                           int K, int nc_pad) {
 #pragma unroll 4
-    for (int idx = threadIdx.x; idx < ncols * K; idx += NTH) {
+    for (int idx = threadIdx.x; idx < nc_pad * K; idx += NTH) {
         const int j = idx / K, k = idx - j * K;
-        const float w = ldg(trans ? W + (long)k * ldw + j0 + j : W + (long)(j0 + j) * ldw + k);
+        float w = 0.f;
+        if (j < ncols) w = ldg(trans ? W + (long)k * ldw + j0 + j : W + (long)(j0 + j) * ldw + k);
         *p32(lds, wl, j, k) = Ty<P>::val(Ty<P>::bits(w));
     }
 }
-// out[row][j] = scale * sum_{k < K} X[row][xc0 + k] wl[j][k] for j < ncols <= 16
-// (raw sums to the fp32 LDS region out), 16 rows: one pass, a thread per
-// (row, k-slice of NTH / 16), every output of the row accumulated in registers,
-// then reduced over the slices by shuffles.
-template <int P>
+// out[row][j] = scale * sum_{k < K} X[row][xc0 + k] wl[j][k] for j < ncols <= NC
+// (raw sums to the fp32 LDS region out; wl holds NC rows, zero past ncols),
+// 16 rows: one pass, a thread per (row, k-slice of NTH / 16) accumulating all
+// NC outputs of its row in registers (no per-column branches: every LDS read of
+// a step is in flight at once), then reduced over the slices by shuffles.
+template <int P, int NC>
 __device__ __forceinline__ void thin(char *lds, R16 in, int xc0, int K, R32 wl, int ncols, R32 out, float scale) {
     constexpr int KS = NTH / TR;
     const int row = threadIdx.x / KS, sl = threadIdx.x % KS;
-    float acc[16];
+    float acc[NC];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+    for (int j = 0; j < NC; ++j) acc[j] = 0.f;
+#pragma unroll 2
     for (int k = sl; k < K; k += KS) {
         const float x = Ty<P>::val(*p16(lds, in, row, xc0 + k));
 #pragma unroll
-        for (int j = 0; j < 16; ++j)
-            if (j < ncols) acc[j] += x * *p32(lds, wl, j, k);
+        for (int j = 0; j < NC; ++j) acc[j] += x * *p32(lds, wl, j, k);
     }
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        if (j >= ncols) break;
+    for (int j = 0; j < NC; ++j) {
 #pragma unroll
         for (int o = KS / 2; o > 0; o >>= 1) acc[j] += __shfl_xor(acc[j], o, 64);
-        if (sl == 0) *p32(lds, out, row, j) = acc[j] * scale;
     }
+    if (sl == 0)
+#pragma unroll
+        for (int j = 0; j < NC; ++j)
+            if (j < ncols) *p32(lds, out, row, j) = acc[j] * scale;
 }
+constexpr int THIN_NC = 8;  // action width <= 8 (7 here); the Q heads use 1
 
 // Gradient operand dP from an fp32 LDS region dy [16][0..N) (thin layers and
 // the loss gradients): dP = dy act'(Y) (Y from global fp32 y[(row0+row)*yld + n]
@@ -516,6 +524,83 @@ __device__ __forceinline__ void store_rows16(char *lds, R16 src, int col0, uint1
         const int row = k / ncols, c = k - row * ncols;
         if (row0 + row < nrows) stg(dst + (long)(row0 + row) * dld + c, *p16(lds, src, row, col0 + c));
     }
+}
+
+// ---------------------------------------------------------------- kernel-start staging
+// A kernel's inputs go global -> registers -> LDS in two phases, so that every
+// load of its start (input rows, thin weights, the first layer's ring) is in
+// flight at once: *_issue() loads without a branch (addresses clamped in
+// bounds, values masked at the store), *_put() stores after zero_lds's barrier.
+// (A load-then-store loop waits one full global latency per element.)
+// RowStage: column c = threadIdx.x (< ncols <= NTH) of the 16 rows.
+struct RowStage {
+    float v[TR];
+};
+__device__ __forceinline__ void row_issue(RowStage &s, const float *src, long sld, int ncols, int row0, int nrows) {
+    const int c = min((int)threadIdx.x, ncols - 1);
+#pragma unroll
+    for (int r = 0; r < TR; ++r) s.v[r] = ldg(src + (long)(row0 + r < nrows ? row0 + r : row0) * sld + c);
+}
+__device__ __forceinline__ void row_add(RowStage &s, const RowStage &o) {
+#pragma unroll
+    for (int r = 0; r < TR; ++r) s.v[r] += o.v[r];
+}
+// -> 16-bit image dst[row][col0 + c] (x scale), rows >= nrows zero
+template <int P>
+__device__ __forceinline__ void row_put16(char *lds, const RowStage &s, R16 dst, int col0, int ncols, int row0,
+                                          int nrows, float scale = 1.f) {
+    if ((int)threadIdx.x < ncols)
+#pragma unroll
+        for (int r = 0; r < TR; ++r)
+            *p16(lds, dst, r, col0 + threadIdx.x) = Ty<P>::bits(row0 + r < nrows ? s.v[r] * scale : 0.f);
+}
+__device__ __forceinline__ void row_put32(char *lds, const RowStage &s, R32 dst, int ncols, int row0, int nrows) {
+    if ((int)threadIdx.x < ncols)
+#pragma unroll
+        for (int r = 0; r < TR; ++r) *p32(lds, dst, r, threadIdx.x) = row0 + r < nrows ? s.v[r] : 0.f;
+}
+// 16-bit rows, column pairs c = 2 threadIdx.x, 2 threadIdx.x + 1 (src and sld even)
+struct Row16Stage {
+    uint32_t v[TR];
+};
+__device__ __forceinline__ void row16_issue(Row16Stage &s, const uint16_t *src, long sld, int ncols, int row0,
+                                            int nrows) {
+    const int c = 2 * min((int)threadIdx.x, (ncols - 1) / 2);
+#pragma unroll
+    for (int r = 0; r < TR; ++r)
+        s.v[r] = ldg((const uint32_t *)(src + (long)(row0 + r < nrows ? row0 + r : row0) * sld + c));
+}
+__device__ __forceinline__ void row16_put(char *lds, const Row16Stage &s, R16 dst, int col0, int ncols, int row0,
+                                          int nrows) {
+    const int c = 2 * threadIdx.x;
+    if (c < ncols)
+#pragma unroll
+        for (int r = 0; r < TR; ++r) {
+            const uint32_t v = row0 + r < nrows ? s.v[r] : 0u;
+            *p16(lds, dst, r, col0 + c) = (uint16_t)(v & 0xffffu);
+            if (c + 1 < ncols) *p16(lds, dst, r, col0 + c + 1) = (uint16_t)(v >> 16);
+        }
+}
+// the thin weights (stage_thin's slice) for k = threadIdx.x (< K <= NTH)
+template <int NC>
+struct ThinStage {
+    float v[NC];
+};
+template <int NC>
+__device__ __forceinline__ void thin_issue(ThinStage<NC> &s, const float *W, long ldw, int j0, bool trans, int ncols,
+                                           int K) {
+    const int k = min((int)threadIdx.x, K - 1);
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+        const int jj = min(j, ncols - 1);
+        s.v[j] = ldg(trans ? W + (long)k * ldw + j0 + jj : W + (long)(j0 + jj) * ldw + k);
+    }
+}
+template <int P, int NC>
+__device__ __forceinline__ void thin_put(char *lds, const ThinStage<NC> &s, R32 wl, int ncols, int K) {
+    if ((int)threadIdx.x < K)
+#pragma unroll
+        for (int j = 0; j < NC; ++j) *p32(lds, wl, j, threadIdx.x) = j < ncols ? Ty<P>::val(Ty<P>::bits(s.v[j])) : 0.f;
 }
 
 // The weight-gradient operands (layer inputs X^T, gradient operands dP^T) are
@@ -706,11 +791,11 @@ __device__ __forceinline__ void layer_fwd(char *lds, u32x4 (&R)[PD][TH], R16 a, 
 
 // A thin forward Linear (N <= 16) on the VALU: out[row][n] = act(x W^T + b) in
 // the fp32 region `out` (and global g when not null).  Ends with a barrier.
-template <int P>
+template <int P, int NC>
 __device__ __forceinline__ void layer_thin_fwd(char *lds, R16 a, const Lin &L, R32 wl, int act, R32 out, int rows,
                                                float *g, long gld, int row0, int nrows, int &si) {
     FSTAMP(si);
-    thin<P>(lds, a, 0, L.K, wl, L.N, out, 1.f);
+    thin<P, NC>(lds, a, 0, L.K, wl, L.N, out, 1.f);
     __syncthreads();
     for (int k = threadIdx.x; k < rows * L.N; k += NTH) {
         const int row = k / L.N, n = k - row * L.N;

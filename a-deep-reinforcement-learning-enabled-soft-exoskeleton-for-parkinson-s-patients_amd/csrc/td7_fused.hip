@@ -100,11 +100,15 @@ __global__ __launch_bounds__(NTH) void select_kernel(SelectArgs a) {
     const int row0 = blockIdx.x * rows;
     int si = 0;
     FSTAMP(si);
+    RowStage so;
+    ThinStage<THIN_NC> tw;
+    row_issue(so, a.obs, a.S, a.S, row0, a.n);
+    thin_issue(tw, a.ac[3].w, a.ac[3].ldw, 0, false, a.A, a.ac[3].K);
+    RING_START(a.zs[0]);
     zero_lds(lds, a.lds_bytes);
     __syncthreads();
-    load_rows<P>(lds, a.X, 0, a.obs, a.S, a.S, rows, row0, a.n);
-    stage_thin<P>(lds, a.TW, a.ac[3].w, a.ac[3].ldw, 0, false, a.A, a.ac[3].K);
-    RING_START(a.zs[0]);
+    row_put16<P>(lds, so, a.X, 0, a.S, row0, a.n);
+    thin_put<P>(lds, tw, a.TW, a.A, a.ac[3].K);
     __syncthreads();
     // zs = fixed_encoder.zs(obs) (:93-97) -> CAT[:, Ha:Ha+Z]
     layer_fwd<P, RT, TH>(lds, R, a.X, a.zs[0], &a.zs[1], a.act_enc, a.H1, 0, NO32, nullptr, 0, row0, a.n, si);
@@ -118,7 +122,7 @@ __global__ __launch_bounds__(NTH) void select_kernel(SelectArgs a) {
     __syncthreads();
     layer_fwd<P, RT, TH>(lds, R, a.CAT, a.ac[1], &a.ac[2], a.act_actor, a.H1, 0, NO32, nullptr, 0, row0, a.n, si);
     layer_fwd<P, RT, TH>(lds, R, a.H1, a.ac[2], (const Lin *)nullptr, a.act_actor, a.H2, 0, NO32, nullptr, 0, row0, a.n, si);
-    layer_thin_fwd<P>(lds, a.H2, a.ac[3], a.TW, ACT_TANH, a.F, rows, nullptr, 0, row0, a.n, si);
+    layer_thin_fwd<P, THIN_NC>(lds, a.H2, a.ac[3], a.TW, ACT_TANH, a.F, rows, nullptr, 0, row0, a.n, si);
     noise_rows<P>(lds, a.F, a.A, rows, row0, a.n, a.nz, a.out, NO16, 0, NO16, 0);
 }
 
@@ -143,11 +147,15 @@ __global__ __launch_bounds__(NTH) void target_a_kernel(TargetArgs a) {
     const int row0 = blockIdx.x * rows, B = a.B, Z = a.Z;
     int si = 0;
     FSTAMP(si);
+    RowStage sn;
+    ThinStage<THIN_NC> tw;
+    row_issue(sn, a.ns, a.S, a.S, row0, B);
+    thin_issue(tw, a.ac[3].w, a.ac[3].ldw, 0, false, a.A, a.ac[3].K);
+    RING_START(a.enc[0]);
     zero_lds(lds, a.lds_a);
     __syncthreads();
-    load_rows<P>(lds, a.X, 0, a.ns, a.S, a.S, rows, row0, B);
-    stage_thin<P>(lds, a.TW, a.ac[3].w, a.ac[3].ldw, 0, false, a.A, a.ac[3].K);
-    RING_START(a.enc[0]);
+    row_put16<P>(lds, sn, a.X, 0, a.S, row0, B);
+    thin_put<P>(lds, tw, a.TW, a.A, a.ac[3].K);
     __syncthreads();
     // fixed_target_zs = fixed_encoder_target.zs(next_state) (:234)
     layer_fwd<P, RT, TH>(lds, R, a.X, a.enc[0], &a.enc[1], a.act_enc, a.H1, 0, NO32, nullptr, 0, row0, B, si);
@@ -161,7 +169,7 @@ __global__ __launch_bounds__(NTH) void target_a_kernel(TargetArgs a) {
     __syncthreads();
     layer_fwd<P, RT, TH>(lds, R, a.CATA, a.ac[1], &a.ac[2], a.act_actor, a.H1, 0, NO32, nullptr, 0, row0, B, si);
     layer_fwd<P, RT, TH>(lds, R, a.H1, a.ac[2], &a.enc[3], a.act_actor, a.H2, 0, NO32, nullptr, 0, row0, B, si);
-    layer_thin_fwd<P>(lds, a.H2, a.ac[3], a.TW, ACT_TANH, a.F, rows, nullptr, 0, row0, B, si);
+    layer_thin_fwd<P, THIN_NC>(lds, a.H2, a.ac[3], a.TW, ACT_TANH, a.F, rows, nullptr, 0, row0, B, si);
     noise_rows<P>(lds, a.F, a.A, rows, row0, B, a.nz, nullptr, a.CATZ, Z, a.OUT, 2 * Z);
     __syncthreads();
     // fixed_target_zsa = fixed_encoder_target.zsa(zs, next_action) (:240) -> OUT[:, 0:Z]
@@ -186,13 +194,20 @@ __global__ __launch_bounds__(NTH) void target_b_kernel(TargetArgs a) {
     const Lin *cr = a.cr + h;  // layer l of head h: cr[2 l]
     int si = 0;
     FSTAMP(si);
+    RowStage sn;
+    Row16Stage sa, sc;
+    ThinStage<1> tw;
+    row_issue(sn, a.ns, a.S, a.S, row0, B);
+    row16_issue(sa, a.img + 2 * Z, ild, a.A, row0, B);
+    row16_issue(sc, a.img, ild, 2 * Z, row0, B);
+    thin_issue(tw, cr[6].w, cr[6].ldw, 0, false, 1, cr[6].K);
+    RING_START(cr[0]);
     zero_lds(lds, a.lds_b);
     __syncthreads();
-    load_rows<P>(lds, a.X, 0, a.ns, a.S, a.S, rows, row0, B);
-    load_rows16(lds, a.X, a.S, a.img + 2 * Z, ild, a.A, rows, row0, B);
-    load_rows16(lds, a.CAT, a.Hc, a.img, ild, 2 * Z, rows, row0, B);
-    stage_thin<P>(lds, a.TW, cr[6].w, cr[6].ldw, 0, false, 1, cr[6].K);
-    RING_START(cr[0]);
+    row_put16<P>(lds, sn, a.X, 0, a.S, row0, B);
+    row16_put(lds, sa, a.X, a.S, a.A, row0, B);
+    row16_put(lds, sc, a.CAT, a.Hc, 2 * Z, row0, B);
+    thin_put<P>(lds, tw, a.TW, 1, cr[6].K);
     __syncthreads();
     // critic_target(s', a', zsa, zs) head h (:109-140): AvgL1Norm(q0(sa)) | zsa | zs -> q1 -> q2 -> q3
     layer_fwd<P, RT, TH>(lds, R, a.X, cr[0], &cr[2], ACT_NONE, NO16, 0, a.F, nullptr, 0, row0, B, si);
@@ -200,7 +215,7 @@ __global__ __launch_bounds__(NTH) void target_b_kernel(TargetArgs a) {
     __syncthreads();
     layer_fwd<P, RT, TH>(lds, R, a.CAT, cr[2], &cr[4], a.act_critic, a.H1, 0, NO32, nullptr, 0, row0, B, si);
     layer_fwd<P, RT, TH>(lds, R, a.H1, cr[4], (const Lin *)nullptr, a.act_critic, a.H2, 0, NO32, nullptr, 0, row0, B, si);
-    layer_thin_fwd<P>(lds, a.H2, cr[6], a.TW, ACT_NONE, a.F, rows, a.qt + h, 2, row0, B, si);
+    layer_thin_fwd<P, 1>(lds, a.H2, cr[6], a.TW, ACT_NONE, a.F, rows, a.qt + h, 2, row0, B, si);
 }
 
 // ---------------------------------------------------------------- fixed embeddings
@@ -222,11 +237,14 @@ __global__ __launch_bounds__(NTH) void fixed_kernel(FixedArgs a) {
     const int row0 = blockIdx.x * rows, B = a.B, Z = a.Z;
     int si = 0;
     FSTAMP(si);
+    RowStage ss, sa;
+    row_issue(ss, a.s, a.S, a.S, row0, B);
+    row_issue(sa, a.act, a.A, a.A, row0, B);
+    RING_START(a.enc[0]);
     zero_lds(lds, a.lds_bytes);
     __syncthreads();
-    load_rows<P>(lds, a.X, 0, a.s, a.S, a.S, rows, row0, B);
-    load_rows<P>(lds, a.CATZ, Z, a.act, a.A, a.A, rows, row0, B);
-    RING_START(a.enc[0]);
+    row_put16<P>(lds, ss, a.X, 0, a.S, row0, B);
+    row_put16<P>(lds, sa, a.CATZ, Z, a.A, row0, B);
     __syncthreads();
     layer_fwd<P, RT, TH>(lds, R, a.X, a.enc[0], &a.enc[1], a.act_enc, a.H1, 0, NO32, nullptr, 0, row0, B, si);
     layer_fwd<P, RT, TH>(lds, R, a.H1, a.enc[1], &a.enc[2], a.act_enc, a.H2, 0, NO32, nullptr, 0, row0, B, si);
@@ -292,7 +310,7 @@ int td7f_select(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7
     a.A = actor[3].n_out;
     a.Z = enc[2].n_out;
     a.Ha = actor[0].n_out;
-    if (actor[0].n_in != a.S || actor[1].n_in != a.Ha + a.Z || a.A > 16) return EXO_EINVAL;
+    if (actor[0].n_in != a.S || actor[1].n_in != a.Ha + a.Z || a.A > THIN_NC || a.S > NTH) return EXO_EINVAL;
     a.out = out;
     a.nz = noise_of(*noise);
     const int rows = SELECT_RT * TR, hmax = std::max(enc[0].n_out, std::max(enc[1].n_out, std::max(a.Ha, actor[1].n_out)));
@@ -302,7 +320,7 @@ int td7f_select(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7
     a.H2 = b.r16(rows, ld16(hmax));
     a.CAT = b.r16(rows, ld16(a.Ha + a.Z));
     a.F = b.r32(rows, std::max(std::max(a.Z, a.Ha), 16));
-    a.TW = b.r32(a.A, actor[3].n_in);
+    a.TW = b.r32(THIN_NC, actor[3].n_in);
     a.lds_bytes = b.off;
     return DISPATCH(prec, th, select_kernel, dim3((n + rows - 1) / rows), b.off, a, (hipStream_t)stream);
 }
@@ -335,7 +353,7 @@ int td7f_target(int32_t prec, const int32_t *act, const td7f_lin *tenc, const td
     a.Hc = tcritic[0].n_out;
     // tcritic is [layer][head]: layer l of head h at 2l + h
     if (tcritic[0].n_in != a.S + a.A || tcritic[2].n_in != a.Hc + 2 * a.Z || tcritic[4].n_in != a.Hc ||
-        tenc[3].n_in != a.Z + a.A || a.A > 16)
+        tenc[3].n_in != a.Z + a.A || a.A > THIN_NC || a.S > NTH)
         return EXO_EINVAL;
     a.nz = noise_of(*noise);
     a.img = img;
@@ -351,7 +369,7 @@ int td7f_target(int32_t prec, const int32_t *act, const td7f_lin *tenc, const td
     a.CATZ = ba.r16(rows, ld16(a.Z + a.A));
     a.OUT = ba.r16(rows, round_up(2 * a.Z + a.A, 8));  // == the image row (16-byte stores)
     a.F = ba.r32(rows, std::max(hmax, 16));
-    a.TW = ba.r32(a.A, tactor[3].n_in);
+    a.TW = ba.r32(THIN_NC, tactor[3].n_in);
     a.lds_a = ba.off;
     Bump bb(1);
     const R16 Xb = bb.r16(rows, ld16(a.S + a.A)), H1b = bb.r16(rows, ld16(hmax)), H2b = bb.r16(rows, ld16(hmax));
@@ -387,7 +405,7 @@ int td7f_fixed(int32_t prec, const int32_t *act, const td7f_lin *fenc, const flo
     a.S = fenc[0].n_in;
     a.Z = fenc[2].n_out;
     a.A = fenc[3].n_in - a.Z;
-    if (a.A <= 0 || a.A > 16) return EXO_EINVAL;
+    if (a.A <= 0 || a.A > THIN_NC || a.S > NTH) return EXO_EINVAL;
     a.zs = zs;
     a.zsa = zsa;
     const int rows = TR;

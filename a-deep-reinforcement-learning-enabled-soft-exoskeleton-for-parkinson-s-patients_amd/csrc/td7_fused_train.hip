@@ -91,15 +91,22 @@ __global__ __launch_bounds__(NTH) void critic_kernel(CriticArgs a) {
     float *y1 = a.y1 + (long)h * B * Hc, *y2 = a.y2 + (long)h * B * Hc;
     int si = 0;
     FSTAMP(si);
-    zero_lds(lds, a.lds_bytes);
-    __syncthreads();
-    load_rows<P>(lds, a.X, 0, a.s, a.S, a.S, TR, row0, B);
-    load_rows<P>(lds, a.X, a.S, a.a, a.A, a.A, TR, row0, B);
-    load_rows<P>(lds, a.CAT, Hc, a.zsa, Z, Z, TR, row0, B);
-    load_rows<P>(lds, a.CAT, Hc + Z, a.zs, Z, Z, TR, row0, B);
-    stage_thin<P>(lds, a.TW, cr[6].w, cr[6].ldw, 0, false, 1, cr[6].K);
+    RowStage ss, sa, sz, szs;
+    ThinStage<1> tw;
+    row_issue(ss, a.s, a.S, a.S, row0, B);
+    row_issue(sa, a.a, a.A, a.A, row0, B);
+    row_issue(sz, a.zsa, Z, Z, row0, B);
+    row_issue(szs, a.zs, Z, Z, row0, B);
+    thin_issue(tw, cr[6].w, cr[6].ldw, 0, false, 1, cr[6].K);
     u32x4 R[PD][TH];
     ring_fill(R, fwd_of(cr[0]));
+    zero_lds(lds, a.lds_bytes);
+    __syncthreads();
+    row_put16<P>(lds, ss, a.X, 0, a.S, row0, B);
+    row_put16<P>(lds, sa, a.X, a.S, a.A, row0, B);
+    row_put16<P>(lds, sz, a.CAT, Hc, Z, row0, B);
+    row_put16<P>(lds, szs, a.CAT, Hc + Z, Z, row0, B);
+    thin_put<P>(lds, tw, a.TW, 1, cr[6].K);
     __syncthreads();
     // forward (:121-126): AvgL1Norm(q0([s, a])) | zsa | zs -> q1 -> q2 -> q3
     layer_fwd<P, 1, TH>(lds, R, a.X, cr[0], &cr[2], ACT_NONE, NO16, 0, a.H0, nullptr, 0, row0, B, si);
@@ -112,7 +119,7 @@ __global__ __launch_bounds__(NTH) void critic_kernel(CriticArgs a) {
     layer_fwd<P, 1, TH>(lds, R, a.H1, cr[4], &b3, a.act, a.H2, 0, NO32, y2, Hc, row0, B, si);
     save_xt(lds, a.H1, 0, Hc, xt[4].x, a.ld, TR, row0);
     save_xt(lds, a.H2, 0, Hc, xt[6].x, a.ld, TR, row0);
-    layer_thin_fwd<P>(lds, a.H2, cr[6], a.TW, ACT_NONE, a.F, TR, nullptr, 0, row0, B, si);
+    layer_thin_fwd<P, 1>(lds, a.H2, cr[6], a.TW, ACT_NONE, a.F, TR, nullptr, 0, row0, B, si);
     // Q_target (:241-246) and the LAP-Huber gradient (:257-259) of this head
     if (threadIdx.x < TR) {
         const int r = threadIdx.x, b = row0 + r;
@@ -177,12 +184,16 @@ __global__ __launch_bounds__(NTH) void encoder_kernel(EncoderArgs a) {
     float *mean = (float *)(lds + a.small_off), *dot = mean + TR;
     int si = 0;
     FSTAMP(si);
-    zero_lds(lds, a.lds_bytes);
-    __syncthreads();
-    load_rows<P>(lds, a.X, 0, a.ns, a.S, a.S, TR, row0, B);
-    load_rows<P>(lds, a.CATZ, Z, a.a, a.A, a.A, TR, row0, B);
+    RowStage sns, sa, ss;
+    row_issue(sns, a.ns, a.S, a.S, row0, B);
+    row_issue(sa, a.a, a.A, a.A, row0, B);
+    row_issue(ss, a.s, a.S, a.S, row0, B);  // put after the next_zs pass
     u32x4 R[PD][TH];
     ring_fill(R, fwd_of(a.e[0]));
+    zero_lds(lds, a.lds_bytes);
+    __syncthreads();
+    row_put16<P>(lds, sns, a.X, 0, a.S, row0, B);
+    row_put16<P>(lds, sa, a.CATZ, Z, a.A, row0, B);
     __syncthreads();
     // next_zs = encoder.zs(next_state) under no_grad (:219-220) -> NZ (fp32)
     layer_fwd<P, 1, TH>(lds, R, a.X, a.e[0], &a.e[1], a.act, a.H1, 0, NO32, nullptr, 0, row0, B, si);
@@ -192,7 +203,7 @@ __global__ __launch_bounds__(NTH) void encoder_kernel(EncoderArgs a) {
     norm_fwd<P>(lds, a.H3, Z, TR, 1e-8f, NO16, 0, NO16, 0, a.NZ, nullptr, 0, nullptr, nullptr, row0, B);
     __syncthreads();
     // zs = encoder.zs(state) (:222), pred_zs = encoder.zsa(zs, action) (:223)
-    load_rows<P>(lds, a.X, 0, a.s, a.S, a.S, TR, row0, B);
+    row_put16<P>(lds, ss, a.X, 0, a.S, row0, B);
     __syncthreads();
     save_xt(lds, a.X, 0, a.S, a.xt[0].x, ld, TR, row0);
     layer_fwd<P, 1, TH>(lds, R, a.X, a.e[0], &a.e[1], a.act, a.H1, 0, NO32, a.y0, He, row0, B, si);
@@ -269,14 +280,19 @@ __global__ __launch_bounds__(NTH) void actor_a_kernel(ActorArgs a) {
     const int row0 = blockIdx.x * TR, B = a.B, Z = a.Z, Ha = a.Ha, He = a.He;
     const long ld = a.ld;
     int si = 0;
-    zero_lds(lds, a.lds);
-    __syncthreads();
-    load_rows<P>(lds, a.X, 0, a.s, a.S, a.S, TR, row0, B);
-    load_rows<P>(lds, a.CATA, Ha, a.zs, Z, Z, TR, row0, B);
-    load_rows<P>(lds, a.CATZ, 0, a.zs, Z, Z, TR, row0, B);
-    stage_thin<P>(lds, a.TW, a.ac[3].w, a.ac[3].ldw, 0, false, a.A, a.ac[3].K);
+    RowStage ss, szs;
+    ThinStage<THIN_NC> tw;
+    row_issue(ss, a.s, a.S, a.S, row0, B);
+    row_issue(szs, a.zs, Z, Z, row0, B);
+    thin_issue(tw, a.ac[3].w, a.ac[3].ldw, 0, false, a.A, a.ac[3].K);
     u32x4 R[PD][TH];
     ring_fill(R, fwd_of(a.ac[0]));
+    zero_lds(lds, a.lds);
+    __syncthreads();
+    row_put16<P>(lds, ss, a.X, 0, a.S, row0, B);
+    row_put16<P>(lds, szs, a.CATA, Ha, Z, row0, B);
+    row_put16<P>(lds, szs, a.CATZ, 0, Z, row0, B);
+    thin_put<P>(lds, tw, a.TW, a.A, a.ac[3].K);
     __syncthreads();
     // actor(state, fixed_zs) (:268, :72-77)
     layer_fwd<P, 1, TH>(lds, R, a.X, a.ac[0], &a.ac[1], ACT_NONE, NO16, 0, a.H0, a.h0, Ha, row0, B, si);
@@ -288,7 +304,7 @@ __global__ __launch_bounds__(NTH) void actor_a_kernel(ActorArgs a) {
     layer_fwd<P, 1, TH>(lds, R, a.H1, a.ac[2], &a.fe[3], a.act_actor, a.H2, 0, NO32, a.ya[1], Ha, row0, B, si);
     save_xt(lds, a.H1, 0, Ha, a.xt[2].x, ld, TR, row0);
     save_xt(lds, a.H2, 0, Ha, a.xt[3].x, ld, TR, row0);
-    layer_thin_fwd<P>(lds, a.H2, a.ac[3], a.TW, ACT_TANH, a.F, TR, a.act_out, a.A, row0, B, si);
+    layer_thin_fwd<P, THIN_NC>(lds, a.H2, a.ac[3], a.TW, ACT_TANH, a.F, TR, a.act_out, a.A, row0, B, si);
     for (int k = threadIdx.x; k < TR * a.A; k += NTH) {
         const int r = k / a.A, c = k - r * a.A;
         *p16(lds, a.CATZ, r, Z + c) = Ty<P>::bits(*p32(lds, a.F, r, c));
@@ -309,15 +325,22 @@ __global__ __launch_bounds__(NTH) void actor_b_kernel(ActorArgs a) {
     float *y1 = a.yc[0] + (long)h * B * Hc, *y2 = a.yc[1] + (long)h * B * Hc;
     int si = 0;
     FSTAMP(si);
-    zero_lds(lds, a.lds);
-    __syncthreads();
-    load_rows<P>(lds, a.X, 0, a.s, a.S, a.S, TR, row0, B);
-    load_rows<P>(lds, a.X, a.S, a.act_out, a.A, a.A, TR, row0, B);
-    load_rows<P>(lds, a.CAT, Hc, a.zsa_out, Z, Z, TR, row0, B);
-    load_rows<P>(lds, a.CAT, Hc + Z, a.zs, Z, Z, TR, row0, B);
-    stage_thin<P>(lds, a.TW, cr[0].w, cr[0].ldw, a.S, true, a.A, Hc);
+    RowStage ss, sa, sz, szs;
+    ThinStage<THIN_NC> tw;
+    row_issue(ss, a.s, a.S, a.S, row0, B);
+    row_issue(sa, a.act_out, a.A, a.A, row0, B);
+    row_issue(sz, a.zsa_out, Z, Z, row0, B);
+    row_issue(szs, a.zs, Z, Z, row0, B);
+    thin_issue(tw, cr[0].w, cr[0].ldw, a.S, true, a.A, Hc);
     u32x4 R[PD][TH];
     ring_fill(R, fwd_of(cr[0]));
+    zero_lds(lds, a.lds);
+    __syncthreads();
+    row_put16<P>(lds, ss, a.X, 0, a.S, row0, B);
+    row_put16<P>(lds, sa, a.X, a.S, a.A, row0, B);
+    row_put16<P>(lds, sz, a.CAT, Hc, Z, row0, B);
+    row_put16<P>(lds, szs, a.CAT, Hc + Z, Z, row0, B);
+    thin_put<P>(lds, tw, a.TW, a.A, Hc);
     __syncthreads();
     // Q = critic(state, actor, zsa, zs) with the updated critic (:270)
     layer_fwd<P, 1, TH>(lds, R, a.X, cr[0], &cr[2], ACT_NONE, NO16, 0, a.H0, nullptr, 0, row0, B, si);
@@ -348,7 +371,7 @@ __global__ __launch_bounds__(NTH) void actor_b_kernel(ActorArgs a) {
     norm_bwd<P>(lds, a.DY, a.H0, mean, Hc, 1e-8f, dot, a.DP0, nullptr, 0, nullptr, row0, B);
     __syncthreads();
     FSTAMP(si);
-    thin<P>(lds, a.DP0, 0, Hc, a.TW, a.A, a.F, 1.f / Ty<P>::gs);
+    thin<P, THIN_NC>(lds, a.DP0, 0, Hc, a.TW, a.A, a.F, 1.f / Ty<P>::gs);
     __syncthreads();
     FSTAMP(si);
     for (int k = threadIdx.x; k < TR * a.A; k += NTH) {
@@ -365,20 +388,23 @@ __global__ __launch_bounds__(NTH) void actor_c_kernel(ActorArgs a) {
     float *mean = (float *)(lds + a.small_off), *dot = mean + TR;
     int si = 0;
     FSTAMP(si);
-    zero_lds(lds, a.lds);
-    __syncthreads();
     // d zsa = sum over the heads -> the fixed encoder's zsa3 dP (no activation)
-#pragma unroll 4
-    for (int k = threadIdx.x; k < TR * Z; k += NTH) {
-        const int r = k / Z, c = k - r * Z, b = row0 + r;
-        const float v = b < B ? ldg(a.dzsa + (long)b * Z + c) + ldg(a.dzsa + ((long)B + b) * Z + c) : 0.f;
-        *p16(lds, a.DP0, r, c) = Ty<P>::bits(v * Ty<P>::gs);
-    }
-    if (threadIdx.x < TR) mean[threadIdx.x] = row0 + (int)threadIdx.x < B ? ldg(a.mean0 + row0 + threadIdx.x) : 0.f;
-    load_rows32(lds, a.H0, a.h0, Ha, Ha, TR, row0, B);
-    stage_thin<P>(lds, a.TW, a.fe[3].w, a.fe[3].ldw, Z, true, A, He);
+    RowStage d0, d1, sh;
+    ThinStage<THIN_NC> tw;
+    row_issue(d0, a.dzsa, Z, Z, row0, B);
+    row_issue(d1, a.dzsa + (long)B * Z, Z, Z, row0, B);
+    row_issue(sh, a.h0, Ha, Ha, row0, B);
+    const float m0 = ldg(a.mean0 + min(row0 + (int)(threadIdx.x % TR), B - 1));
+    thin_issue(tw, a.fe[3].w, a.fe[3].ldw, Z, true, A, He);
     u32x4 R[PD][TH];
     ring_fill(R, bwd_of(a.fe[5], 0));
+    zero_lds(lds, a.lds);
+    __syncthreads();
+    row_add(d0, d1);
+    row_put16<P>(lds, d0, a.DP0, 0, Z, row0, B, Ty<P>::gs);
+    if (threadIdx.x < TR) mean[threadIdx.x] = row0 + (int)threadIdx.x < B ? m0 : 0.f;
+    row_put32(lds, sh, a.H0, Ha, row0, B);
+    thin_put<P>(lds, tw, a.TW, A, He);
     __syncthreads();
     const GDesc nx10 = bwd_of(a.fe[4], 0);
     layer_bwd<P, TH>(lds, R, a.DP0, a.fe[5], 0, He, &nx10, a.act_enc, a.yz[1], He, NO32, nullptr, 0, a.DP1, nullptr,
@@ -388,7 +414,7 @@ __global__ __launch_bounds__(NTH) void actor_c_kernel(ActorArgs a) {
                      row0, B, si);
     // the action columns of zsa1's input (thin), + both critic heads' d action, x tanh'
     FSTAMP(si);
-    thin<P>(lds, a.DP0, 0, He, a.TW, A, a.F, 1.f / Ty<P>::gs);
+    thin<P, THIN_NC>(lds, a.DP0, 0, He, a.TW, A, a.F, 1.f / Ty<P>::gs);
     __syncthreads();
     FSTAMP(si);
     for (int k = threadIdx.x; k < TR * A; k += NTH) {
@@ -574,7 +600,7 @@ int td7f_critic(int32_t prec, const int32_t *act, const td7f_lin *critic, const 
                 int32_t S, int32_t A, float *td, float *q, float *y1, float *y2, const td7f_xt *xt, int64_t ld,
                 void *stream) {
     if (!prec_ok(prec) || !act || !critic || !s || !a || !zs || !zsa || !qt || !reward || !not_done || !lo || !hi ||
-        !run_max || !run_min || !td || !y1 || !y2 || !xt || B <= 0 || S <= 0 || A <= 0 || ld < B || ld % 32)
+        !run_max || !run_min || !td || !y1 || !y2 || !xt || B <= 0 || S <= 0 || S > NTH || A <= 0 || A > THIN_NC || ld < B || ld % 32)
         return EXO_EINVAL;
     const int th = th_of(critic, 8);
     if ((th != 4 && th != 5) || !wb_ok(critic, 8) || !xt_ok(xt, 8)) return EXO_EINVAL;
@@ -635,7 +661,7 @@ int td7f_encoder(int32_t prec, const int32_t *act, const td7f_lin *enc, const fl
     g.He = enc[0].n_out;
     g.Z = enc[2].n_out;
     g.A = enc[3].n_in - g.Z;
-    if (g.A <= 0 || g.A > 16 || enc[1].n_out != g.He || enc[4].n_out != g.He || enc[5].n_out != g.Z || g.Z % 4)
+    if (g.A <= 0 || g.A > THIN_NC || g.S > NTH || enc[1].n_out != g.He || enc[4].n_out != g.He || enc[5].n_out != g.Z || g.Z % 4)
         return EXO_EINVAL;
     g.mse_scale = 2.0f / ((float)B * (float)g.Z);
     g.ld = ld;
@@ -690,7 +716,7 @@ int td7f_actor(int32_t prec, int32_t phase, const int32_t *act, const td7f_lin *
     g.He = fenc[3].n_out;
     g.Hc = critic[0].n_out;
     if (actor[1].n_in != g.Ha + g.Z || fenc[3].n_in != g.Z + g.A || critic[0].n_in != g.S + g.A ||
-        critic[2].n_in != g.Hc + 2 * g.Z || g.A > 16 || g.Hc % 16 || g.Ha % 16)
+        critic[2].n_in != g.Hc + 2 * g.Z || g.A > THIN_NC || g.S > NTH || g.Hc % 16 || g.Ha % 16)
         return EXO_EINVAL;
     g.dq = -1.0f / (2.0f * (float)B);
     g.act_out = u.act_out; g.zsa_out = u.zsa_out; g.h0 = u.h0; g.mean0 = u.mean0;
@@ -710,7 +736,7 @@ int td7f_actor(int32_t prec, int32_t phase, const int32_t *act, const td7f_lin *
         g.H2 = b.r16(TR, ld16(hmax));
         g.H0 = b.r32(TR, g.Ha);
         g.F = b.r32(TR, 16);
-        g.TW = b.r32(g.A, g.Ha);
+        g.TW = b.r32(THIN_NC, g.Ha);
     } else if (phase == 1) {
         g.X = b.r16(TR, ld16(g.S + g.A));
         g.CAT = b.r16(TR, ld16(g.Hc + 2 * g.Z));
@@ -721,14 +747,14 @@ int td7f_actor(int32_t prec, int32_t phase, const int32_t *act, const td7f_lin *
         g.H0 = b.r32(TR, g.Hc);
         g.DY = b.r32(TR, g.Hc);
         g.F = b.r32(TR, 16);
-        g.TW = b.r32(g.A, g.Hc);
+        g.TW = b.r32(THIN_NC, g.Hc);
     } else {
         g.DP0 = b.r16(TR, ld16(std::max(hmax, g.Z)));
         g.DP1 = b.r16(TR, ld16(std::max(hmax, g.Z)));
         g.H0 = b.r32(TR, g.Ha);
         g.DY = b.r32(TR, g.Ha);
         g.F = b.r32(TR, 16);
-        g.TW = b.r32(g.A, g.He);
+        g.TW = b.r32(THIN_NC, g.He);
     }
     const R32 sm = b.r32(1, 2 * TR);
     g.small_off = sm.off;

@@ -8,5 +8,4 @@ rc=$?
 timeout -k 10 120 python -u tools/fused_bench.py > gpurun_out/fused_bench.txt 2>&1 || exit $?
 timeout -k 10 200 python bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-td7-variants > gpurun_out/fused_train_bench.json 2> gpurun_out/fused_train_bench.err || exit $?
 timeout -k 10 150 python -u tools/fused_stamps_train.py > gpurun_out/fused_stamps_train.txt 2>&1 || exit $?
-bash tools/gpu_icache.sh
 exit $rc

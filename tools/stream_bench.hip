@@ -74,6 +74,11 @@ __global__ __launch_bounds__(64 * NWAVE) void dma_kernel(const u32x4 *buf, long 
     if (acc.x == 0x12345678u) sink[threadIdx.x] = acc;
 }
 
+// cold: launch i reads buffer i % NCOLD of a 64 MiB pool (> the 32 MiB of L2,
+// < the Infinity Cache): the weights a fused pass streams come from MALL, not L2
+static int g_cold = 0;
+static const u32x4 *g_pool = nullptr;
+constexpr int NCOLD = 64;
 template <typename K>
 float timeit(K k, int grid, int threads, int lds, const u32x4 *buf, long nblocks, u32x4 *sink) {
     if (lds) hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -84,7 +89,9 @@ float timeit(K k, int grid, int threads, int lds, const u32x4 *buf, long nblocks
     hipEventCreate(&e1);
     hipEventRecord(e0);
     const int reps = 50;
-    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(k, dim3(grid), dim3(threads), lds, 0, buf, nblocks, sink);
+    for (int i = 0; i < reps; ++i)
+        hipLaunchKernelGGL(k, dim3(grid), dim3(threads), lds, 0, g_cold ? g_pool + (long)(i % NCOLD) * nblocks * 64 : buf,
+                           nblocks, sink);
     hipEventRecord(e1);
     hipEventSynchronize(e1);
     float ms;
@@ -99,12 +106,18 @@ int main() {
     hipMalloc(&buf, S);
     hipMalloc(&sink, 1 << 16);
     hipMemset(buf, 1, S);
-    printf("%-34s %6s %9s %12s\n", "variant", "WGs", "us", "GB/s per WG");
+    u32x4 *pool;
+    hipMalloc(&pool, S * NCOLD);
+    hipMemset(pool, 1, S * NCOLD);
+    g_pool = pool;
+    printf("%-34s %6s %5s %9s %12s\n", "variant", "WGs", "cold", "us", "GB/s per WG");
+    for (int cold : {0, 1})
     for (int grid : {64, 256}) {
+        g_cold = cold;
 #define RUN(NAME, K, TH, LDS)                                                                 \
     {                                                                                         \
         const float us = timeit(K, grid, TH, LDS, buf, nblocks, sink);                        \
-        printf("%-34s %6d %9.2f %12.1f\n", NAME, grid, us, S / (us * 1e-6) / 1e9);            \
+        printf("%-34s %6d %5d %9.2f %12.1f\n", NAME, grid, cold, us, S / (us * 1e-6) / 1e9);  \
     }
         RUN("plain   4 waves x 25", (stream_kernel<4, 25, 0>), 256, 0);
         RUN("plain   8 waves x 25", (stream_kernel<8, 25, 0>), 512, 0);
