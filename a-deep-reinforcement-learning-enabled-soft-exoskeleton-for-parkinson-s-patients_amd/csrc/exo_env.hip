@@ -558,6 +558,61 @@ __global__ void tremor_metrics_kernel(Dev S, const float *__restrict__ info, con
     m[15] = nz ? 1.f : 0.f;
 }
 
+// Evaluation-script statistics (Simulation/Evaluate_control_performance.py:
+// 192-260), which differ from the training script's in four places: the
+// reductions divide by |ref + 1e-10| (:197, :201), the SFE/SAA amplitudes are
+// swapped before the DH FK (:208-209), the torque counters look at the env's
+// tremor axes only with <= 0 (:233-241: every axis suppressed / any axis
+// suppressed), and the episode's total-amplitude mean runs over the negative
+// values (:262, :414).  counters [N][5] accumulate: all-axes-suppressed steps,
+// any-axis-suppressed steps, total < 0 steps, total >= 0 steps, sum of the
+// negative totals.
+__global__ void eval_metrics_kernel(Dev S, const float *__restrict__ info, const uint8_t *__restrict__ stepped,
+                                    double L1, double L2, float *__restrict__ counters) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= S.N || (stepped && !stepped[e])) return;
+    const float *in = info + (size_t)e * INFO;
+    const int seq = S.seq[e];
+    bool all_sup = true, any_sup = false;
+    for (int j = 0; j < 7; ++j) {
+        if (!((seq >> j) & 1)) continue;
+        const double ref = in[21 + j];
+        double tr = (fabs((double)in[7 + j]) - fabs(ref)) / fabs(ref + 1e-10) * 100.0;
+        if (!isfinite(tr)) tr = 0.0;
+        all_sup &= tr <= 0.0;
+        any_sup |= tr <= 0.0;
+    }
+    const int cnt = S.counts[e];
+    const double *imu = S.imu + (size_t)S.motion[e] * 5 * S.Lmax;
+    const int col[5] = {2, 3, 4, 0, 1};
+    double q0[7], q1[7], q2[7];
+    for (int j = 0; j < 7; ++j) {
+        const int js = j == 0 ? 1 : (j == 1 ? 0 : j);  // amplitudes with axes 0 / 1 swapped
+        const double o = j < 5 ? imu[col[j] * S.Lmax + cnt] * (PI / 180) : 0.0;
+        q0[j] = o;
+        q1[j] = (double)in[14 + js] * (PI / 180) + o;
+        q2[j] = (double)in[28 + js] * (PI / 180) + o;
+    }
+    double p0[3], p1[3], p2[3];
+    dh_end_effector(q0, L1, L2, p0);
+    dh_end_effector(q1, L1, L2, p1);
+    dh_end_effector(q2, L1, L2, p2);
+    const double ds = sqrt((p1[0] - p0[0]) * (p1[0] - p0[0]) + (p1[1] - p0[1]) * (p1[1] - p0[1]) +
+                           (p1[2] - p0[2]) * (p1[2] - p0[2]));
+    const double du = sqrt((p2[0] - p0[0]) * (p2[0] - p0[0]) + (p2[1] - p0[1]) * (p2[1] - p0[1]) +
+                           (p2[2] - p0[2]) * (p2[2] - p0[2]));
+    const double total = (ds - du) / du * 100.0;
+    float *cn = counters + (size_t)e * 5;
+    if (all_sup) cn[0] += 1;
+    if (any_sup) cn[1] += 1;
+    if (total < 0) {
+        cn[2] += 1;
+        cn[4] += (float)total;
+    } else {
+        cn[3] += 1;
+    }
+}
+
 struct exo_ctx {
     int device = 0;
     int N = 0, n_motions = 0, Lmax = 0;
@@ -981,6 +1036,15 @@ int exo_tremor_metrics(exo_ctx *c, const float *info_dev, const uint8_t *stepped
     hipLaunchKernelGGL(tremor_metrics_kernel, dim3((c->N + 255) / 256), dim3(256), 0, (hipStream_t)stream, c->S,
                        info_dev, stepped_dev, humerus_length, forearm_length, disregard, metrics_dev, counters_dev);
     return check(c, hipGetLastError(), "exo_tremor_metrics");
+}
+
+int exo_eval_metrics(exo_ctx *c, const float *info_dev, const uint8_t *stepped_dev, double humerus_length,
+                     double forearm_length, float *counters_dev, void *stream) {
+    if (!c || !info_dev || !counters_dev) return EXO_EINVAL;
+    DeviceGuard g(c->device);
+    hipLaunchKernelGGL(eval_metrics_kernel, dim3((c->N + 255) / 256), dim3(256), 0, (hipStream_t)stream, c->S,
+                       info_dev, stepped_dev, humerus_length, forearm_length, counters_dev);
+    return check(c, hipGetLastError(), "exo_eval_metrics");
 }
 
 const char *exo_last_error(const exo_ctx *c) { return c ? c->err.c_str() : "null context"; }

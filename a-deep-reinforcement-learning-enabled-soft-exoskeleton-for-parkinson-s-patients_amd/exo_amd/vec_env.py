@@ -184,6 +184,24 @@ class VecExoskeletonEnv:
                   "exo_tremor_metrics", self._ctx)
         return m, counters
 
+    EVAL_COUNTER_NAMES = ("all_axes_suppressed", "any_axis_suppressed", "ampl_total_neg", "ampl_total_nonneg",
+                          "ampl_total_neg_sum")
+
+    def eval_metrics(self, info, stepped=None, counters=None, humerus_length=0.4, forearm_length=0.4):
+        """The evaluation script's per-step statistics
+        (Simulation/Evaluate_control_performance.py:192-260) for the envs the last
+        step advanced, accumulated on the device into counters [N, 5] float32
+        (EVAL_COUNTER_NAMES); see include/exo_amd.h exo_eval_metrics."""
+        if counters is None:
+            counters = torch.zeros((self.n, 5), dtype=torch.float32, device=self.device)
+        st = None
+        if stepped is not None:
+            st = (stepped.view(torch.uint8) if stepped.dtype == torch.bool else stepped.to(torch.uint8)).contiguous()
+        nat.check(nat.lib().exo_eval_metrics(self._ctx, nat.ptr(info.contiguous()), nat.ptr(st), float(humerus_length),
+                                             float(forearm_length), nat.ptr(counters), self._stream()),
+                  "exo_eval_metrics", self._ctx)
+        return counters
+
     STEP_VARIANTS = {"auto": 0, "lanes": 1, "rows": 2}
 
     def set_step_variant(self, name):

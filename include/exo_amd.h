@@ -177,6 +177,19 @@ int exo_tremor_metrics(exo_ctx *c, const float *info_dev, const uint8_t *stepped
                        double forearm_length, double hand_length, int32_t disregard, float *metrics_dev,
                        float *counters_dev, void *stream);
 
+/* The evaluation script's statistics (Simulation/Evaluate_control_performance.py:
+ * 192-260: reductions over |ref + 1e-10|, SFE/SAA amplitudes swapped before the
+ * DH FK, torque counters over the env's tremor axes with <= 0) for every env
+ * the last exo_step advanced; counters_dev [N][5] accumulate:
+ *   steps with every tremor axis suppressed (tremor_when_reduction[i, 1]),
+ *   steps with any tremor axis suppressed (tremor_reduction_in_episode[i]),
+ *   steps with end-effector amplitude change < 0 / >= 0
+ *     (tremor_when_ampl_reduction[i, 1] / [i, 0]),
+ *   the sum of the negative changes (for the episode mean over non-zero
+ *     entries of tremor_ampl_total_reduction_full_ep, :262). */
+int exo_eval_metrics(exo_ctx *c, const float *info_dev, const uint8_t *stepped_dev, double humerus_length,
+                     double forearm_length, float *counters_dev, void *stream);
+
 /* ------------------------------------------------------------------------
  * LAP prioritised replay (Agent/TD7_buffer_multi_agent.py:5-120), one
  * sum tree per stratum (the reference keeps one priority row per env,

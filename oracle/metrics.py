@@ -47,3 +47,27 @@ def step_metrics(torque_val, tremor_torque_val, ampl_val, tremor_ampl_val, origi
         ta = np.where(ta > 0, 0, ta)
         total = 0 if total > 0 else total
     return tr, ta, total, deltas, last_neg
+
+
+def eval_step_counters(torque_val, tremor_torque_val, ampl_val, tremor_ampl_val, original_deg, tremor_sequence,
+                       lengths=(0.4, 0.4, 0.05)):
+    """One env-step of Simulation/Evaluate_control_performance.py:192-247: the
+    counter deltas [all tremor axes suppressed, any tremor axis suppressed,
+    total < 0, total >= 0, total if < 0 else 0] (exo_eval_metrics's counters)."""
+    eps = 1e-10
+    with np.errstate(divide="ignore", invalid="ignore"):
+        tr = np.nan_to_num((np.abs(torque_val) - np.abs(tremor_torque_val)) / np.abs(tremor_torque_val + eps) * 100,
+                           nan=0, posinf=0, neginf=0)
+    sel = tr[np.asarray(tremor_sequence)[:7] == 1]
+    orig = np.radians(np.asarray(original_deg, dtype=np.float64))
+    a = np.array(ampl_val, dtype=np.float64)
+    u = np.array(tremor_ampl_val, dtype=np.float64)
+    a[[0, 1]] = a[[1, 0]]  # :208-209
+    u[[0, 1]] = u[[1, 0]]
+    p0 = end_effector(orig, *lengths)
+    p1 = end_effector(np.radians(a) + orig, *lengths)
+    p2 = end_effector(np.radians(u) + orig, *lengths)
+    ds, du = np.linalg.norm(p1 - p0), np.linalg.norm(p2 - p0)
+    total = (ds - du) / du * 100
+    return np.array([float(np.all(sel <= 0)), float(np.any(sel <= 0)), float(total < 0), float(not total < 0),
+                     total if total < 0 else 0.0])

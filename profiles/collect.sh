@@ -18,4 +18,6 @@ timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex exo_step --o
     python3 bench.py --mode env --steps 100 --warmup 10 --no-cpu-baseline > $OUT/pmc_write.log 2>&1
 timeout -k 10 400 python3 bench.py > $OUT/bench_default.log 2>&1
 timeout -k 10 200 python3 tools/dense_bench.py > $OUT/dense_bench.txt 2>&1
+timeout -k 10 200 python3 tools/fused_bench.py > $OUT/fused_bench.txt 2>&1
+if [ -x tools/stream_bench ]; then timeout -k 10 120 tools/stream_bench > $OUT/stream_bench.txt 2>&1; fi
 find $OUT -name "*.csv" | head -50

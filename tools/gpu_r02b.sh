@@ -1,7 +1,10 @@
 #!/bin/bash
-# GPU box: whole -m gpu suite, then a kernel trace of the default training bench.
+# GPU box: whole -m gpu suite, then the round's profile evidence (profiles/collect.sh).
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r02b_tests.log 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_r02b/train -o run -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-td7-variants > gpurun_out/prof_r02b_bench.log 2>&1
+bash profiles/collect.sh "${1:-r02b}"
+if [ -d policies ]; then
+  timeout -k 10 300 python -u tools/eval_policies.py --out gpurun_out/eval_policies_ideal.json > gpurun_out/eval_policies_ideal.txt 2>&1 || exit $?
+fi

@@ -7,6 +7,13 @@ from collections import defaultdict
 
 
 def classify(n):
+    base = n.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
+    if base.startswith("td7f::"):
+        return "td7 fused (HIP)"
+    if "adam_multi" in base:
+        return "Adam (HIP)"
+    if base.startswith("lap_"):
+        return "LAP (HIP)"
     if "dense_" in n.split("(")[0] or "(anonymous namespace)::dense" in n:
         return "td7_dense (HIP)"
     if "exo_step" in n:
