@@ -50,6 +50,87 @@ def graph_reductions_ok(device, rows=1024, cols=300, replays=3):
     return True
 
 
+class CaptureForkError(RuntimeError):
+    pass
+
+
+def unjoined_streams(events, origin):
+    """Fork/join audit of one capture.  events: in order, ("wait", waiter,
+    waited) for every Stream.wait_stream and ("use", stream) when a
+    `torch.cuda.stream(stream)` block ends (the last point work can have been
+    enqueued there).  A branch is joined when its work up to its last use is
+    ordered before the capture stream `origin`: a wait of the origin on it
+    after that use, or of another branch that is itself joined after that
+    wait.  Returns the branches (streams forked from the captured set) that
+    are not -- the `hipErrorStreamCaptureUnjoined` of capture end."""
+    def key(st):  # torch returns a new Stream object per current_stream() call: key by the raw handle
+        return st.cuda_stream
+    captured, last_use = {key(origin)}, {}
+    joins = {}  # waited -> [(time, waiter)]
+    objs = {}
+    for t, ev in enumerate(events):
+        if ev[0] == "wait":
+            _, w, x = ev
+            objs[key(w)], objs[key(x)] = w, x
+            if key(x) in captured and key(w) not in captured:
+                captured.add(key(w))
+                last_use.setdefault(key(w), t)
+            if key(x) in captured and key(x) != key(origin):
+                joins.setdefault(key(x), []).append((t, key(w)))
+        else:
+            objs[key(ev[1])] = ev[1]
+            if key(ev[1]) in captured:
+                last_use[key(ev[1])] = t
+
+    def ordered(s, t, seen=()):  # is s's work up to time t ordered before origin's end?
+        if s == key(origin):
+            return True
+        return any(tj >= t and w not in seen and ordered(w, tj, seen + (s,)) for tj, w in joins.get(s, ()))
+
+    return [objs[s] for s in captured if s != key(origin) and not ordered(s, last_use.get(s, 0))]
+
+
+class ForkJoinAudit:
+    """Records every Stream.wait_stream and stream-context exit while a graph is
+    captured on `origin`; on exit raises CaptureForkError naming any branch not
+    joined back (after joining it, so that capture end still succeeds)."""
+
+    def __init__(self, origin):
+        self.origin = origin
+        self.events = []
+
+    def __enter__(self):
+        audit = self
+        self._wait = torch.cuda.Stream.wait_stream
+        self._exit = torch.cuda.StreamContext.__exit__
+
+        def wait_stream(st, other):
+            audit.events.append(("wait", st, other))
+            return audit._wait(st, other)
+
+        def ctx_exit(ctx, *a):
+            if ctx.stream is not None:
+                audit.events.append(("use", ctx.stream))
+            return audit._exit(ctx, *a)
+
+        torch.cuda.Stream.wait_stream = wait_stream
+        torch.cuda.StreamContext.__exit__ = ctx_exit
+        return self
+
+    def __exit__(self, exc_type, exc, tb):
+        torch.cuda.Stream.wait_stream = self._wait
+        torch.cuda.StreamContext.__exit__ = self._exit
+        if exc_type is not None:
+            return False
+        bad = unjoined_streams(self.events, self.origin)
+        if bad:
+            for st in bad:
+                self.origin.wait_stream(st)
+            raise CaptureForkError(f"{len(bad)} stream(s) forked from the capture stream were not joined back "
+                                   "before capture end")
+        return False
+
+
 class VecTrainer:
     def __init__(self, env, agent, strata=None, use_graphs=True, warmup_eager=3, exploration="gaussian"):
         self.env, self.agent = env, agent
@@ -199,7 +280,7 @@ class VecTrainer:
         with torch.cuda.stream(s):
             if not self.dp:
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=pool, stream=s):
+                with torch.cuda.graph(g, pool=pool, stream=s), ForkJoinAudit(s):
                     self._pre()
                     self._mid(update_actor)
                     self._post(update_actor)
@@ -211,18 +292,18 @@ class VecTrainer:
                 # work on flat buckets packed/unpacked inside the graphs.
                 L, S = self.agent.learner, self.agent.sync
                 g1, g2, g3 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g1, pool=pool, stream=s):
+                with torch.cuda.graph(g1, pool=pool, stream=s), ForkJoinAudit(s):
                     self._pre()
                     flat_c = S.pack(L.grad_params())
                 pool = g1.pool()
                 flat_a = None
                 scale = 1.0 / S.world
-                with torch.cuda.graph(g2, pool=pool, stream=s):
+                with torch.cuda.graph(g2, pool=pool, stream=s), ForkJoinAudit(s):
                     self._mid(update_actor, flat_c, scale)   # the optimisers read the reduced bucket in place
                     if update_actor:
                         flat_a = S.pack(L.grad_params(actor=True))
                 if update_actor:  # no actor step at this parity: nothing to capture
-                    with torch.cuda.graph(g3, pool=pool, stream=s):
+                    with torch.cuda.graph(g3, pool=pool, stream=s), ForkJoinAudit(s):
                         self._post(update_actor, flat_a, scale)
                 else:
                     g3 = None
