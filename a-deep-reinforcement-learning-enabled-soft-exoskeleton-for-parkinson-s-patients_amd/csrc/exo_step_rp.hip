@@ -20,6 +20,8 @@
 // the ODE), the joint-target motor update after them.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "exo_amd.h"
 #include "exo_model.h"
 
@@ -82,6 +84,39 @@ __device__ __forceinline__ double group_sum(double x) {
     return x;
 }
 
+// The same RHS with every neighbour pull a DPP lane move (VALU, no LDS round
+// trip).  For term m the source column of row r, RP_DCOL[r][m], is one
+// quad_perm pattern shared by both quads of the group (pads take any lane:
+// their coefficient is 0), so D v and K q need one move per term.  I^-1's
+// blocks {0,3,6} and {1,2,4,5} cross the quads: a term's column comes from
+// the own quad (quad_perm of r) in one quad and from the other one
+// (quad_perm of the half-row mirror of r) in the other, picked by a select.
+// Same terms in the same order as row_acc: bit-identical results.
+__device__ __forceinline__ double row_acc_dpp(const RowM &M, bool upper, double T, double q, double v) {
+    double dq = 0.0, kq = 0.0;
+    dq += M.d[0] * dpp_d<0x00>(v); kq += M.s[0] * dpp_d<0x00>(q);  // columns [0,0,0,0] of each quad
+    dq += M.d[1] * dpp_d<0xD5>(v); kq += M.s[1] * dpp_d<0xD5>(q);  // [1,1,1,3]
+    dq += M.d[2] * dpp_d<0xAA>(v); kq += M.s[2] * dpp_d<0xAA>(q);  // [2,2,2,2]
+    dq += M.d[3] * dpp_d<0xFF>(v); kq += M.s[3] * dpp_d<0xFF>(q);  // [3,3,3,3]
+    const double r = T - dq - kq;
+    const double mr = dpp_d<0x141>(r);  // lane i <- lane 7 - i of the 8
+    double a = 0.0;
+    a += M.ii[0] * (upper ? dpp_d<0xFA>(mr) : dpp_d<0x14>(r));
+    a += M.ii[1] * (upper ? dpp_d<0x05>(mr) : dpp_d<0xEB>(r));
+    a += M.ii[2] * (upper ? dpp_d<0xA0>(r) : dpp_d<0x7D>(mr));
+    a += M.ii[3] * (upper ? dpp_d<0x55>(r) : dpp_d<0xAA>(mr));
+    return a;
+}
+
+// selects the pull form (template flag of rk45_rows)
+struct RowD {
+    RowM m;
+    bool upper;
+};
+__device__ __forceinline__ double row_acc(const RowD &M, double T, double q, double v) {
+    return row_acc_dpp(M.m, M.upper, T, q, v);
+}
+
 // acceleration of row r: I^-1 (T - D v - K q), neighbours pulled from the group
 __device__ __forceinline__ double row_acc(const RowM &M, double T, double q, double v) {
     double dq = 0.0, kq = 0.0;
@@ -100,7 +135,8 @@ __device__ __forceinline__ double row_acc(const RowM &M, double T, double q, dou
 
 // scipy RK45 (common.py select_initial_step, rk.py _step_impl) for the row
 // this lane owns; same second-order storage as rk45_solve in exo_model.h.
-__device__ bool rk45_rows(const RowM &M, double T, double &q_out) {
+template <typename RM>
+__device__ bool rk45_rows(const RM &M, double T, double &q_out) {
     const double rtol = 1e-3, atol = 1e-6, tb = DT, inv_sqrt14 = 1.0 / 3.7416573867739413;
     double q = 0.0, v = 0.0;
     double a0 = row_acc(M, T, q, v);
@@ -190,6 +226,7 @@ __device__ __forceinline__ void anchor(const Urdf &U, int link, const double *R2
 // and HBM fetched it up to four times (PMC: 3.1x the algorithmic bytes).
 constexpr int RP_ENVS_PER_BLOCK = 16;
 
+template <bool GATHER>
 __global__ __launch_bounds__(64 * RP_ENVS_PER_BLOCK / 4) void exo_step_rp_kernel(
     Dev S, Urdf U, const float *__restrict__ act, float *__restrict__ obs, float *__restrict__ rew,
     uint8_t *__restrict__ done, float *__restrict__ info, const uint8_t *__restrict__ active) {
@@ -213,6 +250,44 @@ __global__ __launch_bounds__(64 * RP_ENVS_PER_BLOCK / 4) void exo_step_rp_kernel
     for (int j = 0; j < 5; ++j) q5[j] = S.phys_q[(size_t)j * N + e];
 #pragma unroll
     for (int j = 0; j < 6; ++j) refo[j] = S.ref[(size_t)j * N + e];
+    // ---- every other load of the step, issued now: one memory latency for the
+    // whole step instead of one per phase (the loads go out in the order the
+    // phases below consume them; nothing is stored before this point)
+    const int j = r < 7 ? r : 6;  // this lane's actuator (lanes r == 7 duplicate actuator 6 and discard it)
+    double sh1[3], sh2[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        sh1[d] = S.shift[(size_t)((2 * j) * 3 + d) * N + e];
+        sh2[d] = S.shift[(size_t)((2 * j + 1) * 3 + d) * N + e];
+    }
+    double tr[7], pa[7], pa2[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+        tr[i] = S.tremor[((size_t)c * 7 + i) * N + e];
+        pa[i] = S.prev_a[(size_t)i * N + e];
+        pa2[i] = S.prev2_a[(size_t)i * N + e];
+    }
+    const double pa_j = S.prev_a[(size_t)j * N + e];
+    const double tr_j = S.tremor[((size_t)c * 7 + j) * N + e];
+    const int r4 = r & 3;  // tremor rows 0..3 of the observation at c - 1, c + 1
+    const double tm1 = S.tremor[((size_t)(c > 0 ? c - 1 : 0) * 7 + r4) * N + e];
+    const double tp1 = S.tremor[((size_t)(c + 1) * 7 + r4) * N + e];
+    const double c_naxes = cfg(S, C_NAXES, e), c_maxrew = cfg(S, C_MAXREW, e);
+    const double c_nrm = j < 2 ? cfg(S, C_MAXE0, e) : cfg(S, C_MAXS0, e);
+    float posv_old[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) posv_old[d] = S.posv[(size_t)(j * 3 + d) * N + e];
+    RowM M0;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int ds = RP_DSYM[r][m], is = RP_ISYM[r][m];
+        M0.d[m] = ds >= 0 ? S.dnz[(size_t)ds * N + e] : 0.0;
+        M0.s[m] = ds >= 0 ? S.snz[(size_t)ds * N + e] : 0.0;
+        M0.ii[m] = is >= 0 ? S.iinv[(size_t)is * N + e] : 0.0;
+        M0.dsrc[m] = gbase + RP_DCOL[r][m];
+        M0.isrc[m] = gbase + RP_ICOL[r][m];
+    }
+    const int seq = S.seq[e], motion = S.motion[e];
     double R2[9], R4[9], p0[3], p3[3];
     {
         double Rt[9], R0[9], R1[9], R3[9], s, cc;
@@ -229,7 +304,6 @@ __global__ __launch_bounds__(64 * RP_ENVS_PER_BLOCK / 4) void exo_step_rp_kernel
 
     STAMP(1);
     // ---- actuator j = r (lanes r == 7 duplicate actuator 6 and discard it)
-    const int j = r < 7 ? r : 6;
     double k1[3], k2[3], tx, ty, tz;
     float pv[3];
     {
@@ -241,8 +315,8 @@ __global__ __launch_bounds__(64 * RP_ENVS_PER_BLOCK / 4) void exo_step_rp_kernel
         }
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
-            k1[d] += S.shift[(size_t)((2 * j) * 3 + d) * N + e];
-            k2[d] += S.shift[(size_t)((2 * j + 1) * 3 + d) * N + e];
+            k1[d] += sh1[d];
+            k2[d] += sh2[d];
         }
         const double dx = (k2[0] + 5) - (k1[0] + 5), dy = (k2[1] + 5) - (k1[1] + 5), dz = (k2[2] + 5) - (k1[2] + 5);
         const double Fj = (((double)a[j] + 1) / 2) * (j < 2 ? maxE : maxS);
@@ -270,19 +344,13 @@ __global__ __launch_bounds__(64 * RP_ENVS_PER_BLOCK / 4) void exo_step_rp_kernel
     at[1] = tau[2][0] + tau[3][0] + tau[4][0] + tau[6][0] + tau[5][0];
     at[2] = tau[2][2] + tau[3][2] + tau[4][2] + tau[6][2] + tau[5][2];
     at[3] = fabs(tau[0][1]) - fabs(tau[1][1]);
-    double tr[7], Ta[7], pa[7], pa2[7];
+    double Ta[7];
 #pragma unroll
-    for (int i = 0; i < 7; ++i) {
-        tr[i] = S.tremor[((size_t)c * 7 + i) * N + e];
-        Ta[i] = tr[i] + (i < 4 ? at[i] : 0.0);
-        pa[i] = S.prev_a[(size_t)i * N + e];
-        pa2[i] = S.prev2_a[(size_t)i * N + e];
-    }
+    for (int i = 0; i < 7; ++i) Ta[i] = tr[i] + (i < 4 ? at[i] : 0.0);
     // per-lane values of this lane's actuator j / joint row r (dynamic indices
     // into small register arrays would go to scratch)
     const double F_j = (((double)a[j] + 1) / 2) * (j < 2 ? maxE : maxS);
-    const double pa_j = S.prev_a[(size_t)j * N + e];
-    const double tr_r = (r < 7) ? S.tremor[((size_t)c * 7 + r) * N + e] : 0.0;
+    const double tr_r = (r < 7) ? tr_j : 0.0;
     const double at_r = (r == 0) ? at[0] : (r == 1) ? at[1] : (r == 2) ? at[2] : (r == 3) ? at[3] : 0.0;
     const double Ta_r = tr_r + at_r;
     // every lane has read the carried state it needs; lanes of this env now
@@ -292,8 +360,7 @@ __global__ __launch_bounds__(64 * RP_ENVS_PER_BLOCK / 4) void exo_step_rp_kernel
     // ---- reward, done, observation, info, carried state (:341-366, :448-469, :487-570)
     if (grp == 0) {
         if (r == 0) {
-            const int seq = S.seq[e];
-            const double eps = 1e-10, Msum = maxE + maxS, naxes = cfg(S, C_NAXES, e);
+            const double eps = 1e-10, Msum = maxE + maxS, naxes = c_naxes;
             double unw = 0.0, st = 0.0, sa = 0.0, sm = 0.0;
             int nred = 0;
 #pragma unroll
@@ -315,7 +382,7 @@ __global__ __launch_bounds__(64 * RP_ENVS_PER_BLOCK / 4) void exo_step_rp_kernel
             const double r_axis = nred * 0.5;
             const double r_ctl = exp(-(sa / (Msum / 2)) + eps) * 0.05;
             const double r_sm = 0.05 * exp(-(sm / (Msum / 4)) + eps);
-            rew[e] = (float)((r_axis + r_tor + r_sm + r_ctl + r_unw) / cfg(S, C_MAXREW, e));
+            rew[e] = (float)((r_axis + r_tor + r_sm + r_ctl + r_unw) / c_maxrew);
             done[e] = (uint8_t)(c + 1 >= L - 1);
             if (info) {
                 float *io = info + (size_t)e * INFO;
@@ -326,13 +393,13 @@ __global__ __launch_bounds__(64 * RP_ENVS_PER_BLOCK / 4) void exo_step_rp_kernel
         }
         float *o = obs + (size_t)e * OBS;
         if (r < 7) {
-            const double nrm = j < 2 ? cfg(S, C_MAXE0, e) : cfg(S, C_MAXS0, e);
+            const double nrm = c_nrm;
             o[j] = (float)((c > 2 ? pa_j : 0.0) / nrm); // forces at c-1 (zero on an episode's first step)
             o[7 + j] = (float)(F_j / nrm);
 #pragma unroll
             for (int d = 0; d < 3; ++d) {
                 const size_t idx = (size_t)(j * 3 + d) * N + e;
-                o[26 + j * 3 + d] = S.posv[idx];
+                o[26 + j * 3 + d] = posv_old[d];
                 o[47 + j * 3 + d] = pv[d];
                 S.posv[idx] = pv[d];
             }
@@ -357,26 +424,22 @@ __global__ __launch_bounds__(64 * RP_ENVS_PER_BLOCK / 4) void exo_step_rp_kernel
         float *o = obs + (size_t)e * OBS;
 #pragma unroll
         for (int b = 0; b < 3; ++b) {
-            const double v = (b == 1) ? tr_r : S.tremor[((size_t)(c - 1 + b) * 7 + r) * N + e];
+            const double v = (b == 1) ? tr_r : (b == 0 ? tm1 : tp1);
             o[14 + b * 4 + r] = (float)(v / tn);
         }
     }
 
     STAMP(3);
     // ---- the two joint ODE solves (:409-414), one row per lane
-    RowM M;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        const int ds = RP_DSYM[r][m], is = RP_ISYM[r][m];
-        M.d[m] = ds >= 0 ? S.dnz[(size_t)ds * N + e] : 0.0;
-        M.s[m] = ds >= 0 ? S.snz[(size_t)ds * N + e] : 0.0;
-        M.ii[m] = is >= 0 ? S.iinv[(size_t)is * N + e] : 0.0;
-        M.dsrc[m] = gbase + RP_DCOL[r][m];
-        M.isrc[m] = gbase + RP_ICOL[r][m];
-    }
     const double T = (r < 7) ? (grp == 0 ? Ta_r : tr_r) : 0.0;
     double qr;
-    if (!rk45_rows(M, T, qr)) atomicOr(S.err, 1);
+    bool ok;
+    if constexpr (GATHER) {
+        ok = rk45_rows(RowD{M0, r >= 4}, T, qr);
+    } else {
+        ok = rk45_rows(M0, T, qr);
+    }
+    if (!ok) atomicOr(S.err, 1);
     STAMP(4);
     const double qdeg = qr * (180 / PI); // :417-418
     if (info && r < 7) info[(size_t)e * INFO + (grp == 0 ? 14 : 28) + r] = (float)qdeg;
@@ -385,7 +448,7 @@ __global__ __launch_bounds__(64 * RP_ENVS_PER_BLOCK / 4) void exo_step_rp_kernel
     // ---- :421-433 joint targets and the idealised motor step
     // lane r holds q[r]: joint 0 (shoulder z) <- q[2], 1 (y) <- q[0], 2 (x) <- q[1], 3 (elbow y) <- q[3]
     const int joint = (r == 0) ? 1 : (r == 1) ? 2 : (r == 2) ? 0 : r; // r = 3, 4 -> joints 3, 4
-    const double *imu = S.imu + (size_t)S.motion[e] * 5 * S.Lmax;
+    const double *imu = S.imu + (size_t)motion * 5 * S.Lmax;
     const int col = (joint == 0) ? 4 : (joint == 1) ? 3 : (joint == 2) ? 2 : (joint == 3) ? 0 : 1;
     const double ang = imu[col * S.Lmax + c] + (joint < 4 ? qdeg : 0.0);
     bool viol = false;
@@ -417,9 +480,19 @@ extern "C" int exo_debug_set_stamps(unsigned long long *buf) {
 namespace exo {
 hipError_t launch_exo_step_rp(const Dev &S, const Urdf &U, const float *act, float *obs, float *rew, uint8_t *done,
                               float *info, const uint8_t *active, hipStream_t stream) {
-    hipLaunchKernelGGL(exo_step_rp_kernel, dim3((S.N + RP_ENVS_PER_BLOCK - 1) / RP_ENVS_PER_BLOCK),
-                       dim3(64 * RP_ENVS_PER_BLOCK / 4), 0, stream, S, U, act, obs, rew, done, info,
-                       active);
+    // RHS neighbour pulls: LDS permutes (default) or DPP lane moves (EXO_RP_GATHER=1:
+    // bit-identical, measured slower -- 38.2 vs 34.9 us at 4,096 envs; the fp64
+    // pulls are two dword moves each plus the DPP hazard waits, where the
+    // permutes run on the LDS pipe beside the VALU)
+    static const bool gather = [] {
+        const char *v = getenv("EXO_RP_GATHER");
+        return v && v[0] == '1';
+    }();
+    const dim3 grid((S.N + RP_ENVS_PER_BLOCK - 1) / RP_ENVS_PER_BLOCK), block(64 * RP_ENVS_PER_BLOCK / 4);
+    if (gather)
+        hipLaunchKernelGGL(exo_step_rp_kernel<true>, grid, block, 0, stream, S, U, act, obs, rew, done, info, active);
+    else
+        hipLaunchKernelGGL(exo_step_rp_kernel<false>, grid, block, 0, stream, S, U, act, obs, rew, done, info, active);
     return hipGetLastError();
 }
 } // namespace exo
