@@ -147,26 +147,42 @@ class LAP:
                                             self._stream()), "lap_store_batch")
 
     # ------------------------------------------------------------- sample
-    def sample(self):
+    def _slot(self, slot):
+        """Batch buffers of sample(slot=...): the vectorised trainer samples the
+        next iteration's batch into the other slot while this one is in use."""
+        if slot is None:
+            return self._batch, self._idx
+        if not hasattr(self, "_slots"):
+            self._slots = {}
+        if slot not in self._slots:
+            f32 = dict(device=self.device, dtype=torch.float32)
+            B, (S, A) = self._batch[0].shape[0], (self._batch[0].shape[1], self._batch[1].shape[1])
+            sn = torch.empty((2, B, S), **f32)
+            self._slots[slot] = ((sn[0], torch.empty((B, A), **f32), sn[1], torch.empty((B, 1), **f32),
+                                  torch.empty((B, 1), **f32)), torch.empty_like(self._idx))
+        return self._slots[slot]
+
+    def sample(self, slot=None):
         """Agent/TD7_buffer_multi_agent.py:65-111: batch_size rows from every
         stratum, stratum-major, as float32 device tensors (lap_sample_gather:
         descent + gather in one kernel; the returned tensors are reused by the
-        next call)."""
+        next call with the same slot).  self.ind = the sampled indices."""
+        batch, idx = self._slot(slot)
         if self.device_rng:
             # the uniforms drawn inside the kernel (ops.DeviceRNG): no generator launch
             r = self._rng
             nat.check(nat.lib().lap_sample_gather_rng(ctypes.byref(self._desc), ctypes.byref(self._store), r.seed,
                                                       r.tag, r.counter_ptr, r.ticket_ptr, self.batch_size,
-                                                      nat.ptr(self._idx), *[nat.ptr(t) for t in self._batch],
+                                                      nat.ptr(idx), *[nat.ptr(t) for t in batch],
                                                       self._stream()), "lap_sample_gather_rng")
         else:
             self._u.uniform_()
             nat.check(nat.lib().lap_sample_gather(ctypes.byref(self._desc), ctypes.byref(self._store),
-                                                  nat.ptr(self._u), self.batch_size, nat.ptr(self._idx),
-                                                  *[nat.ptr(t) for t in self._batch], self._stream()),
+                                                  nat.ptr(self._u), self.batch_size, nat.ptr(idx),
+                                                  *[nat.ptr(t) for t in batch], self._stream()),
                       "lap_sample_gather")
-        self.ind = self._idx
-        return self._batch
+        self.ind = idx
+        return batch
 
     def sample_indices(self, u):
         """Indices for given uniforms u [E, batch] (parity hook)."""

@@ -155,7 +155,13 @@ class VecTrainer:
         outs = [env.new_outputs(True), env.new_outputs(True)]
         self._outs = [(self._obs[1], *outs[0][1:]), (self._obs[0], *outs[1][1:])]
         self._cur = 0
-        self.active = self.active_table[0].clone()
+        # this step's active mask: the rollout ends by advancing the device step
+        # counter k_dev and selecting the NEXT step's row of the table (an extra
+        # all-False row past the round's end keeps the index in range), so no
+        # host copy runs between graph replays and nothing waits for it
+        self._table_ext = torch.cat([self.active_table, torch.zeros_like(self.active_table[:1])])
+        self._active2d = self.active_table[0:1].clone()
+        self.active = self._active2d[0]
         self.k = 0
         self.use_graphs = use_graphs
         self.warmup_eager = warmup_eager
@@ -182,6 +188,8 @@ class VecTrainer:
         act = ag.select_action_batch(obs, timestep=self.k_dev if self.exploration == "pink" else None)
         nobs, rew, done, info = self.env.step(act, active=self.active, out=self._outs[self._cur])
         ag.replay_buffer.add_batch(obs, act, nobs, rew, done, self.strata, self.active)
+        self.k_dev.add_(1)
+        torch.index_select(self._table_ext, 0, self.k_dev, out=self._active2d)
         self.last_actions = act
 
     @property
@@ -206,15 +214,32 @@ class VecTrainer:
     # bursts after each episode round anyway, Exoskeleton_agent_train.py:208).
     # EXO_ROLLOUT_OVERLAP=0 keeps the serial insert-then-sample order.
     overlap_rollout = os.environ.get("EXO_ROLLOUT_OVERLAP", "1") == "1"
+    # With the rollout overlapped, iteration t+1's batch (which must follow
+    # iteration t's inserts and priority update, and nothing else) is sampled
+    # at the end of iteration t, on the priority branch, into the other of two
+    # batch slots (slot = observation-buffer parity, so a captured graph keeps
+    # reading the slot it was captured with): the sample leaves the head of the
+    # iteration's critical path.  EXO_SAMPLE_PREFETCH=0 samples at the start.
+    prefetch_sample = os.environ.get("EXO_SAMPLE_PREFETCH", "1") == "1"
+
+    def _prefetching(self):
+        return self.prefetch_sample and self.overlap_rollout
 
     def _pre(self):
         ag = self.agent
+        rb = ag.replay_buffer
+        slot = self._cur if self._prefetching() else None
         if self.iters == 0 or not self.overlap_rollout:
             self._rollout()
-            self._batch = ag.replay_buffer.sample()
+            self._batch = rb.sample(slot)
+            self._ind = rb.ind
             self._prio = ag.learner.phase_grads(*self._batch)
             return
-        self._batch = ag.replay_buffer.sample()
+        if self._prefetching():
+            self._batch, self._ind = rb._slot(slot)  # sampled by the previous iteration
+        else:
+            self._batch = rb.sample()
+            self._ind = rb.ind
         cur = torch.cuda.current_stream(self.device)
         if getattr(self, "_rollout_stream", None) is None:
             self._rollout_stream = torch.cuda.Stream(device=self.device)
@@ -243,13 +268,19 @@ class VecTrainer:
             self._pside = self._prio_stream
             self._pside.wait_stream(cur)
             with torch.cuda.stream(self._pside):
-                ag.replay_buffer.update_priority(self._prio)
+                ag.replay_buffer.update_priority(self._prio, self._ind)
+                self._sample_next()
             ag.learner.phase_steps(flat_grad, grad_scale)
         else:
             ag.learner.phase_steps(flat_grad, grad_scale)
-            ag.replay_buffer.update_priority(self._prio)
+            ag.replay_buffer.update_priority(self._prio, self._ind)
+            self._sample_next()
         if update_actor:
             ag.learner.phase_actor_grads(self._batch[0], self._batch[1])
+
+    def _sample_next(self):
+        if self._prefetching():
+            self.agent.replay_buffer.sample(1 - self._cur)
 
     def _join_prio(self):
         if getattr(self, "_pside", None) is not None:
@@ -336,12 +367,11 @@ class VecTrainer:
         if self.k == self.round_len:
             self.env.reset(obs_out=self.obs)
             self.k = 0
+            self.k_dev.zero_()
+            self._active2d.copy_(self.active_table[0:1])
             self.resets += 1
             if self.exploration == "pink":
                 ag.init_episode_noise_device(self.round_len)
-        self.active.copy_(self.active_table[self.k])
-        if self.exploration == "pink":
-            self.k_dev.fill_(self.k)
         L.training_steps += 1
         update_actor = L.training_steps % ag.hp.policy_freq == 0
         L.prefetch_actor = update_actor  # phase_grads may start the actor forward early

@@ -92,5 +92,5 @@ def test_pink_exploration_trainer_runs_in_graphs():
     for _ in range(8):
         tr.step()
     torch.cuda.synchronize()
-    assert len(tr.graphs) == 2 and int(tr.k_dev) == 7
+    assert len(tr.graphs) == 2 and int(tr.k_dev) == 8  # one increment per rollout
     assert torch.isfinite(tr.last_actions).all() and float(tr.last_actions.abs().max()) <= 1.0
