@@ -613,6 +613,20 @@ __global__ void eval_metrics_kernel(Dev S, const float *__restrict__ info, const
     }
 }
 
+// The synchronous-episode trainer's active mask (Simulation/Exoskeleton_agent_
+// train.py:123-125: an env steps while its motion lasts): the step counter k
+// (device int64) advances by one, saturating at rows - 1, and row k of the
+// [rows][n] table is copied to active -- one single-workgroup launch inside
+// the captured iteration, safe however many times a graph is replayed.
+__global__ __launch_bounds__(1024) void active_advance_kernel(const uint8_t *__restrict__ table, int rows, int n,
+                                                              long long *k, uint8_t *__restrict__ active) {
+    const long long k0 = *k;
+    const long long kk = k0 + 1 < rows ? k0 + 1 : rows - 1;
+    for (int e = threadIdx.x; e < n; e += blockDim.x) active[e] = table[(size_t)kk * n + e];
+    __syncthreads();
+    if (threadIdx.x == 0) *k = kk;
+}
+
 struct exo_ctx {
     int device = 0;
     int N = 0, n_motions = 0, Lmax = 0;
@@ -1036,6 +1050,14 @@ int exo_tremor_metrics(exo_ctx *c, const float *info_dev, const uint8_t *stepped
     hipLaunchKernelGGL(tremor_metrics_kernel, dim3((c->N + 255) / 256), dim3(256), 0, (hipStream_t)stream, c->S,
                        info_dev, stepped_dev, humerus_length, forearm_length, disregard, metrics_dev, counters_dev);
     return check(c, hipGetLastError(), "exo_tremor_metrics");
+}
+
+int exo_active_advance(const uint8_t *table_dev, int32_t rows, int32_t n, int64_t *k_dev, uint8_t *active_dev,
+                       void *stream) {
+    if (!table_dev || !k_dev || !active_dev || rows <= 0 || n <= 0) return EXO_EINVAL;
+    hipLaunchKernelGGL(active_advance_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, table_dev, rows, n,
+                       (long long *)k_dev, active_dev);
+    return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 
 int exo_eval_metrics(exo_ctx *c, const float *info_dev, const uint8_t *stepped_dev, double humerus_length,

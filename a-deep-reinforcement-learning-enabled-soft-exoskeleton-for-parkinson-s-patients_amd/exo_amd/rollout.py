@@ -156,12 +156,11 @@ class VecTrainer:
         self._outs = [(self._obs[1], *outs[0][1:]), (self._obs[0], *outs[1][1:])]
         self._cur = 0
         # this step's active mask: the rollout ends by advancing the device step
-        # counter k_dev and selecting the NEXT step's row of the table (an extra
-        # all-False row past the round's end keeps the index in range), so no
-        # host copy runs between graph replays and nothing waits for it
-        self._table_ext = torch.cat([self.active_table, torch.zeros_like(self.active_table[:1])])
-        self._active2d = self.active_table[0:1].clone()
-        self.active = self._active2d[0]
+        # counter k_dev and copying the NEXT step's row of the table
+        # (exo_active_advance; an extra all-False row past the round's end, where
+        # the counter saturates), so no host copy runs between graph replays
+        self._table_ext = torch.cat([self.active_table, torch.zeros_like(self.active_table[:1])]).contiguous()
+        self.active = self.active_table[0].clone()
         self.k = 0
         self.use_graphs = use_graphs
         self.warmup_eager = warmup_eager
@@ -188,8 +187,9 @@ class VecTrainer:
         act = ag.select_action_batch(obs, timestep=self.k_dev if self.exploration == "pink" else None)
         nobs, rew, done, info = self.env.step(act, active=self.active, out=self._outs[self._cur])
         ag.replay_buffer.add_batch(obs, act, nobs, rew, done, self.strata, self.active)
-        self.k_dev.add_(1)
-        torch.index_select(self._table_ext, 0, self.k_dev, out=self._active2d)
+        nat.check(nat.lib().exo_active_advance(nat.ptr(self._table_ext), self._table_ext.shape[0], self.n,
+                                               nat.ptr(self.k_dev), nat.ptr(self.active), nat.stream_ptr(self.device)),
+                  "exo_active_advance")
         self.last_actions = act
 
     @property
@@ -368,7 +368,7 @@ class VecTrainer:
             self.env.reset(obs_out=self.obs)
             self.k = 0
             self.k_dev.zero_()
-            self._active2d.copy_(self.active_table[0:1])
+            self.active.copy_(self.active_table[0])
             self.resets += 1
             if self.exploration == "pink":
                 ag.init_episode_noise_device(self.round_len)

@@ -187,6 +187,13 @@ int exo_tremor_metrics(exo_ctx *c, const float *info_dev, const uint8_t *stepped
  *     (tremor_when_ampl_reduction[i, 1] / [i, 0]),
  *   the sum of the negative changes (for the episode mean over non-zero
  *     entries of tremor_ampl_total_reduction_full_ep, :262). */
+/* The synchronous-episode trainer's active mask on the device
+ * (Simulation/Exoskeleton_agent_train.py:123-125): *k_dev (int64) advances by
+ * one, saturating at rows - 1, and row *k_dev of table_dev [rows][n] (uint8)
+ * is copied to active_dev [n].  Graph-capturable, no host sync. */
+int exo_active_advance(const uint8_t *table_dev, int32_t rows, int32_t n, int64_t *k_dev, uint8_t *active_dev,
+                       void *stream);
+
 int exo_eval_metrics(exo_ctx *c, const float *info_dev, const uint8_t *stepped_dev, double humerus_length,
                      double forearm_length, float *counters_dev, void *stream);
 

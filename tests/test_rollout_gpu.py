@@ -94,3 +94,19 @@ def test_pink_exploration_trainer_runs_in_graphs():
     torch.cuda.synchronize()
     assert len(tr.graphs) == 2 and int(tr.k_dev) == 8  # one increment per rollout
     assert torch.isfinite(tr.last_actions).all() and float(tr.last_actions.abs().max()) <= 1.0
+
+
+def test_active_advance_saturates_and_copies_rows():
+    """exo_active_advance: the device step counter advances by one per call and
+    saturates at the last row, whose copy lands in the active mask (graph
+    replays past a round's end stay in bounds)."""
+    from exo_amd import _native as nat
+    table = (torch.arange(4 * 70, device="cuda").view(4, 70) % 3 == 0).contiguous()
+    k = torch.zeros(1, dtype=torch.int64, device="cuda")
+    act = torch.zeros(70, dtype=torch.bool, device="cuda")
+    for want in (1, 2, 3, 3, 3):
+        nat.check(nat.lib().exo_active_advance(nat.ptr(table), 4, 70, nat.ptr(k), nat.ptr(act),
+                                               nat.stream_ptr(torch.device("cuda", 0))), "exo_active_advance")
+        torch.cuda.synchronize()
+        assert int(k) == want
+        assert torch.equal(act, table[want])
