@@ -33,43 +33,54 @@ struct PackArgs {
     PackJob j[TD7F_MAX_PACK];
 };
 
+// One job per grid row (blockIdx.y: the job's descriptor is uniform -- scalar
+// loads, no search), one 16-byte item per thread.  A forward item is 8
+// consecutive inputs of one output row: two 16-byte loads when they lie inside
+// the matrix and the rows are 16-byte aligned; every other load is issued
+// unconditionally from a clamped address and masked after (no branch splits
+// the batch of loads).
+template <int P>
+__device__ __forceinline__ float w_at(const PackJob &J, int n, int c) {
+    const bool ok = n < J.N && c < J.K;
+    const float x = ldg(J.w + (long)(ok ? n : 0) * J.ld + (ok ? c : 0));
+    return ok ? x : 0.f;
+}
 template <int P>
 __global__ __launch_bounds__(256) void pack_kernel(PackArgs a) {
-    const long total = a.start[a.njobs];
-    for (long it = (long)blockIdx.x * 256 + threadIdx.x; it < total; it += (long)gridDim.x * 256) {
-        int q = 0;
-        while (it >= a.start[q + 1]) ++q;
-        const PackJob &J = a.j[q];
-        long k = it - a.start[q];
-        const long nf = (long)J.ntf * J.ksf * 64;
+    const PackJob J = a.j[blockIdx.y];
+    const long nf = (long)J.ntf * J.ksf * 64, total = nf + (long)J.ntb * J.ksb * 64;
+    const bool vec = (J.ld % 4) == 0 && (reinterpret_cast<uintptr_t>(J.w) & 15) == 0;
+    for (long k = (long)blockIdx.x * 256 + threadIdx.x; k < total; k += (long)gridDim.x * 256) {
         const int l = (int)(k & 63);
-        uint32_t v[4];
+        float x[8];
+        u32x4 *dst;
         if (k < nf) {  // forward: W[16t + (l&15)][32s + 8(l>>4) + j]
             const long blk = k >> 6;
             const int t = (int)(blk / J.ksf), s = (int)(blk % J.ksf);
             const int n = 16 * t + (l & 15), k0 = 32 * s + 8 * (l >> 4);
+            if (vec && n < J.N && k0 + 8 <= J.K) {
+                const floatx4 a0 = ldg((const floatx4 *)(J.w + (long)n * J.ld + k0));
+                const floatx4 a1 = ldg((const floatx4 *)(J.w + (long)n * J.ld + k0 + 4));
+                x[0] = a0[0], x[1] = a0[1], x[2] = a0[2], x[3] = a0[3];
+                x[4] = a1[0], x[5] = a1[1], x[6] = a1[2], x[7] = a1[3];
+            } else {
 #pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-                const int c = k0 + 2 * jj;
-                const float x0 = (n < J.N && c < J.K) ? J.w[(long)n * J.ld + c] : 0.f;
-                const float x1 = (n < J.N && c + 1 < J.K) ? J.w[(long)n * J.ld + c + 1] : 0.f;
-                v[jj] = (uint32_t)Ty<P>::bits(x0) | ((uint32_t)Ty<P>::bits(x1) << 16);
+                for (int j = 0; j < 8; ++j) x[j] = w_at<P>(J, n, k0 + j);
             }
-            J.wf[k] = u32x4{v[0], v[1], v[2], v[3]};
+            dst = J.wf + k;
         } else {  // dX: W[32s + 8(l>>4) + j][16t + (l&15)]
-            k -= nf;
-            const long blk = k >> 6;
+            const long blk = (k - nf) >> 6;
             const int t = (int)(blk / J.ksb), s = (int)(blk % J.ksb);
             const int c = 16 * t + (l & 15), n0 = 32 * s + 8 * (l >> 4);
 #pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-                const int n = n0 + 2 * jj;
-                const float x0 = (n < J.N && c < J.K) ? J.w[(long)n * J.ld + c] : 0.f;
-                const float x1 = (n + 1 < J.N && c < J.K) ? J.w[(long)(n + 1) * J.ld + c] : 0.f;
-                v[jj] = (uint32_t)Ty<P>::bits(x0) | ((uint32_t)Ty<P>::bits(x1) << 16);
-            }
-            J.wb[k] = u32x4{v[0], v[1], v[2], v[3]};
+            for (int j = 0; j < 8; ++j) x[j] = w_at<P>(J, n0 + j, c);
+            dst = J.wb + (k - nf);
         }
+        uint32_t v[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+            v[jj] = (uint32_t)Ty<P>::bits(x[2 * jj]) | ((uint32_t)Ty<P>::bits(x[2 * jj + 1]) << 16);
+        stg(dst, u32x4{v[0], v[1], v[2], v[3]});
     }
 }
 
@@ -283,12 +294,13 @@ int td7f_pack(int32_t prec, int32_t njobs, const td7f_pack_job *jobs, void *stre
                          J.wb ? J.ksb : 0, J.wb ? J.ntb : 0};
         a.start[q + 1] = a.start[q] + (long)J.ntf * J.ksf * 64 + (J.wb ? (long)J.ntb * J.ksb * 64 : 0);
     }
-    const long total = a.start[njobs];
-    const int blocks = (int)std::min<long>(2048, (total + 255) / 256);
+    long most = 0;
+    for (int q = 0; q < njobs; ++q) most = std::max(most, a.start[q + 1] - a.start[q]);
+    const dim3 grid((unsigned)std::min<long>(1024, (most + 255) / 256), (unsigned)njobs);
     if (prec == PREC_BF16)
-        hipLaunchKernelGGL(pack_kernel<PREC_BF16>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
+        hipLaunchKernelGGL(pack_kernel<PREC_BF16>, grid, dim3(256), 0, (hipStream_t)stream, a);
     else
-        hipLaunchKernelGGL(pack_kernel<PREC_F16>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
+        hipLaunchKernelGGL(pack_kernel<PREC_F16>, grid, dim3(256), 0, (hipStream_t)stream, a);
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 
