@@ -14,6 +14,7 @@
 #include "td7_fused.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "philox.h"
 
@@ -85,9 +86,11 @@ __global__ __launch_bounds__(256) void pack_kernel(PackArgs a) {
 }
 
 // ---------------------------------------------------------------- select_action
-// rows per workgroup = 16 SELECT_RT: 1 puts a workgroup on every CU at 4,096 envs
-// (the weight stream per CU, not the MFMA work, bounds these passes)
-constexpr int SELECT_RT = 1;
+// Rows per workgroup = 16 RT.  RT = 1 gives a 4,096-env call one workgroup per
+// CU (fastest alone: the per-CU weight stream bounds the pass); RT = 2 reads
+// each weight half as often and leaves half of the CUs to the graph branches
+// that run beside select_action (EXO_SELECT_RT).  F (the fp32 norm input)
+// overlays H1 | H2, dead whenever F is written.
 struct SelectArgs {
     Lin zs[3], ac[4];
     int act_enc, act_actor;
@@ -96,7 +99,7 @@ struct SelectArgs {
     float *out;
     Noise nz;
     R16 X, H1, H2, CAT;
-    R32 F, TW;
+    R32 F, TW, FT;
     int lds_bytes;
 };
 
@@ -104,21 +107,26 @@ struct SelectArgs {
     u32x4 R[PD][TH];           \
     ring_fill(R, GDesc{(first).wf, (first).ksf, 0})
 
-template <int P, int TH>
+__device__ __forceinline__ R16 rows_of(R16 r, int t) { return R16{r.off + t * TR * r.ld * 2, r.ld}; }
+__device__ __forceinline__ R32 rows_of(R32 r, int t) { return R32{r.off + t * TR * r.ld * 4, r.ld}; }
+
+template <int P, int TH, int RT>
 __global__ __launch_bounds__(NTH) void select_kernel(SelectArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
-    constexpr int RT = SELECT_RT, rows = RT * TR;
+    constexpr int rows = RT * TR;
     const int row0 = blockIdx.x * rows;
     int si = 0;
     FSTAMP(si);
-    RowStage so;
+    RowStage so[RT];
     ThinStage<THIN_NC> tw;
-    row_issue(so, a.obs, a.S, a.S, row0, a.n);
+#pragma unroll
+    for (int t = 0; t < RT; ++t) row_issue(so[t], a.obs, a.S, a.S, row0 + t * TR, a.n);
     thin_issue(tw, a.ac[3].w, a.ac[3].ldw, 0, false, a.A, a.ac[3].K);
     RING_START(a.zs[0]);
     zero_lds(lds, a.lds_bytes);
     __syncthreads();
-    row_put16<P>(lds, so, a.X, 0, a.S, row0, a.n);
+#pragma unroll
+    for (int t = 0; t < RT; ++t) row_put16<P>(lds, so[t], rows_of(a.X, t), 0, a.S, row0 + t * TR, a.n);
     thin_put<P>(lds, tw, a.TW, a.A, a.ac[3].K);
     __syncthreads();
     // zs = fixed_encoder.zs(obs) (:93-97) -> CAT[:, Ha:Ha+Z]
@@ -131,10 +139,27 @@ __global__ __launch_bounds__(NTH) void select_kernel(SelectArgs a) {
     layer_fwd<P, RT, TH>(lds, R, a.X, a.ac[0], &a.ac[1], ACT_NONE, NO16, 0, a.F, nullptr, 0, row0, a.n, si);
     norm_fwd<P>(lds, a.F, a.Ha, rows, 1e-8f, a.CAT, 0, NO16, 0, NO32, nullptr, 0, nullptr, nullptr, row0, a.n);
     __syncthreads();
+    // F overlaid H1 | H2: their zero padding columns (read by the GEMMs below
+    // where the width is not a multiple of 32 PD) are restored before the
+    // epilogues write H1 / H2 (those come after each GEMM's exchange barrier)
+    if (a.F.off == a.H1.off) zero_lds(lds + a.H1.off, a.H2.off + rows * a.H2.ld * 2 - a.H1.off);
     layer_fwd<P, RT, TH>(lds, R, a.CAT, a.ac[1], &a.ac[2], a.act_actor, a.H1, 0, NO32, nullptr, 0, row0, a.n, si);
     layer_fwd<P, RT, TH>(lds, R, a.H1, a.ac[2], (const Lin *)nullptr, a.act_actor, a.H2, 0, NO32, nullptr, 0, row0, a.n, si);
-    layer_thin_fwd<P, THIN_NC>(lds, a.H2, a.ac[3], a.TW, ACT_TANH, a.F, rows, nullptr, 0, row0, a.n, si);
-    noise_rows<P>(lds, a.F, a.A, rows, row0, a.n, a.nz, a.out, NO16, 0, NO16, 0);
+    if constexpr (RT == 1) {
+        layer_thin_fwd<P, THIN_NC>(lds, a.H2, a.ac[3], a.TW, ACT_TANH, a.FT, rows, nullptr, 0, row0, a.n, si);
+    } else {  // thin products per 16-row tile, then bias + tanh over all rows
+        FSTAMP(si);
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+            thin<P, THIN_NC>(lds, rows_of(a.H2, t), 0, a.ac[3].K, a.TW, a.A, rows_of(a.FT, t), 1.f);
+        __syncthreads();
+        for (int k = threadIdx.x; k < rows * a.A; k += NTH) {
+            const int row = k / a.A, c = k - row * a.A;
+            *p32(lds, a.FT, row, c) = act_fwd(ACT_TANH, *p32(lds, a.FT, row, c) + ldg(a.ac[3].b + c));
+        }
+        __syncthreads();
+    }
+    noise_rows<P>(lds, a.FT, a.A, rows, row0, a.n, a.nz, a.out, NO16, 0, NO16, 0);
 }
 
 // ---------------------------------------------------------------- critic target chain
@@ -325,16 +350,34 @@ int td7f_select(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7
     if (actor[0].n_in != a.S || actor[1].n_in != a.Ha + a.Z || a.A > THIN_NC || a.S > NTH) return EXO_EINVAL;
     a.out = out;
     a.nz = noise_of(*noise);
-    const int rows = SELECT_RT * TR, hmax = std::max(enc[0].n_out, std::max(enc[1].n_out, std::max(a.Ha, actor[1].n_out)));
-    Bump b(rows / TR);
+    const char *rt_env = getenv("EXO_SELECT_RT");  // read per call: tests switch it
+    const int RT = rt_env && rt_env[0] == '2' ? 2 : 1;
+    const int rows = RT * TR, hmax = std::max(enc[0].n_out, std::max(enc[1].n_out, std::max(a.Ha, actor[1].n_out)));
+    Bump b(RT);
     a.X = b.r16(rows, ld16(a.S));
     a.H1 = b.r16(rows, ld16(hmax));
     a.H2 = b.r16(rows, ld16(hmax));
+    const int fld = std::max(std::max(a.Z, a.Ha), 16);
+    if (rows * fld * 4 <= a.H2.off + rows * a.H2.ld * 2 - a.H1.off) {
+        a.F = R32{a.H1.off, fld};  // overlays H1 | H2 (both dead whenever F is written)
+    } else {
+        a.F = b.r32(rows, fld);
+    }
     a.CAT = b.r16(rows, ld16(a.Ha + a.Z));
-    a.F = b.r32(rows, std::max(std::max(a.Z, a.Ha), 16));
     a.TW = b.r32(THIN_NC, actor[3].n_in);
+    a.FT = b.r32(rows, 16);
     a.lds_bytes = b.off;
-    return DISPATCH(prec, th, select_kernel, dim3((n + rows - 1) / rows), b.off, a, (hipStream_t)stream);
+    const dim3 grid((n + rows - 1) / rows);
+    const hipStream_t st = (hipStream_t)stream;
+    if (RT == 2)
+        return prec == PREC_BF16 ? (th == 5 ? launch(select_kernel<PREC_BF16, 5, 2>, grid, b.off, a, st)
+                                            : launch(select_kernel<PREC_BF16, 4, 2>, grid, b.off, a, st))
+                                 : (th == 5 ? launch(select_kernel<PREC_F16, 5, 2>, grid, b.off, a, st)
+                                            : launch(select_kernel<PREC_F16, 4, 2>, grid, b.off, a, st));
+    return prec == PREC_BF16 ? (th == 5 ? launch(select_kernel<PREC_BF16, 5, 1>, grid, b.off, a, st)
+                                        : launch(select_kernel<PREC_BF16, 4, 1>, grid, b.off, a, st))
+                             : (th == 5 ? launch(select_kernel<PREC_F16, 5, 1>, grid, b.off, a, st)
+                                        : launch(select_kernel<PREC_F16, 4, 1>, grid, b.off, a, st));
 }
 
 int td7f_target(int32_t prec, const int32_t *act, const td7f_lin *tenc, const td7f_lin *tactor,

@@ -85,11 +85,15 @@ def test_target_chain_matches_per_layer(precision, width, B):
     assert _rel(qt, qt_ref) < REL, _rel(qt, qt_ref)
 
 
-@pytest.mark.parametrize("precision,width,n", [("bf16", None, 4096), ("bf16", None, 1000), ("fp16", None, 4096),
-                                               ("bf16", 256, 96)])
-def test_select_action_matches_per_layer(precision, width, n):
+@pytest.mark.parametrize("precision,width,n,rt", [("bf16", None, 4096, "1"), ("bf16", None, 1000, "1"),
+                                                  ("fp16", None, 4096, "1"), ("bf16", 256, 96, "1"),
+                                                  ("bf16", None, 4096, "2"), ("bf16", None, 1000, "2"),
+                                                  ("fp16", 256, 96, "2")])
+def test_select_action_matches_per_layer(precision, width, n, rt, monkeypatch):
     """Same Philox draws (the exploration stream's counter is rewound), same
-    decrement of exploration_noise (once per env), same clamp."""
+    decrement of exploration_noise (once per env), same clamp; 16 and 32 rows
+    per workgroup (EXO_SELECT_RT)."""
+    monkeypatch.setenv("EXO_SELECT_RT", rt)
     L = _learner(precision, width)
     obs, _ = _inputs(n, 2)
     rng = L._explore_rng
