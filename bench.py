@@ -261,6 +261,62 @@ def critic_gemm_timing(agent, reps=20, replays=10):
     return us, 2.0 * 2 * B * c.w1.shape[1] * c.w1.shape[2]
 
 
+# per-CU L2 weight-stream rate, warm (tools/stream_bench.hip, profiles/r02b_raw/stream_bench.txt:
+# 4-16 waves x 12-25 16-byte loads in flight per wave, 64 workgroups: 112-125 GB/s)
+L2_STREAM_PER_CU_GBS = 125.0
+
+
+def fused_critic_timing(agent, reps=20, replays=10):
+    """The fused critic update pass alone (td7f_critic, csrc/td7_fused_train.hip:
+    both heads' forward, LAP-Huber loss and backward to the gradient operands,
+    Agent/TD7_multi_agent.py:248-262), graph-captured, HIP events around the
+    replays.  Returns dict(us, mfma flop, weight bytes per workgroup,
+    workgroups) or None when the fused path is off."""
+    from exo_amd.fused import _ks, _tiles
+    L = agent.learner
+    fz = L.fused
+    if fz is None:
+        return None
+    hp = agent.hp
+    B = hp.batch_size * agent.env_num
+    dev = L.device
+    tr = fz.train(B)
+    S, A, Z, Hc = tr.S, tr.A, hp.zs_dim, hp.critic_hdim
+    g = torch.Generator(device=dev).manual_seed(0)
+    state = torch.randn(B, S, device=dev, generator=g)
+    action = torch.rand(B, A, device=dev, generator=g) * 2 - 1
+    zs, zsa = torch.randn(B, Z, device=dev, generator=g), torch.randn(B, Z, device=dev, generator=g)
+    qt = torch.randn(B, 2, device=dev, generator=g)
+    reward, nd = torch.rand(B, 1, device=dev, generator=g), torch.ones(B, 1, device=dev)
+    fn = lambda: tr.critic(state, action, zs, zsa, qt, reward, nd)  # noqa: E731
+    fn()
+    st = torch.cuda.Stream(device=dev)
+    st.wait_stream(torch.cuda.current_stream(dev))
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(st):
+        with torch.cuda.graph(gr, stream=st):
+            for _ in range(reps):
+                fn()
+    torch.cuda.current_stream(dev).wait_stream(st)
+    gr.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(replays):
+        gr.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / (reps * replays) * 1e3
+    # MFMA work of both heads (the N = 1 head on the VALU excluded): forward
+    # q0, q1, q2; backward dX of q2 and of q1's q window (q0's dX is not needed)
+    flop = 2 * (2.0 * B * (Hc * (S + A) + Hc * (Hc + 2 * Z) + Hc * Hc) + 2.0 * B * (Hc * Hc + Hc * Hc))
+    # weight fragments one workgroup (16 rows, one head) streams: the forward
+    # packs of q0, q1, q2 and the dX packs of q2 and of q1's first Hc inputs
+    kib = 1024
+    per_wg = kib * _tiles(Hc) * (_ks(S + A) + _ks(Hc + 2 * Z) + _ks(Hc)) + kib * _ks(Hc) * (_tiles(Hc) + Hc // 16)
+    return {"us": us, "flop": flop, "bytes_per_wg": per_wg, "workgroups": 2 * (-(-B // 16))}
+
+
 # the reference's update-to-data ratio: per episode round of its 8 envs
 # (Σ(L-3) = 2,257 active env-steps) it trains round(mean(ep_len)) = 283 steps
 # (Simulation/Exoskeleton_agent_train.py:115,145,208 -> TD7_multi_agent.py:315-325)
@@ -532,7 +588,21 @@ def main():
                 "shape": [2, agent.hp.batch_size * agent.env_num, agent.learner.critic.w1.shape[1],
                           agent.learner.critic.w1.shape[2]],
                 "achieved": cfl / (us * 1e-6) / 1e12, "peak": peak, "unit": "TFLOP/s",
-                "frac": cfl / (us * 1e-6) / 1e12 / peak, "avg_kernel_us": us}
+                "frac": cfl / (us * 1e-6) / 1e12 / peak, "avg_kernel_us": us,
+                "note": "the per-layer kernel of the fp32 and wide paths; the bf16 bench runs fused_critic_roofline"}
+            fc = fused_critic_timing(agent)
+            if fc is not None:
+                gbs = fc["bytes_per_wg"] / (fc["us"] * 1e-6) / 1e9
+                res["fused_critic_roofline"] = {
+                    "kernel": "td7f critic_kernel: both Q heads' forward, LAP-Huber loss and backward in one launch "
+                              "(16 rows x one head per workgroup)",
+                    "bound": "l2_weight_stream_per_cu", "achieved": gbs, "peak": L2_STREAM_PER_CU_GBS,
+                    "unit": "GB/s per workgroup (one workgroup per CU)", "frac": gbs / L2_STREAM_PER_CU_GBS,
+                    "bytes_per_workgroup": fc["bytes_per_wg"], "workgroups": fc["workgroups"],
+                    "avg_kernel_us": fc["us"],
+                    "mfma": {"achieved": fc["flop"] / (fc["us"] * 1e-6) / 1e12, "peak": peak, "unit": "TFLOP/s",
+                             "frac": fc["flop"] / (fc["us"] * 1e-6) / 1e12 / peak, "flop_per_launch": fc["flop"]},
+                    "peak_source": "tools/stream_bench.hip (profiles/r02b_raw/stream_bench.txt)"}
         if agent is not None and args.workload == "configs1" and world == 1 and not args.no_td7_variants:
             res["td7_variants"] = td7_variants(env, dev, args)
         if finite is not None:
