@@ -4,7 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests/test_env_gpu.py tests/test_multibody_gpu.py -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/rp_tests.log 2>&1 || exit $?
-for g in 0 1 0; do
+for g in 0 0; do
   EXO_RP_GATHER=$g timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rp_ab_$g -o run -- python3 bench.py --mode env --steps 300 --warmup 20 --no-cpu-baseline > gpurun_out/rp_ab_$g.log 2>&1 || exit $?
   python3 -c "
 import csv; r=[x for x in csv.DictReader(open('gpurun_out/rp_ab_$g/run_kernel_stats.csv')) if 'exo_step' in x['Name']]
