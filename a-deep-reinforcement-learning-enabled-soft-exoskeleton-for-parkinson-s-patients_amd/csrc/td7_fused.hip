@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include "adam_math.h"
 #include "philox.h"
 
 namespace td7f {
@@ -82,6 +83,155 @@ __global__ __launch_bounds__(256) void pack_kernel(PackArgs a) {
         for (int jj = 0; jj < 4; ++jj)
             v[jj] = (uint32_t)Ty<P>::bits(x[2 * jj]) | ((uint32_t)Ty<P>::bits(x[2 * jj + 1]) << 16);
         stg(dst, u32x4{v[0], v[1], v[2], v[3]});
+    }
+}
+
+// ---------------------------------------------------------------- Adam + packing
+// td7_adam_step_multi (td7_ops.hip) and pack_kernel of the weights it changes
+// in one launch: the thread that updates a weight also writes its packed
+// copies, so the optimiser step and the repack are one node of the update's
+// dependency chain instead of two.  A packed weight [N][K] is cut into 8 x 8
+// tiles; the 8 lanes of a tile update one row's 8 columns each (a forward item
+// is exactly those 8 columns of one row), then swap the 16-bit values through
+// LDS so lane r writes the dX item of column c0 + r (8 consecutive rows).
+// Workgroups [0, jb[njobs]) own the jobs' tiles, the rest stride over the
+// unpacked segments (biases) in 4-element groups as adam_multi_kernel does.
+struct APOpt {
+    float *p, *m, *v, *step;
+    float lr, b1, b2, eps, wd;
+};
+struct APSeg {  // an unpacked segment
+    const float *g;
+    long off;
+    int n, opt;
+};
+struct APJob {  // pointers at W[0][0]: p / m / v in the optimiser's buffers, g in the gradient
+    float *p, *m, *v;
+    const float *g;
+    u32x4 *wf, *wb;
+    int opt, N, K, nch, ksf, ksb, vec;
+};
+struct AdamPackArgs {
+    APOpt o[TD7_ADAM_MAX_OPT];
+    APSeg s[TD7_ADAM_MAX_SEG];
+    int q0[TD7_ADAM_MAX_SEG + 1];
+    APJob j[TD7F_MAX_ADAM_PACK];
+    int jb[TD7F_MAX_ADAM_PACK + 1];
+    int nopt, nseg, njobs;
+    uint32_t *ticket;
+};
+
+template <int P>
+__global__ __launch_bounds__(256) void adam_pack_kernel(AdamPackArgs a) {
+    __shared__ float coef[TD7_ADAM_MAX_OPT][2];
+    __shared__ u32x4 tt[32][8];  // 32 tiles x 8 rows of 8 16-bit values
+    if ((int)threadIdx.x < a.nopt) {
+        const APOpt o = a.o[threadIdx.x];
+        const float t = *o.step + 1.0f;
+        coef[threadIdx.x][0] = o.lr / (1.0f - powf(o.b1, t));
+        coef[threadIdx.x][1] = sqrtf(1.0f - powf(o.b2, t));
+    }
+    __syncthreads();
+    const int b = blockIdx.x;
+    if (b < a.jb[a.njobs]) {
+        int q = 0;
+        while (q + 1 < a.njobs && b >= a.jb[q + 1]) ++q;
+        const APJob &J = a.j[q];
+        const APOpt &o = a.o[J.opt];
+        const float ss = coef[J.opt][0], bc = coef[J.opt][1];
+        const int i = (b - a.jb[q]) * 256 + threadIdx.x;
+        const int tile = i >> 3, r = i & 7;
+        const int G = tile / J.nch, c0 = 8 * (tile - G * J.nch);
+        const int n0 = 8 * G, n = n0 + r;
+        const bool rv = n < J.N;  // false for the whole tile past the last row group
+        float x[8];
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) x[jj] = 0.f;
+        if (rv) {
+            const long e = (long)n * J.K + c0;
+            const int ne = min(8, J.K - c0);
+            float pp[8], mm[8], vv[8], gg[8];
+            if (J.vec) {  // K % 4 == 0, 16-byte aligned rows: ne is 4 or 8
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const long eh = e + (h < ne / 4 ? 4 * h : 0);
+                    const floatx4 p4 = ldg((const floatx4 *)(J.p + eh)), m4 = ldg((const floatx4 *)(J.m + eh));
+                    const floatx4 v4 = ldg((const floatx4 *)(J.v + eh)), g4 = ldg((const floatx4 *)(J.g + eh));
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        pp[4 * h + u] = p4[u], mm[4 * h + u] = m4[u], vv[4 * h + u] = v4[u], gg[4 * h + u] = g4[u];
+                }
+            } else {
+#pragma unroll
+                for (int jj = 0; jj < 8; ++jj) {
+                    const long ej = e + (jj < ne ? jj : 0);
+                    pp[jj] = ldg(J.p + ej), mm[jj] = ldg(J.m + ej), vv[jj] = ldg(J.v + ej), gg[jj] = ldg(J.g + ej);
+                }
+            }
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) adam_one(pp[jj], gg[jj], mm[jj], vv[jj], ss, bc, o.b1, o.b2, o.eps, o.wd, 1.0f);
+            if (J.vec) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    if (h < ne / 4) {
+                        stg((floatx4 *)(J.p + e + 4 * h), floatx4{pp[4 * h], pp[4 * h + 1], pp[4 * h + 2], pp[4 * h + 3]});
+                        stg((floatx4 *)(J.m + e + 4 * h), floatx4{mm[4 * h], mm[4 * h + 1], mm[4 * h + 2], mm[4 * h + 3]});
+                        stg((floatx4 *)(J.v + e + 4 * h), floatx4{vv[4 * h], vv[4 * h + 1], vv[4 * h + 2], vv[4 * h + 3]});
+                    }
+            } else {
+#pragma unroll
+                for (int jj = 0; jj < 8; ++jj)
+                    if (jj < ne) stg(J.p + e + jj, pp[jj]), stg(J.m + e + jj, mm[jj]), stg(J.v + e + jj, vv[jj]);
+            }
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) x[jj] = jj < ne ? pp[jj] : 0.f;
+        }
+        uint32_t w[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+            w[jj] = (uint32_t)Ty<P>::bits(x[2 * jj]) | ((uint32_t)Ty<P>::bits(x[2 * jj + 1]) << 16);
+        if (rv)  // forward item: W[n][c0 .. c0 + 8) (pack_kernel's forward order)
+            stg(J.wf + ((long)(n >> 4) * J.ksf + (c0 >> 5)) * 64 + (n & 15) + 16 * ((c0 & 31) >> 3),
+                u32x4{w[0], w[1], w[2], w[3]});
+        const int slot = threadIdx.x >> 3;
+        tt[slot][r] = u32x4{w[0], w[1], w[2], w[3]};
+        __syncthreads();
+        const int c = c0 + r;
+        if (J.wb && n0 < J.N && c < J.K) {  // dX item: W[n0 .. n0 + 8)[c]
+            const uint16_t *T = reinterpret_cast<const uint16_t *>(&tt[slot][0]);
+            uint32_t d[4];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) d[jj] = (uint32_t)T[16 * jj + r] | ((uint32_t)T[16 * jj + 8 + r] << 16);
+            stg(J.wb + ((long)(c >> 4) * J.ksb + (n0 >> 5)) * 64 + (c & 15) + 16 * ((n0 & 31) >> 3),
+                u32x4{d[0], d[1], d[2], d[3]});
+        }
+    } else if (a.nseg > 0) {
+        const int pb = b - a.jb[a.njobs], npb = gridDim.x - a.jb[a.njobs];
+        for (int gi = pb * 256 + threadIdx.x; gi < a.q0[a.nseg]; gi += npb * 256) {
+            int lo = 0, hi = a.nseg - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (gi >= a.q0[mid]) lo = mid;
+                else hi = mid - 1;
+            }
+            const APSeg sg = a.s[lo];
+            const APOpt o = a.o[sg.opt];
+            const float ss = coef[sg.opt][0], bc = coef[sg.opt][1];
+            const long e0 = 4L * (gi - a.q0[lo]);
+            const int ne = (int)min(4L, (long)sg.n - e0);
+            float *p = o.p + sg.off + e0, *m = o.m + sg.off + e0, *v = o.v + sg.off + e0;
+            const float *g = sg.g + e0;
+            for (int e = 0; e < ne; ++e) adam_one(p[e], g[e], m[e], v[e], ss, bc, o.b1, o.b2, o.eps, o.wd, 1.0f);
+        }
+    }
+    // the last workgroup out advances every optimiser's step count
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t done = atomicAdd(a.ticket, 1u);
+        if (done == gridDim.x - 1) {
+            for (int k = 0; k < a.nopt; ++k) *a.o[k].step = *a.o[k].step + 1.0f;
+            *a.ticket = 0u;
+        }
     }
 }
 
@@ -326,6 +476,69 @@ int td7f_pack(int32_t prec, int32_t njobs, const td7f_pack_job *jobs, void *stre
         hipLaunchKernelGGL(pack_kernel<PREC_BF16>, grid, dim3(256), 0, (hipStream_t)stream, a);
     else
         hipLaunchKernelGGL(pack_kernel<PREC_F16>, grid, dim3(256), 0, (hipStream_t)stream, a);
+    return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
+}
+
+int td7f_adam_pack(int32_t prec, int32_t nopt, float *const *p, float *const *m, float *const *v, float *const *step,
+                   const float *lr, const float *beta1, const float *beta2, const float *eps,
+                   const float *weight_decay, int32_t nseg, const float *const *g, const int64_t *off, const int32_t *n,
+                   const int32_t *opt, int32_t njobs, const td7f_pack_job *jobs, const int32_t *job_seg,
+                   uint32_t *ticket, void *stream) {
+    if ((prec != PREC_BF16 && prec != PREC_F16) || nopt <= 0 || nopt > TD7_ADAM_MAX_OPT || nseg <= 0 ||
+        nseg > TD7_ADAM_MAX_SEG || njobs < 0 || njobs > TD7F_MAX_ADAM_PACK || (njobs && (!jobs || !job_seg)) ||
+        !ticket)
+        return EXO_EINVAL;
+    AdamPackArgs a{};
+    a.nopt = nopt;
+    a.ticket = ticket;
+    for (int k = 0; k < nopt; ++k) {
+        if (!p[k] || !m[k] || !v[k] || !step[k]) return EXO_EINVAL;
+        a.o[k] = APOpt{p[k], m[k], v[k], step[k], lr[k], beta1[k], beta2[k], eps[k], weight_decay[k]};
+    }
+    for (int k = 0; k < nseg; ++k)
+        if (!g[k] || n[k] <= 0 || off[k] < 0 || opt[k] < 0 || opt[k] >= nopt) return EXO_EINVAL;
+    // every job: a contiguous [N][K] block inside its segment; a segment is
+    // covered by its jobs exactly or not at all
+    long covered[TD7_ADAM_MAX_SEG] = {};
+    a.jb[0] = 0;
+    for (int q = 0; q < njobs; ++q) {
+        const td7f_pack_job &J = jobs[q];
+        const int k = job_seg[q];
+        if (k < 0 || k >= nseg || !J.w || !J.wf || J.n_out <= 0 || J.n_in <= 0 || J.ld != J.n_in ||
+            J.ksf * 32 < J.n_in || J.ntf * 16 < J.n_out || (J.wb && (J.ksb * 32 < J.n_out || J.ntb * 16 < J.n_in)))
+            return EXO_EINVAL;
+        const int o = opt[k];
+        const long e = (long)(J.w - p[o]), sz = (long)J.n_out * J.n_in;
+        if (e < off[k] || e + sz > off[k] + n[k]) return EXO_EINVAL;
+        covered[k] += sz;
+        const float *gq = g[k] + (e - off[k]);
+        const bool vec = J.n_in % 4 == 0 &&
+                         ((reinterpret_cast<uintptr_t>(J.w) | reinterpret_cast<uintptr_t>(m[o] + e) |
+                           reinterpret_cast<uintptr_t>(v[o] + e) | reinterpret_cast<uintptr_t>(gq)) & 15) == 0;
+        const int nch = (J.n_in + 7) / 8;
+        a.j[q] = APJob{p[o] + e, m[o] + e, v[o] + e, gq, (u32x4 *)J.wf, (u32x4 *)J.wb, o, J.n_out, J.n_in, nch,
+                       J.ksf, J.wb ? J.ksb : 0, vec ? 1 : 0};
+        const long threads = (long)(J.n_out + 7) / 8 * nch * 8;
+        a.jb[q + 1] = a.jb[q] + (int)((threads + 255) / 256);
+    }
+    a.njobs = njobs;
+    long groups = 0;
+    for (int k = 0; k < nseg; ++k) {
+        if (covered[k] == n[k]) continue;
+        if (covered[k] != 0) return EXO_EINVAL;
+        a.s[a.nseg] = APSeg{g[k], (long)off[k], n[k], opt[k]};
+        a.q0[a.nseg++] = (int)groups;
+        groups += (n[k] + 3) / 4;
+    }
+    if (groups >= (1L << 30)) return EXO_ERANGE;
+    a.q0[a.nseg] = (int)groups;
+    const long plain = std::min<long>(64, (groups + 255) / 256);
+    const unsigned grid = (unsigned)(a.jb[njobs] + plain);
+    if (grid == 0) return EXO_OK;
+    if (prec == PREC_BF16)
+        hipLaunchKernelGGL(adam_pack_kernel<PREC_BF16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
+    else
+        hipLaunchKernelGGL(adam_pack_kernel<PREC_F16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 

@@ -13,6 +13,7 @@
 
 #include <algorithm>
 
+#include "adam_math.h"
 #include "exo_amd.h"
 
 namespace {
@@ -72,15 +73,6 @@ __global__ __launch_bounds__(256) void avgl1_bwd_kernel(const float *__restrict_
 // to finish (ticket counter) stores step + 1 and rearms the ticket, so one
 // launch is the whole optimiser step (HIP-graph safe, no host value).
 constexpr int ADAM_THREADS = 256, ADAM_BLOCKS = 256, ADAM_MULTI_BLOCKS = 256;
-
-__device__ __forceinline__ void adam_one(float &p, float g, float &m, float &v, float step_size, float bc2s,
-                                         float b1, float b2, float eps, float wd, float gscale) {
-    g *= gscale;
-    if (wd != 0.0f) g += wd * p;
-    m += (1.0f - b1) * (g - m); // lerp_(grad, 1 - beta1)
-    v = v * b2 + (1.0f - b2) * g * g;
-    p -= step_size * (m / (sqrtf(v) / bc2s + eps));
-}
 
 // grid-stride over float4 groups (a fixed 512-workgroup grid: few ticket
 // atomics), scalar tail for n % 4

@@ -19,6 +19,7 @@ from . import ops
 PD = 5  # include/exo_amd.h TD7F_PD
 NW = 4  # waves per fused workgroup (csrc/td7_fused.h)
 MAX_PACK = 32
+MAX_ADAM_PACK = 16  # include/exo_amd.h TD7F_MAX_ADAM_PACK
 PREC = {"bf16": 1, "fp16": 2}
 
 
@@ -183,6 +184,42 @@ class FusedNets:
     def pack_all(self):
         self.pack(*self.nets)
 
+    def adam_pack(self, opts, *names):
+        """FlatAdam.step_many(opts) followed by pack(*names), as one
+        td7f_adam_pack launch: the thread that updates a weight writes its
+        packed copies.  Every packed weight must be a parameter (or a head of
+        one) of one of the optimisers; one without a gradient is not stepped
+        and keeps its packed copy."""
+        from .td7 import FlatAdam
+        segs = FlatAdam.segments(opts)
+        if not segs:
+            return
+        nets = [self.nets[n] for n in names]
+        jobs, jseg = [], []
+        for net in nets:
+            for pl in net.layers:
+                ptr = pl.weight.data_ptr()
+                for k, o in enumerate(opts):
+                    e = (ptr - o.flat.data_ptr()) // 4
+                    if 0 <= e < o.flat.numel():
+                        break
+                else:
+                    raise ValueError("adam_pack: a packed weight outside the optimisers' parameters")
+                hit = [i for i, sg in enumerate(segs) if sg[3] == k and sg[1] <= e < sg[1] + sg[2]]
+                if hit:
+                    jobs.append(pl.job())
+                    jseg.append(hit[0])
+        if (len(opts) > FlatAdam.MAX_OPT or len(segs) > FlatAdam.MAX_SEG or len(jobs) > MAX_ADAM_PACK
+                or not all(pl.weight.is_contiguous() for net in nets for pl in net.layers)):
+            FlatAdam.step_many(opts)
+            self.pack(*names)
+            return
+        nj = len(jobs)
+        extra = (nj, (TD7FPackJob * nj)(*jobs), (ctypes.c_int32 * nj)(*jseg))
+        nat.check(nat.lib().td7f_adam_pack(self.prec, *FlatAdam.multi_args(opts, segs, extra)), "td7f_adam_pack")
+        for net in nets:
+            net._ver = net._versions()
+
     def refresh(self, *names):
         for n in names:
             self.nets[n].refresh()
@@ -330,6 +367,9 @@ class FusedTrain:
             for h in range(2):
                 jobs.append(self._job(self.xt_critic[2 * k + h], gw[h], gb[h], rt))
         self.jobs_ec = (nat.TD7FWgJob * len(jobs))(*jobs)
+        ne = len(self.xt_enc)
+        self.jobs_e = (nat.TD7FWgJob * ne)(*jobs[:ne])
+        self.jobs_c = (nat.TD7FWgJob * (len(jobs) - ne))(*jobs[ne:])
         act_p = list(L.actor.parameters())
         ajobs = [self._job(xb, act_p[2 * i].grad, act_p[2 * i + 1].grad, rt) for i, xb in enumerate(self.xt_actor)]
         self.jobs_a = (nat.TD7FWgJob * len(ajobs))(*ajobs)
@@ -366,6 +406,20 @@ class FusedTrain:
         """Every encoder and critic weight/bias gradient (one launch) and the LAP priorities."""
         fz, hp = self.nets, self.L.hp
         nat.check(nat.lib().td7f_wgrad(fz.prec, len(self.jobs_ec), self.jobs_ec, self.ld, self.ld, nat.ptr(self.td),
+                                       nat.ptr(self.prio), self.B, float(hp.alpha), float(hp.min_priority),
+                                       nat.stream_ptr(fz.dev)), "td7f_wgrad")
+        return self.prio
+
+    def wgrad_encoder(self):
+        """The encoder's weight/bias gradients alone (its branch of the update)."""
+        fz = self.nets
+        nat.check(nat.lib().td7f_wgrad(fz.prec, len(self.jobs_e), self.jobs_e, self.ld, self.ld, None, None, 0, 0.0,
+                                       0.0, nat.stream_ptr(fz.dev)), "td7f_wgrad")
+
+    def wgrad_critic(self):
+        """The critic's weight/bias gradients and the LAP priorities."""
+        fz, hp = self.nets, self.L.hp
+        nat.check(nat.lib().td7f_wgrad(fz.prec, len(self.jobs_c), self.jobs_c, self.ld, self.ld, nat.ptr(self.td),
                                        nat.ptr(self.prio), self.B, float(hp.alpha), float(hp.min_priority),
                                        nat.stream_ptr(fz.dev)), "td7f_wgrad")
         return self.prio

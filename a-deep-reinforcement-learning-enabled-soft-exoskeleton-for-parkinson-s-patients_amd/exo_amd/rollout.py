@@ -22,6 +22,7 @@ import numpy as np
 import torch
 
 from . import _native as nat
+from .td7 import ENC_STEP_BRANCH
 
 
 def graph_reductions_ok(device, rows=1024, cols=300, replays=3):
@@ -227,6 +228,9 @@ class VecTrainer:
 
     def _pre(self):
         ag = self.agent
+        # one GPU: the encoder's gradients and step stay on its branch, joined
+        # at the end of the iteration (_join_prio)
+        ag.learner.defer_side_join = ENC_STEP_BRANCH and not self.dp
         rb = ag.replay_buffer
         slot = self._cur if self._prefetching() else None
         if self.iters == 0 or not self.overlap_rollout:
@@ -286,6 +290,7 @@ class VecTrainer:
         if getattr(self, "_pside", None) is not None:
             torch.cuda.current_stream(self.device).wait_stream(self._pside)
             self._pside = None
+        self.agent.learner.join_side()  # the encoder branch's optimiser step
 
     def _post(self, update_actor, flat_grad=None, grad_scale=1.0):
         if update_actor:

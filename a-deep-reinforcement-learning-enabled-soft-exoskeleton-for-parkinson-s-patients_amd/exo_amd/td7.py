@@ -34,6 +34,13 @@ from . import _native as nat
 from . import ops
 from .ops import avg_l1_norm
 
+# fused optimiser step + weight repack (td7f_adam_pack); EXO_ADAM_PACK=0: two launches
+ADAM_PACK = os.environ.get("EXO_ADAM_PACK", "1") != "0"
+# graph-replayed trainer on one GPU, fused: the encoder's weight gradients and
+# step on the encoder's graph branch (TD7Learner.defer_side_join);
+# EXO_ENC_STEP_BRANCH=0 joins the branch before the gradients
+ENC_STEP_BRANCH = os.environ.get("EXO_ENC_STEP_BRANCH", "1") != "0"
+
 
 @dataclass
 class Hyperparameters:
@@ -319,7 +326,6 @@ class FlatAdam(torch.optim.Adam):
 
 
     MAX_OPT, MAX_SEG = 3, 40  # include/exo_amd.h TD7_ADAM_MAX_*
-    _multi_ticket = {}
 
     @staticmethod
     @torch.no_grad()
@@ -328,6 +334,18 @@ class FlatAdam(torch.optim.Adam):
         td7_adam_step_multi launch reading each parameter's gradient where
         autograd left it -- no concatenation into a flat gradient buffer.
         Parameters without a gradient are skipped (torch.optim.Adam)."""
+        segs = FlatAdam.segments(opts)
+        if not segs:
+            return
+        if len(opts) > FlatAdam.MAX_OPT or len(segs) > FlatAdam.MAX_SEG:
+            for o in opts:
+                o.step()
+            return
+        nat.check(nat.lib().td7_adam_step_multi(*FlatAdam.multi_args(opts, segs)), "td7_adam_step_multi")
+
+    @staticmethod
+    def segments(opts):
+        """[(grad, flat offset, numel, optimiser index)] of every parameter with a gradient."""
         segs = []
         for k, o in enumerate(opts):
             off = 0
@@ -335,30 +353,29 @@ class FlatAdam(torch.optim.Adam):
                 if p.grad is not None:
                     segs.append((p.grad.contiguous(), off, p.numel(), k))
                 off += p.numel()
-        if not segs:
-            return
-        if len(opts) > FlatAdam.MAX_OPT or len(segs) > FlatAdam.MAX_SEG:
-            for o in opts:
-                o.step()
-            return
+        return segs
+
+    @staticmethod
+    def multi_args(opts, segs, extra=()):
+        """The arguments of td7_adam_step_multi (td7f_adam_pack: `extra` goes
+        between the segments and the ticket)."""
         dev = opts[0].flat.device
-        ticket = FlatAdam._multi_ticket.get(dev)
-        if ticket is None:
-            if torch.cuda.is_current_stream_capturing():
-                raise RuntimeError("FlatAdam.step_many: run once eagerly before graph capture")
-            ticket = FlatAdam._multi_ticket[dev] = torch.zeros((1,), dtype=torch.int32, device=dev)
+        # the first optimiser's ticket: launches over disjoint optimiser sets
+        # may run concurrently (graph branches), each with its own counter
+        ticket = opts[0]._ticket
         n = len(opts)
         P = lambda ts: (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])  # noqa: E731
         F32 = lambda vs: (ctypes.c_float * n)(*[float(v) for v in vs])  # noqa: E731
         grps = [o.param_groups[0] for o in opts]
         ns = len(segs)
-        nat.check(nat.lib().td7_adam_step_multi(
-            n, P([o.flat for o in opts]), P([o.m for o in opts]), P([o.v for o in opts]), P([o._step for o in opts]),
-            F32([g["lr"] for g in grps]), F32([g["betas"][0] for g in grps]), F32([g["betas"][1] for g in grps]),
-            F32([g["eps"] for g in grps]), F32([g["weight_decay"] for g in grps]), ns,
-            (ctypes.c_void_p * ns)(*[sg[0].data_ptr() for sg in segs]), (ctypes.c_int64 * ns)(*[sg[1] for sg in segs]),
-            (ctypes.c_int32 * ns)(*[sg[2] for sg in segs]), (ctypes.c_int32 * ns)(*[sg[3] for sg in segs]),
-            nat.ptr(ticket), nat.stream_ptr(dev)), "td7_adam_step_multi")
+        return (n, P([o.flat for o in opts]), P([o.m for o in opts]), P([o.v for o in opts]),
+                P([o._step for o in opts]), F32([g["lr"] for g in grps]), F32([g["betas"][0] for g in grps]),
+                F32([g["betas"][1] for g in grps]), F32([g["eps"] for g in grps]),
+                F32([g["weight_decay"] for g in grps]), ns,
+                (ctypes.c_void_p * ns)(*[sg[0].data_ptr() for sg in segs]),
+                (ctypes.c_int64 * ns)(*[sg[1] for sg in segs]), (ctypes.c_int32 * ns)(*[sg[2] for sg in segs]),
+                (ctypes.c_int32 * ns)(*[sg[3] for sg in segs])) + tuple(extra) + (nat.ptr(ticket),
+                                                                                   nat.stream_ptr(dev))
 
 
 class GradSync:
@@ -561,6 +578,11 @@ class TD7Learner:
     # critic update (set per iteration by the trainer through prefetch_actor)
     actor_branch = os.environ.get("EXO_TD7_ACTOR_BRANCH", "1") == "1"
     prefetch_actor = False
+    # True (one GPU, set by the graph-replayed trainer): the fused update leaves
+    # the encoder's weight gradients and optimiser step on the encoder's branch
+    # and the caller joins it (join_side, end of iteration); False: phase_grads
+    # returns with every gradient ordered on the current stream
+    defer_side_join = False
 
     def _encoder_grads(self, state, action, next_state):
         """:219-228 -- loss and gradients of the live encoder."""
@@ -697,10 +719,18 @@ class TD7Learner:
             st.wait_stream(cur)
             return st
 
+        # one GPU: the encoder's weight gradients and optimiser step stay on
+        # its branch (nothing else in the update reads them); data-parallel
+        # runs all-reduce them with the critic's
+        enc_step = (branch and ADAM_PACK and self.defer_side_join and not self.sync.active
+                    and isinstance(self.encoder_optimizer, FlatAdam))
+        self._enc_step_pending = False
         if branch:
             side, tside = stream("_side"), stream("_tside")
             with torch.cuda.stream(side):
                 tr.encoder(state, action, next_state)
+                if enc_step:
+                    tr.wgrad_encoder()
             with torch.cuda.stream(tside):
                 qt = fz.target_heads(next_state, noise)
         else:
@@ -716,9 +746,13 @@ class TD7Learner:
         if branch:
             cur.wait_stream(tside)
         tr.critic(state, action, zs, zsa, qt, reward, not_done)
-        if branch:
-            cur.wait_stream(side)
-        priority = tr.wgrad_encoder_critic()
+        if enc_step:
+            priority = tr.wgrad_critic()
+            self._enc_step_pending = True
+        else:
+            if branch:
+                cur.wait_stream(side)
+            priority = tr.wgrad_encoder_critic()
         if self._actor_fused_pre:
             cur.wait_stream(self._aside)
         self._fixed_zs = zs
@@ -760,6 +794,8 @@ class TD7Learner:
         in grad_params() order (the data-parallel all-reduce bucket), consumed
         in place by FlatAdam."""
         if flat_grad is not None and isinstance(self.encoder_optimizer, FlatAdam):
+            if getattr(self, "_enc_step_pending", False):
+                raise RuntimeError("phase_steps: a flat gradient bucket with the encoder step on its branch")
             ne = self.encoder_optimizer.flat.numel()
             self.encoder_optimizer.step(flat_grad=flat_grad[:ne], grad_scale=grad_scale)
             self.critic_optimizer.step(flat_grad=flat_grad[ne:], grad_scale=grad_scale)
@@ -767,6 +803,17 @@ class TD7Learner:
                 self.fused.pack("encoder", "critic")
             return
         if isinstance(self.encoder_optimizer, FlatAdam) and self.device.type == "cuda":
+            if getattr(self, "_enc_step_pending", False):
+                # the encoder's step on its branch (after its weight gradients),
+                # the critic's on the update's chain
+                self._enc_step_pending = False
+                with torch.cuda.stream(self._side):
+                    self.fused.adam_pack([self.encoder_optimizer], "encoder")
+                self.fused.adam_pack([self.critic_optimizer], "critic")
+                return
+            if self.fused is not None and ADAM_PACK:
+                self.fused.adam_pack([self.encoder_optimizer, self.critic_optimizer], "encoder", "critic")
+                return
             FlatAdam.step_many([self.encoder_optimizer, self.critic_optimizer])
             if self.fused is not None:
                 self.fused.pack("encoder", "critic")
@@ -834,6 +881,9 @@ class TD7Learner:
         if flat_grad is not None and isinstance(self.actor_optimizer, FlatAdam):
             self.actor_optimizer.step(flat_grad=flat_grad, grad_scale=grad_scale)
         elif isinstance(self.actor_optimizer, FlatAdam) and self.device.type == "cuda":
+            if self.fused is not None and ADAM_PACK:
+                self.fused.adam_pack([self.actor_optimizer], "actor")  # select_action reads the packed actor
+                return
             FlatAdam.step_many([self.actor_optimizer])
         else:
             self.actor_optimizer.step()

@@ -455,6 +455,19 @@ typedef struct {
 
 /* Activation codes of the three nets: act[0] encoder, act[1] actor, act[2] critic (1 relu, 2 elu). */
 int td7f_pack(int32_t prec, int32_t njobs, const td7f_pack_job *jobs, void *stream);
+/* td7_adam_step_multi (same arguments, same results bit for bit) fused with
+ * td7f_pack of the weights it changes: job q packs the fp32 weight jobs[q].w,
+ * a contiguous [n_out][n_in] block (ld == n_in) inside segment job_seg[q] of
+ * its optimiser, from the updated values.  A segment is covered exactly by its
+ * jobs or by none (EXO_EINVAL otherwise).  The optimiser step of
+ * Agent/TD7_multi_agent.py:253-255 / :277 followed by the repack the fused
+ * passes need, as one launch. */
+#define TD7F_MAX_ADAM_PACK 16
+int td7f_adam_pack(int32_t prec, int32_t nopt, float *const *p_dev, float *const *m_dev, float *const *v_dev,
+                   float *const *step_dev, const float *lr, const float *beta1, const float *beta2, const float *eps,
+                   const float *weight_decay, int32_t nseg, const float *const *g_dev, const int64_t *off,
+                   const int32_t *n, const int32_t *opt, int32_t njobs, const td7f_pack_job *jobs,
+                   const int32_t *job_seg, uint32_t *ticket_dev, void *stream);
 /* Agent.select_action_batch (TD7_multi_agent.py:192-209 batched): actor(obs,
  * fixed_encoder.zs(obs)) + Gaussian exploration noise -> act_out [n][A].
  * enc: zs1..zs3, actor: l0..l3. */

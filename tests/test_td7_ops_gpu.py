@@ -141,6 +141,6 @@ def test_flat_adam_step_many_matches_separate_steps():
         torch.testing.assert_close(skip.detach(), skip_before, rtol=0, atol=0)
         for a, b in zip(nets, twins):
             for p, q in zip(a.parameters(), b.parameters()):
-                torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-6, atol=1e-7)
+                torch.testing.assert_close(p.detach(), q.detach(), rtol=0, atol=0)
         for o, r in zip(opts, refs):
             assert float(o._step) == float(r._step) == it + 1
