@@ -22,6 +22,7 @@
 // the same lanes).  Bias gradients come from the unrounded fp32 dP (column
 // partials per row tile, summed in td7f_wgrad).
 #include "td7_fused.h"
+#include "adam_math.h"
 
 #include <algorithm>
 
@@ -459,6 +460,15 @@ struct WgJob {
     float *dw, *db;
     int N, K, tiles_k, ntiles_rows;  // tiles_k = ceil(K / 64); row tiles of part
     int first;                        // first workgroup of this job
+    // td7f_wgrad_adam: the layer's Adam step and repack (flat offsets of W[0][0]
+    // and b[0] in optimiser opt's p / m / v; packed operands as td7f_pack)
+    long w_off, b_off;
+    u32x4 *wf, *wb;
+    int ksf, ksb, opt;
+};
+struct WgOpt {
+    float *p, *m, *v, *step;
+    float lr, b1, b2, eps, wd;
 };
 struct WgArgs {
     int njobs, total;
@@ -471,17 +481,25 @@ struct WgArgs {
     int B;
     float alpha, minp;
     WgJob j[TD7F_MAX_WG];
+    WgOpt o[TD7_ADAM_MAX_OPT];
+    int nopt;
+    uint32_t *ticket;
 };
 
 constexpr int PD2 = 8;  // k-steps (32 rows) in flight; the reduction length is a multiple of 32 PD2
 
-template <int P>
+// ADAM: the optimiser step of every weight / bias the launch differentiates
+// (adam_one, bit-identical to td7_adam_step_multi) and the repack of the
+// updated weights (bit-identical to td7f_pack) in the epilogue: the tile's p /
+// m / v are loaded before the k-loop (their latency hides under the MFMAs),
+// the updated 16-bit weights are staged in LDS and written out as whole forward
+// and dX items.  The optimiser step counts advance once (last workgroup out).
+template <int P, bool ADAM>
 __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs a) {
     if ((int)blockIdx.x == a.total) {
         for (int b = threadIdx.x; b < a.B; b += 256)
             stg(a.prio + b, powf(fmaxf(fmaxf(ldg(a.td + 2 * b), ldg(a.td + 2 * b + 1)), a.minp), a.alpha));
-        return;
-    }
+    } else {
     int q = 0;
     while (q + 1 < a.njobs && (int)blockIdx.x >= a.j[q + 1].first) ++q;
     const WgJob &J = a.j[q];
@@ -490,14 +508,36 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs a) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wn = n0 + 32 * (w >> 1), wk = k0 + 32 * (w & 1);
     const long ld = a.ld;
+    float ss = 0.f, bc = 1.f;
+    float pp[2][2][4], mm[2][2][4], vv[2][2][4], bp = 0.f, bm = 0.f, bv = 0.f;
+    if constexpr (ADAM) {
+        const WgOpt &o = a.o[J.opt];
+        const float st = *o.step + 1.0f;
+        ss = o.lr / (1.0f - powf(o.b1, st));
+        bc = sqrtf(1.0f - powf(o.b2, st));
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int v = 0; v < 2; ++v)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int n = wn + 16 * u + 4 * (lane >> 4) + e, k = wk + 16 * v + (lane & 15);
+                    const long i = J.w_off + ((n < J.N && k < J.K) ? (long)n * J.K + k : 0);
+                    pp[u][v][e] = ldg(o.p + i), mm[u][v][e] = ldg(o.m + i), vv[u][v][e] = ldg(o.v + i);
+                }
+        if (k0 == 0 && J.db && w == 0) {
+            const long i = J.b_off + (n0 + lane < J.N ? n0 + lane : 0);
+            bp = ldg(o.p + i), bm = ldg(o.m + i), bv = ldg(o.v + i);
+        }
+    }
     // the operands are in fragment blocks (td7_fused.h blk8): the 16 x 32
     // fragment of operand rows g*16.. and k-step s is the 1 KiB block g * (ld/32) + s;
     // they are padded to multiples of 64 rows (zeros), so every load is in range
-    const uint16_t *ap[2], *bp[2];
+    const uint16_t *ap[2], *bp2[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
         ap[u] = J.dp + (long)((wn + 16 * u) >> 4) * (ld >> 5) * 512 + lane * 8;
-        bp[u] = J.x + (long)((wk + 16 * u) >> 4) * (ld >> 5) * 512 + lane * 8;
+        bp2[u] = J.x + (long)((wk + 16 * u) >> 4) * (ld >> 5) * 512 + lane * 8;
     }
     floatx4 acc[2][2];
 #pragma unroll
@@ -513,7 +553,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs a) {
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             fa[p][u] = ldg((const u32x4 *)(ap[u] + 512 * p));
-            fb[p][u] = ldg((const u32x4 *)(bp[u] + 512 * p));
+            fb[p][u] = ldg((const u32x4 *)(bp2[u] + 512 * p));
             __builtin_amdgcn_sched_barrier(0);
         }
     int s0 = 0;
@@ -529,7 +569,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs a) {
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
                 fa[p][u] = ldg((const u32x4 *)(ap[u] + 512 * (s + PD2)));
-                fb[p][u] = ldg((const u32x4 *)(bp[u] + 512 * (s + PD2)));
+                fb[p][u] = ldg((const u32x4 *)(bp2[u] + 512 * (s + PD2)));
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -541,6 +581,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs a) {
 #pragma unroll
             for (int v = 0; v < 2; ++v) acc[u][v] = Ty<P>::mfma(fa[p][u], fb[p][v], acc[u][v]);
     // C[n][k]: lane holds n = 16u + 4(lane >> 4) + e, k = 16v + (lane & 15)
+    __shared__ alignas(16) uint16_t T[ADAM ? 64 : 1][72];  // the tile's updated 16-bit weights (rows padded to 144 B)
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -549,7 +590,18 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs a) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int n = wn + 16 * u + 4 * (lane >> 4) + e;
-                if (n < J.N && k < J.K) stg(J.dw + (long)n * J.K + k, acc[u][v][e] * (1.f / Ty<P>::gs));
+                const bool ok = n < J.N && k < J.K;
+                const float g = acc[u][v][e] * (1.f / Ty<P>::gs);
+                if (ok) stg(J.dw + (long)n * J.K + k, g);
+                if constexpr (ADAM) {
+                    const WgOpt &o = a.o[J.opt];
+                    adam_one(pp[u][v][e], g, mm[u][v][e], vv[u][v][e], ss, bc, o.b1, o.b2, o.eps, o.wd, 1.0f);
+                    if (ok) {
+                        const long i = J.w_off + (long)n * J.K + k;
+                        stg(o.p + i, pp[u][v][e]), stg(o.m + i, mm[u][v][e]), stg(o.v + i, vv[u][v][e]);
+                    }
+                    T[n - n0][k - k0] = ok ? Ty<P>::bits(pp[u][v][e]) : (uint16_t)0;
+                }
             }
         }
     if (k0 == 0 && J.db) {
@@ -564,7 +616,57 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs a) {
         }
         red[w][lane] = sacc;
         __syncthreads();
-        if (w == 0 && n < J.N) stg(J.db + n, ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]);
+        if (w == 0 && n < J.N) {
+            const float g = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+            stg(J.db + n, g);
+            if constexpr (ADAM) {
+                const WgOpt &o = a.o[J.opt];
+                adam_one(bp, g, bm, bv, ss, bc, o.b1, o.b2, o.eps, o.wd, 1.0f);
+                stg(o.p + J.b_off + n, bp), stg(o.m + J.b_off + n, bm), stg(o.v + J.b_off + n, bv);
+            }
+        }
+    }
+    if constexpr (ADAM) {
+        __syncthreads();
+        // 64 rows x 8 forward items (8 inputs of one output row) and 64 columns
+        // x 8 dX items (8 output rows of one input column): two of each per thread
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int i = threadIdx.x + 256 * h;
+            const int r = i >> 3, c = 8 * (i & 7);
+            const int n = n0 + r, k = k0 + c;
+            if (n < J.N && k < J.K)
+                stg(J.wf + ((long)(n >> 4) * J.ksf + (k >> 5)) * 64 + (n & 15) + 16 * ((k & 31) >> 3),
+                    *(const u32x4 *)&T[r][c]);
+        }
+        if (J.wb) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int i = threadIdx.x + 256 * h;
+                const int c = i & 63, r8 = 8 * (i >> 6);
+                const int n = n0 + r8, k = k0 + c;
+                if (n < J.N && k < J.K) {
+                    uint32_t d[4];
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj) d[jj] = (uint32_t)T[r8 + 2 * jj][c] | ((uint32_t)T[r8 + 2 * jj + 1][c] << 16);
+                    stg(J.wb + ((long)(k >> 4) * J.ksb + (n >> 5)) * 64 + (k & 15) + 16 * ((n & 31) >> 3),
+                        u32x4{d[0], d[1], d[2], d[3]});
+                }
+            }
+        }
+    }
+    }
+    if constexpr (ADAM) {
+        // the last workgroup out advances the optimisers' step counts (every
+        // workgroup read them before its ticket)
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t done = atomicAdd(a.ticket, 1u);
+            if (done == gridDim.x - 1) {
+                for (int k = 0; k < a.nopt; ++k) *a.o[k].step = *a.o[k].step + 1.0f;
+                *a.ticket = 0u;
+            }
+        }
     }
 }
 
@@ -766,12 +868,11 @@ int td7f_actor(int32_t prec, int32_t phase, const int32_t *act, const td7f_lin *
     return DISPATCH(prec, th, actor_c_kernel, grid, b.off, g, st);
 }
 
-int td7f_wgrad(int32_t prec, int32_t njobs, const td7f_wg_job *jobs, int64_t ld, int32_t rows, const float *td,
-               float *prio, int32_t B, float alpha, float min_priority, void *stream) {
+static int wgrad_args(int32_t prec, int32_t njobs, const td7f_wg_job *jobs, int64_t ld, int32_t rows,
+                      const float *td, float *prio, int32_t B, float alpha, float min_priority, WgArgs &g) {
     if (!prec_ok(prec) || njobs <= 0 || njobs > TD7F_MAX_WG || !jobs || rows <= 0 || rows % (32 * PD2) ||
         ld < rows || ld % 32 || (prio && (!td || B <= 0)))
         return EXO_EINVAL;
-    WgArgs g{};
     g.njobs = njobs;
     g.ld = ld;
     g.rows = rows;
@@ -798,10 +899,56 @@ int td7f_wgrad(int32_t prec, int32_t njobs, const td7f_wg_job *jobs, int64_t ld,
     g.B = B;
     g.alpha = alpha;
     g.minp = min_priority;
+    return EXO_OK;
+}
+
+int td7f_wgrad(int32_t prec, int32_t njobs, const td7f_wg_job *jobs, int64_t ld, int32_t rows, const float *td,
+               float *prio, int32_t B, float alpha, float min_priority, void *stream) {
+    WgArgs g{};
+    const int rc = wgrad_args(prec, njobs, jobs, ld, rows, td, prio, B, alpha, min_priority, g);
+    if (rc != EXO_OK) return rc;
     const hipStream_t st = (hipStream_t)stream;
-    const dim3 grid(total + (prio ? 1 : 0));
-    if (prec == PREC_BF16) hipLaunchKernelGGL(wgrad_kernel<PREC_BF16>, grid, dim3(256), 0, st, g);
-    else hipLaunchKernelGGL(wgrad_kernel<PREC_F16>, grid, dim3(256), 0, st, g);
+    const dim3 grid(g.total + (prio ? 1 : 0));
+    if (prec == PREC_BF16) hipLaunchKernelGGL((wgrad_kernel<PREC_BF16, false>), grid, dim3(256), 0, st, g);
+    else hipLaunchKernelGGL((wgrad_kernel<PREC_F16, false>), grid, dim3(256), 0, st, g);
+    return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
+}
+
+int td7f_wgrad_adam(int32_t prec, int32_t njobs, const td7f_wg_job *jobs, int64_t ld, int32_t rows, const float *td,
+                    float *prio, int32_t B, float alpha, float min_priority, int32_t nopt, float *const *p,
+                    float *const *m, float *const *v, float *const *step, const float *lr, const float *beta1,
+                    const float *beta2, const float *eps, const float *weight_decay, const td7f_wg_adam *adam,
+                    uint32_t *ticket, void *stream) {
+    WgArgs g{};
+    const int rc = wgrad_args(prec, njobs, jobs, ld, rows, td, prio, B, alpha, min_priority, g);
+    if (rc != EXO_OK) return rc;
+    if (nopt <= 0 || nopt > TD7_ADAM_MAX_OPT || !adam || !ticket) return EXO_EINVAL;
+    g.nopt = nopt;
+    g.ticket = ticket;
+    for (int k = 0; k < nopt; ++k) {
+        if (!p[k] || !m[k] || !v[k] || !step[k]) return EXO_EINVAL;
+        g.o[k] = WgOpt{p[k], m[k], v[k], step[k], lr[k], beta1[k], beta2[k], eps[k], weight_decay[k]};
+    }
+    for (int q = 0; q < njobs; ++q) {
+        const td7f_wg_adam &A = adam[q];
+        const td7f_wg_job &J = jobs[q];
+        // every layer: weight, bias (its gradient db required) and forward operand
+        if (A.opt < 0 || A.opt >= nopt || A.w_off < 0 || A.b_off < 0 || !J.db || !A.wf ||
+            A.ksf * 32 < J.k || (A.wb && A.ksb * 32 < J.n))
+            return EXO_EINVAL;
+        WgJob &w = g.j[q];
+        w.w_off = A.w_off;
+        w.b_off = A.b_off;
+        w.wf = (u32x4 *)A.wf;
+        w.wb = (u32x4 *)A.wb;
+        w.ksf = A.ksf;
+        w.ksb = A.wb ? A.ksb : 0;
+        w.opt = A.opt;
+    }
+    const hipStream_t st = (hipStream_t)stream;
+    const dim3 grid(g.total + (prio ? 1 : 0));
+    if (prec == PREC_BF16) hipLaunchKernelGGL((wgrad_kernel<PREC_BF16, true>), grid, dim3(256), 0, st, g);
+    else hipLaunchKernelGGL((wgrad_kernel<PREC_F16, true>), grid, dim3(256), 0, st, g);
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 

@@ -89,6 +89,12 @@ class TD7FWgJob(ctypes.Structure):
                 ("n", c_int32), ("k", c_int32), ("row_tiles", c_int32)]
 
 
+class TD7FWgAdam(ctypes.Structure):
+    """td7f_wg_adam (include/exo_amd.h)."""
+    _fields_ = [("opt", c_int32), ("w_off", ctypes.c_int64), ("b_off", ctypes.c_int64), ("wf", c_void_p),
+                ("wb", c_void_p), ("ksf", c_int32), ("ksb", c_int32)]
+
+
 EXPORTS = {
     "exo_create": (c_int32, [P(ExoEnvConfig), c_int32, P(c_double), P(c_int32), c_int32, c_int32, c_uint64, c_int32,
                              P(c_void_p)]),
@@ -191,6 +197,10 @@ EXPORTS = {
                              c_int32, P(TD7FActorBufs), P(TD7FXT), ctypes.c_int64, c_void_p]),
     "td7f_wgrad": (c_int32, [c_int32, c_int32, P(TD7FWgJob), ctypes.c_int64, c_int32, c_void_p, c_void_p, c_int32,
                              ctypes.c_float, ctypes.c_float, c_void_p]),
+    "td7f_wgrad_adam": (c_int32, [c_int32, c_int32, P(TD7FWgJob), ctypes.c_int64, c_int32, c_void_p, c_void_p,
+                                  c_int32, ctypes.c_float, ctypes.c_float, c_int32, c_void_p, c_void_p, c_void_p,
+                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, P(TD7FWgAdam), c_void_p,
+                                  c_void_p]),
 }
 
 _lib = None

@@ -370,10 +370,51 @@ class FusedTrain:
         ne = len(self.xt_enc)
         self.jobs_e = (nat.TD7FWgJob * ne)(*jobs[:ne])
         self.jobs_c = (nat.TD7FWgJob * (len(jobs) - ne))(*jobs[ne:])
+        # td7f_wgrad_adam: where each job's layer sits in its optimiser (None
+        # when the jobs do not cover every parameter of that optimiser)
+        self.adam_e = self._adam_descs(L.encoder_optimizer, nets.nets["encoder"].layers)
+        self.adam_c = self._adam_descs(L.critic_optimizer, nets.nets["critic"].layers)
+        self.adam_a = self._adam_descs(L.actor_optimizer, nets.nets["actor"].layers)
         act_p = list(L.actor.parameters())
         ajobs = [self._job(xb, act_p[2 * i].grad, act_p[2 * i + 1].grad, rt) for i, xb in enumerate(self.xt_actor)]
         self.jobs_a = (nat.TD7FWgJob * len(ajobs))(*ajobs)
         self.ptrs_y_enc = (P * 4)(*[t.data_ptr() for t in self.y_enc])
+
+    @staticmethod
+    def _adam_descs(opt, layers):
+        flat = getattr(opt, "flat", None)
+        if flat is None:
+            return None
+        base, descs, covered = flat.data_ptr(), [], 0
+        for pl in layers:
+            w, b = pl.weight, pl.bias
+            descs.append(nat.TD7FWgAdam(0, (w.data_ptr() - base) // 4, (b.data_ptr() - base) // 4, pl.wf.data_ptr(),
+                                        pl.wb.data_ptr() if pl.wb is not None else None, pl.ksf, pl.ksb))
+            covered += w.numel() + b.numel()
+        return (nat.TD7FWgAdam * len(descs))(*descs) if covered == flat.numel() else None
+
+    def fuses_adam(self):
+        """The weight-gradient launches can carry the optimiser steps (every
+        parameter of the encoder / critic / actor optimisers is one of their layers)."""
+        return all(d is not None for d in (self.adam_e, self.adam_c, self.adam_a))
+
+    def _wgrad(self, jobs, descs, opt, adam, td=None, prio=None, B=0):
+        fz, hp = self.nets, self.L.hp
+        if adam and descs is None:
+            raise RuntimeError("td7f_wgrad_adam: the layers do not cover the optimiser's parameters")
+        st = nat.stream_ptr(fz.dev)
+        alpha, minp = (float(hp.alpha), float(hp.min_priority)) if prio is not None else (0.0, 0.0)
+        if not adam:
+            nat.check(nat.lib().td7f_wgrad(fz.prec, len(jobs), jobs, self.ld, self.ld, td, prio, B, alpha, minp, st),
+                      "td7f_wgrad")
+            return
+        g = opt.param_groups[0]
+        P1 = lambda t: (ctypes.c_void_p * 1)(t.data_ptr())  # noqa: E731
+        F1 = lambda x: (ctypes.c_float * 1)(float(x))  # noqa: E731
+        nat.check(nat.lib().td7f_wgrad_adam(fz.prec, len(jobs), jobs, self.ld, self.ld, td, prio, B, alpha, minp, 1,
+                                            P1(opt.flat), P1(opt.m), P1(opt.v), P1(opt._step), F1(g["lr"]),
+                                            F1(g["betas"][0]), F1(g["betas"][1]), F1(g["eps"]),
+                                            F1(g["weight_decay"]), descs, nat.ptr(opt._ticket), st), "td7f_wgrad_adam")
 
     @staticmethod
     def _job(xb, gw, gb, rt):
@@ -410,18 +451,18 @@ class FusedTrain:
                                        nat.stream_ptr(fz.dev)), "td7f_wgrad")
         return self.prio
 
-    def wgrad_encoder(self):
-        """The encoder's weight/bias gradients alone (its branch of the update)."""
-        fz = self.nets
-        nat.check(nat.lib().td7f_wgrad(fz.prec, len(self.jobs_e), self.jobs_e, self.ld, self.ld, None, None, 0, 0.0,
-                                       0.0, nat.stream_ptr(fz.dev)), "td7f_wgrad")
+    def wgrad_encoder(self, adam=False):
+        """The encoder's weight/bias gradients alone (its branch of the update);
+        adam: with the encoder's optimiser step and repack (td7f_wgrad_adam)."""
+        L = self.L
+        self._wgrad(self.jobs_e, self.adam_e, L.encoder_optimizer, adam)
 
-    def wgrad_critic(self):
-        """The critic's weight/bias gradients and the LAP priorities."""
-        fz, hp = self.nets, self.L.hp
-        nat.check(nat.lib().td7f_wgrad(fz.prec, len(self.jobs_c), self.jobs_c, self.ld, self.ld, nat.ptr(self.td),
-                                       nat.ptr(self.prio), self.B, float(hp.alpha), float(hp.min_priority),
-                                       nat.stream_ptr(fz.dev)), "td7f_wgrad")
+    def wgrad_critic(self, adam=False):
+        """The critic's weight/bias gradients and the LAP priorities; adam: with
+        the critic's optimiser step and repack."""
+        L = self.L
+        self._wgrad(self.jobs_c, self.adam_c, L.critic_optimizer, adam, nat.ptr(self.td),
+                    nat.ptr(self.prio), self.B)
         return self.prio
 
     def actor(self, phase, state, zs):
@@ -432,7 +473,5 @@ class FusedTrain:
                                        ctypes.byref(self.actor_bufs), self._xts(self.xt_actor), self.ld,
                                        nat.stream_ptr(state.device)), f"td7f_actor[{phase}]")
 
-    def wgrad_actor(self):
-        fz = self.nets
-        nat.check(nat.lib().td7f_wgrad(fz.prec, len(self.jobs_a), self.jobs_a, self.ld, self.ld, None, None, 0, 0.0,
-                                       0.0, nat.stream_ptr(fz.dev)), "td7f_wgrad")
+    def wgrad_actor(self, adam=False):
+        self._wgrad(self.jobs_a, self.adam_a, self.L.actor_optimizer, adam)

@@ -40,6 +40,9 @@ ADAM_PACK = os.environ.get("EXO_ADAM_PACK", "1") != "0"
 # step on the encoder's graph branch (TD7Learner.defer_side_join);
 # EXO_ENC_STEP_BRANCH=0 joins the branch before the gradients
 ENC_STEP_BRANCH = os.environ.get("EXO_ENC_STEP_BRANCH", "1") != "0"
+# ...and every optimiser step (encoder, critic, actor) inside its weight-gradient
+# launch (td7f_wgrad_adam); EXO_WGRAD_ADAM=0: separate td7f_adam_pack launches
+WGRAD_ADAM = os.environ.get("EXO_WGRAD_ADAM", "1") != "0"
 
 
 @dataclass
@@ -724,13 +727,14 @@ class TD7Learner:
         # runs all-reduce them with the critic's
         enc_step = (branch and ADAM_PACK and self.defer_side_join and not self.sync.active
                     and isinstance(self.encoder_optimizer, FlatAdam))
+        wg_adam = enc_step and WGRAD_ADAM and tr.fuses_adam()
         self._enc_step_pending = False
         if branch:
             side, tside = stream("_side"), stream("_tside")
             with torch.cuda.stream(side):
                 tr.encoder(state, action, next_state)
                 if enc_step:
-                    tr.wgrad_encoder()
+                    tr.wgrad_encoder(adam=wg_adam)
             with torch.cuda.stream(tside):
                 qt = fz.target_heads(next_state, noise)
         else:
@@ -747,8 +751,9 @@ class TD7Learner:
             cur.wait_stream(tside)
         tr.critic(state, action, zs, zsa, qt, reward, not_done)
         if enc_step:
-            priority = tr.wgrad_critic()
+            priority = tr.wgrad_critic(adam=wg_adam)
             self._enc_step_pending = True
+            self._steps_in_wgrad = wg_adam
         else:
             if branch:
                 cur.wait_stream(side)
@@ -807,6 +812,8 @@ class TD7Learner:
                 # the encoder's step on its branch (after its weight gradients),
                 # the critic's on the update's chain
                 self._enc_step_pending = False
+                if self._steps_in_wgrad:  # already applied by the weight-gradient launches
+                    return
                 with torch.cuda.stream(self._side):
                     self.fused.adam_pack([self.encoder_optimizer], "encoder")
                 self.fused.adam_pack([self.critic_optimizer], "critic")
@@ -834,7 +841,11 @@ class TD7Learner:
             self._actor_fused_pre = False
             tr.actor(1, st, self._fixed_zs)
             tr.actor(2, st, self._fixed_zs)
-            tr.wgrad_actor()
+            # graph-replayed trainer on one GPU: the actor's optimiser step and
+            # repack in the weight-gradient launch (phase_actor_step has nothing left)
+            self._actor_step_done = (self.defer_side_join and WGRAD_ADAM and ADAM_PACK and not self.sync.active
+                                     and isinstance(self.actor_optimizer, FlatAdam) and tr.fuses_adam())
+            tr.wgrad_actor(adam=self._actor_step_done)
             return
         fixed_zs = self._fixed_zs
         pre, self._actor_pre = getattr(self, "_actor_pre", None), None
@@ -878,6 +889,11 @@ class TD7Learner:
         return cache[1]
 
     def phase_actor_step(self, flat_grad=None, grad_scale=1.0):
+        if getattr(self, "_actor_step_done", False):
+            self._actor_step_done = False
+            if flat_grad is not None:
+                raise RuntimeError("phase_actor_step: a flat gradient bucket after the fused actor step")
+            return
         if flat_grad is not None and isinstance(self.actor_optimizer, FlatAdam):
             self.actor_optimizer.step(flat_grad=flat_grad, grad_scale=grad_scale)
         elif isinstance(self.actor_optimizer, FlatAdam) and self.device.type == "cuda":

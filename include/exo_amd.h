@@ -548,6 +548,28 @@ typedef struct {
 } td7f_wg_job;
 int td7f_wgrad(int32_t prec, int32_t njobs, const td7f_wg_job *jobs, int64_t ld, int32_t rows, const float *td_dev,
                float *prio_dev, int32_t B, float alpha, float min_priority, void *stream);
+/* Where job q's layer lives in its optimiser: W[0][0] and b[0] at flat offsets
+ * w_off / b_off of optimiser opt's p / m / v; its packed operands (td7f_pack_job). */
+typedef struct {
+    int32_t opt;
+    int64_t w_off, b_off;
+    void *wf;
+    void *wb;
+    int32_t ksf, ksb;
+} td7f_wg_adam;
+/* td7f_wgrad followed by the optimiser step of every weight and bias the jobs
+ * differentiate (every job needs db) and the repack of the updated weights,
+ * in one launch: dw / db are still written, and p / m / v, the step counts
+ * (nopt FlatAdams, td7_adam_step_multi's arguments) and the packed operands end
+ * bit-identical to td7f_wgrad + td7_adam_step_multi + td7f_pack.  The weight
+ * gradients, optimiser step and repack of TD7_multi_agent.py:253-255 / :275-277
+ * as one node of the update's dependency chain; the caller makes sure the jobs
+ * cover every parameter of the optimisers (torch's Adam steps all of them). */
+int td7f_wgrad_adam(int32_t prec, int32_t njobs, const td7f_wg_job *jobs, int64_t ld, int32_t rows,
+                    const float *td_dev, float *prio_dev, int32_t B, float alpha, float min_priority, int32_t nopt,
+                    float *const *p_dev, float *const *m_dev, float *const *v_dev, float *const *step_dev,
+                    const float *lr, const float *beta1, const float *beta2, const float *eps,
+                    const float *weight_decay, const td7f_wg_adam *adam, uint32_t *ticket_dev, void *stream);
 
 #ifdef __cplusplus
 }

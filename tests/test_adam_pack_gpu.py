@@ -117,3 +117,45 @@ def test_adam_pack_rejects_partial_segment_cover():
     jobs = (TD7FPackJob * 1)(pl.job())
     rc = nat.lib().td7f_adam_pack(1, *FlatAdam.multi_args([o], segs, (1, jobs, (ctypes.c_int32 * 1)(k))))
     assert rc == -22  # EXO_EINVAL
+
+
+def _batch(B, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    s = torch.randn(B, 80, device="cuda", generator=g)
+    a = torch.rand(B, 7, device="cuda", generator=g) * 2 - 1
+    ns = torch.randn(B, 80, device="cuda", generator=g)
+    r = torch.randn(B, 1, device="cuda", generator=g)
+    nd = torch.ones(B, 1, device="cuda")
+    return s, a, ns, r, nd
+
+
+@pytest.mark.parametrize("precision,width,B", [("bf16", None, 1024), ("fp16", 256, 1000)])
+def test_wgrad_adam_matches_wgrad_then_adam_pack(precision, width, B):
+    """td7f_wgrad_adam == td7f_wgrad + td7f_adam_pack bit for bit (gradients,
+    parameters, moments, step counts, packed operands, LAP priorities) for the
+    encoder, critic and actor launches of one update, three steps running."""
+    L = _learner(precision, width)
+    F = L.fused
+    tr = F.train(B)
+    assert tr.fuses_adam()
+    cases = [("encoder", [L.encoder_optimizer], tr.wgrad_encoder, tr.enc_grad),
+             ("critic", [L.critic_optimizer], tr.wgrad_critic, tr.critic_grad),
+             ("actor", [L.actor_optimizer], tr.wgrad_actor, tr.actor_grad)]
+    with torch.no_grad():
+        for step in range(3):
+            batch = _batch(B, step)
+            L.phase_grads(*batch)  # fills the transposed operands of every layer
+            L.phase_actor_grads(batch[0], batch[1])
+            for name, opts, wgrad, grad in cases:
+                nets = [F.nets[name]]
+                before = _state(opts, nets)
+                wgrad(adam=False)
+                F.adam_pack(opts, name)
+                ref = _state(opts, nets) + [grad.clone(), tr.prio.clone()]
+                _restore(opts, nets, before)
+                grad.zero_()
+                wgrad(adam=True)
+                got = _state(opts, nets) + [grad.clone(), tr.prio.clone()]
+                for k, (a, b) in enumerate(zip(got, ref)):
+                    assert torch.equal(a, b), f"step {step} {name}: tensor {k} differs"
+    assert all(float(o._step) == 3.0 for _, opts, _, _ in cases for o in opts)
