@@ -817,11 +817,12 @@ int exo_step(exo_ctx *c, const float *act_dev, float *obs_dev, float *rew_dev, u
              const uint8_t *active_dev, void *stream) {
     if (!c || !act_dev || !obs_dev || !rew_dev || !done_dev) return EXO_EINVAL;
     DeviceGuard g(c->device);
-    const bool rows = c->step_variant == EXO_STEP_ROWS || (c->step_variant == EXO_STEP_AUTO && c->N <= 16384);
+    const bool shared = c->step_variant == EXO_STEP_ROWS_SHARED;
+    const bool rows = shared || c->step_variant == EXO_STEP_ROWS || (c->step_variant == EXO_STEP_AUTO && c->N <= 16384);
     hipError_t e;
     if (rows) {
         e = launch_exo_step_rp(c->S, c->U, act_dev, obs_dev, rew_dev, done_dev, info_dev, active_dev,
-                               (hipStream_t)stream);
+                               (hipStream_t)stream, shared);
     } else {
         const int threads = 256, lanes = 2 * c->N;
         hipLaunchKernelGGL(exo_step_kernel, dim3((lanes + threads - 1) / threads), dim3(threads), 0,
@@ -1030,7 +1031,7 @@ int exo_set_state_host(exo_ctx *c, int32_t env, const double *in) {
 }
 
 int exo_set_step_variant(exo_ctx *c, int32_t variant) {
-    if (!c || variant < EXO_STEP_AUTO || variant > EXO_STEP_ROWS) return EXO_EINVAL;
+    if (!c || variant < EXO_STEP_AUTO || variant > EXO_STEP_ROWS_SHARED) return EXO_EINVAL;
     c->step_variant = variant;
     return EXO_OK;
 }

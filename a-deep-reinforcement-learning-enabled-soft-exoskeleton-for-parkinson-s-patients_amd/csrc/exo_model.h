@@ -392,7 +392,7 @@ __host__ __device__ inline double philox_u01(uint64_t seed, uint32_t env, uint32
 #ifndef EXO_HOST_ONLY
 // row-parallel step (csrc/exo_step_rp.hip): 16 lanes per env, for small env counts
 hipError_t launch_exo_step_rp(const Dev &S, const Urdf &U, const float *act, float *obs, float *rew, uint8_t *done,
-                              float *info, const uint8_t *active, hipStream_t stream);
+                              float *info, const uint8_t *active, hipStream_t stream, bool shared = false);
 // multibody stepSimulation (csrc/exo_multibody.hip) of the envs with flag[e] != 0
 // (flag NULL = all); tgt [5][N]; clear_flag: zero the flags afterwards
 struct MbModel;

@@ -226,13 +226,13 @@ __device__ __forceinline__ void anchor(const Urdf &U, int link, const double *R2
 // and HBM fetched it up to four times (PMC: 3.1x the algorithmic bytes).
 constexpr int RP_ENVS_PER_BLOCK = 16;
 
-template <bool GATHER>
-__global__ __launch_bounds__(64 * RP_ENVS_PER_BLOCK / 4) void exo_step_rp_kernel(
+template <bool GATHER, int EPB = RP_ENVS_PER_BLOCK>
+__global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
     Dev S, Urdf U, const float *__restrict__ act, float *__restrict__ obs, float *__restrict__ rew,
     uint8_t *__restrict__ done, float *__restrict__ info, const uint8_t *__restrict__ active) {
     const int lane = threadIdx.x & 63;
     const int sub = lane & 15, grp = sub >> 3, r = sub & 7, gbase = lane & ~7, ebase = lane & ~15;
-    const int e = blockIdx.x * RP_ENVS_PER_BLOCK + (threadIdx.x >> 4);
+    const int e = blockIdx.x * EPB + (threadIdx.x >> 4);
     if (e >= S.N) return;
     const int N = S.N, c = S.counts[e], L = S.L[e];
     if ((active && !active[e]) || c >= L - 1) return; // uniform over the env's 16 lanes
@@ -479,7 +479,7 @@ extern "C" int exo_debug_set_stamps(unsigned long long *buf) {
 
 namespace exo {
 hipError_t launch_exo_step_rp(const Dev &S, const Urdf &U, const float *act, float *obs, float *rew, uint8_t *done,
-                              float *info, const uint8_t *active, hipStream_t stream) {
+                              float *info, const uint8_t *active, hipStream_t stream, bool shared) {
     // RHS neighbour pulls: LDS permutes (default) or DPP lane moves (EXO_RP_GATHER=1:
     // bit-identical, measured slower -- 38.2 vs 34.9 us at 4,096 envs; the fp64
     // pulls are two dword moves each plus the DPP hazard waits, where the
@@ -488,6 +488,17 @@ hipError_t launch_exo_step_rp(const Dev &S, const Urdf &U, const float *act, flo
         const char *v = getenv("EXO_RP_GATHER");
         return v && v[0] == '1';
     }();
+    // shared: 32 envs per 512-thread workgroup (two waves per SIMD, a CU
+    // filled by one workgroup): 4,096 envs take 128 CUs and leave the rest
+    // whole for kernels running beside the step (the trainer's fused TD7
+    // passes need a CU's full register file); 16 envs / 256 threads spread
+    // over every CU (fastest alone)
+    if (shared && !gather) {
+        const dim3 grid((S.N + 31) / 32), block(512);
+        hipLaunchKernelGGL((exo_step_rp_kernel<false, 32>), grid, block, 0, stream, S, U, act, obs, rew, done, info,
+                           active);
+        return hipGetLastError();
+    }
     const dim3 grid((S.N + RP_ENVS_PER_BLOCK - 1) / RP_ENVS_PER_BLOCK), block(64 * RP_ENVS_PER_BLOCK / 4);
     if (gather)
         hipLaunchKernelGGL(exo_step_rp_kernel<true>, grid, block, 0, stream, S, U, act, obs, rew, done, info, active);

@@ -169,6 +169,10 @@ class VecTrainer:
         self.resets = 0  # episode-round resets done by step()
         self.graphs = {}
         self.dp = agent.sync.active  # tests set it to exercise the 3-graph layout at world 1
+        # the env step shares the GPU with the TD7 passes: packed into half the
+        # CUs (512-thread workgroups) unless the caller chose a kernel variant
+        if getattr(env, "step_variant", None) == "auto" and os.environ.get("EXO_TRAIN_STEP_SHARED", "1") == "1":
+            env.set_step_variant("rows_shared")
         self.last_actions = None
         # exploration: "gaussian" (TD7_multi_agent.py select_action) or "pink"
         # (TD7_multi_agent_Pink_noise.py: one coloured sequence per episode round)

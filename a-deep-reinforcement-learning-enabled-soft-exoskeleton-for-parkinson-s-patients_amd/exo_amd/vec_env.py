@@ -202,13 +202,17 @@ class VecExoskeletonEnv:
                   "exo_eval_metrics", self._ctx)
         return counters
 
-    STEP_VARIANTS = {"auto": 0, "lanes": 1, "rows": 2}
+    STEP_VARIANTS = {"auto": 0, "lanes": 1, "rows": 2, "rows_shared": 3}
+    step_variant = "auto"
 
     def set_step_variant(self, name):
         """exo_step kernel: 'lanes' (one lane per ODE solve), 'rows' (16 lanes per
-        env), 'auto' (rows for N <= 16384)."""
+        env), 'auto' (rows for N <= 16384), 'rows_shared' (rows, 32 envs per
+        512-thread workgroup: half the CUs at 4,096 envs, for a GPU shared with
+        concurrent kernels -- the graph-replayed trainer picks it)."""
         nat.check(nat.lib().exo_set_step_variant(self._ctx, self.STEP_VARIANTS[name]), "exo_set_step_variant",
                   self._ctx)
+        self.step_variant = name
 
     # ----------------------------------------------------- physics model
     @staticmethod

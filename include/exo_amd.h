@@ -113,10 +113,13 @@ int exo_set_state_host(exo_ctx *ctx, int32_t env, const double *in);
 /* Kernel variant of exo_step: EXO_STEP_LANES = one lane per ODE solve (best
  * throughput at large N), EXO_STEP_ROWS = 16 lanes per env, one joint row per
  * lane (lowest latency at small N), EXO_STEP_AUTO (default) = ROWS for
- * N <= 16384.  Both compute the same step. */
+ * N <= 16384, EXO_STEP_ROWS_SHARED = ROWS packed 32 envs per 512-thread
+ * workgroup (half the CUs at 4,096 envs: for a GPU shared with concurrent
+ * kernels, the training loop).  All compute the same step. */
 #define EXO_STEP_AUTO 0
 #define EXO_STEP_LANES 1
 #define EXO_STEP_ROWS 2
+#define EXO_STEP_ROWS_SHARED 3
 int exo_set_step_variant(exo_ctx *ctx, int32_t variant);
 
 /* ------------------------------------------------------------------------

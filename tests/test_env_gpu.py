@@ -26,7 +26,7 @@ def _close_obs(a, b):
     np.testing.assert_allclose(a, b, rtol=2e-6, atol=2e-6)
 
 
-VARIANTS = ["rows", "lanes"]
+VARIANTS = ["rows", "lanes", "rows_shared"]
 
 
 def _batched_golden_env(variant="auto"):
@@ -217,13 +217,18 @@ def test_kernel_variants_agree():
     rng = np.random.default_rng(4)
     for k in range(40):
         a = torch.as_tensor(rng.uniform(-1, 1, (1030, 7)).astype(np.float32), device=envs[0].device)
-        outs = [e.step(a) for e in envs]
-        o0, o1 = [[t.cpu().numpy() for t in (o[0], o[1], o[3])] for o in outs]
-        np.testing.assert_allclose(o0[0], o1[0], rtol=1e-6, atol=1e-7)
-        np.testing.assert_allclose(o0[1], o1[1], rtol=1e-6, atol=1e-8)
-        np.testing.assert_allclose(o0[2], o1[2], rtol=1e-5, atol=1e-7)
+        outs = [[t.cpu().numpy() for t in (o[0], o[1], o[3])] for o in (e.step(a) for e in envs)]
+        o0 = outs[0]
+        for o1 in outs[1:]:
+            np.testing.assert_allclose(o0[0], o1[0], rtol=1e-6, atol=1e-7)
+            np.testing.assert_allclose(o0[1], o1[1], rtol=1e-6, atol=1e-8)
+            np.testing.assert_allclose(o0[2], o1[2], rtol=1e-5, atol=1e-7)
     for i in (0, 513, 1029):
-        np.testing.assert_allclose(envs[0].get_state(i), envs[1].get_state(i), rtol=1e-9, atol=1e-12)
+        for e in envs[1:]:
+            np.testing.assert_allclose(envs[0].get_state(i), e.get_state(i), rtol=1e-9, atol=1e-12)
+    # the two row-parallel launch shapes run the same code per env: bit-identical
+    for i in (0, 513, 1029):
+        np.testing.assert_array_equal(envs[0].get_state(i), envs[2].get_state(i))
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
