@@ -439,8 +439,18 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / n
 
-    def kernel_timing(n):
-        """exo_step_kernel alone, HIP events on the launch stream, all envs active."""
+    def kernel_timing(n, variant=None):
+        """exo_step_kernel alone, HIP events on the launch stream, all envs active
+        (variant: the env's kernel variant for this measurement, restored after)."""
+        prev = env.step_variant
+        if variant is not None:
+            env.set_step_variant(variant)
+        try:
+            return _kernel_timing(n)
+        finally:
+            env.set_step_variant(prev)
+
+    def _kernel_timing(n):
         env.reset()
         evs = []
         for _ in range(n):
@@ -471,10 +481,16 @@ def main():
     elapsed = time.perf_counter() - t0
     resets_in_window = (trainer.resets if trainer is not None else state.get("resets", 0)) - resets0
     reset_ms = reset_timing()
+    loop_kern_ms = None
     if ev:  # env mode: the timed launches themselves
         kern_ms, kern_active = float(np.mean([a.elapsed_time(b) for a, b in ev])), env_steps / args.steps
     else:   # train mode: the env kernel is inside graph replays; time it separately afterwards
-        kern_ms, kern_active = kernel_timing(min(args.kernel_timing_steps, int(Ls.min()) - 3))
+        # the roofline kernel: the env step's default shape alone (the shape
+        # profiles/*_env kernel stats time); the trainer runs the rows_shared
+        # shape beside the TD7 passes -- timed alone too, reported with it
+        nk = min(args.kernel_timing_steps, int(Ls.min()) - 3)
+        kern_ms, kern_active = kernel_timing(nk, "auto")
+        loop_kern_ms = kernel_timing(nk)[0] if env.step_variant != "auto" else None
     # Whole-round rate, independent of where the K-iteration window falls in
     # the 344-step episode round: one round = round_len iterations (active
     # env-steps A_round = sum over k of the envs still running) + one reset.
@@ -542,6 +558,11 @@ def main():
                          "bytes_per_env_step": BYTES_PER_ENV_STEP, "avg_kernel_ms": kern_ms,
                          "active_envs_per_launch": active_avg},
         }
+        if loop_kern_ms is not None:
+            res["roofline"]["training_loop_variant"] = {
+                "variant": env.step_variant, "avg_kernel_ms_alone": loop_kern_ms,
+                "note": "32 envs per 512-thread workgroup: half the CUs at 4,096 envs, so the fused TD7 "
+                        "workgroups beside it keep whole CUs (DESIGN.md 4)"}
         vfl, vsrc = pmc_valu_flops(N) if args.physics == "ideal" and N <= 16384 else (None, None)
         if vfl and kern_active == N:
             # the env kernel is fp64-VALU/latency bound -- its
