@@ -283,6 +283,36 @@ __host__ __device__ __forceinline__ double rms14(const double *x) {
     return sqrt(s) / 3.7416573867739413; // np.linalg.norm(x) / 14 ** 0.5 (scipy common.py norm)
 }
 
+// x^(-1/5) for the step-size controller (scipy rk.py `error_norm **
+// error_exponent`, common.py select_initial_step): the library pow(double) is a
+// ~100-instruction dependent chain (extended-precision log and exp), paid once
+// per step attempt on the solve's critical path.  Here: a float seed from the
+// hardware v_log_f32 / v_exp_f32 (relative error ~3e-7), then one
+// second-order correction in fp64: with e = 1 - x*y^5,
+// x^(-1/5) = y*(1 - e)^(-1/5) = y*(1 + e/5 + 3e^2/25 + O(e^3)); |e| < 2e-6,
+// so the truncation is < 1e-18 (checked against long-double powers on 4e5
+// arguments in [1e-30, 1e30]: within 1 ulp of x^-0.2, as numpy's pow is).
+// Outside [1e-30, 1e30] (float range), for NaN and in host builds the library
+// pow runs.
+#ifndef EXO_FASTPOW
+#define EXO_FASTPOW 1
+#endif
+__host__ __device__ __forceinline__ double pow_m5th(double x) {
+#if EXO_FASTPOW && defined(__HIP_DEVICE_COMPILE__)
+    if (!(x > 1e-30 && x < 1e30)) return pow(x, -0.2);
+    const float l2 = __builtin_amdgcn_logf((float)x); // log2
+    const float yf = __builtin_amdgcn_exp2f(-0.2f * l2);
+    const double y = (double)yf, y2 = y * y, y5 = y2 * y2 * y;
+    const double e = fma(-x, y5, 1.0);
+    const double r = fma(y * e, fma(e, 0.12, 0.2), y);
+    // the double -0.2 is -(1/5 + 1.11e-17): x^-0.2 = x^(-1/5) * (1 - 1.11e-17 ln x)
+    // (up to 7 ulp at x = 1e30 without it); within 1 ulp of pow(x, -0.2) after it
+    return fma(r, -1.1102230246251565e-17 * 0.6931471805599453 * (double)l2, r);
+#else
+    return pow(x, -0.2);
+#endif
+}
+
 // Returns false if scipy would have failed (step size underflow) or the
 // attempt guard tripped; q_out is then NaN.
 __host__ __device__ inline bool rk45_solve(const OdeM &M, const double *T, double *q_out) {
@@ -306,7 +336,7 @@ __host__ __device__ inline bool rk45_solve(const OdeM &M, const double *T, doubl
 #pragma unroll
         for (int i = 0; i < 7; ++i) { tmp[i] = (y1v[i] - 0.0) / atol; tmp[7 + i] = (a1[i] - a0[i]) / atol; }
         const double d2 = rms14(tmp) / h0;
-        const double h1 = (d1 <= 1e-15 && d2 <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : pow(0.01 / fmax(d1, d2), 0.2);
+        const double h1 = (d1 <= 1e-15 && d2 <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : 1.0 / pow_m5th(0.01 / fmax(d1, d2));
         h_abs = fmin(fmin(100 * h0, h1), tb);
     }
     double t = 0.0;
@@ -359,7 +389,7 @@ __host__ __device__ inline bool rk45_solve(const OdeM &M, const double *T, doubl
             }
             const double en = rms14(e);
             if (en < 1) {
-                double factor = (en == 0) ? 10.0 : fmin(10.0, 0.9 * pow(en, -0.2));
+                double factor = (en == 0) ? 10.0 : fmin(10.0, 0.9 * pow_m5th(en));
                 if (rejected) factor = fmin(1.0, factor);
                 h_abs *= factor;
                 t = t_new;
@@ -367,7 +397,7 @@ __host__ __device__ inline bool rk45_solve(const OdeM &M, const double *T, doubl
                 for (int i = 0; i < 7; ++i) { q[i] = qs[i]; v[i] = vs[i]; a0[i] = A[6][i]; }
                 accepted = true;
             } else {
-                h_abs *= fmax(0.2, 0.9 * pow(en, -0.2));
+                h_abs *= fmax(0.2, 0.9 * pow_m5th(en));
                 rejected = true;
             }
         }

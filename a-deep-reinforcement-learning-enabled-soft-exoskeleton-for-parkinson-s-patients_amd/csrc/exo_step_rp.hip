@@ -149,7 +149,7 @@ __device__ bool rk45_rows(const RM &M, double T, double &q_out) {
         const double a1 = row_acc(M, T, 0.0, y1v);
         const double xq = y1v / atol, xv = (a1 - a0) / atol;
         const double d2 = sqrt(group_sum(xq * xq + xv * xv)) * inv_sqrt14 / h0;
-        const double h1 = (d1 <= 1e-15 && d2 <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : pow(0.01 / fmax(d1, d2), 0.2);
+        const double h1 = (d1 <= 1e-15 && d2 <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : 1.0 / pow_m5th(0.01 / fmax(d1, d2));
         h_abs = fmin(fmin(100 * h0, h1), tb);
     }
     double t = 0.0;
@@ -194,7 +194,7 @@ __device__ bool rk45_rows(const RM &M, double T, double &q_out) {
             const double e_v = ev * h / (atol + fmax(fabs(v), fabs(vs)) * rtol);
             const double en = sqrt(group_sum(e_q * e_q + e_v * e_v)) * inv_sqrt14;
             if (en < 1) {
-                double factor = (en == 0) ? 10.0 : fmin(10.0, 0.9 * pow(en, -0.2));
+                double factor = (en == 0) ? 10.0 : fmin(10.0, 0.9 * pow_m5th(en));
                 if (rejected) factor = fmin(1.0, factor);
                 h_abs *= factor;
                 t = t_new;
@@ -203,7 +203,7 @@ __device__ bool rk45_rows(const RM &M, double T, double &q_out) {
                 a0 = A[6];
                 accepted = true;
             } else {
-                h_abs *= fmax(0.2, 0.9 * pow(en, -0.2));
+                h_abs *= fmax(0.2, 0.9 * pow_m5th(en));
                 rejected = true;
             }
         }
