@@ -6,7 +6,7 @@
 // lanes: lanes 0-7 run the actuated solve, lanes 8-15 the tremor-only solve,
 // and lane r of a group owns joint row r of the 7-DOF ODE (row 7 pads).  The
 // RHS a = I^-1 (T - D v - K q) needs the other rows' q, v and r: they are
-// pulled with wavefront permutes (ds_bpermute) inside the 8-lane group; the
+// exchanged through wave-private LDS slots inside the 8-lane group; the
 // RK45 error norm is an 8-lane butterfly sum, so every lane of a group takes
 // the same step-size decisions.  The arithmetic is the same as the one-lane
 // kernel (same per-row summation orders), so the two variants agree to
@@ -115,6 +115,44 @@ struct RowD {
 };
 __device__ __forceinline__ double row_acc(const RowD &M, double T, double q, double v) {
     return row_acc_dpp(M.m, M.upper, T, q, v);
+}
+
+// The same RHS with the neighbour values exchanged through LDS: each lane
+// stores its (q, v) as one 16-byte write and reads its 4 source rows' pairs
+// as 16-byte reads (5 LDS ops where the permutes take 16 32-bit moves), then
+// r the same way (1 + 4 ops instead of 8).  Wave-private slots (one per lane),
+// so no workgroup barrier: a wavefront's LDS ops execute in order, and the
+// wave_barrier keeps the compiler from moving the reads above the write.
+// Same terms in the same order as row_acc: bit-identical results.
+struct RowL {
+    RowM m;
+    double2 *qv;    // [64 x waves] workgroup slots
+    double *rr;
+    int self, wbase; // this lane's slot, its wavefront's first slot
+};
+__device__ __forceinline__ double row_acc(const RowL &M, double T, double q, double v) {
+    M.qv[M.self] = make_double2(q, v);
+    __builtin_amdgcn_wave_barrier();
+    double2 p[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) p[m] = M.qv[M.wbase + M.m.dsrc[m]];
+    double dq = 0.0, kq = 0.0;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        dq += M.m.d[m] * p[m].y;
+        kq += M.m.s[m] * p[m].x;
+    }
+    const double r = T - dq - kq;
+    M.rr[M.self] = r;
+    __builtin_amdgcn_wave_barrier();
+    double rs[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) rs[m] = M.rr[M.wbase + M.m.isrc[m]];
+    double a = 0.0;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) a += M.m.ii[m] * rs[m];
+    __builtin_amdgcn_wave_barrier();
+    return a;
 }
 
 // acceleration of row r: I^-1 (T - D v - K q), neighbours pulled from the group
@@ -226,7 +264,8 @@ __device__ __forceinline__ void anchor(const Urdf &U, int link, const double *R2
 // and HBM fetched it up to four times (PMC: 3.1x the algorithmic bytes).
 constexpr int RP_ENVS_PER_BLOCK = 16;
 
-template <bool GATHER, int EPB = RP_ENVS_PER_BLOCK>
+// PULL: the RHS neighbour exchange -- 0 LDS permutes, 1 DPP lane moves, 2 LDS slots (default)
+template <int PULL, int EPB = RP_ENVS_PER_BLOCK>
 __global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
     Dev S, Urdf U, const float *__restrict__ act, float *__restrict__ obs, float *__restrict__ rew,
     uint8_t *__restrict__ done, float *__restrict__ info, const uint8_t *__restrict__ active) {
@@ -434,8 +473,12 @@ __global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
     const double T = (r < 7) ? (grp == 0 ? Ta_r : tr_r) : 0.0;
     double qr;
     bool ok;
-    if constexpr (GATHER) {
+    if constexpr (PULL == 1) {
         ok = rk45_rows(RowD{M0, r >= 4}, T, qr);
+    } else if constexpr (PULL == 2) {
+        __shared__ double2 s_qv[64 * EPB / 4];
+        __shared__ double s_rr[64 * EPB / 4];
+        ok = rk45_rows(RowL{M0, s_qv, s_rr, (int)threadIdx.x, (int)(threadIdx.x & ~63u)}, T, qr);
     } else {
         ok = rk45_rows(M0, T, qr);
     }
@@ -480,30 +523,37 @@ extern "C" int exo_debug_set_stamps(unsigned long long *buf) {
 namespace exo {
 hipError_t launch_exo_step_rp(const Dev &S, const Urdf &U, const float *act, float *obs, float *rew, uint8_t *done,
                               float *info, const uint8_t *active, hipStream_t stream, bool shared) {
-    // RHS neighbour pulls: LDS permutes (default) or DPP lane moves (EXO_RP_GATHER=1:
-    // bit-identical, measured slower -- 38.2 vs 34.9 us at 4,096 envs; the fp64
-    // pulls are two dword moves each plus the DPP hazard waits, where the
-    // permutes run on the LDS pipe beside the VALU)
-    static const bool gather = [] {
+    // RHS neighbour exchange (EXO_RP_GATHER, all bit-identical): 2 = wave-private
+    // LDS slots, 16-byte writes / reads (default: 26.8 vs 31.1 us at 4,096 envs,
+    // profiles/r02f_raw/ab_pull.txt); 0 = LDS permutes (ds_bpermute, 4 32-bit
+    // moves per (q, v) pull); 1 = DPP lane moves (slower still: two dword moves
+    // per fp64 pull plus the DPP hazard waits -- 38.2 vs 34.9 us against 0)
+    static const int pull = [] {
         const char *v = getenv("EXO_RP_GATHER");
-        return v && v[0] == '1';
+        return v ? atoi(v) : 2;
     }();
     // shared: 32 envs per 512-thread workgroup (two waves per SIMD, a CU
     // filled by one workgroup): 4,096 envs take 128 CUs and leave the rest
     // whole for kernels running beside the step (the trainer's fused TD7
     // passes need a CU's full register file); 16 envs / 256 threads spread
     // over every CU (fastest alone)
-    if (shared && !gather) {
+    if (shared && pull != 1) {
         const dim3 grid((S.N + 31) / 32), block(512);
-        hipLaunchKernelGGL((exo_step_rp_kernel<false, 32>), grid, block, 0, stream, S, U, act, obs, rew, done, info,
-                           active);
+        if (pull == 2)
+            hipLaunchKernelGGL((exo_step_rp_kernel<2, 32>), grid, block, 0, stream, S, U, act, obs, rew, done, info,
+                               active);
+        else
+            hipLaunchKernelGGL((exo_step_rp_kernel<0, 32>), grid, block, 0, stream, S, U, act, obs, rew, done, info,
+                               active);
         return hipGetLastError();
     }
     const dim3 grid((S.N + RP_ENVS_PER_BLOCK - 1) / RP_ENVS_PER_BLOCK), block(64 * RP_ENVS_PER_BLOCK / 4);
-    if (gather)
-        hipLaunchKernelGGL(exo_step_rp_kernel<true>, grid, block, 0, stream, S, U, act, obs, rew, done, info, active);
+    if (pull == 1)
+        hipLaunchKernelGGL(exo_step_rp_kernel<1>, grid, block, 0, stream, S, U, act, obs, rew, done, info, active);
+    else if (pull == 2)
+        hipLaunchKernelGGL(exo_step_rp_kernel<2>, grid, block, 0, stream, S, U, act, obs, rew, done, info, active);
     else
-        hipLaunchKernelGGL(exo_step_rp_kernel<false>, grid, block, 0, stream, S, U, act, obs, rew, done, info, active);
+        hipLaunchKernelGGL(exo_step_rp_kernel<0>, grid, block, 0, stream, S, U, act, obs, rew, done, info, active);
     return hipGetLastError();
 }
 } // namespace exo

@@ -1,0 +1,26 @@
+#!/bin/bash
+# GPU box: env parity tests with the LDS-slot RHS exchange (EXO_RP_GATHER=2), then
+# exo_step_rp kernel time (env bench, rocprof) and the training loop for pull forms 0 / 2, alternated
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+EXO_RP_GATHER=2 timeout -k 10 300 python -u -m pytest tests/test_env_gpu.py tests/test_rollout_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pull_tests.log 2>&1 || exit $?
+out=gpurun_out/ab_pull.txt
+: > $out
+for rep in 1 2; do
+  for g in 0 2; do
+    rm -rf gpurun_out/envab
+    EXO_RP_GATHER=$g timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/envab -o run -- python3 bench.py --mode env --steps 300 --warmup 20 --no-cpu-baseline > gpurun_out/envab.log 2>&1 || exit $?
+    python3 -c "
+import csv; r=[x for x in csv.DictReader(open('gpurun_out/envab/run_kernel_stats.csv')) if 'exo_step' in x['Name']]
+print('env GATHER=$g', [(x['Calls'], round(float(x['AverageNs'])/1e3,2), round(float(x['MinNs'])/1e3,2)) for x in r])" >> $out
+  done
+done
+for rep in 1 2; do
+  for g in 0 2; do
+    EXO_RP_GATHER=$g timeout -k 10 200 python3 bench.py --steps 300 --warmup 50 --no-cpu-baseline > gpurun_out/pull_bench_$g.json 2>gpurun_out/pull_bench_err.log || exit $?
+    python3 -c "
+import json; d=json.loads(open('gpurun_out/pull_bench_$g.json').read().strip().splitlines()[-1]); print('train GATHER=$g', round(d['value']), round(d['ms_per_step'],4), d['roofline']['avg_kernel_ms'], d['roofline']['training_loop_variant']['avg_kernel_ms_alone'])" >> $out
+  done
+done
+cat $out
