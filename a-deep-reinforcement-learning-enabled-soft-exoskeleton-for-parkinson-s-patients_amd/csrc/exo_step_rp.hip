@@ -278,10 +278,7 @@ __global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
     STAMP(0);
 
     const double maxS = S.maxSE[e], maxE = S.maxSE[(size_t)N + e];
-    double F[7];
     const float *a = act + (size_t)e * ACT;
-#pragma unroll
-    for (int j = 0; j < 7; ++j) F[j] = (((double)a[j] + 1) / 2) * (j < 2 ? maxE : maxS); // :256-266
 
     // ---- forward kinematics of the state left by the last stepSimulation (all lanes)
     double q5[5], refo[6], refn[6];
@@ -299,14 +296,8 @@ __global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
         sh1[d] = S.shift[(size_t)((2 * j) * 3 + d) * N + e];
         sh2[d] = S.shift[(size_t)((2 * j + 1) * 3 + d) * N + e];
     }
-    double tr[7], pa[7], pa2[7];
-#pragma unroll
-    for (int i = 0; i < 7; ++i) {
-        tr[i] = S.tremor[((size_t)c * 7 + i) * N + e];
-        pa[i] = S.prev_a[(size_t)i * N + e];
-        pa2[i] = S.prev2_a[(size_t)i * N + e];
-    }
     const double pa_j = S.prev_a[(size_t)j * N + e];
+    const double pa2_j = S.prev2_a[(size_t)j * N + e];
     const double tr_j = S.tremor[((size_t)c * 7 + j) * N + e];
     const int r4 = r & 3;  // tremor rows 0..3 of the observation at c - 1, c + 1
     const double tm1 = S.tremor[((size_t)(c > 0 ? c - 1 : 0) * 7 + r4) * N + e];
@@ -378,44 +369,52 @@ __global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
         tau[jj][1] = shfl_d(ty, ebase + jj);
         tau[jj][2] = shfl_d(tz, ebase + jj);
     }
+    STAMP(6);
     double at[4]; // :394-400, actuator order 3, 4, 5, 7, 6
     at[0] = tau[2][1] + tau[3][1] + tau[4][1] + tau[6][1] + tau[5][1];
     at[1] = tau[2][0] + tau[3][0] + tau[4][0] + tau[6][0] + tau[5][0];
     at[2] = tau[2][2] + tau[3][2] + tau[4][2] + tau[6][2] + tau[5][2];
     at[3] = fabs(tau[0][1]) - fabs(tau[1][1]);
-    double Ta[7];
-#pragma unroll
-    for (int i = 0; i < 7; ++i) Ta[i] = tr[i] + (i < 4 ? at[i] : 0.0);
     // per-lane values of this lane's actuator j / joint row r (dynamic indices
     // into small register arrays would go to scratch)
-    const double F_j = (((double)a[j] + 1) / 2) * (j < 2 ? maxE : maxS);
+    const double F_j = (((double)a[j] + 1) / 2) * (j < 2 ? maxE : maxS); // :256-266
     const double tr_r = (r < 7) ? tr_j : 0.0;
     const double at_r = (r == 0) ? at[0] : (r == 1) ? at[1] : (r == 2) ? at[2] : (r == 3) ? at[3] : 0.0;
     const double Ta_r = tr_r + at_r;
     // every lane has read the carried state it needs; lanes of this env now
     // overwrite it (counts, ref, posv, prev actions, later the joints)
-    __syncthreads();
+    // an env's 16 lanes sit in one wavefront, so only this wave's own loads
+    // must have returned before its lanes overwrite the carried state: wait for
+    // them (vmcnt 0; the "memory" clobber keeps the compiler from moving a
+    // store above it) instead of a workgroup barrier, which also waited for the
+    // other waves of the workgroup
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    // reward terms (:341-366), term i on lane r = i of the actuated group (no
+    // divergent per-term branches in one lane: every lane takes its two
+    // divisions at once), summed over the 8-lane group by the butterfly; the
+    // sums' order differs from the reference's i = 0..6 loop only by rounding
+    double g_unw, g_st, g_nred, g_sa, g_sm;
+    {
+        const double eps = 1e-10;
+        const bool live = r < 7, axis = r < 4, sel = axis && ((seq >> r) & 1);
+        const double Tabs = fabs(Ta_r), tabs = fabs(tr_r);
+        const double st_i = (Tabs - tabs) / tabs + 1;
+        const double vv = (Tabs - tabs) / (tabs + eps) * 100;
+        const double d = F_j - 2 * pa_j + pa2_j;
+        g_unw = group_sum((axis && !sel) ? Tabs : 0.0);
+        g_st = group_sum(sel ? st_i : 0.0);
+        g_nred = group_sum((live && isfinite(vv) && vv < 0) ? 1.0 : 0.0);
+        g_sa = group_sum(live ? F_j : 0.0);
+        g_sm = group_sum(live ? d * d : 0.0);
+    }
 
     // ---- reward, done, observation, info, carried state (:341-366, :448-469, :487-570)
     if (grp == 0) {
         if (r == 0) {
             const double eps = 1e-10, Msum = maxE + maxS, naxes = c_naxes;
-            double unw = 0.0, st = 0.0, sa = 0.0, sm = 0.0;
-            int nred = 0;
-#pragma unroll
-            for (int i = 0; i < 7; ++i) {
-                const double Tabs = fabs(Ta[i]), tabs = fabs(tr[i]);
-                if (i < 4) {
-                    if ((seq >> i) & 1) st += (Tabs - tabs) / tabs + 1;
-                    else unw += Tabs;
-                }
-                const double vv = (Tabs - tabs) / (tabs + eps) * 100;
-                if (isfinite(vv) && vv < 0) nred++;
-                sa += F[i];
-                const double d = F[i] - 2 * pa[i] + pa2[i];
-                sm += d * d;
-            }
-            sm /= 7;
+            const double unw = g_unw, st = g_st, sa = g_sa, sm = g_sm / 7;
+            const int nred = (int)g_nred;
             const double r_unw = exp(-(unw / (Msum / 4 / naxes)) + eps) * 0.5;
             const double r_tor = exp((-st + eps) / naxes) * 0.9;
             const double r_axis = nred * 0.5;
@@ -430,6 +429,7 @@ __global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
             }
             S.counts[e] = c + 1;
         }
+        STAMP(7);
         float *o = obs + (size_t)e * OBS;
         if (r < 7) {
             const double nrm = c_nrm;

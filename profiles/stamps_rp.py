@@ -40,6 +40,11 @@ for k in range(60):
             res.setdefault(p, []).append(float(np.median(d[:, i])))
         res.setdefault("total_median", []).append(float(np.median(tot)))
         res.setdefault("total_max", []).append(float(np.max(tot)))
+        full = buf.view(blocks, 8).cpu().numpy().astype(np.int64)
+        if (full[:, 6] > 0).all() and (full[:, 7] > 0).all():  # sub-phases of torques+reward+obs+state
+            res.setdefault("sub:torque_table", []).append(float(np.median(full[:, 6] - full[:, 2])))
+            res.setdefault("sub:sync+reward", []).append(float(np.median(full[:, 7] - full[:, 6])))
+            res.setdefault("sub:obs+state", []).append(float(np.median(full[:, 3] - full[:, 7])))
 summary = {k: float(np.median(v)) for k, v in res.items()}
 summary["shares"] = {p: summary[p] / summary["total_median"] for p in phases}
 print(json.dumps(summary, indent=1))
