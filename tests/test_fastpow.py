@@ -1,0 +1,31 @@
+"""The RK45 step-size controller's x^-0.2 (pow_m5th, csrc/exo_model.h) restated in numpy:
+a float32 seed (the device takes it from v_log_f32 / v_exp_f32; numpy's float32 log2 / exp2
+are at least as coarse), one second-order fp64 correction and the correction for the double
+-0.2 being -(1/5 + 1.1e-17).  Pins the accuracy claim of DESIGN.md section 4: within 1 ulp of
+x ** -0.2 (the value scipy's rk.py computes, `error_norm ** error_exponent`) over the range
+the device path takes, [1e-30, 1e30].  The device kernels themselves are held to the
+reference traces by tests/test_env_gpu.py."""
+import numpy as np
+
+
+def _pow_m5th(x):
+    l2 = np.log2(x.astype(np.float32))
+    y = np.exp2(np.float32(-0.2) * l2).astype(np.float64)
+    y2 = y * y
+    y5 = y2 * y2 * y
+    e = 1.0 - x * y5
+    r = y * e * (e * 0.12 + 0.2) + y
+    return r * (-1.1102230246251565e-17 * 0.6931471805599453 * l2.astype(np.float64)) + r
+
+
+def test_fast_inverse_fifth_root_within_one_ulp():
+    rng = np.random.default_rng(0)
+    x = np.concatenate([10 ** rng.uniform(-29.9, 29.9, 100_000), rng.uniform(0.5, 2.0, 50_000),
+                        10 ** rng.uniform(-3, 3, 50_000)])
+    ref = np.power(x.astype(np.longdouble), np.longdouble(np.float64(-0.2))).astype(np.float64)
+    ulp = np.abs(_pow_m5th(x) - ref) / np.spacing(ref)
+    assert ulp.max() <= 1.0
+    # without the exponent correction the error grows with |ln x| (7 ulp at 1e30)
+    l2 = np.log2(x.astype(np.float32)).astype(np.float64)
+    r = _pow_m5th(x) / (1 - 1.1102230246251565e-17 * 0.6931471805599453 * l2)
+    assert (np.abs(r - ref) / np.spacing(ref)).max() > 2
