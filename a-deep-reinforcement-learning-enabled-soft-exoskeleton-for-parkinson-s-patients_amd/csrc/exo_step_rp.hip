@@ -59,6 +59,28 @@ constexpr int RP_ICOL[8][4] = {{0, 3, 6, 7}, {1, 2, 4, 5}, {1, 2, 4, 5}, {0, 3, 
 constexpr int RP_ISYM[8][4] = {{0, 1, 2, -1}, {6, 7, 8, 9}, {7, 10, 11, 12}, {1, 3, 4, -1},
                                {8, 11, 13, 14}, {9, 12, 14, 15}, {2, 4, 5, -1}, {-1, -1, -1, -1}};
 
+// The tables above indexed by the lane's row r (a runtime value) compile to
+// global loads of the table, each followed by a wait for EVERY outstanding
+// load (vmcnt(0)) before the dependent load of the matrix entry could issue:
+// the kernel-start load burst was drained 4+ times in a row.  Packed into
+// 64-bit immediates instead (byte r of column m = entry + 1): pure ALU.
+constexpr unsigned long long pack_col(const int (&t)[8][4], int m) {
+    unsigned long long v = 0;
+    for (int r = 0; r < 8; ++r) v |= (unsigned long long)(t[r][m] + 1) << (8 * r);
+    return v;
+}
+__device__ __forceinline__ int tab_at(unsigned long long k, int r) { return (int)((k >> (8 * r)) & 0xff) - 1; }
+// K_LINK[k] (exo_model.h) for a runtime k < 14, likewise
+constexpr unsigned long long pack_klink(int k0) {
+    unsigned long long v = 0;
+    for (int k = k0; k < k0 + 8 && k < 14; ++k) v |= (unsigned long long)K_LINK[k] << (8 * (k - k0));
+    return v;
+}
+__device__ __forceinline__ int klink(int k) {
+    constexpr unsigned long long lo = pack_klink(0), hi = pack_klink(8);
+    return (int)(((k < 8 ? lo : hi) >> (8 * (k & 7))) & 0xff);
+}
+
 struct RowM {
     double d[4], s[4], ii[4];
     int dsrc[4], isrc[4];
@@ -310,12 +332,24 @@ __global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
     RowM M0;
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
-        const int ds = RP_DSYM[r][m], is = RP_ISYM[r][m];
-        M0.d[m] = ds >= 0 ? S.dnz[(size_t)ds * N + e] : 0.0;
-        M0.s[m] = ds >= 0 ? S.snz[(size_t)ds * N + e] : 0.0;
-        M0.ii[m] = is >= 0 ? S.iinv[(size_t)is * N + e] : 0.0;
-        M0.dsrc[m] = gbase + RP_DCOL[r][m];
-        M0.isrc[m] = gbase + RP_ICOL[r][m];
+        constexpr unsigned long long KDS[4] = {pack_col(RP_DSYM, 0), pack_col(RP_DSYM, 1), pack_col(RP_DSYM, 2),
+                                               pack_col(RP_DSYM, 3)};
+        constexpr unsigned long long KIS[4] = {pack_col(RP_ISYM, 0), pack_col(RP_ISYM, 1), pack_col(RP_ISYM, 2),
+                                               pack_col(RP_ISYM, 3)};
+        constexpr unsigned long long KDC[4] = {pack_col(RP_DCOL, 0), pack_col(RP_DCOL, 1), pack_col(RP_DCOL, 2),
+                                               pack_col(RP_DCOL, 3)};
+        constexpr unsigned long long KIC[4] = {pack_col(RP_ICOL, 0), pack_col(RP_ICOL, 1), pack_col(RP_ICOL, 2),
+                                               pack_col(RP_ICOL, 3)};
+        const int ds = tab_at(KDS[m], r), is = tab_at(KIS[m], r);
+        // unconditional loads (field 0 for the pad entries), zeroed by a select
+        const double dv = S.dnz[(size_t)(ds >= 0 ? ds : 0) * N + e];
+        const double sv = S.snz[(size_t)(ds >= 0 ? ds : 0) * N + e];
+        const double iv = S.iinv[(size_t)(is >= 0 ? is : 0) * N + e];
+        M0.d[m] = ds >= 0 ? dv : 0.0;
+        M0.s[m] = ds >= 0 ? sv : 0.0;
+        M0.ii[m] = is >= 0 ? iv : 0.0;
+        M0.dsrc[m] = gbase + tab_at(KDC[m], r);
+        M0.isrc[m] = gbase + tab_at(KIC[m], r);
     }
     const int seq = S.seq[e], motion = S.motion[e];
     double R2[9], R4[9], p0[3], p3[3];
@@ -337,11 +371,12 @@ __global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
     double k1[3], k2[3], tx, ty, tz;
     float pv[3];
     {
-        anchor(U, K_LINK[2 * j], R2, p0, R4, p3, k1);
-        anchor(U, K_LINK[2 * j + 1], R2, p0, R4, p3, k2);
+        const int kl1 = klink(2 * j), kl2 = klink(2 * j + 1);
+        anchor(U, kl1, R2, p0, R4, p3, k1);
+        anchor(U, kl2, R2, p0, R4, p3, k2);
         if (S.mb_q) { // multibody mode: the k-links sit at their prismatic joint positions
-            slide(U, K_LINK[2 * j], R2, R4, S.mb_q[(size_t)K_LINK[2 * j] * N + e], k1);
-            slide(U, K_LINK[2 * j + 1], R2, R4, S.mb_q[(size_t)K_LINK[2 * j + 1] * N + e], k2);
+            slide(U, kl1, R2, R4, S.mb_q[(size_t)kl1 * N + e], k1);
+            slide(U, kl2, R2, R4, S.mb_q[(size_t)kl2 * N + e], k2);
         }
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
