@@ -31,7 +31,8 @@ marked "FIX n" below:
 Other departures: stdout is not teed into a Logger and the reward curves are
 saved as .npz instead of plotted (reporting layer, out of scope); --save_dir
 replaces the hard-coded "AGENT_NNS/test_agent" prefix; --max_rounds bounds a
-run for tests.
+run for tests; --precision picks the TD7 MFMA operands (fp32 = the reference).
+The vectorised form of this schedule is exo_amd.rollout.RefScheduleTrainer.
 """
 import argparse
 import os
@@ -99,6 +100,8 @@ def parse_args(argv=None):
     p.add_argument("--save_dir", default="AGENT_NNS", help="checkpoint directory (reference: AGENT_NNS)")
     p.add_argument("--max_rounds", default=None, type=int, help="stop after this many episode rounds")
     p.add_argument("--buffer_size", default=None, type=int, help="LAP rows per env (reference: 2.5e5)")
+    p.add_argument("--precision", default="fp32", choices=["fp32", "bf16", "fp16"],
+                   help="TD7 MFMA operands (reference: fp32)")
     p.add_argument("--quiet", default=False, action="store_true")
     return p.parse_args(argv)
 
@@ -170,7 +173,7 @@ def train(args):
     E = len(envs)
     obs_dim, act_dim = envs[0].observation_space.shape[0], envs[0].action_space.shape[0]
     agent = Agent(state_dim=obs_dim, action_dim=act_dim, max_action=1, learning_steps=args.n_steps, env_num=E,
-                  buffer_size=args.buffer_size)
+                  buffer_size=args.buffer_size, precision=args.precision)
     max_lengths = [env.return_max_length() for env in envs]
     steps_per_round = sum(max_lengths)
     os.makedirs(args.save_dir, exist_ok=True)

@@ -619,12 +619,28 @@ __global__ void eval_metrics_kernel(Dev S, const float *__restrict__ info, const
 // [rows][n] table is copied to active -- one single-workgroup launch inside
 // the captured iteration, safe however many times a graph is replayed.
 __global__ __launch_bounds__(1024) void active_advance_kernel(const uint8_t *__restrict__ table, int rows, int n,
-                                                              long long *k, uint8_t *__restrict__ active) {
+                                                              long long *k, uint8_t *__restrict__ active,
+                                                              int32_t *count) {
+    __shared__ int wsum[16];
     const long long k0 = *k;
     const long long kk = k0 + 1 < rows ? k0 + 1 : rows - 1;
-    for (int e = threadIdx.x; e < n; e += blockDim.x) active[e] = table[(size_t)kk * n + e];
+    int c = 0;
+    for (int e = threadIdx.x; e < n; e += blockDim.x) {
+        const uint8_t v = table[(size_t)kk * n + e];
+        active[e] = v;
+        c += v != 0;
+    }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
     __syncthreads();
-    if (threadIdx.x == 0) *k = kk;
+    if (threadIdx.x == 0) {
+        *k = kk;
+        if (count) {
+            int t = 0;
+            for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += wsum[w];
+            *count = t;
+        }
+    }
 }
 
 struct exo_ctx {
@@ -1054,10 +1070,10 @@ int exo_tremor_metrics(exo_ctx *c, const float *info_dev, const uint8_t *stepped
 }
 
 int exo_active_advance(const uint8_t *table_dev, int32_t rows, int32_t n, int64_t *k_dev, uint8_t *active_dev,
-                       void *stream) {
+                       int32_t *count_dev, void *stream) {
     if (!table_dev || !k_dev || !active_dev || rows <= 0 || n <= 0) return EXO_EINVAL;
     hipLaunchKernelGGL(active_advance_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, table_dev, rows, n,
-                       (long long *)k_dev, active_dev);
+                       (long long *)k_dev, active_dev, count_dev);
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 

@@ -274,6 +274,104 @@ __global__ __launch_bounds__(UPD_THREADS) void lap_store_rank_kernel(float *tree
     }
 }
 
+// LAP.add with the reference's SHARED pointer (:49-63), called for every
+// active env of one vectorised step in env order -- what the training script's
+// per-env loop does (Exoskeleton_agent_train.py:139-142).  The c-th add writes
+// slot ptr0 + #{multiples of E in [count0, c)} of its stratum (the pointer
+// advances after an add whose count is a multiple of E = num_envs, :59-61), so
+// env 0's first transition sits one slot behind the others and, when envs are
+// done, two adds of one stratum can land in the same slot -- the later one
+// wins, as the reference's overwrite.  One workgroup: a block scan ranks the
+// active rows (rank_row[r] = row), every active row checks the next E-1 ranks
+// for a same-stratum, same-slot successor (two counts share a slot only if no
+// multiple of E lies between them), winners get slot_of / row_of, losers and
+// inactive rows -1.  ref = {ptr, count, size}; every stratum's size = size
+// (the reference samples every row against the one shared size, :76).
+__device__ __forceinline__ long long mult_below(long long x, int E) { return (x + E - 1) / E; }
+
+__global__ __launch_bounds__(UPD_THREADS) void lap_store_ref_slots_kernel(int capacity, int E, long long *ref,
+                                                                          int32_t *ring_size,
+                                                                          const int32_t *strata,
+                                                                          const uint8_t *active, int n,
+                                                                          int32_t *rank_row, int32_t *slot_of,
+                                                                          int32_t *row_of) {
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    __shared__ int wsum[UPD_THREADS / 64];
+    __shared__ int chunk_total;
+    const long long ptr0 = ref[0], count0 = ref[1], size0 = ref[2];
+    const long long m0 = mult_below(count0, E);
+    int offset = 0;
+    for (int base = 0; base < n; base += STORE_CHUNK) {
+        int f[4], cnt = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = base + 4 * t + k;
+            f[k] = (i < n && strata[i] >= 0 && strata[i] < E && (!active || active[i])) ? 1 : 0;
+            cnt += f[k];
+        }
+        int incl = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += v;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        if (t == 0) {
+            int acc = 0;
+            for (int k = 0; k < UPD_THREADS / 64; ++k) {
+                const int v = wsum[k];
+                wsum[k] = acc;
+                acc += v;
+            }
+            chunk_total = acc;
+        }
+        __syncthreads();
+        int rank = offset + wsum[wv] + incl - cnt;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = base + 4 * t + k;
+            if (i >= n) continue;
+            if (f[k]) {
+                rank_row[rank] = i;
+                row_of[i] = rank; // the rank, until the winner pass below
+                ++rank;
+            } else {
+                row_of[i] = -1;
+                slot_of[i] = -1;
+            }
+        }
+        offset += chunk_total;
+        __syncthreads();
+    }
+    __threadfence_block();
+    __syncthreads();
+    const int n_act = offset;
+    for (int i = t; i < n; i += blockDim.x) {
+        const int r = row_of[i];
+        if (r < 0) continue;
+        const long long mr = mult_below(count0 + r, E);
+        const int s = strata[i];
+        bool win = true;
+        for (int q = r + 1; q < min(r + E, n_act); ++q) {
+            if (mult_below(count0 + q, E) != mr) break; // slots only grow with the rank
+            if (strata[rank_row[q]] == s) win = false;
+        }
+        const int slot = (int)((ptr0 + (mr - m0)) % capacity);
+        slot_of[i] = win ? slot : -1;
+        row_of[i] = win ? s * (capacity + 1) + slot : -1;
+    }
+    __syncthreads();
+    const long long adv = mult_below(count0 + n_act, E) - m0;
+    const long long size = min(size0 + adv, (long long)capacity);
+    for (int s = t; s < E; s += blockDim.x) ring_size[s] = (int32_t)size;
+    if (t == 0) {
+        ref[0] = (ptr0 + adv) % capacity;
+        ref[1] = count0 + n_act;
+        ref[2] = size;
+    }
+}
+
 __global__ __launch_bounds__(256) void lap_store_copy_kernel(lap_storage_desc st, const float *state,
                                                              const float *action, const float *next_state,
                                                              const float *reward, const uint8_t *done,
@@ -453,6 +551,27 @@ int lap_store_batch(const lap_tree_desc *t, const lap_storage_desc *st, const fl
     if (hipGetLastError() != hipSuccess) return EXO_EDEVICE;
     hipLaunchKernelGGL(lap_store_copy_kernel, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, *st, state,
                        action, next_state, reward, done, action_scale, n, row_ws);
+    return rc(hipGetLastError());
+}
+
+int lap_store_batch_ref(const lap_tree_desc *t, const lap_storage_desc *st, int64_t *ref_dev, const float *state,
+                        const float *action, const float *next_state, const float *reward, const uint8_t *done,
+                        const int32_t *strata, const uint8_t *active, float action_scale, int32_t n,
+                        int32_t *ws_dev, void *stream) {
+    if (!valid(t) || !st || !st->state || !st->action || !st->next_state || !st->reward || !st->not_done ||
+        !st->size || st->state_dim <= 0 || st->action_dim <= 0 || !ref_dev || !state || !action || !next_state ||
+        !reward || !done || !strata || !ws_dev || n < 0 || action_scale == 0.0f)
+        return EXO_EINVAL;
+    if (n == 0) return EXO_OK;
+    int32_t *rank_row = ws_dev, *slot_of = ws_dev + n, *row_of = ws_dev + 2 * n;
+    hipLaunchKernelGGL(lap_store_ref_slots_kernel, dim3(1), dim3(UPD_THREADS), 0, (hipStream_t)stream, t->capacity,
+                       t->n_strata, (long long *)ref_dev, st->size, strata, active, n, rank_row, slot_of, row_of);
+    if (hipGetLastError() != hipSuccess) return EXO_EDEVICE;
+    hipLaunchKernelGGL(lap_add_kernel, dim3(t->n_strata), dim3(UPD_THREADS), 0, (hipStream_t)stream, t->tree,
+                       t->max_priority, t->cap, levels_of(t), t->capacity, strata, slot_of, n);
+    if (hipGetLastError() != hipSuccess) return EXO_EDEVICE;
+    hipLaunchKernelGGL(lap_store_copy_kernel, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, *st, state,
+                       action, next_state, reward, done, action_scale, n, row_of);
     return rc(hipGetLastError());
 }
 

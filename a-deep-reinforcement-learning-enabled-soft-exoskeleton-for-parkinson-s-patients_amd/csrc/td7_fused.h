@@ -739,6 +739,7 @@ struct Noise {
     float *sigma;
     float sigma_dec, clip, scale;
     const float *z;  // given standard normals (null: Philox)
+    const int32_t *dec_count;  // non-null: sigma -= sigma_dec * *dec_count (active envs of the step)
 };
 
 // ---------------------------------------------------------------- stamps
@@ -847,7 +848,7 @@ __device__ __forceinline__ void noise_rows(char *lds, R32 a, int A, int rows, in
     if (threadIdx.x == 0) {
         __threadfence();
         if (atomicAdd(nz.ticket, 1u) == gridDim.x * gridDim.y - 1) {
-            *nz.sigma = sg - nz.sigma_dec;
+            *nz.sigma = sg - (nz.dec_count ? nz.sigma_dec * (float)*nz.dec_count : nz.sigma_dec);
             if (!nz.z) *nz.counter = call + 1ull;
             *nz.ticket = 0u;
         }
@@ -879,7 +880,7 @@ inline Lin lin_of(const td7f_lin &l) {
     return Lin{(const u32x4 *)l.wf, (const u32x4 *)l.wb, l.b, l.n_out, l.n_in, l.ksf, l.ksb, l.w, (long)l.ldw};
 }
 inline Noise noise_of(const td7f_noise &n) {
-    return Noise{n.seed, n.tag, n.counter, n.ticket, n.sigma, n.sigma_dec, n.clip, n.scale, n.z};
+    return Noise{n.seed, n.tag, n.counter, n.ticket, n.sigma, n.sigma_dec, n.clip, n.scale, n.z, n.dec_count};
 }
 
 // tiles per wave of the MFMA layers: every layer wider than 16 outputs must be

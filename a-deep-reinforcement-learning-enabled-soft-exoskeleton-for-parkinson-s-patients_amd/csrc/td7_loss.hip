@@ -105,7 +105,7 @@ __global__ __launch_bounds__(T) void noisy_action_kernel(const float *a, const f
 __global__ __launch_bounds__(T) void noisy_action_rng_kernel(const float *a, uint64_t seed, uint32_t tag,
                                                              unsigned long long *counter, uint32_t *ticket,
                                                              float *sigma, float sigma_dec, float clip, float scale,
-                                                             float *out, int n) {
+                                                             float *out, int n, const int32_t *dec_count) {
     const float sg = *sigma;
     const unsigned long long call = *counter;
     for (int j = blockIdx.x * T + threadIdx.x; 2 * j < n; j += gridDim.x * T) {
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(T) void noisy_action_rng_kernel(const float *a, uin
     if (threadIdx.x == 0) {
         __threadfence();
         if (atomicAdd(ticket, 1u) == gridDim.x - 1) {
-            *sigma = sg - sigma_dec;
+            *sigma = sg - (dec_count ? sigma_dec * (float)*dec_count : sigma_dec);
             *counter = call + 1ull;
             *ticket = 0u;
         }
@@ -225,11 +225,11 @@ int td7_noisy_action(const float *a, const float *noise, float *sigma, float sig
 
 int td7_noisy_action_rng(const float *a, uint64_t seed, uint32_t tag, unsigned long long *counter,
                          uint32_t *ticket, float *sigma, float sigma_dec, float clip, float scale, float *out,
-                         int32_t n, void *stream) {
+                         int32_t n, const int32_t *dec_count, void *stream) {
     if (!a || !counter || !ticket || !sigma || !out || n < 0) return EXO_EINVAL;
     const int blocks = std::max(1, std::min(256, (n / 2 + T - 1) / T));
     hipLaunchKernelGGL(noisy_action_rng_kernel, dim3(blocks), dim3(T), 0, (hipStream_t)stream, a, seed, tag, counter,
-                       ticket, sigma, sigma_dec, clip, scale, out, n);
+                       ticket, sigma, sigma_dec, clip, scale, out, n, dec_count);
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 

@@ -68,7 +68,8 @@ class TD7FNoise(ctypes.Structure):
     """td7f_noise (include/exo_amd.h)."""
     _fields_ = [("seed", c_uint64), ("tag", ctypes.c_uint32), ("pad0", ctypes.c_uint32), ("counter", c_void_p),
                 ("ticket", c_void_p), ("sigma", c_void_p), ("sigma_dec", ctypes.c_float), ("clip", ctypes.c_float),
-                ("scale", ctypes.c_float), ("pad1", c_int32), ("z", c_void_p)]
+                ("scale", ctypes.c_float), ("pad1", c_int32), ("z", c_void_p),
+                ("dec_count", c_void_p)]
 
 
 class TD7FXT(ctypes.Structure):
@@ -120,7 +121,7 @@ EXPORTS = {
     "exo_destroy": (None, [c_void_p]),
     "exo_tremor_metrics": (c_int32, [c_void_p, c_void_p, c_void_p, c_double, c_double, c_double, c_int32, c_void_p,
                                      c_void_p, c_void_p]),
-    "exo_active_advance": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
+    "exo_active_advance": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "exo_eval_metrics": (c_int32, [c_void_p, c_void_p, c_void_p, c_double, c_double, c_void_p, c_void_p]),
     "lap_tree_floats": (c_int32, [c_int32, c_int32]),
     "lap_init": (c_int32, [c_void_p, c_void_p]),
@@ -131,6 +132,8 @@ EXPORTS = {
     "lap_totals": (c_int32, [c_void_p, c_void_p, c_void_p]),
     "lap_store_batch": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_void_p, ctypes.c_float, c_int32, c_void_p, c_void_p]),
+    "lap_store_batch_ref": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_void_p, c_void_p, ctypes.c_float, c_int32, c_void_p, c_void_p]),
     "lap_sample_gather_rng": (c_int32, [c_void_p, c_void_p, ctypes.c_uint64, ctypes.c_uint32, c_void_p, c_void_p,
                                         c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_void_p]),
@@ -175,7 +178,8 @@ EXPORTS = {
                                          c_void_p, c_void_p, c_long, c_long, c_int32, c_int32, c_int32, c_int32,
                                          ctypes.c_float, c_void_p]),
     "td7_noisy_action_rng": (c_int32, [c_void_p, ctypes.c_uint64, ctypes.c_uint32, c_void_p, c_void_p, c_void_p,
-                                       ctypes.c_float, ctypes.c_float, ctypes.c_float, c_void_p, c_int32, c_void_p]),
+                                       ctypes.c_float, ctypes.c_float, ctypes.c_float, c_void_p, c_int32, c_void_p,
+                                       c_void_p]),
     "td7_dense_bwd_weight": (c_int32, [c_void_p, c_long, c_long, c_void_p, c_long, c_long, c_void_p, c_long,
                                        c_long, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32,
                                        c_void_p]),

@@ -116,8 +116,11 @@ def critic_layers(critic):
 
 def supported(learner):
     """The fused path applies: GPU, bf16/fp16 operands, the reference's
-    activations, every hidden width 49..320 (packed tiles per wave 4 or 5),
-    critic / actor / encoder of the reference shapes."""
+    activations, and every hidden width (zs_dim, enc_hdim, critic_hdim,
+    actor_hdim) a multiple of 4 in 241..320 -- 16-wide tiles per wave of 4 or 5
+    (NW = 4 waves), all widths in the same tile class.  Anything else (the
+    wide configuration, fp32 operands, widths below 241) runs the per-layer
+    kernels."""
     hp = learner.hp
     if learner.device.type != "cuda" or learner.precision not in PREC:
         return False
@@ -225,22 +228,29 @@ class FusedNets:
             self.nets[n].refresh()
 
     # ------------------------------------------------------------- noise
-    def _noise(self, rng, sigma, dec, clip, scale, z=None):
+    def _noise(self, rng, sigma, dec, clip, scale, z=None, dec_count=None):
         return TD7FNoise(rng.seed, rng.tag, 0, rng.counter_ptr, rng.ticket_ptr, sigma.data_ptr(), float(dec),
-                         float(clip), float(scale), 0, z.data_ptr() if z is not None else None)
+                         float(clip), float(scale), 0, z.data_ptr() if z is not None else None,
+                         dec_count.data_ptr() if dec_count is not None else None)
 
     # ------------------------------------------------------------- passes
     @torch.no_grad()
-    def select(self, obs, scale=1.0):
+    def select(self, obs, scale=1.0, dec_count=None):
         """select_action_batch with Gaussian exploration (one launch): actor(obs,
         fixed_encoder.zs(obs)) + N(0, exploration_noise) per element, clamped,
-        times max_action; exploration_noise decreases once per env."""
+        times max_action; exploration_noise decreases once per env (dec_count:
+        an int32 device scalar -- once per env counted there, the active envs
+        of a vectorised step)."""
         L = self.L
         self.refresh("fixed_encoder", "actor")
         obs = obs.contiguous()
         n = obs.shape[0]
         out = torch.empty((n, L.actor.l3.out_features), dtype=torch.float32, device=obs.device)
-        nz = self._noise(L._explore_rng, L.exploration_noise_t, L.action_noise_decrease * n, 0.0, scale)
+        if dec_count is not None:
+            nz = self._noise(L._explore_rng, L.exploration_noise_t, L.action_noise_decrease, 0.0, scale,
+                             dec_count=dec_count)
+        else:
+            nz = self._noise(L._explore_rng, L.exploration_noise_t, L.action_noise_decrease * n, 0.0, scale)
         fe, ac = self.nets["fixed_encoder"].layers, self.nets["actor"].layers
         nat.check(nat.lib().td7f_select(self.prec, self.act, _lin_array(fe[:3]), self.nets["actor"].array,
                                         nat.ptr(obs), n, ctypes.byref(nz), nat.ptr(out), nat.stream_ptr(obs.device)),

@@ -575,12 +575,13 @@ class DeviceRNG:
         return self.state.data_ptr() + 8
 
 
-def noisy_action(a, noise, sigma, sigma_dec, clip=0.0, scale=1.0, rng=None):
+def noisy_action(a, noise, sigma, sigma_dec, clip=0.0, scale=1.0, rng=None, dec_count=None):
     """clamp(a + c(noise * sigma), -1, 1) * scale with c = clamp(+-clip) when
     clip > 0, then sigma -= sigma_dec in place (sigma: device scalar tensor).
     One td7_noisy_action launch on a GPU; the reference expressions on a CPU.
     noise=None: standard normal noise -- drawn inside the kernel from `rng`
-    (a DeviceRNG) on a GPU, torch.randn_like on a CPU."""
+    (a DeviceRNG) on a GPU, torch.randn_like on a CPU.  dec_count (int32
+    device scalar, GPU with rng): sigma -= sigma_dec * dec_count instead."""
     if noise is None and a.is_cuda:
         if rng is None:
             raise ValueError("noisy_action: noise=None needs a DeviceRNG on the GPU")
@@ -589,7 +590,7 @@ def noisy_action(a, noise, sigma, sigma_dec, clip=0.0, scale=1.0, rng=None):
         nat.check(nat.lib().td7_noisy_action_rng(nat.ptr(a), rng.seed, rng.tag, rng.counter_ptr, rng.ticket_ptr,
                                                  nat.ptr(sigma),
                                                  float(sigma_dec), float(clip), float(scale), nat.ptr(out), a.numel(),
-                                                 nat.stream_ptr(a.device)), "td7_noisy_action_rng")
+                                                 nat.ptr(dec_count), nat.stream_ptr(a.device)), "td7_noisy_action_rng")
         return out
     if noise is None:
         noise = torch.randn_like(a)

@@ -12,7 +12,12 @@ Two insert paths:
                     (ptr advances when count % num_envs == 0 BEFORE count is
                     incremented, :59-63);
 * add_batch(...) -- one vectorised env step: a ring per stratum, one slot per
-                    active env-step (documented divergence).
+                    active env-step (SURVEY.md A.6: documented divergence);
+* add_batch_ref(...) -- one vectorised env step as the training script's
+                    per-env add loop (Exoskeleton_agent_train.py:139-142): the
+                    reference's shared pointer, kept on the device
+                    (lap_store_batch_ref), so a vectorised run fills the buffer
+                    slot for slot like the script's sequential adds.
 """
 import ctypes
 import os
@@ -60,6 +65,9 @@ class LAP:
         self.size_s = torch.zeros((E,), **i32)
         self._row0 = (torch.arange(E, device=self.device, dtype=torch.int64) * (C + 1))
         self.ind = None
+        # reference pointer of add_batch_ref: int64 {ptr, count, size} on the device
+        self.ref_state = torch.zeros((3,), dtype=torch.int64, device=self.device)
+        self._ref_ws = None
         self._u = torch.empty((E, self.batch_size), **f32)
         # sample() draws its uniforms in the kernel (EXO_DEVICE_RNG=0: torch.rand + lap_sample_gather)
         from .ops import DeviceRNG
@@ -146,6 +154,42 @@ class LAP:
                                             nat.ptr(act), float(self.normalize_actions), n, nat.ptr(self._row_ws),
                                             self._stream()), "lap_store_batch")
 
+    def add_batch_ref(self, state, action, next_state, reward, done, strata, active=None):
+        """LAP.add (:49-63) for every active row in row order -- the training
+        script's per-env loop over one vectorised step -- with the reference's
+        shared pointer (ref_state, device-resident): env 0's first transition
+        one slot behind the others, a done env's slot re-used by the next adds,
+        one shared sampling size.  Three kernels, no host synchronisation
+        (lap_store_batch_ref)."""
+        n = state.shape[0]
+        if self._ref_ws is None or self._ref_ws.numel() < 3 * n:
+            self._ref_ws = torch.empty((3 * n,), dtype=torch.int32, device=self.device)
+
+        def f32(t, shape):
+            t = t.to(device=self.device, dtype=torch.float32).reshape(shape)
+            return t if t.is_contiguous() else t.contiguous()
+
+        st = f32(state, (n, self.state_dim))
+        nx = f32(next_state, (n, self.state_dim))
+        ac = f32(action, (n, self.action_dim))
+        rw = f32(reward, (n,))
+        dn = done if done.dtype == torch.uint8 else (done.view(torch.uint8) if done.dtype == torch.bool
+                                                     else done.to(torch.uint8))
+        dn = dn.reshape(n).contiguous()
+        sr = (strata if strata.dtype == torch.int32 else strata.to(torch.int32)).contiguous()
+        act = None
+        if active is not None:
+            act = (active.view(torch.uint8) if active.dtype == torch.bool else active.to(torch.uint8)).contiguous()
+        nat.check(nat.lib().lap_store_batch_ref(ctypes.byref(self._desc), ctypes.byref(self._store),
+                                                nat.ptr(self.ref_state), nat.ptr(st), nat.ptr(ac), nat.ptr(nx),
+                                                nat.ptr(rw), nat.ptr(dn), nat.ptr(sr), nat.ptr(act),
+                                                float(self.normalize_actions), n, nat.ptr(self._ref_ws),
+                                                self._stream()), "lap_store_batch_ref")
+
+    def ref_pointer(self):
+        """(ptr, count, size) of add_batch_ref (host sync)."""
+        return tuple(int(v) for v in self.ref_state.cpu())
+
     # ------------------------------------------------------------- sample
     def _slot(self, slot):
         """Batch buffers of sample(slot=...): the vectorised trainer samples the
@@ -210,4 +254,5 @@ class LAP:
             t.zero_()
         self.ptr_s.zero_()
         self.size_s.zero_()
+        self.ref_state.zero_()
         self._init_tree()

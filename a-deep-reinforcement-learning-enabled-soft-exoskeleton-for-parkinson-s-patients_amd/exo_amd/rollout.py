@@ -133,7 +133,8 @@ class ForkJoinAudit:
 
 
 class VecTrainer:
-    def __init__(self, env, agent, strata=None, use_graphs=True, warmup_eager=3, exploration="gaussian"):
+    def __init__(self, env, agent, strata=None, use_graphs=True, warmup_eager=3, exploration="gaussian",
+                 shared_step=True):
         self.env, self.agent = env, agent
         self.device = env.device
         self.n = env.n
@@ -162,6 +163,9 @@ class VecTrainer:
         # the counter saturates), so no host copy runs between graph replays
         self._table_ext = torch.cat([self.active_table, torch.zeros_like(self.active_table[:1])]).contiguous()
         self.active = self.active_table[0].clone()
+        # envs running at this step = the script's select_action calls (:125-128),
+        # written by exo_active_advance with the next step's mask
+        self.active_count = torch.full((1,), int(self.active_counts[0]), dtype=torch.int32, device=self.device)
         self.k = 0
         self.use_graphs = use_graphs
         self.warmup_eager = warmup_eager
@@ -173,7 +177,7 @@ class VecTrainer:
         # CUs (512-thread workgroups) unless the caller chose a kernel variant.
         # Only where 'auto' runs the row-parallel kernel (N <= 16,384): above it
         # the two-lane kernel is the fast one (65,536 envs: 106 vs 291 us)
-        if (getattr(env, "step_variant", None) == "auto" and env.n <= 16384
+        if (shared_step and getattr(env, "step_variant", None) == "auto" and env.n <= 16384
                 and os.environ.get("EXO_TRAIN_STEP_SHARED", "1") == "1"):
             env.set_step_variant("rows_shared")
         self.last_actions = None
@@ -192,13 +196,25 @@ class VecTrainer:
     def _rollout(self):
         ag = self.agent
         obs = self.obs
-        act = ag.select_action_batch(obs, timestep=self.k_dev if self.exploration == "pink" else None)
+        act = ag.select_action_batch(obs, timestep=self.k_dev if self.exploration == "pink" else None,
+                                     dec_count=self.active_count)
         nobs, rew, done, info = self.env.step(act, active=self.active, out=self._outs[self._cur])
         ag.replay_buffer.add_batch(obs, act, nobs, rew, done, self.strata, self.active)
-        nat.check(nat.lib().exo_active_advance(nat.ptr(self._table_ext), self._table_ext.shape[0], self.n,
-                                               nat.ptr(self.k_dev), nat.ptr(self.active), nat.stream_ptr(self.device)),
-                  "exo_active_advance")
+        self._advance()
         self.last_actions = act
+
+    def _advance(self):
+        """The next step's active mask and count on the device (exo_active_advance)."""
+        nat.check(nat.lib().exo_active_advance(nat.ptr(self._table_ext), self._table_ext.shape[0], self.n,
+                                               nat.ptr(self.k_dev), nat.ptr(self.active), nat.ptr(self.active_count),
+                                               nat.stream_ptr(self.device)), "exo_active_advance")
+
+    def _round_start(self):
+        """Device step counter, active mask and count back to the first step of a round."""
+        self.k = 0
+        self.k_dev.zero_()
+        self.active.copy_(self.active_table[0])
+        self.active_count.fill_(int(self.active_counts[0]))
 
     @property
     def obs(self):
@@ -233,12 +249,17 @@ class VecTrainer:
     def _prefetching(self):
         return self.prefetch_sample and self.overlap_rollout
 
-    def _pre(self):
+    def _pre(self, rollout=True):
         ag = self.agent
         # one GPU: the encoder's gradients and step stay on its branch, joined
         # at the end of the iteration (_join_prio)
         ag.learner.defer_side_join = ENC_STEP_BRANCH and not self.dp
         rb = ag.replay_buffer
+        if not rollout:  # a training step alone (Agent.train): sample, then the gradients
+            self._batch = rb.sample()
+            self._ind = rb.ind
+            self._prio = ag.learner.phase_grads(*self._batch)
+            return
         slot = self._cur if self._prefetching() else None
         if self.iters == 0 or not self.overlap_rollout:
             self._rollout()
@@ -269,9 +290,10 @@ class VecTrainer:
     # all-reduce of max_priority follows it).  EXO_PRIO_BRANCH=0 serialises.
     prio_branch = os.environ.get("EXO_PRIO_BRANCH", "1") == "1"
 
-    def _mid(self, update_actor, flat_grad=None, grad_scale=1.0):
+    def _mid(self, update_actor, flat_grad=None, grad_scale=1.0, rollout=True):
         ag = self.agent
         self._pside = None
+        self._mid_rollout = rollout
         if self.prio_branch and not self.dp:
             cur = torch.cuda.current_stream(self.device)
             if getattr(self, "_prio_stream", None) is None:
@@ -290,32 +312,40 @@ class VecTrainer:
             ag.learner.phase_actor_grads(self._batch[0], self._batch[1])
 
     def _sample_next(self):
-        if self._prefetching():
+        if self._prefetching() and self._mid_rollout:
             self.agent.replay_buffer.sample(1 - self._cur)
 
     def _join_prio(self):
         if getattr(self, "_pside", None) is not None:
             torch.cuda.current_stream(self.device).wait_stream(self._pside)
             self._pside = None
-        self.agent.learner.join_side()  # the encoder branch's optimiser step
+        L = self.agent.learner
+        L.join_side()  # the encoder branch's optimiser step
+        # the deferred-join mode belongs to this iteration only: an update()
+        # called later (Agent.train) must not leave work on the branch
+        L.defer_side_join = False
 
     def _post(self, update_actor, flat_grad=None, grad_scale=1.0):
         if update_actor:
             self.agent.learner.phase_actor_step(flat_grad, grad_scale)
 
-    def _eager(self, update_actor):
+    def _eager(self, update_actor, rollout=True):
         L = self.agent.learner
-        self._pre()
+        self._pre(rollout)
         L.sync.allreduce_grads(L.grad_params())
-        self._mid(update_actor)
+        self._mid(update_actor, rollout=rollout)
         self.agent.sync.max_(self.agent.replay_buffer._maxp)
         if update_actor:
             L.sync.allreduce_grads(L.grad_params(actor=True))
         self._post(update_actor)
         self._join_prio()
 
-    def _capture(self, update_actor):
-        """Capture this parity's iteration; the capture itself performs one real iteration."""
+    def _key(self, update_actor, rollout):
+        return (update_actor, self._cur) if rollout else ("train", update_actor)
+
+    def _capture(self, update_actor, rollout=True):
+        """Capture this parity's iteration (rollout=False: a training step
+        alone); the capture itself performs one real iteration."""
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         pool = None  # one private pool per parity: the two parities replay in alternation
@@ -324,8 +354,8 @@ class VecTrainer:
             if not self.dp:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=pool, stream=s), ForkJoinAudit(s):
-                    self._pre()
-                    self._mid(update_actor)
+                    self._pre(rollout)
+                    self._mid(update_actor, rollout=rollout)
                     self._post(update_actor)
                     self._join_prio()
                 parts = [g]
@@ -336,13 +366,13 @@ class VecTrainer:
                 L, S = self.agent.learner, self.agent.sync
                 g1, g2, g3 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g1, pool=pool, stream=s), ForkJoinAudit(s):
-                    self._pre()
+                    self._pre(rollout)
                     flat_c = S.pack(L.grad_params())
                 pool = g1.pool()
                 flat_a = None
                 scale = 1.0 / S.world
                 with torch.cuda.graph(g2, pool=pool, stream=s), ForkJoinAudit(s):
-                    self._mid(update_actor, flat_c, scale)   # the optimisers read the reduced bucket in place
+                    self._mid(update_actor, flat_c, scale, rollout)  # the optimisers read the reduced bucket in place
                     if update_actor:
                         flat_a = S.pack(L.grad_params(actor=True))
                 if update_actor:  # no actor step at this parity: nothing to capture
@@ -352,12 +382,12 @@ class VecTrainer:
                     g3 = None
                 parts = [g1, g2, g3, flat_c, flat_a]
         torch.cuda.current_stream(self.device).wait_stream(s)
-        self.graphs[(update_actor, self._cur)] = parts
+        self.graphs[self._key(update_actor, rollout)] = parts
         # capture records but does not execute: run the iteration now
-        self._replay(update_actor)
+        self._replay(update_actor, rollout)
 
-    def _replay(self, update_actor):
-        parts = self.graphs[(update_actor, self._cur)]
+    def _replay(self, update_actor, rollout=True):
+        parts = self.graphs[self._key(update_actor, rollout)]
         if not self.dp:
             parts[0].replay()
             return
@@ -378,9 +408,7 @@ class VecTrainer:
         L = ag.learner
         if self.k == self.round_len:
             self.env.reset(obs_out=self.obs)
-            self.k = 0
-            self.k_dev.zero_()
-            self.active.copy_(self.active_table[0])
+            self._round_start()
             self.resets += 1
             if self.exploration == "pink":
                 ag.init_episode_noise_device(self.round_len)
@@ -401,3 +429,157 @@ class VecTrainer:
         self.iters += 1
         self._cur ^= 1  # the next observation is in the other buffer
         return n_active
+
+
+class RefScheduleTrainer(VecTrainer):
+    """The reference training script's schedule on N device envs
+    (Simulation/Exoskeleton_agent_train.py:110-211), where VecTrainer trains one
+    step per vectorised env step:
+
+    * per episode round every env resets (:111-113) and the score starts at
+      the reset's second value (counts = 2); the envs step synchronously until
+      the longest motion ends (:123), done envs idle (:126, :140);
+    * actions are uniform in [-1, 1) until the warm-up has passed, then
+      select_action with Gaussian exploration (:125-131) -- noise scale
+      decremented once per running env (:207);
+    * every running env's transition goes to the replay in env order with the
+      reference's shared pointer (LAP.add_batch_ref; ref_replay=False: the
+      per-stratum rings of add_batch) -- no training during the rollout;
+    * after the round, agent.maybe_train_and_checkpoint(round(mean(ep_len)),
+      mean(score)) (:208): its train_and_reset runs that many TD7 steps as a
+      burst, each a HIP-graph replay of Agent.train (sample, update, priority
+      update, target refresh every 250 steps), and refreshes the policy
+      checkpoint by the reference's rule (TD7_multi_agent.py:296-325);
+    * the warm-up switch after the round (:210-211): steps_count counts active
+      env-steps over all data-parallel ranks.
+
+    One rollout step = select / uniform actions -> exo_step -> score -> replay
+    insert -> next active mask, replayed from a captured graph per (random,
+    observation buffer).  Parity hooks (eager rollout):
+    action_source(trainer, random) -> [N, 7] actions of this step on the host
+    (rows of idle envs ignored) instead of the device draws / batched
+    select_action -- e.g. the script's own per-env np.random.uniform and
+    select_action calls; reset_source(round, obs_out) resets every env (e.g.
+    from injected draw streams) instead of exo_reset."""
+
+    def __init__(self, env, agent, warmup=25_000, strata=None, use_graphs=True, ref_replay=True,
+                 action_source=None, reset_source=None, warmup_eager=2):
+        super().__init__(env, agent, strata=strata, use_graphs=use_graphs, warmup_eager=warmup_eager,
+                         shared_step=False)
+        # the rollout runs alone (no TD7 pass beside it): the env step's own fast shape
+        if getattr(env, "step_variant", None) == "rows_shared":
+            env.set_step_variant("auto")
+        self.warmup = int(warmup)
+        self.ref_replay = ref_replay
+        self.action_source, self.reset_source = action_source, reset_source
+        self.world = agent.sync.world
+        self.steps_count = 0      # :146, over every rank's envs
+        self.allow_train = False  # :87, :210-211
+        self.rounds = 0
+        self.updates = 0
+        dev = self.device
+        self.score = torch.zeros(self.n, dtype=torch.float64, device=dev)
+        self._rand_act = torch.zeros((self.n, 7), dtype=torch.float32, device=dev)
+        Ls = env.lengths_host
+        self.ep_len = Ls - 2  # starts at 1 (:115), +1 per step (:145) for L-3 steps
+        self.round_env_steps = int((Ls - 3).sum())
+        self.active_host = np.stack([Ls - 3 > k for k in range(self.round_len)])
+        self._train_iters = 0
+        self._roll_iters = 0
+        self.trace = []
+
+    # ------------------------------------------------------------ rollout
+    def _rollout_ref(self, random, injected=False):
+        ag = self.agent
+        obs = self.obs
+        if injected:
+            act = self._rand_act
+        elif random:
+            act = self._rand_act.uniform_(-1.0, 1.0)
+        else:
+            act = ag.select_action_batch(obs, dec_count=self.active_count)
+        nobs, rew, done, info = self.env.step(act, active=self.active, out=self._outs[self._cur])
+        self.score.add_(torch.where(self.active, rew.double(), 0.0))  # :144
+        add = ag.replay_buffer.add_batch_ref if self.ref_replay else ag.replay_buffer.add_batch
+        add(obs, act, nobs, rew, done, self.strata, self.active)  # :142
+        self._advance()
+        self.last_actions = act
+
+    def _roll_step(self, random):
+        if self.action_source is not None:
+            a = np.asarray(self.action_source(self, random), dtype=np.float32).reshape(self.n, -1)
+            self._rand_act.copy_(torch.as_tensor(a, device=self.device))
+            self._rollout_ref(random, injected=True)
+        elif not self.use_graphs or self._roll_iters < self.warmup_eager:
+            self._rollout_ref(random)
+        else:
+            key = ("roll", bool(random), self._cur)
+            g = self.graphs.get(key)
+            if g is None:
+                s = torch.cuda.Stream(device=self.device)
+                s.wait_stream(torch.cuda.current_stream(self.device))
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.stream(s):
+                    with torch.cuda.graph(g, stream=s), ForkJoinAudit(s):
+                        self._rollout_ref(random)
+                torch.cuda.current_stream(self.device).wait_stream(s)
+                self.graphs[key] = g
+            g.replay()
+        self._roll_iters += 1
+        self.k += 1
+        self._cur ^= 1
+
+    # ----------------------------------------------------------- training
+    def train_step(self):
+        """One Agent.train() (TD7_multi_agent.py:211-293 with the LAP sample and
+        priority update, TD7_buffer_multi_agent.py:65-117) as a graph replay."""
+        ag, L = self.agent, self.agent.learner
+        L.training_steps += 1
+        update_actor = L.training_steps % ag.hp.policy_freq == 0
+        L.prefetch_actor = update_actor
+        # both policy-update parities run eagerly once before their capture
+        if not self.use_graphs or self._train_iters < max(2, self.warmup_eager):
+            self._eager(update_actor, rollout=False)
+        elif self._key(update_actor, False) not in self.graphs:
+            self._capture(update_actor, rollout=False)
+        else:
+            self._replay(update_actor, rollout=False)
+        L.prefetch_actor = False
+        if L.maybe_update_targets():
+            ag.replay_buffer.reset_max_priority()
+            ag.sync.max_(ag.replay_buffer._maxp)
+        self._train_iters += 1
+
+    # -------------------------------------------------------------- round
+    def run_round(self):
+        """One episode round (:111-211); returns (active env-steps of this
+        rank, training steps of the burst)."""
+        ag, L = self.agent, self.agent.learner
+        if self.reset_source is not None:
+            self.reset_source(self.rounds, self.obs)
+        else:
+            self.env.reset(obs_out=self.obs)
+        self.score.fill_(2.0)  # reset() returns (obs, counts = 2) into score[i] (:112)
+        self._round_start()
+        random = not self.allow_train
+        for _ in range(self.round_len):
+            self._roll_step(random)
+        self.resets += 1
+        # :208 -- the host sees one value per round: the mean episode return
+        ep_return = float(np.mean(self.score.cpu().numpy()))
+        ep_timesteps = round(np.mean(self.ep_len))
+        before, refreshed = L.training_steps, ag.checkpoint_refreshes
+        ag.maybe_train_and_checkpoint(ep_timesteps, ep_return, train=self.train_step)
+        burst = L.training_steps - before
+        self.updates += burst
+        self.steps_count += self.round_env_steps * self.world
+        if self.steps_count > self.warmup:  # :210-211
+            self.allow_train = True
+        self.rounds += 1
+        self.trace.append(dict(round=self.rounds, random_actions=random, ep_return=ep_return,
+                               ep_timesteps=ep_timesteps, training_steps=L.training_steps,
+                               eps_since_update=ag.eps_since_update, best_min_return=ag.best_min_return,
+                               min_return=ag.min_return, max_eps_before_update=ag.max_eps_before_update,
+                               checkpoint_refreshed=ag.checkpoint_refreshes > refreshed,
+                               steps_count=self.steps_count))
+        return self.round_env_steps, burst

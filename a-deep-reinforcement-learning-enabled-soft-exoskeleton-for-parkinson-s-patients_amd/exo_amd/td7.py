@@ -917,6 +917,12 @@ class TD7Learner:
         self.training_steps += 1
         if update_actor is None:
             update_actor = self.training_steps % self.hp.policy_freq == 0
+        # an eager update is self-contained: every branch it forks is joined
+        # before it returns and an actor forward is prefetched only for an
+        # update that consumes it (the graph-replayed trainers set both flags
+        # per iteration and join themselves)
+        self.defer_side_join = False
+        self.prefetch_actor = bool(update_actor)
         priority = self.phase_grads(state, action, next_state, reward, not_done, noise)
         self.sync.allreduce_grads(self.grad_params())
         self.phase_steps()
@@ -924,6 +930,8 @@ class TD7Learner:
             self.phase_actor_grads(state, action)
             self.sync.allreduce_grads(self.grad_params(actor=True))
             self.phase_actor_step()
+        self.prefetch_actor = False
+        self.join_side()
         return priority
 
     def sync_bounds(self):
@@ -993,6 +1001,7 @@ class Agent:
         self.max_eps_before_update = 1
         self.min_return = 1e8
         self.best_min_return = -1e8
+        self.checkpoint_refreshes = 0  # policy checkpoints taken (:307-310), for traces
 
     # the reference exposes the nets and counters on the agent itself
     def __getattr__(self, name):
@@ -1060,17 +1069,20 @@ class Agent:
         return self.noise_dev
 
     @torch.no_grad()
-    def select_action_batch(self, obs, use_checkpoint=False, use_exploration=True, timestep=None):
+    def select_action_batch(self, obs, use_checkpoint=False, use_exploration=True, timestep=None, dec_count=None):
         """Device-resident batched actions for the vectorised loop (no host sync).
         timestep (int64 device tensor [1]): Pink-noise exploration -- column
         `timestep` of the episode's noise (init_episode_noise_device) is added
         to every env's action, as the reference's batched Pink select_action
         does (:218-226), and exploration_noise decreases once per call (:225);
         otherwise Gaussian noise per env (TD7_multi_agent.py:205-207), one
-        decrement per env (the training script's per-env calls)."""
+        decrement per env (the training script's per-env calls) -- dec_count
+        (int32 device scalar): one per env counted there, the envs still
+        running at this step of a synchronous round (the script calls
+        select_action only for envs that are not done, :125-128)."""
         fz = self.learner.fused
         if fz is not None and use_exploration and timestep is None and not use_checkpoint and obs.is_cuda:
-            return fz.select(obs, scale=self.max_action)  # zs, actor and the noise in one launch
+            return fz.select(obs, scale=self.max_action, dec_count=dec_count)  # zs, actor and the noise in one launch
         a = self.learner.act(obs, use_checkpoint)
         if use_exploration and timestep is not None:
             col = self.noise_dev.index_select(1, timestep).t()           # [1, action_dim]
@@ -1079,6 +1091,9 @@ class Agent:
         if use_exploration:
             L = self.learner
             noise = None if (a.is_cuda and L._device_rng) else torch.randn_like(a)
+            if noise is None and dec_count is not None:
+                return ops.noisy_action(a, None, L.exploration_noise_t, L.action_noise_decrease,
+                                        scale=self.max_action, rng=L._explore_rng, dec_count=dec_count)
             return ops.noisy_action(a, noise, L.exploration_noise_t, L.action_noise_decrease * a.shape[0],
                                     scale=self.max_action, rng=L._explore_rng)
         return a.clamp(-1, 1) * self.max_action
@@ -1093,8 +1108,10 @@ class Agent:
             self.replay_buffer.reset_max_priority()
             self.sync.max_(self.replay_buffer._maxp)  # :120 over every rank's leaves
 
-    def maybe_train_and_checkpoint(self, ep_timesteps, ep_return):
-        """:296-312 (the episode return is MIN-reduced over data-parallel ranks)."""
+    def maybe_train_and_checkpoint(self, ep_timesteps, ep_return, train=None):
+        """:296-312 (the episode return is MIN-reduced over data-parallel ranks).
+        train: the callable one training step runs (default self.train; the
+        vectorised reference-schedule trainer passes its graph-replayed step)."""
         self.eps_since_update += 1
         self.timesteps_since_update += ep_timesteps
         r = float(ep_return)
@@ -1104,20 +1121,22 @@ class Agent:
             r = -float(t)
         self.min_return = min(self.min_return, r)
         if self.min_return < self.best_min_return:
-            self.train_and_reset()
+            self.train_and_reset(train)
         elif self.eps_since_update == self.max_eps_before_update:
             self.best_min_return = self.min_return
             self.learner.checkpoint_actor.load_state_dict(self.learner.actor.state_dict())
             self.learner.checkpoint_encoder.load_state_dict(self.learner.fixed_encoder.state_dict())
-            self.train_and_reset()
+            self.checkpoint_refreshes += 1
+            self.train_and_reset(train)
 
-    def train_and_reset(self):
+    def train_and_reset(self, train=None):
         """:315-325"""
+        train = self.train if train is None else train
         for _ in range(self.timesteps_since_update):
             if self.learner.training_steps == self.hp.steps_before_checkpointing:
                 self.best_min_return *= self.hp.reset_weight
                 self.max_eps_before_update = self.hp.max_eps_when_checkpointing
-            self.train()
+            train()
         self.eps_since_update = 0
         self.timesteps_since_update = 0
         self.min_return = 1e8

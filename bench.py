@@ -114,6 +114,8 @@ def parse():
                     help="env-only launches timed with HIP events for the roofline line")
     ap.add_argument("--no-td7-variants", action="store_true",
                     help="skip the fp32-TD7 and 256-wide-alias sub-lines (configs[1] train mode)")
+    ap.add_argument("--no-reference-schedule", action="store_true",
+                    help="skip the reference-schedule sub-line (RefScheduleTrainer, train mode)")
     a = ap.parse_args()
     if a.envs is None:
         a.envs = {"configs1": 4096, "dr_sweep": 16384, "wide": 65536}[a.workload]
@@ -321,6 +323,60 @@ def fused_critic_timing(agent, reps=20, replays=10):
 # (Σ(L-3) = 2,257 active env-steps) it trains round(mean(ep_len)) = 283 steps
 # (Simulation/Exoskeleton_agent_train.py:115,145,208 -> TD7_multi_agent.py:315-325)
 REFERENCE_ENV_STEPS_PER_UPDATE = 2257 / 283
+
+
+def reference_schedule(env, dev, args, hp, rounds=3, warm_rounds=2):
+    """The reference training script's schedule on the same envs
+    (exo_amd.rollout.RefScheduleTrainer, Simulation/Exoskeleton_agent_train.py:
+    110-211): per episode round a synchronous rollout of every env (uniform
+    actions until 25,000 env-steps, then select_action with exploration;
+    transitions inserted with the reference's shared replay pointer), then
+    maybe_train_and_checkpoint's burst of round(mean(ep_len)) = 283
+    graph-replayed TD7 steps with the policy-checkpoint rule.  Fresh agent;
+    `warm_rounds` untimed (the first is the random warm-up and captures the
+    graphs), then `rounds` timed with the rollout and the burst timed apart."""
+    from exo_amd.rollout import RefScheduleTrainer
+    from exo_amd.td7 import Agent
+    torch.manual_seed(2)
+    ag = Agent(80, 7, 1, env_num=8, hp=hp, device=dev, precision=args.precision, n_envs=env.n, graph_safe=True)
+    tr = RefScheduleTrainer(env, ag, warmup=25_000)
+    for _ in range(warm_rounds):
+        tr.run_round()
+    torch.cuda.synchronize()
+    # the rollout and the burst of each round timed apart (host clock, synchronised)
+    t_roll = t_burst = 0.0
+    orig = ag.maybe_train_and_checkpoint
+
+    def timed_burst(ep_timesteps, ep_return, train=None):
+        nonlocal t_burst
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        orig(ep_timesteps, ep_return, train=train)
+        torch.cuda.synchronize()
+        t_burst += time.perf_counter() - t
+    ag.maybe_train_and_checkpoint = timed_burst
+    env_steps = updates = 0
+    t0 = time.perf_counter()
+    for _ in range(rounds):
+        n, b = tr.run_round()
+        env_steps += n
+        updates += b
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t_roll = dt - t_burst
+    out = {"env_steps_per_sec": env_steps / dt, "grad_steps_per_sec": updates / dt,
+           "burst_grad_steps_per_sec": updates / t_burst, "rollout_env_steps_per_sec": env_steps / t_roll,
+           "ms_per_round": dt / rounds * 1e3, "rollout_ms_per_round": t_roll / rounds * 1e3,
+           "burst_ms_per_round": t_burst / rounds * 1e3, "updates_per_round": updates / rounds,
+           "env_steps_per_round": env_steps / rounds, "rounds_timed": rounds,
+           "env_steps_per_grad_step": env_steps / max(updates, 1),
+           "checkpoint_refreshes": ag.checkpoint_refreshes, "replay": "reference shared pointer (add_batch_ref)",
+           "note": "Exoskeleton_agent_train.py:110-211 on the device: warm-up 25,000 env-steps of uniform actions, "
+                   "then select_action with Gaussian exploration; per round round(mean(ep_len)) = 283 "
+                   "graph-replayed Agent.train steps and the policy-checkpoint rule (TD7_multi_agent.py:296-325)"}
+    ag.maybe_train_and_checkpoint = orig
+    del tr, ag
+    return out
 
 
 def td7_variants(env, dev, args, iters=60, warmup=8):
@@ -629,6 +685,8 @@ def main():
                     "peak_source": "tools/stream_bench.hip (profiles/r02b_raw/stream_bench.txt)"}
         if agent is not None and args.workload == "configs1" and world == 1 and not args.no_td7_variants:
             res["td7_variants"] = td7_variants(env, dev, args)
+        if agent is not None and world == 1 and not args.no_reference_schedule:
+            res["reference_schedule"] = reference_schedule(env, dev, args, agent.hp)
         if finite is not None:
             res["weights_finite"] = all(finite.values()) or finite
         if dp_sync is not None:

@@ -193,9 +193,11 @@ int exo_tremor_metrics(exo_ctx *c, const float *info_dev, const uint8_t *stepped
 /* The synchronous-episode trainer's active mask on the device
  * (Simulation/Exoskeleton_agent_train.py:123-125): *k_dev (int64) advances by
  * one, saturating at rows - 1, and row *k_dev of table_dev [rows][n] (uint8)
- * is copied to active_dev [n].  Graph-capturable, no host sync. */
+ * is copied to active_dev [n]; count_dev (int32, may be NULL) receives the
+ * number of active envs of that row -- the number of select_action calls the
+ * script makes at that step (:125-128).  Graph-capturable, no host sync. */
 int exo_active_advance(const uint8_t *table_dev, int32_t rows, int32_t n, int64_t *k_dev, uint8_t *active_dev,
-                       void *stream);
+                       int32_t *count_dev, void *stream);
 
 int exo_eval_metrics(exo_ctx *c, const float *info_dev, const uint8_t *stepped_dev, double humerus_length,
                      double forearm_length, float *counters_dev, void *stream);
@@ -262,6 +264,20 @@ int lap_store_batch(const lap_tree_desc *t, const lap_storage_desc *st, const fl
                     const float *action_dev, const float *next_state_dev, const float *reward_dev,
                     const uint8_t *done_dev, const int32_t *strata_dev, const uint8_t *active_dev, float action_scale,
                     int32_t n, int32_t *row_ws_dev, void *stream);
+
+/* LAP.add (Agent/TD7_buffer_multi_agent.py:49-63) called once per active env
+ * of one vectorised step, in env order -- the training script's per-env loop
+ * (Simulation/Exoskeleton_agent_train.py:139-142) -- with the reference's
+ * SHARED pointer: ref_dev = int64 {ptr, count, size} (zero = a fresh buffer),
+ * the c-th add writes slot ptr + #{multiples of n_strata in [count, c)} of
+ * stratum strata[i] (env 0's first transition one slot behind, overwrites when
+ * envs are done: the later add wins), every stratum's sampling size set to the
+ * shared size.  Same stored values as lap_store_batch.  ws_dev: 3n int32
+ * scratch. */
+int lap_store_batch_ref(const lap_tree_desc *t, const lap_storage_desc *st, int64_t *ref_dev,
+                        const float *state_dev, const float *action_dev, const float *next_state_dev,
+                        const float *reward_dev, const uint8_t *done_dev, const int32_t *strata_dev,
+                        const uint8_t *active_dev, float action_scale, int32_t n, int32_t *ws_dev, void *stream);
 
 /* LAP.sample (:65-111): batch draws per stratum (u_dev [n_strata][batch]),
  * indices -> idx_dev [n_strata][batch], the sampled rows gathered into
@@ -336,10 +352,13 @@ int td7_noisy_action(const float *a_dev, const float *noise_dev, float *sigma_de
 /* td7_noisy_action with the noise drawn in the kernel: element 2j+t is normal t
  * (Box-Muller) of Philox4x32-10 block (j, call, tag) under key seed, call =
  * *counter_dev, which advances by one per launch (graph-replay safe);
- * ticket_dev: one uint32, zero at the first call, left zero. */
+ * ticket_dev: one uint32, zero at the first call, left zero.  dec_count_dev
+ * (int32, may be NULL): sigma -= sigma_dec * *dec_count_dev instead of
+ * sigma_dec -- one decrement per select_action call of the script, i.e. per
+ * ACTIVE env (TD7_multi_agent.py:207, Exoskeleton_agent_train.py:125-128). */
 int td7_noisy_action_rng(const float *a_dev, uint64_t seed, uint32_t tag, unsigned long long *counter_dev,
                          uint32_t *ticket_dev, float *sigma_dev, float sigma_dec, float clip, float scale,
-                         float *out_dev, int32_t n, void *stream);
+                         float *out_dev, int32_t n, const int32_t *dec_count_dev, void *stream);
 /* F.mse_loss (encoder loss, TD7_multi_agent.py:226): *loss = mean (x - y)^2;
  * backward dx = 2 (x - y) / n * (*g).  ws_dev: TD7_MSE_WS floats, zeroed once
  * by the caller (block partials + a ticket the kernel leaves at zero); one
@@ -454,6 +473,7 @@ typedef struct {
     float sigma_dec, clip, scale;
     int32_t pad1;
     const float *z;
+    const int32_t *dec_count; /* non-NULL: sigma -= sigma_dec * *dec_count (td7_noisy_action_rng) */
 } td7f_noise;
 
 /* Activation codes of the three nets: act[0] encoder, act[1] actor, act[2] critic (1 relu, 2 elu). */

@@ -179,3 +179,37 @@ def test_sample_never_returns_the_slot_at_size():
     # holds slots 0-4, strata 1-2 slots 1-5 (their slot 0 was never written)
     assert set(np.unique(idx[0])) == {0, 1, 2, 3, 4}
     assert set(np.unique(idx[1])) == set(np.unique(idx[2])) == {1, 2, 3, 4}
+
+
+def test_add_batch_ref_equals_sequential_reference_adds():
+    """lap_store_batch_ref == LAP.add (:49-63) called once per active row in row
+    order: stored transitions, leaves, sums, the shared pointer and size --
+    random strata (several rows per stratum), random active masks (overwrites
+    of one slot by two adds of a stratum between pointer advances: the later
+    add wins), a pointer that wraps the capacity."""
+    rng = np.random.default_rng(3)
+    E, C, N = 4, 40, 19
+    seq, vec = _lap(E, C, 4), _lap(E, C, 4)
+    for step in range(30):
+        st = rng.normal(size=(N, 80)).astype(np.float32)
+        nx = rng.normal(size=(N, 80)).astype(np.float32)
+        ac = rng.uniform(-1, 1, (N, 7)).astype(np.float32)
+        rw = rng.normal(size=N).astype(np.float32)
+        dn = rng.random(N) < 0.1
+        strata = rng.integers(0, E, N).astype(np.int32)
+        active = rng.random(N) < (0.3 if step % 3 else 0.9)
+        if step % 7 == 3:  # a max_priority other than 1 for the new leaves
+            pr = torch.full((E * 4,), 1.0 + step, device="cuda")
+            for lap in (seq, vec):
+                lap.update_priority(pr, ind=torch.zeros((E, 4), dtype=torch.int32, device="cuda"))
+        for i in np.flatnonzero(active):
+            seq.add(st[i], ac[i], nx[i], float(rw[i]), bool(dn[i]), tremor_num=int(strata[i]))
+        T = lambda a: torch.as_tensor(a, device="cuda")  # noqa: E731
+        vec.add_batch_ref(T(st), T(ac), T(nx), T(rw), T(dn), T(strata), T(active))
+        torch.cuda.synchronize()
+        assert vec.ref_pointer() == (seq.ptr, seq.count, seq.size), step
+        for name in ("state", "action", "next_state", "reward", "not_done"):
+            torch.testing.assert_close(getattr(vec, name)[:, :C], getattr(seq, name)[:, :C], rtol=0, atol=0)
+        torch.testing.assert_close(vec._tree, seq._tree, rtol=0, atol=0)
+        assert torch.equal(vec.size_s, seq.size_s)
+    assert seq.count > 2 * C  # the pointer wrapped

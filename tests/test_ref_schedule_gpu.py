@@ -1,0 +1,190 @@
+"""The reference training schedule in the vectorised trainer:
+exo_amd.rollout.RefScheduleTrainer against the drop-in training-script mirror
+(<pkg>/Simulation/Exoskeleton_agent_train.py, the reference's
+Simulation/Exoskeleton_agent_train.py:110-211 with FIX 1-4).
+
+Both runs: 8 envs (one per motion), seed 0, the same injected reset draws per
+(round, env), the script's own action choice (np.random.uniform during the
+warm-up, then the drop-in's per-env select_action with Gaussian exploration,
+drawn from np.random in the script's order -- injected into the trainer
+through its action_source hook).  Everything else is each side's own code:
+the mirror steps 8 one-env objects, adds transitions one by one with
+LAP.add(tremor_num=i) and calls Agent.train() eagerly inside
+maybe_train_and_checkpoint; the trainer steps all envs in one launch, inserts
+with lap_store_batch_ref (the shared pointer on the device) and replays its
+training steps from HIP graphs.  The per-round decision trace
+(training_steps, eps_since_update, min/best_min_return, checkpoint refreshes)
+and the final weights -- live and checkpoint nets, optimiser moments -- must
+agree bit for bit."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import PKG
+
+pytestmark = pytest.mark.gpu
+
+E = 8
+BUF = 4096
+
+
+def _draws(rnd, motion, L):
+    from exo_amd.vec_env import draws_per_episode
+    return np.random.default_rng(7919 * rnd + motion).random(draws_per_episode(L))
+
+
+def _record(agent, trace):
+    """Wrap agent.maybe_train_and_checkpoint to append its state after each round."""
+    orig = agent.maybe_train_and_checkpoint
+
+    def wrapped(ep_timesteps, ep_return, train=None):
+        refreshed = agent.checkpoint_refreshes
+        orig(ep_timesteps, ep_return, train=train)
+        L = agent.learner
+        trace.append((ep_timesteps, ep_return, L.training_steps, agent.eps_since_update, agent.min_return,
+                      agent.best_min_return, agent.max_eps_before_update,
+                      agent.checkpoint_refreshes - refreshed))
+    agent.maybe_train_and_checkpoint = wrapped
+
+
+def _run_mirror(tmp_path, rounds, warmup, precision, monkeypatch):
+    sys.path.insert(0, os.path.join(PKG, "Simulation"))
+    import Exoskeleton_agent_train as drv
+    from exo_amd import td7
+
+    class InjectedEnv(drv.ExoskeletonEnv_train):
+        def __init__(self, *a, **kw):
+            super().__init__(*a, seed=1234, **kw)  # explicit seed: no np.random draw at construction
+            self._round = 0
+
+        def reset(self):
+            obs = self._vec.reset_from_draws([0], [_draws(self._round, int(self.file_num), self.max_count)])
+            self._round += 1
+            self._done = False
+            self.state = obs[0].cpu().numpy()
+            return self.state, self.counts
+
+    trace = []
+    orig_init = td7.Agent.__init__
+
+    def init(self, *a, **kw):
+        orig_init(self, *a, **kw)
+        _record(self, trace)
+    monkeypatch.setattr(drv, "ExoskeletonEnv_train", InjectedEnv)
+    monkeypatch.setattr(td7.Agent, "__init__", init)
+    args = drv.parse_args(["--seed", "0", "--n_steps", "1000000", "--warmup", str(warmup), "--save_dir",
+                           str(tmp_path), "--buffer_size", str(BUF), "--max_rounds", str(rounds), "--quiet",
+                           "--precision", precision])
+    out = drv.train(args)
+    monkeypatch.undo()
+    return out["agent"], trace, out["steps"]
+
+
+def _run_trainer(rounds, warmup, precision):
+    import random
+    from exo_amd import VecExoskeletonEnv
+    from exo_amd.rollout import RefScheduleTrainer
+    from exo_amd.td7 import Agent
+
+    torch.manual_seed(0)
+    np.random.seed(0)
+    random.seed(0)
+    env = VecExoskeletonEnv(E, seed=1234)
+    agent = Agent(80, 7, 1, learning_steps=1000000, env_num=E, buffer_size=BUF, precision=precision)
+    trace = []
+    _record(agent, trace)
+    rs = np.random.mtrand._rand  # the script's global np.random stream (seeded above)
+
+    def actions(tr, random_phase):
+        """The script's choice per running env, in env order (:125-131)."""
+        act = np.zeros((E, 7))
+        obs = tr.obs.cpu().numpy() if not random_phase else None
+        for i in np.flatnonzero(tr.active_host[tr.k]):
+            if random_phase:
+                act[i] = np.clip(rs.uniform(-1, 1, 7), -1, 1)
+            else:
+                act[i] = agent.select_action(obs[i].astype(np.float64), use_checkpoint=False, use_exploration=True)
+        return act
+
+    def resets(rnd, obs_out):
+        Ls = env.lengths_host
+        env.reset_from_draws(np.arange(E), [_draws(rnd, m, int(Ls[m])) for m in range(E)], obs_out=obs_out)
+
+    tr = RefScheduleTrainer(env, agent, warmup=warmup, action_source=actions, reset_source=resets)
+    for _ in range(rounds):
+        tr.run_round()
+    torch.cuda.synchronize()
+    return agent, trace, tr
+
+
+@pytest.mark.parametrize("precision,rounds", [("fp32", 4), ("bf16", 3)])
+def test_ref_schedule_matches_training_mirror(tmp_path, monkeypatch, precision, rounds):
+    warmup = 3257  # rounds 1-2 random (steps_count 2,257 <= warmup < 4,514: :210-211), then the policy
+    ag_m, tr_m, steps_m = _run_mirror(tmp_path, rounds, warmup, precision, monkeypatch)
+    ag_v, tr_v, trainer = _run_trainer(rounds, warmup, precision)
+    assert steps_m == trainer.steps_count == rounds * 2257
+    assert [t[0] for t in tr_m] == [283] * rounds  # round(mean(ep_len)) of the 8 motions
+    # the decision trace, bit for bit
+    assert len(tr_m) == len(tr_v) == rounds
+    for r, (a, b) in enumerate(zip(tr_m, tr_v)):
+        assert a == b, f"round {r + 1}: mirror {a} vs trainer {b}"
+    assert sum(t[7] for t in tr_v) >= 1  # at least one checkpoint refresh happened
+    # the replay: same shared pointer state, same stored transitions and priorities
+    rb_m, rb_v = ag_m.replay_buffer, ag_v.replay_buffer
+    assert (rb_m.ptr, rb_m.count, rb_m.size) == rb_v.ref_pointer()
+    n = rb_m.size + 1
+    for name in ("state", "action", "next_state", "reward", "not_done"):
+        torch.testing.assert_close(getattr(rb_v, name)[:, :n], getattr(rb_m, name)[:, :n], rtol=0, atol=0)
+    torch.testing.assert_close(rb_v._tree, rb_m._tree, rtol=0, atol=0)
+    # the nets after the bursts: live, target, checkpoint, optimiser moments
+    Lm, Lv = ag_m.learner, ag_v.learner
+    for name in ("actor", "critic", "encoder", "actor_target", "critic_target", "fixed_encoder",
+                 "fixed_encoder_target", "checkpoint_actor", "checkpoint_encoder"):
+        for p, q in zip(getattr(Lm, name).parameters(), getattr(Lv, name).parameters()):
+            torch.testing.assert_close(q, p, rtol=0, atol=0, msg=name)
+    for opt in ("actor_optimizer", "critic_optimizer", "encoder_optimizer"):
+        torch.testing.assert_close(getattr(Lv, opt).m, getattr(Lm, opt).m, rtol=0, atol=0)
+        torch.testing.assert_close(getattr(Lv, opt).v, getattr(Lm, opt).v, rtol=0, atol=0)
+    assert float(Lv.exploration_noise_t) == float(Lm.exploration_noise_t) < ag_m.hp.exploration_noise
+    assert len([k for k in trainer.graphs if k[0] == "train"]) == 2  # bursts replayed from graphs
+
+
+def test_ref_schedule_device_path():
+    """Without hooks: device uniform warm-up actions, then the batched fused
+    select_action (bf16) whose exploration noise drops once per RUNNING env;
+    graph-replayed rollouts and bursts; the schedule's bookkeeping."""
+    from exo_amd import VecExoskeletonEnv
+    from exo_amd.rollout import RefScheduleTrainer
+    from exo_amd.td7 import Agent
+    torch.manual_seed(0)
+    N = 64
+    env = VecExoskeletonEnv(N, seed=5)
+    agent = Agent(80, 7, 1, learning_steps=100000, env_num=E, buffer_size=2 * BUF, precision="bf16", n_envs=N)
+    tr = RefScheduleTrainer(env, agent, warmup=1)
+    A = int((env.lengths_host - 3).sum())
+    n1, b1 = tr.run_round()  # random actions (allow_train is set after this round)
+    assert (n1, b1) == (A, 283) and tr.allow_train and tr.trace[0]["random_actions"]
+    s0 = float(agent.learner.exploration_noise_t)
+    n2, b2 = tr.run_round()  # the policy
+    torch.cuda.synchronize()
+    assert (n2, b2) == (A, 283) and not tr.trace[1]["random_actions"]
+    # one decrement per select_action call of the script = per running env-step (:125-128, :207)
+    want = s0 - A * agent.learner.action_noise_decrease
+    # (344 f32 decrements of at most half an ulp each; decrementing by all N envs would be 4e-3 lower)
+    assert abs(float(agent.learner.exploration_noise_t) - want) < 5e-6
+    assert agent.learner.training_steps == 2 * 283 and tr.steps_count == 2 * A
+    assert tr.trace[0]["checkpoint_refreshed"]  # the first round always checkpoints (best_min_return = -1e8)
+    # the shared pointer advanced once per E adds
+    ptr, count, size = agent.replay_buffer.ref_pointer()
+    assert count == 2 * A and ptr == size == -(-2 * A // E)
+    assert int(agent.replay_buffer.size_s.min()) == int(agent.replay_buffer.size_s.max()) == size
+    assert ("roll", True, 0) in tr.graphs and ("roll", False, 0) in tr.graphs
+    assert ("train", True) in tr.graphs and ("train", False) in tr.graphs
+    for m in (agent.learner.actor, agent.learner.critic, agent.learner.encoder):
+        assert all(torch.isfinite(p).all() for p in m.parameters())
+    # the checkpoint policy acts (a refresh copied the actor of its round)
+    a = agent.select_action(np.zeros((3, 80), np.float32), use_checkpoint=True, use_exploration=False)
+    assert np.isfinite(a).all() and a.shape == (3, 7)

@@ -104,9 +104,13 @@ def test_active_advance_saturates_and_copies_rows():
     table = (torch.arange(4 * 70, device="cuda").view(4, 70) % 3 == 0).contiguous()
     k = torch.zeros(1, dtype=torch.int64, device="cuda")
     act = torch.zeros(70, dtype=torch.bool, device="cuda")
+    cnt = torch.full((1,), -1, dtype=torch.int32, device="cuda")
     for want in (1, 2, 3, 3, 3):
         nat.check(nat.lib().exo_active_advance(nat.ptr(table), 4, 70, nat.ptr(k), nat.ptr(act),
+                                               nat.ptr(cnt) if want != 2 else None,
                                                nat.stream_ptr(torch.device("cuda", 0))), "exo_active_advance")
         torch.cuda.synchronize()
         assert int(k) == want
         assert torch.equal(act, table[want])
+        if want != 2:  # the active count of the copied row (NULL: left alone)
+            assert int(cnt) == int(table[want].sum())
