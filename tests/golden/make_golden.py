@@ -43,6 +43,10 @@ numbers it produces are written here):
   recorded episodes, train() stubbed (``--only checkpoint_policy``).
 * ``select_action.npz`` - batched ``select_action`` of
   ``Agent/TD7_multi_agent_Pink_noise.py:209`` with exploration off.
+* ``select_action_full.npz`` - the same at the bench's widths (zs / enc 300,
+  critic 320, actor 300 and 320) on 256 real observations, checkpoint and
+  perturbed live nets rebuilt by the test from seeds (``--only
+  select_action_full``; cases in tests/helpers.py).
 """
 import json
 import os
@@ -624,6 +628,39 @@ def make_select_action(rng):
     out["state"] = st
     out["action_ckpt"] = agent.select_action(st, use_checkpoint=True, use_exploration=False)
     out["action_live"] = agent.select_action(st, use_checkpoint=False, use_exploration=False)
+    return out
+
+
+# select_action at the bench's widths: the cases, observations and perturbation
+# live in tests/helpers.py (the GPU test rebuilds the nets from them)
+sys.path.insert(0, os.path.dirname(HERE))
+from helpers import SELECT_FULL, select_full_perturb, select_full_states  # noqa: E402
+
+
+def make_select_action_full():
+    """The Pink agent's batched select_action (Agent/TD7_multi_agent_Pink_noise.py:
+    209-228) at the bench's widths, exploration off, on 256 real observations:
+    checkpoint nets = the torch.manual_seed(seed) initialisation (the build's
+    seeded init is bit-exact, tests/test_td7_full.py), live actor and fixed
+    encoder perturbed by select_full_perturb.  No weights are stored: the test
+    rebuilds them from the seed."""
+    import torch
+    import Agent.TD7_multi_agent_Pink_noise as tp
+    st = select_full_states()
+    out = {"state": st}
+    for name, kw, seed in SELECT_FULL:
+        torch.manual_seed(seed)
+        hp = tp.Hyperparameters(**kw)
+        agent = tp.Agent(80, 7, 1, hp=hp, env_num=8)
+        select_full_perturb(agent.actor, 1000 * seed)
+        select_full_perturb(agent.fixed_encoder, 1000 * seed + 500)
+        out[f"{name}.ckpt"] = agent.select_action(st, use_checkpoint=True, use_exploration=False)
+        out[f"{name}.live"] = agent.select_action(st, use_checkpoint=False, use_exploration=False)
+        out[f"{name}.widths"] = np.array([hp.zs_dim, hp.enc_hdim, hp.critic_hdim, hp.actor_hdim])
+        with torch.no_grad():  # fp64 sums of the live nets: the test checks its rebuild against them
+            out[f"{name}.live_sum"] = np.array([float(sum(p.double().sum() for p in m.parameters()))
+                                                for m in (agent.actor, agent.fixed_encoder)])
+        del agent
     return out
 
 

@@ -109,3 +109,31 @@ def td7_full_sample_index(name, numel):
         return np.arange(numel, dtype=np.int64)
     seed = sum(ord(c) * (i + 1) for i, c in enumerate(name))
     return np.sort(np.random.Generator(np.random.PCG64(seed)).choice(numel, TD7_FULL_SAMPLES, replace=False))
+
+
+# ----------------------------------------------------------------------------
+# select_action_full.npz (make_golden.py --only select_action_full): select_action
+# at the bench's widths: (name, Hyperparameters overrides, torch seed).
+# The Pink agent's defaults (zs / enc 300, critic 320, actor 300, the shipped
+# checkpoints' shapes) and TD7_multi_agent.py's actor width 320 (the bench).
+SELECT_FULL = [("pink300", {}, 41), ("actor320", {"actor_hdim": 320}, 42)]
+SELECT_FULL_ROWS = 256
+SELECT_FULL_PERTURB = 0.02
+
+
+def select_full_states():
+    """SELECT_FULL_ROWS real observations: every 7th step of the motion-0..7
+    golden traces (env_m*.npz step_obs, the reference env's own outputs)."""
+    obs = np.concatenate([np.load(os.path.join(GOLDEN, f"env_m{m}.npz"))["step_obs"] for m in range(8)])
+    return obs[::7][:SELECT_FULL_ROWS].astype(np.float32)
+
+
+def select_full_perturb(module, seed):
+    """Move the live nets off the checkpoint copies: p += PERTURB * N(0, 1)
+    from PCG64(seed + k) for the k-th parameter (named_parameters order);
+    tests/test_select_full_gpu.py applies the same to the build's nets."""
+    import torch
+    with torch.no_grad():
+        for k, (_, p) in enumerate(module.named_parameters()):
+            z = np.random.Generator(np.random.PCG64(seed + k)).normal(0, 1, tuple(p.shape)).astype(np.float32)
+            p.add_(SELECT_FULL_PERTURB * torch.from_numpy(z))
