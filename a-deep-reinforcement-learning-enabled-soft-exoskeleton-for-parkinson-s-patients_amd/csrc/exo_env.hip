@@ -137,7 +137,7 @@ __global__ __launch_bounds__(64) void exo_reset_kernel(Dev S, Urdf U, const uint
     }
 #pragma unroll
     for (int i = 0; i < 7; ++i) { mn[i] = wave_min(mn[i]); mx[i] = wave_max(mx[i]); }
-    const double jmax0[7] = {2.5, 5, 10, 5, 5, 0.5, 0.5};
+    // joint_max_values (:59): the shipped table unless exo_set_tremor_model chose another
 #pragma unroll
     for (int k = 0; k < T_PER_LANE; ++k) {
         const int t = lane + 64 * k;
@@ -145,9 +145,13 @@ __global__ __launch_bounds__(64) void exo_reset_kernel(Dev S, Urdf U, const uint
 #pragma unroll
             for (int i = 0; i < 7; ++i) {
                 const double acc = (a1[i] * wv1[k] + a2[i] * wv2[k] + nz[k]) * (double)((seq >> i) & 1);
-                double v = (-1 + 2 * (acc - mn[i]) / (mx[i] - mn[i])) * (jmax0[i] * mag);
+                double v = (-1 + 2 * (acc - mn[i]) / (mx[i] - mn[i])) * (S.tjmax[i] * mag);
                 if (!isfinite(v)) v = 0.0; // np.nan_to_num (:67)
-                const double sgn = (D(3 + L + i * (L + 2) + 2 + t) < 0.5) ? -1.0 : 1.0;
+                // np.random.choice([-1, 1], L) per sample (:70); the diagnostic
+                // models use the axis's first sign draw for every sample, or none
+                const int ts = S.tsign == EXO_TREMOR_SIGN_PER_AXIS ? 0 : t;
+                const double sgn = (S.tsign != EXO_TREMOR_SIGN_NONE && D(3 + L + i * (L + 2) + 2 + ts) < 0.5) ? -1.0
+                                                                                                                : 1.0;
                 v *= sgn;
                 S.tremor[((size_t)t * 7 + i) * N + e] = v;
                 if (t < 3 && i < 4) sTrem[t][i] = v;
@@ -780,6 +784,7 @@ int exo_create(const exo_env_config *cfgs, int32_t n_envs, const double *motion_
         return EXO_ENOMEM;
     }
     S.motion = motion_d; S.L = L_d; S.seq = seq_d; S.cfg = cfg_d; S.imu = imu_d;
+    exo_set_tremor_model(c, nullptr, EXO_TREMOR_SIGN_PER_SAMPLE); // the shipped tremor (generate_parkinson_tremor.py:59, :70)
     hipError_t e = hipMemcpy(motion_d, mot.data(), N * 4, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(L_d, L.data(), N * 4, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(seq_d, seq.data(), N * 4, hipMemcpyHostToDevice);
@@ -1049,6 +1054,18 @@ int exo_set_state_host(exo_ctx *c, int32_t env, const double *in) {
 int exo_set_step_variant(exo_ctx *c, int32_t variant) {
     if (!c || variant < EXO_STEP_AUTO || variant > EXO_STEP_ROWS_SHARED) return EXO_EINVAL;
     c->step_variant = variant;
+    return EXO_OK;
+}
+
+int exo_set_tremor_model(exo_ctx *c, const double *jmax7, int32_t sign_mode) {
+    if (!c || sign_mode < EXO_TREMOR_SIGN_PER_SAMPLE || sign_mode > EXO_TREMOR_SIGN_NONE) return EXO_EINVAL;
+    static const double shipped[7] = {2.5, 5, 10, 5, 5, 0.5, 0.5}; // generate_parkinson_tremor.py:59
+    for (int i = 0; i < 7; ++i) {
+        const double v = jmax7 ? jmax7[i] : shipped[i];
+        if (!(v >= 0) || !(v < 1e6)) return fail(c, EXO_EINVAL, "exo_set_tremor_model: invalid joint maximum");
+        c->S.tjmax[i] = v;
+    }
+    c->S.tsign = sign_mode;
     return EXO_OK;
 }
 

@@ -128,6 +128,9 @@ struct Dev {
     double *mb_q, *mb_qd;            // [19][N] joint positions / velocities (rows 0..4 mirror phys_q)
     double *mb_tgt;                  // [5][N] POSITION_CONTROL targets written by the step kernel (rad)
     uint8_t *mb_flag;                // [N] 1 = the step kernel stepped the env, the physics kernel follows
+    // tremor model of the reset (exo_set_tremor_model): per-axis maxima and sign mode
+    double tjmax[7];                 // joint_max_values (generate_parkinson_tremor.py:59)
+    int32_t tsign;                   // EXO_TREMOR_SIGN_*: per sample (:70), one per axis, none
 };
 
 __host__ __device__ inline void matmul3(const double *A, const double *B, double *C) {

@@ -214,6 +214,19 @@ class VecExoskeletonEnv:
                   self._ctx)
         self.step_variant = name
 
+    TREMOR_SIGN = {"per_sample": 0, "per_axis": 1, "none": 2}
+
+    def set_tremor_model(self, jmax=None, sign="per_sample"):
+        """Tremor of later resets (diagnostic, include/exo_amd.h
+        exo_set_tremor_model): jmax = joint_max_values [7] before the
+        magnitude (None: the shipped generate_parkinson_tremor.py:59 table);
+        sign = 'per_sample' (the shipped :70), 'per_axis' or 'none'."""
+        j = None if jmax is None else np.ascontiguousarray(jmax, dtype=np.float64)
+        if j is not None and j.shape != (7,):
+            raise ValueError("jmax must hold 7 values")
+        nat.check(nat.lib().exo_set_tremor_model(self._ctx, None if j is None else j.ctypes.data_as(nat.P(ctypes.c_double)),
+                                                 self.TREMOR_SIGN[sign]), "exo_set_tremor_model", self._ctx)
+
     # ----------------------------------------------------- physics model
     @staticmethod
     def multibody_params(**overrides):

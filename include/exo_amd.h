@@ -122,6 +122,19 @@ int exo_set_state_host(exo_ctx *ctx, int32_t env, const double *in);
 #define EXO_STEP_ROWS_SHARED 3
 int exo_set_step_variant(exo_ctx *ctx, int32_t variant);
 
+/* Tremor model of later resets (diagnostic; the default is the shipped code):
+ * jmax7 = joint_max_values before the magnitude (generate_parkinson_tremor.py:59;
+ * NULL = the shipped {2.5, 5, 10, 5, 5, 0.5, 0.5}), sign_mode = how
+ * np.random.choice([-1, 1], L) (:70) applies: EXO_TREMOR_SIGN_PER_SAMPLE (the
+ * shipped code), EXO_TREMOR_SIGN_PER_AXIS (the axis's first sign draw for
+ * every sample), EXO_TREMOR_SIGN_NONE.  The draw stream is unchanged.  Used
+ * to test which code revision produced the authors' Evaluation_logs (their
+ * per-env blocks print max torques of exactly {10, 5, 2.5, 5} on axes 0-3). */
+#define EXO_TREMOR_SIGN_PER_SAMPLE 0
+#define EXO_TREMOR_SIGN_PER_AXIS 1
+#define EXO_TREMOR_SIGN_NONE 2
+int exo_set_tremor_model(exo_ctx *ctx, const double *jmax7, int32_t sign_mode);
+
 /* ------------------------------------------------------------------------
  * Physics of stepSimulation (Exoskeleton_env.py:433, Bullet 3.2.5 -- absent
  * here).  EXO_PHYS_IDEAL (default): the idealised position motors of

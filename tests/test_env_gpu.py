@@ -276,3 +276,44 @@ def test_domain_randomisation_sweep_matches_oracle(variant):
             _close_obs(outs[k][0][e], ob)
             np.testing.assert_allclose(outs[k][1][e], r, rtol=2e-6, atol=1e-7)
             np.testing.assert_allclose(outs[k][2][e], info, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("model", [("shipped", None, "per_sample"), ("docstring_axis", [10, 5, 2.5, 5, 5, .5, .5], "per_axis"),
+                                   ("docstring_none", [10, 5, 2.5, 5, 5, .5, .5], "none")])
+def test_tremor_model_knob(model):
+    """exo_set_tremor_model (the diagnostic tremor models of tools/eval_hypotheses.py):
+    the reset's tremor table against a numpy restatement of
+    generate_parkinson_tremor.py:5-73 fed the same draws, with the given
+    joint maxima and sign mode; the draw stream is the same in every mode."""
+    from exo_amd import VecExoskeletonEnv, draws_per_episode
+    name, jmax, sign = model
+    n = 8
+    seq = np.array([1, 1, 1, 1, 0, 1, 0])
+    env = VecExoskeletonEnv(n, seed=3, tremor_sequence=seq, tremor_amplitude_range=(0.9, 1.1))
+    env.set_tremor_model(jmax, sign)
+    J = np.array(jmax if jmax is not None else [2.5, 5, 10, 5, 5, 0.5, 0.5])
+    rng = np.random.default_rng(11)
+    draws = [rng.random(draws_per_episode(int(L))) for L in env.lengths_host]
+    env.reset_from_draws(np.arange(n), draws)
+    for e in range(n):
+        L, u = int(env.lengths_host[e]), draws[e]
+        mag = 0.9 + u[0] * 0.2
+        f1, f2 = 4 + 2 * u[1], 8 + 2 * u[2]
+        t = np.linspace(0, L / 40, L)
+        w1, w2, noise = np.sin(2 * np.pi * f1 * t), np.sin(2 * np.pi * f2 * t), u[3:3 + L] * 0.001
+        want = np.zeros((7, L))
+        for i in range(7):
+            b = 3 + L + i * (L + 2)
+            a1, a2 = 10 ** ((-5 + 5 * u[b]) / 20), 10 ** ((-20 + 10 * u[b + 1]) / 20)
+            acc = (a1 * w1 + a2 * w2 + noise) * seq[i]
+            with np.errstate(invalid="ignore"):
+                v = np.nan_to_num((-1 + 2 * (acc - acc.min()) / (acc.max() - acc.min())) * J[i] * mag)
+            s = {"per_sample": np.where(u[b + 2:b + 2 + L] < 0.5, -1.0, 1.0),
+                 "per_axis": np.where(u[b + 2] < 0.5, -1.0, 1.0), "none": 1.0}[sign]
+            want[i] = v * s
+        np.testing.assert_allclose(env.tremor(e), want, rtol=0, atol=1e-12 * J.max(), err_msg=f"{name} env {e}")
+    if sign != "per_sample":  # no per-sample flips: every axis reaches its maximum jmax * magnitude
+        for e in range(n):
+            mx = env.tremor(e).max(axis=1)
+            mag = 0.9 + draws[e][0] * 0.2
+            np.testing.assert_allclose(mx[seq == 1], (J * mag)[seq == 1], rtol=1e-12)
