@@ -339,7 +339,9 @@ __host__ __device__ inline bool rk45_solve(const OdeM &M, const double *T, doubl
 #pragma unroll
         for (int i = 0; i < 7; ++i) { tmp[i] = (y1v[i] - 0.0) / atol; tmp[7 + i] = (a1[i] - a0[i]) / atol; }
         const double d2 = rms14(tmp) / h0;
-        const double h1 = (d1 <= 1e-15 && d2 <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : 1.0 / pow_m5th(0.01 / fmax(d1, d2));
+        // scipy's (0.01 / max(d1, d2)) ** (1 / (order + 1)) with the library pow:
+        // once per solve, and 1 / pow_m5th would add a rounding (<= 3 ulp)
+        const double h1 = (d1 <= 1e-15 && d2 <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : pow(0.01 / fmax(d1, d2), 0.2);
         h_abs = fmin(fmin(100 * h0, h1), tb);
     }
     double t = 0.0;

@@ -209,7 +209,8 @@ __device__ bool rk45_rows(const RM &M, double T, double &q_out) {
         const double a1 = row_acc(M, T, 0.0, y1v);
         const double xq = y1v / atol, xv = (a1 - a0) / atol;
         const double d2 = sqrt(group_sum(xq * xq + xv * xv)) * inv_sqrt14 / h0;
-        const double h1 = (d1 <= 1e-15 && d2 <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : 1.0 / pow_m5th(0.01 / fmax(d1, d2));
+        // scipy's (0.01 / max(d1, d2)) ** 0.2 with the library pow (once per solve)
+        const double h1 = (d1 <= 1e-15 && d2 <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : pow(0.01 / fmax(d1, d2), 0.2);
         h_abs = fmin(fmin(100 * h0, h1), tb);
     }
     double t = 0.0;

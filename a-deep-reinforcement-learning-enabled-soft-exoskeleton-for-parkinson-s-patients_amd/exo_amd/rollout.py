@@ -17,6 +17,7 @@ Host-side bookkeeping left outside the graphs: the env reset at the end of a
 round, the target-network refresh every 250 steps (:284-293).
 """
 import os
+import threading
 
 import numpy as np
 import torch
@@ -94,33 +95,61 @@ def unjoined_streams(events, origin):
 class ForkJoinAudit:
     """Records every Stream.wait_stream and stream-context exit while a graph is
     captured on `origin`; on exit raises CaptureForkError naming any branch not
-    joined back (after joining it, so that capture end still succeeds)."""
+    joined back (after joining it, so that capture end still succeeds).
+
+    The two torch methods are patched once for all audits alive in the
+    process (a depth count: nested audits unpatch when the outermost exits),
+    and an audit records only the calls made on the thread that opened it --
+    another thread's captures and waits stay out of its log."""
+
+    _lock = threading.Lock()
+    _depth = 0
+    _orig = None
+    _open = []  # audits currently entered (any thread)
 
     def __init__(self, origin):
         self.origin = origin
         self.events = []
+        self._thread = None
+
+    @classmethod
+    def _record(cls, ev):
+        me = threading.get_ident()
+        for audit in list(cls._open):
+            if audit._thread == me:
+                audit.events.append(ev)
 
     def __enter__(self):
-        audit = self
-        self._wait = torch.cuda.Stream.wait_stream
-        self._exit = torch.cuda.StreamContext.__exit__
+        cls = ForkJoinAudit
+        self._thread = threading.get_ident()
+        with cls._lock:
+            if cls._depth == 0:
+                wait0, exit0 = torch.cuda.Stream.wait_stream, torch.cuda.StreamContext.__exit__
+                cls._orig = (wait0, exit0)
 
-        def wait_stream(st, other):
-            audit.events.append(("wait", st, other))
-            return audit._wait(st, other)
+                def wait_stream(st, other):
+                    cls._record(("wait", st, other))
+                    return wait0(st, other)
 
-        def ctx_exit(ctx, *a):
-            if ctx.stream is not None:
-                audit.events.append(("use", ctx.stream))
-            return audit._exit(ctx, *a)
+                def ctx_exit(ctx, *a):
+                    if ctx.stream is not None:
+                        cls._record(("use", ctx.stream))
+                    return exit0(ctx, *a)
 
-        torch.cuda.Stream.wait_stream = wait_stream
-        torch.cuda.StreamContext.__exit__ = ctx_exit
+                torch.cuda.Stream.wait_stream = wait_stream
+                torch.cuda.StreamContext.__exit__ = ctx_exit
+            cls._depth += 1
+            cls._open.append(self)
         return self
 
     def __exit__(self, exc_type, exc, tb):
-        torch.cuda.Stream.wait_stream = self._wait
-        torch.cuda.StreamContext.__exit__ = self._exit
+        cls = ForkJoinAudit
+        with cls._lock:
+            cls._open.remove(self)
+            cls._depth -= 1
+            if cls._depth == 0:
+                torch.cuda.Stream.wait_stream, torch.cuda.StreamContext.__exit__ = cls._orig
+                cls._orig = None
         if exc_type is not None:
             return False
         bad = unjoined_streams(self.events, self.origin)

@@ -73,3 +73,30 @@ def test_trainer_captures_are_fork_join_clean(prio_branch, monkeypatch):
         tr.step()
     torch.cuda.synchronize()
     assert len(tr.graphs) >= 2
+
+
+def test_audit_is_reentrant_and_thread_scoped(monkeypatch):
+    """nested audits unpatch only when the outermost exits, and an
+    audit records only its own thread's waits (CPU: the torch methods are
+    replaced by stubs first, so no stream is needed)."""
+    import threading
+
+    import torch
+    from exo_amd.rollout import ForkJoinAudit
+    calls = []
+    monkeypatch.setattr(torch.cuda.Stream, "wait_stream", lambda st, other: calls.append((st, other)))
+    stub_wait = torch.cuda.Stream.wait_stream
+    o, a, b = S(1), S(2), S(3)
+    outer, inner = ForkJoinAudit(o), ForkJoinAudit(o)
+    with outer:
+        torch.cuda.Stream.wait_stream(a, o)
+        with inner:
+            torch.cuda.Stream.wait_stream(o, a)
+            t = threading.Thread(target=lambda: torch.cuda.Stream.wait_stream(b, o))  # not ours
+            t.start()
+            t.join()
+        assert torch.cuda.Stream.wait_stream is not stub_wait  # still patched for the outer audit
+    assert torch.cuda.Stream.wait_stream is stub_wait  # restored once the outermost exits
+    assert [e[1:] for e in outer.events] == [(a, o), (o, a)]
+    assert [e[1:] for e in inner.events] == [(o, a)]
+    assert len(calls) == 3  # every call reached the original method

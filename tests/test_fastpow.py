@@ -29,3 +29,4 @@ def test_fast_inverse_fifth_root_within_one_ulp():
     l2 = np.log2(x.astype(np.float32)).astype(np.float64)
     r = _pow_m5th(x) / (1 - 1.1102230246251565e-17 * 0.6931471805599453 * l2)
     assert (np.abs(r - ref) / np.spacing(ref)).max() > 2
+
