@@ -662,6 +662,7 @@ struct exo_ctx {
     MbModel mb{};
     double *mb_q = nullptr, *mb_qd = nullptr, *mb_tgt = nullptr;
     uint8_t *mb_flag = nullptr;
+    unsigned long long *step_clock = nullptr; // exo_set_step_clock
     std::string err;
 };
 
@@ -834,14 +835,35 @@ int exo_reset_from_draws(exo_ctx *c, const int32_t *env_ids_host, int32_t n, con
     return check(c, e, "exo_reset_from_draws");
 }
 
+// The step clock (exo_set_step_clock): one-lane kernels on the step's stream
+// either side of the step launch read the 100 MHz wall clock; the second adds
+// the interval to clk[1] and counts it in clk[2].  Stream order makes them
+// bracket the step kernel inside a captured graph as well as eagerly.
+namespace {
+__global__ void step_clock_kernel(unsigned long long *clk, int end) {
+    const unsigned long long t = wall_clock64();
+    if (!end) {
+        clk[0] = t;
+    } else {
+        clk[1] += t - clk[0];
+        clk[2] += 1;
+    }
+}
+} // namespace
+
 int exo_step(exo_ctx *c, const float *act_dev, float *obs_dev, float *rew_dev, uint8_t *done_dev, float *info_dev,
              const uint8_t *active_dev, void *stream) {
     if (!c || !act_dev || !obs_dev || !rew_dev || !done_dev) return EXO_EINVAL;
     DeviceGuard g(c->device);
     const bool shared = c->step_variant == EXO_STEP_ROWS_SHARED;
     const bool rows = shared || c->step_variant == EXO_STEP_ROWS || (c->step_variant == EXO_STEP_AUTO && c->N <= 16384);
-    hipError_t e;
-    if (rows) {
+    hipError_t e = hipSuccess;
+    if (c->step_clock) {
+        hipLaunchKernelGGL(step_clock_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, c->step_clock, 0);
+        e = hipGetLastError();
+    }
+    if (e != hipSuccess) {
+    } else if (rows) {
         e = launch_exo_step_rp(c->S, c->U, act_dev, obs_dev, rew_dev, done_dev, info_dev, active_dev,
                                (hipStream_t)stream, shared);
     } else {
@@ -852,6 +874,10 @@ int exo_step(exo_ctx *c, const float *act_dev, float *obs_dev, float *rew_dev, u
     }
     if (e == hipSuccess && c->physics == EXO_PHYS_MULTIBODY) // stepSimulation (:433) of the envs just stepped
         e = launch_exo_multibody(c->S, c->U, c->mb, c->S.mb_tgt, c->S.mb_flag, 1, (hipStream_t)stream);
+    if (e == hipSuccess && c->step_clock) {
+        hipLaunchKernelGGL(step_clock_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, c->step_clock, 1);
+        e = hipGetLastError();
+    }
     return check(c, e, "exo_step");
 }
 
@@ -1054,6 +1080,18 @@ int exo_set_state_host(exo_ctx *c, int32_t env, const double *in) {
 int exo_set_step_variant(exo_ctx *c, int32_t variant) {
     if (!c || variant < EXO_STEP_AUTO || variant > EXO_STEP_ROWS_SHARED) return EXO_EINVAL;
     c->step_variant = variant;
+    return EXO_OK;
+}
+
+int exo_set_step_clock(exo_ctx *c, unsigned long long *clock_dev, double *ticks_per_ms) {
+    if (!c) return EXO_EINVAL;
+    c->step_clock = clock_dev;
+    if (ticks_per_ms) {
+        int khz = 0;
+        hipError_t e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device);
+        if (e != hipSuccess || khz <= 0) return check(c, e != hipSuccess ? e : hipErrorInvalidValue, "exo_set_step_clock");
+        *ticks_per_ms = (double)khz;
+    }
     return EXO_OK;
 }
 

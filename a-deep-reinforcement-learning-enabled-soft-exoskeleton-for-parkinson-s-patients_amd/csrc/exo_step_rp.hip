@@ -41,6 +41,9 @@ __device__ unsigned long long *g_exo_stamps;
         if (g_exo_stamps && (threadIdx.x & 63) == __builtin_amdgcn_readfirstlane(threadIdx.x & 63))               \
             g_exo_stamps[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + (k)] = _t;                                                      \
     } while (0)
+// RK45 step attempts (accepted + rejected) of each env's two solves, [2][N]
+// (tools/rk45_hist.py: the configs[3] slowest-env histogram)
+__device__ int32_t *g_exo_rksteps;
 #else
 #define STAMP(k) do {} while (0)
 #endif
@@ -196,7 +199,7 @@ __device__ __forceinline__ double row_acc(const RowM &M, double T, double q, dou
 // scipy RK45 (common.py select_initial_step, rk.py _step_impl) for the row
 // this lane owns; same second-order storage as rk45_solve in exo_model.h.
 template <typename RM>
-__device__ bool rk45_rows(const RM &M, double T, double &q_out) {
+__device__ bool rk45_rows(const RM &M, double T, double &q_out, int &attempts) {
     const double rtol = 1e-3, atol = 1e-6, tb = DT, inv_sqrt14 = 1.0 / 3.7416573867739413;
     double q = 0.0, v = 0.0;
     double a0 = row_acc(M, T, q, v);
@@ -270,6 +273,7 @@ __device__ bool rk45_rows(const RM &M, double T, double &q_out) {
         }
     }
     q_out = ok ? q : NAN;
+    attempts = guard;
     return ok;
 }
 
@@ -509,16 +513,20 @@ __global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
     const double T = (r < 7) ? (grp == 0 ? Ta_r : tr_r) : 0.0;
     double qr;
     bool ok;
+    int attempts = 0;
     if constexpr (PULL == 1) {
-        ok = rk45_rows(RowD{M0, r >= 4}, T, qr);
+        ok = rk45_rows(RowD{M0, r >= 4}, T, qr, attempts);
     } else if constexpr (PULL == 2) {
         __shared__ double2 s_qv[64 * EPB / 4];
         __shared__ double s_rr[64 * EPB / 4];
-        ok = rk45_rows(RowL{M0, s_qv, s_rr, (int)threadIdx.x, (int)(threadIdx.x & ~63u)}, T, qr);
+        ok = rk45_rows(RowL{M0, s_qv, s_rr, (int)threadIdx.x, (int)(threadIdx.x & ~63u)}, T, qr, attempts);
     } else {
-        ok = rk45_rows(M0, T, qr);
+        ok = rk45_rows(M0, T, qr, attempts);
     }
     if (!ok) atomicOr(S.err, 1);
+#ifdef EXO_STAMPS
+    if (g_exo_rksteps && r == 0) g_exo_rksteps[(size_t)grp * N + e] = attempts;
+#endif
     STAMP(4);
     const double qdeg = qr * (180 / PI); // :417-418
     if (info && r < 7) info[(size_t)e * INFO + (grp == 0 ? 14 : 28) + r] = (float)qdeg;
@@ -553,6 +561,9 @@ __global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
 #ifdef EXO_STAMPS
 extern "C" int exo_debug_set_stamps(unsigned long long *buf) {
     return hipMemcpyToSymbol(HIP_SYMBOL(g_exo_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -5;
+}
+extern "C" int exo_debug_set_rksteps(int32_t *buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_exo_rksteps), &buf, sizeof(buf)) == hipSuccess ? 0 : -5;
 }
 #endif
 

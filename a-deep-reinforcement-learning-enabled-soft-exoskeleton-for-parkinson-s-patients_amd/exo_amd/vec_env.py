@@ -227,6 +227,26 @@ class VecExoskeletonEnv:
         nat.check(nat.lib().exo_set_tremor_model(self._ctx, None if j is None else j.ctypes.data_as(nat.P(ctypes.c_double)),
                                                  self.TREMOR_SIGN[sign]), "exo_set_tremor_model", self._ctx)
 
+    def set_step_clock(self, on=True):
+        """Step clock (include/exo_amd.h exo_set_step_clock): every later step
+        launch -- eager or inside a captured graph -- is bracketed by device
+        wall-clock reads on its stream.  Returns the clock tensor (int64 [3]:
+        last start, summed ticks, steps); read it with step_clock_ms()."""
+        if not on:
+            nat.check(nat.lib().exo_set_step_clock(self._ctx, None, None), "exo_set_step_clock", self._ctx)
+            return None
+        self._clock = torch.zeros(3, dtype=torch.int64, device=self.device)
+        rate = ctypes.c_double(0.0)
+        nat.check(nat.lib().exo_set_step_clock(self._ctx, nat.ptr(self._clock), ctypes.byref(rate)),
+                  "exo_set_step_clock", self._ctx)
+        self._clock_rate = rate.value  # ticks per ms
+        return self._clock
+
+    def step_clock_ms(self):
+        """(mean ms per bracketed step launch, steps) of the step clock; synchronises."""
+        _, ticks, n = (int(x) for x in self._clock.cpu())
+        return (ticks / self._clock_rate / n if n else float("nan")), n
+
     # ----------------------------------------------------- physics model
     @staticmethod
     def multibody_params(**overrides):

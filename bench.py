@@ -446,6 +446,10 @@ def main():
         agent = Agent(80, 7, 1, env_num=8, hp=hp, device=dev, precision=args.precision, n_envs=N,
                       process_group=dist.group.WORLD if world > 1 else None, graph_safe=not args.eager)
         trainer = VecTrainer(env, agent, use_graphs=not args.eager)
+    # configs[3] / [4]: the env step inside the timed window itself -- device
+    # wall-clock reads on the step's stream either side of every step launch,
+    # captured into the trainer's graphs with it (exo_set_step_clock)
+    clock = env.set_step_clock() if (trainer is not None and args.workload != "configs1") else None
     out = env.new_outputs(True)
     state = {"k": 0, "obs": env.reset() if trainer is None else None}  # the trainer resets its envs itself
     ev = []
@@ -519,6 +523,34 @@ def main():
         torch.cuda.synchronize()
         return float(np.mean([a.elapsed_time(b) for a, b in evs])), float(min(n, round_len) and N)
 
+    def loop_kernel_timing(n):
+        """The env step kernel on the training loop's own inputs (VERDICT r2 item
+        6): one rollout at a time, eager, exactly as the trainer's rollout branch
+        runs it -- the policy's exploring actions for the current observations,
+        the current active mask, mid-round state, the loop's kernel variant --
+        with HIP events around the step launch on its stream.  After the timed
+        window (it advances the trainer like its own rollouts do, without the
+        TD7 update).  Returns (ms per launch, mean active envs per launch)."""
+        tr = trainer
+        evs, act_n = [], []
+        for _ in range(n):
+            if tr.k == tr.round_len:
+                env.reset(obs_out=tr.obs)
+                tr._round_start()
+            a = agent.select_action_batch(tr.obs, dec_count=tr.active_count)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            nobs, rew, done, _ = env.step(a, active=tr.active, out=tr._outs[tr._cur])
+            e1.record()
+            evs.append((e0, e1))
+            act_n.append(int(tr.active_counts[tr.k]))
+            agent.replay_buffer.add_batch(tr.obs, a, nobs, rew, done, tr.strata, tr.active)
+            tr._advance()
+            tr.k += 1
+            tr._cur ^= 1
+        torch.cuda.synchronize()
+        return float(np.mean([x.elapsed_time(y) for x, y in evs])), float(np.mean(act_n))
+
     for _ in range(args.warmup):
         one_step(False)
     torch.cuda.synchronize()
@@ -526,6 +558,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     resets0 = trainer.resets if trainer is not None else state.get("resets", 0)
+    if clock is not None:
+        clock.zero_()
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
     env_steps = 0
     for _ in range(args.steps):
@@ -536,6 +571,10 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     resets_in_window = (trainer.resets if trainer is not None else state.get("resets", 0)) - resets0
+    window_clock = None
+    if clock is not None:
+        window_clock = env.step_clock_ms()
+        env.set_step_clock(False)
     reset_ms = reset_timing()
     loop_kern_ms = None
     if ev:  # env mode: the timed launches themselves
@@ -545,8 +584,23 @@ def main():
         # profiles/*_env kernel stats time); the trainer runs the rows_shared
         # shape beside the TD7 passes -- timed alone too, reported with it
         nk = min(args.kernel_timing_steps, int(Ls.min()) - 3)
-        kern_ms, kern_active = kernel_timing(nk, "auto")
+        # configs[3] / [4]: one whole round of the loop's launches (every round
+        # position once: the launch time varies ~5x with which stiff
+        # domain-randomised envs are still running, profiles/r03_dr)
+        loop_ms, loop_active = loop_kernel_timing(nk if args.workload == "configs1" else round_len)
+        alone_ms, alone_active = kernel_timing(nk, "auto")
         loop_kern_ms = kernel_timing(nk)[0] if env.step_variant != "auto" else None
+        if args.workload == "configs1":
+            # the driver's line keeps the default shape alone, all envs active
+            # (the launch the committed PMC traffic and the env-mode rocprof
+            # summary describe); the loop's own workload is reported beside it
+            kern_ms, kern_active = alone_ms, alone_active
+        else:
+            # configs[3] / [4]: the loop's own workload in the timed window (a
+            # freshly reset env stepped with U(-1, 1) actions is not what these
+            # loops run, and the slowest domain-randomised env of a round sets
+            # every launch of that round: profiles/r03_dr)
+            kern_ms, kern_active = window_clock[0], env_steps / args.steps
     # Whole-round rate, independent of where the K-iteration window falls in
     # the 344-step episode round: one round = round_len iterations (active
     # env-steps A_round = sum over k of the envs still running) + one reset.
@@ -614,6 +668,22 @@ def main():
                          "bytes_per_env_step": BYTES_PER_ENV_STEP, "avg_kernel_ms": kern_ms,
                          "active_envs_per_launch": active_avg},
         }
+        if ev == [] and agent is not None:
+            res["roofline"]["measured_on"] = ("default shape alone, all envs active, U(-1, 1) actions"
+                                              if args.workload == "configs1" else
+                                              "the timed window's own step launches inside the graph-replayed "
+                                              "training loop: device wall-clock reads either side of each launch "
+                                              "on its stream (exo_set_step_clock), averaged over the window")
+            if window_clock is not None:
+                res["roofline"]["window_step_clock"] = {"avg_ms": window_clock[0], "launches": window_clock[1],
+                                                        "ms_per_iteration": elapsed / args.steps * 1e3}
+            res["roofline"]["loop_workload"] = {
+                "measured_on": "one whole round of rollout launches after the window, eager, HIP events "
+                               "(the round after the window: other domain-randomisation draws)",
+                "avg_kernel_ms": loop_ms, "active_envs_per_launch": loop_active, "variant": env.step_variant,
+                "achieved_gbs": BYTES_PER_ENV_STEP * loop_active / (loop_ms * 1e-3) / 1e9,
+                "frac": BYTES_PER_ENV_STEP * loop_active / (loop_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+            res["roofline"]["alone_default_shape"] = {"avg_kernel_ms": alone_ms, "active_envs_per_launch": alone_active}
         if loop_kern_ms is not None:
             res["roofline"]["training_loop_variant"] = {
                 "variant": env.step_variant, "avg_kernel_ms_alone": loop_kern_ms,

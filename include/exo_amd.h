@@ -122,6 +122,14 @@ int exo_set_state_host(exo_ctx *ctx, int32_t env, const double *in);
 #define EXO_STEP_ROWS_SHARED 3
 int exo_set_step_variant(exo_ctx *ctx, int32_t variant);
 
+/* Step clock (measurement; no reference counterpart): with clock_dev non-NULL
+ * (3 device uint64), every later exo_step -- eager or captured into a graph --
+ * brackets its launches with two one-lane kernels on its stream that read the
+ * device wall clock; clock_dev[1] accumulates the bracketed ticks and
+ * clock_dev[2] counts the steps.  *ticks_per_ms (if non-NULL) receives the
+ * clock rate.  NULL turns it off for later launches. */
+int exo_set_step_clock(exo_ctx *ctx, unsigned long long *clock_dev, double *ticks_per_ms);
+
 /* Tremor model of later resets (diagnostic; the default is the shipped code):
  * jmax7 = joint_max_values before the magnitude (generate_parkinson_tremor.py:59;
  * NULL = the shipped {2.5, 5, 10, 5, 5, 0.5, 0.5}), sign_mode = how
