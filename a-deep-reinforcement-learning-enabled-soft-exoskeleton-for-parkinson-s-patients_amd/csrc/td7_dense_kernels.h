@@ -7,6 +7,7 @@
 
 #include <cstdint>
 #include <cstdlib>
+#include <type_traits>
 
 #include "exo_amd.h"
 
@@ -244,10 +245,16 @@ __global__ __launch_bounds__(64 * NW) void dense_gemm_kernel(GemmArgs a) {
     // summed from the UNROUNDED dP in fp32 here, as the wgrad kernel does, not
     // taken from the rounded MFMA column; bsum[tl] = this lane's part of row
     // i0 + 16 tl + c
-    const bool bias_tile = P != PREC_F32 && a.B.ones_col >= j0 && a.B.ones_col < j0 + 32;
+    // The loop is compiled twice: the workgroups whose tile holds the ones
+    // column (one column of tiles) inject the ones and sum the bias; the rest
+    // run a loop without either (the per-element checks cost 60 % on the wide
+    // configuration's fp16 weight gradients, profiles/r03_wide_summary.md).
+    const bool ones_tile = a.B.ones_col >= j0 && a.B.ones_col < j0 + 32;
+    const bool bias_tile = P != PREC_F32 && ones_tile;
     float bsum[2] = {0.f, 0.f};
 
-    auto load = [&](int grp, Frag &fa, Frag &fy, Frag &fb) {
+    auto load = [&](auto ones, int grp, Frag &fa, Frag &fy, Frag &fb) {
+        constexpr bool ONES = decltype(ones)::value;
 #pragma unroll
         for (int sp = 0; sp < SPG; ++sp) {
             const int k = grp * SPG + sp;           // k-th step of this wave
@@ -261,7 +268,7 @@ __global__ __launch_bounds__(64 * NW) void dense_gemm_kernel(GemmArgs a) {
             if (AG >= 0)
                 load_step<AV>(ry, gg * (int)a.A.ysg, (int)a.A.ysi, (int)a.A.ysr, i0, c, a.I, r0, a.R, q, fy.v[sp], full);
             load_step<BV>(rb, gg * (int)a.B.sg, (int)a.B.si, (int)a.B.sr, j0, c, a.J, r0, a.R, q, fb.v[sp], full);
-            if (a.B.ones_col >= 0) { // bwd-weight: column ones_col of B is all ones (-> bias gradient)
+            if constexpr (ONES) { // bwd-weight: column ones_col of B is all ones (-> bias gradient)
 #pragma unroll
                 for (int tl = 0; tl < 2; ++tl)
                     if (j0 + 16 * tl + c == a.B.ones_col)
@@ -270,7 +277,8 @@ __global__ __launch_bounds__(64 * NW) void dense_gemm_kernel(GemmArgs a) {
             }
         }
     };
-    auto mma = [&](const Frag &fa, const Frag &fy, const Frag &fb) {
+    auto mma = [&](auto ones, const Frag &fa, const Frag &fy, const Frag &fb) {
+        constexpr bool ONES = decltype(ones)::value;
         if constexpr (P != PREC_F32) {
 #pragma unroll
             for (int sp = 0; sp < SPG; ++sp) {
@@ -279,9 +287,14 @@ __global__ __launch_bounds__(64 * NW) void dense_gemm_kernel(GemmArgs a) {
                 for (int tl = 0; tl < 2; ++tl)
 #pragma unroll
                     for (int jj = 0; jj < 4; ++jj) {
-                        const float dp = AG >= 0 ? fa.v[sp][tl][jj] * act_grad_t<AG>(fy.v[sp][tl][jj]) : fa.v[sp][tl][jj];
-                        if (bias_tile) bsum[tl] += dp;
-                        av[tl][jj] = AG >= 0 ? dp * grad_scale<P>() : dp;
+                        if constexpr (ONES) {
+                            const float dp = AG >= 0 ? fa.v[sp][tl][jj] * act_grad_t<AG>(fy.v[sp][tl][jj]) : fa.v[sp][tl][jj];
+                            bsum[tl] += dp;
+                            av[tl][jj] = AG >= 0 ? dp * grad_scale<P>() : dp;
+                        } else { // (x g) 2^10 == x (g 2^10): the scale folds into act'
+                            av[tl][jj] = AG >= 0 ? fa.v[sp][tl][jj] * (act_grad_t<AG>(fy.v[sp][tl][jj]) * grad_scale<P>())
+                                                 : fa.v[sp][tl][jj];
+                        }
                     }
 #pragma unroll
                 for (int x = 0; x < 2; ++x)
@@ -305,15 +318,19 @@ __global__ __launch_bounds__(64 * NW) void dense_gemm_kernel(GemmArgs a) {
                         acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[x], fb.v[sp][y][jj], acc[x][y], 0, 0, 0);
             }
     };
-    Frag a0, y0, b0, a1, y1, b1;
-    if (ngrp > 0) load(0, a0, y0, b0);
-    for (int grp = 0; grp < ngrp; grp += 2) {
-        if (grp + 1 < ngrp) load(grp + 1, a1, y1, b1);
-        mma(a0, y0, b0);
-        if (grp + 1 >= ngrp) break;
-        if (grp + 2 < ngrp) load(grp + 2, a0, y0, b0);
-        mma(a1, y1, b1);
-    }
+    auto run = [&](auto ones) {
+        Frag a0, y0, b0, a1, y1, b1;
+        if (ngrp > 0) load(ones, 0, a0, y0, b0);
+        for (int grp = 0; grp < ngrp; grp += 2) {
+            if (grp + 1 < ngrp) load(ones, grp + 1, a1, y1, b1);
+            mma(ones, a0, y0, b0);
+            if (grp + 1 >= ngrp) break;
+            if (grp + 2 < ngrp) load(ones, grp + 2, a0, y0, b0);
+            mma(ones, a1, y1, b1);
+        }
+    };
+    if (ones_tile) run(std::true_type{});
+    else run(std::false_type{});
     if (bias_tile)
 #pragma unroll
         for (int tl = 0; tl < 2; ++tl) {

@@ -317,3 +317,51 @@ def test_tremor_model_knob(model):
             mx = env.tremor(e).max(axis=1)
             mag = 0.9 + draws[e][0] * 0.2
             np.testing.assert_allclose(mx[seq == 1], (J * mag)[seq == 1], rtol=1e-12)
+
+
+def test_step_clock_brackets_every_step_launch():
+    """exo_set_step_clock (bench.py's in-window env-step time for configs[3] /
+    [4]): counts every step launch, eager and graph-replayed, measures a
+    positive time no longer than the HIP-event time around the same launches,
+    leaves the step's outputs unchanged, and stops counting when turned off."""
+    from exo_amd import VecExoskeletonEnv
+    n = 64
+    outs = []
+    for clocked in (False, True):
+        env = VecExoskeletonEnv(n, seed=5)
+        env.reset()
+        clk = env.set_step_clock() if clocked else None
+        g = torch.Generator(device="cuda").manual_seed(9)
+        obs = []
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            act = torch.rand((n, 7), device="cuda", generator=g) * 2 - 1
+            obs.append(env.step(act)[0].clone())
+        e1.record()
+        torch.cuda.synchronize()
+        outs.append(torch.stack(obs))
+        if clocked:
+            ms, cnt = env.step_clock_ms()
+            assert cnt == 5 and 0 < ms <= e0.elapsed_time(e1) / 5 * 1.05
+            # captured: the clock kernels replay with the step
+            act = torch.zeros((n, 7), device="cuda")
+            o = env.new_outputs(True)
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph, stream=s):
+                    env.step(act, out=o)
+            torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+            base = int(clk[2])
+            for _ in range(3):
+                graph.replay()
+            torch.cuda.synchronize()
+            assert int(clk[2]) == base + 3
+            env.set_step_clock(False)
+            env.step(act)
+            torch.cuda.synchronize()
+            assert int(clk[2]) == base + 3
+    torch.testing.assert_close(outs[0], outs[1], rtol=0, atol=0)

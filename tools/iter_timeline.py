@@ -17,7 +17,9 @@ def main(path, verbose=False):
     ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r["Queue_Id"]) for r in rows))
     steps = [i for i, k in enumerate(ks) if "exo_step" in k[2]]
     # training iterations (the bench's kernel-timing phase launches the step kernel alone)
-    pairs = [(a, b) for a, b in zip(steps[:-1], steps[1:]) if b - a > 20][-6:-1]
+    # (graph-replayed iterations: a TD7 pass between two step launches, under 2 ms)
+    pairs = [(a, b) for a, b in zip(steps[:-1], steps[1:]) if b - a > 10
+             and any("encoder_kernel" in k[2] for k in ks[a:b]) and ks[b][0] - ks[a][0] < 2_000_000][-6:-1]
     spans = []
     for a, b in pairs:
         it = ks[a:b]
