@@ -37,6 +37,10 @@ extern template void launch_fwd_lds_p<PREC_BF16, false>(const GemmArgs &, dim3, 
 extern template void launch_fwd_lds_p<PREC_F16, false>(const GemmArgs &, dim3, int, hipStream_t);
 extern template void launch_fwd_lds_p<PREC_BF16, true>(const GemmArgs &, dim3, int, hipStream_t);
 extern template void launch_fwd_lds_p<PREC_F16, true>(const GemmArgs &, dim3, int, hipStream_t);
+extern template void launch_fwd_big_p<PREC_BF16, false>(const GemmArgs &, dim3, int, hipStream_t);
+extern template void launch_fwd_big_p<PREC_F16, false>(const GemmArgs &, dim3, int, hipStream_t);
+extern template void launch_fwd_big_p<PREC_BF16, true>(const GemmArgs &, dim3, int, hipStream_t);
+extern template void launch_fwd_big_p<PREC_F16, true>(const GemmArgs &, dim3, int, hipStream_t);
 TD7_EXTERN(PREC_F32)
 TD7_EXTERN(PREC_BF16)
 TD7_EXTERN(PREC_F16)
@@ -105,6 +109,43 @@ int launch_fwd(const GemmArgs &a, int groups_grid, int prec, hipStream_t s, bool
         const char *e = std::getenv("EXO_FWD_LDS");
         return !(e && e[0] == '0');
     }();
+    // the largest layers: 256 x 128 tiles and 16x16x32 MFMAs (dense_fwd_big_kernel)
+    // when they number >= 256 and the operands allow 16-byte chunks of 8
+    // (K % 8, rows 16-byte aligned; CAT boundaries at multiples of 64);
+    // EXO_FWD_BIG=0 disables it
+    static const bool big_on = [] {
+        const char *e = std::getenv("EXO_FWD_BIG");
+        return !(e && e[0] == '0');
+    }();
+    // tile 128 x 256 (half the re-reads of X of 256 x 128: 419 vs 429 us at
+    // 65,536 x 1,024 x 1,024, 692 vs 746 on [a | zs]; EXO_FWD_BIG=2 picks 256 x 128)
+    static const int big_bm = [] {
+        const char *e = std::getenv("EXO_FWD_BIG");
+        return (e && e[0] == '2') ? 256 : 128;
+    }();
+    const int big_bn = big_bm == 256 ? 128 : 256;
+    const long tbig = (long)((a.I + big_bm - 1) / big_bm) * ((a.J + big_bn - 1) / big_bn) * groups_grid;
+    auto al16 = [](const void *p) { return ((uintptr_t)p & 15) == 0; };
+    bool big = prec != PREC_F32 && big_on && tbig >= 256 && a.R >= 256 && a.R % 8 == 0 && a.J >= 128 &&
+               a.B.si % 4 == 0 && a.B.sg % 4 == 0 && al16(a.B.p);
+    if (big && cat) {
+        for (int sg = 0; sg < CAT_MAX && a.cat.kb[sg] < a.R; ++sg)
+            big = big && a.cat.kb[sg] % BIG_BK == 0 && a.cat.ld[sg] % 4 == 0 && a.cat.sg[sg] % 4 == 0 &&
+                  al16(a.cat.p[sg]);
+    } else if (big) {
+        big = a.A.si % 4 == 0 && a.A.sg % 4 == 0 && al16(a.A.p);
+    }
+    if (big) {
+        dim3 grid((a.J + big_bn - 1) / big_bn, (a.I + big_bm - 1) / big_bm, groups_grid);
+        if (cat) {
+            if (prec == PREC_BF16) launch_fwd_big_p<PREC_BF16, true>(a, grid, big_bm, s);
+            else launch_fwd_big_p<PREC_F16, true>(a, grid, big_bm, s);
+        } else {
+            if (prec == PREC_BF16) launch_fwd_big_p<PREC_BF16, false>(a, grid, big_bm, s);
+            else launch_fwd_big_p<PREC_F16, false>(a, grid, big_bm, s);
+        }
+        return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
+    }
     const long t64 = (long)((a.I + 63) / 64) * ((a.J + 63) / 64) * groups_grid;
     if (prec != PREC_F32 && lds_on && a.J >= 64 && ((t64 >= 256 && a.R >= 256) || (t64 >= 2048 && a.R >= 64))) {
         const long t128 = (long)((a.I + 127) / 128) * ((a.J + 127) / 128) * groups_grid;

@@ -11,4 +11,6 @@ template void launch_fwd_norm_p<PREC_BF16, false>(const GemmArgs &, dim3, float 
 template void launch_fwd_norm_p<PREC_BF16, true>(const GemmArgs &, dim3, float *, float *, float, hipStream_t);
 template void launch_fwd_lds_p<PREC_BF16, false>(const GemmArgs &, dim3, int, hipStream_t);
 template void launch_fwd_lds_p<PREC_BF16, true>(const GemmArgs &, dim3, int, hipStream_t);
+template void launch_fwd_big_p<PREC_BF16, false>(const GemmArgs &, dim3, int, hipStream_t);
+template void launch_fwd_big_p<PREC_BF16, true>(const GemmArgs &, dim3, int, hipStream_t);
 } // namespace td7dense

@@ -954,6 +954,191 @@ void launch_fwd_lds_p(const GemmArgs &a, dim3 grid, int bm, hipStream_t s) {
 #undef FWD_LDS
 }
 
+// ---- forward of the largest layers: 128 x 256 tiles, 16x16x32 MFMA ----------
+// Y = act(X W^T + b) where the output tiles number >= 256 and K is a multiple
+// of 8 (the wide configuration's update at 8 x 1,024 rows and its policy over
+// 65,536 envs: M = 8,192-65,536, N = 1,024, K = 1,024-3,072).
+// dense_fwd_lds_kernel above stages 32-deep slices for 16x16x16 MFMAs from
+// 8-byte LDS reads; here a 512-thread workgroup (8 waves, each a 64 x 64
+// sub-tile of 4 x 4 accumulators) stages 64-deep slices: every thread loads 6
+// chunks of 8 consecutive fp32 (two 16-byte buffer loads each) of the tile's
+// X and W rows, rounds them to 16-bit and writes one 16-byte LDS store per
+// chunk; each wave reads its A and B fragments as ds_read_b128 (4 + 4 per
+// 32-deep step) for 16 v_mfma_f32_16x16x32 (twice the K of the 16x16x16 form).
+// The chunk column of row r is stored at (chunk ^ ((r >> 1) & 7)): the
+// fragment reads of every ds_read_b128 lane group (MI355X_MICROARCH.md, LDS
+// table) then hit 16 distinct 16-byte bank quads.  The next slice's global
+// loads are in flight under the current slice's MFMAs (two LDS buffers, one
+// barrier per slice); workgroups go to the XCDs in runs of consecutive tiles
+// (xcd_tile), so the column tiles of one row block of X share an L2.  CAT
+// operands need segment boundaries at multiples of 64 (a slice then lies in
+// one segment).  Same products and fp32 accumulation as the other forward
+// kernels; the summation order differs (K in 32-steps).  Measured
+// (profiles/r03_big_raw): 1.1-1.6x the LDS kernel on the concatenated
+// layers, level at 65,536 x 1,024 x 1,024 -- ~390-500 TF/s, bound by the
+// fp32 operands' load latency with one slice in flight (~2.7 us per 64-deep
+// slice at 8,192 rows; a second register set spills).
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 halfx8_t __attribute__((ext_vector_type(8)));
+
+template <int P>
+__device__ __forceinline__ uint32_t pack_h2(float lo, float hi) {
+    return (uint32_t)to_half_bits<P>(lo) | ((uint32_t)to_half_bits<P>(hi) << 16);
+}
+
+template <int P>
+__device__ __forceinline__ floatx4 mfma_k32(uint32_t4 a, uint32_t4 b, floatx4 c) {
+    if constexpr (P == PREC_F16)
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(halfx8_t, a), __builtin_bit_cast(halfx8_t, b),
+                                                      c, 0, 0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
+                                                       c, 0, 0, 0);
+}
+
+constexpr int BIG_BK = 64, BIG_CH = BIG_BK / 8;
+
+template <int EP, int P, bool CAT, int BM, int BN>
+__global__ __launch_bounds__(512) void dense_fwd_big_kernel(GemmArgs a) {
+    constexpr int BK = BIG_BK, CH = BIG_CH, WN = BN / 64;
+    constexpr int AC = BM * CH / 512, BC = BN * CH / 512; // chunks per thread per slice
+    __shared__ uint32_t4 As[2][BM * CH];
+    __shared__ uint32_t4 Bs[2][BN * CH];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, q = lane >> 4, c = lane & 15;
+    const int wm = w / WN, wn = w % WN;
+    const int3 tile = xcd_tile();
+    const int i0 = tile.y * BM, j0 = tile.x * BN, g = tile.z;
+    const int K = a.R, nk = (K + BK - 1) / BK;
+    const int lr = t >> 3, lc = t & 7; // this thread's chunks: rows lr + 64 j, chunk column lc
+    const __amdgpu_buffer_rsrc_t rb = rsrc(a.B.p + g * a.B.sg);
+    __amdgpu_buffer_rsrc_t ra = rsrc(CAT ? a.cat.p[0] : a.A.p + g * a.A.sg);
+    int lda = CAT ? a.cat.ld[0] : (int)a.A.si, kbase = 0, seg = 0;
+    uint32_t4 xa[AC][2], xb[BC][2];
+    auto gload = [&](int kt) {
+        const int k0 = kt * BK;
+        if constexpr (CAT) { // the slice's segment (boundaries are multiples of BK)
+            const int s = cat_seg(a.cat, k0);
+            if (s != seg || kt == 0) {
+                seg = s;
+                const float *p = a.cat.p[0];
+                long gs = a.cat.sg[0];
+                int ld = a.cat.ld[0], kb = 0;
+#pragma unroll
+                for (int m = 1; m < CAT_MAX; ++m)
+                    if (s == m) p = a.cat.p[m], gs = a.cat.sg[m], ld = a.cat.ld[m], kb = a.cat.kb[m];
+                ra = rsrc(p + g * gs);
+                lda = ld;
+                kbase = kb;
+            }
+        }
+        const int k = k0 + 8 * lc;
+        const bool kin = k < K;
+#pragma unroll
+        for (int j = 0; j < AC; ++j) {
+            const int row = i0 + lr + 64 * j;
+            const int off = (row * lda + k - kbase) * 4;
+            const bool ok = kin & (row < a.I);
+            xa[j][0] = __builtin_amdgcn_raw_buffer_load_b128(ra, ok ? off : BUF_OOB, 0, 0);
+            xa[j][1] = __builtin_amdgcn_raw_buffer_load_b128(ra, ok ? off + 16 : BUF_OOB, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < BC; ++j) {
+            const int col = j0 + lr + 64 * j;
+            const int off = (col * (int)a.B.si + k) * 4;
+            const bool ok = kin & (col < a.J);
+            xb[j][0] = __builtin_amdgcn_raw_buffer_load_b128(rb, ok ? off : BUF_OOB, 0, 0);
+            xb[j][1] = __builtin_amdgcn_raw_buffer_load_b128(rb, ok ? off + 16 : BUF_OOB, 0, 0);
+        }
+    };
+    auto cvt = [&](const uint32_t4 (&v)[2]) {
+        uint32_t4 h;
+        h[0] = pack_h2<P>(__uint_as_float(v[0][0]), __uint_as_float(v[0][1]));
+        h[1] = pack_h2<P>(__uint_as_float(v[0][2]), __uint_as_float(v[0][3]));
+        h[2] = pack_h2<P>(__uint_as_float(v[1][0]), __uint_as_float(v[1][1]));
+        h[3] = pack_h2<P>(__uint_as_float(v[1][2]), __uint_as_float(v[1][3]));
+        return h;
+    };
+    auto lwrite = [&](int buf) {
+#pragma unroll
+        for (int j = 0; j < AC; ++j) {
+            const int r = lr + 64 * j;
+            As[buf][r * CH + (lc ^ ((r >> 1) & 7))] = cvt(xa[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < BC; ++j) {
+            const int r = lr + 64 * j;
+            Bs[buf][r * CH + (lc ^ ((r >> 1) & 7))] = cvt(xb[j]);
+        }
+    };
+    floatx4 acc[4][4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[x][y] = floatx4{0.f, 0.f, 0.f, 0.f};
+    auto compute = [&](int buf) {
+#pragma unroll
+        for (int s = 0; s < BK / 32; ++s) {
+            const int kc = 4 * s + q;
+            uint32_t4 af[4], bf[4];
+#pragma unroll
+            for (int x = 0; x < 4; ++x) {
+                const int r = wm * 64 + 16 * x + c;
+                af[x] = As[buf][r * CH + (kc ^ ((r >> 1) & 7))];
+            }
+#pragma unroll
+            for (int y = 0; y < 4; ++y) {
+                const int r = wn * 64 + 16 * y + c;
+                bf[y] = Bs[buf][r * CH + (kc ^ ((r >> 1) & 7))];
+            }
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int y = 0; y < 4; ++y) acc[x][y] = mfma_k32<P>(af[x], bf[y], acc[x][y]);
+        }
+    };
+    // (a second register set two slices ahead spills at 256 VGPRs: measured
+    // per slice ~2.7 us at 8,192 rows, the loads' latency -- see DESIGN)
+    gload(0);
+    lwrite(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        if (kt + 1 < nk) gload(kt + 1);
+        compute(kt & 1);
+        if (kt + 1 < nk) lwrite((kt + 1) & 1);
+        __syncthreads();
+    }
+    // acc[x][y][i] is C[i0 + 64 wm + 16x + 4q + i][j0 + 64 wn + 16y + c]
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+        const int col = j0 + wn * 64 + 16 * y + c;
+        if (col >= a.J) continue;
+        const float bv = a.bias ? a.bias[g * a.bsg + col] : 0.f;
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = i0 + wm * 64 + 16 * x + 4 * q + i;
+                if (row < a.I) a.C[g * a.csg + (long)row * a.csi + (long)col * a.csj] = act_fwd_t<EP>(acc[x][y][i] + bv);
+            }
+    }
+}
+
+template <int P, bool CAT>
+void launch_fwd_big_p(const GemmArgs &a, dim3 grid, int bm, hipStream_t s) {
+#define FWD_BIG(EPv)                                                                                               \
+    do {                                                                                                         \
+        if (bm == 256) hipLaunchKernelGGL((dense_fwd_big_kernel<EPv, P, CAT, 256, 128>), grid, dim3(512), 0, s, a); \
+        else hipLaunchKernelGGL((dense_fwd_big_kernel<EPv, P, CAT, 128, 256>), grid, dim3(512), 0, s, a);           \
+    } while (0)
+    switch (a.act) {
+    case ACT_RELU: FWD_BIG(ACT_RELU); break;
+    case ACT_ELU: FWD_BIG(ACT_ELU); break;
+    case ACT_TANH: FWD_BIG(ACT_TANH); break;
+    default: FWD_BIG(ACT_NONE); break;
+    }
+#undef FWD_BIG
+}
+
 // ---- bwd-weight on the output-contiguous layout ------------------------------
 // dW[g][i][j] = sum_m dP[m][i] X[m][j], dP = dY * act'(Y), db[g][i] = sum_m dP[m][i].
 // Both operands are contiguous along the OUTPUT dimensions (i resp. j) and

@@ -428,3 +428,35 @@ def test_wide_critic_concat_layer_fp16(m):
         scale = max(1.0, float(r.abs().max()))
         tol = 1e-5 if name == "db" else 1e-4
         torch.testing.assert_close(got[name].double(), r, rtol=tol, atol=tol * scale, msg=name)
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+@pytest.mark.parametrize("g,m,n,k,cat", [(1, 8200, 1000, 1032, False), (2, 8192, 1024, 3072, True),
+                                         (1, 16384, 1024, 2048, True), (1, 8192, 1024, 1000, True),
+                                         (2, 4100, 520, 1024, False)])
+def test_big_forward_kernel_is_the_gemm_of_rounded_operands(prec, g, m, n, k, cat):
+    """The 256 x 128-tile forward (dense_fwd_big_kernel: >= 256 such tiles, K %
+    8 == 0; the wide configuration's update at 8 x 1,024 rows and its policy
+    over 65,536 envs): ragged M, N and K (K = 1,032: a partial 64-deep slice),
+    two groups, concatenated inputs with 64-aligned boundaries ([q | zsa | zs],
+    [a | zs]) and one with a boundary at 384 + 616 (k = 1,000: not 64-aligned,
+    the dispatcher keeps the LDS kernel) -- the GEMM of the operands rounded
+    to 16 bits with fp32 accumulation, ELU epilogue."""
+    from exo_amd import ops
+    torch.manual_seed(m + n + k + g)
+    dt = _ROUND[prec]
+    w = torch.randn(g, n, k, device="cuda") / k ** 0.5 if g > 1 else torch.randn(n, k, device="cuda") / k ** 0.5
+    b = torch.randn(g, n, device="cuda") if g > 1 else torch.randn(n, device="cuda")
+    if cat:
+        widths = [k // 3] * 3 if k == 3072 else ([k // 2] * 2 if k == 2048 else [384, k - 384])
+        parts = [torch.randn(g, m, widths[0], device="cuda") if g > 1 else torch.randn(m, widths[0], device="cuda")]
+        parts += [torch.randn(m, wd, device="cuda") for wd in widths[1:]]
+        with ops.matrix_precision(prec):
+            y = ops.dense_cat(parts, w, b, 2)
+        x = torch.cat([parts[0]] + [p.expand(g, m, p.shape[-1]) if g > 1 else p for p in parts[1:]], -1)
+    else:
+        x = torch.randn(g, m, k, device="cuda") if g > 1 else torch.randn(m, k, device="cuda")
+        with ops.matrix_precision(prec):
+            y = ops.dense(x, w, b, 2)
+    ref = torch.nn.functional.elu(x.to(dt).float() @ w.to(dt).float().transpose(-1, -2) + b.unsqueeze(-2))
+    torch.testing.assert_close(y, ref.reshape(y.shape), rtol=1e-4, atol=1e-4)
