@@ -53,6 +53,32 @@ BYTES_PER_ENV_STEP = sum(STEP_READ_BYTES.values()) + sum(STEP_WRITE_BYTES.values
 
 
 FP64_VALU_PEAK_TFS = 78.6   # MI355X fp64 vector peak (AMD spec)
+
+# Useful fp64 flops of one env step: the step's arithmetic done once per env
+# by a scalar (one-lane) implementation of the kernel's algorithm, as opposed
+# to the PMC count of issued lane-flops (16 lanes per env, the FK on every
+# lane, a pad row per 8-lane group).  Counted by hand from csrc/exo_step_rp.hip
+# (a flop per add / mul / div, 2 per FMA, sqrt / exp / sincos polynomials as
+# their flops):
+#   RHS a = I^-1 (T - D v - K q): D and K 21 nonzeros (42 + 42), T - dq - kq 14,
+#     I^-1 25 nonzeros (50)                                          -> 148
+#   one RK45 step attempt: 6 RHS 888, stage sums 665 (7 rows x sum over
+#     stages 1..5 of 4 st + 7), solution 182, error terms 224, norm 31,
+#     step control 10                                                -> 2,000
+#   per solve: scipy's initial step (2 RHS + norms)                  -> 385
+#   FK 506, 7 actuators 567, torque sums 16, reward 180, observation 30,
+#     joint targets 30                                               -> 1,329
+# useful = 2 x 385 + attempts x 2,000 + 1,329, attempts = the env's actuated +
+# tremor-only step attempts (accepted + rejected), measured in the loop by
+# tools/rk45_hist.py (profiles/r03_dr_raw/rk45_hist_configs1.json).
+USEFUL_FLOPS = {"rhs": 148, "attempt": 2000, "initial_step": 385, "non_ode": 1329}
+
+
+def useful_fp64_flops_per_env_step():
+    f = os.path.join(REPO, "profiles", "r03_dr_raw", "rk45_hist_configs1.json")
+    att = sum(json.load(open(f))["actuated_vs_tremor_only_mean"])
+    return (2 * USEFUL_FLOPS["initial_step"] + att * USEFUL_FLOPS["attempt"] + USEFUL_FLOPS["non_ode"],
+            att, os.path.relpath(f, REPO))
 FP32_MFMA_PEAK_TFS = 157.3  # v_mfma_f32_*_f32 dense peak (MI355X_MICROARCH.md)
 BF16_MFMA_PEAK_TFS = 2500.0  # bf16 / fp16 dense MFMA peak (MI355X_MICROARCH.md, no sparsity)
 MFMA_PEAK_TFS = {"fp32": FP32_MFMA_PEAK_TFS, "bf16": BF16_MFMA_PEAK_TFS, "fp16": BF16_MFMA_PEAK_TFS}
@@ -696,7 +722,16 @@ def main():
             res["valu_roofline"] = {"kernel": res["roofline"]["kernel"], "bound": "valu",
                                     "achieved": vfl / (kern_ms * 1e-3) / 1e12, "peak": FP64_VALU_PEAK_TFS,
                                     "unit": "TFLOP/s (fp64)", "frac": vfl / (kern_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFS,
-                                    "flops_per_launch": vfl, "flops_source": vsrc}
+                                    "flops_per_launch": vfl, "flops_source": vsrc,
+                                    "flops_kind": "issued lane-flops (PMC, every lane of the wave)"}
+            if args.workload == "configs1":
+                uf, att, usrc = useful_fp64_flops_per_env_step()
+                ua = uf * N / (kern_ms * 1e-3) / 1e12
+                res["valu_roofline"]["useful"] = {
+                    "flops_per_env_step": uf, "achieved": ua, "frac": ua / FP64_VALU_PEAK_TFS,
+                    "issued_over_useful": vfl / (uf * N), "rk45_attempts_per_env_step": att, "attempts_source": usrc,
+                    "model": "bench.py USEFUL_FLOPS: the step's arithmetic once per env (a scalar implementation "
+                             "of the kernel's algorithm), counted by hand"}
         if args.physics == "multibody":
             # q, qd of 19 joints read + written (f64), 5 targets, 1 flag byte read + cleared
             mb_ms = multibody_timing()
