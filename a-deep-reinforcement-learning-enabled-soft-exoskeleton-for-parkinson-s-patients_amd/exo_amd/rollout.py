@@ -318,12 +318,18 @@ class VecTrainer:
     # (before the next sample).  Data-parallel runs keep it in place (the MAX
     # all-reduce of max_priority follows it).  EXO_PRIO_BRANCH=0 serialises.
     prio_branch = os.environ.get("EXO_PRIO_BRANCH", "1") == "1"
+    # r03: only when this iteration also updates the actor (the branch then
+    # runs beside the actor's passes); otherwise the update and the next
+    # sample follow the critic's weight gradients on the iteration's stream,
+    # with no cross-queue hand-off on the critical path (EXO_PRIO_BRANCH_ALL=1:
+    # the branch in every iteration, the r02 layout)
+    prio_branch_all = os.environ.get("EXO_PRIO_BRANCH_ALL", "0") == "1"
 
     def _mid(self, update_actor, flat_grad=None, grad_scale=1.0, rollout=True):
         ag = self.agent
         self._pside = None
         self._mid_rollout = rollout
-        if self.prio_branch and not self.dp:
+        if self.prio_branch and not self.dp and (update_actor or self.prio_branch_all):
             cur = torch.cuda.current_stream(self.device)
             if getattr(self, "_prio_stream", None) is None:
                 self._prio_stream = torch.cuda.Stream(device=self.device)

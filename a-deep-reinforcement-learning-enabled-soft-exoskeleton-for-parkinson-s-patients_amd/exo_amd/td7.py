@@ -34,6 +34,11 @@ from . import _native as nat
 from . import ops
 from .ops import avg_l1_norm
 
+# fused schedule variant (r03, off): the critic target chain on the update's
+# own stream and the fixed embeddings on a branch, so the critic's join waits
+# on a branch that finished early -- measured 307 vs 304 us per iteration
+# (profiles/r03_sched_raw/ab.txt); EXO_TD7_TARGET_ON_MAIN=1 turns it on
+TARGET_ON_MAIN = os.environ.get("EXO_TD7_TARGET_ON_MAIN", "0") == "1"
 # fused optimiser step + weight repack (td7f_adam_pack); EXO_ADAM_PACK=0: two launches
 ADAM_PACK = os.environ.get("EXO_ADAM_PACK", "1") != "0"
 # graph-replayed trainer on one GPU, fused: the encoder's weight gradients and
@@ -729,26 +734,48 @@ class TD7Learner:
                     and isinstance(self.encoder_optimizer, FlatAdam))
         wg_adam = enc_step and WGRAD_ADAM and tr.fuses_adam()
         self._enc_step_pending = False
-        if branch:
-            side, tside = stream("_side"), stream("_tside")
+        self._actor_fused_pre = False
+        if branch and TARGET_ON_MAIN:
+            # the critic target chain (target_a -> target_b, the longest branch
+            # before the critic) on the iteration's own stream, the fixed
+            # embeddings beside it: the critic's join then waits on a branch
+            # that finished long before (a satisfied cross-queue wait) instead
+            # of putting a cross-queue hand-off on the critical path
+            side, fside = stream("_side"), stream("_fside")
             with torch.cuda.stream(side):
                 tr.encoder(state, action, next_state)
                 if enc_step:
                     tr.wgrad_encoder(adam=wg_adam)
-            with torch.cuda.stream(tside):
-                qt = fz.target_heads(next_state, noise)
-        else:
-            tr.encoder(state, action, next_state)
+            with torch.cuda.stream(fside):
+                zs, zsa = fz.fixed(state, action)
+            if self.prefetch_actor and self.actor_branch:
+                aside = stream("_aside")
+                aside.wait_stream(fside)
+                with torch.cuda.stream(aside):
+                    tr.actor(0, state, zs)
+                self._actor_fused_pre = True
             qt = fz.target_heads(next_state, noise)
-        zs, zsa = fz.fixed(state, action)
-        self._actor_fused_pre = False
-        if branch and self.prefetch_actor and self.actor_branch:
-            aside = stream("_aside")
-            with torch.cuda.stream(aside):
-                tr.actor(0, state, zs)
-            self._actor_fused_pre = True
-        if branch:
-            cur.wait_stream(tside)
+            cur.wait_stream(fside)
+        else:
+            if branch:
+                side, tside = stream("_side"), stream("_tside")
+                with torch.cuda.stream(side):
+                    tr.encoder(state, action, next_state)
+                    if enc_step:
+                        tr.wgrad_encoder(adam=wg_adam)
+                with torch.cuda.stream(tside):
+                    qt = fz.target_heads(next_state, noise)
+            else:
+                tr.encoder(state, action, next_state)
+                qt = fz.target_heads(next_state, noise)
+            zs, zsa = fz.fixed(state, action)
+            if branch and self.prefetch_actor and self.actor_branch:
+                aside = stream("_aside")
+                with torch.cuda.stream(aside):
+                    tr.actor(0, state, zs)
+                self._actor_fused_pre = True
+            if branch:
+                cur.wait_stream(tside)
         tr.critic(state, action, zs, zsa, qt, reward, not_done)
         if enc_step:
             priority = tr.wgrad_critic(adam=wg_adam)
