@@ -498,7 +498,7 @@ class RefScheduleTrainer(VecTrainer):
     from injected draw streams) instead of exo_reset."""
 
     def __init__(self, env, agent, warmup=25_000, strata=None, use_graphs=True, ref_replay=True,
-                 action_source=None, reset_source=None, warmup_eager=2):
+                 action_source=None, reset_source=None, warmup_eager=2, round_graph=None):
         super().__init__(env, agent, strata=strata, use_graphs=use_graphs, warmup_eager=warmup_eager,
                          shared_step=False)
         # the rollout runs alone (no TD7 pass beside it): the env step's own fast shape
@@ -522,9 +522,32 @@ class RefScheduleTrainer(VecTrainer):
         self._train_iters = 0
         self._roll_iters = 0
         self.trace = []
+        # one graph per rollout round (round_graph): the round's steps replayed
+        # as one graph, each step's replay insert on a branch beside the next
+        # step's select_action (joined before that step's env step, which
+        # overwrites the observation buffer the insert reads); the insert's
+        # active mask comes from a per-parity copy (the step's own mask is
+        # advanced in place for the next step)
+        # off by default: measured no faster (40.0-40.4 vs 39.4-39.5 ms per
+        # 4,096-env rollout round, profiles/r03_refsched_raw): the select_action
+        # workgroups hold every CU, so the overlapped insert kernels wait for
+        # CUs (lap_add 9 -> 34 us) and the next env step waits for them
+        if round_graph is None:  # EXO_REF_ROUND_GRAPH=1: the round graph
+            round_graph = os.environ.get("EXO_REF_ROUND_GRAPH", "0") == "1"
+        self.round_graph = bool(round_graph)
+        self._ins_stream = None
+        self._ins_pending = False
+        self._act_prev = torch.zeros((2, self.n), dtype=torch.bool, device=dev)
+        self._round_graphs = {}
+        self._eager_kinds = set()
 
     # ------------------------------------------------------------ rollout
-    def _rollout_ref(self, random, injected=False):
+    def _seen_eager(self, random):
+        """A round graph is captured only after a per-step round of the same
+        kind (random / policy) allocated its buffers."""
+        return bool(random) in self._eager_kinds
+
+    def _rollout_ref(self, random, injected=False, overlap=False):
         ag = self.agent
         obs = self.obs
         if injected:
@@ -533,12 +556,52 @@ class RefScheduleTrainer(VecTrainer):
             act = self._rand_act.uniform_(-1.0, 1.0)
         else:
             act = ag.select_action_batch(obs, dec_count=self.active_count)
+        cur = torch.cuda.current_stream(self.device) if overlap else None
+        if self._ins_pending:  # the previous step's insert reads the buffer this step overwrites
+            cur.wait_stream(self._ins_stream)
+            self._ins_pending = False
         nobs, rew, done, info = self.env.step(act, active=self.active, out=self._outs[self._cur])
-        self.score.add_(torch.where(self.active, rew.double(), 0.0))  # :144
+        self.score.add_(rew.where(self.active, 0.0))  # :144 (float32 into the float64 score, 2 launches)
         add = ag.replay_buffer.add_batch_ref if self.ref_replay else ag.replay_buffer.add_batch
-        add(obs, act, nobs, rew, done, self.strata, self.active)  # :142
+        if overlap:
+            mask = self._act_prev[self._cur]
+            mask.copy_(self.active)
+            if self._ins_stream is None:
+                self._ins_stream = torch.cuda.Stream(device=self.device)
+            self._ins_stream.wait_stream(cur)
+            with torch.cuda.stream(self._ins_stream):
+                add(obs, act, nobs, rew, done, self.strata, mask)  # :142
+            self._ins_pending = True
+        else:
+            add(obs, act, nobs, rew, done, self.strata, self.active)  # :142
         self._advance()
         self.last_actions = act
+
+    def _roll_round(self, random):
+        """The whole rollout of a round (round_len steps) as one graph replay,
+        captured on first use per (random, starting observation parity)."""
+        key = ("round", bool(random), self._cur)
+        g = self._round_graphs.get(key)
+        if g is None:
+            s = torch.cuda.Stream(device=self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            g = torch.cuda.CUDAGraph()
+            cur0 = self._cur
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s), ForkJoinAudit(s):
+                    for _ in range(self.round_len):
+                        self._rollout_ref(random, overlap=True)
+                        self._cur ^= 1
+                    if self._ins_pending:
+                        s.wait_stream(self._ins_stream)
+                        self._ins_pending = False
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            self._cur = cur0
+            self._round_graphs[key] = g
+        g.replay()
+        self._roll_iters += self.round_len
+        self.k += self.round_len
+        self._cur ^= self.round_len & 1
 
     def _roll_step(self, random):
         if self.action_source is not None:
@@ -597,8 +660,13 @@ class RefScheduleTrainer(VecTrainer):
         self.score.fill_(2.0)  # reset() returns (obs, counts = 2) into score[i] (:112)
         self._round_start()
         random = not self.allow_train
-        for _ in range(self.round_len):
-            self._roll_step(random)
+        if (self.round_graph and self.use_graphs and self.action_source is None
+                and self._roll_iters >= max(self.warmup_eager, 1) and self._seen_eager(random)):
+            self._roll_round(random)
+        else:
+            for _ in range(self.round_len):
+                self._roll_step(random)
+                self._eager_kinds.add(bool(random))
         self.resets += 1
         # :208 -- the host sees one value per round: the mean episode return
         ep_return = float(np.mean(self.score.cpu().numpy()))

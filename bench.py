@@ -351,7 +351,7 @@ def fused_critic_timing(agent, reps=20, replays=10):
 REFERENCE_ENV_STEPS_PER_UPDATE = 2257 / 283
 
 
-def reference_schedule(env, dev, args, hp, rounds=3, warm_rounds=2):
+def reference_schedule(env, dev, args, hp, rounds=3, warm_rounds=3):
     """The reference training script's schedule on the same envs
     (exo_amd.rollout.RefScheduleTrainer, Simulation/Exoskeleton_agent_train.py:
     110-211): per episode round a synchronous rollout of every env (uniform
@@ -360,7 +360,8 @@ def reference_schedule(env, dev, args, hp, rounds=3, warm_rounds=2):
     maybe_train_and_checkpoint's burst of round(mean(ep_len)) = 283
     graph-replayed TD7 steps with the policy-checkpoint rule.  Fresh agent;
     `warm_rounds` untimed (the first is the random warm-up and captures the
-    graphs), then `rounds` timed with the rollout and the burst timed apart."""
+    graphs, the third captures the policy round's rollout graph), then
+    `rounds` timed with the rollout and the burst timed apart."""
     from exo_amd.rollout import RefScheduleTrainer
     from exo_amd.td7 import Agent
     torch.manual_seed(2)

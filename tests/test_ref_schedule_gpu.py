@@ -188,3 +188,45 @@ def test_ref_schedule_device_path():
     # the checkpoint policy acts (a refresh copied the actor of its round)
     a = agent.select_action(np.zeros((3, 80), np.float32), use_checkpoint=True, use_exploration=False)
     assert np.isfinite(a).all() and a.shape == (3, 7)
+
+
+def test_round_graph_rollout_matches_per_step_rollout():
+    """RefScheduleTrainer's round graph (the round's rollout steps as one graph,
+    each step's replay insert on a branch beside the next step's select_action)
+    against per-step graph replays: after every round (with its training
+    burst) the replay storage and sum trees, the episode scores, the env state and every network weight are bit-identical (five
+    rounds: a random and a policy round per step, then the round graphs of
+    both starting parities, captured and replayed)."""
+    from exo_amd import VecExoskeletonEnv
+    from exo_amd.rollout import RefScheduleTrainer
+    from exo_amd.td7 import Agent, Hyperparameters
+    outs = []
+    for rg in (False, True):
+        torch.manual_seed(3)
+        N = 32
+        env = VecExoskeletonEnv(N, seed=9)
+        hp = Hyperparameters(batch_size=32)  # the bench's widths: the fused select in the round graph
+        agent = Agent(80, 7, 1, hp=hp, learning_steps=100000, env_num=E, buffer_size=2 * BUF, precision="bf16",
+                      n_envs=N, graph_safe=True)
+        tr = RefScheduleTrainer(env, agent, warmup=1, round_graph=rg)
+        scores = []
+        for _ in range(5):  # random, policy (per-step), then round graphs: captured and replayed
+            tr.run_round()
+            scores.append(tr.score.clone())
+        torch.cuda.synchronize()
+        rb = agent.replay_buffer
+        # (_u: the host-RNG sampling scratch, unused and uninitialised with the device RNG)
+        st = {k: v.detach().clone() for k, v in rb.__dict__.items() if isinstance(v, torch.Tensor) and k != "_u"}
+        w = [p.detach().clone() for m in (agent.learner.actor, agent.learner.critic, agent.learner.encoder)
+             for p in m.parameters()]
+        obs = tr.obs.clone()
+        outs.append((st, w, scores, obs, [t["training_steps"] for t in tr.trace]))
+    a, b = outs
+    assert a[4] == b[4]
+    for k in a[0]:
+        torch.testing.assert_close(a[0][k], b[0][k], rtol=0, atol=0, msg=f"replay {k}")
+    for x, y in zip(a[1], b[1]):
+        torch.testing.assert_close(x, y, rtol=0, atol=0)
+    for x, y in zip(a[2], b[2]):
+        torch.testing.assert_close(x, y, rtol=0, atol=0)
+    torch.testing.assert_close(a[3], b[3], rtol=0, atol=0)

@@ -1,0 +1,12 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/r03_refsched
+mkdir -p $O
+timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_ref_schedule_gpu.py > $O/tests.log 2>&1; tail -2 $O/tests.log
+for rep in 1 2; do
+  timeout -k 10 300 python bench.py --steps 100 --warmup 20 --no-cpu-baseline --no-td7-variants > $O/run.log 2>&1 || { tail $O/run.log; exit 1; }
+  python3 -c "
+import json; d=json.loads([l for l in open('$O/run.log') if l.startswith('{\"metric')][-1]); r=d['reference_schedule']
+print('score-2-launch', round(r['env_steps_per_sec']/1e6,3), 'M env-steps/s', round(r['ms_per_round'],2), 'ms/round', round(r['rollout_ms_per_round'],2), 'rollout ms', round(r['burst_ms_per_round'],2), 'burst ms', round(r['grad_steps_per_sec']), 'grad/s')" | tee -a $O/ab.txt
+done
