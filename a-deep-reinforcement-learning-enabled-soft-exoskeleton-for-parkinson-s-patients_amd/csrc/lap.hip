@@ -282,11 +282,12 @@ __global__ __launch_bounds__(UPD_THREADS) void lap_store_rank_kernel(float *tree
 // env 0's first transition sits one slot behind the others and, when envs are
 // done, two adds of one stratum can land in the same slot -- the later one
 // wins, as the reference's overwrite.  One workgroup: a block scan ranks the
-// active rows (rank_row[r] = row), every active row checks the next E-1 ranks
-// for a same-stratum, same-slot successor (two counts share a slot only if no
-// multiple of E lies between them), winners get slot_of / row_of, losers and
-// inactive rows -1.  ref = {ptr, count, size}; every stratum's size = size
-// (the reference samples every row against the one shared size, :76).
+// active rows (rank_row[r] = the stratum of rank r), every active row checks
+// the next E-1 ranks for a same-stratum, same-slot successor (two counts share
+// a slot only if no multiple of E lies between them), winners get slot_of /
+// row_of, losers and inactive rows -1.  ref = {ptr, count, size}; every
+// stratum's size = size (the reference samples every row against the one
+// shared size, :76).
 __device__ __forceinline__ long long mult_below(long long x, int E) { return (x + E - 1) / E; }
 
 __global__ __launch_bounds__(UPD_THREADS) void lap_store_ref_slots_kernel(int capacity, int E, long long *ref,
@@ -333,8 +334,8 @@ __global__ __launch_bounds__(UPD_THREADS) void lap_store_ref_slots_kernel(int ca
             const int i = base + 4 * t + k;
             if (i >= n) continue;
             if (f[k]) {
-                rank_row[rank] = i;
-                row_of[i] = rank; // the rank, until the winner pass below
+                rank_row[rank] = strata[i]; // the stratum of each rank (the winner pass reads it)
+                row_of[i] = rank;           // the rank, until the winner pass below
                 ++rank;
             } else {
                 row_of[i] = -1;
@@ -353,11 +354,16 @@ __global__ __launch_bounds__(UPD_THREADS) void lap_store_ref_slots_kernel(int ca
         const long long mr = mult_below(count0 + r, E);
         const int s = strata[i];
         bool win = true;
-        for (int q = r + 1; q < min(r + E, n_act); ++q) {
-            if (mult_below(count0 + q, E) != mr) break; // slots only grow with the rank
-            if (strata[rank_row[q]] == s) win = false;
-        }
-        const int slot = (int)((ptr0 + (mr - m0)) % capacity);
+        // ranks r < q share r's slot while count0 + q <= mr E (ceil((count0 + q) / E) == mr):
+        // one 64-bit product instead of a 64-bit division per candidate, and the
+        // candidate's stratum read directly (one load, not rank -> row -> stratum)
+        const long long qend = mr * E - count0;
+        const int qmax = (int)min((long long)min(r + E, n_act) - 1, qend);
+        for (int q = r + 1; q <= qmax; ++q) win &= rank_row[q] != s;
+        long long v = ptr0 + (mr - m0); // ptr0 < capacity, mr - m0 <= n / E + 1
+        if (v >= capacity) v -= capacity;
+        if (v >= capacity) v %= capacity;
+        const int slot = (int)v;
         slot_of[i] = win ? slot : -1;
         row_of[i] = win ? s * (capacity + 1) + slot : -1;
     }
