@@ -444,7 +444,10 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     backend = os.environ.get("EXO_DIST_BACKEND", "nccl")
-    if world > 1:
+    # EXO_FORCE_DIST=1 (under torchrun, one rank): the data-parallel layout and
+    # its collectives at world 1, so a one-GPU box runs the RCCL path too
+    dist_on = world > 1 or os.environ.get("EXO_FORCE_DIST") == "1"
+    if dist_on:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -471,7 +474,7 @@ def main():
         if args.batch:
             hp.batch_size = args.batch
         agent = Agent(80, 7, 1, env_num=8, hp=hp, device=dev, precision=args.precision, n_envs=N,
-                      process_group=dist.group.WORLD if world > 1 else None, graph_safe=not args.eager)
+                      process_group=dist.group.WORLD if dist_on else None, graph_safe=not args.eager)
         trainer = VecTrainer(env, agent, use_graphs=not args.eager)
     # configs[3] / [4]: the env step inside the timed window itself -- device
     # wall-clock reads on the step's stream either side of every step launch,
@@ -583,7 +586,7 @@ def main():
     for _ in range(args.warmup):
         one_step(False)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     resets0 = trainer.resets if trainer is not None else state.get("resets", 0)
@@ -595,7 +598,7 @@ def main():
     for _ in range(args.steps):
         env_steps += one_step(True)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -638,7 +641,7 @@ def main():
     # ranks (max of the ranks' times).
     t = torch.tensor([elapsed, float(env_steps), (elapsed - resets_in_window * reset_ms * 1e-3) / args.steps,
                       reset_ms * 1e-3], device=dev, dtype=torch.float64)
-    if world > 1:
+    if dist_on:
         tmax, tsum = t.clone(), t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
@@ -655,7 +658,7 @@ def main():
                   for n, m in (("actor", agent.learner.actor), ("critic", agent.learner.critic),
                                ("encoder", agent.learner.encoder))}
     dp_sync = dp_ck = None
-    if agent is not None and world > 1:
+    if agent is not None and dist_on:
         # data-parallel replicas must hold bit-identical weights
         ck = torch.stack([torch.cat([p.detach().reshape(-1) for p in m.parameters()]).double().sum()
                           for m in (agent.learner.actor, agent.learner.critic, agent.learner.encoder)]
@@ -682,7 +685,7 @@ def main():
                                    + (f", TD7 batch 8x{agent.hp.batch_size}" if agent else ", env only"),
                        "envs_per_gpu": N, "mode": args.mode, "physics": args.physics,
                        "parallelism": f"env-shard x{world}"
-                       + (" + TD7 DP all-reduce" if agent and world > 1 else "")},
+                       + (" + TD7 DP all-reduce" if agent and dist_on else "")},
             "value_formula": "whole episode rounds: world * A_round / (round_len * t_iter + t_reset); A_round = "
                              f"{A_round:.0f} active env-steps per {round_len}-iteration round and rank, t_iter = "
                              f"{t_iter * 1e3:.4f} ms (window time minus {resets_in_window} reset(s), per iteration), "
@@ -807,7 +810,7 @@ def main():
                 td7 = (agent.hp, agent.hp.batch_size * agent.env_num, total_env_steps / args.steps)
             res["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, args.cpu_threads, td7)
         print(json.dumps(res))
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

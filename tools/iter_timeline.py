@@ -37,11 +37,12 @@ def main(path, verbose=False):
         spans.append((t1 - t0, busy, ksum, len(it)))
         print(f"iteration: span {(t1 - t0) / 1e3:.1f} us, busy {busy / 1e3:.1f} us, idle {(t1 - t0 - busy) / 1e3:.1f} us,"
               f" sum of kernel durations {ksum / 1e3:.1f} us, {len(it)} kernels")
-    if verbose:
-        a, b = pairs[-1]
-        t0 = ks[a][0]
-        for s, e, n, q in ks[a:b]:
-            print(f"{(s - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f}  q{q:>2}  {short(n)}")
+    if verbose:  # the last two iterations (one of each policy-update parity)
+        for a, b in pairs[-2:]:
+            t0 = ks[a][0]
+            print(f"-- iteration of {(ks[b][0] - t0) / 1e3:.1f} us")
+            for s, e, n, q in ks[a:b]:
+                print(f"{(s - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f}  q{q:>2}  {short(n)}")
 
 
 if __name__ == "__main__":
