@@ -393,10 +393,14 @@ class GradSync:
     def __init__(self, group=None):
         self.group = group
         self.world = dist.get_world_size(group) if group is not None else 1
+        # EXO_FORCE_DIST=1 (bench.py under torchrun with one rank): the
+        # data-parallel layout and its collectives at world 1, so a one-GPU box
+        # runs the RCCL path the multi-GPU runs take
+        self.forced = group is not None and os.environ.get("EXO_FORCE_DIST") == "1"
 
     @property
     def active(self):
-        return self.world > 1
+        return self.world > 1 or self.forced
 
     def allreduce_grads(self, params):
         if not self.active:

@@ -213,3 +213,38 @@ def test_add_batch_ref_equals_sequential_reference_adds():
         torch.testing.assert_close(vec._tree, seq._tree, rtol=0, atol=0)
         assert torch.equal(vec.size_s, seq.size_s)
     assert seq.count > 2 * C  # the pointer wrapped
+
+
+def test_wave_descent_and_subtree_rebuild_match_the_binary_tree():
+    """r03d kernels (lap.hip rebuild_subtrees, prefix_total_wave, descend_wave)
+    with NON-integer priorities at full depth (2^18 leaves): after batched
+    updates with duplicates every internal node is exactly left + right in
+    fp32 (the level-by-level recomputation's sums), and the wavefront descent
+    of sample() returns exactly the per-thread binary descent of
+    sample_indices() -- the same comparisons and subtractions."""
+    E, C, B = 3, 250_000, 512
+    lap = _lap(E, C, B)
+    assert lap._cap == 1 << 18
+    rng = np.random.default_rng(7)
+    prio = rng.gamma(0.7, 2.0, (E, C)).astype(np.float32) + np.float32(1e-3)
+    _set_priorities(lap, prio)
+    for _ in range(4):  # random batches with duplicates, like update_priority after a sample
+        idx = rng.integers(0, C, (E, B)).astype(np.int32)
+        idx[:, 1::7] = idx[:, ::7][:, :idx[:, 1::7].shape[1]]
+        p = rng.uniform(0.1, 5.0, (E, B)).astype(np.float32)
+        lap.update_priority(torch.as_tensor(p.reshape(-1), device="cuda"),
+                            ind=torch.as_tensor(idx, device="cuda"))
+    T = lap._tree.cpu().numpy()
+    cap = lap._cap
+    for s in range(E):
+        np.testing.assert_array_equal(T[s, 1:cap], T[s, 2:2 * cap:2] + T[s, 3:2 * cap:2])
+    for size in (C, 180_001, 77):
+        lap.size_s.fill_(size)
+        u = torch.as_tensor(rng.uniform(0, 1, (E, B)).astype(np.float32), device="cuda")
+        want = lap.sample_indices(u).cpu().numpy()
+        lap.device_rng = False
+        lap._u.copy_(u)
+        lap._u.uniform_ = lambda: lap._u  # keep the injected uniforms
+        lap.sample()
+        np.testing.assert_array_equal(lap.ind.cpu().numpy(), want)
+        assert want.max() < size
