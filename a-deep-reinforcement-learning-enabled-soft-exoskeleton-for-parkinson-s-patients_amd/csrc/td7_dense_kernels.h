@@ -975,9 +975,11 @@ void launch_fwd_lds_p(const GemmArgs &a, dim3 grid, int bm, hipStream_t s) {
 // one segment).  Same products and fp32 accumulation as the other forward
 // kernels; the summation order differs (K in 32-steps).  Measured
 // (profiles/r03_big_raw): 1.1-1.6x the LDS kernel on the concatenated
-// layers, level at 65,536 x 1,024 x 1,024 -- ~390-500 TF/s, bound by the
-// fp32 operands' load latency with one slice in flight (~2.7 us per 64-deep
-// slice at 8,192 rows; a second register set spills).
+// layers, level at 65,536 x 1,024 x 1,024 -- ~390-500 TF/s.  r03d: slices
+// two ahead (the next slice rounded to 16-bit early, freeing its fp32
+// registers): 691 -> 623 us on [a | zs], 205 -> 182 on the wide critic's
+// concatenated layer; neither operand's footprint bounds the 1,024 x 1,024
+// layers (profiles/r03d_raw).
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef _Float16 halfx8_t __attribute__((ext_vector_type(8)));
 
@@ -1096,17 +1098,52 @@ __global__ __launch_bounds__(512) void dense_fwd_big_kernel(GemmArgs a) {
                 for (int y = 0; y < 4; ++y) acc[x][y] = mfma_k32<P>(af[x], bf[y], acc[x][y]);
         }
     };
-    // (a second register set two slices ahead spills at 256 VGPRs: measured
-    // per slice ~2.7 us at 8,192 rows, the loads' latency -- see DESIGN)
     gload(0);
     lwrite(0);
     __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-        if (kt + 1 < nk) gload(kt + 1);
+    // two slices ahead (nk >= 4): slice kt+1's fp32 registers (loaded during
+    // the previous iteration) are rounded to 16-bit at the top of iteration
+    // kt, which frees them for slice kt+2's loads -- a whole iteration of
+    // cover for every load at 24 more VGPRs than one slice ahead (r03d:
+    // 211 VGPRs, no spill; the concatenated layers 1.1x, 65,536 x 1,024 x
+    // 1,024 level; profiles/r03d_raw/big_fwd_pipe2.txt)
+    auto lwrite16 = [&](int buf, const uint32_t4 (&ha)[AC], const uint32_t4 (&hb)[BC]) {
+#pragma unroll
+        for (int j = 0; j < AC; ++j) {
+            const int r = lr + 64 * j;
+            As[buf][r * CH + (lc ^ ((r >> 1) & 7))] = ha[j];
+        }
+#pragma unroll
+        for (int j = 0; j < BC; ++j) {
+            const int r = lr + 64 * j;
+            Bs[buf][r * CH + (lc ^ ((r >> 1) & 7))] = hb[j];
+        }
+    };
+    gload(1);
+    int kt = 0;
+    for (; kt + 2 < nk; ++kt) {
+        uint32_t4 ha[AC], hb[BC];
+#pragma unroll
+        for (int j = 0; j < AC; ++j) ha[j] = cvt(xa[j]);
+#pragma unroll
+        for (int j = 0; j < BC; ++j) hb[j] = cvt(xb[j]);
+        gload(kt + 2);
         compute(kt & 1);
-        if (kt + 1 < nk) lwrite((kt + 1) & 1);
+        lwrite16((kt + 1) & 1, ha, hb);
         __syncthreads();
     }
+    {
+        uint32_t4 ha[AC], hb[BC];
+#pragma unroll
+        for (int j = 0; j < AC; ++j) ha[j] = cvt(xa[j]);
+#pragma unroll
+        for (int j = 0; j < BC; ++j) hb[j] = cvt(xb[j]);
+        compute(kt & 1);
+        lwrite16((kt + 1) & 1, ha, hb);
+        __syncthreads();
+        ++kt;
+    }
+    compute(kt & 1);
     // acc[x][y][i] is C[i0 + 64 wm + 16x + 4q + i][j0 + 64 wn + 16y + c]
 #pragma unroll
     for (int y = 0; y < 4; ++y) {
