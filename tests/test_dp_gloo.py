@@ -74,3 +74,29 @@ def test_data_parallel_matches_single_process(tmp_path):
         for k, v in getattr(S, n).state_dict().items():
             np.testing.assert_allclose(r0[f"{n}.{k}"].numpy(), v.numpy(), rtol=2e-5, atol=2e-6, err_msg=f"{n}.{k}")
     assert float(r0["max"]) == float(S.max) and float(r0["min"]) == float(S.min)
+
+
+def _forced_worker(rank, world, port, outdir):
+    sys.path.insert(0, HERE)
+    import helpers  # noqa: F401  (puts the package on sys.path)
+    os.environ["EXO_FORCE_DIST"] = "1"
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    from exo_amd.td7 import GradSync
+    s = GradSync(dist.group.WORLD)
+    flat = torch.arange(6, dtype=torch.float32)
+    s.allreduce_flat(flat)  # one rank: SUM is the identity
+    t = torch.tensor([3.0])
+    s.max_(t)
+    torch.save({"active": s.active, "world": s.world, "flat": flat, "t": t,
+                "plain": GradSync(None).active}, os.path.join(outdir, "forced.pt"))
+    dist.destroy_process_group()
+
+
+def test_force_dist_activates_the_collectives_at_world_one(tmp_path):
+    """EXO_FORCE_DIST=1 (bench.py under torchrun with one rank): GradSync is
+    active with a process group of one, so the data-parallel layout and its
+    collectives run; without a group it stays inactive."""
+    mp.spawn(_forced_worker, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True)
+    r = torch.load(os.path.join(tmp_path, "forced.pt"), weights_only=True)
+    assert r["active"] is True and r["world"] == 1 and r["plain"] is False
+    assert torch.equal(r["flat"], torch.arange(6, dtype=torch.float32)) and float(r["t"]) == 3.0
