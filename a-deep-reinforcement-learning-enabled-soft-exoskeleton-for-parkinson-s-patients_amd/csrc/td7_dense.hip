@@ -254,6 +254,16 @@ extern "C" {
  * 1 relu, 2 elu, 3 tanh), bits 8-15 the MFMA operand precision (Prec). */
 int td7_dense_fwd(const float *x, long xsg, long ldx, const float *w, const float *b, float *y, long ysg, long ldy,
                   int32_t groups, int32_t m, int32_t n, int32_t k, int32_t act, void *stream) {
+    return td7_dense_fwd_w16(x, xsg, ldx, w, b, y, ysg, ldy, groups, m, n, k, act, nullptr, stream);
+}
+
+/* td7_dense_fwd with W also given rounded to the MFMA operand type (bf16 /
+ * fp16 bits, [G][N][K] contiguous, w16 = W.to(dtype)): the large-layer kernel
+ * then loads 16-bit weights instead of rounding fp32 ones per slice -- the
+ * same operand values, bit-identical results; ignored by the other kernels
+ * and at fp32.  w16 may be null. */
+int td7_dense_fwd_w16(const float *x, long xsg, long ldx, const float *w, const float *b, float *y, long ysg, long ldy,
+                      int32_t groups, int32_t m, int32_t n, int32_t k, int32_t act, const uint16_t *w16, void *stream) {
     if (!x || !w || !y || groups <= 0 || m < 0 || n <= 0 || k <= 0) return EXO_EINVAL;
     const int prec = act >> 8;
     act &= 0xFF;
@@ -274,6 +284,7 @@ int td7_dense_fwd(const float *x, long xsg, long ldx, const float *w, const floa
     a.bsg = n;
     a.act = act;
     a.j_bias = -1;
+    a.b16 = prec != PREC_F32 ? w16 : nullptr;
     return launch_fwd(a, groups, prec, (hipStream_t)stream);
 }
 
@@ -285,6 +296,13 @@ int td7_dense_fwd(const float *x, long xsg, long ldx, const float *w, const floa
 int td7_dense_fwd_cat(int32_t nseg, const float *const *xs, const long *xsg, const long *ldx, const int32_t *widths,
                       const float *w, const float *b, float *y, long ysg, long ldy, int32_t groups, int32_t m, int32_t n,
                       int32_t act, void *stream) {
+    return td7_dense_fwd_cat_w16(nseg, xs, xsg, ldx, widths, w, b, y, ysg, ldy, groups, m, n, act, nullptr, stream);
+}
+
+/* td7_dense_fwd_cat with W also given rounded to 16 bits (see td7_dense_fwd_w16) */
+int td7_dense_fwd_cat_w16(int32_t nseg, const float *const *xs, const long *xsg, const long *ldx,
+                          const int32_t *widths, const float *w, const float *b, float *y, long ysg, long ldy,
+                          int32_t groups, int32_t m, int32_t n, int32_t act, const uint16_t *w16, void *stream) {
     if (!w || !y || groups <= 0 || m < 0 || n <= 0) return EXO_EINVAL;
     const int prec = act >> 8;
     act &= 0xFF;
@@ -307,6 +325,7 @@ int td7_dense_fwd_cat(int32_t nseg, const float *const *xs, const long *xsg, con
     a.bsg = n;
     a.act = act;
     a.j_bias = -1;
+    a.b16 = prec != PREC_F32 ? w16 : nullptr;
     return launch_fwd(a, groups, prec, (hipStream_t)stream, true);
 }
 

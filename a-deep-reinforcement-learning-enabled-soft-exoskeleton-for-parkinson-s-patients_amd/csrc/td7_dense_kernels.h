@@ -149,6 +149,9 @@ struct GemmArgs {
     float *bias_grad;  // bwd-weight: column j == J_bias goes to bias_grad[g*bgsg + i]
     long bgsg;
     int j_bias;        // -1: none
+    // forward, dense_fwd_big_kernel: W already rounded to the MFMA operand
+    // type, [G][N][K] contiguous 16-bit (null: round the fp32 W as it is loaded)
+    const uint16_t *b16;
 };
 
 // Workgroup tile 32x32 (2x2 v_mfma_f32_16x16x4_f32 tiles per wave, four
@@ -1000,7 +1003,7 @@ __device__ __forceinline__ floatx4 mfma_k32(uint32_t4 a, uint32_t4 b, floatx4 c)
 
 constexpr int BIG_BK = 64, BIG_CH = BIG_BK / 8;
 
-template <int EP, int P, bool CAT, int BM, int BN>
+template <int EP, int P, bool CAT, int BM, int BN, bool BH = false>
 __global__ __launch_bounds__(512) void dense_fwd_big_kernel(GemmArgs a) {
     constexpr int BK = BIG_BK, CH = BIG_CH, WN = BN / 64;
     constexpr int AC = BM * CH / 512, BC = BN * CH / 512; // chunks per thread per slice
@@ -1012,7 +1015,8 @@ __global__ __launch_bounds__(512) void dense_fwd_big_kernel(GemmArgs a) {
     const int i0 = tile.y * BM, j0 = tile.x * BN, g = tile.z;
     const int K = a.R, nk = (K + BK - 1) / BK;
     const int lr = t >> 3, lc = t & 7; // this thread's chunks: rows lr + 64 j, chunk column lc
-    const __amdgpu_buffer_rsrc_t rb = rsrc(a.B.p + g * a.B.sg);
+    const __amdgpu_buffer_rsrc_t rb =
+        BH ? rsrc(reinterpret_cast<const float *>(a.b16 + (long)g * a.J * a.R)) : rsrc(a.B.p + g * a.B.sg);
     __amdgpu_buffer_rsrc_t ra = rsrc(CAT ? a.cat.p[0] : a.A.p + g * a.A.sg);
     int lda = CAT ? a.cat.ld[0] : (int)a.A.si, kbase = 0, seg = 0;
     uint32_t4 xa[AC][2], xb[BC][2];
@@ -1046,10 +1050,14 @@ __global__ __launch_bounds__(512) void dense_fwd_big_kernel(GemmArgs a) {
 #pragma unroll
         for (int j = 0; j < BC; ++j) {
             const int col = j0 + lr + 64 * j;
-            const int off = (col * (int)a.B.si + k) * 4;
             const bool ok = kin & (col < a.J);
-            xb[j][0] = __builtin_amdgcn_raw_buffer_load_b128(rb, ok ? off : BUF_OOB, 0, 0);
-            xb[j][1] = __builtin_amdgcn_raw_buffer_load_b128(rb, ok ? off + 16 : BUF_OOB, 0, 0);
+            if constexpr (BH) {  // 8 consecutive 16-bit weights: one load, no rounding
+                xb[j][0] = __builtin_amdgcn_raw_buffer_load_b128(rb, ok ? (col * a.R + k) * 2 : BUF_OOB, 0, 0);
+            } else {
+                const int off = (col * (int)a.B.si + k) * 4;
+                xb[j][0] = __builtin_amdgcn_raw_buffer_load_b128(rb, ok ? off : BUF_OOB, 0, 0);
+                xb[j][1] = __builtin_amdgcn_raw_buffer_load_b128(rb, ok ? off + 16 : BUF_OOB, 0, 0);
+            }
         }
     };
     auto cvt = [&](const uint32_t4 (&v)[2]) {
@@ -1069,7 +1077,7 @@ __global__ __launch_bounds__(512) void dense_fwd_big_kernel(GemmArgs a) {
 #pragma unroll
         for (int j = 0; j < BC; ++j) {
             const int r = lr + 64 * j;
-            Bs[buf][r * CH + (lc ^ ((r >> 1) & 7))] = cvt(xb[j]);
+            Bs[buf][r * CH + (lc ^ ((r >> 1) & 7))] = BH ? xb[j][0] : cvt(xb[j]);
         }
     };
     floatx4 acc[4][4];
@@ -1126,7 +1134,7 @@ __global__ __launch_bounds__(512) void dense_fwd_big_kernel(GemmArgs a) {
 #pragma unroll
         for (int j = 0; j < AC; ++j) ha[j] = cvt(xa[j]);
 #pragma unroll
-        for (int j = 0; j < BC; ++j) hb[j] = cvt(xb[j]);
+        for (int j = 0; j < BC; ++j) hb[j] = BH ? xb[j][0] : cvt(xb[j]);
         gload(kt + 2);
         compute(kt & 1);
         lwrite16((kt + 1) & 1, ha, hb);
@@ -1137,7 +1145,7 @@ __global__ __launch_bounds__(512) void dense_fwd_big_kernel(GemmArgs a) {
 #pragma unroll
         for (int j = 0; j < AC; ++j) ha[j] = cvt(xa[j]);
 #pragma unroll
-        for (int j = 0; j < BC; ++j) hb[j] = cvt(xb[j]);
+        for (int j = 0; j < BC; ++j) hb[j] = BH ? xb[j][0] : cvt(xb[j]);
         compute(kt & 1);
         lwrite16((kt + 1) & 1, ha, hb);
         __syncthreads();
@@ -1165,6 +1173,8 @@ void launch_fwd_big_p(const GemmArgs &a, dim3 grid, int bm, hipStream_t s) {
 #define FWD_BIG(EPv)                                                                                               \
     do {                                                                                                         \
         if (bm == 256) hipLaunchKernelGGL((dense_fwd_big_kernel<EPv, P, CAT, 256, 128>), grid, dim3(512), 0, s, a); \
+        else if (a.b16)                                                                                          \
+            hipLaunchKernelGGL((dense_fwd_big_kernel<EPv, P, CAT, 128, 256, true>), grid, dim3(512), 0, s, a);     \
         else hipLaunchKernelGGL((dense_fwd_big_kernel<EPv, P, CAT, 128, 256>), grid, dim3(512), 0, s, a);           \
     } while (0)
     switch (a.act) {

@@ -167,6 +167,11 @@ EXPORTS = {
                                           c_int32, c_void_p]),
     "td7_dense_fwd_cat": (c_int32, [c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                     c_long, c_long, c_int32, c_int32, c_int32, c_int32, c_void_p]),
+    "td7_dense_fwd_w16": (c_int32, [c_void_p, c_long, c_long, c_void_p, c_void_p, c_void_p, c_long, c_long,
+                                    c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p]),
+    "td7_dense_fwd_cat_w16": (c_int32, [c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                        c_void_p, c_long, c_long, c_int32, c_int32, c_int32, c_int32, c_void_p,
+                                        c_void_p]),
     "td7_dense_bwd_weight_cat": (c_int32, [c_void_p, c_long, c_long, c_void_p, c_long, c_long, c_int32, c_void_p,
                                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32,
                                            c_int32, c_void_p]),

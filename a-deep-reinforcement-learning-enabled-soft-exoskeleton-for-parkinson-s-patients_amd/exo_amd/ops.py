@@ -84,6 +84,20 @@ def _engine_needs(ctx, i):
         return True
 
 
+# the large-layer forward kernel reads W already rounded to 16 bits (one
+# conversion per call, ~2 MB at 1,024 x 1,024) when M reaches this many rows
+# at bf16 / fp16 operands (r03d: configs[4]'s select over 65,536 envs and the
+# update at 8 x 1,024); EXO_FWD_W16=0 keeps the in-kernel rounding
+W16_MIN_ROWS = 8192 if os.environ.get("EXO_FWD_W16", "1") != "0" else 1 << 62
+
+
+def _w16(w, prec, M, K):
+    """W rounded to the MFMA operand type for td7_dense_fwd*_w16, or None."""
+    if prec == 0 or M < W16_MIN_ROWS or K < 256:
+        return None
+    return w.to(torch.bfloat16 if prec == PRECISIONS["bf16"] else torch.float16)
+
+
 def _rows(t):
     """(tensor with unit column stride, row stride)."""
     if t.stride(-1) != 1:
@@ -122,9 +136,10 @@ class _DenseFn(torch.autograd.Function):
         prec = _matrix_prec
         if prec or M <= _DenseFn.fwd_kernel_max_rows:
             y = torch.empty((G, M, N) if grouped else (M, N), dtype=torch.float32, device=x.device)
-            nat.check(nat.lib().td7_dense_fwd(nat.ptr(x), xsg, ldx, nat.ptr(w), nat.ptr(bb), nat.ptr(y),
-                                              M * N, N, G, M, N, K, act | prec << 8, nat.stream_ptr(x.device)),
-                      "td7_dense_fwd")
+            w16 = _w16(w, prec, M, K)
+            nat.check(nat.lib().td7_dense_fwd_w16(nat.ptr(x), xsg, ldx, nat.ptr(w), nat.ptr(bb), nat.ptr(y),
+                                                  M * N, N, G, M, N, K, act | prec << 8, nat.ptr(w16),
+                                                  nat.stream_ptr(x.device)), "td7_dense_fwd")
         else:
             y = _torch_dense(x, w, bb, act)
         ctx.save_for_backward(x, w, y)
@@ -182,8 +197,10 @@ class _DenseCatFn(torch.autograd.Function):
         seg = ((ctypes.c_void_p * n)(*[p.data_ptr() for p in parts]), (ctypes.c_long * n)(*sgs),
                (ctypes.c_long * n)(*lds), (ctypes.c_int32 * n)(*widths))
         y = torch.empty((G, M, N) if grouped else (M, N), dtype=torch.float32, device=w.device)
-        nat.check(nat.lib().td7_dense_fwd_cat(n, *seg, nat.ptr(w), nat.ptr(bb), nat.ptr(y), M * N, N, G, M, N,
-                                              act | prec << 8, nat.stream_ptr(w.device)), "td7_dense_fwd_cat")
+        w16 = _w16(w, prec, M, K)
+        nat.check(nat.lib().td7_dense_fwd_cat_w16(n, *seg, nat.ptr(w), nat.ptr(bb), nat.ptr(y), M * N, N, G, M, N,
+                                                  act | prec << 8, nat.ptr(w16), nat.stream_ptr(w.device)),
+                  "td7_dense_fwd_cat")
         ctx.save_for_backward(w, y, *parts)
         ctx.meta = (grouped, G, M, N, K, act | prec << 8, b is not None, widths, sgs, lds)
         # ctx.next_functions has one entry per TENSOR input: argument index -> entry

@@ -412,6 +412,18 @@ int td7_dense_bwd_data(const float *dy_dev, long dysg, long lddy, const float *y
 int td7_dense_fwd_cat(int32_t nseg, const float *const *xs_dev, const long *xsg, const long *ldx,
                       const int32_t *widths, const float *w_dev, const float *b_dev, float *y_dev, long ysg, long ldy,
                       int32_t groups, int32_t m, int32_t n, int32_t act, void *stream);
+/* td7_dense_fwd / td7_dense_fwd_cat (the same Linear + activation of
+ * Agent/TD7_multi_agent.py:61-140) with W also given rounded to the MFMA
+ * operand type (w16_dev: bf16 / fp16 bits, [G][N][K] contiguous, may be null):
+ * the large-layer kernel loads it instead of rounding the fp32 W per slice --
+ * bit-identical results. */
+int td7_dense_fwd_w16(const float *x_dev, long xsg, long ldx, const float *w_dev, const float *b_dev, float *y_dev,
+                      long ysg, long ldy, int32_t groups, int32_t m, int32_t n, int32_t k, int32_t act,
+                      const uint16_t *w16_dev, void *stream);
+int td7_dense_fwd_cat_w16(int32_t nseg, const float *const *xs_dev, const long *xsg, const long *ldx,
+                          const int32_t *widths, const float *w_dev, const float *b_dev, float *y_dev, long ysg,
+                          long ldy, int32_t groups, int32_t m, int32_t n, int32_t act, const uint16_t *w16_dev,
+                          void *stream);
 
 /* y = AvgL1Norm(X W^T + b) per output row (Agent/TD7_multi_agent.py:53-54
  * after a Linear without activation, :61 / :103 / :126), N <= 320: one launch

@@ -460,3 +460,35 @@ def test_big_forward_kernel_is_the_gemm_of_rounded_operands(prec, g, m, n, k, ca
             y = ops.dense(x, w, b, 2)
     ref = torch.nn.functional.elu(x.to(dt).float() @ w.to(dt).float().transpose(-1, -2) + b.unsqueeze(-2))
     torch.testing.assert_close(y, ref.reshape(y.shape), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+@pytest.mark.parametrize("g,m,n,k,cat", [(1, 8200, 1000, 1032, False), (2, 8192, 1024, 3072, True),
+                                         (1, 16384, 1024, 2048, True), (2, 8192, 520, 1024, False)])
+def test_big_forward_with_16bit_weights_is_bit_identical(prec, g, m, n, k, cat):
+    """td7_dense_fwd*_w16 (r03d): the large-layer kernel reading W already
+    rounded to bf16 / fp16 (W.to(dtype), one conversion per call) returns
+    exactly what it returns rounding the fp32 W itself (RNE both ways)."""
+    from exo_amd import ops
+    torch.manual_seed(g + m + n + k)
+    w = torch.randn(g, n, k, device="cuda") / k ** 0.5 if g > 1 else torch.randn(n, k, device="cuda") / k ** 0.5
+    w[..., 0, :4] = torch.tensor([1.0 + 2.0 ** -9, -3.0e-8, 65504.0, 1.0e-30])  # ties, tiny, fp16 max, bf16-only
+    b = torch.randn(g, n, device="cuda") if g > 1 else torch.randn(n, device="cuda")
+    if cat:
+        widths = [k // 3] * 3 if k == 3072 else [k // 2] * 2
+        parts = [torch.randn(g, m, widths[0], device="cuda") if g > 1 else torch.randn(m, widths[0], device="cuda")]
+        parts += [torch.randn(m, wd, device="cuda") for wd in widths[1:]]
+        run = lambda: ops.dense_cat(parts, w, b, 2)  # noqa: E731
+    else:
+        x = torch.randn(g, m, k, device="cuda") if g > 1 else torch.randn(m, k, device="cuda")
+        run = lambda: ops.dense(x, w, b, 2)  # noqa: E731
+    old = ops.W16_MIN_ROWS
+    try:
+        with ops.matrix_precision(prec):
+            ops.W16_MIN_ROWS = 1 << 62
+            y32 = run()
+            ops.W16_MIN_ROWS = 8192
+            y16 = run()
+    finally:
+        ops.W16_MIN_ROWS = old
+    assert torch.equal(y16, y32)
