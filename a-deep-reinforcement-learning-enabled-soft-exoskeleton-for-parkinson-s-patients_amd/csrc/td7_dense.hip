@@ -132,9 +132,14 @@ int launch_fwd(const GemmArgs &a, int groups_grid, int prec, hipStream_t s, bool
         for (int sg = 0; sg < CAT_MAX && a.cat.kb[sg] < a.R; ++sg)
             big = big && a.cat.kb[sg] % BIG_BK == 0 && a.cat.ld[sg] % 4 == 0 && a.cat.sg[sg] % 4 == 0 &&
                   al16(a.cat.p[sg]);
+    } else if (big && a.a16) {
+        big = a.A.si % 8 == 0 && a.A.sg % 8 == 0 && al16(a.a16);
     } else if (big) {
         big = a.A.si % 4 == 0 && a.A.sg % 4 == 0 && al16(a.A.p);
     }
+    // 16-bit input / output (td7_dense_fwd_h): the 128 x 256 big kernel with
+    // 16-bit weights only; anything else is the caller's fp32 fallback
+    if ((a.a16 || a.c16) && !(big && big_bm == 128 && a.b16)) return EXO_ERANGE;
     if (big) {
         dim3 grid((a.J + big_bn - 1) / big_bn, (a.I + big_bm - 1) / big_bm, groups_grid);
         if (cat) {
@@ -297,6 +302,71 @@ int td7_dense_fwd_cat(int32_t nseg, const float *const *xs, const long *xsg, con
                       const float *w, const float *b, float *y, long ysg, long ldy, int32_t groups, int32_t m, int32_t n,
                       int32_t act, void *stream) {
     return td7_dense_fwd_cat_w16(nseg, xs, xsg, ldx, widths, w, b, y, ysg, ldy, groups, m, n, act, nullptr, stream);
+}
+
+/* td7_dense_fwd_w16 on an inference chain (no backward): X and / or Y as
+ * 16-bit values of the MFMA operand type (x16 / y16; the fp32 pointer of the
+ * same operand null) -- the values the consumer rounds its operand to, so a
+ * chain of layers gives bit-identical results with half the activation
+ * bytes.  Only where the large-layer kernel runs (else EXO_ERANGE: fall back to
+ * fp32).  w16 required. */
+int td7_dense_fwd_h(const float *x, const uint16_t *x16, long xsg, long ldx, const float *w, const float *b,
+                    float *y, uint16_t *y16, long ysg, long ldy, int32_t groups, int32_t m, int32_t n, int32_t k,
+                    int32_t act, const uint16_t *w16, void *stream) {
+    if ((!x == !x16) || (!y == !y16) || !w || !w16 || groups <= 0 || m < 0 || n <= 0 || k <= 0) return EXO_EINVAL;
+    const int prec = act >> 8;
+    act &= 0xFF;
+    if (act > 3 || prec < PREC_BF16 || prec > PREC_F16) return EXO_EINVAL;
+    if (m == 0) return EXO_OK;
+    GemmArgs a{};
+    a.A = plain(x ? x : reinterpret_cast<const float *>(x16), xsg, ldx, 1);
+    a.a16 = x16;
+    a.B = plain(w, (long)n * k, k, 1);
+    a.I = m;
+    a.J = n;
+    a.R = k;
+    a.groups_red = 1;
+    a.C = y;
+    a.c16 = y16;
+    a.csg = ysg;
+    a.csi = ldy;
+    a.csj = 1;
+    a.bias = b;
+    a.bsg = n;
+    a.act = act;
+    a.j_bias = -1;
+    a.b16 = w16;
+    return launch_fwd(a, groups, prec, (hipStream_t)stream);
+}
+
+/* td7_dense_fwd_cat_w16 with a 16-bit output (td7_dense_fwd_h's Y) */
+int td7_dense_fwd_cat_h(int32_t nseg, const float *const *xs, const long *xsg, const long *ldx,
+                        const int32_t *widths, const float *w, const float *b, uint16_t *y16, long ysg, long ldy,
+                        int32_t groups, int32_t m, int32_t n, int32_t act, const uint16_t *w16, void *stream) {
+    if (!w || !w16 || !y16 || groups <= 0 || m < 0 || n <= 0) return EXO_EINVAL;
+    const int prec = act >> 8;
+    act &= 0xFF;
+    if (act > 3 || prec < PREC_BF16 || prec > PREC_F16) return EXO_EINVAL;
+    GemmArgs a{};
+    const int k = make_cat(a.cat, nseg, xs, xsg, ldx, widths);
+    if (k <= 0) return EXO_EINVAL;
+    if (m == 0) return EXO_OK;
+    a.A = plain(xs[0], 0, 0, 1);
+    a.B = plain(w, (long)n * k, k, 1);
+    a.I = m;
+    a.J = n;
+    a.R = k;
+    a.groups_red = 1;
+    a.c16 = y16;
+    a.csg = ysg;
+    a.csi = ldy;
+    a.csj = 1;
+    a.bias = b;
+    a.bsg = n;
+    a.act = act;
+    a.j_bias = -1;
+    a.b16 = w16;
+    return launch_fwd(a, groups, prec, (hipStream_t)stream, true);
 }
 
 /* td7_dense_fwd_cat with W also given rounded to 16 bits (see td7_dense_fwd_w16) */

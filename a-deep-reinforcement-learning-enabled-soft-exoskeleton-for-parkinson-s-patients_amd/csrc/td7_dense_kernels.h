@@ -152,6 +152,11 @@ struct GemmArgs {
     // forward, dense_fwd_big_kernel: W already rounded to the MFMA operand
     // type, [G][N][K] contiguous 16-bit (null: round the fp32 W as it is loaded)
     const uint16_t *b16;
+    // dense_fwd_big_kernel, inference chains (td7_dense_fwd_h): the input X
+    // (non-concatenated) and / or the output Y as 16-bit values of the MFMA
+    // operand type -- what the consumer rounds its input to anyway (null: fp32)
+    const uint16_t *a16;
+    uint16_t *c16;
 };
 
 // Workgroup tile 32x32 (2x2 v_mfma_f32_16x16x4_f32 tiles per wave, four
@@ -1003,8 +1008,9 @@ __device__ __forceinline__ floatx4 mfma_k32(uint32_t4 a, uint32_t4 b, floatx4 c)
 
 constexpr int BIG_BK = 64, BIG_CH = BIG_BK / 8;
 
-template <int EP, int P, bool CAT, int BM, int BN, bool BH = false>
+template <int EP, int P, bool CAT, int BM, int BN, bool BH = false, bool AH = false, bool CHF = false>
 __global__ __launch_bounds__(512) void dense_fwd_big_kernel(GemmArgs a) {
+    static_assert(!(AH && CAT), "16-bit X only without concatenation");
     constexpr int BK = BIG_BK, CH = BIG_CH, WN = BN / 64;
     constexpr int AC = BM * CH / 512, BC = BN * CH / 512; // chunks per thread per slice
     __shared__ uint32_t4 As[2][BM * CH];
@@ -1017,7 +1023,8 @@ __global__ __launch_bounds__(512) void dense_fwd_big_kernel(GemmArgs a) {
     const int lr = t >> 3, lc = t & 7; // this thread's chunks: rows lr + 64 j, chunk column lc
     const __amdgpu_buffer_rsrc_t rb =
         BH ? rsrc(reinterpret_cast<const float *>(a.b16 + (long)g * a.J * a.R)) : rsrc(a.B.p + g * a.B.sg);
-    __amdgpu_buffer_rsrc_t ra = rsrc(CAT ? a.cat.p[0] : a.A.p + g * a.A.sg);
+    __amdgpu_buffer_rsrc_t ra = AH ? rsrc(reinterpret_cast<const float *>(a.a16 + g * a.A.sg))
+                                   : rsrc(CAT ? a.cat.p[0] : a.A.p + g * a.A.sg);
     int lda = CAT ? a.cat.ld[0] : (int)a.A.si, kbase = 0, seg = 0;
     uint32_t4 xa[AC][2], xb[BC][2];
     auto gload = [&](int kt) {
@@ -1042,10 +1049,14 @@ __global__ __launch_bounds__(512) void dense_fwd_big_kernel(GemmArgs a) {
 #pragma unroll
         for (int j = 0; j < AC; ++j) {
             const int row = i0 + lr + 64 * j;
-            const int off = (row * lda + k - kbase) * 4;
             const bool ok = kin & (row < a.I);
-            xa[j][0] = __builtin_amdgcn_raw_buffer_load_b128(ra, ok ? off : BUF_OOB, 0, 0);
-            xa[j][1] = __builtin_amdgcn_raw_buffer_load_b128(ra, ok ? off + 16 : BUF_OOB, 0, 0);
+            if constexpr (AH) {  // 8 consecutive 16-bit inputs: one load, no rounding
+                xa[j][0] = __builtin_amdgcn_raw_buffer_load_b128(ra, ok ? (row * lda + k) * 2 : BUF_OOB, 0, 0);
+            } else {
+                const int off = (row * lda + k - kbase) * 4;
+                xa[j][0] = __builtin_amdgcn_raw_buffer_load_b128(ra, ok ? off : BUF_OOB, 0, 0);
+                xa[j][1] = __builtin_amdgcn_raw_buffer_load_b128(ra, ok ? off + 16 : BUF_OOB, 0, 0);
+            }
         }
 #pragma unroll
         for (int j = 0; j < BC; ++j) {
@@ -1072,7 +1083,7 @@ __global__ __launch_bounds__(512) void dense_fwd_big_kernel(GemmArgs a) {
 #pragma unroll
         for (int j = 0; j < AC; ++j) {
             const int r = lr + 64 * j;
-            As[buf][r * CH + (lc ^ ((r >> 1) & 7))] = cvt(xa[j]);
+            As[buf][r * CH + (lc ^ ((r >> 1) & 7))] = AH ? xa[j][0] : cvt(xa[j]);
         }
 #pragma unroll
         for (int j = 0; j < BC; ++j) {
@@ -1132,7 +1143,7 @@ __global__ __launch_bounds__(512) void dense_fwd_big_kernel(GemmArgs a) {
     for (; kt + 2 < nk; ++kt) {
         uint32_t4 ha[AC], hb[BC];
 #pragma unroll
-        for (int j = 0; j < AC; ++j) ha[j] = cvt(xa[j]);
+        for (int j = 0; j < AC; ++j) ha[j] = AH ? xa[j][0] : cvt(xa[j]);
 #pragma unroll
         for (int j = 0; j < BC; ++j) hb[j] = BH ? xb[j][0] : cvt(xb[j]);
         gload(kt + 2);
@@ -1143,7 +1154,7 @@ __global__ __launch_bounds__(512) void dense_fwd_big_kernel(GemmArgs a) {
     {
         uint32_t4 ha[AC], hb[BC];
 #pragma unroll
-        for (int j = 0; j < AC; ++j) ha[j] = cvt(xa[j]);
+        for (int j = 0; j < AC; ++j) ha[j] = AH ? xa[j][0] : cvt(xa[j]);
 #pragma unroll
         for (int j = 0; j < BC; ++j) hb[j] = BH ? xb[j][0] : cvt(xb[j]);
         compute(kt & 1);
@@ -1163,7 +1174,12 @@ __global__ __launch_bounds__(512) void dense_fwd_big_kernel(GemmArgs a) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int row = i0 + wm * 64 + 16 * x + 4 * q + i;
-                if (row < a.I) a.C[g * a.csg + (long)row * a.csi + (long)col * a.csj] = act_fwd_t<EP>(acc[x][y][i] + bv);
+                if (row < a.I) {
+                    const float v = act_fwd_t<EP>(acc[x][y][i] + bv);
+                    const long at = g * a.csg + (long)row * a.csi + (long)col * a.csj;
+                    if constexpr (CHF) a.c16[at] = to_half_bits<P>(v);
+                    else a.C[at] = v;
+                }
             }
     }
 }
@@ -1173,6 +1189,12 @@ void launch_fwd_big_p(const GemmArgs &a, dim3 grid, int bm, hipStream_t s) {
 #define FWD_BIG(EPv)                                                                                               \
     do {                                                                                                         \
         if (bm == 256) hipLaunchKernelGGL((dense_fwd_big_kernel<EPv, P, CAT, 256, 128>), grid, dim3(512), 0, s, a); \
+        else if (a.b16 && a.c16 && a.a16 && !CAT)                                                                \
+            hipLaunchKernelGGL((dense_fwd_big_kernel<EPv, P, CAT, 128, 256, true, !CAT, true>), grid, dim3(512), 0, s, a); \
+        else if (a.b16 && a.a16 && !CAT)                                                                         \
+            hipLaunchKernelGGL((dense_fwd_big_kernel<EPv, P, CAT, 128, 256, true, !CAT, false>), grid, dim3(512), 0, s, a); \
+        else if (a.b16 && a.c16)                                                                                 \
+            hipLaunchKernelGGL((dense_fwd_big_kernel<EPv, P, CAT, 128, 256, true, false, true>), grid, dim3(512), 0, s, a); \
         else if (a.b16)                                                                                          \
             hipLaunchKernelGGL((dense_fwd_big_kernel<EPv, P, CAT, 128, 256, true>), grid, dim3(512), 0, s, a);     \
         else hipLaunchKernelGGL((dense_fwd_big_kernel<EPv, P, CAT, 128, 256>), grid, dim3(512), 0, s, a);           \

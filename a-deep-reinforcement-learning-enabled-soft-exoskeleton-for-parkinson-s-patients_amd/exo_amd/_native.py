@@ -172,6 +172,11 @@ EXPORTS = {
     "td7_dense_fwd_cat_w16": (c_int32, [c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_void_p, c_long, c_long, c_int32, c_int32, c_int32, c_int32, c_void_p,
                                         c_void_p]),
+    "td7_dense_fwd_h": (c_int32, [c_void_p, c_void_p, c_long, c_long, c_void_p, c_void_p, c_void_p, c_void_p,
+                                  c_long, c_long, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p]),
+    "td7_dense_fwd_cat_h": (c_int32, [c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_long, c_long, c_int32, c_int32, c_int32, c_int32, c_void_p,
+                                      c_void_p]),
     "td7_dense_bwd_weight_cat": (c_int32, [c_void_p, c_long, c_long, c_void_p, c_long, c_long, c_int32, c_void_p,
                                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32,
                                            c_int32, c_void_p]),

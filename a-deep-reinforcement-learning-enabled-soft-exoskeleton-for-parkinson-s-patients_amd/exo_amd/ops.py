@@ -98,6 +98,39 @@ def _w16(w, prec, M, K):
     return w.to(torch.bfloat16 if prec == PRECISIONS["bf16"] else torch.float16)
 
 
+_HALF = {PRECISIONS["bf16"]: torch.bfloat16, PRECISIONS["fp16"]: torch.float16}
+EXO_ERANGE = -34
+# EXO_FWD_HALF=0: inference chains keep fp32 activations (half_out ignored)
+HALF_CHAIN = os.environ.get("EXO_FWD_HALF", "1") != "0"
+
+
+def _half_ok(M, K, grouped):
+    """An inference-chain layer (no autograd) that the large-layer kernel runs
+    with 16-bit weights: its input / output may be 16-bit (td7_dense_fwd_h)."""
+    return (HALF_CHAIN and _matrix_prec in _HALF and not grouped and not torch.is_grad_enabled() and M >= W16_MIN_ROWS
+            and K >= 256 and not torch.is_autocast_enabled())
+
+
+def _dense_h(x, w, b, act, half_out):
+    """td7_dense_fwd_h: x fp32 or 16-bit (the matrix precision's type), y fp32
+    or 16-bit; None where the large-layer kernel does not apply."""
+    prec = _matrix_prec
+    M, K, N = x.shape[-2], x.shape[-1], w.shape[-2]
+    w = w.contiguous()
+    x, ldx = _rows(x)
+    x16 = x.dtype != torch.float32
+    y = torch.empty((M, N), dtype=_HALF[prec] if half_out else torch.float32, device=x.device)
+    bb = b.contiguous() if b is not None else None
+    rc = nat.lib().td7_dense_fwd_h(None if x16 else nat.ptr(x), nat.ptr(x) if x16 else None, 0, ldx, nat.ptr(w),
+                                   nat.ptr(bb), None if half_out else nat.ptr(y), nat.ptr(y) if half_out else None,
+                                   M * N, N, 1, M, N, K, act | prec << 8, nat.ptr(_w16(w, prec, M, K)),
+                                   nat.stream_ptr(x.device))
+    if rc == EXO_ERANGE:
+        return None
+    nat.check(rc, "td7_dense_fwd_h")
+    return y
+
+
 def _rows(t):
     """(tensor with unit column stride, row stride)."""
     if t.stride(-1) != 1:
@@ -353,18 +386,41 @@ def _cat_ok(parts, w):
     return True
 
 
-def dense_cat(parts, w, b, act=0):
+def dense_cat(parts, w, b, act=0, half_out=False):
     """dense(torch.cat(parts, -1), w, b, act) reading the parts in place (parts
     of a grouped layer may be [G,M,k] or shared [M,k]).  Falls back to the
-    concatenation where the fused kernels do not apply."""
+    concatenation where the fused kernels do not apply.  half_out: as dense."""
     if _CAT and w.is_cuda and w.dtype == torch.float32 and not torch.is_autocast_enabled() and _cat_ok(parts, w) \
             and (_matrix_prec or parts[0].shape[-2] <= _DenseFn.fwd_kernel_max_rows):
+        if half_out and _half_ok(parts[0].shape[-2], w.shape[-1], w.dim() == 3):
+            y = _dense_cat_h(parts, w, b, act)
+            if y is not None:
+                return y
         return _DenseCatFn.apply(w, b, act, *parts)
     grouped = w.dim() == 3
     if grouped and any(p.dim() == 3 for p in parts):
         G = w.shape[0]
         parts = [p if p.dim() == 3 else p.unsqueeze(0).expand(G, *p.shape) for p in parts]
     return dense(torch.cat(parts, -1), w, b, act, concat_grad_cols(parts))
+
+
+def _dense_cat_h(parts, w, b, act):
+    """td7_dense_fwd_cat_h: the concatenated layer with a 16-bit output, or None."""
+    prec = _matrix_prec
+    N, K = w.shape[-2], w.shape[-1]
+    w = w.contiguous()
+    parts = [_rows(p)[0] for p in parts]
+    M, n = parts[0].shape[-2], len(parts)
+    seg = ((ctypes.c_void_p * n)(*[p.data_ptr() for p in parts]), (ctypes.c_long * n)(*([0] * n)),
+           (ctypes.c_long * n)(*[p.stride(-2) for p in parts]), (ctypes.c_int32 * n)(*[p.shape[-1] for p in parts]))
+    y = torch.empty((M, N), dtype=_HALF[prec], device=w.device)
+    bb = b.contiguous() if b is not None else None
+    rc = nat.lib().td7_dense_fwd_cat_h(n, *seg, nat.ptr(w), nat.ptr(bb), nat.ptr(y), M * N, N, 1, M, N,
+                                       act | prec << 8, nat.ptr(_w16(w, prec, M, K)), nat.stream_ptr(w.device))
+    if rc == EXO_ERANGE:
+        return None
+    nat.check(rc, "td7_dense_fwd_cat_h")
+    return y
 
 
 _CAT = os.environ.get("EXO_TD7_CAT", "1") != "0"
@@ -487,13 +543,27 @@ def _torch_dense(x, w, b, act):
     return y
 
 
-def dense(x, w, b, act=0, dx_cols=None):
+def dense(x, w, b, act=0, dx_cols=None, half_out=False):
     """Linear + activation (act code, see ACT_CODES) -- td7_dense kernels on a
     GPU for fp32 tensors; the reference's torch expression otherwise.
     dx_cols = (c0, c1): only input columns [c0, c1) need a gradient (x is a
-    concatenation whose other parts do not require one)."""
+    concatenation whose other parts do not require one).
+    Inference chains (r03d): half_out=True asks for y as the 16-bit values
+    the next layer rounds its input to (returned where the large-layer kernel
+    runs, fp32 otherwise), and a 16-bit x (such a y) is read as it is --
+    bit-identical to the fp32 chain."""
+    if x.device.type == "cuda" and x.dtype in (torch.bfloat16, torch.float16) and w.dtype == torch.float32:
+        if x.dtype == _HALF.get(_matrix_prec) and _half_ok(x.shape[-2], x.shape[-1], w.dim() == 3):
+            y = _dense_h(x, w, b, act, half_out)
+            if y is not None:
+                return y
+        x = x.float()
     if x.device.type == "cuda" and x.dtype == torch.float32 and w.dtype == torch.float32 \
             and not torch.is_autocast_enabled():
+        if half_out and _half_ok(x.shape[-2], x.shape[-1], w.dim() == 3):
+            y = _dense_h(x, w, b, act, True)
+            if y is not None:
+                return y
         return _DenseFn.apply(x, w, b, act, dx_cols)
     return _torch_dense(x, w, b, act)
 

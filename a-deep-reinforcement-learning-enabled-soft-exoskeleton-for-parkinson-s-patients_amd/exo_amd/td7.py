@@ -118,7 +118,9 @@ class Actor(nn.Module):
             a = self.activ(self.l2(a))
             return torch.tanh(self.l3(a))
         a = ops.dense_norm([state], self.l0.weight, self.l0.bias)
-        a = ops.dense_cat([a, zs], self.l1.weight, self.l1.bias, act)
+        # inference at the wide configuration's sizes: l1's output handed to
+        # l2 as the 16-bit values l2 rounds it to (ops.dense half_out)
+        a = ops.dense_cat([a, zs], self.l1.weight, self.l1.bias, act, half_out=True)
         a = ops.dense(a, self.l2.weight, self.l2.bias, act)
         return ops.dense(a, self.l3.weight, self.l3.bias, ops.ACT_CODES["tanh"])
 
@@ -143,7 +145,7 @@ class Encoder(nn.Module):
             zs = self.activ(self.zs2(zs))
             return AvgL1Norm(self.zs3(zs))
         zs = ops.dense(state, self.zs1.weight, self.zs1.bias, act)
-        zs = ops.dense(zs, self.zs2.weight, self.zs2.bias, act)
+        zs = ops.dense(zs, self.zs2.weight, self.zs2.bias, act, half_out=True)  # see Actor.forward
         return ops.dense_norm([zs], self.zs3.weight, self.zs3.bias)
 
     def zsa(self, zs, action):

@@ -424,6 +424,20 @@ int td7_dense_fwd_cat_w16(int32_t nseg, const float *const *xs_dev, const long *
                           const int32_t *widths, const float *w_dev, const float *b_dev, float *y_dev, long ysg,
                           long ldy, int32_t groups, int32_t m, int32_t n, int32_t act, const uint16_t *w16_dev,
                           void *stream);
+/* The same Linear + activation on an inference chain (select_action,
+ * TD7_multi_agent.py:192-209 / Pink :209-228; no backward): X (x16_dev) and /
+ * or Y (y16_dev) as 16-bit values of the MFMA operand type -- exactly what the
+ * consumer rounds its operand to, so a chain is bit-identical with half the
+ * activation bytes; the fp32 pointer of a 16-bit operand is null.  Only where
+ * the large-layer kernel runs: EXO_ERANGE otherwise (the caller falls back to
+ * fp32).  w16_dev required. */
+int td7_dense_fwd_h(const float *x_dev, const uint16_t *x16_dev, long xsg, long ldx, const float *w_dev,
+                    const float *b_dev, float *y_dev, uint16_t *y16_dev, long ysg, long ldy, int32_t groups, int32_t m,
+                    int32_t n, int32_t k, int32_t act, const uint16_t *w16_dev, void *stream);
+int td7_dense_fwd_cat_h(int32_t nseg, const float *const *xs_dev, const long *xsg, const long *ldx,
+                        const int32_t *widths, const float *w_dev, const float *b_dev, uint16_t *y16_dev, long ysg,
+                        long ldy, int32_t groups, int32_t m, int32_t n, int32_t act, const uint16_t *w16_dev,
+                        void *stream);
 
 /* y = AvgL1Norm(X W^T + b) per output row (Agent/TD7_multi_agent.py:53-54
  * after a Linear without activation, :61 / :103 / :126), N <= 320: one launch

@@ -492,3 +492,39 @@ def test_big_forward_with_16bit_weights_is_bit_identical(prec, g, m, n, k, cat):
     finally:
         ops.W16_MIN_ROWS = old
     assert torch.equal(y16, y32)
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_inference_chain_with_16bit_activations_is_bit_identical(prec):
+    """ops.dense / dense_cat half_out (r03d, td7_dense_fwd_h / _cat_h): the
+    wide configuration's select chain -- zs1 -> zs2 (16-bit out) -> zs3 +
+    AvgL1Norm and l0 -> l1 = [a | zs] (16-bit out) -> l2 -> l3 -- under no_grad
+    equals the fp32-activation chain bit for bit (every consumer rounds its
+    input to the same 16-bit values); with autograd on nothing is 16-bit."""
+    from exo_amd import ops
+    from exo_amd.td7 import Actor, Encoder
+    torch.manual_seed(5)
+    enc = Encoder(80, 7, 1024, 1024).cuda()
+    actor = Actor(80, 7, 1024, 1024).cuda()
+    state = torch.randn(8192, 80, device="cuda")
+
+    def chain():
+        zs = enc.zs(state)
+        return zs, actor(state, zs)
+
+    old = ops.W16_MIN_ROWS
+    try:
+        with ops.matrix_precision(prec), torch.no_grad():
+            ops.W16_MIN_ROWS = 1 << 62
+            zs32, a32 = chain()
+            ops.W16_MIN_ROWS = 8192
+            zs16, a16 = chain()
+            h = ops.dense(state, enc.zs1.weight, enc.zs1.bias, 2)
+            assert ops.dense(h, enc.zs2.weight, enc.zs2.bias, 2, half_out=True).dtype != torch.float32
+        with ops.matrix_precision(prec):
+            h = ops.dense(state, enc.zs1.weight, enc.zs1.bias, 2)
+            assert ops.dense(h, enc.zs2.weight, enc.zs2.bias, 2, half_out=True).dtype == torch.float32
+    finally:
+        ops.W16_MIN_ROWS = old
+    assert zs16.dtype == a16.dtype == torch.float32
+    assert torch.equal(zs16, zs32) and torch.equal(a16, a32)
