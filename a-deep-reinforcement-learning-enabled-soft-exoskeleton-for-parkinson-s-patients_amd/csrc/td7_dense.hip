@@ -138,8 +138,15 @@ int launch_fwd(const GemmArgs &a, int groups_grid, int prec, hipStream_t s, bool
         big = a.A.si % 4 == 0 && a.A.sg % 4 == 0 && al16(a.A.p);
     }
     // 16-bit input / output (td7_dense_fwd_h): the 128 x 256 big kernel with
-    // 16-bit weights only; anything else is the caller's fp32 fallback
-    if ((a.a16 || a.c16) && !(big && big_bm == 128 && a.b16)) return EXO_ERANGE;
+    // 16-bit weights, or a 16-bit output of the 128 x 128 LDS kernel (fp32 X:
+    // the K = 80 first layers); anything else is the caller's fp32 fallback
+    if (a.a16 || a.c16) {
+        const long t64 = (long)((a.I + 63) / 64) * ((a.J + 63) / 64) * groups_grid;
+        const long t128 = (long)((a.I + 127) / 128) * ((a.J + 127) / 128) * groups_grid;
+        const bool lds128 = !big && !a.a16 && prec != PREC_F32 && lds_on && a.J >= 64 &&
+                            ((t64 >= 256 && a.R >= 256) || (t64 >= 2048 && a.R >= 64)) && t128 >= 256;
+        if (!(big && big_bm == 128 && a.b16) && !lds128) return EXO_ERANGE;
+    }
     if (big) {
         dim3 grid((a.J + big_bn - 1) / big_bn, (a.I + big_bm - 1) / big_bm, groups_grid);
         if (cat) {

@@ -814,7 +814,7 @@ __device__ __forceinline__ uint16_t to_half_bits(float v) {
     else return __builtin_bit_cast(uint16_t, (__bf16)v);
 }
 
-template <int EP, int P, int BM, int BN, bool CAT>
+template <int EP, int P, int BM, int BN, bool CAT, bool CHF = false>
 __global__ __launch_bounds__(256) void dense_fwd_lds_kernel(GemmArgs a) {
     constexpr int BK = 32, LDK = 40;                 // halves per LDS row (32 + 8 pad)
     constexpr int AL = BM * BK / 256 / 4, BL = BN * BK / 256 / 4;  // 16-byte loads per thread per slice
@@ -941,7 +941,12 @@ __global__ __launch_bounds__(256) void dense_fwd_lds_kernel(GemmArgs a) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const int row = i0 + wm * (BM / 2) + 16 * x + 4 * q + k;
-                if (row < a.I) a.C[g * a.csg + (long)row * a.csi + (long)col * a.csj] = act_fwd_t<EP>(acc[x][y][k] + bv);
+                if (row < a.I) {
+                    const float v = act_fwd_t<EP>(acc[x][y][k] + bv);
+                    const long at = g * a.csg + (long)row * a.csi + (long)col * a.csj;
+                    if constexpr (CHF) a.c16[at] = to_half_bits<P>(v);  // td7_dense_fwd_h's 16-bit Y
+                    else a.C[at] = v;
+                }
             }
     }
 }
@@ -950,7 +955,9 @@ template <int P, bool CAT>
 void launch_fwd_lds_p(const GemmArgs &a, dim3 grid, int bm, hipStream_t s) {
 #define FWD_LDS(EPv)                                                                                    \
     do {                                                                                              \
-        if (bm == 128) hipLaunchKernelGGL((dense_fwd_lds_kernel<EPv, P, 128, 128, CAT>), grid, dim3(256), 0, s, a); \
+        if (bm == 128 && a.c16)                                                                        \
+            hipLaunchKernelGGL((dense_fwd_lds_kernel<EPv, P, 128, 128, CAT, true>), grid, dim3(256), 0, s, a); \
+        else if (bm == 128) hipLaunchKernelGGL((dense_fwd_lds_kernel<EPv, P, 128, 128, CAT>), grid, dim3(256), 0, s, a); \
         else hipLaunchKernelGGL((dense_fwd_lds_kernel<EPv, P, 64, 64, CAT>), grid, dim3(256), 0, s, a);          \
     } while (0)
     switch (a.act) {

@@ -11,6 +11,8 @@
 //             else gx_rk = gy_rk / eps            (torch.clamp passes no gradient)
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <algorithm>
 
 #include "adam_math.h"
@@ -38,6 +40,33 @@ __global__ __launch_bounds__(256) void avgl1_fwd_kernel(const float *__restrict_
     const float s = fmaxf(m, eps);
     float *yr = y + (size_t)r * cols;
     for (int j = lane; j < cols; j += 64) yr[j] = xr[j] / s;
+    if (lane == 0) s_out[r] = m;
+}
+
+// The same per-row sums with the row kept in registers (cols <= 64 MAXJ): every
+// load of a row in flight at once and no second read for the division (r03d:
+// the wide configuration's 65,536 x 1,024 norms).  Lane l still adds
+// |x[l]|, |x[l + 64]|, ... in that order: bit-identical to avgl1_fwd_kernel.
+template <int MAXJ>
+__global__ __launch_bounds__(256) void avgl1_fwd_reg_kernel(const float *__restrict__ x, float *__restrict__ y,
+                                                            float *__restrict__ s_out, int rows, int cols, float eps) {
+    const int r = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= rows) return;
+    const float *xr = x + (size_t)r * cols;
+    float v[MAXJ];
+#pragma unroll
+    for (int i = 0; i < MAXJ; ++i) v[i] = lane + 64 * i < cols ? xr[lane + 64 * i] : 0.f;
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXJ; ++i)
+        if (lane + 64 * i < cols) acc += fabsf(v[i]);
+    const float m = wave_sum(acc) / cols;
+    const float s = fmaxf(m, eps);
+    float *yr = y + (size_t)r * cols;
+#pragma unroll
+    for (int i = 0; i < MAXJ; ++i)
+        if (lane + 64 * i < cols) yr[lane + 64 * i] = v[i] / s;
     if (lane == 0) s_out[r] = m;
 }
 
@@ -214,8 +243,13 @@ int td7_avgl1norm_fwd(const float *x, float *y, float *mean_out, int32_t rows, i
                       void *stream) {
     if (!x || !y || !mean_out || rows < 0 || cols <= 0) return EXO_EINVAL;
     if (rows == 0) return EXO_OK;
-    hipLaunchKernelGGL(avgl1_fwd_kernel, dim3((rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK), dim3(256), 0,
-                       (hipStream_t)stream, x, y, mean_out, rows, cols, eps);
+    const dim3 grid((rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK);
+    const char *reg_env = getenv("EXO_AVGL1_REG");  // read per call: the bit-identity test switches it
+    if (cols > 256 && cols <= 1024 && !(reg_env && reg_env[0] == '0'))
+        hipLaunchKernelGGL(avgl1_fwd_reg_kernel<16>, grid, dim3(256), 0, (hipStream_t)stream, x, y, mean_out, rows,
+                           cols, eps);
+    else
+        hipLaunchKernelGGL(avgl1_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, y, mean_out, rows, cols, eps);
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 

@@ -93,7 +93,7 @@ W16_MIN_ROWS = 8192 if os.environ.get("EXO_FWD_W16", "1") != "0" else 1 << 62
 
 def _w16(w, prec, M, K):
     """W rounded to the MFMA operand type for td7_dense_fwd*_w16, or None."""
-    if prec == 0 or M < W16_MIN_ROWS or K < 256:
+    if prec == 0 or M < W16_MIN_ROWS or K < 64:
         return None
     return w.to(torch.bfloat16 if prec == PRECISIONS["bf16"] else torch.float16)
 
@@ -105,10 +105,11 @@ HALF_CHAIN = os.environ.get("EXO_FWD_HALF", "1") != "0"
 
 
 def _half_ok(M, K, grouped):
-    """An inference-chain layer (no autograd) that the large-layer kernel runs
-    with 16-bit weights: its input / output may be 16-bit (td7_dense_fwd_h)."""
+    """An inference-chain layer (no autograd) at the large-layer sizes: its
+    input / output may be 16-bit (td7_dense_fwd_h; the C side answers
+    EXO_ERANGE where no 16-bit-capable kernel runs)."""
     return (HALF_CHAIN and _matrix_prec in _HALF and not grouped and not torch.is_grad_enabled() and M >= W16_MIN_ROWS
-            and K >= 256 and not torch.is_autocast_enabled())
+            and K >= 64 and not torch.is_autocast_enabled())
 
 
 def _dense_h(x, w, b, act, half_out):

@@ -144,8 +144,8 @@ class Encoder(nn.Module):
             zs = self.activ(self.zs1(state))
             zs = self.activ(self.zs2(zs))
             return AvgL1Norm(self.zs3(zs))
-        zs = ops.dense(state, self.zs1.weight, self.zs1.bias, act)
-        zs = ops.dense(zs, self.zs2.weight, self.zs2.bias, act, half_out=True)  # see Actor.forward
+        zs = ops.dense(state, self.zs1.weight, self.zs1.bias, act, half_out=True)  # see Actor.forward
+        zs = ops.dense(zs, self.zs2.weight, self.zs2.bias, act, half_out=True)
         return ops.dense_norm([zs], self.zs3.weight, self.zs3.bias)
 
     def zsa(self, zs, action):

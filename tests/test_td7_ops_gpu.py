@@ -144,3 +144,18 @@ def test_flat_adam_step_many_matches_separate_steps():
                 torch.testing.assert_close(p.detach(), q.detach(), rtol=0, atol=0)
         for o, r in zip(opts, refs):
             assert float(o._step) == float(r._step) == it + 1
+
+
+@pytest.mark.parametrize("cols", [300, 1000, 1024])
+def test_avgl1norm_register_kernel_is_bit_identical(cols, monkeypatch):
+    """avgl1_fwd_reg_kernel (r03d: rows of 257-1,024 kept in registers, one
+    read) adds each lane's elements in the same order as avgl1_fwd_kernel."""
+    from exo_amd.ops import avg_l1_norm
+    torch.manual_seed(cols)
+    x = torch.randn(4099, cols, device="cuda") * torch.rand(4099, 1, device="cuda") ** 4
+    x[7] = 0.0  # a clamped row (mean < eps)
+    with torch.no_grad():
+        y_reg = avg_l1_norm(x)
+        monkeypatch.setenv("EXO_AVGL1_REG", "0")
+        y_old = avg_l1_norm(x)
+    assert torch.equal(y_reg, y_old)

@@ -2,9 +2,9 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/r03d_half
+O=gpurun_out/r03d_half2
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_td7_dense_gpu.py tests/test_configs_gpu.py tests/test_td7_full.py tests/test_library.py tests/test_rollout_gpu.py tests/test_select_full_gpu.py > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_td7_dense_gpu.py tests/test_td7_ops_gpu.py tests/test_configs_gpu.py tests/test_td7_full.py tests/test_library.py tests/test_rollout_gpu.py tests/test_select_full_gpu.py > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
 for v in 0 1; do
   echo "== EXO_FWD_HALF=$v" >> $O/fwd_bench.txt
