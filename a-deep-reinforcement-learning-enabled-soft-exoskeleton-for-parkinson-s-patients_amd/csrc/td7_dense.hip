@@ -130,8 +130,8 @@ int launch_fwd(const GemmArgs &a, int groups_grid, int prec, hipStream_t s, bool
                a.B.si % 4 == 0 && a.B.sg % 4 == 0 && al16(a.B.p);
     if (big && cat) {
         for (int sg = 0; sg < CAT_MAX && a.cat.kb[sg] < a.R; ++sg)
-            big = big && a.cat.kb[sg] % BIG_BK == 0 && a.cat.ld[sg] % 4 == 0 && a.cat.sg[sg] % 4 == 0 &&
-                  al16(a.cat.p[sg]);
+            big = big && a.cat.kb[sg] % BIG_BK == 0 && a.cat.ld[sg] % (a.a16 ? 8 : 4) == 0 &&
+                  a.cat.sg[sg] % 4 == 0 && al16(a.cat.p[sg]);
     } else if (big && a.a16) {
         big = a.A.si % 8 == 0 && a.A.sg % 8 == 0 && al16(a.a16);
     } else if (big) {
@@ -140,6 +140,7 @@ int launch_fwd(const GemmArgs &a, int groups_grid, int prec, hipStream_t s, bool
     // 16-bit input / output (td7_dense_fwd_h): the 128 x 256 big kernel with
     // 16-bit weights, or a 16-bit output of the 128 x 128 LDS kernel (fp32 X:
     // the K = 80 first layers); anything else is the caller's fp32 fallback
+    if (cat && a.a16 && !a.c16) return EXO_ERANGE;  // 16-bit segments: the CHF variant only
     if (a.a16 || a.c16) {
         const long t64 = (long)((a.I + 63) / 64) * ((a.J + 63) / 64) * groups_grid;
         const long t128 = (long)((a.I + 127) / 128) * ((a.J + 127) / 128) * groups_grid;
@@ -346,19 +347,23 @@ int td7_dense_fwd_h(const float *x, const uint16_t *x16, long xsg, long ldx, con
     return launch_fwd(a, groups, prec, (hipStream_t)stream);
 }
 
-/* td7_dense_fwd_cat_w16 with a 16-bit output (td7_dense_fwd_h's Y) */
-int td7_dense_fwd_cat_h(int32_t nseg, const float *const *xs, const long *xsg, const long *ldx,
+/* td7_dense_fwd_cat_w16 with a 16-bit output (td7_dense_fwd_h's Y); xs16: the
+ * segments are 16-bit values too (the big kernel's 16-bit X, per segment) */
+int td7_dense_fwd_cat_h(int32_t nseg, const void *const *xs_, int32_t xs16, const long *xsg, const long *ldx,
                         const int32_t *widths, const float *w, const float *b, uint16_t *y16, long ysg, long ldy,
                         int32_t groups, int32_t m, int32_t n, int32_t act, const uint16_t *w16, void *stream) {
-    if (!w || !w16 || !y16 || groups <= 0 || m < 0 || n <= 0) return EXO_EINVAL;
+    if (!xs_ || !w || !w16 || !y16 || groups <= 0 || m < 0 || n <= 0 || xs16 < 0 || xs16 > 1) return EXO_EINVAL;
+    const float *const *xs = reinterpret_cast<const float *const *>(xs_);
     const int prec = act >> 8;
     act &= 0xFF;
     if (act > 3 || prec < PREC_BF16 || prec > PREC_F16) return EXO_EINVAL;
+    if (xs16 && groups != 1) return EXO_ERANGE;
     GemmArgs a{};
     const int k = make_cat(a.cat, nseg, xs, xsg, ldx, widths);
     if (k <= 0) return EXO_EINVAL;
     if (m == 0) return EXO_OK;
     a.A = plain(xs[0], 0, 0, 1);
+    if (xs16) a.a16 = reinterpret_cast<const uint16_t *>(xs[0]);  // marks the segments 16-bit
     a.B = plain(w, (long)n * k, k, 1);
     a.I = m;
     a.J = n;

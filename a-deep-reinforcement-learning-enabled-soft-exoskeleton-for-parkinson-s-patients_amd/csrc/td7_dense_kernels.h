@@ -1017,7 +1017,6 @@ constexpr int BIG_BK = 64, BIG_CH = BIG_BK / 8;
 
 template <int EP, int P, bool CAT, int BM, int BN, bool BH = false, bool AH = false, bool CHF = false>
 __global__ __launch_bounds__(512) void dense_fwd_big_kernel(GemmArgs a) {
-    static_assert(!(AH && CAT), "16-bit X only without concatenation");
     constexpr int BK = BIG_BK, CH = BIG_CH, WN = BN / 64;
     constexpr int AC = BM * CH / 512, BC = BN * CH / 512; // chunks per thread per slice
     __shared__ uint32_t4 As[2][BM * CH];
@@ -1030,8 +1029,10 @@ __global__ __launch_bounds__(512) void dense_fwd_big_kernel(GemmArgs a) {
     const int lr = t >> 3, lc = t & 7; // this thread's chunks: rows lr + 64 j, chunk column lc
     const __amdgpu_buffer_rsrc_t rb =
         BH ? rsrc(reinterpret_cast<const float *>(a.b16 + (long)g * a.J * a.R)) : rsrc(a.B.p + g * a.B.sg);
-    __amdgpu_buffer_rsrc_t ra = AH ? rsrc(reinterpret_cast<const float *>(a.a16 + g * a.A.sg))
-                                   : rsrc(CAT ? a.cat.p[0] : a.A.p + g * a.A.sg);
+    // AH with CAT: the segments' pointers hold 16-bit values (non-grouped only)
+    __amdgpu_buffer_rsrc_t ra = CAT  ? rsrc(a.cat.p[0])
+                                : AH ? rsrc(reinterpret_cast<const float *>(a.a16 + g * a.A.sg))
+                                     : rsrc(a.A.p + g * a.A.sg);
     int lda = CAT ? a.cat.ld[0] : (int)a.A.si, kbase = 0, seg = 0;
     uint32_t4 xa[AC][2], xb[BC][2];
     auto gload = [&](int kt) {
@@ -1046,7 +1047,8 @@ __global__ __launch_bounds__(512) void dense_fwd_big_kernel(GemmArgs a) {
 #pragma unroll
                 for (int m = 1; m < CAT_MAX; ++m)
                     if (s == m) p = a.cat.p[m], gs = a.cat.sg[m], ld = a.cat.ld[m], kb = a.cat.kb[m];
-                ra = rsrc(p + g * gs);
+                ra = AH ? rsrc(reinterpret_cast<const float *>(reinterpret_cast<const uint16_t *>(p) + g * gs))
+                        : rsrc(p + g * gs);
                 lda = ld;
                 kbase = kb;
             }
@@ -1058,7 +1060,7 @@ __global__ __launch_bounds__(512) void dense_fwd_big_kernel(GemmArgs a) {
             const int row = i0 + lr + 64 * j;
             const bool ok = kin & (row < a.I);
             if constexpr (AH) {  // 8 consecutive 16-bit inputs: one load, no rounding
-                xa[j][0] = __builtin_amdgcn_raw_buffer_load_b128(ra, ok ? (row * lda + k) * 2 : BUF_OOB, 0, 0);
+                xa[j][0] = __builtin_amdgcn_raw_buffer_load_b128(ra, ok ? (row * lda + k - kbase) * 2 : BUF_OOB, 0, 0);
             } else {
                 const int off = (row * lda + k - kbase) * 4;
                 xa[j][0] = __builtin_amdgcn_raw_buffer_load_b128(ra, ok ? off : BUF_OOB, 0, 0);
@@ -1196,10 +1198,10 @@ void launch_fwd_big_p(const GemmArgs &a, dim3 grid, int bm, hipStream_t s) {
 #define FWD_BIG(EPv)                                                                                               \
     do {                                                                                                         \
         if (bm == 256) hipLaunchKernelGGL((dense_fwd_big_kernel<EPv, P, CAT, 256, 128>), grid, dim3(512), 0, s, a); \
-        else if (a.b16 && a.c16 && a.a16 && !CAT)                                                                \
-            hipLaunchKernelGGL((dense_fwd_big_kernel<EPv, P, CAT, 128, 256, true, !CAT, true>), grid, dim3(512), 0, s, a); \
+        else if (a.b16 && a.c16 && a.a16)                                                                        \
+            hipLaunchKernelGGL((dense_fwd_big_kernel<EPv, P, CAT, 128, 256, true, true, true>), grid, dim3(512), 0, s, a); \
         else if (a.b16 && a.a16 && !CAT)                                                                         \
-            hipLaunchKernelGGL((dense_fwd_big_kernel<EPv, P, CAT, 128, 256, true, !CAT, false>), grid, dim3(512), 0, s, a); \
+            hipLaunchKernelGGL((dense_fwd_big_kernel<EPv, P, CAT, 128, 256, true, true, false>), grid, dim3(512), 0, s, a); \
         else if (a.b16 && a.c16)                                                                                 \
             hipLaunchKernelGGL((dense_fwd_big_kernel<EPv, P, CAT, 128, 256, true, false, true>), grid, dim3(512), 0, s, a); \
         else if (a.b16)                                                                                          \

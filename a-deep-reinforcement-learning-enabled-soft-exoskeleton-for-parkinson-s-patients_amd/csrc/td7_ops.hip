@@ -47,7 +47,15 @@ __global__ __launch_bounds__(256) void avgl1_fwd_kernel(const float *__restrict_
 // load of a row in flight at once and no second read for the division (r03d:
 // the wide configuration's 65,536 x 1,024 norms).  Lane l still adds
 // |x[l]|, |x[l + 64]|, ... in that order: bit-identical to avgl1_fwd_kernel.
-template <int MAXJ>
+// OUT = 1 / 2 (td7_avgl1norm_fwd_h): y written as bf16 / fp16 bits (RNE), the
+// values an MFMA consumer rounds it to; s_out may then be null.
+template <int OUT>
+__device__ __forceinline__ void avgl1_store(float *y, long i, float v) {
+    if constexpr (OUT == 0) y[i] = v;
+    else if constexpr (OUT == 1) reinterpret_cast<uint16_t *>(y)[i] = __builtin_bit_cast(uint16_t, (__bf16)v);
+    else reinterpret_cast<uint16_t *>(y)[i] = __builtin_bit_cast(uint16_t, (_Float16)v);
+}
+template <int MAXJ, int OUT = 0>
 __global__ __launch_bounds__(256) void avgl1_fwd_reg_kernel(const float *__restrict__ x, float *__restrict__ y,
                                                             float *__restrict__ s_out, int rows, int cols, float eps) {
     const int r = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
@@ -63,11 +71,10 @@ __global__ __launch_bounds__(256) void avgl1_fwd_reg_kernel(const float *__restr
         if (lane + 64 * i < cols) acc += fabsf(v[i]);
     const float m = wave_sum(acc) / cols;
     const float s = fmaxf(m, eps);
-    float *yr = y + (size_t)r * cols;
 #pragma unroll
     for (int i = 0; i < MAXJ; ++i)
-        if (lane + 64 * i < cols) yr[lane + 64 * i] = v[i] / s;
-    if (lane == 0) s_out[r] = m;
+        if (lane + 64 * i < cols) avgl1_store<OUT>(y, (long)r * cols + lane + 64 * i, v[i] / s);
+    if (lane == 0 && s_out) s_out[r] = m;
 }
 
 __global__ __launch_bounds__(256) void avgl1_bwd_kernel(const float *__restrict__ x, const float *__restrict__ m_in,
@@ -250,6 +257,26 @@ int td7_avgl1norm_fwd(const float *x, float *y, float *mean_out, int32_t rows, i
                            cols, eps);
     else
         hipLaunchKernelGGL(avgl1_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, y, mean_out, rows, cols, eps);
+    return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
+}
+
+/* td7_avgl1norm_fwd writing y as 16-bit values (prec 1 = bf16, 2 = fp16 bits,
+ * round to nearest even) for an inference chain whose next layer rounds its
+ * input to that type anyway (bit-identical results, half the bytes);
+ * mean_out may be null.  256 < cols <= 1,024 (else EXO_ERANGE: use fp32). */
+int td7_avgl1norm_fwd_h(const float *x, uint16_t *y16, float *mean_out, int32_t rows, int32_t cols, float eps,
+                        int32_t prec, void *stream) {
+    if (!x || !y16 || rows < 0 || cols <= 0 || prec < 1 || prec > 2) return EXO_EINVAL;
+    if (cols <= 256 || cols > 1024) return EXO_ERANGE;
+    if (rows == 0) return EXO_OK;
+    const dim3 grid((rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK);
+    float *y = reinterpret_cast<float *>(y16);
+    if (prec == 1)
+        hipLaunchKernelGGL((avgl1_fwd_reg_kernel<16, 1>), grid, dim3(256), 0, (hipStream_t)stream, x, y, mean_out, rows,
+                           cols, eps);
+    else
+        hipLaunchKernelGGL((avgl1_fwd_reg_kernel<16, 2>), grid, dim3(256), 0, (hipStream_t)stream, x, y, mean_out, rows,
+                           cols, eps);
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 

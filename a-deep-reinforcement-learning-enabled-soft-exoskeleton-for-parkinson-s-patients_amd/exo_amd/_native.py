@@ -155,6 +155,8 @@ EXPORTS = {
     "td7_mse_fwd": (c_int32, [c_void_p, c_void_p, ctypes.c_int64, c_void_p, c_void_p, c_void_p]),
     "td7_mse_bwd": (c_int32, [c_void_p, c_void_p, c_void_p, ctypes.c_int64, c_void_p, c_void_p]),
     "td7_avgl1norm_fwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, ctypes.c_float, c_void_p]),
+    "td7_avgl1norm_fwd_h": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, ctypes.c_float, c_int32,
+                                      c_void_p]),
     "td7_avgl1norm_bwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, ctypes.c_float,
                                     c_void_p]),
     "td7_dense_fwd": (c_int32, [c_void_p, c_long, c_long, c_void_p, c_void_p, c_void_p, c_long, c_long,
@@ -174,7 +176,7 @@ EXPORTS = {
                                         c_void_p]),
     "td7_dense_fwd_h": (c_int32, [c_void_p, c_void_p, c_long, c_long, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_long, c_long, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p]),
-    "td7_dense_fwd_cat_h": (c_int32, [c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+    "td7_dense_fwd_cat_h": (c_int32, [c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                       c_void_p, c_long, c_long, c_int32, c_int32, c_int32, c_int32, c_void_p,
                                       c_void_p]),
     "td7_dense_bwd_weight_cat": (c_int32, [c_void_p, c_long, c_long, c_void_p, c_long, c_long, c_int32, c_void_p,

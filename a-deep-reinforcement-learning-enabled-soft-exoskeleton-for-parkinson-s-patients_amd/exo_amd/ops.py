@@ -347,10 +347,11 @@ _NORM = os.environ.get("EXO_TD7_NORM_FUSED", "1") != "0"
 _NORM_SMALL = os.environ.get("EXO_TD7_NORM_SMALL", "1") != "0"
 
 
-def dense_norm(parts, w, b):
+def dense_norm(parts, w, b, half_out=False):
     """AvgL1Norm(dense(torch.cat(parts, -1), w, b)) -- one fused launch on the
     GPU where it applies (N <= 320, the concatenated-input rules of
-    dense_cat); the two ops otherwise."""
+    dense_cat); the two ops otherwise.  half_out: as dense (an inference chain
+    at the large-layer sizes gets the norm as 16-bit values, avg_l1_norm_h)."""
     ok = (_NORM and w.is_cuda and w.dtype == torch.float32 and not torch.is_autocast_enabled()
           and w.shape[-2] <= 320 and (_matrix_prec or parts[0].shape[-2] <= _DenseFn.fwd_kernel_max_rows)
           and (_NORM_SMALL or parts[0].shape[-2] >= 2048))
@@ -366,7 +367,25 @@ def dense_norm(parts, w, b):
                                              or any(p.requires_grad for p in parts))
         return _DenseNormFn.apply(w, b, train, *parts)
     y = dense_cat(parts, w, b, 0) if len(parts) > 1 else dense(parts[0], w, b, 0)
+    if half_out and y.is_cuda and y.dtype == torch.float32 and y.dim() == 2 \
+            and _half_ok(y.shape[0], w.shape[-1], w.dim() == 3):
+        h = avg_l1_norm_h(y, _matrix_prec)
+        if h is not None:
+            return h
     return avg_l1_norm(y)
+
+
+def avg_l1_norm_h(y, prec, eps=1e-8):
+    """AvgL1Norm of fp32 rows as 16-bit values of the MFMA operand type
+    (td7_avgl1norm_fwd_h, no autograd), or None outside its width range."""
+    y = y.contiguous()
+    out = torch.empty(y.shape, dtype=_HALF[prec], device=y.device)
+    rc = nat.lib().td7_avgl1norm_fwd_h(nat.ptr(y), nat.ptr(out), None, y.shape[0], y.shape[1], float(eps), prec,
+                                       nat.stream_ptr(y.device))
+    if rc == EXO_ERANGE:
+        return None
+    nat.check(rc, "td7_avgl1norm_fwd_h")
+    return out
 
 
 def _cat_ok(parts, w):
@@ -391,6 +410,16 @@ def dense_cat(parts, w, b, act=0, half_out=False):
     """dense(torch.cat(parts, -1), w, b, act) reading the parts in place (parts
     of a grouped layer may be [G,M,k] or shared [M,k]).  Falls back to the
     concatenation where the fused kernels do not apply.  half_out: as dense."""
+    if w.dtype == torch.float32 and any(p.dtype in (torch.bfloat16, torch.float16) for p in parts):
+        # 16-bit parts (avg_l1_norm_h outputs on an inference chain): all of
+        # them read as 16-bit by the large-layer kernel, else as fp32 -- the same
+        # values, the consumer rounds them to the same type
+        if all(p.dtype == _HALF.get(_matrix_prec) for p in parts) and half_out \
+                and _half_ok(parts[0].shape[-2], w.shape[-1], w.dim() == 3):
+            y = _dense_cat_h(parts, w, b, act, xs16=True)
+            if y is not None:
+                return y
+        parts = [p.float() if p.dtype in (torch.bfloat16, torch.float16) else p for p in parts]
     if _CAT and w.is_cuda and w.dtype == torch.float32 and not torch.is_autocast_enabled() and _cat_ok(parts, w) \
             and (_matrix_prec or parts[0].shape[-2] <= _DenseFn.fwd_kernel_max_rows):
         if half_out and _half_ok(parts[0].shape[-2], w.shape[-1], w.dim() == 3):
@@ -405,8 +434,9 @@ def dense_cat(parts, w, b, act=0, half_out=False):
     return dense(torch.cat(parts, -1), w, b, act, concat_grad_cols(parts))
 
 
-def _dense_cat_h(parts, w, b, act):
-    """td7_dense_fwd_cat_h: the concatenated layer with a 16-bit output, or None."""
+def _dense_cat_h(parts, w, b, act, xs16=False):
+    """td7_dense_fwd_cat_h: the concatenated layer with a 16-bit output (and
+    16-bit parts when xs16), or None."""
     prec = _matrix_prec
     N, K = w.shape[-2], w.shape[-1]
     w = w.contiguous()
@@ -416,7 +446,7 @@ def _dense_cat_h(parts, w, b, act):
            (ctypes.c_long * n)(*[p.stride(-2) for p in parts]), (ctypes.c_int32 * n)(*[p.shape[-1] for p in parts]))
     y = torch.empty((M, N), dtype=_HALF[prec], device=w.device)
     bb = b.contiguous() if b is not None else None
-    rc = nat.lib().td7_dense_fwd_cat_h(n, *seg, nat.ptr(w), nat.ptr(bb), nat.ptr(y), M * N, N, 1, M, N,
+    rc = nat.lib().td7_dense_fwd_cat_h(n, seg[0], int(xs16), *seg[1:], nat.ptr(w), nat.ptr(bb), nat.ptr(y), M * N, N, 1, M, N,
                                        act | prec << 8, nat.ptr(_w16(w, prec, M, K)), nat.stream_ptr(w.device))
     if rc == EXO_ERANGE:
         return None

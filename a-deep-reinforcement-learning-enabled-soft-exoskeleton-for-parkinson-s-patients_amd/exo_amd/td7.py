@@ -117,9 +117,11 @@ class Actor(nn.Module):
             a = self.activ(self.l1(a))
             a = self.activ(self.l2(a))
             return torch.tanh(self.l3(a))
-        a = ops.dense_norm([state], self.l0.weight, self.l0.bias)
-        # inference at the wide configuration's sizes: l1's output handed to
-        # l2 as the 16-bit values l2 rounds it to (ops.dense half_out)
+        # inference at the wide configuration's sizes: l0's norm and l1's
+        # output handed on as the 16-bit values l1 / l2 round them to
+        # (ops.dense_norm / dense half_out; zs too when the caller asked
+        # Encoder.zs for it)
+        a = ops.dense_norm([state], self.l0.weight, self.l0.bias, half_out=True)
         a = ops.dense_cat([a, zs], self.l1.weight, self.l1.bias, act, half_out=True)
         a = ops.dense(a, self.l2.weight, self.l2.bias, act)
         return ops.dense(a, self.l3.weight, self.l3.bias, ops.ACT_CODES["tanh"])
@@ -138,7 +140,9 @@ class Encoder(nn.Module):
         self.zsa2 = nn.Linear(hdim, hdim)
         self.zsa3 = nn.Linear(hdim, zs_dim)
 
-    def zs(self, state):
+    def zs(self, state, half_out=False):
+        """half_out: at the large-layer inference sizes zs may come back as
+        16-bit values (for Actor.forward's [a | zs], select_action)."""
         act = ops.act_code(self.activ)
         if act is None:
             zs = self.activ(self.zs1(state))
@@ -146,7 +150,7 @@ class Encoder(nn.Module):
             return AvgL1Norm(self.zs3(zs))
         zs = ops.dense(state, self.zs1.weight, self.zs1.bias, act, half_out=True)  # see Actor.forward
         zs = ops.dense(zs, self.zs2.weight, self.zs2.bias, act, half_out=True)
-        return ops.dense_norm([zs], self.zs3.weight, self.zs3.bias)
+        return ops.dense_norm([zs], self.zs3.weight, self.zs3.bias, half_out=half_out)
 
     def zsa(self, zs, action):
         act = ops.act_code(self.activ)
@@ -994,10 +998,10 @@ class TD7Learner:
     def act(self, state, use_checkpoint=False):
         with self._autocast():
             if use_checkpoint:
-                zs = self.checkpoint_encoder.zs(state)
+                zs = self.checkpoint_encoder.zs(state, half_out=True)
                 a = self.checkpoint_actor(state, zs)
             else:
-                zs = self.fixed_encoder.zs(state)
+                zs = self.fixed_encoder.zs(state, half_out=True)
                 a = self.actor(state, zs)
         return a.float()
 

@@ -321,6 +321,11 @@ int lap_sample_gather_rng(const lap_tree_desc *t, const lap_storage_desc *st, ui
 /* y = x / max(mean|x|, eps) per row; mean_out[rows] keeps mean|x| for backward. */
 int td7_avgl1norm_fwd(const float *x_dev, float *y_dev, float *mean_out_dev, int32_t rows, int32_t cols, float eps,
                       void *stream);
+/* The same with y as 16-bit values (prec 1 = bf16, 2 = fp16 bits, RNE) for an
+ * inference chain whose next layer rounds its input to that type (bit-identical,
+ * half the bytes); mean_out may be null; 256 < cols <= 1,024, else EXO_ERANGE. */
+int td7_avgl1norm_fwd_h(const float *x_dev, uint16_t *y16_dev, float *mean_out_dev, int32_t rows, int32_t cols,
+                        float eps, int32_t prec, void *stream);
 /* gradient of the above w.r.t. x given dL/dy. */
 int td7_avgl1norm_bwd(const float *x_dev, const float *mean_dev, const float *gy_dev, float *gx_dev, int32_t rows,
                       int32_t cols, float eps, void *stream);
@@ -434,7 +439,9 @@ int td7_dense_fwd_cat_w16(int32_t nseg, const float *const *xs_dev, const long *
 int td7_dense_fwd_h(const float *x_dev, const uint16_t *x16_dev, long xsg, long ldx, const float *w_dev,
                     const float *b_dev, float *y_dev, uint16_t *y16_dev, long ysg, long ldy, int32_t groups, int32_t m,
                     int32_t n, int32_t k, int32_t act, const uint16_t *w16_dev, void *stream);
-int td7_dense_fwd_cat_h(int32_t nseg, const float *const *xs_dev, const long *xsg, const long *ldx,
+/* td7_dense_fwd_cat_h: xs16 = 1 takes every segment as 16-bit values (the
+ * AvgL1Norm outputs of td7_avgl1norm_fwd_h), 0 as fp32. */
+int td7_dense_fwd_cat_h(int32_t nseg, const void *const *xs_dev, int32_t xs16, const long *xsg, const long *ldx,
                         const int32_t *widths, const float *w_dev, const float *b_dev, uint16_t *y16_dev, long ysg,
                         long ldy, int32_t groups, int32_t m, int32_t n, int32_t act, const uint16_t *w16_dev,
                         void *stream);

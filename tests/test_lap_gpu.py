@@ -248,3 +248,40 @@ def test_wave_descent_and_subtree_rebuild_match_the_binary_tree():
         lap.sample()
         np.testing.assert_array_equal(lap.ind.cpu().numpy(), want)
         assert want.max() < size
+
+
+@pytest.mark.parametrize("C", [25_000, 5_000])
+def test_store_span_propagation_keeps_the_tree_exact(C):
+    """lap_store_rank_kernel (r03d): a stratum's new slots are one ring span
+    whose ancestors are recomputed once (propagate_span) -- over several
+    4,096-row chunks, ring wrap-around, and (C = 5,000) more rows in one call
+    than the ring holds.  Non-integer priorities already in the tree: every
+    internal node must be exactly left + right, the new leaves max_priority,
+    the others untouched, and ptr / size as the sequential ring."""
+    E, n = 3, 20_000
+    lap = _lap(E, C, 64)
+    rng = np.random.default_rng(11)
+    prio = rng.gamma(0.7, 2.0, (E, C)).astype(np.float32) + np.float32(1e-3)
+    _set_priorities(lap, prio)
+    p0 = lap.max_priority
+    want = prio.copy()
+    ptr, size = np.zeros(E, np.int64), np.zeros(E, np.int64)
+    for step in range(4):
+        strata = rng.integers(0, E, n).astype(np.int32)
+        active = rng.uniform(size=n) < 0.8
+        obs = torch.zeros(n, 80, device="cuda")
+        lap.add_batch(obs, torch.zeros(n, 7, device="cuda"), obs, torch.zeros(n, device="cuda"),
+                      torch.zeros(n, device="cuda"), torch.as_tensor(strata, device="cuda"),
+                      torch.as_tensor(active, device="cuda"))
+        for s in range(E):
+            k = int(np.sum((strata == s) & active))
+            want[s, (ptr[s] + np.arange(k)) % C] = p0
+            ptr[s] = (ptr[s] + k) % C
+            size[s] = min(size[s] + k, C)
+    np.testing.assert_array_equal(lap.ptr_s.cpu().numpy(), ptr)
+    np.testing.assert_array_equal(lap.size_s.cpu().numpy(), size)
+    np.testing.assert_array_equal(lap.priority.cpu().numpy(), want)
+    T = lap._tree.cpu().numpy()
+    cap = lap._cap
+    for s in range(E):
+        np.testing.assert_array_equal(T[s, 1:cap], T[s, 2:2 * cap:2] + T[s, 3:2 * cap:2])

@@ -508,8 +508,8 @@ def test_inference_chain_with_16bit_activations_is_bit_identical(prec):
     actor = Actor(80, 7, 1024, 1024).cuda()
     state = torch.randn(8192, 80, device="cuda")
 
-    def chain():
-        zs = enc.zs(state)
+    def chain(half_zs=False):
+        zs = enc.zs(state, half_out=half_zs)
         return zs, actor(state, zs)
 
     old = ops.W16_MIN_ROWS
@@ -519,6 +519,9 @@ def test_inference_chain_with_16bit_activations_is_bit_identical(prec):
             zs32, a32 = chain()
             ops.W16_MIN_ROWS = 8192
             zs16, a16 = chain()
+            # r03d: the AvgL1Norm outputs as 16-bit (td7_avgl1norm_fwd_h) and
+            # l1 reading both segments of [a | zs] as 16-bit (select_action)
+            zsh, ah = chain(half_zs=True)
             h = ops.dense(state, enc.zs1.weight, enc.zs1.bias, 2)
             assert ops.dense(h, enc.zs2.weight, enc.zs2.bias, 2, half_out=True).dtype != torch.float32
         with ops.matrix_precision(prec):
@@ -528,3 +531,6 @@ def test_inference_chain_with_16bit_activations_is_bit_identical(prec):
         ops.W16_MIN_ROWS = old
     assert zs16.dtype == a16.dtype == torch.float32
     assert torch.equal(zs16, zs32) and torch.equal(a16, a32)
+    half = torch.bfloat16 if prec == "bf16" else torch.float16
+    assert zsh.dtype == half and torch.equal(zsh, zs32.to(half))
+    assert ah.dtype == torch.float32 and torch.equal(ah, a32)

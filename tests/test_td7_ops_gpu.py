@@ -159,3 +159,22 @@ def test_avgl1norm_register_kernel_is_bit_identical(cols, monkeypatch):
         monkeypatch.setenv("EXO_AVGL1_REG", "0")
         y_old = avg_l1_norm(x)
     assert torch.equal(y_reg, y_old)
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_avgl1norm_16bit_output_is_the_rounded_fp32_norm(prec):
+    """td7_avgl1norm_fwd_h (r03d, select_action's AvgL1Norm outputs at the
+    wide sizes): the fp32 kernel's values rounded to nearest even, bit for
+    bit; outside 256 < cols <= 1,024 it answers EXO_ERANGE (None)."""
+    from exo_amd import ops
+    p = ops.PRECISIONS[prec]
+    half = torch.bfloat16 if prec == "bf16" else torch.float16
+    torch.manual_seed(3)
+    for cols in (1024, 520):
+        x = torch.randn(3001, cols, device="cuda") * torch.rand(3001, 1, device="cuda") ** 4
+        x[5] = 0.0
+        with torch.no_grad():
+            y = ops.avg_l1_norm(x)
+            h = ops.avg_l1_norm_h(x, p)
+        assert h.dtype == half and torch.equal(h, y.to(half))
+    assert ops.avg_l1_norm_h(torch.randn(64, 256, device="cuda"), p) is None
