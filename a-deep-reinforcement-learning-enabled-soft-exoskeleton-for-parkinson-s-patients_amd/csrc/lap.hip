@@ -63,6 +63,52 @@ __device__ void propagate(float *T, int cap, int levels, const int32_t *slot, in
     __syncthreads();
 }
 
+// The same recomputation for the leaves of a ring span: `count` consecutive
+// slots from `first`, wrapping at `capacity` (all of them once count reaches
+// it).  The ancestors of a contiguous leaf range at one level are a contiguous
+// node range, so each level is a loop over (at most two) node ranges instead
+// of a per-slot list; the nodes recomputed, and every sum, are the ones
+// propagate computes for the same slots.
+__device__ void propagate_span(float *T, int cap, int levels, int capacity, int first, int count) {
+    __shared__ float top[TOPN];
+    if (count <= 0) return;
+    int a0 = first, e0 = first + count, a1 = 0, e1 = 0;  // [a0, e0) and [a1, e1)
+    if (count >= capacity) {
+        a0 = 0;
+        e0 = capacity;
+    } else if (e0 > capacity) {
+        e1 = e0 - capacity;
+        e0 = capacity;
+    }
+    int lv = 1;
+    for (; lv <= levels && ((2 * cap) >> lv) > TOPN / 2; ++lv) {
+        __syncthreads();
+        const int lo0 = (cap + a0) >> lv, n0 = ((cap + e0 - 1) >> lv) - lo0 + 1;
+        const int lo1 = (cap + a1) >> lv, n1 = e1 > a1 ? ((cap + e1 - 1) >> lv) - lo1 + 1 : 0;
+        for (int k = threadIdx.x; k < n0 + n1; k += blockDim.x) {
+            const int node = k < n0 ? lo0 + k : lo1 + k - n0;
+            T[node] = T[2 * node] + T[2 * node + 1];
+        }
+    }
+    __syncthreads();
+    if (lv > levels) return;
+    const int lim = min(TOPN, 2 * cap);
+    for (int i = threadIdx.x; i < lim; i += blockDim.x) top[i] = T[i];
+    for (; lv <= levels; ++lv) {
+        __syncthreads();
+        const int lo0 = (cap + a0) >> lv, n0 = ((cap + e0 - 1) >> lv) - lo0 + 1;
+        const int lo1 = (cap + a1) >> lv, n1 = e1 > a1 ? ((cap + e1 - 1) >> lv) - lo1 + 1 : 0;
+        for (int k = threadIdx.x; k < n0 + n1; k += blockDim.x) {
+            const int node = k < n0 ? lo0 + k : lo1 + k - n0;
+            top[node] = top[2 * node] + top[2 * node + 1];
+        }
+    }
+    __syncthreads();
+    const int wb = min(TOPN / 2, cap);
+    for (int i = 1 + threadIdx.x; i < wb; i += blockDim.x) T[i] = top[i];
+    __syncthreads();
+}
+
 // LAP.add: new items get max_priority (:56-57).  The items of this block's
 // stratum are gathered in chunks of ADD_CHUNK into LDS, their leaves written,
 // then their ancestors recomputed.
@@ -203,29 +249,43 @@ __global__ void lap_init_kernel(float *maxp) { *maxp = 1.0f; } // max_priority =
 // stratum s go to consecutive ring slots starting at ptr[s], in env order.
 // Phase 1 (one workgroup per stratum): block scan of "row i is active and in
 // stratum s" -> slot of every row (the trash row `capacity` for inactive ones),
-// new leaves = max_priority and their ancestors, ring pointer and size.
+// new leaves = max_priority, ring pointer and size; the stratum's new slots are
+// one ring span, whose ancestors are recomputed once after the last chunk
+// (propagate_span; r03d: a propagate per 4,096-row chunk made the 65,536-env
+// store 158 us).
 // Phase 2 (many workgroups): one wavefront per row copies its transition.
 constexpr int STORE_CHUNK = UPD_THREADS * 4;
 
+template <int RANK_RPT>
 __global__ __launch_bounds__(UPD_THREADS) void lap_store_rank_kernel(float *tree, const float *maxp, int cap,
                                                                      int levels, int capacity, int32_t *ring_ptr,
                                                                      int32_t *ring_size, const int32_t *strata,
                                                                      const uint8_t *active, int n, int32_t *row_of) {
     const int s = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
     float *T = stratum_tree(tree, s, cap);
-    __shared__ int32_t mine[STORE_CHUNK];
     __shared__ int wsum[UPD_THREADS / 64];
     __shared__ int chunk_total;
     const float p = *maxp;
     const int ptr0 = ring_ptr[s];
     const int row0 = s * (capacity + 1);
     int offset = 0; // rows of this stratum placed by earlier chunks
-    for (int base = 0; base < n; base += STORE_CHUNK) {
-        int f[4], cnt = 0;
+    // RANK_RPT consecutive rows per thread (their strata kept in registers):
+    // 16 above 16,384 envs -- 4 chunks of 16,384 rows at 65,536 envs instead of
+    // 16 of 4,096, each chunk paying a load latency and two barriers -- and 4
+    // below (one chunk at 4,096 envs either way; 16 serial rows per thread
+    // measured 16.2 vs 15.0 us there, profiles/r03d_raw/lap2)
+    for (int base = 0; base < n; base += RANK_RPT * UPD_THREADS) {
+        int st[RANK_RPT], cnt = 0;
+        bool f[RANK_RPT];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int i = base + 4 * t + k;
-            f[k] = (i < n && strata[i] == s && (!active || active[i])) ? 1 : 0;
+        for (int k = 0; k < RANK_RPT; ++k) {
+            const int i = base + RANK_RPT * t + k;
+            st[k] = i < n ? strata[i] : -1;
+            f[k] = i < n && (!active || active[i]);
+        }
+#pragma unroll
+        for (int k = 0; k < RANK_RPT; ++k) {
+            f[k] = f[k] && st[k] == s;
             cnt += f[k];
         }
         // block-wide exclusive scan of cnt
@@ -249,15 +309,15 @@ __global__ __launch_bounds__(UPD_THREADS) void lap_store_rank_kernel(float *tree
         __syncthreads();
         int rank = offset + wsum[wv] + incl - cnt;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int i = base + 4 * t + k;
-            if (i < n && s == 0 && (strata[i] < 0 || strata[i] >= (int)gridDim.x)) row_of[i] = -1; // no stratum
-            if (i >= n || strata[i] != s) continue;
+        for (int k = 0; k < RANK_RPT; ++k) {
+            const int i = base + RANK_RPT * t + k;
+            if (i >= n) continue;
+            if (s == 0 && (st[k] < 0 || st[k] >= (int)gridDim.x)) row_of[i] = -1; // no stratum
+            if (st[k] != s) continue;
             if (f[k]) {
                 const int slot = (ptr0 + rank) % capacity;
                 row_of[i] = row0 + slot;
                 T[cap + slot] = p;
-                mine[rank - offset] = slot;
                 ++rank;
             } else {
                 row_of[i] = row0 + capacity; // inactive env: the trash row
@@ -265,9 +325,9 @@ __global__ __launch_bounds__(UPD_THREADS) void lap_store_rank_kernel(float *tree
         }
         const int total = chunk_total;
         __syncthreads();
-        propagate(T, cap, levels, mine, min(total, STORE_CHUNK));
         offset += total;
     }
+    propagate_span(T, cap, levels, capacity, ptr0, offset);
     if (t == 0) {
         ring_ptr[s] = (ptr0 + offset) % capacity;
         ring_size[s] = min(ring_size[s] + offset, capacity);
@@ -551,9 +611,14 @@ int lap_store_batch(const lap_tree_desc *t, const lap_storage_desc *st, const fl
         !reward || !done || !strata || !row_ws || n < 0 || action_scale == 0.0f)
         return EXO_EINVAL;
     if (n == 0) return EXO_OK;
-    hipLaunchKernelGGL(lap_store_rank_kernel, dim3(t->n_strata), dim3(UPD_THREADS), 0, (hipStream_t)stream, t->tree,
-                       t->max_priority, t->cap, levels_of(t), t->capacity, st->ptr, st->size, strata, active, n,
-                       row_ws);
+    if (n > 4 * STORE_CHUNK)
+        hipLaunchKernelGGL(lap_store_rank_kernel<16>, dim3(t->n_strata), dim3(UPD_THREADS), 0, (hipStream_t)stream,
+                           t->tree, t->max_priority, t->cap, levels_of(t), t->capacity, st->ptr, st->size, strata,
+                           active, n, row_ws);
+    else
+        hipLaunchKernelGGL(lap_store_rank_kernel<4>, dim3(t->n_strata), dim3(UPD_THREADS), 0, (hipStream_t)stream,
+                           t->tree, t->max_priority, t->cap, levels_of(t), t->capacity, st->ptr, st->size, strata,
+                           active, n, row_ws);
     if (hipGetLastError() != hipSuccess) return EXO_EDEVICE;
     hipLaunchKernelGGL(lap_store_copy_kernel, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, *st, state,
                        action, next_state, reward, done, action_scale, n, row_ws);
