@@ -621,16 +621,21 @@ __global__ void eval_metrics_kernel(Dev S, const float *__restrict__ info, const
 // train.py:123-125: an env steps while its motion lasts): the step counter k
 // (device int64) advances by one, saturating at rows - 1, and row k of the
 // [rows][n] table is copied to active -- one single-workgroup launch inside
-// the captured iteration, safe however many times a graph is replayed.
+// the captured iteration, safe however many times a graph is replayed.  With
+// score != nullptr the step's episode scores are accumulated first from the
+// mask being replaced (:144, score += reward where the env stepped: float32
+// reward into the float64 score, the value torch's where + add_ produce).
 __global__ __launch_bounds__(1024) void active_advance_kernel(const uint8_t *__restrict__ table, int rows, int n,
                                                               long long *k, uint8_t *__restrict__ active,
-                                                              int32_t *count) {
+                                                              int32_t *count, const float *__restrict__ rew,
+                                                              double *__restrict__ score) {
     __shared__ int wsum[16];
     const long long k0 = *k;
     const long long kk = k0 + 1 < rows ? k0 + 1 : rows - 1;
     int c = 0;
     for (int e = threadIdx.x; e < n; e += blockDim.x) {
         const uint8_t v = table[(size_t)kk * n + e];
+        if (score) score[e] += active[e] ? (double)rew[e] : 0.0;
         active[e] = v;
         c += v != 0;
     }
@@ -1128,7 +1133,15 @@ int exo_active_advance(const uint8_t *table_dev, int32_t rows, int32_t n, int64_
                        int32_t *count_dev, void *stream) {
     if (!table_dev || !k_dev || !active_dev || rows <= 0 || n <= 0) return EXO_EINVAL;
     hipLaunchKernelGGL(active_advance_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, table_dev, rows, n,
-                       (long long *)k_dev, active_dev, count_dev);
+                       (long long *)k_dev, active_dev, count_dev, (const float *)nullptr, (double *)nullptr);
+    return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
+}
+
+int exo_active_advance_score(const uint8_t *table_dev, int32_t rows, int32_t n, int64_t *k_dev, uint8_t *active_dev,
+                             int32_t *count_dev, const float *reward_dev, double *score_dev, void *stream) {
+    if (!table_dev || !k_dev || !active_dev || !reward_dev || !score_dev || rows <= 0 || n <= 0) return EXO_EINVAL;
+    hipLaunchKernelGGL(active_advance_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, table_dev, rows, n,
+                       (long long *)k_dev, active_dev, count_dev, reward_dev, score_dev);
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 

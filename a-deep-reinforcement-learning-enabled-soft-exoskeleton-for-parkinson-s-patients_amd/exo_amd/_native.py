@@ -124,6 +124,8 @@ EXPORTS = {
     "exo_set_tremor_model": (c_int32, [c_void_p, c_void_p, c_int32]),
     "exo_set_step_clock": (c_int32, [c_void_p, c_void_p, c_void_p]),
     "exo_active_advance": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "exo_active_advance_score": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                           c_void_p]),
     "exo_eval_metrics": (c_int32, [c_void_p, c_void_p, c_void_p, c_double, c_double, c_void_p, c_void_p]),
     "lap_tree_floats": (c_int32, [c_int32, c_int32]),
     "lap_init": (c_int32, [c_void_p, c_void_p]),

@@ -232,8 +232,16 @@ class VecTrainer:
         self._advance()
         self.last_actions = act
 
-    def _advance(self):
-        """The next step's active mask and count on the device (exo_active_advance)."""
+    def _advance(self, rew=None, score=None):
+        """The next step's active mask and count on the device (exo_active_advance);
+        with rew / score: score += rew where the replaced mask is set, in the same
+        launch (exo_active_advance_score)."""
+        if score is not None:
+            nat.check(nat.lib().exo_active_advance_score(
+                nat.ptr(self._table_ext), self._table_ext.shape[0], self.n, nat.ptr(self.k_dev), nat.ptr(self.active),
+                nat.ptr(self.active_count), nat.ptr(rew), nat.ptr(score), nat.stream_ptr(self.device)),
+                "exo_active_advance_score")
+            return
         nat.check(nat.lib().exo_active_advance(nat.ptr(self._table_ext), self._table_ext.shape[0], self.n,
                                                nat.ptr(self.k_dev), nat.ptr(self.active), nat.ptr(self.active_count),
                                                nat.stream_ptr(self.device)), "exo_active_advance")
@@ -532,14 +540,21 @@ class RefScheduleTrainer(VecTrainer):
         # 4,096-env rollout round, profiles/r03_refsched_raw): the select_action
         # workgroups hold every CU, so the overlapped insert kernels wait for
         # CUs (lap_add 9 -> 34 us) and the next env step waits for them
+        # EXO_REF_ROUND_GRAPH=2 (round_graph="serial"): the round graph with each
+        # step's insert in line (no branch), so the only change from the per-step
+        # replays is one graph launch per round instead of one per step
         if round_graph is None:  # EXO_REF_ROUND_GRAPH=1: the round graph
-            round_graph = os.environ.get("EXO_REF_ROUND_GRAPH", "0") == "1"
+            round_graph = {"1": True, "2": "serial"}.get(os.environ.get("EXO_REF_ROUND_GRAPH", "0"), False)
         self.round_graph = bool(round_graph)
+        self.round_overlap = round_graph != "serial"
         self._ins_stream = None
         self._ins_pending = False
         self._act_prev = torch.zeros((2, self.n), dtype=torch.bool, device=dev)
         self._round_graphs = {}
         self._eager_kinds = set()
+        # the episode scores (:144) accumulated inside the mask advance launch;
+        # EXO_REF_FUSED_SCORE=0: torch's where + add_ (2 launches per step)
+        self.fused_score = os.environ.get("EXO_REF_FUSED_SCORE", "1") == "1"
 
     # ------------------------------------------------------------ rollout
     def _seen_eager(self, random):
@@ -561,7 +576,8 @@ class RefScheduleTrainer(VecTrainer):
             cur.wait_stream(self._ins_stream)
             self._ins_pending = False
         nobs, rew, done, info = self.env.step(act, active=self.active, out=self._outs[self._cur])
-        self.score.add_(rew.where(self.active, 0.0))  # :144 (float32 into the float64 score, 2 launches)
+        if not self.fused_score:
+            self.score.add_(rew.where(self.active, 0.0))  # :144 (float32 into the float64 score, 2 launches)
         add = ag.replay_buffer.add_batch_ref if self.ref_replay else ag.replay_buffer.add_batch
         if overlap:
             mask = self._act_prev[self._cur]
@@ -574,7 +590,10 @@ class RefScheduleTrainer(VecTrainer):
             self._ins_pending = True
         else:
             add(obs, act, nobs, rew, done, self.strata, self.active)  # :142
-        self._advance()
+        if self.fused_score:  # :144 in the mask advance (the insert above read the mask first)
+            self._advance(rew, self.score)
+        else:
+            self._advance()
         self.last_actions = act
 
     def _roll_round(self, random):
@@ -590,7 +609,7 @@ class RefScheduleTrainer(VecTrainer):
             with torch.cuda.stream(s):
                 with torch.cuda.graph(g, stream=s), ForkJoinAudit(s):
                     for _ in range(self.round_len):
-                        self._rollout_ref(random, overlap=True)
+                        self._rollout_ref(random, overlap=self.round_overlap)
                         self._cur ^= 1
                     if self._ins_pending:
                         s.wait_stream(self._ins_stream)

@@ -219,6 +219,13 @@ int exo_tremor_metrics(exo_ctx *c, const float *info_dev, const uint8_t *stepped
  * script makes at that step (:125-128).  Graph-capturable, no host sync. */
 int exo_active_advance(const uint8_t *table_dev, int32_t rows, int32_t n, int64_t *k_dev, uint8_t *active_dev,
                        int32_t *count_dev, void *stream);
+/* exo_active_advance that first adds this step's rewards into the episode
+ * scores of the envs active under the mask it replaces:
+ * score_dev[e] (float64) += active_dev[e] ? reward_dev[e] (float32) : 0.0
+ * (Simulation/Exoskeleton_agent_train.py:144 `score[i] += reward`), one launch
+ * instead of torch's where + add_. */
+int exo_active_advance_score(const uint8_t *table_dev, int32_t rows, int32_t n, int64_t *k_dev, uint8_t *active_dev,
+                             int32_t *count_dev, const float *reward_dev, double *score_dev, void *stream);
 
 int exo_eval_metrics(exo_ctx *c, const float *info_dev, const uint8_t *stepped_dev, double humerus_length,
                      double forearm_length, float *counters_dev, void *stream);

@@ -201,7 +201,7 @@ def test_round_graph_rollout_matches_per_step_rollout():
     from exo_amd.rollout import RefScheduleTrainer
     from exo_amd.td7 import Agent, Hyperparameters
     outs = []
-    for rg in (False, True):
+    for rg in (False, True, "serial"):
         torch.manual_seed(3)
         N = 32
         env = VecExoskeletonEnv(N, seed=9)
@@ -221,12 +221,41 @@ def test_round_graph_rollout_matches_per_step_rollout():
              for p in m.parameters()]
         obs = tr.obs.clone()
         outs.append((st, w, scores, obs, [t["training_steps"] for t in tr.trace]))
-    a, b = outs
-    assert a[4] == b[4]
-    for k in a[0]:
-        torch.testing.assert_close(a[0][k], b[0][k], rtol=0, atol=0, msg=f"replay {k}")
-    for x, y in zip(a[1], b[1]):
+    a = outs[0]
+    for b in outs[1:]:  # the branch-overlapped and the serial ("serial": inserts in line) round graphs
+        assert a[4] == b[4]
+        for k in a[0]:
+            torch.testing.assert_close(a[0][k], b[0][k], rtol=0, atol=0, msg=f"replay {k}")
+        for x, y in zip(a[1], b[1]):
+            torch.testing.assert_close(x, y, rtol=0, atol=0)
+        for x, y in zip(a[2], b[2]):
+            torch.testing.assert_close(x, y, rtol=0, atol=0)
+        torch.testing.assert_close(a[3], b[3], rtol=0, atol=0)
+
+
+def test_fused_score_matches_torch_where_add():
+    """The episode scores accumulated inside the mask-advance launch
+    (exo_active_advance_score) are bit-identical to torch's
+    score.add_(rew.where(active, 0.0)) (Exoskeleton_agent_train.py:144), over
+    a random and a policy round with envs finishing at different steps."""
+    from exo_amd import VecExoskeletonEnv
+    from exo_amd.rollout import RefScheduleTrainer
+    from exo_amd.td7 import Agent, Hyperparameters
+    outs = []
+    for fused in (False, True):
+        torch.manual_seed(5)
+        N = 24
+        env = VecExoskeletonEnv(N, seed=4)
+        agent = Agent(80, 7, 1, hp=Hyperparameters(batch_size=32), learning_steps=100000, env_num=E,
+                      buffer_size=2 * BUF, precision="bf16", n_envs=N, graph_safe=True)
+        tr = RefScheduleTrainer(env, agent, warmup=1)
+        tr.fused_score = fused
+        scores = []
+        for _ in range(3):
+            tr.run_round()
+            scores.append(tr.score.clone())
+        torch.cuda.synchronize()
+        outs.append((scores, [t["ep_return"] for t in tr.trace]))
+    for x, y in zip(outs[0][0], outs[1][0]):
         torch.testing.assert_close(x, y, rtol=0, atol=0)
-    for x, y in zip(a[2], b[2]):
-        torch.testing.assert_close(x, y, rtol=0, atol=0)
-    torch.testing.assert_close(a[3], b[3], rtol=0, atol=0)
+    assert outs[0][1] == outs[1][1]
