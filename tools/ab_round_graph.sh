@@ -6,7 +6,7 @@ set -o pipefail
 O=gpurun_out/${1:-ab_rg}
 mkdir -p $O
 timeout -k 10 240 python -u -m pytest tests/test_ref_schedule_gpu.py -x -q --timeout 200 --timeout-method thread > $O/test.log 2>&1 || exit 1
-for i in 1 2 3; do
+for i in $(seq 1 ${2:-3}); do
   for v in 0:0 0:1 2:1 1:1; do
     rg=${v%:*}; fs=${v#*:}
     EXO_REF_ROUND_GRAPH=$rg EXO_REF_FUSED_SCORE=$fs timeout -k 10 200 python bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-td7-variants > $O/b_${rg}_${fs}_$i.log 2>&1 || exit 1
