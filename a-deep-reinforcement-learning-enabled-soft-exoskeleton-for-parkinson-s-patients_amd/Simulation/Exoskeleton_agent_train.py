@@ -182,6 +182,7 @@ def train(args):
     allow_train = False
     steps_count, rounds = 0, 0
     scores, agent_rew, avg_agent_rew, std_score, median_tremor_sup = [], [], [], [], []
+    round_stats = []  # the global outputs of every round (:292-317), for comparisons
     sup_avg_hist = []
     observation = np.zeros((E, obs_dim))
     actions = np.zeros((E, act_dim))
@@ -254,6 +255,14 @@ def train(args):
             f"avg {np.nanmean(sup_avg):.3f}% median {np.nanmean(sup_med):.3f}%; angle suppression "
             f"{(nz_a.mean() if nz_a.size else 0.0):.3f}%, amplitude reduction in {occ_a:.2f}% of steps, "
             f"total amplitude suppression {(nz_tot.mean() if nz_tot.size else 0.0):.3f}%")
+        round_stats.append(dict(
+            avg_reward=float(np.mean(gotten)), reward_pct=float(np.mean(pct)), avg_rewards_pct=float(np.mean(avg_r)),
+            median_rewards_pct=float(np.median(avg_r)), tremor_reduction_occurrence=float(occ),
+            any_axis_reduction_pct=float(np.sum(stats.red_in_episode) / steps_per_round * 100),
+            overall_suppression_avg=float(np.nanmean(sup_avg)), overall_suppression_median=float(np.nanmean(sup_med)),
+            angle_suppression=float(nz_a.mean() if nz_a.size else 0.0), amplitude_reduction_occurrence=float(occ_a),
+            total_amplitude_suppression=float(nz_tot.mean() if nz_tot.size else 0.0),
+            suppression_avg_per_env=sup_avg.copy(), suppression_median_per_env=sup_med.copy()))
         std_score.append(np.std(avg_agent_rew[-100:], axis=0))
         median_tremor_sup.append(np.nanmean(sup_med))
 
@@ -265,7 +274,7 @@ def train(args):
     h, rem = divmod(int(time.time() - t_start), 3600)
     log(f"Script executed in {h} hours, {rem // 60} minutes, and {rem % 60} seconds.")
     return dict(agent=agent, steps=steps_count, rounds=rounds, scores=np.array(scores), agent_rew=agent_rew_a,
-                save_prefix=save_prefix)
+                save_prefix=save_prefix, round_stats=round_stats)
 
 
 if __name__ == "__main__":

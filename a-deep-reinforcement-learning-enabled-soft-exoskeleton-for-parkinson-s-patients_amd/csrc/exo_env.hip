@@ -504,7 +504,12 @@ __global__ void tremor_metrics_kernel(Dev S, const float *__restrict__ info, con
                                       double L1, double L2, int disregard, float *__restrict__ metrics,
                                       float *__restrict__ counters) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= S.N || (stepped && !stepped[e])) return;
+    if (e >= S.N) return;
+    if (stepped && !stepped[e]) {  // a done env's row of the step is zeros (:201-203); counters untouched
+        float4 *m4 = reinterpret_cast<float4 *>(metrics + (size_t)e * 16);
+        for (int j = 0; j < 4; ++j) m4[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        return;
+    }
     const float *in = info + (size_t)e * INFO;
     double tr[7], ta[7];
     for (int j = 0; j < 7; ++j) {

@@ -17,6 +17,8 @@
 // searchsorted_left(cumsum(p), u * sum(p)).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdint>
 #include <string>
 
 #include "philox.h"
@@ -438,6 +440,235 @@ __global__ __launch_bounds__(UPD_THREADS) void lap_store_ref_slots_kernel(int ca
     }
 }
 
+// r04: lap_store_batch_ref as ONE launch (the three
+// launches above cost ~28 us per 4,096-env step of the reference schedule).
+// Grid (E strata) x (K copy parts), 1024 threads.  Every workgroup ranks the
+// active rows (the same block scan, chunks of STORE_CHUNK rows) and keeps, for
+// ITS stratum, the rows in rank order (LDS).  The winner test needs no rank ->
+// stratum table: a row loses iff the next active row of the SAME stratum
+// shares its slot (the c-th add's slot depends only on ceil((count0 + c) / E),
+// so same-slot ranks are consecutive and all lie within [r, mr E - count0]).
+// Part 0 writes the winners' leaves (max_priority) and recomputes the span
+// [ptr0, last slot] of its stratum (propagate_span: nodes whose children did
+// not change are recomputed to the same sum); every part copies the winners
+// with stratum-row index = part (mod K).  The last workgroup out (ticket
+// ws[0]) advances the shared pointer and the strata's sampling size.
+// Bit-identical to the three launches (tests/test_lap_gpu.py).
+__device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+__device__ __forceinline__ void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
+
+template <bool VEC>
+__device__ __forceinline__ void copy_rows(const lap_storage_desc &st, const float *state, const float *action,
+                                          const float *next_state, const float *reward, const uint8_t *done,
+                                          float action_scale, const int32_t *ri, const int32_t *sl, int s,
+                                          int capacity, int j0, int step, int m, int t, int nt) {
+    const int sd = st.state_dim, ad = st.action_dim;
+    const int sdv = VEC ? sd / 4 : sd;        // state items per row (float4 or float)
+    const int per = 2 * sdv + ad + 2;         // state, next_state, action, reward, not_done
+    const int nrows = j0 < m ? (m - j0 + step - 1) / step : 0;
+    const int items = nrows * per;
+    constexpr int U = 4;  // items in flight per thread: loads first, then stores
+    for (int it0 = t; it0 < items; it0 += U * nt) {
+        float4 v[U];
+        long dst[U];
+        int kind[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int it = it0 + u * nt;
+            kind[u] = -1;
+            if (it >= items) continue;
+            const int q = it / per, c = it - q * per, j = j0 + q * step;
+            const int slot = sl[j];
+            if (slot < 0) continue;
+            const long r = (long)s * (capacity + 1) + slot;
+            const long i = ri[j];
+            if (c < 2 * sdv) {
+                const bool nx = c >= sdv;
+                const int e = nx ? c - sdv : c;
+                const float *src = (nx ? next_state : state) + i * sd;
+                if (VEC) {
+                    v[u] = ld4(src + 4 * e);
+                    dst[u] = r * sd + 4 * e;
+                } else {
+                    v[u].x = src[e];
+                    dst[u] = r * sd + e;
+                }
+                kind[u] = nx ? 1 : 0;
+            } else if (c < 2 * sdv + ad) {
+                const int e = c - 2 * sdv;
+                v[u].x = action[i * ad + e] / action_scale;
+                dst[u] = r * ad + e;
+                kind[u] = 2;
+            } else if (c == 2 * sdv + ad) {
+                v[u].x = reward[i];
+                dst[u] = r;
+                kind[u] = 3;
+            } else {
+                v[u].x = 1.0f - (done[i] ? 1.0f : 0.0f);
+                dst[u] = r;
+                kind[u] = 4;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            switch (kind[u]) {
+            case 0:
+                if (VEC) st4(st.state + dst[u], v[u]); else st.state[dst[u]] = v[u].x;
+                break;
+            case 1:
+                if (VEC) st4(st.next_state + dst[u], v[u]); else st.next_state[dst[u]] = v[u].x;
+                break;
+            case 2: st.action[dst[u]] = v[u].x; break;
+            case 3: st.reward[dst[u]] = v[u].x; break;
+            case 4: st.not_done[dst[u]] = v[u].x; break;
+            default: break;
+            }
+        }
+    }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(UPD_THREADS) void lap_store_ref_fused_kernel(
+    float *tree, const float *maxp, int cap, int levels, int capacity, int E, long long *ref, int32_t *ring_size,
+    lap_storage_desc st, const float *state, const float *action, const float *next_state, const float *reward,
+    const uint8_t *done, float action_scale, const int32_t *strata, const uint8_t *active, int n,
+    uint32_t *ticket) {
+    const int s = blockIdx.x, part = blockIdx.y, K = gridDim.y;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    __shared__ int wsum[UPD_THREADS / 64];
+    __shared__ int chunk_tot, chunk_m;
+    __shared__ int32_t rk[STORE_CHUNK], ri[STORE_CHUNK], sl[STORE_CHUNK];
+    __shared__ int carry_r, carry_i, carry_J, carry_slot;  // the chunk's last row of stratum s, decided later
+    float *T = stratum_tree(tree, s, cap);
+    const long long ptr0 = ref[0], count0 = ref[1], size0 = ref[2];
+    const long long m0 = mult_below(count0, E);
+    const float p = *maxp;
+    auto slot_of = [&](long long r) -> int {
+        long long v = ptr0 + (mult_below(count0 + r, E) - m0);
+        if (v >= capacity) v -= capacity;
+        if (v >= capacity) v %= capacity;
+        return (int)v;
+    };
+    if (t == 0) carry_r = -1;
+    int offset = 0, soff = 0;  // active rows / stratum-s rows before this chunk
+    for (int base = 0; base < n; base += STORE_CHUNK) {
+        int cnt = 0, gcnt = 0;
+        bool f[4], g[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = base + 4 * t + k;
+            const int sk = i < n ? strata[i] : -1;
+            f[k] = i < n && sk >= 0 && sk < E && (!active || active[i]);
+            g[k] = f[k] && sk == s;
+            cnt += f[k];
+            gcnt += g[k];
+        }
+        // block-wide exclusive scan of (cnt, gcnt) packed in one int (each <= STORE_CHUNK < 2^16)
+        int incl = cnt | (gcnt << 16);
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += v;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        if (t == 0) {
+            int acc = 0;
+            for (int k = 0; k < UPD_THREADS / 64; ++k) {
+                const int v = wsum[k];
+                wsum[k] = acc;
+                acc += v;
+            }
+            chunk_tot = acc & 0xFFFF;
+            chunk_m = acc >> 16;
+        }
+        __syncthreads();
+        const int ex = wsum[wv] + incl - (cnt | (gcnt << 16));
+        int rank = offset + (ex & 0xFFFF), j = ex >> 16;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (g[k]) {
+                rk[j] = rank;
+                ri[j] = base + 4 * t + k;
+                ++j;
+            }
+            rank += f[k];
+        }
+        __syncthreads();
+        const int m = chunk_m;
+        // the previous chunk's last row of stratum s: its successor is rk[0]
+        if (t == 0) {
+            carry_slot = -1;
+            if (carry_r >= 0 && m > 0) {
+                const long long mr = mult_below(count0 + carry_r, E);
+                if ((long long)rk[0] > mr * E - count0) {  // no same-slot successor: a winner
+                    carry_slot = slot_of(carry_r);
+                    if (part == 0) T[cap + carry_slot] = p;
+                }
+                carry_r = -1;
+            }
+        }
+        __syncthreads();
+        if (carry_slot >= 0 && wv == 0 && carry_J % K == part)
+            copy_rows<VEC>(st, state, action, next_state, reward, done, action_scale, &carry_i, &carry_slot, s,
+                           capacity, 0, 1, 1, lane, 64);
+        for (int jj = t; jj < m; jj += UPD_THREADS) {
+            const int r = rk[jj];
+            if (jj + 1 == m) {  // successor unknown until a later chunk (or none: a winner)
+                carry_r = r;
+                carry_i = ri[jj];
+                carry_J = soff + jj;
+                sl[jj] = -1;
+                continue;
+            }
+            const long long mr = mult_below(count0 + r, E);
+            const bool win = (long long)rk[jj + 1] > mr * E - count0;
+            const int slot = win ? slot_of(r) : -1;
+            sl[jj] = slot;
+            if (win && part == 0) T[cap + slot] = p;
+        }
+        __syncthreads();
+        // this part's share of the chunk's winners: stratum-row index = part (mod K)
+        const int j0 = ((part - soff) % K + K) % K;
+        copy_rows<VEC>(st, state, action, next_state, reward, done, action_scale, ri, sl, s, capacity, j0, K, m, t,
+                       UPD_THREADS);
+        offset += chunk_tot;
+        soff += m;
+        __syncthreads();
+    }
+    // the last row of stratum s has no successor: a winner
+    if (t == 0) {
+        carry_slot = -1;
+        if (carry_r >= 0) {
+            carry_slot = slot_of(carry_r);
+            if (part == 0) T[cap + carry_slot] = p;
+        }
+    }
+    __syncthreads();
+    if (carry_slot >= 0 && wv == 0 && carry_J % K == part)
+        copy_rows<VEC>(st, state, action, next_state, reward, done, action_scale, &carry_i, &carry_slot, s, capacity,
+                       0, 1, 1, lane, 64);
+    const int n_act = offset;
+    if (part == 0 && n_act > 0) {
+        __syncthreads();
+        const long long last = mult_below(count0 + n_act - 1, E) - m0;  // slots ptr0 .. ptr0 + last
+        propagate_span(T, cap, levels, capacity, (int)ptr0, (int)min(last + 1, (long long)capacity));
+    }
+    __syncthreads();
+    if (t == 0) {
+        __threadfence();
+        if (atomicAdd(ticket, 1u) == (uint32_t)(E * K - 1)) {  // every workgroup has read ref
+            const long long adv = mult_below(count0 + n_act, E) - m0;
+            const long long size = min(size0 + adv, (long long)capacity);
+            for (int q = 0; q < E; ++q) ring_size[q] = (int32_t)size;
+            ref[0] = (ptr0 + adv) % capacity;
+            ref[1] = count0 + n_act;
+            ref[2] = size;
+            *ticket = 0u;
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void lap_store_copy_kernel(lap_storage_desc st, const float *state,
                                                              const float *action, const float *next_state,
                                                              const float *reward, const uint8_t *done,
@@ -643,6 +874,33 @@ int lap_store_batch_ref(const lap_tree_desc *t, const lap_storage_desc *st, int6
     if (hipGetLastError() != hipSuccess) return EXO_EDEVICE;
     hipLaunchKernelGGL(lap_store_copy_kernel, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, *st, state,
                        action, next_state, reward, done, action_scale, n, row_of);
+    return rc(hipGetLastError());
+}
+
+int lap_store_batch_ref_fused(const lap_tree_desc *t, const lap_storage_desc *st, int64_t *ref_dev,
+                              const float *state, const float *action, const float *next_state, const float *reward,
+                              const uint8_t *done, const int32_t *strata, const uint8_t *active, float action_scale,
+                              int32_t n, uint32_t *ticket_dev, void *stream) {
+    if (!valid(t) || !st || !st->state || !st->action || !st->next_state || !st->reward || !st->not_done ||
+        !st->size || st->state_dim <= 0 || st->action_dim <= 0 || !ref_dev || !state || !action || !next_state ||
+        !reward || !done || !strata || !ticket_dev || n < 0 || action_scale == 0.0f)
+        return EXO_EINVAL;
+    if (n == 0) return EXO_OK;
+    const int E = t->n_strata;
+    const int K = std::max(1, std::min(16, (n + E * 256 - 1) / (E * 256)));
+    auto al16 = [](const void *p) { return ((uintptr_t)p & 15u) == 0; };
+    const bool vec = st->state_dim % 4 == 0 && al16(state) && al16(next_state) && al16(st->state) &&
+                     al16(st->next_state);
+    if (vec)
+        hipLaunchKernelGGL(lap_store_ref_fused_kernel<true>, dim3(E, K), dim3(UPD_THREADS), 0, (hipStream_t)stream,
+                           t->tree, t->max_priority, t->cap, levels_of(t), t->capacity, E, (long long *)ref_dev,
+                           st->size, *st, state, action, next_state, reward, done, action_scale, strata, active, n,
+                           ticket_dev);
+    else
+        hipLaunchKernelGGL(lap_store_ref_fused_kernel<false>, dim3(E, K), dim3(UPD_THREADS), 0, (hipStream_t)stream,
+                           t->tree, t->max_priority, t->cap, levels_of(t), t->capacity, E, (long long *)ref_dev,
+                           st->size, *st, state, action, next_state, reward, done, action_scale, strata, active, n,
+                           ticket_dev);
     return rc(hipGetLastError());
 }
 

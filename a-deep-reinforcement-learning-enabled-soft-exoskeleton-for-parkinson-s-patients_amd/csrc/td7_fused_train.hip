@@ -175,34 +175,66 @@ struct EncoderArgs {
     R32 H3, NZ, DY;
     int small_off;
     int lds_bytes;
+    // grid.y == 2 (r04): workgroup row 0 computes next_zs and publishes it
+    // here ([row tiles * 16][Z] fp32) with a per-tile flag; row 1 runs the rest
+    float *nz;
+    int32_t *flag;  // [row tiles]: 1 = published; the consumer clears it
 };
 
+// grid.y == 1: one workgroup per 16 rows runs the whole pass (next_zs first).
+// grid.y == 2 (r04): the no-grad next_zs chain (3 of the
+// pass's ~14 serial layers) runs on its own workgroup row: row 0 computes it
+// and publishes it to global memory (agent-scope release of a per-tile flag:
+// the two workgroups may sit on different XCDs' L2s), row 1 runs zs(s), zsa
+// and the backward and waits for the flag only at the mse gradient.  The
+// dispatcher issues the grid in order, so every producer is resident or done
+// before any consumer spins: no deadlock.  Same arithmetic in the same order:
+// bit-identical to grid.y == 1 (tests/test_fused_gpu.py).
 template <int P, int TH>
 __global__ __launch_bounds__(NTH) void encoder_kernel(EncoderArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int row0 = blockIdx.x * TR, B = a.B, Z = a.Z, He = a.He, tile = blockIdx.x;
     const long ld = a.ld;
+    const bool split = gridDim.y == 2, producer = split && blockIdx.y == 0;
     float *mean = (float *)(lds + a.small_off), *dot = mean + TR;
     int si = 0;
     FSTAMP(si);
     RowStage sns, sa, ss;
-    row_issue(sns, a.ns, a.S, a.S, row0, B);
-    row_issue(sa, a.a, a.A, a.A, row0, B);
-    row_issue(ss, a.s, a.S, a.S, row0, B);  // put after the next_zs pass
+    if (!split || producer) row_issue(sns, a.ns, a.S, a.S, row0, B);
+    if (!producer) {
+        row_issue(sa, a.a, a.A, a.A, row0, B);
+        row_issue(ss, a.s, a.S, a.S, row0, B);  // put after the next_zs pass
+    }
     u32x4 R[PD][TH];
     ring_fill(R, fwd_of(a.e[0]));
     zero_lds(lds, a.lds_bytes);
     __syncthreads();
-    row_put16<P>(lds, sns, a.X, 0, a.S, row0, B);
-    row_put16<P>(lds, sa, a.CATZ, Z, a.A, row0, B);
-    __syncthreads();
-    // next_zs = encoder.zs(next_state) under no_grad (:219-220) -> NZ (fp32)
-    layer_fwd<P, 1, TH>(lds, R, a.X, a.e[0], &a.e[1], a.act, a.H1, 0, NO32, nullptr, 0, row0, B, si);
-    layer_fwd<P, 1, TH>(lds, R, a.H1, a.e[1], &a.e[2], a.act, a.H2, 0, NO32, nullptr, 0, row0, B, si);
-    const GDesc z1 = fwd_of(a.e[0]);
-    layer_fwd<P, 1, TH>(lds, R, a.H2, a.e[2], &z1, ACT_NONE, NO16, 0, a.H3, nullptr, 0, row0, B, si);
-    norm_fwd<P>(lds, a.H3, Z, TR, 1e-8f, NO16, 0, NO16, 0, a.NZ, nullptr, 0, nullptr, nullptr, row0, B);
-    __syncthreads();
+    if (!split || producer) {
+        row_put16<P>(lds, sns, a.X, 0, a.S, row0, B);
+        if (!producer) row_put16<P>(lds, sa, a.CATZ, Z, a.A, row0, B);
+        __syncthreads();
+        // next_zs = encoder.zs(next_state) under no_grad (:219-220) -> NZ (fp32)
+        layer_fwd<P, 1, TH>(lds, R, a.X, a.e[0], &a.e[1], a.act, a.H1, 0, NO32, nullptr, 0, row0, B, si);
+        layer_fwd<P, 1, TH>(lds, R, a.H1, a.e[1], &a.e[2], a.act, a.H2, 0, NO32, nullptr, 0, row0, B, si);
+        const GDesc z1 = fwd_of(a.e[0]);
+        layer_fwd<P, 1, TH>(lds, R, a.H2, a.e[2], producer ? nullptr : &z1, ACT_NONE, NO16, 0, a.H3, nullptr, 0,
+                            row0, B, si);
+        norm_fwd<P>(lds, a.H3, Z, TR, 1e-8f, NO16, 0, NO16, 0, a.NZ, nullptr, 0, nullptr, nullptr, row0, B);
+        __syncthreads();
+        if (producer) {
+            float *dst = a.nz + (long)row0 * Z;
+            for (int k = threadIdx.x; k < TR * Z; k += NTH) {
+                const int r = k / Z, c = k - r * Z;
+                dst[k] = *p32(lds, a.NZ, r, c);
+            }
+            __threadfence();  // every thread's rows written back past its XCD's L2
+            __syncthreads();
+            if (threadIdx.x == 0) __hip_atomic_store(a.flag + tile, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+    } else {
+        row_put16<P>(lds, sa, a.CATZ, Z, a.A, row0, B);
+    }
     // zs = encoder.zs(state) (:222), pred_zs = encoder.zsa(zs, action) (:223)
     row_put16<P>(lds, ss, a.X, 0, a.S, row0, B);
     __syncthreads();
@@ -221,6 +253,21 @@ __global__ __launch_bounds__(NTH) void encoder_kernel(EncoderArgs a) {
     layer_fwd<P, 1, TH>(lds, R, a.H1, a.e[4], &a.e[5], a.act, a.H2, 0, NO32, a.y3, He, row0, B, si);
     save_xt(lds, a.H2, 0, He, a.xt[5].x, ld, TR, row0);
     layer_fwd<P, 1, TH>(lds, R, a.H2, a.e[5], &b6, ACT_NONE, NO16, 0, a.DY, nullptr, 0, row0, B, si);
+    if (split) {  // next_zs from this tile's producer
+        if (threadIdx.x == 0) {
+            while (__hip_atomic_load(a.flag + tile, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0)
+                __builtin_amdgcn_s_sleep(2);
+            __hip_atomic_store(a.flag + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
+        }
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const float *src = a.nz + (long)row0 * Z;
+        for (int k = threadIdx.x; k < TR * Z; k += NTH) {
+            const int r = k / Z, c = k - r * Z;
+            *p32(lds, a.NZ, r, c) = src[k];
+        }
+        __syncthreads();
+    }
     // d mse(pred, next_zs) / d pred = 2 (pred - next_zs) / (B zs_dim) (:226)
     for (int k = threadIdx.x; k < TR * Z; k += NTH) {
         const int r = k / Z, c = k - r * Z;
@@ -741,8 +788,10 @@ int td7f_critic(int32_t prec, const int32_t *act, const td7f_lin *critic, const 
 }
 
 int td7f_encoder(int32_t prec, const int32_t *act, const td7f_lin *enc, const float *s, const float *a,
-                 const float *ns, int32_t B, float *const *y, const td7f_xt *xt, int64_t ld, void *stream) {
-    if (!prec_ok(prec) || !act || !enc || !s || !a || !ns || !y || !xt || B <= 0 || ld < B || ld % 32)
+                 const float *ns, int32_t B, float *const *y, const td7f_xt *xt, int64_t ld, float *nz_ws,
+                 int32_t *flag_ws, void *stream) {
+    if (!prec_ok(prec) || !act || !enc || !s || !a || !ns || !y || !xt || B <= 0 || ld < B || ld % 32 ||
+        (!nz_ws) != (!flag_ws))
         return EXO_EINVAL;
     const int th = th_of(enc, 6);
     if ((th != 4 && th != 5) || !wb_ok(enc, 6) || !xt_ok(xt, 6)) return EXO_EINVAL;
@@ -781,7 +830,9 @@ int td7f_encoder(int32_t prec, const int32_t *act, const td7f_lin *enc, const fl
     const R32 sm = b.r32(1, 2 * TR);
     g.small_off = sm.off;
     g.lds_bytes = b.off;
-    return DISPATCH(prec, th, encoder_kernel, dim3((B + TR - 1) / TR), b.off, g, (hipStream_t)stream);
+    g.nz = nz_ws;
+    g.flag = flag_ws;
+    return DISPATCH(prec, th, encoder_kernel, dim3((B + TR - 1) / TR, nz_ws ? 2 : 1), b.off, g, (hipStream_t)stream);
 }
 
 int td7f_actor(int32_t prec, int32_t phase, const int32_t *act, const td7f_lin *actor, const td7f_lin *fenc,

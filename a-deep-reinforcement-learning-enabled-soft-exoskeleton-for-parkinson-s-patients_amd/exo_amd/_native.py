@@ -138,6 +138,9 @@ EXPORTS = {
                                   c_void_p, ctypes.c_float, c_int32, c_void_p, c_void_p]),
     "lap_store_batch_ref": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                       c_void_p, c_void_p, c_void_p, ctypes.c_float, c_int32, c_void_p, c_void_p]),
+    "lap_store_batch_ref_fused": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                            c_void_p, c_void_p, c_void_p, ctypes.c_float, c_int32, c_void_p,
+                                            c_void_p]),
     "lap_sample_gather_rng": (c_int32, [c_void_p, c_void_p, ctypes.c_uint64, ctypes.c_uint32, c_void_p, c_void_p,
                                         c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_void_p]),
@@ -212,7 +215,7 @@ EXPORTS = {
     "td7f_critic": (c_int32, [c_int32, P(c_int32), P(TD7FLin)] + [c_void_p] * 7 + [ctypes.c_float]
                     + [c_void_p] * 4 + [c_int32] * 3 + [c_void_p] * 4 + [P(TD7FXT), ctypes.c_int64, c_void_p]),
     "td7f_encoder": (c_int32, [c_int32, P(c_int32), P(TD7FLin), c_void_p, c_void_p, c_void_p, c_int32, P(c_void_p),
-                               P(TD7FXT), ctypes.c_int64, c_void_p]),
+                               P(TD7FXT), ctypes.c_int64, c_void_p, c_void_p, c_void_p]),
     "td7f_actor": (c_int32, [c_int32, c_int32, P(c_int32), P(TD7FLin), P(TD7FLin), P(TD7FLin), c_void_p, c_void_p,
                              c_int32, P(TD7FActorBufs), P(TD7FXT), ctypes.c_int64, c_void_p]),
     "td7f_wgrad": (c_int32, [c_int32, c_int32, P(TD7FWgJob), ctypes.c_int64, c_int32, c_void_p, c_void_p, c_int32,

@@ -10,6 +10,7 @@ FusedNets owns the packed copies of every net the update reads and the
 launch wrappers; TD7Learner routes its passes here when `fused` is on.
 """
 import ctypes
+import os
 
 import torch
 
@@ -235,22 +236,23 @@ class FusedNets:
 
     # ------------------------------------------------------------- passes
     @torch.no_grad()
-    def select(self, obs, scale=1.0, dec_count=None):
+    def select(self, obs, scale=1.0, dec_count=None, world=1):
         """select_action_batch with Gaussian exploration (one launch): actor(obs,
         fixed_encoder.zs(obs)) + N(0, exploration_noise) per element, clamped,
         times max_action; exploration_noise decreases once per env (dec_count:
         an int32 device scalar -- once per env counted there, the active envs
-        of a vectorised step)."""
+        of a vectorised step; times `world`, the data-parallel ranks stepping
+        as many envs each)."""
         L = self.L
         self.refresh("fixed_encoder", "actor")
         obs = obs.contiguous()
         n = obs.shape[0]
         out = torch.empty((n, L.actor.l3.out_features), dtype=torch.float32, device=obs.device)
+        dec = L.action_noise_decrease * world
         if dec_count is not None:
-            nz = self._noise(L._explore_rng, L.exploration_noise_t, L.action_noise_decrease, 0.0, scale,
-                             dec_count=dec_count)
+            nz = self._noise(L._explore_rng, L.exploration_noise_t, dec, 0.0, scale, dec_count=dec_count)
         else:
-            nz = self._noise(L._explore_rng, L.exploration_noise_t, L.action_noise_decrease * n, 0.0, scale)
+            nz = self._noise(L._explore_rng, L.exploration_noise_t, dec * n, 0.0, scale)
         fe, ac = self.nets["fixed_encoder"].layers, self.nets["actor"].layers
         nat.check(nat.lib().td7f_select(self.prec, self.act, _lin_array(fe[:3]), self.nets["actor"].array,
                                         nat.ptr(obs), n, ctypes.byref(nz), nat.ptr(out), nat.stream_ptr(obs.device)),
@@ -389,6 +391,10 @@ class FusedTrain:
         ajobs = [self._job(xb, act_p[2 * i].grad, act_p[2 * i + 1].grad, rt) for i, xb in enumerate(self.xt_actor)]
         self.jobs_a = (nat.TD7FWgJob * len(ajobs))(*ajobs)
         self.ptrs_y_enc = (P * 4)(*[t.data_ptr() for t in self.y_enc])
+        # the encoder pass with zs(s') on its own workgroup row (r04; EXO_ENC_SPLIT=0: one row)
+        self.enc_split = os.environ.get("EXO_ENC_SPLIT", "1") != "0"
+        self.enc_nz = torch.zeros((rt * 16, Z), **f32)
+        self.enc_flag = torch.zeros((rt,), dtype=torch.int32, device=dev)
 
     @staticmethod
     def _adam_descs(opt, layers):
@@ -439,9 +445,10 @@ class FusedTrain:
     def encoder(self, state, action, next_state):
         fz = self.nets
         fz.refresh("encoder")
+        nz, fl = (self.enc_nz, self.enc_flag) if self.enc_split else (None, None)
         nat.check(nat.lib().td7f_encoder(fz.prec, fz.act, fz.nets["encoder"].array, nat.ptr(state), nat.ptr(action),
                                          nat.ptr(next_state), self.B, self.ptrs_y_enc, self._xts(self.xt_enc), self.ld,
-                                         nat.stream_ptr(state.device)), "td7f_encoder")
+                                         nat.ptr(nz), nat.ptr(fl), nat.stream_ptr(state.device)), "td7f_encoder")
 
     def critic(self, state, action, zs, zsa, qt, reward, not_done):
         fz, L = self.nets, self.L

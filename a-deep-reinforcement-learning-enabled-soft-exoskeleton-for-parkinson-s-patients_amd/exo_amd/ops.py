@@ -684,6 +684,12 @@ class DeviceRNG:
         # [call number, ticket (uint32 in the low half)]
         self.state = torch.zeros((2,), dtype=torch.int64, device=device)
 
+    def fold(self, rank):
+        """A rank's own stream (data parallel): the key mixed with the rank."""
+        if rank:
+            self.seed = (self.seed ^ ((int(rank) * 0x94D049BB133111EB) & (2 ** 64 - 1))) & (2 ** 64 - 1)
+        return self
+
     @property
     def counter_ptr(self):
         return self.state.data_ptr()
@@ -699,7 +705,8 @@ def noisy_action(a, noise, sigma, sigma_dec, clip=0.0, scale=1.0, rng=None, dec_
     One td7_noisy_action launch on a GPU; the reference expressions on a CPU.
     noise=None: standard normal noise -- drawn inside the kernel from `rng`
     (a DeviceRNG) on a GPU, torch.randn_like on a CPU.  dec_count (int32
-    device scalar, GPU with rng): sigma -= sigma_dec * dec_count instead."""
+    device scalar): sigma -= sigma_dec * dec_count instead (in the noise
+    kernel with the device RNG; one more small launch with given / host noise)."""
     if noise is None and a.is_cuda:
         if rng is None:
             raise ValueError("noisy_action: noise=None needs a DeviceRNG on the GPU")
@@ -717,13 +724,19 @@ def noisy_action(a, noise, sigma, sigma_dec, clip=0.0, scale=1.0, rng=None, dec_
         if clip > 0:
             e = e.clamp(-clip, clip)
         out = (a + e).clamp(-1, 1) * scale
-        sigma -= sigma_dec
+        if dec_count is not None:
+            sigma -= sigma_dec * dec_count.to(sigma.dtype).reshape(sigma.shape)
+        else:
+            sigma -= sigma_dec
         return out
     a = a.contiguous()
     out = torch.empty_like(a)
-    nat.check(nat.lib().td7_noisy_action(nat.ptr(a), nat.ptr(noise.contiguous()), nat.ptr(sigma), float(sigma_dec),
+    nat.check(nat.lib().td7_noisy_action(nat.ptr(a), nat.ptr(noise.contiguous()), nat.ptr(sigma),
+                                         0.0 if dec_count is not None else float(sigma_dec),
                                          float(clip), float(scale), nat.ptr(out), a.numel(),
                                          nat.stream_ptr(a.device)), "td7_noisy_action")
+    if dec_count is not None:
+        sigma.sub_(dec_count.to(sigma.dtype).reshape(sigma.shape) * sigma_dec)
     return out
 
 

@@ -68,6 +68,7 @@ class LAP:
         # reference pointer of add_batch_ref: int64 {ptr, count, size} on the device
         self.ref_state = torch.zeros((3,), dtype=torch.int64, device=self.device)
         self._ref_ws = None
+        self.ref_insert_fused = os.environ.get("EXO_REF_INSERT_FUSED", "1") != "0"
         self._u = torch.empty((E, self.batch_size), **f32)
         # sample() draws its uniforms in the kernel (EXO_DEVICE_RNG=0: torch.rand + lap_sample_gather)
         from .ops import DeviceRNG
@@ -159,11 +160,13 @@ class LAP:
         script's per-env loop over one vectorised step -- with the reference's
         shared pointer (ref_state, device-resident): env 0's first transition
         one slot behind the others, a done env's slot re-used by the next adds,
-        one shared sampling size.  Three kernels, no host synchronisation
-        (lap_store_batch_ref)."""
+        one shared sampling size.  One kernel (lap_store_batch_ref_fused, r04;
+        EXO_REF_INSERT_FUSED=0: the three launches of lap_store_batch_ref), no
+        host synchronisation."""
         n = state.shape[0]
         if self._ref_ws is None or self._ref_ws.numel() < 3 * n:
-            self._ref_ws = torch.empty((3 * n,), dtype=torch.int32, device=self.device)
+            # zeroed: its first word is the fused launch's ticket (left zero)
+            self._ref_ws = torch.zeros((3 * n,), dtype=torch.int32, device=self.device)
 
         def f32(t, shape):
             t = t.to(device=self.device, dtype=torch.float32).reshape(shape)
@@ -180,11 +183,12 @@ class LAP:
         act = None
         if active is not None:
             act = (active.view(torch.uint8) if active.dtype == torch.bool else active.to(torch.uint8)).contiguous()
-        nat.check(nat.lib().lap_store_batch_ref(ctypes.byref(self._desc), ctypes.byref(self._store),
-                                                nat.ptr(self.ref_state), nat.ptr(st), nat.ptr(ac), nat.ptr(nx),
-                                                nat.ptr(rw), nat.ptr(dn), nat.ptr(sr), nat.ptr(act),
-                                                float(self.normalize_actions), n, nat.ptr(self._ref_ws),
-                                                self._stream()), "lap_store_batch_ref")
+        fn = "lap_store_batch_ref_fused" if self.ref_insert_fused else "lap_store_batch_ref"
+        nat.check(getattr(nat.lib(), fn)(ctypes.byref(self._desc), ctypes.byref(self._store),
+                                         nat.ptr(self.ref_state), nat.ptr(st), nat.ptr(ac), nat.ptr(nx),
+                                         nat.ptr(rw), nat.ptr(dn), nat.ptr(sr), nat.ptr(act),
+                                         float(self.normalize_actions), n, nat.ptr(self._ref_ws),
+                                         self._stream()), fn)
 
     def ref_pointer(self):
         """(ptr, count, size) of add_batch_ref (host sync)."""

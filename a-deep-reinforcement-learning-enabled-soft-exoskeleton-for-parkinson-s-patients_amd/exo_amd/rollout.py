@@ -9,10 +9,14 @@ and done envs stay idle until the longest motion ends.
 Everything inside an iteration is device work with no host synchronisation,
 so it is captured once into HIP graphs and replayed:
   * world == 1: one graph per policy-update parity (actor updated or not);
-  * world  > 1: the collectives (RCCL) run eagerly between graphs: the
-    encoder/critic gradient bucket after `pre` (rollout + grads), a MAX of
-    max_priority after `mid` (optimiser steps + priorities + actor grads),
-    the actor bucket before `post` (actor step).
+  * world  > 1 on RCCL: the same one graph with the collectives captured in
+    it (VecTrainer._inline): the encoder's gradient bucket all-reduced on the
+    encoder's branch, the critic's before its step, a MAX of max_priority
+    after the priority update, the actor's bucket before its step;
+  * world  > 1 on gloo (or EXO_DP_CAPTURE=0): the collectives run eagerly
+    between three graphs: the encoder/critic gradient bucket after `pre`
+    (rollout + grads), a MAX of max_priority after `mid` (optimiser steps +
+    priorities + actor grads), the actor bucket before `post` (actor step).
 Host-side bookkeeping left outside the graphs: the env reset at the end of a
 round, the target-network refresh every 250 steps (:284-293).
 """
@@ -50,6 +54,14 @@ def graph_reductions_ok(device, rows=1024, cols=300, replays=3):
                 "capture). Set DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 before the first GPU call -- importing "
                 "exo_amd before touching the GPU does it -- or use VecTrainer(use_graphs=False).")
     return True
+
+
+def _np_median(x):
+    """numpy's median of a 1-D tensor (the mean of the two middle values for
+    an even count; torch.median returns the lower one)."""
+    v = x.sort().values
+    n = v.numel()
+    return v[n // 2] if n % 2 else (v[n // 2 - 1] + v[n // 2]) / 2
 
 
 class CaptureForkError(RuntimeError):
@@ -201,7 +213,11 @@ class VecTrainer:
         self.iters = 0
         self.resets = 0  # episode-round resets done by step()
         self.graphs = {}
-        self.dp = agent.sync.active  # tests set it to exercise the 3-graph layout at world 1
+        self.dp = agent.sync.active  # tests set it to exercise the data-parallel layouts at world 1
+        # data parallel on RCCL: the collectives run inside the iteration's one
+        # graph (GradSync.graph_capturable; EXO_DP_CAPTURE=0 or gloo: three
+        # graphs per iteration with eager all-reduces between them)
+        self.dp_inline = bool(self.dp and use_graphs and agent.sync.graph_capturable(self.device))
         # the env step shares the GPU with the TD7 passes: packed into half the
         # CUs (512-thread workgroups) unless the caller chose a kernel variant.
         # Only where 'auto' runs the row-parallel kernel (N <= 16,384): above it
@@ -290,7 +306,7 @@ class VecTrainer:
         ag = self.agent
         # one GPU: the encoder's gradients and step stay on its branch, joined
         # at the end of the iteration (_join_prio)
-        ag.learner.defer_side_join = ENC_STEP_BRANCH and not self.dp
+        ag.learner.defer_side_join = ENC_STEP_BRANCH and (not self.dp or self.dp_inline)
         rb = ag.replay_buffer
         if not rollout:  # a training step alone (Agent.train): sample, then the gradients
             self._batch = rb.sample()
@@ -333,23 +349,37 @@ class VecTrainer:
     # the branch in every iteration, the r02 layout)
     prio_branch_all = os.environ.get("EXO_PRIO_BRANCH_ALL", "0") == "1"
 
-    def _mid(self, update_actor, flat_grad=None, grad_scale=1.0, rollout=True):
+    def _mid(self, update_actor, flat_grad=None, grad_scale=1.0, rollout=True, inline=False):
+        """inline (data parallel, collectives inside the iteration): the global
+        max_priority (MAX all-reduce, SURVEY 8e / TD7_buffer_multi_agent.py:116)
+        right after the priority update, on a branch joined at the end of the
+        iteration -- nothing before the next iteration's inserts reads it."""
         ag = self.agent
         self._pside = None
         self._mid_rollout = rollout
-        if self.prio_branch and not self.dp and (update_actor or self.prio_branch_all):
-            cur = torch.cuda.current_stream(self.device)
+        cur = torch.cuda.current_stream(self.device)
+
+        def prio_stream():
             if getattr(self, "_prio_stream", None) is None:
                 self._prio_stream = torch.cuda.Stream(device=self.device)
-            self._pside = self._prio_stream
+            return self._prio_stream
+        if self.prio_branch and (not self.dp or inline) and (update_actor or self.prio_branch_all):
+            self._pside = prio_stream()
             self._pside.wait_stream(cur)
             with torch.cuda.stream(self._pside):
                 ag.replay_buffer.update_priority(self._prio, self._ind)
+                if inline:
+                    ag.sync.max_(ag.replay_buffer._maxp)
                 self._sample_next()
             ag.learner.phase_steps(flat_grad, grad_scale)
         else:
             ag.learner.phase_steps(flat_grad, grad_scale)
             ag.replay_buffer.update_priority(self._prio, self._ind)
+            if inline:
+                self._pside = prio_stream()
+                self._pside.wait_stream(cur)
+                with torch.cuda.stream(self._pside):
+                    ag.sync.max_(ag.replay_buffer._maxp)
             self._sample_next()
         if update_actor:
             ag.learner.phase_actor_grads(self._batch[0], self._batch[1])
@@ -372,7 +402,30 @@ class VecTrainer:
         if update_actor:
             self.agent.learner.phase_actor_step(flat_grad, grad_scale)
 
+    def _inline(self, update_actor, rollout=True):
+        """One iteration with the data-parallel collectives in line (RCCL,
+        captured into the iteration's graph like every other launch): the
+        encoder bucket's AVG all-reduce on the encoder's branch (inside
+        phase_grads), the critic bucket's before the optimiser steps, the MAX
+        of max_priority after the priority update, the actor bucket's before
+        the actor's step.  All ranks capture the collectives in this one
+        order, each on the process group's stream."""
+        ag, L = self.agent, self.agent.learner
+        L.dp_inline = True
+        try:
+            self._pre(rollout)
+            flat_c = L.allreduce_phase_grads(self._batch[0].shape[0])
+            self._mid(update_actor, flat_c, 1.0, rollout, inline=True)
+            flat_a = L.allreduce_actor_grads() if update_actor else None
+            self._post(update_actor, flat_a, 1.0)
+            self._join_prio()
+        finally:
+            L.dp_inline = False
+
     def _eager(self, update_actor, rollout=True):
+        if self.dp_inline:
+            self._inline(update_actor, rollout)
+            return
         L = self.agent.learner
         self._pre(rollout)
         L.sync.allreduce_grads(L.grad_params())
@@ -394,13 +447,16 @@ class VecTrainer:
         pool = None  # one private pool per parity: the two parities replay in alternation
         parts = []
         with torch.cuda.stream(s):
-            if not self.dp:
+            if not self.dp or self.dp_inline:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=pool, stream=s), ForkJoinAudit(s):
-                    self._pre(rollout)
-                    self._mid(update_actor, rollout=rollout)
-                    self._post(update_actor)
-                    self._join_prio()
+                    if self.dp_inline:
+                        self._inline(update_actor, rollout)
+                    else:
+                        self._pre(rollout)
+                        self._mid(update_actor, rollout=rollout)
+                        self._post(update_actor)
+                        self._join_prio()
                 parts = [g]
             else:
                 # Each parity's graphs own their gradient buffers (set_to_none
@@ -431,7 +487,7 @@ class VecTrainer:
 
     def _replay(self, update_actor, rollout=True):
         parts = self.graphs[self._key(update_actor, rollout)]
-        if not self.dp:
+        if not self.dp or self.dp_inline:
             parts[0].replay()
             return
         S = self.agent.sync
@@ -506,7 +562,7 @@ class RefScheduleTrainer(VecTrainer):
     from injected draw streams) instead of exo_reset."""
 
     def __init__(self, env, agent, warmup=25_000, strata=None, use_graphs=True, ref_replay=True,
-                 action_source=None, reset_source=None, warmup_eager=2, round_graph=None):
+                 action_source=None, reset_source=None, warmup_eager=2, round_graph=None, stats=None):
         super().__init__(env, agent, strata=strata, use_graphs=use_graphs, warmup_eager=warmup_eager,
                          shared_step=False)
         # the rollout runs alone (no TD7 pass beside it): the env step's own fast shape
@@ -522,7 +578,11 @@ class RefScheduleTrainer(VecTrainer):
         self.updates = 0
         dev = self.device
         self.score = torch.zeros(self.n, dtype=torch.float64, device=dev)
-        self._rand_act = torch.zeros((self.n, 7), dtype=torch.float32, device=dev)
+        self._rand_act = torch.zeros((self.n, 7), dtype=torch.float32, device=dev)  # injected actions
+        # the warm-up's uniform actions, one buffer per observation parity: in
+        # the overlapped round graph step k's replay insert (on its branch)
+        # still reads step k's actions while step k+1 draws its own
+        self._rand_acts = torch.zeros((2, self.n, 7), dtype=torch.float32, device=dev)
         Ls = env.lengths_host
         self.ep_len = Ls - 2  # starts at 1 (:115), +1 per step (:145) for L-3 steps
         self.round_env_steps = int((Ls - 3).sum())
@@ -555,12 +615,80 @@ class RefScheduleTrainer(VecTrainer):
         # the episode scores (:144) accumulated inside the mask advance launch;
         # EXO_REF_FUSED_SCORE=0: torch's where + add_ (2 launches per step)
         self.fused_score = os.environ.get("EXO_REF_FUSED_SCORE", "1") == "1"
+        # the script's per-step tremor statistics (:149-205: exo_tremor_metrics
+        # into a [round_len, N, 16] device record + per-env counters, 2
+        # launches per step) and its per-round outputs (:213-317, round_stats()
+        # -> self.round_stats); stats=None: EXO_REF_STATS=1 turns them on
+        self.stats = (os.environ.get("EXO_REF_STATS", "0") == "1") if stats is None else bool(stats)
+        self.round_stats = []
+        self._stat_bufs = None
 
     # ------------------------------------------------------------ rollout
     def _seen_eager(self, random):
         """A round graph is captured only after a per-step round of the same
         kind (random / policy) allocated its buffers."""
-        return bool(random) in self._eager_kinds
+        return (bool(random), self.stats) in self._eager_kinds
+
+    def _stats_buffers(self):
+        if self._stat_bufs is None:
+            f32 = dict(dtype=torch.float32, device=self.device)
+            self._stat_bufs = (torch.zeros((self.n, 16), **f32), torch.zeros((self.round_len, self.n, 16), **f32),
+                               torch.zeros((self.n, 6), **f32))
+            self._pct_hist = []
+        return self._stat_bufs
+
+    def _step_stats(self, info):
+        """:149-200 for this step: the envs running at this step (the mask
+        before its advance) into row k of the round record, the counters
+        accumulated."""
+        step, rec, ctr = self._stats_buffers()
+        self.env.tremor_metrics(info, stepped=self.active, counters=ctr, out=step)
+        rec.index_copy_(0, self.k_dev, step.unsqueeze(0))
+
+    @torch.no_grad()
+    def compute_round_stats(self):
+        """The training script's per-round outputs (:213-317) from the round's
+        device record, over all N envs (the script's 8): per env the mean and
+        median of the non-zero torque suppressions within its first
+        max_length rows (:233-247), then the global line (:292-317).  One host
+        sync.  Returns a dict of floats."""
+        step, rec, ctr = self._stats_buffers()
+        dev = self.device
+        Ls = torch.as_tensor(self.env.lengths_host, device=dev)
+        T = self.round_len
+        inlen = torch.arange(T, device=dev)[:, None] < Ls[None, :]            # tred[:max_lengths[i], i]
+        tred = rec[..., 0:7].double()
+        ared = rec[..., 7:14].double()
+        tot = rec[..., 14].double()
+        v = torch.where(inlen[..., None] & (tred != 0), tred, torch.nan)      # [T, N, 7]
+        v = v.permute(1, 0, 2).reshape(self.n, -1)
+        cnt = (~v.isnan()).sum(1)
+        sup_avg = v.nansum(1) / cnt                                           # NaN for an env with none
+        srt = torch.sort(torch.where(v.isnan(), torch.inf, v), dim=1).values
+        lo = ((cnt - 1).clamp(min=0) // 2)[:, None]
+        hi = (cnt // 2).clamp(max=v.shape[1] - 1)[:, None]
+        sup_med = torch.where(cnt > 0, (srt.gather(1, lo)[:, 0] + srt.gather(1, hi)[:, 0]) / 2, torch.nan)
+        ep_len = torch.as_tensor(self.ep_len, device=dev, dtype=torch.float64)
+        gotten = self.score - 2.0                                             # score - initial_score (:215)
+        pct = gotten / ep_len * 100
+        self._pct_hist = (self._pct_hist + [pct])[-100:]
+        avg_r = torch.stack(self._pct_hist).mean(0)                           # mean of agent_rew[-100:] (:219)
+        nz_a, nz_t = ared[ared != 0], tot[tot != 0]
+        c = ctr.double().sum(0)
+        vals = torch.stack([
+            gotten.mean(), pct.mean(), avg_r.mean(), _np_median(avg_r),
+            c[1] / (c[0] + c[1]) * 100, c[2] / float(Ls.sum()) * 100,
+            sup_avg.nanmean(), sup_med.nanmean(),
+            nz_a.mean() if nz_a.numel() else torch.zeros((), dtype=torch.float64, device=dev),
+            c[4] / (c[3] + c[4]) * 100,
+            nz_t.mean() if nz_t.numel() else torch.zeros((), dtype=torch.float64, device=dev)]).cpu().tolist()
+        keys = ("avg_reward", "reward_pct", "avg_rewards_pct", "median_rewards_pct", "tremor_reduction_occurrence",
+                "any_axis_reduction_pct", "overall_suppression_avg", "overall_suppression_median",
+                "angle_suppression", "amplitude_reduction_occurrence", "total_amplitude_suppression")
+        out = dict(zip(keys, vals))
+        out["suppression_avg_per_env"] = sup_avg.cpu().numpy()
+        out["suppression_median_per_env"] = sup_med.cpu().numpy()
+        return out
 
     def _rollout_ref(self, random, injected=False, overlap=False):
         ag = self.agent
@@ -568,7 +696,7 @@ class RefScheduleTrainer(VecTrainer):
         if injected:
             act = self._rand_act
         elif random:
-            act = self._rand_act.uniform_(-1.0, 1.0)
+            act = self._rand_acts[self._cur].uniform_(-1.0, 1.0)
         else:
             act = ag.select_action_batch(obs, dec_count=self.active_count)
         cur = torch.cuda.current_stream(self.device) if overlap else None
@@ -576,6 +704,8 @@ class RefScheduleTrainer(VecTrainer):
             cur.wait_stream(self._ins_stream)
             self._ins_pending = False
         nobs, rew, done, info = self.env.step(act, active=self.active, out=self._outs[self._cur])
+        if self.stats:
+            self._step_stats(info)
         if not self.fused_score:
             self.score.add_(rew.where(self.active, 0.0))  # :144 (float32 into the float64 score, 2 launches)
         add = ag.replay_buffer.add_batch_ref if self.ref_replay else ag.replay_buffer.add_batch
@@ -599,7 +729,7 @@ class RefScheduleTrainer(VecTrainer):
     def _roll_round(self, random):
         """The whole rollout of a round (round_len steps) as one graph replay,
         captured on first use per (random, starting observation parity)."""
-        key = ("round", bool(random), self._cur)
+        key = ("round", bool(random), self._cur, self.stats)
         g = self._round_graphs.get(key)
         if g is None:
             s = torch.cuda.Stream(device=self.device)
@@ -630,7 +760,7 @@ class RefScheduleTrainer(VecTrainer):
         elif not self.use_graphs or self._roll_iters < self.warmup_eager:
             self._rollout_ref(random)
         else:
-            key = ("roll", bool(random), self._cur)
+            key = ("roll", bool(random), self._cur, self.stats)
             g = self.graphs.get(key)
             if g is None:
                 s = torch.cuda.Stream(device=self.device)
@@ -678,6 +808,8 @@ class RefScheduleTrainer(VecTrainer):
             self.env.reset(obs_out=self.obs)
         self.score.fill_(2.0)  # reset() returns (obs, counts = 2) into score[i] (:112)
         self._round_start()
+        if self.stats:
+            self._stats_buffers()[2].zero_()  # the round's counters (:117-121)
         random = not self.allow_train
         if (self.round_graph and self.use_graphs and self.action_source is None
                 and self._roll_iters >= max(self.warmup_eager, 1) and self._seen_eager(random)):
@@ -685,7 +817,7 @@ class RefScheduleTrainer(VecTrainer):
         else:
             for _ in range(self.round_len):
                 self._roll_step(random)
-                self._eager_kinds.add(bool(random))
+                self._eager_kinds.add((bool(random), self.stats))
         self.resets += 1
         # :208 -- the host sees one value per round: the mean episode return
         ep_return = float(np.mean(self.score.cpu().numpy()))
@@ -697,6 +829,8 @@ class RefScheduleTrainer(VecTrainer):
         self.steps_count += self.round_env_steps * self.world
         if self.steps_count > self.warmup:  # :210-211
             self.allow_train = True
+        if self.stats:
+            self.round_stats.append(self.compute_round_stats())
         self.rounds += 1
         self.trace.append(dict(round=self.rounds, random_actions=random, ep_return=ep_return,
                                ep_timesteps=ep_timesteps, training_steps=L.training_steps,

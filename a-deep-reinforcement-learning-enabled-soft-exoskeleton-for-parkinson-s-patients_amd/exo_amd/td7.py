@@ -399,14 +399,75 @@ class GradSync:
     def __init__(self, group=None):
         self.group = group
         self.world = dist.get_world_size(group) if group is not None else 1
+        self.rank = dist.get_rank(group) if group is not None else 0
+        self.backend = dist.get_backend(group) if group is not None else None
         # EXO_FORCE_DIST=1 (bench.py under torchrun with one rank): the
         # data-parallel layout and its collectives at world 1, so a one-GPU box
         # runs the RCCL path the multi-GPU runs take
         self.forced = group is not None and os.environ.get("EXO_FORCE_DIST") == "1"
+        self._capture_ok = None
 
     @property
     def active(self):
         return self.world > 1 or self.forced
+
+    def avg_(self, flat):
+        """In-place average over the ranks (RCCL: one ncclAvg all-reduce; gloo:
+        SUM then 1/world).  A no-op on one process."""
+        if not self.active:
+            return flat
+        if self.backend == "nccl":
+            dist.all_reduce(flat, op=dist.ReduceOp.AVG, group=self.group)
+        else:
+            dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+            flat.mul_(1.0 / self.world)
+        return flat
+
+    def graph_capturable(self, device):
+        """Whether the collectives can run INSIDE the trainers' captured HIP
+        graphs (RCCL stream capture): the nccl backend, EXO_DP_CAPTURE != 0,
+        and a captured AVG / MAX all-reduce pair that replays correctly on
+        every rank -- checked once, the ranks' verdicts MIN-reduced so all of
+        them take the same layout.  gloo collectives run on the host and
+        cannot be captured."""
+        if not self.active or self.backend != "nccl":
+            return False
+        if self._capture_ok is None:
+            ok = os.environ.get("EXO_DP_CAPTURE", "1") != "0"
+            if ok:
+                try:
+                    ok = self._capture_selftest(device)
+                except Exception:  # capture refused by the runtime / RCCL: the eager layout
+                    ok = False
+            flag = torch.tensor([1.0 if ok else 0.0], device=device)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+            self._capture_ok = bool(float(flag) == 1.0)
+        return self._capture_ok
+
+    def _capture_selftest(self, device, replays=3):
+        x = torch.zeros(1024, device=device)
+        y = torch.zeros(1, device=device)
+        self.avg_(x)  # eager first: communicator set up outside the capture
+        dist.all_reduce(y, op=dist.ReduceOp.MAX, group=self.group)
+        cur = torch.cuda.current_stream(device)
+        s = torch.cuda.Stream(device=device)
+        s.wait_stream(cur)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                self.avg_(x)
+                dist.all_reduce(y, op=dist.ReduceOp.MAX, group=self.group)
+        cur.wait_stream(s)
+        ok = True
+        for k in range(replays):
+            x.fill_(float(self.rank + 1 + k))
+            y.fill_(float(self.rank + 2 * k))
+            g.replay()
+            torch.cuda.synchronize(device)
+            want = (self.world + 1) / 2.0 + k
+            ok = ok and bool((x - want).abs().max() <= 1e-5 * want) and float(y) == self.world - 1 + 2 * k
+        del g
+        return ok
 
     def allreduce_grads(self, params):
         if not self.active:
@@ -601,6 +662,11 @@ class TD7Learner:
     # and the caller joins it (join_side, end of iteration); False: phase_grads
     # returns with every gradient ordered on the current stream
     defer_side_join = False
+    # True (data parallel, collectives inside the iteration, set per iteration
+    # by the trainer): the fused update all-reduces the encoder's gradient
+    # bucket on the encoder's branch, between its weight-gradient launch and
+    # its optimiser step, like the one-GPU layout keeps that step there
+    dp_inline = False
 
     def _encoder_grads(self, state, action, next_state):
         """:219-228 -- loss and gradients of the live encoder."""
@@ -738,11 +804,15 @@ class TD7Learner:
             return st
 
         # one GPU: the encoder's weight gradients and optimiser step stay on
-        # its branch (nothing else in the update reads them); data-parallel
-        # runs all-reduce them with the critic's
-        enc_step = (branch and ADAM_PACK and self.defer_side_join and not self.sync.active
+        # its branch (nothing else in the update reads them); data parallel
+        # with the collectives inside the iteration: the same, with the
+        # encoder bucket's all-reduce between them on the branch (the step is
+        # then a td7f_adam_pack launch); eager data parallel: all-reduced with
+        # the critic's
+        inline = self.sync.active and self.dp_inline
+        enc_step = (branch and ADAM_PACK and self.defer_side_join and (not self.sync.active or inline)
                     and isinstance(self.encoder_optimizer, FlatAdam))
-        wg_adam = enc_step and WGRAD_ADAM and tr.fuses_adam()
+        wg_adam = enc_step and WGRAD_ADAM and tr.fuses_adam() and not self.sync.active
         self._enc_step_pending = False
         self._actor_fused_pre = False
         if branch and TARGET_ON_MAIN:
@@ -756,6 +826,8 @@ class TD7Learner:
                 tr.encoder(state, action, next_state)
                 if enc_step:
                     tr.wgrad_encoder(adam=wg_adam)
+                    if inline:
+                        self.sync.avg_(tr.enc_grad)
             with torch.cuda.stream(fside):
                 zs, zsa = fz.fixed(state, action)
             if self.prefetch_actor and self.actor_branch:
@@ -773,6 +845,8 @@ class TD7Learner:
                     tr.encoder(state, action, next_state)
                     if enc_step:
                         tr.wgrad_encoder(adam=wg_adam)
+                        if inline:
+                            self.sync.avg_(tr.enc_grad)
                 with torch.cuda.stream(tside):
                     qt = fz.target_heads(next_state, noise)
             else:
@@ -883,7 +957,9 @@ class TD7Learner:
             self._actor_step_done = (self.defer_side_join and WGRAD_ADAM and ADAM_PACK and not self.sync.active
                                      and isinstance(self.actor_optimizer, FlatAdam) and tr.fuses_adam())
             tr.wgrad_actor(adam=self._actor_step_done)
+            self._actor_bucket = tr.actor_grad
             return
+        self._actor_bucket = None
         fixed_zs = self._fixed_zs
         pre, self._actor_pre = getattr(self, "_actor_pre", None), None
         with self._autocast():
@@ -942,6 +1018,34 @@ class TD7Learner:
             self.actor_optimizer.step()
         if self.fused is not None:
             self.fused.pack("actor")  # select_action reads the packed actor
+
+    # Data parallel with the collectives inside the iteration (the trainers'
+    # one-graph layout): each optimiser phase's gradients are averaged in
+    # place between the weight-gradient launches and the optimiser steps.
+    def allreduce_phase_grads(self, B):
+        """After phase_grads: the encoder + critic gradients averaged over the
+        ranks.  Fused with the encoder's step on its branch: its bucket was
+        reduced there, the critic's flat gradient buffer is reduced here and
+        None is returned (phase_steps reads the gradients in place); otherwise
+        one packed bucket of both is reduced and returned for
+        phase_steps(flat_grad=...)."""
+        if getattr(self, "_enc_step_pending", False):
+            self.sync.avg_(self.fused.train(B).critic_grad)
+            return None
+        flat = GradSync.pack(self.grad_params())
+        self.sync.avg_(flat)
+        return flat
+
+    def allreduce_actor_grads(self):
+        """After phase_actor_grads: the actor's gradients averaged over the
+        ranks (the fused flat gradient buffer in place -> None; otherwise a
+        packed bucket for phase_actor_step(flat_grad=...))."""
+        if getattr(self, "_actor_bucket", None) is not None:
+            self.sync.avg_(self._actor_bucket)
+            return None
+        flat = GradSync.pack(self.grad_params(actor=True))
+        self.sync.avg_(flat)
+        return flat
 
     def grad_params(self, actor=False):
         if actor:
@@ -1026,6 +1130,12 @@ class Agent:
         size = int(buffer_size if buffer_size is not None else self.hp.buffer_size)
         self.replay_buffer = LAP(state_dim, action_dim, self.device, env_num, size, self.hp.batch_size, max_action,
                                  normalize_actions=True, prioritized=True)
+        if self.sync.world > 1:
+            # data parallel: every rank explores and samples its own replay shard
+            # with its own streams (the weights are rank 0's broadcast)
+            for rng in (self.learner._explore_rng, self.replay_buffer._rng):
+                if rng is not None:
+                    rng.fold(self.sync.rank)
         self.max_action = max_action
         self.offline = offline
         self._init_checkpointing()
@@ -1113,13 +1223,16 @@ class Agent:
         to every env's action, as the reference's batched Pink select_action
         does (:218-226), and exploration_noise decreases once per call (:225);
         otherwise Gaussian noise per env (TD7_multi_agent.py:205-207), one
-        decrement per env (the training script's per-env calls) -- dec_count
+        decrement per env (the training script's per-env calls; under data
+        parallelism per env of every rank: the ranks' envs are the script's
+        envs, and every rank's replica takes all of their decrements) -- dec_count
         (int32 device scalar): one per env counted there, the envs still
         running at this step of a synchronous round (the script calls
         select_action only for envs that are not done, :125-128)."""
         fz = self.learner.fused
         if fz is not None and use_exploration and timestep is None and not use_checkpoint and obs.is_cuda:
-            return fz.select(obs, scale=self.max_action, dec_count=dec_count)  # zs, actor and the noise in one launch
+            # zs, actor and the noise in one launch
+            return fz.select(obs, scale=self.max_action, dec_count=dec_count, world=self.sync.world)
         a = self.learner.act(obs, use_checkpoint)
         if use_exploration and timestep is not None:
             col = self.noise_dev.index_select(1, timestep).t()           # [1, action_dim]
@@ -1128,10 +1241,11 @@ class Agent:
         if use_exploration:
             L = self.learner
             noise = None if (a.is_cuda and L._device_rng) else torch.randn_like(a)
-            if noise is None and dec_count is not None:
-                return ops.noisy_action(a, None, L.exploration_noise_t, L.action_noise_decrease,
-                                        scale=self.max_action, rng=L._explore_rng, dec_count=dec_count)
-            return ops.noisy_action(a, noise, L.exploration_noise_t, L.action_noise_decrease * a.shape[0],
+            dec = L.action_noise_decrease * self.sync.world
+            if dec_count is not None:
+                return ops.noisy_action(a, noise, L.exploration_noise_t, dec, scale=self.max_action,
+                                        rng=L._explore_rng, dec_count=dec_count)
+            return ops.noisy_action(a, noise, L.exploration_noise_t, dec * a.shape[0],
                                     scale=self.max_action, rng=L._explore_rng)
         return a.clamp(-1, 1) * self.max_action
 

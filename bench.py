@@ -351,7 +351,7 @@ def fused_critic_timing(agent, reps=20, replays=10):
 REFERENCE_ENV_STEPS_PER_UPDATE = 2257 / 283
 
 
-def reference_schedule(env, dev, args, hp, rounds=3, warm_rounds=3):
+def reference_schedule(env, dev, args, hp, rounds=3, warm_rounds=3, group=None):
     """The reference training script's schedule on the same envs
     (exo_amd.rollout.RefScheduleTrainer, Simulation/Exoskeleton_agent_train.py:
     110-211): per episode round a synchronous rollout of every env (uniform
@@ -361,11 +361,17 @@ def reference_schedule(env, dev, args, hp, rounds=3, warm_rounds=3):
     graph-replayed TD7 steps with the policy-checkpoint rule.  Fresh agent;
     `warm_rounds` untimed (the first is the random warm-up and captures the
     graphs, the third captures the policy round's rollout graph), then
-    `rounds` timed with the rollout and the burst timed apart."""
+    `rounds` timed with the rollout and the burst timed apart.  Data parallel
+    (group): every rank runs its envs; the warm-up counts every rank's
+    env-steps, the checkpoint rule sees the MIN of the ranks' returns, the
+    bursts' gradients are all-reduced; times are the max over
+    ranks and env-steps the sum."""
     from exo_amd.rollout import RefScheduleTrainer
     from exo_amd.td7 import Agent
-    torch.manual_seed(2)
-    ag = Agent(80, 7, 1, env_num=8, hp=hp, device=dev, precision=args.precision, n_envs=env.n, graph_safe=True)
+    rank = dist.get_rank(group) if group is not None else 0
+    torch.manual_seed(2 + rank)  # per-rank warm-up actions; the weights are rank 0's broadcast
+    ag = Agent(80, 7, 1, env_num=8, hp=hp, device=dev, precision=args.precision, n_envs=env.n, graph_safe=True,
+               process_group=group)
     tr = RefScheduleTrainer(env, ag, warmup=25_000)
     for _ in range(warm_rounds):
         tr.run_round()
@@ -390,6 +396,11 @@ def reference_schedule(env, dev, args, hp, rounds=3, warm_rounds=3):
         updates += b
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    if group is not None:  # max of the ranks' times, sum of their env-steps
+        t = torch.tensor([dt, t_burst, -float(env_steps)], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        dt, t_burst = float(t[0]), float(t[1])
+        env_steps = int(-float(t[2])) * dist.get_world_size(group)
     t_roll = dt - t_burst
     out = {"env_steps_per_sec": env_steps / dt, "grad_steps_per_sec": updates / dt,
            "burst_grad_steps_per_sec": updates / t_burst, "rollout_env_steps_per_sec": env_steps / t_roll,
@@ -398,12 +409,20 @@ def reference_schedule(env, dev, args, hp, rounds=3, warm_rounds=3):
            "env_steps_per_round": env_steps / rounds, "rounds_timed": rounds,
            "env_steps_per_grad_step": env_steps / max(updates, 1),
            "checkpoint_refreshes": ag.checkpoint_refreshes, "replay": "reference shared pointer (add_batch_ref)",
+           "n_gpus": dist.get_world_size(group) if group is not None else 1,
+           "dp_layout": dp_layout(tr) if group is not None else None,
            "note": "Exoskeleton_agent_train.py:110-211 on the device: warm-up 25,000 env-steps of uniform actions, "
                    "then select_action with Gaussian exploration; per round round(mean(ep_len)) = 283 "
                    "graph-replayed Agent.train steps and the policy-checkpoint rule (TD7_multi_agent.py:296-325)"}
     ag.maybe_train_and_checkpoint = orig
     del tr, ag
     return out
+
+
+def dp_layout(trainer):
+    if not trainer.dp:
+        return None
+    return "one graph, collectives captured (RCCL)" if trainer.dp_inline else "three graphs, eager collectives"
 
 
 def td7_variants(env, dev, args, iters=60, warmup=8):
@@ -583,6 +602,29 @@ def main():
         torch.cuda.synchronize()
         return float(np.mean([x.elapsed_time(y) for x, y in evs])), float(np.mean(act_n))
 
+    def measured_round_timing():
+        """One whole episode round timed end to end (SURVEY
+        8(d) config 2 "whole rounds"): after the window, iterate untimed to the
+        round boundary, then time exactly round_len iterations -- the first
+        runs the episode reset -- bracketed by barrier + synchronize, max over
+        ranks.  Returns (seconds, active env-steps of this rank)."""
+        while trainer.k != trainer.round_len:
+            trainer.step()
+        torch.cuda.synchronize()
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        n = sum(trainer.step() for _ in range(trainer.round_len))
+        torch.cuda.synchronize()
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize()
+        dt = torch.tensor([time.perf_counter() - t], device=dev, dtype=torch.float64)
+        if dist_on:
+            dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+        return float(dt), n
+
     for _ in range(args.warmup):
         one_step(False)
     torch.cuda.synchronize()
@@ -607,6 +649,7 @@ def main():
     if clock is not None:
         window_clock = env.step_clock_ms()
         env.set_step_clock(False)
+    measured_round = measured_round_timing() if trainer is not None else None
     reset_ms = reset_timing()
     loop_kern_ms = None
     if ev:  # env mode: the timed launches themselves
@@ -658,6 +701,10 @@ def main():
                   for n, m in (("actor", agent.learner.actor), ("critic", agent.learner.critic),
                                ("encoder", agent.learner.encoder))}
     dp_sync = dp_ck = None
+    ref_sched = None
+    if agent is not None and args.mode == "train" and not args.no_reference_schedule:
+        # every rank (collectives inside); rank 0 reports
+        ref_sched = reference_schedule(env, dev, args, agent.hp, group=dist.group.WORLD if dist_on else None)
     if agent is not None and dist_on:
         # data-parallel replicas must hold bit-identical weights
         ck = torch.stack([torch.cat([p.detach().reshape(-1) for p in m.parameters()]).double().sum()
@@ -691,6 +738,13 @@ def main():
                              f"{t_iter * 1e3:.4f} ms (window time minus {resets_in_window} reset(s), per iteration), "
                              f"t_reset = {t_reset * 1e3:.4f} ms (exo_reset_kernel, HIP events)",
             "window_value": total_env_steps / elapsed,
+            "measured_round_value": (world * measured_round[1] / measured_round[0]) if measured_round else None,
+            "measured_round": ({"seconds": measured_round[0], "iterations": round_len,
+                                "active_env_steps_per_rank": measured_round[1],
+                                "value_over_measured": round_value / (world * measured_round[1] / measured_round[0]),
+                                "note": "one whole episode round (reset + round_len graph-replayed iterations) "
+                                        "timed end to end after the window, max over ranks"}
+                               if measured_round else None),
             "env_kernel_env_steps_per_sec": active_avg / (kern_ms * 1e-3),
             "roofline": {"kernel": ("exo_step_rp_kernel" if N <= 16384 else "exo_step_kernel")
                                    + (" + exo_multibody_kernel" if args.physics == "multibody" else ""), "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
@@ -796,8 +850,10 @@ def main():
                     "peak_source": "tools/stream_bench.hip (profiles/r02b_raw/stream_bench.txt)"}
         if agent is not None and args.workload == "configs1" and world == 1 and not args.no_td7_variants:
             res["td7_variants"] = td7_variants(env, dev, args)
-        if agent is not None and world == 1 and not args.no_reference_schedule:
-            res["reference_schedule"] = reference_schedule(env, dev, args, agent.hp)
+        if dp_sync is not None:
+            res["dp_layout"] = dp_layout(trainer)
+        if ref_sched is not None:
+            res["reference_schedule"] = ref_sched
         if finite is not None:
             res["weights_finite"] = all(finite.values()) or finite
         if dp_sync is not None:

@@ -193,7 +193,7 @@ void exo_destroy(exo_ctx *ctx);
  *     change (1; DH FK of Utilities/calculate_arm_end_effector_points.py:18-50
  *     on the IMU angles with the suppressed / unsuppressed tremor amplitudes),
  *     any-nonzero flag (1); with disregard != 0 positive values are zeroed
- *     (:186-191);
+ *     (:186-191); the rows of envs not stepped are zeros (:201-203);
  *   counters_dev [N][6] (accumulated): tremor_when_reduction[0..1],
  *     tremor_reduction_in_episode, tremor_when_ampl_reduction[0..1],
  *     tremor_ampl_total_reduction_ep (last negative value). */
@@ -306,6 +306,16 @@ int lap_store_batch_ref(const lap_tree_desc *t, const lap_storage_desc *st, int6
                         const float *state_dev, const float *action_dev, const float *next_state_dev,
                         const float *reward_dev, const uint8_t *done_dev, const int32_t *strata_dev,
                         const uint8_t *active_dev, float action_scale, int32_t n, int32_t *ws_dev, void *stream);
+
+/* lap_store_batch_ref as ONE launch (the same stored rows, leaves, sums,
+ * pointer and sizes, bit for bit): grid n_strata x (copy parts); the last
+ * workgroup out advances ref_dev.  ticket_dev: one uint32, zero at the first
+ * call, left zero. */
+int lap_store_batch_ref_fused(const lap_tree_desc *t, const lap_storage_desc *st, int64_t *ref_dev,
+                              const float *state_dev, const float *action_dev, const float *next_state_dev,
+                              const float *reward_dev, const uint8_t *done_dev, const int32_t *strata_dev,
+                              const uint8_t *active_dev, float action_scale, int32_t n, uint32_t *ticket_dev,
+                              void *stream);
 
 /* LAP.sample (:65-111): batch draws per stratum (u_dev [n_strata][batch]),
  * indices -> idx_dev [n_strata][batch], the sampled rows gathered into
@@ -596,9 +606,13 @@ int td7f_critic(int32_t prec, const int32_t *act, const td7f_lin *critic, const 
                 void *stream);
 /* Encoder update (TD7_multi_agent.py:219-228): zs(s') (no grad), zs(s),
  * zsa(zs, a), d mse / d pred and the dX chain of all six layers.  y: four
- * [B][enc_hdim] fp32 scratch buffers (zs1, zs2, zsa1, zsa2 activations). */
+ * [B][enc_hdim] fp32 scratch buffers (zs1, zs2, zsa1, zsa2 activations).
+ * nz_ws / flag_ws (both or neither): zs(s') on its own workgroup row --
+ * nz_ws [ceil(B/16)*16][zs_dim] fp32 scratch, flag_ws [ceil(B/16)] int32,
+ * zero at the first call and left zero. */
 int td7f_encoder(int32_t prec, const int32_t *act, const td7f_lin *enc, const float *s_dev, const float *a_dev,
-                 const float *ns_dev, int32_t B, float *const *y, const td7f_xt *xt, int64_t ld, void *stream);
+                 const float *ns_dev, int32_t B, float *const *y, const td7f_xt *xt, int64_t ld, float *nz_ws,
+                 int32_t *flag_ws, void *stream);
 /* Actor update (TD7_multi_agent.py:266-277) in three launches: phase 0 actor(s,
  * fixed_zs) and fixed_encoder.zsa of it; phase 1 the (updated) critic on them and
  * d(-mean Q) back to the action and zsa inputs per head; phase 2 the fixed zsa

@@ -1,14 +1,26 @@
-"""Data-parallel training iteration on the GPU: 2 ranks (gloo, both pinned to
-cuda:0 so it runs on a 1-GPU box) through bench.py's DP path -- HIP-graph
-segments with the gradient all-reduces between them.  The replicas' weights
-must stay bit-identical."""
+"""Data-parallel training on the GPU.
+
+* gloo ranks pinned to cuda:0 (several ranks on a 1-GPU box) through bench.py's
+  DP path and through tests/dp_worker.py at configs[2]'s per-rank shape (4,096
+  envs per rank; 2 and 8 ranks): three graphs per iteration with the gradient
+  all-reduces between them.  The replicas' weights must stay bit-identical and
+  every rank's env trajectories must match the oracle.
+* RCCL at world 1 (RCCL refuses two ranks on one device): the one-graph layout
+  with the collectives captured inside it, bit-identical to the one-GPU graph.
+* The reference schedule (RefScheduleTrainer) on 2 ranks: steps counted over
+  ranks, MIN-reduced episode returns, one checkpoint decision sequence, a
+  global max_priority."""
 import json
 import os
 import socket
 import subprocess
 import sys
 
+import numpy as np
 import pytest
+import torch
+
+from helpers import model_host, philox_draws
 
 pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -57,5 +69,140 @@ def test_rccl_data_parallel_layout_at_world_one():
     assert res["n_gpus"] == 1
     assert "DP all-reduce" in res["config"]["parallelism"]
     assert res["dp_weights_in_sync"] is True
+    assert res["dp_layout"] == "one graph, collectives captured (RCCL)"
     assert res["weights_finite"] is True, res["weights_finite"]
     assert res["value"] > 0
+
+
+def _run_workers(tmp_path, world, mode, extra, timeout=900):
+    env = dict(os.environ, EXO_BENCH_DEVICE="0", EXO_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(REPO, "tests", "dp_worker.py"),
+           "--mode", mode, "--out", str(tmp_path)] + extra
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=REPO)
+    assert out.returncode == 0, out.stderr[-4000:]
+    return [json.load(open(os.path.join(tmp_path, f"out_r{r}.json"))) for r in range(world)]
+
+
+def _oracle_replay(tmp_path, rank, n_envs, iters):
+    """The rank's sampled envs (seed 1000 + rank, motion e mod 8, defaults) on
+    the oracle: the constructor's episode 0, the trainer's reset (episode 1),
+    then the recorded actions; states, next states and rewards compared."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    from exo_amd import motions
+    from test_env_gpu import _close_obs, env_kwargs_default
+    rows = np.load(os.path.join(tmp_path, f"rows_r{rank}.npz"))
+    angles, lengths = motions.load()
+    lib = model_host()
+    cfg = env_kwargs_default()
+    for e in rows["envs"]:
+        e = int(e)
+        m = e % 8
+        L = int(lengths[m])
+        oe = O.OracleEnv(angles[m][:, :L], cfg["seq"], cfg["amp"], cfg["h1"], cfg["h2"], 40.0, 20.0, 0.02, 0.03, 0.1)
+        oe.reset(philox_draws(L, 1000 + rank, e, 0, lib))
+        ob = oe.reset(philox_draws(L, 1000 + rank, e, 1, lib))
+        st, ac, ns, rw = (rows[f"{k}_{e}"] for k in ("state", "action", "next_state", "reward"))
+        assert st.shape == (iters, 80)
+        _close_obs(st[0], ob)
+        for k in range(iters):
+            if k:
+                np.testing.assert_array_equal(st[k], ns[k - 1])
+            ob, r, dn, info, _ = oe.step(ac[k].astype(np.float64))
+            _close_obs(ns[k], ob)
+            np.testing.assert_allclose(rw[k], r, rtol=2e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("world,iters", [(2, 16), (8, 8)])
+def test_data_parallel_at_configs2_shape_per_rank(tmp_path, world, iters):
+    """configs[2]'s per-rank shape: 4,096 envs per rank (2 ranks: 8,192 envs;
+    8 ranks: 32,768 -- configs[2]'s whole job, every rank pinned to the one
+    GPU over gloo).  Replicas bit-identical; each rank's envs (its own seed)
+    replayed on the oracle from its replay rows."""
+    outs = _run_workers(tmp_path, world, "vec", ["--envs", "4096", "--iters", str(iters)])
+    assert [o["rank"] for o in outs] == list(range(world))
+    assert all(o["dp_inline"] is False for o in outs)  # gloo: the eager-collective layout
+    assert all(o["checksums"] == outs[0]["checksums"] for o in outs)
+    assert all(o["training_steps"] == iters for o in outs)
+    for r in (0, world - 1):
+        _oracle_replay(tmp_path, r, 4096, iters)
+
+
+def test_reference_schedule_on_two_ranks(tmp_path):
+    """RefScheduleTrainer with 2 ranks (gloo on one GPU), 64 envs each, 3 rounds
+    (a random warm-up round, then the policy): steps_count counts both ranks'
+    env-steps (Exoskeleton_agent_train.py:146, 210-211), the episode return
+    the checkpoint rule sees is the MIN over the ranks' round returns
+    (TD7_multi_agent.py:296-312), every rank takes the same checkpoint
+    decisions and training bursts, the replicas and the global max_priority
+    (TD7_buffer_multi_agent.py:116, 120) agree, and the exploration noise fell
+    by one decrement per env-step of EVERY rank."""
+    outs = _run_workers(tmp_path, 2, "ref", ["--envs", "64", "--rounds", "3"])
+    A = outs[0]["round_env_steps"]
+    assert A == 8 * 2257
+    for o in outs:
+        assert o["steps_count"] == 3 * A * 2
+        assert [t["steps_count"] for t in o["trace"]] == [A * 2, 2 * A * 2, 3 * A * 2]
+        assert [t["random_actions"] for t in o["trace"]] == [True, False, False]
+        assert o["training_steps"] == 3 * 283
+    keys = ("training_steps", "eps_since_update", "best_min_return", "max_eps_before_update",
+            "checkpoint_refreshed", "ep_timesteps")
+    for a, b in zip(outs[0]["trace"], outs[1]["trace"]):
+        assert {k: a[k] for k in keys} == {k: b[k] for k in keys}
+    # round 1 always checkpoints (best_min_return = -1e8): best_min_return = the MIN-reduced return
+    r1 = [o["trace"][0] for o in outs]
+    assert r1[0]["checkpoint_refreshed"]
+    assert r1[0]["ep_return"] != r1[1]["ep_return"]  # the ranks' envs differ (seed 1000 + rank)
+    assert r1[0]["best_min_return"] == min(t["ep_return"] for t in r1)
+    assert outs[0]["checksums"] == outs[1]["checksums"]  # weights and max_priority
+    assert outs[0]["exploration_noise"] == outs[1]["exploration_noise"]
+    from exo_amd.td7 import Hyperparameters
+    hp = Hyperparameters()
+    want = hp.exploration_noise - 2 * A * 2 * hp.exploration_noise / 100000  # 2 policy rounds, both ranks' envs
+    assert abs(outs[0]["exploration_noise"] - want) < 2e-5
+
+
+def test_rccl_inline_layout_is_bit_identical_to_the_one_gpu_graph(monkeypatch):
+    """RCCL world 1 (EXO_FORCE_DIST=1): VecTrainer captures each iteration as
+    ONE graph with the AVG all-reduces of the encoder (on its branch), critic
+    and actor buckets and the MAX of max_priority inside it.  At world 1 every
+    collective is the identity, so the run must equal the one-GPU graph bit
+    for bit -- weights, optimiser moments, replay trees -- and so must the
+    eager-collective three-graph layout (EXO_DP_CAPTURE=0)."""
+    import torch.distributed as dist
+    from exo_amd import VecExoskeletonEnv
+    from exo_amd.rollout import VecTrainer
+    from exo_amd.td7 import Agent
+
+    def run(group, capture="1"):
+        monkeypatch.setenv("EXO_FORCE_DIST", "1" if group is not None else "0")
+        monkeypatch.setenv("EXO_DP_CAPTURE", capture)
+        torch.manual_seed(11)
+        env = VecExoskeletonEnv(512, seed=21)
+        ag = Agent(80, 7, 1, env_num=8, precision="bf16", n_envs=512, process_group=group, graph_safe=True,
+                   buffer_size=8192)
+        tr = VecTrainer(env, ag)
+        for _ in range(14):
+            tr.step()
+        torch.cuda.synchronize()
+        L = ag.learner
+        st = [p.detach().clone() for m in (L.actor, L.critic, L.encoder, L.fixed_encoder) for p in m.parameters()]
+        st += [getattr(L, o).m.clone() for o in ("actor_optimizer", "critic_optimizer", "encoder_optimizer")]
+        st += [ag.replay_buffer._tree.clone(), ag.replay_buffer._maxp.clone(), L.max.clone(), L.min.clone()]
+        return tr, st
+
+    tr0, ref = run(None)
+    assert not tr0.dp
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        for capture, inline in (("1", True), ("0", False)):
+            tr, st = run(dist.group.WORLD, capture)
+            assert tr.dp and tr.dp_inline is inline
+            if inline:
+                assert all(len(parts) == 1 for parts in tr.graphs.values())
+            for i, (x, y) in enumerate(zip(ref, st)):
+                torch.testing.assert_close(y, x, rtol=0, atol=0, msg=f"tensor {i} (capture={capture})")
+    finally:
+        dist.destroy_process_group()

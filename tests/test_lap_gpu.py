@@ -181,15 +181,18 @@ def test_sample_never_returns_the_slot_at_size():
     assert set(np.unique(idx[1])) == set(np.unique(idx[2])) == {1, 2, 3, 4}
 
 
-def test_add_batch_ref_equals_sequential_reference_adds():
-    """lap_store_batch_ref == LAP.add (:49-63) called once per active row in row
-    order: stored transitions, leaves, sums, the shared pointer and size --
-    random strata (several rows per stratum), random active masks (overwrites
-    of one slot by two adds of a stratum between pointer advances: the later
-    add wins), a pointer that wraps the capacity."""
+@pytest.mark.parametrize("fused", [True, False])
+def test_add_batch_ref_equals_sequential_reference_adds(fused):
+    """lap_store_batch_ref (fused: the one-launch lap_store_batch_ref_fused) ==
+    LAP.add (:49-63) called once per active row in row order: stored
+    transitions, leaves, sums, the shared pointer and size -- random strata
+    (several rows per stratum), random active masks (overwrites of one slot by
+    two adds of a stratum between pointer advances: the later add wins), a
+    pointer that wraps the capacity."""
     rng = np.random.default_rng(3)
     E, C, N = 4, 40, 19
     seq, vec = _lap(E, C, 4), _lap(E, C, 4)
+    vec.ref_insert_fused = fused
     for step in range(30):
         st = rng.normal(size=(N, 80)).astype(np.float32)
         nx = rng.normal(size=(N, 80)).astype(np.float32)
@@ -213,6 +216,48 @@ def test_add_batch_ref_equals_sequential_reference_adds():
         torch.testing.assert_close(vec._tree, seq._tree, rtol=0, atol=0)
         assert torch.equal(vec.size_s, seq.size_s)
     assert seq.count > 2 * C  # the pointer wrapped
+
+
+@pytest.mark.parametrize("E,C,N", [(8, 5000, 10_000), (8, 30_000, 4096), (5, 3000, 9001)])
+def test_fused_ref_insert_equals_three_launch_insert(E, C, N):
+    """lap_store_batch_ref_fused (one launch, r04) against the three-launch
+    lap_store_batch_ref (pinned to the sequential adds above) at the rollout's
+    sizes: several 4,096-row chunks (a stratum's last row of a chunk decided by
+    the next chunk), more copy parts than one, non-integer priorities already
+    in the tree, masks with whole runs of done envs, ring wrap-around; the
+    storage, every tree node, the shared pointer and the sizes bit for bit,
+    and every internal node exactly left + right."""
+    rng = np.random.default_rng(E * 1000 + N)
+    a, b = _lap(E, C, 64), _lap(E, C, 64)
+    a.ref_insert_fused, b.ref_insert_fused = False, True
+    prio = rng.gamma(0.7, 2.0, (E, C)).astype(np.float32) + np.float32(1e-3)
+    for lap in (a, b):
+        _set_priorities(lap, prio)
+    T = lambda x: torch.as_tensor(x, device="cuda")  # noqa: E731
+    strata = (np.arange(N) % E).astype(np.int32)
+    for step in range(6):
+        st = rng.normal(size=(N, 80)).astype(np.float32)
+        nx = rng.normal(size=(N, 80)).astype(np.float32)
+        ac = rng.uniform(-1, 1, (N, 7)).astype(np.float32)
+        rw = rng.normal(size=N).astype(np.float32)
+        dn = rng.random(N) < 0.05
+        if step % 2:
+            strata = rng.integers(0, E, N).astype(np.int32)
+        active = rng.random(N) < [1.0, 0.6, 0.05, 0.95, 0.3, 1.0][step]
+        active[rng.integers(0, N - 600):][:500] = False  # a run of done envs
+        for lap in (a, b):
+            lap.add_batch_ref(T(st), T(ac), T(nx), T(rw), T(dn), T(strata), T(active))
+        torch.cuda.synchronize()
+        assert a.ref_pointer() == b.ref_pointer(), step
+        for name in ("state", "action", "next_state", "reward", "not_done"):
+            torch.testing.assert_close(getattr(b, name), getattr(a, name), rtol=0, atol=0)
+        torch.testing.assert_close(b._tree, a._tree, rtol=0, atol=0)
+        assert torch.equal(a.size_s, b.size_s)
+        assert int(b._ref_ws[0]) == 0  # the ticket is left zero
+    tr = b._tree.cpu().numpy()
+    cap = b._cap
+    for s in range(E):
+        np.testing.assert_array_equal(tr[s, 1:cap], tr[s, 2:2 * cap:2] + tr[s, 3:2 * cap:2])
 
 
 def test_wave_descent_and_subtree_rebuild_match_the_binary_tree():

@@ -48,6 +48,7 @@ def test_device_metrics_match_oracle_on_live_env():
         mh, ih = m.cpu().numpy(), info.cpu().numpy().astype(np.float64)
         for e in range(n):
             if not bool(active[e]):
+                assert not mh[e].any()  # a done env's row of the step is zeros (:201-203)
                 continue
             orig = env.original_joint_angles(e)
             tr, ta, tot, cnt, last = M.step_metrics(ih[e, INFO_SLICES["torque_val"]], ih[e, INFO_SLICES["tremor_torque_val"]],

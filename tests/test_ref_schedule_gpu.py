@@ -80,6 +80,7 @@ def _run_mirror(tmp_path, rounds, warmup, precision, monkeypatch):
                            "--precision", precision])
     out = drv.train(args)
     monkeypatch.undo()
+    _run_mirror.round_stats = out["round_stats"]
     return out["agent"], trace, out["steps"]
 
 
@@ -113,7 +114,7 @@ def _run_trainer(rounds, warmup, precision):
         Ls = env.lengths_host
         env.reset_from_draws(np.arange(E), [_draws(rnd, m, int(Ls[m])) for m in range(E)], obs_out=obs_out)
 
-    tr = RefScheduleTrainer(env, agent, warmup=warmup, action_source=actions, reset_source=resets)
+    tr = RefScheduleTrainer(env, agent, warmup=warmup, action_source=actions, reset_source=resets, stats=True)
     for _ in range(rounds):
         tr.run_round()
     torch.cuda.synchronize()
@@ -150,6 +151,17 @@ def test_ref_schedule_matches_training_mirror(tmp_path, monkeypatch, precision, 
         torch.testing.assert_close(getattr(Lv, opt).v, getattr(Lm, opt).v, rtol=0, atol=0)
     assert float(Lv.exploration_noise_t) == float(Lm.exploration_noise_t) < ag_m.hp.exploration_noise
     assert len([k for k in trainer.graphs if k[0] == "train"]) == 2  # bursts replayed from graphs
+    # the script's per-round tremor statistics (:149-205, :213-317) on the
+    # device (exo_tremor_metrics, fp32 per step) against the mirror's numpy
+    _check_round_stats(_run_mirror.round_stats, trainer.round_stats, rounds)
+
+
+def _check_round_stats(want, got, rounds):
+    assert len(want) == len(got) == rounds
+    for r, (a, b) in enumerate(zip(want, got)):
+        assert set(a) == set(b)
+        for k in a:
+            np.testing.assert_allclose(b[k], a[k], rtol=1e-4, atol=2e-4, err_msg=f"round {r + 1}: {k}")
 
 
 def test_ref_schedule_device_path():
@@ -181,7 +193,7 @@ def test_ref_schedule_device_path():
     ptr, count, size = agent.replay_buffer.ref_pointer()
     assert count == 2 * A and ptr == size == -(-2 * A // E)
     assert int(agent.replay_buffer.size_s.min()) == int(agent.replay_buffer.size_s.max()) == size
-    assert ("roll", True, 0) in tr.graphs and ("roll", False, 0) in tr.graphs
+    assert ("roll", True, 0, False) in tr.graphs and ("roll", False, 0, False) in tr.graphs
     assert ("train", True) in tr.graphs and ("train", False) in tr.graphs
     for m in (agent.learner.actor, agent.learner.critic, agent.learner.encoder):
         assert all(torch.isfinite(p).all() for p in m.parameters())
@@ -194,23 +206,26 @@ def test_round_graph_rollout_matches_per_step_rollout():
     """RefScheduleTrainer's round graph (the round's rollout steps as one graph,
     each step's replay insert on a branch beside the next step's select_action)
     against per-step graph replays: after every round (with its training
-    burst) the replay storage and sum trees, the episode scores, the env state and every network weight are bit-identical (five
-    rounds: a random and a policy round per step, then the round graphs of
-    both starting parities, captured and replayed)."""
+    burst) the replay storage and sum trees, the episode scores, the env state and every network weight are bit-identical (six
+    rounds: three random ones -- per step, then the random round graph
+    captured and replayed, whose uniform actions of step k+1 must not reach
+    step k's insert still running on its branch -- then three policy rounds
+    the same way)."""
     from exo_amd import VecExoskeletonEnv
     from exo_amd.rollout import RefScheduleTrainer
     from exo_amd.td7 import Agent, Hyperparameters
     outs = []
+    N = 32
+    A = N // E * 2257  # active env-steps per round
     for rg in (False, True, "serial"):
         torch.manual_seed(3)
-        N = 32
         env = VecExoskeletonEnv(N, seed=9)
         hp = Hyperparameters(batch_size=32)  # the bench's widths: the fused select in the round graph
         agent = Agent(80, 7, 1, hp=hp, learning_steps=100000, env_num=E, buffer_size=2 * BUF, precision="bf16",
                       n_envs=N, graph_safe=True)
-        tr = RefScheduleTrainer(env, agent, warmup=1, round_graph=rg)
+        tr = RefScheduleTrainer(env, agent, warmup=2 * A + 1, round_graph=rg)
         scores = []
-        for _ in range(5):  # random, policy (per-step), then round graphs: captured and replayed
+        for _ in range(6):  # 3 random, 3 policy: per step, then the round graph captured and replayed
             tr.run_round()
             scores.append(tr.score.clone())
         torch.cuda.synchronize()
@@ -221,6 +236,9 @@ def test_round_graph_rollout_matches_per_step_rollout():
              for p in m.parameters()]
         obs = tr.obs.clone()
         outs.append((st, w, scores, obs, [t["training_steps"] for t in tr.trace]))
+        assert [t["random_actions"] for t in tr.trace] == [True] * 3 + [False] * 3
+        if rg:
+            assert {k[:2] for k in tr._round_graphs} == {("round", True), ("round", False)}
     a = outs[0]
     for b in outs[1:]:  # the branch-overlapped and the serial ("serial": inserts in line) round graphs
         assert a[4] == b[4]
