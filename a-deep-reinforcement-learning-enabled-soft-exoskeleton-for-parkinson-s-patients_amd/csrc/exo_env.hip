@@ -94,6 +94,7 @@ __global__ __launch_bounds__(64) void exo_reset_kernel(Dev S, Urdf U, const uint
     if (e >= S.N) return;
     if (!ids && mask && !mask[e]) return;
     const int lane = threadIdx.x;
+    if (S.pend && lane == 0) S.pend[e] = 0;  // a solve still carried by a budgeted step is dropped
     const int N = S.N, L = S.L[e], seq = S.seq[e];
     const uint32_t ep = S.episode[e];
     const Draws D{draws ? draws + (size_t)blockIdx.x * draw_stride : nullptr, seed, (uint32_t)e, ep};
@@ -863,10 +864,94 @@ __global__ void step_clock_kernel(unsigned long long *clk, int end) {
 
 int exo_step(exo_ctx *c, const float *act_dev, float *obs_dev, float *rew_dev, uint8_t *done_dev, float *info_dev,
              const uint8_t *active_dev, void *stream) {
+    return exo_step_carry(c, act_dev, obs_dev, rew_dev, done_dev, info_dev, active_dev, nullptr, stream);
+}
+
+namespace {
+bool rows_variant(const exo_ctx *c) {
+    return c->step_variant == EXO_STEP_ROWS_SHARED || c->step_variant == EXO_STEP_ROWS ||
+           (c->step_variant == EXO_STEP_AUTO && c->N <= 16384);
+}
+
+__global__ __launch_bounds__(1024) void budget_advance_kernel(const int32_t *counts, const int32_t *L,
+                                                              const uint8_t *pend, int n, uint8_t *active,
+                                                              int32_t *count, int32_t *remaining,
+                                                              long long *steps_total) {
+    __shared__ int wsum[2][16];
+    int a = 0, rem = 0;
+    for (int e = threadIdx.x; e < n; e += blockDim.x) {
+        const bool run = counts[e] < L[e] - 1, p = pend[e] != 0;
+        active[e] = run && !p;
+        a += run && !p;
+        rem += run || p;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        a += __shfl_xor(a, o, 64);
+        rem += __shfl_xor(rem, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        wsum[0][threadIdx.x >> 6] = a;
+        wsum[1][threadIdx.x >> 6] = rem;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int ta = 0, tr = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+            ta += wsum[0][w];
+            tr += wsum[1][w];
+        }
+        if (steps_total) *steps_total += *count;  // the envs the last launch stepped
+        *count = ta;
+        *remaining = tr;
+    }
+}
+} // namespace
+
+int exo_set_step_budget(exo_ctx *c, int32_t budget) {
+    if (!c || budget < 0) return EXO_EINVAL;
+    DeviceGuard g(c->device);
+    if (budget > 0 && (!rows_variant(c) || c->physics != EXO_PHYS_IDEAL))
+        return fail(c, EXO_EINVAL, "exo_set_step_budget: row-parallel step kernels and idealised physics only");
+    int rc = check(c, hipDeviceSynchronize(), "exo_set_step_budget");
+    if (rc) return rc;
+    if (budget == 0) {
+        if (c->S.pend) {
+            std::vector<uint8_t> p(c->N);
+            rc = check(c, hipMemcpy(p.data(), c->S.pend, c->N, hipMemcpyDeviceToHost), "exo_set_step_budget");
+            if (rc) return rc;
+            for (uint8_t v : p)
+                if (v) return fail(c, EXO_EINVAL, "exo_set_step_budget: a solve is still pending");
+        }
+        c->S.budget = 0;
+        return EXO_OK;
+    }
+    if (!c->S.pend) {
+        c->S.pend = dalloc<uint8_t>(c, c->N);
+        c->S.rk = dalloc<double>(c, (size_t)RK_FIELDS * c->N);
+        if (!c->S.pend || !c->S.rk) return fail(c, EXO_ENOMEM, "exo_set_step_budget: out of memory");
+    }
+    c->S.budget = budget;
+    return EXO_OK;
+}
+
+int exo_budget_advance(exo_ctx *c, uint8_t *active_dev, int32_t *count_dev, int32_t *remaining_dev,
+                       int64_t *steps_total_dev, void *stream) {
+    if (!c || !active_dev || !count_dev || !remaining_dev) return EXO_EINVAL;
+    if (!c->S.pend) return fail(c, EXO_EINVAL, "exo_budget_advance: no step budget set");
+    DeviceGuard g(c->device);
+    hipLaunchKernelGGL(budget_advance_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, c->S.counts, c->S.L,
+                       c->S.pend, c->N, active_dev, count_dev, remaining_dev, (long long *)steps_total_dev);
+    return check(c, hipGetLastError(), "exo_budget_advance");
+}
+
+int exo_step_carry(exo_ctx *c, const float *act_dev, float *obs_dev, float *rew_dev, uint8_t *done_dev,
+                   float *info_dev, const uint8_t *active_dev, const float *obs_cur_dev, void *stream) {
     if (!c || !act_dev || !obs_dev || !rew_dev || !done_dev) return EXO_EINVAL;
     DeviceGuard g(c->device);
     const bool shared = c->step_variant == EXO_STEP_ROWS_SHARED;
-    const bool rows = shared || c->step_variant == EXO_STEP_ROWS || (c->step_variant == EXO_STEP_AUTO && c->N <= 16384);
+    const bool rows = rows_variant(c);
+    if (c->S.budget > 0 && (!rows || c->physics != EXO_PHYS_IDEAL))
+        return fail(c, EXO_EINVAL, "exo_step: the step budget needs the row-parallel kernel and idealised physics");
     hipError_t e = hipSuccess;
     if (c->step_clock) {
         hipLaunchKernelGGL(step_clock_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, c->step_clock, 0);
@@ -875,7 +960,7 @@ int exo_step(exo_ctx *c, const float *act_dev, float *obs_dev, float *rew_dev, u
     if (e != hipSuccess) {
     } else if (rows) {
         e = launch_exo_step_rp(c->S, c->U, act_dev, obs_dev, rew_dev, done_dev, info_dev, active_dev,
-                               (hipStream_t)stream, shared);
+                               (hipStream_t)stream, shared, obs_cur_dev);
     } else {
         const int threads = 256, lanes = 2 * c->N;
         hipLaunchKernelGGL(exo_step_kernel, dim3((lanes + threads - 1) / threads), dim3(threads), 0,
@@ -908,6 +993,8 @@ void exo_multibody_default_params(exo_mb_params *p) {
 
 int exo_set_physics(exo_ctx *c, int32_t mode, const exo_mb_params *params) {
     if (!c || (mode != EXO_PHYS_IDEAL && mode != EXO_PHYS_MULTIBODY)) return EXO_EINVAL;
+    if (mode == EXO_PHYS_MULTIBODY && c->S.budget > 0)
+        return fail(c, EXO_EINVAL, "exo_set_physics: the step budget needs idealised physics");
     exo_mb_params p;
     exo_multibody_default_params(&p);
     if (params) p = *params;
@@ -1088,6 +1175,8 @@ int exo_set_state_host(exo_ctx *c, int32_t env, const double *in) {
 }
 
 int exo_set_step_variant(exo_ctx *c, int32_t variant) {
+    if (c && c->S.budget > 0 && variant == EXO_STEP_LANES)
+        return fail(c, EXO_EINVAL, "exo_set_step_variant: the step budget needs a row-parallel kernel");
     if (!c || variant < EXO_STEP_AUTO || variant > EXO_STEP_ROWS_SHARED) return EXO_EINVAL;
     c->step_variant = variant;
     return EXO_OK;

@@ -131,7 +131,14 @@ struct Dev {
     // tremor model of the reset (exo_set_tremor_model): per-axis maxima and sign mode
     double tjmax[7];                 // joint_max_values (generate_parkinson_tremor.py:59)
     int32_t tsign;                   // EXO_TREMOR_SIGN_*: per sample (:70), one per axis, none
+    // budgeted step (exo_set_step_budget; row-parallel kernels): at most `budget`
+    // RK45 step attempts per solve and launch, an unfinished solve's state carried
+    // to the next launch; an env with a pending solve starts no new step
+    int32_t budget;                  // 0 = unlimited (pend / rk unused)
+    uint8_t *pend;                   // [N] bit 0: the actuated solve pending, bit 1: the tremor-only solve
+    double *rk;                      // [RK_FIELDS][N] carried solver state (exo_step_rp.hip rk_field)
 };
+constexpr int RK_FIELDS = 72;       // 16 lanes x (q, v, a0, T) + 2 groups x (t, h_abs, attempts, flags)
 
 __host__ __device__ inline void matmul3(const double *A, const double *B, double *C) {
 #pragma unroll
@@ -427,7 +434,8 @@ __host__ __device__ inline double philox_u01(uint64_t seed, uint32_t env, uint32
 #ifndef EXO_HOST_ONLY
 // row-parallel step (csrc/exo_step_rp.hip): 16 lanes per env, for small env counts
 hipError_t launch_exo_step_rp(const Dev &S, const Urdf &U, const float *act, float *obs, float *rew, uint8_t *done,
-                              float *info, const uint8_t *active, hipStream_t stream, bool shared = false);
+                              float *info, const uint8_t *active, hipStream_t stream, bool shared = false,
+                              const float *obs_cur = nullptr);
 // multibody stepSimulation (csrc/exo_multibody.hip) of the envs with flag[e] != 0
 // (flag NULL = all); tgt [5][N]; clear_flag: zero the flags afterwards
 struct MbModel;

@@ -198,83 +198,149 @@ __device__ __forceinline__ double row_acc(const RowM &M, double T, double q, dou
 
 // scipy RK45 (common.py select_initial_step, rk.py _step_impl) for the row
 // this lane owns; same second-order storage as rk45_solve in exo_model.h.
+// The solver's whole state between two step attempts: this row's (q, v) and
+// FSAL acceleration a0, and the group-uniform t, h_abs, attempt count and
+// "inside a step after a rejection" flags -- a budgeted launch stops between
+// two attempts and the next launch continues from exactly this state.
+struct RkState {
+    double q, v, a0, t, h_abs;
+    int guard;
+    bool rejected, in_step;
+};
+
 template <typename RM>
-__device__ bool rk45_rows(const RM &M, double T, double &q_out, int &attempts) {
-    const double rtol = 1e-3, atol = 1e-6, tb = DT, inv_sqrt14 = 1.0 / 3.7416573867739413;
-    double q = 0.0, v = 0.0;
-    double a0 = row_acc(M, T, q, v);
-    double h_abs;
+__device__ __forceinline__ void rk45_begin(const RM &M, double T, RkState &s) {
+    const double atol = 1e-6, tb = DT, inv_sqrt14 = 1.0 / 3.7416573867739413;
+    s.q = 0.0;
+    s.v = 0.0;
+    s.a0 = row_acc(M, T, 0.0, 0.0);
     {
-        const double x1 = a0 / atol;
+        const double x1 = s.a0 / atol;
         const double d1 = sqrt(group_sum(x1 * x1)) * inv_sqrt14;
         const double h0 = 1e-6;
-        const double y1v = h0 * a0;
+        const double y1v = h0 * s.a0;
         const double a1 = row_acc(M, T, 0.0, y1v);
-        const double xq = y1v / atol, xv = (a1 - a0) / atol;
+        const double xq = y1v / atol, xv = (a1 - s.a0) / atol;
         const double d2 = sqrt(group_sum(xq * xq + xv * xv)) * inv_sqrt14 / h0;
         // scipy's (0.01 / max(d1, d2)) ** 0.2 with the library pow (once per solve)
         const double h1 = (d1 <= 1e-15 && d2 <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : pow(0.01 / fmax(d1, d2), 0.2);
-        h_abs = fmin(fmin(100 * h0, h1), tb);
+        s.h_abs = fmin(fmin(100 * h0, h1), tb);
     }
-    double t = 0.0;
-    int guard = 0;
-    bool ok = true;
-    while (t != tb && ok) {
-        const double min_step = 10 * fabs(nextafter(t, INFINITY) - t);
-        if (h_abs < min_step) h_abs = min_step;
-        bool rejected = false, accepted = false;
-        while (!accepted) {
-            if (h_abs < min_step || ++guard > 4096) { ok = false; break; }
-            double t_new = t + h_abs;
-            if (t_new - tb > 0) t_new = tb;
-            const double h = t_new - t, h2 = h * h;
-            h_abs = fabs(h);
-            double A[7];
-            A[0] = a0;
-            double qs = 0.0, vs = 0.0;
+    s.t = 0.0;
+    s.guard = 0;
+    s.rejected = s.in_step = false;
+}
+
+// Step attempts until t reaches dt: 1 = done, -1 = failed (step too small /
+// 4,096 attempts), 0 = `budget` (> 0) attempts used in this call with the
+// solve unfinished (the state is left between two attempts).  The attempt
+// sequence, and every value, is the one of an uninterrupted solve.
+template <typename RM>
+__device__ int rk45_advance(const RM &M, double T, RkState &s, int budget) {
+    const double rtol = 1e-3, atol = 1e-6, tb = DT, inv_sqrt14 = 1.0 / 3.7416573867739413;
+    int used = 0;
+    while (s.t != tb) {
+        const double min_step = 10 * fabs(nextafter(s.t, INFINITY) - s.t);
+        if (!s.in_step) {  // a new step (rk.py _step_impl): h_abs raised to min_step
+            if (s.h_abs < min_step) s.h_abs = min_step;
+            s.rejected = false;
+            s.in_step = true;
+        }
+        if (budget > 0 && used == budget) return 0;
+        if (s.h_abs < min_step || ++s.guard > 4096) return -1;
+        ++used;
+        const double q = s.q, v = s.v;
+        double t_new = s.t + s.h_abs;
+        if (t_new - tb > 0) t_new = tb;
+        const double h = t_new - s.t, h2 = h * h;
+        s.h_abs = fabs(h);
+        double A[7];
+        A[0] = s.a0;
+        double qs = 0.0, vs = 0.0;
 #pragma unroll
-            for (int st = 1; st < 6; ++st) {
-                double dv = 0.0, dq = 0.0;
+        for (int st = 1; st < 6; ++st) {
+            double dv = 0.0, dq = 0.0;
 #pragma unroll
-                for (int l = 0; l < st; ++l) { dv += A[l] * RK_A[st][l]; dq += A[l] * RKN.AA[st][l]; }
-                vs = v + dv * h;
-                qs = q + RKN.C[st] * h * v + dq * h2;
-                A[st] = row_acc(M, T, qs, vs);
-            }
-            {
-                double dv = A[0] * RK_B[0], dq = A[0] * RKN.BB[0] + A[1] * RKN.BB[1];
+            for (int l = 0; l < st; ++l) { dv += A[l] * RK_A[st][l]; dq += A[l] * RKN.AA[st][l]; }
+            vs = v + dv * h;
+            qs = q + RKN.C[st] * h * v + dq * h2;
+            A[st] = row_acc(M, T, qs, vs);
+        }
+        {
+            double dv = A[0] * RK_B[0], dq = A[0] * RKN.BB[0] + A[1] * RKN.BB[1];
 #pragma unroll
-                for (int l = 2; l < 5; ++l) { dv += A[l] * RK_B[l]; dq += A[l] * RKN.BB[l]; }
-                dv += A[5] * RK_B[5];
-                vs = v + h * dv; // y_new
-                qs = q + h * v + dq * h2;
-            }
-            A[6] = row_acc(M, T, qs, vs);
-            double ev = A[0] * RK_E[0], eq = A[0] * RKN.EE[0] + A[1] * RKN.EE[1];
+            for (int l = 2; l < 5; ++l) { dv += A[l] * RK_B[l]; dq += A[l] * RKN.BB[l]; }
+            dv += A[5] * RK_B[5];
+            vs = v + h * dv; // y_new
+            qs = q + h * v + dq * h2;
+        }
+        A[6] = row_acc(M, T, qs, vs);
+        double ev = A[0] * RK_E[0], eq = A[0] * RKN.EE[0] + A[1] * RKN.EE[1];
 #pragma unroll
-            for (int l = 2; l < 6; ++l) { ev += A[l] * RK_E[l]; eq += A[l] * RKN.EE[l]; }
-            ev += A[6] * RK_E[6];
-            const double e_q = eq * h2 / (atol + fmax(fabs(q), fabs(qs)) * rtol);
-            const double e_v = ev * h / (atol + fmax(fabs(v), fabs(vs)) * rtol);
-            const double en = sqrt(group_sum(e_q * e_q + e_v * e_v)) * inv_sqrt14;
-            if (en < 1) {
-                double factor = (en == 0) ? 10.0 : fmin(10.0, 0.9 * pow_m5th(en));
-                if (rejected) factor = fmin(1.0, factor);
-                h_abs *= factor;
-                t = t_new;
-                q = qs;
-                v = vs;
-                a0 = A[6];
-                accepted = true;
-            } else {
-                h_abs *= fmax(0.2, 0.9 * pow_m5th(en));
-                rejected = true;
-            }
+        for (int l = 2; l < 6; ++l) { ev += A[l] * RK_E[l]; eq += A[l] * RKN.EE[l]; }
+        ev += A[6] * RK_E[6];
+        const double e_q = eq * h2 / (atol + fmax(fabs(q), fabs(qs)) * rtol);
+        const double e_v = ev * h / (atol + fmax(fabs(v), fabs(vs)) * rtol);
+        const double en = sqrt(group_sum(e_q * e_q + e_v * e_v)) * inv_sqrt14;
+        if (en < 1) {
+            double factor = (en == 0) ? 10.0 : fmin(10.0, 0.9 * pow_m5th(en));
+            if (s.rejected) factor = fmin(1.0, factor);
+            s.h_abs *= factor;
+            s.t = t_new;
+            s.q = qs;
+            s.v = vs;
+            s.a0 = A[6];
+            s.in_step = false;
+        } else {
+            s.h_abs *= fmax(0.2, 0.9 * pow_m5th(en));
+            s.rejected = true;
         }
     }
-    q_out = ok ? q : NAN;
-    attempts = guard;
+    return 1;
+}
+
+// the uninterrupted solve
+template <typename RM>
+__device__ __forceinline__ bool rk45_rows(const RM &M, double T, double &q_out, int &attempts) {
+    RkState s;
+    rk45_begin(M, T, s);
+    const bool ok = rk45_advance(M, T, s, 0) > 0;
+    q_out = ok ? s.q : NAN;
+    attempts = s.guard;
     return ok;
+}
+
+// carried state of a budgeted solve: lane field f of sub-lane sb (0..15),
+// group field f of group g (t, h_abs, attempts, flags)
+__device__ __forceinline__ size_t rk_lane(int sb, int f, int e, int N) { return (size_t)(sb * 4 + f) * N + e; }
+__device__ __forceinline__ size_t rk_grp(int g, int f, int e, int N) { return (size_t)(64 + g * 4 + f) * N + e; }
+
+__device__ __forceinline__ void rk_save(const Dev &S, int e, int sub, int grp, int r, const RkState &s, double T) {
+    const int N = S.N;
+    S.rk[rk_lane(sub, 0, e, N)] = s.q;
+    S.rk[rk_lane(sub, 1, e, N)] = s.v;
+    S.rk[rk_lane(sub, 2, e, N)] = s.a0;
+    S.rk[rk_lane(sub, 3, e, N)] = T;
+    if (r == 0) {
+        S.rk[rk_grp(grp, 0, e, N)] = s.t;
+        S.rk[rk_grp(grp, 1, e, N)] = s.h_abs;
+        S.rk[rk_grp(grp, 2, e, N)] = (double)s.guard;
+        S.rk[rk_grp(grp, 3, e, N)] = (double)((s.rejected ? 1 : 0) | (s.in_step ? 2 : 0));
+    }
+}
+
+__device__ __forceinline__ void rk_load(const Dev &S, int e, int sub, int grp, RkState &s, double &T) {
+    const int N = S.N;
+    s.q = S.rk[rk_lane(sub, 0, e, N)];
+    s.v = S.rk[rk_lane(sub, 1, e, N)];
+    s.a0 = S.rk[rk_lane(sub, 2, e, N)];
+    T = S.rk[rk_lane(sub, 3, e, N)];
+    s.t = S.rk[rk_grp(grp, 0, e, N)];
+    s.h_abs = S.rk[rk_grp(grp, 1, e, N)];
+    s.guard = (int)S.rk[rk_grp(grp, 2, e, N)];
+    const int fl = (int)S.rk[rk_grp(grp, 3, e, N)];
+    s.rejected = fl & 1;
+    s.in_step = (fl & 2) != 0;
 }
 
 // CoM of link `link` (one of the 14 actuator anchors) given the FK frames.
@@ -285,6 +351,120 @@ __device__ __forceinline__ void anchor(const Urdf &U, int link, const double *R2
     else xform(R2, p0, U.xyz[link], o);
 }
 
+// The solve of this lane's row with the selected RHS exchange (template PULL
+// of the kernel): begin (a fresh solve) or continue the carried state `s`,
+// at most `budget` attempts (0: to the end).
+template <int PULL, int EPB>
+__device__ __forceinline__ int solve_rows(const RowM &M0, int r, double T, RkState &s, bool begin, int budget) {
+    if constexpr (PULL == 1) {
+        const RowD M{M0, r >= 4};
+        if (begin) rk45_begin(M, T, s);
+        return rk45_advance(M, T, s, budget);
+    } else if constexpr (PULL == 2) {
+        __shared__ double2 s_qv[64 * EPB / 4];
+        __shared__ double s_rr[64 * EPB / 4];
+        const RowL M{M0, s_qv, s_rr, (int)threadIdx.x, (int)(threadIdx.x & ~63u)};
+        if (begin) rk45_begin(M, T, s);
+        return rk45_advance(M, T, s, budget);
+    } else {
+        if (begin) rk45_begin(M0, T, s);
+        return rk45_advance(M0, T, s, budget);
+    }
+}
+
+// The sparse RHS rows of this lane (row r of the env's I^-1, D, S).
+__device__ __forceinline__ RowM load_rows(const Dev &S, int e, int r, int gbase) {
+    const int N = S.N;
+    RowM M0;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        constexpr unsigned long long KDS[4] = {pack_col(RP_DSYM, 0), pack_col(RP_DSYM, 1), pack_col(RP_DSYM, 2),
+                                               pack_col(RP_DSYM, 3)};
+        constexpr unsigned long long KIS[4] = {pack_col(RP_ISYM, 0), pack_col(RP_ISYM, 1), pack_col(RP_ISYM, 2),
+                                               pack_col(RP_ISYM, 3)};
+        constexpr unsigned long long KDC[4] = {pack_col(RP_DCOL, 0), pack_col(RP_DCOL, 1), pack_col(RP_DCOL, 2),
+                                               pack_col(RP_DCOL, 3)};
+        constexpr unsigned long long KIC[4] = {pack_col(RP_ICOL, 0), pack_col(RP_ICOL, 1), pack_col(RP_ICOL, 2),
+                                               pack_col(RP_ICOL, 3)};
+        const int ds = tab_at(KDS[m], r), is = tab_at(KIS[m], r);
+        // unconditional loads (field 0 for the pad entries), zeroed by a select
+        const double dv = S.dnz[(size_t)(ds >= 0 ? ds : 0) * N + e];
+        const double sv = S.snz[(size_t)(ds >= 0 ? ds : 0) * N + e];
+        const double iv = S.iinv[(size_t)(is >= 0 ? is : 0) * N + e];
+        M0.d[m] = ds >= 0 ? dv : 0.0;
+        M0.s[m] = ds >= 0 ? sv : 0.0;
+        M0.ii[m] = is >= 0 ? iv : 0.0;
+        M0.dsrc[m] = gbase + tab_at(KDC[m], r);
+        M0.isrc[m] = gbase + tab_at(KIC[m], r);
+    }
+    return M0;
+}
+
+// After a solve of the step whose counter was c (:417-433): the amplitude
+// into info (both groups), then -- actuated group -- the joint targets, the
+// idealised motor step or the multibody targets, and the
+// joint-range violation count.
+__device__ __forceinline__ void finish_solve(const Dev &S, const Urdf &U, int e, int grp, int r, int ebase, int c,
+                                             int motion, double qr, float *info) {
+    const int N = S.N;
+    const double qdeg = qr * (180 / PI); // :417-418
+    if (info && r < 7) info[(size_t)e * INFO + (grp == 0 ? 14 : 28) + r] = (float)qdeg;
+    if (grp != 0) return;
+    // ---- :421-433 joint targets and the idealised motor step (SURVEY.md A.2)
+    // lane r holds q[r]: joint 0 (shoulder z) <- q[2], 1 (y) <- q[0], 2 (x) <- q[1], 3 (elbow y) <- q[3]
+    const int joint = (r == 0) ? 1 : (r == 1) ? 2 : (r == 2) ? 0 : r; // r = 3, 4 -> joints 3, 4
+    const double *imu = S.imu + (size_t)motion * 5 * S.Lmax;
+    const int col = (joint == 0) ? 4 : (joint == 1) ? 3 : (joint == 2) ? 2 : (joint == 3) ? 0 : 1;
+    const double ang = imu[col * S.Lmax + c] + (joint < 4 ? qdeg : 0.0);
+    bool viol = false;
+    if (r < 5) {
+        if (S.mb_tgt) { // multibody mode: exo_multibody_kernel runs stepSimulation next
+            S.mb_tgt[(size_t)joint * N + e] = ang * (PI / 180);
+            if (r == 0) S.mb_flag[e] = 1;
+        } else {
+            const double q0 = S.phys_q[(size_t)joint * N + e];
+            const double nq = q0 + 0.1 * (ang * (PI / 180) - q0);
+            S.phys_q[(size_t)joint * N + e] = fmin(fmax(nq, U.lo[joint]), U.hi[joint]);
+        }
+        const double lo[4] = {-80, -40, -151.5, -10}, hi[4] = {80, 160.5, 33.5, 150};
+        if (joint < 4) viol = !(lo[joint] < ang && ang < hi[joint]); // check_movement_boundaries (:594-605)
+    }
+    const unsigned long long m = __ballot(viol);
+    if (r == 0 && ((m >> ebase) & 0xFull)) S.viol[e] += 1;
+}
+
+// Budgeted step, an env whose solve(s) a previous launch left unfinished: no
+// new step in this launch (its action is not consumed, the caller's mask
+// leaves it out); its observation row is carried into this launch's output
+// buffer (obs_cur -> obs: the trainer alternates two buffers); each pending
+// group continues its solve, and a solve that completes finishes its step.
+template <int PULL, int EPB>
+__device__ void resume_env(const Dev &S, const Urdf &U, int e, int sub, int grp, int r, int gbase, int ebase,
+                           int pend, float *obs, const float *obs_cur, float *info) {
+    if (obs_cur) {
+#pragma unroll
+        for (int k = 0; k < OBS / 16; ++k) obs[(size_t)e * OBS + sub + 16 * k] = obs_cur[(size_t)e * OBS + sub + 16 * k];
+    }
+    const bool mine = (pend >> grp) & 1;
+    int res = 1;
+    RkState st;
+    if (mine) {
+        const RowM M0 = load_rows(S, e, r, gbase);
+        double T;
+        rk_load(S, e, sub, grp, st, T);
+        res = solve_rows<PULL, EPB>(M0, r, T, st, false, S.budget);
+        if (res == 0) rk_save(S, e, sub, grp, r, st, T);
+        if (res < 0) atomicOr(S.err, 1);
+    }
+    const unsigned long long m = __ballot(mine && res == 0 && r == 0);
+    if (sub == 0) S.pend[e] = (uint8_t)(((m >> ebase) & 1) | (((m >> (ebase + 8)) & 1) << 1));
+    if (!mine || res == 0) return;
+#ifdef EXO_STAMPS
+    if (g_exo_rksteps && r == 0) g_exo_rksteps[(size_t)grp * S.N + e] = st.guard;  // the solve's total attempts
+#endif
+    finish_solve(S, U, e, grp, r, ebase, S.counts[e] - 1, S.motion[e], res > 0 ? st.q : NAN, info);
+}
+
 // 16 envs (4 wavefronts) per workgroup: the state is SoA over envs, so one
 // 128-byte line of a double field holds 16 consecutive envs -- a 4-env
 // workgroup left each line to four workgroups on (round-robin) different XCDs
@@ -292,15 +472,24 @@ __device__ __forceinline__ void anchor(const Urdf &U, int link, const double *R2
 constexpr int RP_ENVS_PER_BLOCK = 16;
 
 // PULL: the RHS neighbour exchange -- 0 LDS permutes, 1 DPP lane moves, 2 LDS slots (default)
-template <int PULL, int EPB = RP_ENVS_PER_BLOCK>
+// BUD: budgeted solves (S.budget > 0, S.pend / S.rk allocated; exo_set_step_budget)
+template <int PULL, int EPB = RP_ENVS_PER_BLOCK, bool BUD = false>
 __global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
     Dev S, Urdf U, const float *__restrict__ act, float *__restrict__ obs, float *__restrict__ rew,
-    uint8_t *__restrict__ done, float *__restrict__ info, const uint8_t *__restrict__ active) {
+    uint8_t *__restrict__ done, float *__restrict__ info, const uint8_t *__restrict__ active,
+    const float *__restrict__ obs_cur) {
     const int lane = threadIdx.x & 63;
     const int sub = lane & 15, grp = sub >> 3, r = sub & 7, gbase = lane & ~7, ebase = lane & ~15;
     const int e = blockIdx.x * EPB + (threadIdx.x >> 4);
     if (e >= S.N) return;
     const int N = S.N, c = S.counts[e], L = S.L[e];
+    if constexpr (BUD) {
+        const int pend = S.pend[e];  // uniform over the env's 16 lanes
+        if (pend) {
+            resume_env<PULL, EPB>(S, U, e, sub, grp, r, gbase, ebase, pend, obs, obs_cur, info);
+            return;
+        }
+    }
     if ((active && !active[e]) || c >= L - 1) return; // uniform over the env's 16 lanes
     STAMP(0);
 
@@ -334,28 +523,7 @@ __global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
     float posv_old[3];
 #pragma unroll
     for (int d = 0; d < 3; ++d) posv_old[d] = S.posv[(size_t)(j * 3 + d) * N + e];
-    RowM M0;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        constexpr unsigned long long KDS[4] = {pack_col(RP_DSYM, 0), pack_col(RP_DSYM, 1), pack_col(RP_DSYM, 2),
-                                               pack_col(RP_DSYM, 3)};
-        constexpr unsigned long long KIS[4] = {pack_col(RP_ISYM, 0), pack_col(RP_ISYM, 1), pack_col(RP_ISYM, 2),
-                                               pack_col(RP_ISYM, 3)};
-        constexpr unsigned long long KDC[4] = {pack_col(RP_DCOL, 0), pack_col(RP_DCOL, 1), pack_col(RP_DCOL, 2),
-                                               pack_col(RP_DCOL, 3)};
-        constexpr unsigned long long KIC[4] = {pack_col(RP_ICOL, 0), pack_col(RP_ICOL, 1), pack_col(RP_ICOL, 2),
-                                               pack_col(RP_ICOL, 3)};
-        const int ds = tab_at(KDS[m], r), is = tab_at(KIS[m], r);
-        // unconditional loads (field 0 for the pad entries), zeroed by a select
-        const double dv = S.dnz[(size_t)(ds >= 0 ? ds : 0) * N + e];
-        const double sv = S.snz[(size_t)(ds >= 0 ? ds : 0) * N + e];
-        const double iv = S.iinv[(size_t)(is >= 0 ? is : 0) * N + e];
-        M0.d[m] = ds >= 0 ? dv : 0.0;
-        M0.s[m] = ds >= 0 ? sv : 0.0;
-        M0.ii[m] = is >= 0 ? iv : 0.0;
-        M0.dsrc[m] = gbase + tab_at(KDC[m], r);
-        M0.isrc[m] = gbase + tab_at(KIC[m], r);
-    }
+    const RowM M0 = load_rows(S, e, r, gbase);
     const int seq = S.seq[e], motion = S.motion[e];
     double R2[9], R4[9], p0[3], p3[3];
     {
@@ -511,48 +679,21 @@ __global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
     STAMP(3);
     // ---- the two joint ODE solves (:409-414), one row per lane
     const double T = (r < 7) ? (grp == 0 ? Ta_r : tr_r) : 0.0;
-    double qr;
-    bool ok;
-    int attempts = 0;
-    if constexpr (PULL == 1) {
-        ok = rk45_rows(RowD{M0, r >= 4}, T, qr, attempts);
-    } else if constexpr (PULL == 2) {
-        __shared__ double2 s_qv[64 * EPB / 4];
-        __shared__ double s_rr[64 * EPB / 4];
-        ok = rk45_rows(RowL{M0, s_qv, s_rr, (int)threadIdx.x, (int)(threadIdx.x & ~63u)}, T, qr, attempts);
-    } else {
-        ok = rk45_rows(M0, T, qr, attempts);
+    RkState st;
+    const int res = solve_rows<PULL, EPB>(M0, r, T, st, true, BUD ? S.budget : 0);
+    if constexpr (BUD) {
+        // unfinished within the budget: the state is carried to the next launch
+        if (res == 0) rk_save(S, e, sub, grp, r, st, T);
+        const unsigned long long pm = __ballot(res == 0 && r == 0);
+        if (sub == 0) S.pend[e] = (uint8_t)(((pm >> ebase) & 1) | (((pm >> (ebase + 8)) & 1) << 1));
+        if (res == 0) return;
     }
-    if (!ok) atomicOr(S.err, 1);
+    if (res < 0) atomicOr(S.err, 1);
 #ifdef EXO_STAMPS
-    if (g_exo_rksteps && r == 0) g_exo_rksteps[(size_t)grp * N + e] = attempts;
+    if (g_exo_rksteps && r == 0) g_exo_rksteps[(size_t)grp * N + e] = st.guard;
 #endif
     STAMP(4);
-    const double qdeg = qr * (180 / PI); // :417-418
-    if (info && r < 7) info[(size_t)e * INFO + (grp == 0 ? 14 : 28) + r] = (float)qdeg;
-    if (grp != 0) return;
-
-    // ---- :421-433 joint targets and the idealised motor step (SURVEY.md A.2)
-    // lane r holds q[r]: joint 0 (shoulder z) <- q[2], 1 (y) <- q[0], 2 (x) <- q[1], 3 (elbow y) <- q[3]
-    const int joint = (r == 0) ? 1 : (r == 1) ? 2 : (r == 2) ? 0 : r; // r = 3, 4 -> joints 3, 4
-    const double *imu = S.imu + (size_t)motion * 5 * S.Lmax;
-    const int col = (joint == 0) ? 4 : (joint == 1) ? 3 : (joint == 2) ? 2 : (joint == 3) ? 0 : 1;
-    const double ang = imu[col * S.Lmax + c] + (joint < 4 ? qdeg : 0.0);
-    bool viol = false;
-    if (r < 5) {
-        if (S.mb_tgt) { // multibody mode: exo_multibody_kernel runs stepSimulation next
-            S.mb_tgt[(size_t)joint * N + e] = ang * (PI / 180);
-            if (r == 0) S.mb_flag[e] = 1;
-        } else {
-            const double q0 = S.phys_q[(size_t)joint * N + e];
-            const double nq = q0 + 0.1 * (ang * (PI / 180) - q0);
-            S.phys_q[(size_t)joint * N + e] = fmin(fmax(nq, U.lo[joint]), U.hi[joint]);
-        }
-        const double lo[4] = {-80, -40, -151.5, -10}, hi[4] = {80, 160.5, 33.5, 150};
-        if (joint < 4) viol = !(lo[joint] < ang && ang < hi[joint]); // check_movement_boundaries (:594-605)
-    }
-    const unsigned long long m = __ballot(viol);
-    if (r == 0 && ((m >> ebase) & 0xFull)) S.viol[e] += 1;
+    finish_solve(S, U, e, grp, r, ebase, c, motion, res > 0 ? st.q : NAN, info);
     STAMP(5);
 }
 
@@ -569,7 +710,8 @@ extern "C" int exo_debug_set_rksteps(int32_t *buf) {
 
 namespace exo {
 hipError_t launch_exo_step_rp(const Dev &S, const Urdf &U, const float *act, float *obs, float *rew, uint8_t *done,
-                              float *info, const uint8_t *active, hipStream_t stream, bool shared) {
+                              float *info, const uint8_t *active, hipStream_t stream, bool shared,
+                              const float *obs_cur) {
     // RHS neighbour exchange (EXO_RP_GATHER, all bit-identical): 2 = wave-private
     // LDS slots, 16-byte writes / reads (default: 26.8 vs 31.1 us at 4,096 envs,
     // profiles/r02f_raw/ab_pull.txt); 0 = LDS permutes (ds_bpermute, 4 32-bit
@@ -584,23 +726,39 @@ hipError_t launch_exo_step_rp(const Dev &S, const Urdf &U, const float *act, flo
     // whole for kernels running beside the step (the trainer's fused TD7
     // passes need a CU's full register file); 16 envs / 256 threads spread
     // over every CU (fastest alone)
+    // budgeted solves (exo_set_step_budget): the LDS-slot exchange only
+    if (S.budget > 0) {
+        if (shared) {
+            hipLaunchKernelGGL((exo_step_rp_kernel<2, 32, true>), dim3((S.N + 31) / 32), dim3(512), 0, stream, S, U,
+                               act, obs, rew, done, info, active, obs_cur);
+        } else {
+            hipLaunchKernelGGL((exo_step_rp_kernel<2, RP_ENVS_PER_BLOCK, true>),
+                               dim3((S.N + RP_ENVS_PER_BLOCK - 1) / RP_ENVS_PER_BLOCK),
+                               dim3(64 * RP_ENVS_PER_BLOCK / 4), 0, stream, S, U, act, obs, rew, done, info, active,
+                               obs_cur);
+        }
+        return hipGetLastError();
+    }
     if (shared && pull != 1) {
         const dim3 grid((S.N + 31) / 32), block(512);
         if (pull == 2)
             hipLaunchKernelGGL((exo_step_rp_kernel<2, 32>), grid, block, 0, stream, S, U, act, obs, rew, done, info,
-                               active);
+                               active, obs_cur);
         else
             hipLaunchKernelGGL((exo_step_rp_kernel<0, 32>), grid, block, 0, stream, S, U, act, obs, rew, done, info,
-                               active);
+                               active, obs_cur);
         return hipGetLastError();
     }
     const dim3 grid((S.N + RP_ENVS_PER_BLOCK - 1) / RP_ENVS_PER_BLOCK), block(64 * RP_ENVS_PER_BLOCK / 4);
     if (pull == 1)
-        hipLaunchKernelGGL(exo_step_rp_kernel<1>, grid, block, 0, stream, S, U, act, obs, rew, done, info, active);
+        hipLaunchKernelGGL(exo_step_rp_kernel<1>, grid, block, 0, stream, S, U, act, obs, rew, done, info, active,
+                           obs_cur);
     else if (pull == 2)
-        hipLaunchKernelGGL(exo_step_rp_kernel<2>, grid, block, 0, stream, S, U, act, obs, rew, done, info, active);
+        hipLaunchKernelGGL(exo_step_rp_kernel<2>, grid, block, 0, stream, S, U, act, obs, rew, done, info, active,
+                           obs_cur);
     else
-        hipLaunchKernelGGL(exo_step_rp_kernel<0>, grid, block, 0, stream, S, U, act, obs, rew, done, info, active);
+        hipLaunchKernelGGL(exo_step_rp_kernel<0>, grid, block, 0, stream, S, U, act, obs, rew, done, info, active,
+                           obs_cur);
     return hipGetLastError();
 }
 } // namespace exo

@@ -38,8 +38,9 @@ __device__ __forceinline__ float *stratum_tree(float *tree, int s, int cap) { re
 // fewer -- and the recomputed nodes [1, TOPN/2) are written back.  The same
 // additions in the same order: the sums are bit-identical.
 constexpr int TOPN = 8192;
-__device__ void propagate(float *T, int cap, int levels, const int32_t *slot, int n) {
-    __shared__ float top[TOPN];
+// top: the caller's LDS array of TOPN floats; on return (true) it holds the
+// final nodes [1, min(TOPN, 2 cap)) (false: no level was staged, T holds them)
+__device__ bool propagate_top(float *T, int cap, int levels, const int32_t *slot, int n, float *top) {
     int lv = 1;
     for (; lv <= levels && ((2 * cap) >> lv) > TOPN / 2; ++lv) {
         __syncthreads();
@@ -49,7 +50,7 @@ __device__ void propagate(float *T, int cap, int levels, const int32_t *slot, in
         }
     }
     __syncthreads();
-    if (lv > levels) return;
+    if (lv > levels) return false;
     const int lim = min(TOPN, 2 * cap);
     for (int i = threadIdx.x; i < lim; i += blockDim.x) top[i] = T[i];
     for (; lv <= levels; ++lv) {
@@ -63,6 +64,11 @@ __device__ void propagate(float *T, int cap, int levels, const int32_t *slot, in
     const int wb = min(TOPN / 2, cap);
     for (int i = 1 + threadIdx.x; i < wb; i += blockDim.x) T[i] = top[i];
     __syncthreads();
+    return true;
+}
+__device__ void propagate(float *T, int cap, int levels, const int32_t *slot, int n) {
+    __shared__ float top[TOPN];
+    propagate_top(T, cap, levels, slot, n, top);
 }
 
 // The same recomputation for the leaves of a ring span: `count` consecutive
@@ -612,6 +618,7 @@ __global__ __launch_bounds__(UPD_THREADS) void lap_store_ref_fused_kernel(
         if (carry_slot >= 0 && wv == 0 && carry_J % K == part)
             copy_rows<VEC>(st, state, action, next_state, reward, done, action_scale, &carry_i, &carry_slot, s,
                            capacity, 0, 1, 1, lane, 64);
+        __syncthreads();  // the loop below sets the next carry: wave 0 must be done reading this one
         for (int jj = t; jj < m; jj += UPD_THREADS) {
             const int r = rk[jj];
             if (jj + 1 == m) {  // successor unknown until a later chunk (or none: a winner)
@@ -764,6 +771,116 @@ __global__ __launch_bounds__(256) void lap_sample_gather_kernel(const float *tre
 }
 
 
+// LAP.update_priority (:113-117) and the NEXT LAP.sample (:65-111) as ONE
+// launch (r04: lap_update_kernel + lap_sample_gather_kernel were 32 us plus a
+// queue hand-off at the end of every critic-only iteration).  One workgroup
+// per stratum: the update exactly as lap_update_kernel (last duplicate wins,
+// level-synchronous ancestors, the max_priority atomic), whose staged top
+// levels stay in LDS; then the stratum's `batch` draws (Philox block d =
+// s * batch + b of call *counter, as lap_sample_gather_kernel) descend with
+// the nodes below TOPN read from LDS, and the workgroup gathers their rows.
+// The same sums and comparisons: bit-identical to the two launches.
+__global__ __launch_bounds__(UPD_THREADS) void lap_update_sample_kernel(float *tree, float *maxp, int cap, int levels,
+                                                                        int capacity, const int32_t *idx_in,
+                                                                        const float *prio, int batch,
+                                                                        const int32_t *size, lap_storage_desc st,
+                                                                        SampleRng rng, int32_t *idx_out,
+                                                                        float *o_state, float *o_action, float *o_next,
+                                                                        float *o_reward, float *o_not_done) {
+    const int s = blockIdx.x;
+    float *T = stratum_tree(tree, s, cap);
+    const int32_t *I = idx_in + (size_t)s * batch;
+    const float *P = prio + (size_t)s * batch;
+    __shared__ float red[UPD_THREADS / 64];
+    __shared__ int32_t li[UPD_THREADS];
+    __shared__ float top[TOPN];
+    __shared__ int32_t pick[UPD_THREADS];
+    const unsigned long long call = *rng.counter;  // read before any workgroup can take the ticket
+    float mx = 0.0f;
+    for (int b0 = 0; b0 < batch; b0 += UPD_THREADS) {
+        const int nb = min(UPD_THREADS, batch - b0);
+        __syncthreads();
+        if ((int)threadIdx.x < nb) li[threadIdx.x] = I[b0 + threadIdx.x];
+        __syncthreads();
+        const int b = b0 + threadIdx.x;
+        if (b < batch) {
+            const int me = li[threadIdx.x];
+            bool last = true;
+            for (int k = threadIdx.x + 1; k < nb; ++k) last &= (li[k] != me);
+            for (int b2 = b0 + nb; b2 < batch; ++b2) last &= (I[b2] != me);
+            if (last) T[cap + me] = P[b];
+            mx = fmaxf(mx, P[b]);
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+    const bool staged = propagate_top(T, cap, levels, I, batch, top);
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) mx = fmaxf(mx, red[w]);
+        atomicMax(reinterpret_cast<int *>(maxp), __float_as_int(mx));
+    }
+    // ---- the next batch of this stratum
+    const int lim = staged ? min(TOPN, 2 * cap) : 0;
+    auto node_at = [&](int node) { return node < lim ? top[node] : T[node]; };
+    const int sz = size[s];
+    for (int b = threadIdx.x; b < batch; b += UPD_THREADS) {
+        const int d = s * batch + b;
+        uint32_t r[4];
+        philox_block(rng.seed, rng.tag, call, (uint32_t)d, r);
+        float tot;
+        if (sz >= cap) {
+            tot = node_at(1);
+        } else {  // prefix_total
+            tot = 0.0f;
+            int node = 1;
+            for (int lv = levels - 1; lv >= 0; --lv) {
+                if ((sz >> lv) & 1) {
+                    tot += node_at(2 * node);
+                    node = 2 * node + 1;
+                } else {
+                    node = 2 * node;
+                }
+            }
+        }
+        float val = u01_open_hi(r[0]) * tot;
+        int node = 1;
+        for (int lv = 0; lv < levels; ++lv) {
+            const float left = node_at(2 * node), right = node_at(2 * node + 1);
+            if (val <= left || right <= 0.0f) {
+                node = 2 * node;
+            } else {
+                val -= left;
+                node = 2 * node + 1;
+            }
+        }
+        int i = node - cap;
+        if (i >= sz) i = sz > 0 ? sz - 1 : 0;
+        idx_out[d] = i;
+        if (b < UPD_THREADS) pick[b] = i;
+    }
+    __syncthreads();
+    // gather: (draw, item) over the workgroup, items = state, next_state, action, reward, not_done
+    const int sd = st.state_dim, ad = st.action_dim, per = 2 * sd + ad + 2;
+    for (int it = threadIdx.x; it < min(batch, UPD_THREADS) * per; it += UPD_THREADS) {
+        const int b = it / per, c = it - b * per;
+        const long d = (long)s * batch + b;
+        const long row = (long)s * (capacity + 1) + pick[b];
+        if (c < sd) o_state[d * sd + c] = st.state[row * sd + c];
+        else if (c < 2 * sd) o_next[d * sd + c - sd] = st.next_state[row * sd + c - sd];
+        else if (c < 2 * sd + ad) o_action[d * ad + c - 2 * sd] = st.action[row * ad + c - 2 * sd];
+        else if (c == 2 * sd + ad) o_reward[d] = st.reward[row];
+        else o_not_done[d] = st.not_done[row];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(rng.ticket, 1u) == gridDim.x - 1) {
+            *rng.counter = call + 1ull;
+            *rng.ticket = 0u;
+        }
+    }
+}
+
 int rc(hipError_t e) { return e == hipSuccess ? EXO_OK : EXO_EDEVICE; }
 
 int levels_of(const lap_tree_desc *t) {
@@ -914,6 +1031,20 @@ int lap_sample_gather(const lap_tree_desc *t, const lap_storage_desc *st, const 
     hipLaunchKernelGGL(lap_sample_gather_kernel, dim3((total + 3) / 4), dim3(256), 0, (hipStream_t)stream, t->tree,
                        t->cap, levels_of(t), t->capacity, u, st->size, batch, total, idx, *st, out_state, out_action,
                        out_next_state, out_reward, out_not_done, SampleRng{0, 0, nullptr, nullptr});
+    return rc(hipGetLastError());
+}
+
+int lap_update_sample_rng(const lap_tree_desc *t, const lap_storage_desc *st, const int32_t *idx_in,
+                          const float *prio, int32_t batch, uint64_t seed, uint32_t tag, unsigned long long *counter,
+                          uint32_t *ticket, int32_t *idx_out, float *out_state, float *out_action,
+                          float *out_next_state, float *out_reward, float *out_not_done, void *stream) {
+    if (!valid(t) || !st || !st->size || !idx_in || !prio || !counter || !ticket || !idx_out || batch <= 0 ||
+        batch > UPD_THREADS || !out_state || !out_action || !out_next_state || !out_reward || !out_not_done)
+        return EXO_EINVAL;
+    hipLaunchKernelGGL(lap_update_sample_kernel, dim3(t->n_strata), dim3(UPD_THREADS), 0, (hipStream_t)stream,
+                       t->tree, t->max_priority, t->cap, levels_of(t), t->capacity, idx_in, prio, batch, st->size,
+                       *st, SampleRng{seed, tag, counter, ticket}, idx_out, out_state, out_action, out_next_state,
+                       out_reward, out_not_done);
     return rc(hipGetLastError());
 }
 

@@ -112,6 +112,9 @@ EXPORTS = {
     "exo_set_state_host": (c_int32, [c_void_p, c_int32, P(c_double)]),
     "exo_set_seed": (c_int32, [c_void_p, c_uint64]),
     "exo_set_step_variant": (c_int32, [c_void_p, c_int32]),
+    "exo_set_step_budget": (c_int32, [c_void_p, c_int32]),
+    "exo_step_carry": (c_int32, [c_void_p] * 9),
+    "exo_budget_advance": (c_int32, [c_void_p] * 6),
     "exo_multibody_default_params": (None, [P(ExoMbParams)]),
     "exo_set_physics": (c_int32, [c_void_p, c_int32, P(ExoMbParams)]),
     "exo_multibody_advance": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -141,6 +144,9 @@ EXPORTS = {
     "lap_store_batch_ref_fused": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                             c_void_p, c_void_p, c_void_p, ctypes.c_float, c_int32, c_void_p,
                                             c_void_p]),
+    "lap_update_sample_rng": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, ctypes.c_uint64,
+                                        ctypes.c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                        c_void_p, c_void_p, c_void_p]),
     "lap_sample_gather_rng": (c_int32, [c_void_p, c_void_p, ctypes.c_uint64, ctypes.c_uint32, c_void_p, c_void_p,
                                         c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_void_p]),

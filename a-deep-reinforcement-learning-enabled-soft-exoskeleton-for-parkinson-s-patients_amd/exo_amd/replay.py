@@ -248,6 +248,29 @@ class LAP:
         nat.check(nat.lib().lap_update(ctypes.byref(self._desc), nat.ptr(ind), nat.ptr(pr), ind.shape[1],
                                        self._stream()), "lap_update")
 
+    # LAP.update_priority + the next sample as one launch (lap_update_sample_rng,
+    # r04); EXO_LAP_FUSED=0: the two launches
+    fuse_update_sample = os.environ.get("EXO_LAP_FUSED", "1") != "0"
+
+    def update_priority_and_sample(self, priority, ind=None, slot=None):
+        """update_priority(priority, ind) then sample(slot), the same values; one
+        launch with the device RNG (the sampled batch in the slot's buffers,
+        self.ind = its indices)."""
+        ind = self.ind if ind is None else ind
+        if not (self.device_rng and self.fuse_update_sample and self.batch_size <= 1024):
+            self.update_priority(priority, ind)
+            return self.sample(slot)
+        pr = priority.detach().to(torch.float32).reshape(-1).contiguous()
+        assert pr.numel() == ind.numel()
+        batch, idx = self._slot(slot)
+        r = self._rng
+        nat.check(nat.lib().lap_update_sample_rng(ctypes.byref(self._desc), ctypes.byref(self._store), nat.ptr(ind),
+                                                  nat.ptr(pr), ind.shape[1], r.seed, r.tag, r.counter_ptr,
+                                                  r.ticket_ptr, nat.ptr(idx), *[nat.ptr(t) for t in batch],
+                                                  self._stream()), "lap_update_sample_rng")
+        self.ind = idx
+        return batch
+
     def reset_max_priority(self):
         nat.check(nat.lib().lap_reset_max(ctypes.byref(self._desc), self._stream()), "lap_reset_max")
 

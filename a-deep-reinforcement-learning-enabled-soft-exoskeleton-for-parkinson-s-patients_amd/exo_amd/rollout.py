@@ -232,6 +232,17 @@ class VecTrainer:
             raise ValueError(f"exploration must be 'gaussian' or 'pink', not {exploration!r}")
         self.exploration = exploration
         self.k_dev = torch.zeros((1,), dtype=torch.int64, device=self.device)
+        # budgeted env steps (env.set_step_budget, BASELINE configs[3]): a stiff
+        # env's solve spans launches; the step mask then comes from the device
+        # (exo_budget_advance: episode not over and no solve pending) and a
+        # round lasts until every env finished (`remaining` read by the host
+        # once the round's round_len iterations are done)
+        self.budget = int(getattr(env, "step_budget", 0))
+        if self.budget:
+            if exploration == "pink":
+                raise ValueError("Pink exploration indexes its noise by the round's step: not with a step budget")
+            self._remaining = torch.zeros((1,), dtype=torch.int32, device=self.device)
+            self._steps_total = torch.zeros((1,), dtype=torch.int64, device=self.device)
         if exploration == "pink":
             agent.init_episode_noise_device(self.round_len)
         if use_graphs and os.environ.get("EXO_GRAPH_CHECK", "1") != "0":
@@ -243,7 +254,8 @@ class VecTrainer:
         obs = self.obs
         act = ag.select_action_batch(obs, timestep=self.k_dev if self.exploration == "pink" else None,
                                      dec_count=self.active_count)
-        nobs, rew, done, info = self.env.step(act, active=self.active, out=self._outs[self._cur])
+        nobs, rew, done, info = self.env.step(act, active=self.active, out=self._outs[self._cur],
+                                              obs_cur=obs if self.budget else None)
         ag.replay_buffer.add_batch(obs, act, nobs, rew, done, self.strata, self.active)
         self._advance()
         self.last_actions = act
@@ -251,7 +263,11 @@ class VecTrainer:
     def _advance(self, rew=None, score=None):
         """The next step's active mask and count on the device (exo_active_advance);
         with rew / score: score += rew where the replaced mask is set, in the same
-        launch (exo_active_advance_score)."""
+        launch (exo_active_advance_score).  Step budget: the mask from the
+        envs' own progress (exo_budget_advance)."""
+        if self.budget:
+            self.env.budget_advance(self.active, self.active_count, self._remaining, self._steps_total)
+            return
         if score is not None:
             nat.check(nat.lib().exo_active_advance_score(
                 nat.ptr(self._table_ext), self._table_ext.shape[0], self.n, nat.ptr(self.k_dev), nat.ptr(self.active),
@@ -367,26 +383,31 @@ class VecTrainer:
             self._pside = prio_stream()
             self._pside.wait_stream(cur)
             with torch.cuda.stream(self._pside):
-                ag.replay_buffer.update_priority(self._prio, self._ind)
+                self._update_and_sample_next()
                 if inline:
                     ag.sync.max_(ag.replay_buffer._maxp)
-                self._sample_next()
             ag.learner.phase_steps(flat_grad, grad_scale)
         else:
             ag.learner.phase_steps(flat_grad, grad_scale)
-            ag.replay_buffer.update_priority(self._prio, self._ind)
+            self._update_and_sample_next()
             if inline:
                 self._pside = prio_stream()
                 self._pside.wait_stream(cur)
                 with torch.cuda.stream(self._pside):
                     ag.sync.max_(ag.replay_buffer._maxp)
-            self._sample_next()
         if update_actor:
             ag.learner.phase_actor_grads(self._batch[0], self._batch[1])
 
-    def _sample_next(self):
+    def _update_and_sample_next(self):
+        """LAP.update_priority of this iteration's batch, then (prefetching) the
+        next iteration's batch into the other slot -- one launch
+        (LAP.update_priority_and_sample).  The MAX all-reduce of max_priority
+        (data parallel) follows; the sample does not read it."""
+        rb = self.agent.replay_buffer
         if self._prefetching() and self._mid_rollout:
-            self.agent.replay_buffer.sample(1 - self._cur)
+            rb.update_priority_and_sample(self._prio, self._ind, 1 - self._cur)
+        else:
+            rb.update_priority(self._prio, self._ind)
 
     def _join_prio(self):
         if getattr(self, "_pside", None) is not None:
@@ -501,11 +522,24 @@ class VecTrainer:
             g3.replay()
 
     # ------------------------------------------------------------- step
+    def next_step_resets(self):
+        """Whether the next step() starts a new episode round: after round_len
+        iterations, and with a step budget once no env is left unfinished (a
+        host read of the device count)."""
+        if self.k < self.round_len:
+            return False
+        return not self.budget or int(self._remaining.item()) == 0
+
+    def env_steps_total(self):
+        """Step budget: the env-steps taken so far (device counter, host sync)."""
+        return int(self._steps_total.item())
+
     def step(self):
-        """One training iteration; returns the number of active env-steps."""
+        """One training iteration; returns the number of active env-steps (with
+        a step budget 0: the count stays on the device, env_steps_total())."""
         ag = self.agent
         L = ag.learner
-        if self.k == self.round_len:
+        if self.next_step_resets():
             self.env.reset(obs_out=self.obs)
             self._round_start()
             self.resets += 1
@@ -523,7 +557,7 @@ class VecTrainer:
         if L.maybe_update_targets():
             ag.replay_buffer.reset_max_priority()
             ag.sync.max_(ag.replay_buffer._maxp)
-        n_active = int(self.active_counts[self.k])
+        n_active = 0 if self.budget else int(self.active_counts[self.k])
         self.k += 1
         self.iters += 1
         self._cur ^= 1  # the next observation is in the other buffer
@@ -563,6 +597,8 @@ class RefScheduleTrainer(VecTrainer):
 
     def __init__(self, env, agent, warmup=25_000, strata=None, use_graphs=True, ref_replay=True,
                  action_source=None, reset_source=None, warmup_eager=2, round_graph=None, stats=None):
+        if getattr(env, "step_budget", 0):
+            raise ValueError("RefScheduleTrainer steps the script's synchronous episodes: no step budget")
         super().__init__(env, agent, strata=strata, use_graphs=use_graphs, warmup_eager=warmup_eager,
                          shared_step=False)
         # the rollout runs alone (no TD7 pass beside it): the env step's own fast shape

@@ -121,12 +121,15 @@ class VecExoskeletonEnv:
         nat.check(nat.lib().exo_reset(self._ctx, nat.ptr(m), nat.ptr(obs), self._stream()), "exo_reset", self._ctx)
         return obs
 
-    def step(self, actions, active=None, out=None, with_info=True):
+    def step(self, actions, active=None, out=None, with_info=True, obs_cur=None):
         """One step for every env (Exoskeleton_env.py:368-471).
 
         actions: float32 [N, 7] device tensor in [-1, 1].  active: optional
         bool/uint8 [N]; inactive envs and envs already done are skipped and
-        their rows in the outputs are left untouched.  Returns
+        their rows in the outputs are left untouched.  With a step budget
+        (set_step_budget) an env with a pending solve continues it instead of
+        stepping and, given obs_cur (the current observations), copies its row
+        into the output buffer.  Returns
         (obs [N,80] f32, reward [N] f32, done [N] bool, info [N,40] f32 or None)."""
         a = actions
         if a.dtype != torch.float32 or not a.is_contiguous() or a.device != self.device:
@@ -141,10 +144,30 @@ class VecExoskeletonEnv:
                 act = active.view(torch.uint8)  # same bytes, no conversion kernel
             else:
                 act = active.to(device=self.device, dtype=torch.uint8).contiguous()
-        rc = nat.lib().exo_step(self._ctx, nat.ptr(a), nat.ptr(obs), nat.ptr(rew), nat.ptr(done),
-                                nat.ptr(info) if with_info else None, nat.ptr(act), self._stream())
+        rc = nat.lib().exo_step_carry(self._ctx, nat.ptr(a), nat.ptr(obs), nat.ptr(rew), nat.ptr(done),
+                                      nat.ptr(info) if with_info else None, nat.ptr(act), nat.ptr(obs_cur),
+                                      self._stream())
         nat.check(rc, "exo_step", self._ctx)
         return obs, rew, done.view(torch.bool), info
+
+    step_budget = 0
+
+    def set_step_budget(self, budget):
+        """At most `budget` RK45 step attempts per ODE solve and launch (0 = no
+        limit; include/exo_amd.h exo_set_step_budget): a stiff env's solve
+        continues over several launches, its trajectory unchanged, instead of
+        holding every launch for its whole solve."""
+        nat.check(nat.lib().exo_set_step_budget(self._ctx, int(budget)), "exo_set_step_budget", self._ctx)
+        self.step_budget = int(budget)
+
+    def budget_advance(self, active, count, remaining, steps_total=None):
+        """Budget mode's mask for the next launch (exo_budget_advance): active
+        (bool [N]) = envs that will start a step, count (int32 [1]) their
+        number, remaining (int32 [1]) the envs not finished, steps_total (int64
+        [1]) += the envs the last launch stepped."""
+        nat.check(nat.lib().exo_budget_advance(self._ctx, nat.ptr(active), nat.ptr(count), nat.ptr(remaining),
+                                               nat.ptr(steps_total), self._stream()), "exo_budget_advance",
+                  self._ctx)
 
     def new_outputs(self, with_info=True):
         d = self.device

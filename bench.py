@@ -132,6 +132,9 @@ def parse():
     ap.add_argument("--precision", choices=["bf16", "fp16", "fp32"], default=None,
                     help="TD7 MFMA operands (workload default: bf16 per configs[1], fp16 for wide)")
     ap.add_argument("--batch", type=int, default=None, help="TD7 rows per stratum (default 128)")
+    ap.add_argument("--step-budget", type=int, default=None,
+                    help="RK45 attempts per solve and env-step launch (exo_set_step_budget; default: 0 = no limit, "
+                         "dr_sweep 160)")
     ap.add_argument("--cpu-threads", type=int, default=None, help="threads of the multi-core CPU baseline")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -147,6 +150,8 @@ def parse():
         a.envs = {"configs1": 4096, "dr_sweep": 16384, "wide": 65536}[a.workload]
     if a.precision is None:
         a.precision = "fp16" if a.workload == "wide" else "bf16"
+    if a.step_budget is None:
+        a.step_budget = 160 if a.workload == "dr_sweep" and a.mode == "train" else 0
     return a
 
 
@@ -414,6 +419,28 @@ def reference_schedule(env, dev, args, hp, rounds=3, warm_rounds=3, group=None):
            "note": "Exoskeleton_agent_train.py:110-211 on the device: warm-up 25,000 env-steps of uniform actions, "
                    "then select_action with Gaussian exploration; per round round(mean(ep_len)) = 283 "
                    "graph-replayed Agent.train steps and the policy-checkpoint rule (TD7_multi_agent.py:296-325)"}
+    # the script's per-step tremor statistics (:149-205) and per-round outputs
+    # (:213-317) on the device (RefScheduleTrainer(stats=True)): one round to
+    # capture the rollout graphs with them, then rounds timed as above
+    tr.stats = True
+    tr.run_round()
+    torch.cuda.synchronize()
+    t_burst = 0.0
+    t0 = time.perf_counter()
+    for _ in range(2):
+        tr.run_round()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if group is not None:
+        t = torch.tensor([dt, t_burst], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        dt, t_burst = float(t[0]), float(t[1])
+    st = {k: v for k, v in tr.round_stats[-1].items() if not k.endswith("_per_env")}
+    out["tremor_statistics"] = {
+        "rollout_ms_per_round_with": (dt - t_burst) / 2 * 1e3, "rollout_ms_per_round_without": t_roll / rounds * 1e3,
+        "last_round": st,
+        "note": "Exoskeleton_agent_train.py:149-205 per rollout step (exo_tremor_metrics + a row of the round's "
+                "device record, 2 launches) and :213-317 per round (one host sync), RefScheduleTrainer(stats=True)"}
     ag.maybe_train_and_checkpoint = orig
     del tr, ag
     return out
@@ -494,6 +521,8 @@ def main():
             hp.batch_size = args.batch
         agent = Agent(80, 7, 1, env_num=8, hp=hp, device=dev, precision=args.precision, n_envs=N,
                       process_group=dist.group.WORLD if dist_on else None, graph_safe=not args.eager)
+        if args.step_budget:
+            env.set_step_budget(args.step_budget)
         trainer = VecTrainer(env, agent, use_graphs=not args.eager)
     # configs[3] / [4]: the env step inside the timed window itself -- device
     # wall-clock reads on the step's stream either side of every step launch,
@@ -585,16 +614,17 @@ def main():
         tr = trainer
         evs, act_n = [], []
         for _ in range(n):
-            if tr.k == tr.round_len:
+            if tr.next_step_resets():
                 env.reset(obs_out=tr.obs)
                 tr._round_start()
             a = agent.select_action_batch(tr.obs, dec_count=tr.active_count)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            nobs, rew, done, _ = env.step(a, active=tr.active, out=tr._outs[tr._cur])
+            nobs, rew, done, _ = env.step(a, active=tr.active, out=tr._outs[tr._cur],
+                                          obs_cur=tr.obs if tr.budget else None)
             e1.record()
             evs.append((e0, e1))
-            act_n.append(int(tr.active_counts[tr.k]))
+            act_n.append(int(tr.active_count) if tr.budget else int(tr.active_counts[tr.k]))
             agent.replay_buffer.add_batch(tr.obs, a, nobs, rew, done, tr.strata, tr.active)
             tr._advance()
             tr.k += 1
@@ -608,14 +638,18 @@ def main():
         round boundary, then time exactly round_len iterations -- the first
         runs the episode reset -- bracketed by barrier + synchronize, max over
         ranks.  Returns (seconds, active env-steps of this rank)."""
-        while trainer.k != trainer.round_len:
+        while not trainer.next_step_resets():
             trainer.step()
         torch.cuda.synchronize()
         if dist_on:
             dist.barrier()
         torch.cuda.synchronize()
         t = time.perf_counter()
-        n = sum(trainer.step() for _ in range(trainer.round_len))
+        n = trainer.step()  # the episode reset and the round's first iteration
+        its = 1
+        while not trainer.next_step_resets():
+            n += trainer.step()
+            its += 1
         torch.cuda.synchronize()
         if dist_on:
             dist.barrier()
@@ -623,7 +657,9 @@ def main():
         dt = torch.tensor([time.perf_counter() - t], device=dev, dtype=torch.float64)
         if dist_on:
             dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-        return float(dt), n
+        if trainer.budget:  # every env finishes its episode within the round
+            n = int(active_per_k.sum())
+        return float(dt), n, its
 
     for _ in range(args.warmup):
         one_step(False)
@@ -632,6 +668,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     resets0 = trainer.resets if trainer is not None else state.get("resets", 0)
+    steps0 = trainer.env_steps_total() if trainer is not None and trainer.budget else None
     if clock is not None:
         clock.zero_()
         torch.cuda.synchronize()
@@ -645,6 +682,8 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     resets_in_window = (trainer.resets if trainer is not None else state.get("resets", 0)) - resets0
+    if steps0 is not None:  # step budget: the window's env-steps are counted on the device
+        env_steps = trainer.env_steps_total() - steps0
     window_clock = None
     if clock is not None:
         window_clock = env.step_clock_ms()
@@ -695,6 +734,10 @@ def main():
         t_iter, t_reset = float(t[2]), float(t[3])
     A_round = float(active_per_k.sum())
     round_value = world * A_round / (round_len * t_iter + t_reset)
+    if measured_round is not None and trainer.budget:
+        # a budgeted round lasts as many iterations as its stiffest env needs:
+        # the whole measured round is the value
+        round_value = world * measured_round[1] / measured_round[0]
     finite = None
     if agent is not None:
         finite = {n: bool(torch.isfinite(torch.cat([p.detach().reshape(-1) for p in m.parameters()])).all())
@@ -731,15 +774,19 @@ def main():
             "config": {"workload": WORKLOADS[args.workload]
                                    + (f", TD7 batch 8x{agent.hp.batch_size}" if agent else ", env only"),
                        "envs_per_gpu": N, "mode": args.mode, "physics": args.physics,
+                       "step_budget": args.step_budget,
                        "parallelism": f"env-shard x{world}"
                        + (" + TD7 DP all-reduce" if agent and dist_on else "")},
-            "value_formula": "whole episode rounds: world * A_round / (round_len * t_iter + t_reset); A_round = "
-                             f"{A_round:.0f} active env-steps per {round_len}-iteration round and rank, t_iter = "
-                             f"{t_iter * 1e3:.4f} ms (window time minus {resets_in_window} reset(s), per iteration), "
-                             f"t_reset = {t_reset * 1e3:.4f} ms (exo_reset_kernel, HIP events)",
+            "value_formula": ("whole episode rounds: world * A_round / (round_len * t_iter + t_reset); A_round = "
+                              f"{A_round:.0f} active env-steps per {round_len}-iteration round and rank, t_iter = "
+                              f"{t_iter * 1e3:.4f} ms (window time minus {resets_in_window} reset(s), per iteration), "
+                              f"t_reset = {t_reset * 1e3:.4f} ms (exo_reset_kernel, HIP events)")
+                             if not (trainer is not None and trainer.budget) else
+                             ("step budget: world * A_round / (one whole measured round incl. its reset); the round "
+                              f"lasts as many iterations as its stiffest env needs (measured_round.iterations)"),
             "window_value": total_env_steps / elapsed,
             "measured_round_value": (world * measured_round[1] / measured_round[0]) if measured_round else None,
-            "measured_round": ({"seconds": measured_round[0], "iterations": round_len,
+            "measured_round": ({"seconds": measured_round[0], "iterations": measured_round[2],
                                 "active_env_steps_per_rank": measured_round[1],
                                 "value_over_measured": round_value / (world * measured_round[1] / measured_round[0]),
                                 "note": "one whole episode round (reset + round_len graph-replayed iterations) "

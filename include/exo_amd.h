@@ -122,6 +122,31 @@ int exo_set_state_host(exo_ctx *ctx, int32_t env, const double *in);
 #define EXO_STEP_ROWS_SHARED 3
 int exo_set_step_variant(exo_ctx *ctx, int32_t variant);
 
+/* Budgeted step (no reference counterpart; BASELINE configs[3]'s stiff
+ * domain-randomised envs): with budget > 0 each launch of exo_step runs at most
+ * `budget` RK45 step attempts per ODE solve (Utilities/calculate_joint_angles.py:
+ * 5-22); a solve left unfinished keeps its exact solver state on the device and
+ * continues in the next launch, and its env starts no new step until both
+ * solves of its step are done (the step's observation, reward and done were
+ * already written when it started: they never depend on the solves).  Every
+ * env's trajectory is the unbudgeted one.  Row-parallel kernels only (ROWS /
+ * ROWS_SHARED / AUTO at N <= 16384), idealised physics only.  budget 0
+ * restores unbudgeted launches (refused while a solve is pending). */
+int exo_set_step_budget(exo_ctx *ctx, int32_t budget);
+/* exo_step with, in budget mode, the current observation buffer obs_cur_dev
+ * [N][80] (may be NULL): an env resuming a pending solve copies its row into
+ * obs_dev, so alternating observation buffers stay current. */
+int exo_step_carry(exo_ctx *ctx, const float *act_dev, float *obs_dev, float *rew_dev, uint8_t *done_dev,
+                   float *info_dev, const uint8_t *active_dev, const float *obs_cur_dev, void *stream);
+/* Budget mode's step mask on the device: active_dev[e] = the env will start a
+ * step in the next launch (episode not over, no pending solve), *count_dev
+ * (int32) their number, *remaining_dev (int32) the envs not finished (episode
+ * not over or a solve pending: 0 = the round is over), *steps_total_dev (int64,
+ * may be NULL) += the previous *count_dev (the envs the last launch stepped).
+ * One workgroup, graph-capturable. */
+int exo_budget_advance(exo_ctx *ctx, uint8_t *active_dev, int32_t *count_dev, int32_t *remaining_dev,
+                       int64_t *steps_total_dev, void *stream);
+
 /* Step clock (measurement; no reference counterpart): with clock_dev non-NULL
  * (3 device uint64), every later exo_step -- eager or captured into a graph --
  * brackets its launches with two one-lane kernels on its stream that read the
@@ -323,6 +348,15 @@ int lap_store_batch_ref_fused(const lap_tree_desc *t, const lap_storage_desc *st
 int lap_sample_gather(const lap_tree_desc *t, const lap_storage_desc *st, const float *u_dev, int32_t batch,
                       int32_t *idx_dev, float *out_state, float *out_action, float *out_next_state,
                       float *out_reward, float *out_not_done, void *stream);
+/* LAP.update_priority (:113-117) followed by the next LAP.sample (:65-111)
+ * as ONE launch: the priorities prio_dev of the draws idx_in_dev, then the
+ * next batch drawn and gathered exactly as lap_sample_gather_rng (same
+ * counter stream) into idx_dev / out_*.  batch <= 1024. */
+int lap_update_sample_rng(const lap_tree_desc *t, const lap_storage_desc *st, const int32_t *idx_in_dev,
+                          const float *prio_dev, int32_t batch, uint64_t seed, uint32_t tag,
+                          unsigned long long *counter_dev, uint32_t *ticket_dev, int32_t *idx_dev, float *out_state,
+                          float *out_action, float *out_next_state, float *out_reward, float *out_not_done,
+                          void *stream);
 /* lap_sample_gather with the uniforms drawn inside the kernel (Philox4x32-10,
  * key seed, counter words (draw index, call, tag)); *counter_dev (the call
  * number) advances by one per launch, ticket_dev: one uint32, zero at the first

@@ -260,6 +260,42 @@ def test_fused_ref_insert_equals_three_launch_insert(E, C, N):
         np.testing.assert_array_equal(tr[s, 1:cap], tr[s, 2:2 * cap:2] + tr[s, 3:2 * cap:2])
 
 
+@pytest.mark.parametrize("C,B,size", [(30_000, 128, 30_000), (30_000, 128, 17_001), (40, 16, 40), (250_000, 64, 99)])
+def test_update_and_sample_in_one_launch_equals_two(C, B, size):
+    """lap_update_sample_rng (r04): LAP.update_priority then the next sample in
+    ONE launch -- the descent reading the top levels the update left in LDS --
+    against update_priority() then sample(): every tree node, max_priority,
+    the sampled indices and gathered rows, and the RNG call counter, bit for
+    bit; non-integer priorities, duplicate update indices, sampling sizes below
+    the capacity (the prefix-total path), small and full-depth trees."""
+    E = 8
+    rng = np.random.default_rng(C + B)
+    a, b = _lap(E, C, B), _lap(E, C, B)
+    prio = rng.gamma(0.7, 2.0, (E, C)).astype(np.float32) + np.float32(1e-3)
+    for lap in (a, b):
+        _set_priorities(lap, prio)
+        for name in ("state", "action", "next_state", "reward", "not_done"):
+            t = getattr(lap, name)
+            t.copy_(torch.as_tensor(np.random.default_rng(5).normal(size=t.shape).astype(np.float32)))
+        lap.size_s.fill_(size)
+    b.fuse_update_sample = True
+    for it in range(4):
+        idx = rng.integers(0, size, (E, B)).astype(np.int32)
+        idx[:, 1::5] = idx[:, ::5][:, :idx[:, 1::5].shape[1]]  # duplicates: the last one wins
+        p = torch.as_tensor(rng.uniform(0.1, 9.0, E * B).astype(np.float32), device="cuda")
+        ind = torch.as_tensor(idx, device="cuda")
+        a.update_priority(p, ind)
+        ba = a.sample(it % 2)
+        bb = b.update_priority_and_sample(p, ind, it % 2)
+        torch.cuda.synchronize()
+        torch.testing.assert_close(b._tree, a._tree, rtol=0, atol=0)
+        assert float(a._maxp) == float(b._maxp)
+        assert torch.equal(a.ind, b.ind)
+        for x, y in zip(ba, bb):
+            torch.testing.assert_close(y, x, rtol=0, atol=0)
+        assert torch.equal(a._rng.state, b._rng.state)
+
+
 def test_wave_descent_and_subtree_rebuild_match_the_binary_tree():
     """r03d kernels (lap.hip rebuild_subtrees, prefix_total_wave, descend_wave)
     with NON-integer priorities at full depth (2^18 leaves): after batched

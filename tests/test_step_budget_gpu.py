@@ -1,0 +1,209 @@
+"""Budgeted env steps (exo_set_step_budget): at most B RK45
+step attempts per ODE solve and launch, an unfinished solve carried to the
+next launch with its exact solver state (t, h, the row values, the FSAL
+acceleration, the attempt count and the after-a-rejection flag), its env
+starting no new step meanwhile.
+
+The contract: every env's trajectory is the unbudgeted one.  Each env is
+driven by its own action sequence (acts[j, e] at ITS step j, whatever launch
+that falls in) and its observations, rewards, torques / reward components and
+final carried state must equal the unbudgeted run's bit for bit; at configs[3]'s
+16,384 domain-randomised envs, with one env forced stiff (its inertia-matrix
+noise drawn at the extremes), a sample is replayed on the oracle too."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import REPO, model_host, philox_draws
+
+pytestmark = pytest.mark.gpu
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+
+INFO_AT_STEP = np.r_[0:14, 21:28, 35:40]  # info written when the step starts (the amplitudes follow the solves)
+
+
+def _unbudgeted(env, acts):
+    K = acts.shape[0]
+    obs, rew, info = [], [], []
+    o = env.new_outputs(True)
+    for k in range(K):
+        ob, r, _, inf = env.step(torch.as_tensor(acts[k], device=env.device), out=o)
+        obs.append(ob.cpu().numpy().copy())
+        rew.append(r.cpu().numpy().copy())
+        info.append(inf.cpu().numpy()[:, INFO_AT_STEP].copy())
+    return np.stack(obs), np.stack(rew), np.stack(info)
+
+
+def _budgeted(env, obs0, acts, budget):
+    """Launch until every env took its K steps and no solve is pending; returns
+    the per-(step, env) records, the launch count and each env's longest run
+    of launches spent on one pending solve."""
+    K, N = acts.shape[:2]
+    dev = env.device
+    env.set_step_budget(budget)
+    active = torch.ones(N, dtype=torch.bool, device=dev)
+    count = torch.zeros(1, dtype=torch.int32, device=dev)
+    rem = torch.zeros(1, dtype=torch.int32, device=dev)
+    obs = np.zeros((K, N, 80), np.float32)
+    rew = np.zeros((K, N), np.float32)
+    info = np.zeros((K, N, INFO_AT_STEP.size), np.float32)
+    j = np.zeros(N, np.int64)
+    outs = [env.new_outputs(True), env.new_outputs(True)]
+    cur, par, launches = obs0, 0, 0
+    streak, best = np.zeros(N, np.int64), np.zeros(N, np.int64)
+    act_h = active.cpu().numpy()
+    ar = np.arange(N)
+    while True:
+        mask = act_h & (j < K)
+        a = acts[np.minimum(j, K - 1), ar]
+        ob, r, _, inf = env.step(torch.as_tensor(a, device=dev), active=torch.as_tensor(mask, device=dev),
+                                 out=outs[par], obs_cur=cur)
+        launches += 1
+        idx = np.flatnonzero(mask)
+        obh, rh, ih = ob.cpu().numpy(), r.cpu().numpy(), inf.cpu().numpy()
+        obs[j[idx], idx] = obh[idx]
+        rew[j[idx], idx] = rh[idx]
+        info[j[idx], idx] = ih[idx][:, INFO_AT_STEP]
+        j[idx] += 1
+        env.budget_advance(active, count, rem)
+        act_h = active.cpu().numpy().astype(bool)
+        assert int(count) == act_h.sum()
+        pending = ~act_h  # episodes are not over at K steps: inactive = a solve pending
+        streak = np.where(pending, streak + 1, 0)
+        best = np.maximum(best, streak)
+        cur, par = ob, par ^ 1
+        if (j == K).all() and act_h.all():
+            break
+        assert launches < 200 * K, "budgeted launches do not converge"
+    env.set_step_budget(0)
+    return obs, rew, info, launches, best
+
+
+def _pair(N, seed, variant, **kw):
+    from exo_amd import VecExoskeletonEnv
+    envs = []
+    for _ in range(2):
+        e = VecExoskeletonEnv(N, seed=seed, **kw)
+        e.set_step_variant(variant)
+        envs.append(e)
+    return envs
+
+
+@pytest.mark.parametrize("variant", ["rows", "rows_shared"])
+@pytest.mark.parametrize("budget", [1, 3])
+def test_budgeted_steps_equal_unbudgeted(variant, budget):
+    """1,030 envs (a partial last workgroup), default randomisation; a budget
+    of 1 or 3 attempts leaves almost every solve pending for several launches."""
+    N, K = 1030, 10
+    ea, eb = _pair(N, 31, variant)
+    oa, ob0 = ea.reset(), eb.reset()
+    torch.testing.assert_close(oa, ob0, rtol=0, atol=0)
+    acts = np.random.default_rng(budget).uniform(-1, 1, (K, N, 7)).astype(np.float32)
+    wo, wr, wi = _unbudgeted(ea, acts)
+    go, gr, gi, launches, best = _budgeted(eb, ob0, acts, budget)
+    np.testing.assert_array_equal(go, wo)
+    np.testing.assert_array_equal(gr, wr)
+    np.testing.assert_array_equal(gi, wi)
+    for e in (0, 1, 515, 1029):
+        np.testing.assert_array_equal(eb.get_state(e), ea.get_state(e))
+    assert launches > 2 * K and best.max() >= 2  # the carry was exercised
+
+
+def _stiff_draws(L, seed, env_id, lib):
+    """Episode draws of env `env_id` with its inertia-matrix noise at the
+    extremes of U(-f, f): diagonal entries shrunk, couplings grown."""
+    d = philox_draws(L, seed, env_id, 1, lib)
+    base = 17 + 8 * L
+    for r in range(7):
+        for c in range(7):
+            d[base + 7 * r + c] = 0.0 if r == c else 1.0 - 1e-12
+    return d
+
+
+def test_budgeted_domain_randomisation_sweep_with_a_stiff_env():
+    """configs[3]: 16,384 envs with per-env DR draws, budget 16; env 4101 is
+    forced stiff.  Budgeted == unbudgeted bit for bit over 6 steps of every
+    env, the stiff env spends the most launches on one solve, and sampled envs
+    (the stiff one included) match the oracle."""
+    import oracle as O
+    from exo_amd import motions
+    from test_env_gpu import _close_obs, env_kwargs_default
+    N, K, seed, stiff = 16384, 6, 2024, 4101
+    rng = np.random.default_rng(3)
+    mat_f = rng.uniform(0.05, 0.25, N)
+    mat_f[stiff] = 0.25
+    act_r = rng.uniform(0.0, 0.1, N)
+    shift_r = rng.uniform(0.0, 0.04, N)
+    kw = dict(matrix_noise_fraction=mat_f, dr_actuator_range=act_r, dr_actuator_end_pos_shift=shift_r,
+              tremor_amplitude_range=(0.1, 1.0))
+    ea, eb = _pair(N, seed, "rows_shared", **kw)
+    lib = model_host()
+    angles, lengths = motions.load()
+    Ls = int(lengths[stiff % 8])
+    sd = _stiff_draws(Ls, seed, stiff, lib)
+    obs0 = []
+    for env in (ea, eb):
+        o = env.reset()
+        env.reset_from_draws([stiff], [sd], obs_out=o)
+        obs0.append(o)
+    torch.testing.assert_close(obs0[0], obs0[1], rtol=0, atol=0)
+    acts = rng.uniform(-1, 1, (K, N, 7)).astype(np.float32)
+    wo, wr, wi = _unbudgeted(ea, acts)
+    go, gr, gi, launches, best = _budgeted(eb, obs0[1], acts, 16)
+    np.testing.assert_array_equal(go, wo)
+    np.testing.assert_array_equal(gr, wr)
+    np.testing.assert_array_equal(gi, wi)
+    for e in (0, 5, stiff, 9999, 16383):
+        np.testing.assert_array_equal(eb.get_state(e), ea.get_state(e))
+    print(f"budget 16: {launches} launches for {K} steps; longest pending run: stiff env {best[stiff]}, "
+          f"median env {int(np.median(best))}, max {best.max()} (env {int(best.argmax())})")
+    assert best[stiff] >= 3 and best[stiff] > np.median(best)
+    cfg = env_kwargs_default()
+    o0 = obs0[1].cpu().numpy()
+    for e in (0, 9999, stiff):
+        m = e % 8
+        L = int(lengths[m])
+        oe = O.OracleEnv(angles[m][:, :L], cfg["seq"], np.array([0.1, 1.0]), cfg["h1"], cfg["h2"], 40.0, 20.0,
+                         shift_r[e], act_r[e], mat_f[e])
+        oe.reset(philox_draws(L, seed, e, 0, lib))
+        ob = oe.reset(philox_draws(L, seed, e, 1, lib))
+        if e == stiff:
+            ob = oe.reset(sd)
+        _close_obs(o0[e], ob)
+        for k in range(K):
+            ob, r, dn, info, _ = oe.step(acts[k][e].astype(np.float64))
+            _close_obs(go[k, e], ob)
+            np.testing.assert_allclose(gr[k, e], r, rtol=2e-6, atol=1e-7)
+
+
+def test_trainer_with_a_step_budget_runs_whole_rounds():
+    """VecTrainer with env.set_step_budget: the step mask from the device, every
+    env completes its episode each round (the env-step counter = sum(L - 3) per
+    round), rounds end when no env is left unfinished, weights stay finite."""
+    from exo_amd import VecExoskeletonEnv
+    from exo_amd.rollout import VecTrainer
+    from exo_amd.td7 import Agent, Hyperparameters
+    torch.manual_seed(1)
+    N = 256
+    env = VecExoskeletonEnv(N, seed=8, matrix_noise_fraction=0.25)
+    env.set_step_budget(4)
+    ag = Agent(80, 7, 1, env_num=8, hp=Hyperparameters(batch_size=32), precision="bf16", n_envs=N, graph_safe=True,
+               buffer_size=8192)
+    tr = VecTrainer(env, ag)
+    A = int((env.lengths_host - 3).sum())
+    its = 0
+    while tr.resets < 1:
+        tr.step()
+        its += 1
+        assert its < 4000
+    torch.cuda.synchronize()
+    # the step that reset also ran the new round's first iteration (all N envs)
+    assert tr.env_steps_total() == A + N
+    assert its - 1 > tr.round_len  # budget 4 stretched the round
+    for _ in range(5):
+        tr.step()
+    for m in (ag.learner.actor, ag.learner.critic, ag.learner.encoder):
+        assert all(torch.isfinite(p).all() for p in m.parameters())

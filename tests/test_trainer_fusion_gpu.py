@@ -53,3 +53,21 @@ def test_optimiser_placement_does_not_change_training(mode, monkeypatch):
         t2.step()
     torch.cuda.synchronize()
     _assert_same(_params(a2), ref)
+
+
+def test_fused_priority_update_and_next_sample_does_not_change_training(monkeypatch):
+    """LAP.update_priority + the next iteration's sample as one launch
+    (lap_update_sample_rng, r04) against the two launches: the same weights
+    and replay trees after 12 graph-replayed iterations (a target refresh
+    included)."""
+    from exo_amd.replay import LAP
+    outs = []
+    for fused in (False, True):
+        monkeypatch.setattr(LAP, "fuse_update_sample", fused)
+        t, a = _make(seed=4)
+        for _ in range(12):
+            t.step()
+        torch.cuda.synchronize()
+        outs.append((_params(a), a.replay_buffer._tree.clone()))
+    _assert_same(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])

@@ -54,8 +54,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=60)
     ap.add_argument("--launches", type=int, default=40)
     ap.add_argument("--eager-launches", type=int, default=0)
+    ap.add_argument("--budget", type=int, default=0,
+                    help="exo_set_step_budget: a solve's attempts are then recorded in the launch that finishes it")
     a = ap.parse_args()
     env, ag, kw = make(a.workload)
+    if a.budget:
+        env.set_step_budget(a.budget)
     tr = VecTrainer(env, ag)
     for _ in range(a.warmup):
         tr.step()
@@ -116,7 +120,7 @@ def main():
     wm = np.concatenate(wave_max)
     hist, edges = np.histogram(both, bins=[1, 2, 3, 4, 5, 6, 8, 10, 15, 20, 30, 50, 100, 200, 500, 5000])
     out = {
-        "workload": a.workload, "envs": N, "launches": len(launch_max), "round_steps": ks,
+        "workload": a.workload, "envs": N, "launches": len(launch_max), "round_steps": ks, "step_budget": a.budget,
         "per_env_step_attempts": {"solves": "max of the actuated and the tremor-only solve",
                                   "mean": float(both.mean()), "median": float(np.median(both)),
                                   "p99": float(np.percentile(both, 99)), "p999": float(np.percentile(both, 99.9)),
