@@ -415,7 +415,10 @@ __host__ __device__ inline bool rk45_solve(const OdeM &M, const double *T, doubl
         }
     }
 #pragma unroll
-    for (int i = 0; i < 7; ++i) q_out[i] = ok ? q[i] : NAN;
+    // scipy's solve_ivp on failure (rk.py: step size below the spacing of t):
+    // status -1 and sol.y up to the last accepted step, whose q the reference
+    // takes (calculate_joint_angles.py:20); `ok` flags it (sticky error bit)
+    for (int i = 0; i < 7; ++i) q_out[i] = q[i];
     return ok;
 }
 

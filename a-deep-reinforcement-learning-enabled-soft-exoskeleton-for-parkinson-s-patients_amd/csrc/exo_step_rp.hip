@@ -305,7 +305,7 @@ __device__ __forceinline__ bool rk45_rows(const RM &M, double T, double &q_out, 
     RkState s;
     rk45_begin(M, T, s);
     const bool ok = rk45_advance(M, T, s, 0) > 0;
-    q_out = ok ? s.q : NAN;
+    q_out = s.q;  // on failure the last accepted q, as scipy's sol.y[:, -1] (exo_model.h rk45_solve)
     attempts = s.guard;
     return ok;
 }
@@ -462,7 +462,7 @@ __device__ void resume_env(const Dev &S, const Urdf &U, int e, int sub, int grp,
 #ifdef EXO_STAMPS
     if (g_exo_rksteps && r == 0) g_exo_rksteps[(size_t)grp * S.N + e] = st.guard;  // the solve's total attempts
 #endif
-    finish_solve(S, U, e, grp, r, ebase, S.counts[e] - 1, S.motion[e], res > 0 ? st.q : NAN, info);
+    finish_solve(S, U, e, grp, r, ebase, S.counts[e] - 1, S.motion[e], st.q, info);
 }
 
 // 16 envs (4 wavefronts) per workgroup: the state is SoA over envs, so one
@@ -693,7 +693,9 @@ __global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
     if (g_exo_rksteps && r == 0) g_exo_rksteps[(size_t)grp * N + e] = st.guard;
 #endif
     STAMP(4);
-    finish_solve(S, U, e, grp, r, ebase, c, motion, res > 0 ? st.q : NAN, info);
+    // a failed solve (step below the spacing of t, or the device's 4,096-attempt
+    // guard) continues from its last accepted q, as scipy's sol.y[:, -1]
+    finish_solve(S, U, e, grp, r, ebase, c, motion, st.q, info);
     STAMP(5);
 }
 

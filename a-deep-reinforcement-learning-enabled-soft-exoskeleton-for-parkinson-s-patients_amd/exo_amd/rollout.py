@@ -365,36 +365,22 @@ class VecTrainer:
     # the branch in every iteration, the r02 layout)
     prio_branch_all = os.environ.get("EXO_PRIO_BRANCH_ALL", "0") == "1"
 
-    def _mid(self, update_actor, flat_grad=None, grad_scale=1.0, rollout=True, inline=False):
-        """inline (data parallel, collectives inside the iteration): the global
-        max_priority (MAX all-reduce, SURVEY 8e / TD7_buffer_multi_agent.py:116)
-        right after the priority update, on a branch joined at the end of the
-        iteration -- nothing before the next iteration's inserts reads it."""
+    def _mid(self, update_actor, flat_grad=None, grad_scale=1.0, rollout=True):
         ag = self.agent
         self._pside = None
         self._mid_rollout = rollout
-        cur = torch.cuda.current_stream(self.device)
-
-        def prio_stream():
+        if self.prio_branch and not self.dp and (update_actor or self.prio_branch_all):
+            cur = torch.cuda.current_stream(self.device)
             if getattr(self, "_prio_stream", None) is None:
                 self._prio_stream = torch.cuda.Stream(device=self.device)
-            return self._prio_stream
-        if self.prio_branch and (not self.dp or inline) and (update_actor or self.prio_branch_all):
-            self._pside = prio_stream()
+            self._pside = self._prio_stream
             self._pside.wait_stream(cur)
             with torch.cuda.stream(self._pside):
                 self._update_and_sample_next()
-                if inline:
-                    ag.sync.max_(ag.replay_buffer._maxp)
             ag.learner.phase_steps(flat_grad, grad_scale)
         else:
             ag.learner.phase_steps(flat_grad, grad_scale)
             self._update_and_sample_next()
-            if inline:
-                self._pside = prio_stream()
-                self._pside.wait_stream(cur)
-                with torch.cuda.stream(self._pside):
-                    ag.sync.max_(ag.replay_buffer._maxp)
         if update_actor:
             ag.learner.phase_actor_grads(self._batch[0], self._batch[1])
 
@@ -431,13 +417,30 @@ class VecTrainer:
         of max_priority after the priority update, the actor bucket's before
         the actor's step.  All ranks capture the collectives in this one
         order, each on the process group's stream."""
-        ag, L = self.agent, self.agent.learner
+        ag, L, S = self.agent, self.agent.learner, self.agent.sync
         L.dp_inline = True
         try:
             self._pre(rollout)
+            self._mid_rollout = rollout
+            # the priority update and the next sample on a branch beside the
+            # critic bucket's all-reduce and step; its MAX of max_priority is
+            # captured after the critic bucket's all-reduce (one collective
+            # stream: capture order is execution order on every rank)
+            cur = torch.cuda.current_stream(self.device)
+            if getattr(self, "_prio_stream", None) is None:
+                self._prio_stream = torch.cuda.Stream(device=self.device)
+            self._pside = self._prio_stream
+            self._pside.wait_stream(cur)
+            with torch.cuda.stream(self._pside):
+                self._update_and_sample_next()
             flat_c = L.allreduce_phase_grads(self._batch[0].shape[0])
-            self._mid(update_actor, flat_c, 1.0, rollout, inline=True)
-            flat_a = L.allreduce_actor_grads() if update_actor else None
+            with torch.cuda.stream(self._pside):
+                S.max_(ag.replay_buffer._maxp)
+            L.phase_steps(flat_c, 1.0)
+            flat_a = None
+            if update_actor:
+                L.phase_actor_grads(self._batch[0], self._batch[1])
+                flat_a = L.allreduce_actor_grads()
             self._post(update_actor, flat_a, 1.0)
             self._join_prio()
         finally:

@@ -453,11 +453,20 @@ class GradSync:
         s = torch.cuda.Stream(device=device)
         s.wait_stream(cur)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.stream(s):
-            with torch.cuda.graph(g, stream=s):
-                self.avg_(x)
-                dist.all_reduce(y, op=dist.ReduceOp.MAX, group=self.group)
+        captured = True
+        try:
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s):
+                    self.avg_(x)
+                    dist.all_reduce(y, op=dist.ReduceOp.MAX, group=self.group)
+        except Exception:
+            captured = False
         cur.wait_stream(s)
+        # a replay runs the collectives: only if EVERY rank captured them
+        flag = torch.tensor([1.0 if captured else 0.0], device=device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+        if float(flag) != 1.0:
+            return False
         ok = True
         for k in range(replays):
             x.fill_(float(self.rank + 1 + k))

@@ -139,7 +139,11 @@ int oracle_solve_diff_eq(const double *I, const double *D, const double *K, cons
         if (h_abs < min_step) h_abs = min_step;
         int rejected = 0;
         for (;;) {
-            if (h_abs < min_step) return -1;
+            if (h_abs < min_step) { /* scipy: status -1, sol.y up to the last accepted step */
+                for (int i = 0; i < 7; ++i) q_out[i] = y[i];
+                if (nfev) *nfev = s.nfev;
+                return 1;
+            }
             double h = h_abs, t_new = t + h;
             if (t_new - t_bound > 0) t_new = t_bound;
             h = t_new - t;
@@ -485,8 +489,9 @@ int oracle_env_step(oracle_env *e, const double *a, float *obs, double *reward, 
     double tr[7], T[7];
     for (int j = 0; j < 7; ++j) { tr[j] = e->tremor[j * L + c]; T[j] = tr[j] + at[j]; }
     double qa[7], qt[7];
-    if (oracle_solve_diff_eq(e->I, e->D, e->S, T, qa, NULL)) return -2;
-    if (oracle_solve_diff_eq(e->I, e->D, e->S, tr, qt, NULL)) return -2;
+    /* a failed solve (> 0) continues from its last accepted q, as solve_ivp */
+    if (oracle_solve_diff_eq(e->I, e->D, e->S, T, qa, NULL) < 0) return -2;
+    if (oracle_solve_diff_eq(e->I, e->D, e->S, tr, qt, NULL) < 0) return -2;
     const double r2d = 180 / M_PI, d2r = M_PI / 180;
     for (int j = 0; j < 7; ++j) { qa[j] *= r2d; qt[j] *= r2d; }
     /* :421-431; imu columns: 0 elbow_y, 1 elbow_z, 2 shoulder_x, 3 shoulder_y, 4 shoulder_z */

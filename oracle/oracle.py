@@ -71,8 +71,11 @@ def solve_diff_eq(I, D, K, T):
     n = ctypes.c_int(0)
     args = [np.ascontiguousarray(x, dtype=np.float64) for x in (I, D, K, T)]
     rc = lib().oracle_solve_diff_eq(*[_p(a) for a in args], _p(q), ctypes.byref(n))
-    if rc != 0:
-        raise RuntimeError("RK45 step size too small")
+    if rc < 0:
+        raise RuntimeError("RK45 solve failed")
+    # rc 1: scipy's "required step size is less than spacing between numbers" --
+    # solve_ivp returns status -1 with sol.y up to the last accepted step, whose
+    # q the reference uses (calculate_joint_angles.py:20): q is that
     return q, n.value
 
 

@@ -77,7 +77,8 @@ def _budgeted(env, obs0, acts, budget):
         cur, par = ob, par ^ 1
         if (j == K).all() and act_h.all():
             break
-        assert launches < 200 * K, "budgeted launches do not converge"
+        # a solve takes at most 4,096 attempts (the device guard): budget-sized slices of them
+        assert launches < K * (4096 // budget + 2) + 50, "budgeted launches do not converge"
     env.set_step_budget(0)
     return obs, rew, info, launches, best
 
@@ -188,8 +189,8 @@ def test_trainer_with_a_step_budget_runs_whole_rounds():
     from exo_amd.td7 import Agent, Hyperparameters
     torch.manual_seed(1)
     N = 256
-    env = VecExoskeletonEnv(N, seed=8, matrix_noise_fraction=0.25)
-    env.set_step_budget(4)
+    env = VecExoskeletonEnv(N, seed=8)
+    env.set_step_budget(3)
     ag = Agent(80, 7, 1, env_num=8, hp=Hyperparameters(batch_size=32), precision="bf16", n_envs=N, graph_safe=True,
                buffer_size=8192)
     tr = VecTrainer(env, ag)
@@ -198,11 +199,11 @@ def test_trainer_with_a_step_budget_runs_whole_rounds():
     while tr.resets < 1:
         tr.step()
         its += 1
-        assert its < 4000
+        assert its < 20 * tr.round_len
     torch.cuda.synchronize()
     # the step that reset also ran the new round's first iteration (all N envs)
     assert tr.env_steps_total() == A + N
-    assert its - 1 > tr.round_len  # budget 4 stretched the round
+    assert its - 1 > tr.round_len  # budget 3 stretched the round
     for _ in range(5):
         tr.step()
     for m in (ag.learner.actor, ag.learner.critic, ag.learner.encoder):
