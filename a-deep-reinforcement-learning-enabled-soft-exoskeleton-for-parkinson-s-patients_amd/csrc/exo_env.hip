@@ -905,6 +905,36 @@ __global__ __launch_bounds__(1024) void budget_advance_kernel(const int32_t *cou
         *remaining = tr;
     }
 }
+
+// Auto-reset episodes (VecTrainer episodes="async"): an env whose episode is
+// over (its done step was taken: counts >= L - 1) is reset right away (mask
+// for exo_reset_kernel; a solve still carried for that final step is dropped
+// by the reset) and steps again in the next launch; every other env steps
+// unless a budgeted solve is pending.  count = the envs of the next launch,
+// steps_total += the envs the last launch stepped.
+__global__ __launch_bounds__(1024) void episode_advance_kernel(const int32_t *counts, const int32_t *L,
+                                                               const uint8_t *pend, int n, uint8_t *active,
+                                                               int32_t *count, uint8_t *reset,
+                                                               long long *steps_total) {
+    __shared__ int wsum[16];
+    int a = 0;
+    for (int e = threadIdx.x; e < n; e += blockDim.x) {
+        const bool fin = counts[e] >= L[e] - 1, p = pend && pend[e] != 0;
+        reset[e] = fin;
+        const bool run = fin || !p;
+        active[e] = run;
+        a += run;
+    }
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = a;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int ta = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) ta += wsum[w];
+        if (steps_total) *steps_total += *count;
+        *count = ta;
+    }
+}
 } // namespace
 
 int exo_set_step_budget(exo_ctx *c, int32_t budget) {
@@ -942,6 +972,22 @@ int exo_budget_advance(exo_ctx *c, uint8_t *active_dev, int32_t *count_dev, int3
     hipLaunchKernelGGL(budget_advance_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, c->S.counts, c->S.L,
                        c->S.pend, c->N, active_dev, count_dev, remaining_dev, (long long *)steps_total_dev);
     return check(c, hipGetLastError(), "exo_budget_advance");
+}
+
+int exo_episode_advance(exo_ctx *c, uint8_t *active_dev, int32_t *count_dev, uint8_t *reset_mask_dev,
+                        int64_t *steps_total_dev, float *obs_dev, void *stream) {
+    if (!c || !active_dev || !count_dev || !reset_mask_dev || !obs_dev) return EXO_EINVAL;
+    DeviceGuard g(c->device);
+    const hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(episode_advance_kernel, dim3(1), dim3(1024), 0, s, c->S.counts, c->S.L, c->S.pend, c->N,
+                       active_dev, count_dev, reset_mask_dev, (long long *)steps_total_dev);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(exo_reset_kernel, dim3(c->N), dim3(64), 0, s, c->S, c->U, reset_mask_dev,
+                           (const int32_t *)nullptr, (const double *)nullptr, 0, c->seed, obs_dev);
+        e = hipGetLastError();
+    }
+    return check(c, e, "exo_episode_advance");
 }
 
 int exo_step_carry(exo_ctx *c, const float *act_dev, float *obs_dev, float *rew_dev, uint8_t *done_dev,

@@ -117,6 +117,63 @@ __device__ void propagate_span(float *T, int cap, int levels, int capacity, int 
     __syncthreads();
 }
 
+// propagate_span for a span that does not wrap and holds at most SPAN_LDS - 2
+// leaves, every level in LDS: the span's nodes of one level are a contiguous
+// range [lo, hi] whose children are [lo & ~1, hi | 1] of the level below --
+// the span's own recomputed nodes plus at most one unchanged sibling at each
+// end.  The siblings of every level are outside the span, so nothing in this
+// launch writes them: all of them are loaded up front (one round trip), the
+// span's leaves once, and then each level is one barrier of LDS work whose
+// results also go to the tree (stores nothing waits for).  The same operands
+// in the same order as propagate_span: bit-identical.  Returns false (nothing
+// done) when the span does not qualify.
+constexpr int SPAN_LDS = 4096;
+constexpr int SPAN_LEVELS = 32;
+__device__ bool propagate_span_lds(float *T, int cap, int levels, int capacity, int first, int count,
+                                   float *buf /* 2 SPAN_LDS */, float *edge /* 2 SPAN_LEVELS */) {
+    const int a = cap + first, e = cap + first + count - 1;  // leaf nodes [a, e]
+    if (count <= 0 || first + count > capacity || count > SPAN_LDS - 2 || levels >= SPAN_LEVELS) return false;
+    // edge[2 lv], edge[2 lv + 1]: the unchanged left / right sibling at level lv
+    // (the children of level lv + 1's range), when that range needs one
+    const int t = threadIdx.x;
+    if (t < 2 * levels) {
+        const int lv = t >> 1, right = t & 1;
+        const int lo = a >> lv, hi = e >> lv;
+        if (!right && (lo & 1)) edge[t] = T[lo - 1];
+        if (right && !(hi & 1)) edge[t] = T[hi + 1];
+    }
+    float *A = buf, *B = buf + SPAN_LDS;
+    // level 0: A[c - (a & ~1)] for c in [a & ~1, e | 1]
+    {
+        const int base = a & ~1;
+        for (int c = a + t; c <= e; c += blockDim.x) A[c - base] = T[c];
+    }
+    __syncthreads();
+    if (t == 0) {
+        if (a & 1) A[0] = edge[0];
+        if (!(e & 1)) A[(e | 1) - (a & ~1)] = edge[1];
+    }
+    for (int lv = 1; lv <= levels; ++lv) {
+        __syncthreads();
+        const int lo = a >> lv, hi = e >> lv, cbase = (a >> (lv - 1)) & ~1, nbase = lo & ~1;
+        for (int node = lo + t; node <= hi; node += blockDim.x) {
+            const int c = 2 * node - cbase;
+            const float v = A[c] + A[c + 1];
+            T[node] = v;
+            B[node - nbase] = v;
+        }
+        if (t == 0 && lv < levels) {
+            if (lo & 1) B[0] = edge[2 * lv];
+            if (!(hi & 1)) B[(hi | 1) - nbase] = edge[2 * lv + 1];
+        }
+        float *tmp = A;
+        A = B;
+        B = tmp;
+    }
+    __syncthreads();
+    return true;
+}
+
 // LAP.add: new items get max_priority (:56-57).  The items of this block's
 // stratum are gathered in chunks of ADD_CHUNK into LDS, their leaves written,
 // then their ancestors recomputed.
@@ -546,6 +603,9 @@ __global__ __launch_bounds__(UPD_THREADS) void lap_store_ref_fused_kernel(
     __shared__ int32_t rk[STORE_CHUNK], ri[STORE_CHUNK], sl[STORE_CHUNK];
     __shared__ int carry_r, carry_i, carry_J, carry_slot;  // the chunk's last row of stratum s, decided later
     float *T = stratum_tree(tree, s, cap);
+    // K > 1: part 0 writes the leaves and propagates, parts 1..K-1 copy the rows
+    // (copy part of stratum-row j: 1 + j mod (K - 1)); K == 1: part 0 does both
+    const int KC = K > 1 ? K - 1 : 1, cpart = K > 1 ? part - 1 : 0;
     const long long ptr0 = ref[0], count0 = ref[1], size0 = ref[2];
     const long long m0 = mult_below(count0, E);
     const float p = *maxp;
@@ -615,7 +675,7 @@ __global__ __launch_bounds__(UPD_THREADS) void lap_store_ref_fused_kernel(
             }
         }
         __syncthreads();
-        if (carry_slot >= 0 && wv == 0 && carry_J % K == part)
+        if (carry_slot >= 0 && wv == 0 && carry_J % KC == cpart)
             copy_rows<VEC>(st, state, action, next_state, reward, done, action_scale, &carry_i, &carry_slot, s,
                            capacity, 0, 1, 1, lane, 64);
         __syncthreads();  // the loop below sets the next carry: wave 0 must be done reading this one
@@ -635,10 +695,12 @@ __global__ __launch_bounds__(UPD_THREADS) void lap_store_ref_fused_kernel(
             if (win && part == 0) T[cap + slot] = p;
         }
         __syncthreads();
-        // this part's share of the chunk's winners: stratum-row index = part (mod K)
-        const int j0 = ((part - soff) % K + K) % K;
-        copy_rows<VEC>(st, state, action, next_state, reward, done, action_scale, ri, sl, s, capacity, j0, K, m, t,
-                       UPD_THREADS);
+        // this part's share of the chunk's winners: stratum-row index = cpart (mod KC)
+        if (cpart >= 0) {
+            const int j0 = ((cpart - soff) % KC + KC) % KC;
+            copy_rows<VEC>(st, state, action, next_state, reward, done, action_scale, ri, sl, s, capacity, j0, KC, m,
+                           t, UPD_THREADS);
+        }
         offset += chunk_tot;
         soff += m;
         __syncthreads();
@@ -652,18 +714,20 @@ __global__ __launch_bounds__(UPD_THREADS) void lap_store_ref_fused_kernel(
         }
     }
     __syncthreads();
-    if (carry_slot >= 0 && wv == 0 && carry_J % K == part)
+    if (carry_slot >= 0 && wv == 0 && carry_J % KC == cpart)
         copy_rows<VEC>(st, state, action, next_state, reward, done, action_scale, &carry_i, &carry_slot, s, capacity,
                        0, 1, 1, lane, 64);
     const int n_act = offset;
     if (part == 0 && n_act > 0) {
+        __shared__ float span_buf[2 * SPAN_LDS], span_edge[2 * SPAN_LEVELS];
         __syncthreads();
         const long long last = mult_below(count0 + n_act - 1, E) - m0;  // slots ptr0 .. ptr0 + last
-        propagate_span(T, cap, levels, capacity, (int)ptr0, (int)min(last + 1, (long long)capacity));
+        const int cnt = (int)min(last + 1, (long long)capacity);
+        if (!propagate_span_lds(T, cap, levels, capacity, (int)ptr0, cnt, span_buf, span_edge))
+            propagate_span(T, cap, levels, capacity, (int)ptr0, cnt);
     }
     __syncthreads();
-    if (t == 0) {
-        __threadfence();
+    if (t == 0) {  // ref was read (and used) before this add: no fence needed
         if (atomicAdd(ticket, 1u) == (uint32_t)(E * K - 1)) {  // every workgroup has read ref
             const long long adv = mult_below(count0 + n_act, E) - m0;
             const long long size = min(size0 + adv, (long long)capacity);
@@ -859,21 +923,64 @@ __global__ __launch_bounds__(UPD_THREADS) void lap_update_sample_kernel(float *t
         if (b < UPD_THREADS) pick[b] = i;
     }
     __syncthreads();
-    // gather: (draw, item) over the workgroup, items = state, next_state, action, reward, not_done
-    const int sd = st.state_dim, ad = st.action_dim, per = 2 * sd + ad + 2;
-    for (int it = threadIdx.x; it < min(batch, UPD_THREADS) * per; it += UPD_THREADS) {
-        const int b = it / per, c = it - b * per;
-        const long d = (long)s * batch + b;
-        const long row = (long)s * (capacity + 1) + pick[b];
-        if (c < sd) o_state[d * sd + c] = st.state[row * sd + c];
-        else if (c < 2 * sd) o_next[d * sd + c - sd] = st.next_state[row * sd + c - sd];
-        else if (c < 2 * sd + ad) o_action[d * ad + c - 2 * sd] = st.action[row * ad + c - 2 * sd];
-        else if (c == 2 * sd + ad) o_reward[d] = st.reward[row];
-        else o_not_done[d] = st.not_done[row];
+    // gather: (draw, item) over the workgroup, items = state, next_state (float4
+    // where the rows are 16-byte aligned), action, reward, not_done; GU items
+    // per thread loaded before any is stored (the stores may alias the loads as
+    // far as the compiler knows: item by item, every load would wait for the
+    // previous store -- r04 first cut, 54 us per launch)
+    const int sd = st.state_dim, ad = st.action_dim;
+    const bool v4 = (sd & 3) == 0 && ((reinterpret_cast<uintptr_t>(st.state) | reinterpret_cast<uintptr_t>(st.next_state) |
+                                       reinterpret_cast<uintptr_t>(o_state) | reinterpret_cast<uintptr_t>(o_next)) & 15) == 0;
+    const int sv = v4 ? sd / 4 : sd, per = 2 * sv + ad + 2;
+    const int items = min(batch, UPD_THREADS) * per;
+    constexpr int GU = 8;
+    for (int it0 = threadIdx.x; it0 < items; it0 += GU * UPD_THREADS) {
+        float4 v[GU];
+        float *dst[GU];
+        bool wide[GU];
+#pragma unroll
+        for (int u = 0; u < GU; ++u) {
+            const int it = it0 + u * UPD_THREADS;
+            dst[u] = nullptr;
+            wide[u] = false;
+            if (it >= items) continue;
+            const int b = it / per, c = it - b * per;
+            const long d = (long)s * batch + b;
+            const long row = (long)s * (capacity + 1) + pick[b];
+            if (c < 2 * sv) {
+                const bool nx = c >= sv;
+                const int e = nx ? c - sv : c;
+                const float *src = (nx ? st.next_state : st.state) + row * sd;
+                float *o = (nx ? o_next : o_state) + d * sd;
+                if (v4) {
+                    v[u] = ld4(src + 4 * e);
+                    dst[u] = o + 4 * e;
+                    wide[u] = true;
+                } else {
+                    v[u].x = src[e];
+                    dst[u] = o + e;
+                }
+            } else if (c < 2 * sv + ad) {
+                const int e = c - 2 * sv;
+                v[u].x = st.action[row * ad + e];
+                dst[u] = o_action + d * ad + e;
+            } else if (c == 2 * sv + ad) {
+                v[u].x = st.reward[row];
+                dst[u] = o_reward + d;
+            } else {
+                v[u].x = st.not_done[row];
+                dst[u] = o_not_done + d;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < GU; ++u) {
+            if (!dst[u]) continue;
+            if (wide[u]) st4(dst[u], v[u]);
+            else *dst[u] = v[u].x;
+        }
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
+    if (threadIdx.x == 0) {  // `call` was read (and used) before this add: no fence needed
         if (atomicAdd(rng.ticket, 1u) == gridDim.x - 1) {
             *rng.counter = call + 1ull;
             *rng.ticket = 0u;
@@ -1004,7 +1111,8 @@ int lap_store_batch_ref_fused(const lap_tree_desc *t, const lap_storage_desc *st
         return EXO_EINVAL;
     if (n == 0) return EXO_OK;
     const int E = t->n_strata;
-    const int K = std::max(1, std::min(16, (n + E * 256 - 1) / (E * 256)));
+    // part 0 of a stratum: leaves + ancestors; parts 1..K-1: ~64 rows of the copy each
+    const int K = 1 + std::max(1, std::min(15, (n + E * 64 - 1) / (E * 64)));
     auto al16 = [](const void *p) { return ((uintptr_t)p & 15u) == 0; };
     const bool vec = st->state_dim % 4 == 0 && al16(state) && al16(next_state) && al16(st->state) &&
                      al16(st->next_state);

@@ -115,6 +115,7 @@ EXPORTS = {
     "exo_set_step_budget": (c_int32, [c_void_p, c_int32]),
     "exo_step_carry": (c_int32, [c_void_p] * 9),
     "exo_budget_advance": (c_int32, [c_void_p] * 6),
+    "exo_episode_advance": (c_int32, [c_void_p] * 7),
     "exo_multibody_default_params": (None, [P(ExoMbParams)]),
     "exo_set_physics": (c_int32, [c_void_p, c_int32, P(ExoMbParams)]),
     "exo_multibody_advance": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -391,8 +391,12 @@ class FusedTrain:
         ajobs = [self._job(xb, act_p[2 * i].grad, act_p[2 * i + 1].grad, rt) for i, xb in enumerate(self.xt_actor)]
         self.jobs_a = (nat.TD7FWgJob * len(ajobs))(*ajobs)
         self.ptrs_y_enc = (P * 4)(*[t.data_ptr() for t in self.y_enc])
-        # the encoder pass with zs(s') on its own workgroup row (r04; EXO_ENC_SPLIT=0: one row)
-        self.enc_split = os.environ.get("EXO_ENC_SPLIT", "1") != "0"
+        # the encoder pass with zs(s') on its own workgroup row (r04, EXO_ENC_SPLIT=1).
+        # Off by default: alone the split pass is shorter, but inside the training
+        # iteration its extra 64 workgroups take CUs from the concurrent target /
+        # fixed passes on the critical chain (0.320 vs 0.299 ms per iteration,
+        # profiles/r04b_raw/bench_ab_*.log)
+        self.enc_split = os.environ.get("EXO_ENC_SPLIT", "0") == "1"
         self.enc_nz = torch.zeros((rt * 16, Z), **f32)
         self.enc_flag = torch.zeros((rt,), dtype=torch.int32, device=dev)
 

@@ -175,7 +175,7 @@ class ForkJoinAudit:
 
 class VecTrainer:
     def __init__(self, env, agent, strata=None, use_graphs=True, warmup_eager=3, exploration="gaussian",
-                 shared_step=True):
+                 shared_step=True, episodes=None):
         self.env, self.agent = env, agent
         self.device = env.device
         self.n = env.n
@@ -243,6 +243,24 @@ class VecTrainer:
                 raise ValueError("Pink exploration indexes its noise by the round's step: not with a step budget")
             self._remaining = torch.zeros((1,), dtype=torch.int32, device=self.device)
             self._steps_total = torch.zeros((1,), dtype=torch.int64, device=self.device)
+        # episodes: "sync" -- the script's synchronous rounds (every env resets
+        # when the longest motion ends, envs that finished early idle until
+        # then) -- or "async" -- each env resets in place as soon as its own
+        # episode ends (exo_episode_advance inside the iteration, no host work
+        # between rounds), so every launch steps every env that has no
+        # pending budgeted solve.  EXO_EPISODES picks the default.
+        if episodes is None:
+            episodes = os.environ.get("EXO_EPISODES", "sync")
+        if episodes not in ("sync", "async"):
+            raise ValueError(f"episodes must be 'sync' or 'async', not {episodes!r}")
+        self.episodes = episodes
+        if episodes == "async":
+            if exploration == "pink":
+                raise ValueError("Pink exploration indexes its noise by the round's step: not with async episodes")
+            self.active.fill_(True)
+            self.active_count.fill_(self.n)
+            if not self.budget:
+                self._steps_total = torch.zeros((1,), dtype=torch.int64, device=self.device)
         if exploration == "pink":
             agent.init_episode_noise_device(self.round_len)
         if use_graphs and os.environ.get("EXO_GRAPH_CHECK", "1") != "0":
@@ -264,7 +282,12 @@ class VecTrainer:
         """The next step's active mask and count on the device (exo_active_advance);
         with rew / score: score += rew where the replaced mask is set, in the same
         launch (exo_active_advance_score).  Step budget: the mask from the
-        envs' own progress (exo_budget_advance)."""
+        envs' own progress (exo_budget_advance).  Async episodes: finished
+        envs reset in place, into the observation buffer the step wrote
+        (exo_episode_advance)."""
+        if self.episodes == "async":
+            self.env.episode_advance(self.active, self.active_count, self._outs[self._cur][0], self._steps_total)
+            return
         if self.budget:
             self.env.budget_advance(self.active, self.active_count, self._remaining, self._steps_total)
             return
@@ -529,17 +552,20 @@ class VecTrainer:
         """Whether the next step() starts a new episode round: after round_len
         iterations, and with a step budget once no env is left unfinished (a
         host read of the device count)."""
-        if self.k < self.round_len:
+        if self.episodes == "async" or self.k < self.round_len:
             return False
         return not self.budget or int(self._remaining.item()) == 0
 
     def env_steps_total(self):
-        """Step budget: the env-steps taken so far (device counter, host sync)."""
+        """Step budget / async episodes: the env-steps taken so far (device
+        counter, host sync; the last launch's envs are added by the next
+        advance)."""
         return int(self._steps_total.item())
 
     def step(self):
         """One training iteration; returns the number of active env-steps (with
-        a step budget 0: the count stays on the device, env_steps_total())."""
+        a step budget: 0, the count stays on the device, env_steps_total();
+        async episodes without a budget: every env, N)."""
         ag = self.agent
         L = ag.learner
         if self.next_step_resets():
@@ -560,7 +586,12 @@ class VecTrainer:
         if L.maybe_update_targets():
             ag.replay_buffer.reset_max_priority()
             ag.sync.max_(ag.replay_buffer._maxp)
-        n_active = 0 if self.budget else int(self.active_counts[self.k])
+        if self.budget:
+            n_active = 0
+        elif self.episodes == "async":
+            n_active = self.n
+        else:
+            n_active = int(self.active_counts[self.k])
         self.k += 1
         self.iters += 1
         self._cur ^= 1  # the next observation is in the other buffer
@@ -603,7 +634,7 @@ class RefScheduleTrainer(VecTrainer):
         if getattr(env, "step_budget", 0):
             raise ValueError("RefScheduleTrainer steps the script's synchronous episodes: no step budget")
         super().__init__(env, agent, strata=strata, use_graphs=use_graphs, warmup_eager=warmup_eager,
-                         shared_step=False)
+                         shared_step=False, episodes="sync")
         # the rollout runs alone (no TD7 pass beside it): the env step's own fast shape
         if getattr(env, "step_variant", None) == "rows_shared":
             env.set_step_variant("auto")

@@ -169,6 +169,19 @@ class VecExoskeletonEnv:
                                                nat.ptr(steps_total), self._stream()), "exo_budget_advance",
                   self._ctx)
 
+    def episode_advance(self, active, count, obs_out, steps_total=None):
+        """Auto-reset (exo_episode_advance): envs whose episode is over are
+        reset in place, their observations written into obs_out (the buffer
+        the last step wrote); active (bool [N]) = the envs of the next launch
+        (all but those with a pending budgeted solve), count (int32 [1]) their
+        number, steps_total (int64 [1]) += the envs the last launch stepped."""
+        if getattr(self, "_reset_ws", None) is None:
+            self._reset_ws = torch.zeros((self.n,), dtype=torch.uint8, device=self.device)
+        self._check_out(obs_out, (self.n, OBS_DIM), torch.float32)
+        nat.check(nat.lib().exo_episode_advance(self._ctx, nat.ptr(active), nat.ptr(count), nat.ptr(self._reset_ws),
+                                                nat.ptr(steps_total), nat.ptr(obs_out), self._stream()),
+                  "exo_episode_advance", self._ctx)
+
     def new_outputs(self, with_info=True):
         d = self.device
         return (torch.empty((self.n, OBS_DIM), dtype=torch.float32, device=d),

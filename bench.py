@@ -132,6 +132,9 @@ def parse():
     ap.add_argument("--precision", choices=["bf16", "fp16", "fp32"], default=None,
                     help="TD7 MFMA operands (workload default: bf16 per configs[1], fp16 for wide)")
     ap.add_argument("--batch", type=int, default=None, help="TD7 rows per stratum (default 128)")
+    ap.add_argument("--episodes", choices=["sync", "async"], default=None,
+                    help="VecTrainer episodes: sync = the script's synchronous rounds, async = each env resets in "
+                         "place when its episode ends (exo_episode_advance); default: EXO_EPISODES or sync")
     ap.add_argument("--step-budget", type=int, default=None,
                     help="RK45 attempts per solve and env-step launch (exo_set_step_budget; default: 0 = no limit, "
                          "dr_sweep 160)")
@@ -523,7 +526,8 @@ def main():
                       process_group=dist.group.WORLD if dist_on else None, graph_safe=not args.eager)
         if args.step_budget:
             env.set_step_budget(args.step_budget)
-        trainer = VecTrainer(env, agent, use_graphs=not args.eager)
+        trainer = VecTrainer(env, agent, use_graphs=not args.eager, episodes=args.episodes)
+        args.episodes = trainer.episodes
     # configs[3] / [4]: the env step inside the timed window itself -- device
     # wall-clock reads on the step's stream either side of every step launch,
     # captured into the trainer's graphs with it (exo_set_step_clock)
@@ -624,7 +628,7 @@ def main():
                                           obs_cur=tr.obs if tr.budget else None)
             e1.record()
             evs.append((e0, e1))
-            act_n.append(int(tr.active_count) if tr.budget else int(tr.active_counts[tr.k]))
+            act_n.append(int(tr.active_count) if (tr.budget or tr.episodes == "async") else int(tr.active_counts[tr.k]))
             agent.replay_buffer.add_batch(tr.obs, a, nobs, rew, done, tr.strata, tr.active)
             tr._advance()
             tr.k += 1
@@ -669,6 +673,7 @@ def main():
     torch.cuda.synchronize()
     resets0 = trainer.resets if trainer is not None else state.get("resets", 0)
     steps0 = trainer.env_steps_total() if trainer is not None and trainer.budget else None
+    async_eps = trainer is not None and trainer.episodes == "async"
     if clock is not None:
         clock.zero_()
         torch.cuda.synchronize()
@@ -688,7 +693,9 @@ def main():
     if clock is not None:
         window_clock = env.step_clock_ms()
         env.set_step_clock(False)
-    measured_round = measured_round_timing() if trainer is not None else None
+    # async episodes: no rounds (every env resets in place inside the timed
+    # iterations), the window itself is the whole-job rate
+    measured_round = measured_round_timing() if trainer is not None and not async_eps else None
     reset_ms = reset_timing()
     loop_kern_ms = None
     if ev:  # env mode: the timed launches themselves
@@ -734,7 +741,9 @@ def main():
         t_iter, t_reset = float(t[2]), float(t[3])
     A_round = float(active_per_k.sum())
     round_value = world * A_round / (round_len * t_iter + t_reset)
-    if measured_round is not None and trainer.budget:
+    if async_eps:
+        round_value = total_env_steps / elapsed
+    elif measured_round is not None and trainer.budget:
         # a budgeted round lasts as many iterations as its stiffest env needs:
         # the whole measured round is the value
         round_value = world * measured_round[1] / measured_round[0]
@@ -775,9 +784,13 @@ def main():
                                    + (f", TD7 batch 8x{agent.hp.batch_size}" if agent else ", env only"),
                        "envs_per_gpu": N, "mode": args.mode, "physics": args.physics,
                        "step_budget": args.step_budget,
+                       **({"episodes": args.episodes} if trainer is not None else {}),
                        "parallelism": f"env-shard x{world}"
                        + (" + TD7 DP all-reduce" if agent and dist_on else "")},
-            "value_formula": ("whole episode rounds: world * A_round / (round_len * t_iter + t_reset); A_round = "
+            "value_formula": ("async episodes: the timed window's env-steps (every launch steps every env without a "
+                              "pending budgeted solve; episodes end and reset in place inside the window) / window "
+                              "time, summed over ranks (max of the ranks' times)") if async_eps else
+                             ("whole episode rounds: world * A_round / (round_len * t_iter + t_reset); A_round = "
                               f"{A_round:.0f} active env-steps per {round_len}-iteration round and rank, t_iter = "
                               f"{t_iter * 1e3:.4f} ms (window time minus {resets_in_window} reset(s), per iteration), "
                               f"t_reset = {t_reset * 1e3:.4f} ms (exo_reset_kernel, HIP events)")

@@ -113,29 +113,18 @@ def test_budgeted_steps_equal_unbudgeted(variant, budget):
     assert launches > 2 * K and best.max() >= 2  # the carry was exercised
 
 
-def _stiff_draws(L, seed, env_id, lib):
-    """Episode draws of env `env_id` with its inertia-matrix noise at the
-    extremes of U(-f, f): diagonal entries shrunk, couplings grown."""
-    d = philox_draws(L, seed, env_id, 1, lib)
-    base = 17 + 8 * L
-    for r in range(7):
-        for c in range(7):
-            d[base + 7 * r + c] = 0.0 if r == c else 1.0 - 1e-12
-    return d
-
-
 def test_budgeted_domain_randomisation_sweep_with_a_stiff_env():
-    """configs[3]: 16,384 envs with per-env DR draws, budget 16; env 4101 is
-    forced stiff.  Budgeted == unbudgeted bit for bit over 6 steps of every
-    env, the stiff env spends the most launches on one solve, and sampled envs
-    (the stiff one included) match the oracle."""
+    """configs[3]: 16,384 envs with per-env DR draws (seed 2024: a few of them
+    stiff, one at the device's 4,096-attempt guard), budget 16.  Budgeted ==
+    unbudgeted bit for bit over 6 steps of every env; the stiffest env below
+    the guard spends several launches on one solve and matches the oracle, as
+    do two ordinary envs."""
     import oracle as O
     from exo_amd import motions
     from test_env_gpu import _close_obs, env_kwargs_default
-    N, K, seed, stiff = 16384, 6, 2024, 4101
+    N, K, seed, budget = 16384, 6, 2024, 16
     rng = np.random.default_rng(3)
     mat_f = rng.uniform(0.05, 0.25, N)
-    mat_f[stiff] = 0.25
     act_r = rng.uniform(0.0, 0.1, N)
     shift_r = rng.uniform(0.0, 0.04, N)
     kw = dict(matrix_noise_fraction=mat_f, dr_actuator_range=act_r, dr_actuator_end_pos_shift=shift_r,
@@ -143,23 +132,20 @@ def test_budgeted_domain_randomisation_sweep_with_a_stiff_env():
     ea, eb = _pair(N, seed, "rows_shared", **kw)
     lib = model_host()
     angles, lengths = motions.load()
-    Ls = int(lengths[stiff % 8])
-    sd = _stiff_draws(Ls, seed, stiff, lib)
-    obs0 = []
-    for env in (ea, eb):
-        o = env.reset()
-        env.reset_from_draws([stiff], [sd], obs_out=o)
-        obs0.append(o)
+    obs0 = [env.reset() for env in (ea, eb)]
     torch.testing.assert_close(obs0[0], obs0[1], rtol=0, atol=0)
     acts = rng.uniform(-1, 1, (K, N, 7)).astype(np.float32)
     wo, wr, wi = _unbudgeted(ea, acts)
-    go, gr, gi, launches, best = _budgeted(eb, obs0[1], acts, 16)
+    go, gr, gi, launches, best = _budgeted(eb, obs0[1], acts, budget)
     np.testing.assert_array_equal(go, wo)
     np.testing.assert_array_equal(gr, wr)
     np.testing.assert_array_equal(gi, wi)
-    for e in (0, 5, stiff, 9999, 16383):
+    # the stiffest env whose solves stay under the guard (the oracle has none:
+    # scipy's solver would go on past 4,096 attempts)
+    stiff = int(np.argmax(np.where(best < 4096 // budget - 1, best, -1)))
+    for e in (0, 5, stiff, int(best.argmax()), 9999, 16383):
         np.testing.assert_array_equal(eb.get_state(e), ea.get_state(e))
-    print(f"budget 16: {launches} launches for {K} steps; longest pending run: stiff env {best[stiff]}, "
+    print(f"budget {budget}: {launches} launches for {K} steps; longest pending run: env {stiff} {best[stiff]}, "
           f"median env {int(np.median(best))}, max {best.max()} (env {int(best.argmax())})")
     assert best[stiff] >= 3 and best[stiff] > np.median(best)
     cfg = env_kwargs_default()
@@ -171,8 +157,6 @@ def test_budgeted_domain_randomisation_sweep_with_a_stiff_env():
                          shift_r[e], act_r[e], mat_f[e])
         oe.reset(philox_draws(L, seed, e, 0, lib))
         ob = oe.reset(philox_draws(L, seed, e, 1, lib))
-        if e == stiff:
-            ob = oe.reset(sd)
         _close_obs(o0[e], ob)
         for k in range(K):
             ob, r, dn, info, _ = oe.step(acts[k][e].astype(np.float64))
