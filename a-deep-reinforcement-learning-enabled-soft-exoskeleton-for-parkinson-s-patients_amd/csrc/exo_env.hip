@@ -84,20 +84,17 @@ __device__ void invert(double *a /* n*n, destroyed */, double *inv) {
 //   17+8L: I noise (49), D noise (49), S noise (49), 164+8L: shift (42),
 //   206+8L: shoulder force scale, elbow force scale.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void exo_reset_kernel(Dev S, Urdf U, const uint8_t *mask, const int32_t *ids,
-                                                       const double *draws, int draw_stride, uint64_t seed,
-                                                       float *obs) {
+// One env's reset by one wavefront (block of 64); draws: its injected stream or
+// nullptr (Philox).
+__device__ void reset_one(const Dev &S, const Urdf &U, int e, const double *draws, uint64_t seed, float *obs) {
     // numpy evaluates every expression of the reset without fused multiply-add;
     // keep the rounding identical (bit-exact D, S, shift and force scales).
 #pragma clang fp contract(off)
-    const int e = ids ? ids[blockIdx.x] : (int)blockIdx.x;
-    if (e >= S.N) return;
-    if (!ids && mask && !mask[e]) return;
     const int lane = threadIdx.x;
     if (S.pend && lane == 0) S.pend[e] = 0;  // a solve still carried by a budgeted step is dropped
     const int N = S.N, L = S.L[e], seq = S.seq[e];
     const uint32_t ep = S.episode[e];
-    const Draws D{draws ? draws + (size_t)blockIdx.x * draw_stride : nullptr, seed, (uint32_t)e, ep};
+    const Draws D{draws, seed, (uint32_t)e, ep};
 
     __shared__ double sI[49], sD[49], sS[49], sShift[42], sTrem[3][4], sInv[NINV];
 
@@ -223,7 +220,7 @@ __global__ __launch_bounds__(64) void exo_reset_kernel(Dev S, Urdf U, const uint
 #pragma unroll
     for (int j = 0; j < 6; ++j) refc[j] = S.ref[(size_t)j * N + e];
     link_coms(U, q, act, ref);
-    float *o = obs + (size_t)e * OBS;
+    float *o = obs ? obs + (size_t)e * OBS : nullptr;
     float ob[OBS];
 #pragma unroll
     for (int i = 0; i < 14; ++i) ob[i] = 0.0f; // ep_state_values forces are zero at c-2, c-1
@@ -254,6 +251,26 @@ __global__ __launch_bounds__(64) void exo_reset_kernel(Dev S, Urdf U, const uint
 #pragma unroll
         for (int i = 0; i < OBS; i += 4) *reinterpret_cast<float4 *>(o + i) = make_float4(ob[i], ob[i + 1], ob[i + 2], ob[i + 3]);
     }
+}
+
+// reset (Exoskeleton_env.py:473-478 -> initialize_movement, :193-254): one
+// wavefront per env -- every env, the envs of a mask, or listed envs with
+// their injected draw streams
+__global__ __launch_bounds__(64) void exo_reset_kernel(Dev S, Urdf U, const uint8_t *mask, const int32_t *ids,
+                                                       const double *draws, int draw_stride, uint64_t seed,
+                                                       float *obs) {
+    const int e = ids ? ids[blockIdx.x] : (int)blockIdx.x;
+    if (e >= S.N) return;
+    if (!ids && mask && !mask[e]) return;
+    reset_one(S, U, e, draws ? draws + (size_t)blockIdx.x * draw_stride : nullptr, seed, obs);
+}
+
+// the envs listed in ids[0 .. *n_ids) (exo_episode_advance's compacted list):
+// a small fixed grid, each wavefront taking every gridDim.x-th listed env
+__global__ __launch_bounds__(64) void exo_reset_list_kernel(Dev S, Urdf U, const int32_t *ids,
+                                                            const int32_t *n_ids, uint64_t seed, float *obs) {
+    const int n = *n_ids;
+    for (int k = blockIdx.x; k < n; k += gridDim.x) reset_one(S, U, ids[k], nullptr, seed, obs);
 }
 
 // ---------------------------------------------------------------------------
@@ -907,21 +924,25 @@ __global__ __launch_bounds__(1024) void budget_advance_kernel(const int32_t *cou
 }
 
 // Auto-reset episodes (VecTrainer episodes="async"): an env whose episode is
-// over (its done step was taken: counts >= L - 1) is reset right away (mask
-// for exo_reset_kernel; a solve still carried for that final step is dropped
-// by the reset) and steps again in the next launch; every other env steps
-// unless a budgeted solve is pending.  count = the envs of the next launch,
-// steps_total += the envs the last launch stepped.
+// over (its done step was taken: counts >= L - 1) is reset (mask for
+// exo_reset_kernel) once that step's solve is complete -- the final step's
+// motor update sets joint state the reset keeps, so a budgeted final solve
+// still pending finishes in later launches first -- and steps again in the
+// next launch; every env without a pending solve steps.  count = the envs of
+// the next launch, steps_total += the envs the last launch stepped.
 __global__ __launch_bounds__(1024) void episode_advance_kernel(const int32_t *counts, const int32_t *L,
                                                                const uint8_t *pend, int n, uint8_t *active,
-                                                               int32_t *count, uint8_t *reset,
+                                                               int32_t *count, int32_t *reset_ids,
                                                                long long *steps_total) {
     __shared__ int wsum[16];
+    __shared__ int nres;
+    if (threadIdx.x == 0) nres = 0;
+    __syncthreads();
     int a = 0;
     for (int e = threadIdx.x; e < n; e += blockDim.x) {
         const bool fin = counts[e] >= L[e] - 1, p = pend && pend[e] != 0;
-        reset[e] = fin;
-        const bool run = fin || !p;
+        if (fin && !p) reset_ids[atomicAdd(&nres, 1)] = e;  // list order is immaterial: resets are per env
+        const bool run = !p;
         active[e] = run;
         a += run;
     }
@@ -933,6 +954,7 @@ __global__ __launch_bounds__(1024) void episode_advance_kernel(const int32_t *co
         for (int w = 0; w < (int)(blockDim.x >> 6); ++w) ta += wsum[w];
         if (steps_total) *steps_total += *count;
         *count = ta;
+        reset_ids[n] = nres;
     }
 }
 } // namespace
@@ -974,17 +996,17 @@ int exo_budget_advance(exo_ctx *c, uint8_t *active_dev, int32_t *count_dev, int3
     return check(c, hipGetLastError(), "exo_budget_advance");
 }
 
-int exo_episode_advance(exo_ctx *c, uint8_t *active_dev, int32_t *count_dev, uint8_t *reset_mask_dev,
+int exo_episode_advance(exo_ctx *c, uint8_t *active_dev, int32_t *count_dev, int32_t *reset_ws_dev,
                         int64_t *steps_total_dev, float *obs_dev, void *stream) {
-    if (!c || !active_dev || !count_dev || !reset_mask_dev || !obs_dev) return EXO_EINVAL;
+    if (!c || !active_dev || !count_dev || !reset_ws_dev || !obs_dev) return EXO_EINVAL;
     DeviceGuard g(c->device);
     const hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(episode_advance_kernel, dim3(1), dim3(1024), 0, s, c->S.counts, c->S.L, c->S.pend, c->N,
-                       active_dev, count_dev, reset_mask_dev, (long long *)steps_total_dev);
+                       active_dev, count_dev, reset_ws_dev, (long long *)steps_total_dev);
     hipError_t e = hipGetLastError();
-    if (e == hipSuccess) {
-        hipLaunchKernelGGL(exo_reset_kernel, dim3(c->N), dim3(64), 0, s, c->S, c->U, reset_mask_dev,
-                           (const int32_t *)nullptr, (const double *)nullptr, 0, c->seed, obs_dev);
+    if (e == hipSuccess) {  // a few envs end per launch (N / episode length): 64 wavefronts cover them
+        hipLaunchKernelGGL(exo_reset_list_kernel, dim3(std::min(c->N, 64)), dim3(64), 0, s, c->S, c->U, reset_ws_dev,
+                           reset_ws_dev + c->N, c->seed, obs_dev);
         e = hipGetLastError();
     }
     return check(c, e, "exo_episode_advance");

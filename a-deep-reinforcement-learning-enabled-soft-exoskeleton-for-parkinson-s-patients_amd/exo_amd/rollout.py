@@ -558,8 +558,7 @@ class VecTrainer:
 
     def env_steps_total(self):
         """Step budget / async episodes: the env-steps taken so far (device
-        counter, host sync; the last launch's envs are added by the next
-        advance)."""
+        counter, host sync)."""
         return int(self._steps_total.item())
 
     def step(self):

@@ -176,7 +176,7 @@ class VecExoskeletonEnv:
         (all but those with a pending budgeted solve), count (int32 [1]) their
         number, steps_total (int64 [1]) += the envs the last launch stepped."""
         if getattr(self, "_reset_ws", None) is None:
-            self._reset_ws = torch.zeros((self.n,), dtype=torch.uint8, device=self.device)
+            self._reset_ws = torch.zeros((self.n + 1,), dtype=torch.int32, device=self.device)
         self._check_out(obs_out, (self.n, OBS_DIM), torch.float32)
         nat.check(nat.lib().exo_episode_advance(self._ctx, nat.ptr(active), nat.ptr(count), nat.ptr(self._reset_ws),
                                                 nat.ptr(steps_total), nat.ptr(obs_out), self._stream()),

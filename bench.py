@@ -146,6 +146,8 @@ def parse():
                     help="env-only launches timed with HIP events for the roofline line")
     ap.add_argument("--no-td7-variants", action="store_true",
                     help="skip the fp32-TD7 and 256-wide-alias sub-lines (configs[1] train mode)")
+    ap.add_argument("--no-sync-rounds", action="store_true",
+                    help="skip the synchronous-round comparison of the async-episode loop (configs[1])")
     ap.add_argument("--no-reference-schedule", action="store_true",
                     help="skip the reference-schedule sub-line (RefScheduleTrainer, train mode)")
     a = ap.parse_args()
@@ -154,7 +156,13 @@ def parse():
     if a.precision is None:
         a.precision = "fp16" if a.workload == "wide" else "bf16"
     if a.step_budget is None:
-        a.step_budget = 160 if a.workload == "dr_sweep" and a.mode == "train" else 0
+        # configs[3]: 96 attempts per launch (profiles/r04d_raw: 25.3 M env-steps/s with async
+        # episodes at 96, 21.5 M at 160, 10.5 M unbudgeted)
+        a.step_budget = 96 if a.workload == "dr_sweep" and a.mode == "train" else 0
+    if a.episodes is None:
+        # the vectorised trainer's own episodes: every env resets in place when its
+        # episode ends (EXO_EPISODES=sync: the script's synchronous rounds)
+        a.episodes = os.environ.get("EXO_EPISODES", "async")
     return a
 
 
@@ -357,6 +365,51 @@ def fused_critic_timing(agent, reps=20, replays=10):
 # (Σ(L-3) = 2,257 active env-steps) it trains round(mean(ep_len)) = 283 steps
 # (Simulation/Exoskeleton_agent_train.py:115,145,208 -> TD7_multi_agent.py:315-325)
 REFERENCE_ENV_STEPS_PER_UPDATE = 2257 / 283
+
+
+def sync_rounds(env, dev, args, hp, group=None, warm=40):
+    """The same training loop with the script's synchronous episode rounds
+    (VecTrainer episodes="sync": every env resets when the longest motion ends,
+    envs whose motion ended idle until then), for comparison with the default
+    async episodes: fresh agent on the bench's envs, `warm` untimed iterations,
+    then one whole round (its reset included) timed end to end, barrier +
+    synchronize on both sides, max over ranks; active env-steps summed."""
+    from exo_amd.rollout import VecTrainer
+    from exo_amd.td7 import Agent
+    rank = dist.get_rank(group) if group is not None else 0
+    torch.manual_seed(5 + rank)
+    ag = Agent(80, 7, 1, env_num=8, hp=hp, device=dev, precision=args.precision, n_envs=env.n, graph_safe=True,
+               process_group=group)
+    tr = VecTrainer(env, ag, episodes="sync")
+    for _ in range(warm):
+        tr.step()
+    while not tr.next_step_resets():
+        tr.step()
+
+    def sync_all():
+        torch.cuda.synchronize()
+        if group is not None:
+            dist.barrier(group)
+        torch.cuda.synchronize()
+
+    sync_all()
+    t = time.perf_counter()
+    n, its = tr.step(), 1
+    while not tr.next_step_resets():
+        n += tr.step()
+        its += 1
+    sync_all()
+    v = torch.tensor([time.perf_counter() - t, float(n)], device=dev, dtype=torch.float64)
+    if group is not None:
+        dt = v[:1].clone()
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX, group=group)
+        dist.all_reduce(v, op=dist.ReduceOp.SUM, group=group)
+        v[0] = dt[0]
+    sec, total = float(v[0]), float(v[1])
+    return {"value": total / sec, "seconds": sec, "iterations": its, "ms_per_iteration": sec / its * 1e3,
+            "active_env_steps": total,
+            "note": "VecTrainer(episodes='sync'): one whole round incl. its reset, timed end to end after "
+                    f"{warm} warm-up iterations; envs whose motion ended idle until the round's longest ends"}
 
 
 def reference_schedule(env, dev, args, hp, rounds=3, warm_rounds=3, group=None):
@@ -757,6 +810,10 @@ def main():
     if agent is not None and args.mode == "train" and not args.no_reference_schedule:
         # every rank (collectives inside); rank 0 reports
         ref_sched = reference_schedule(env, dev, args, agent.hp, group=dist.group.WORLD if dist_on else None)
+    sync_cmp = None
+    if (agent is not None and args.mode == "train" and async_eps and args.workload == "configs1"
+            and not args.no_sync_rounds):
+        sync_cmp = sync_rounds(env, dev, args, agent.hp, group=dist.group.WORLD if dist_on else None)
     if agent is not None and dist_on:
         # data-parallel replicas must hold bit-identical weights
         ck = torch.stack([torch.cat([p.detach().reshape(-1) for p in m.parameters()]).double().sum()
@@ -861,7 +918,7 @@ def main():
         if agent is not None:
             gs = args.steps / elapsed  # data-parallel ranks share one update: a grad step is per iteration
             res["grad_steps_per_sec"] = gs
-            per_update = A_round / round_len
+            per_update = (total_env_steps / world / args.steps) if async_eps else A_round / round_len
             ref_ratio = REFERENCE_ENV_STEPS_PER_UPDATE
             res["update_to_data"] = {
                 "env_steps_per_grad_step": world * per_update,
@@ -914,6 +971,8 @@ def main():
             res["dp_layout"] = dp_layout(trainer)
         if ref_sched is not None:
             res["reference_schedule"] = ref_sched
+        if sync_cmp is not None:
+            res["sync_rounds"] = sync_cmp
         if finite is not None:
             res["weights_finite"] = all(finite.values()) or finite
         if dp_sync is not None:

@@ -148,16 +148,17 @@ int exo_budget_advance(exo_ctx *ctx, uint8_t *active_dev, int32_t *count_dev, in
                        int64_t *steps_total_dev, void *stream);
 
 /* Auto-reset episodes (the vectorised trainer's asynchronous mode): after a
- * step launch, every env whose episode is over (its done step was taken) is
- * reset in place -- exo_reset for those envs, its observation written into
- * obs_dev (the buffer the step just wrote) -- and the mask of the next launch
- * is written: every env, except (step budget) one whose solve is pending.
+ * step launch, every env whose episode is over (its done step was taken and,
+ * with a step budget, that step's solve is complete) is reset in place --
+ * exo_reset for those envs, its observation written into obs_dev (the buffer
+ * the step just wrote) -- and the mask of the next launch is written: every
+ * env, except (step budget) one whose solve is pending.
  * count_dev = that mask's population, steps_total_dev (int64, optional) += the
- * previous *count_dev (the envs the last launch stepped).  reset_mask_dev:
- * uint8 [N] workspace (the envs reset).  Replaces the training script's
- * per-round reset (Simulation/Exoskeleton_agent_train.py:111-113) with a
- * per-env one, as a vectorised env's auto-reset. */
-int exo_episode_advance(exo_ctx *c, uint8_t *active_dev, int32_t *count_dev, uint8_t *reset_mask_dev,
+ * previous *count_dev (the envs the last launch stepped).  reset_ws_dev:
+ * int32 [N + 1] workspace (the envs reset, their number at [N]).  Replaces the
+ * training script's per-round reset (Simulation/Exoskeleton_agent_train.py:
+ * 111-113) with a per-env one, as a vectorised env's auto-reset. */
+int exo_episode_advance(exo_ctx *c, uint8_t *active_dev, int32_t *count_dev, int32_t *reset_ws_dev,
                         int64_t *steps_total_dev, float *obs_dev, void *stream);
 
 /* Step clock (measurement; no reference counterpart): with clock_dev non-NULL
