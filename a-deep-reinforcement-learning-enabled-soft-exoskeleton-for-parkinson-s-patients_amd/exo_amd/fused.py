@@ -270,15 +270,16 @@ class FusedNets:
         return buf
 
     @torch.no_grad()
-    def target_heads(self, next_state, noise=None):
+    def target_heads(self, next_state, noise=None, out=None):
         """Both heads of critic_target(s', a'(s'), zsa', zs') [B, 2] with a' the
         noisy target action (:233-241); two launches.  noise: given standard
-        normals [B, A] (parity tests) instead of the device stream."""
+        normals [B, A] (parity tests) instead of the device stream.  out: a
+        [B, 2] fp32 buffer to write (else a new tensor)."""
         L = self.L
         self.refresh("fixed_encoder_target", "actor_target", "critic_target")
         ns = next_state.contiguous()
         B = ns.shape[0]
-        qt = torch.empty((B, 2), dtype=torch.float32, device=ns.device)
+        qt = out if out is not None else torch.empty((B, 2), dtype=torch.float32, device=ns.device)
         z = noise.to(device=ns.device, dtype=torch.float32).contiguous() if noise is not None else None
         nz = self._noise(L._noise_rng, L.target_policy_noise, L.policy_noise_decrease, L.hp.noise_clip, 1.0, z)
         nat.check(nat.lib().td7f_target(self.prec, self.act, self.nets["fixed_encoder_target"].array,
@@ -288,14 +289,18 @@ class FusedNets:
         return qt
 
     @torch.no_grad()
-    def fixed(self, state, action):
-        """(fixed_encoder.zs(state), fixed_encoder.zsa(zs, action)), one launch (:248-249)."""
+    def fixed(self, state, action, out=None):
+        """(fixed_encoder.zs(state), fixed_encoder.zsa(zs, action)), one launch
+        (:248-249); out: a (zs, zsa) pair of [B, Z] fp32 buffers to write."""
         self.refresh("fixed_encoder")
         s, a = state.contiguous(), action.contiguous()
         B = s.shape[0]
         Z = self.L.hp.zs_dim
-        zs = torch.empty((B, Z), dtype=torch.float32, device=s.device)
-        zsa = torch.empty((B, Z), dtype=torch.float32, device=s.device)
+        if out is not None:
+            zs, zsa = out
+        else:
+            zs = torch.empty((B, Z), dtype=torch.float32, device=s.device)
+            zsa = torch.empty((B, Z), dtype=torch.float32, device=s.device)
         nat.check(nat.lib().td7f_fixed(self.prec, self.act, self.nets["fixed_encoder"].array, nat.ptr(s), nat.ptr(a),
                                        B, nat.ptr(zs), nat.ptr(zsa), nat.stream_ptr(s.device)), "td7f_fixed")
         return zs, zsa

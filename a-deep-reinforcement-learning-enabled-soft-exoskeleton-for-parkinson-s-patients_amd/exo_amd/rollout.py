@@ -341,6 +341,23 @@ class VecTrainer:
     def _prefetching(self):
         return self.prefetch_sample and self.overlap_rollout
 
+    # r04: with the next batch sampled at the end of an iteration, its fixed
+    # embeddings and target heads are computed right after it (beside the
+    # actor update of an actor iteration) into one of two persistent slots
+    # (TD7Learner.prefetch_targets); the next iteration's critic pass starts
+    # at once.  Not before a target refresh (the refresh changes those nets),
+    # not in the data-parallel three-graph layout.  EXO_TARGET_PREFETCH=0: off.
+    prefetch_targets = os.environ.get("EXO_TARGET_PREFETCH", "1") == "1"
+    _pre_in = _pre_out = False
+
+    def _target_prefetch_flags(self):
+        L = self.agent.learner
+        ok = (self.prefetch_targets and self._prefetching() and L.fused is not None and self.iters > 0
+              and (not self.dp or self.dp_inline))
+        pre_in = ok and L.prefetch_ready(self._cur)
+        pre_out = ok and L.training_steps % L.hp.target_update_rate != 0
+        return pre_in, pre_out
+
     def _pre(self, rollout=True):
         ag = self.agent
         # one GPU: the encoder's gradients and step stay on its branch, joined
@@ -361,6 +378,8 @@ class VecTrainer:
             return
         if self._prefetching():
             self._batch, self._ind = rb._slot(slot)  # sampled by the previous iteration
+            if self._pre_in:
+                ag.learner.pre_in = slot  # and its critic inputs computed there too
         else:
             self._batch = rb.sample()
             self._ind = rb.ind
@@ -415,6 +434,9 @@ class VecTrainer:
         rb = self.agent.replay_buffer
         if self._prefetching() and self._mid_rollout:
             rb.update_priority_and_sample(self._prio, self._ind, 1 - self._cur)
+            if self._pre_out:
+                b = rb._slot(1 - self._cur)[0]
+                self.agent.learner.prefetch_targets(b[0], b[1], b[2], 1 - self._cur)
         else:
             rb.update_priority(self._prio, self._ind)
 
@@ -484,7 +506,7 @@ class VecTrainer:
         self._join_prio()
 
     def _key(self, update_actor, rollout):
-        return (update_actor, self._cur) if rollout else ("train", update_actor)
+        return (update_actor, self._cur, self._pre_in, self._pre_out) if rollout else ("train", update_actor)
 
     def _capture(self, update_actor, rollout=True):
         """Capture this parity's iteration (rollout=False: a training step
@@ -576,12 +598,22 @@ class VecTrainer:
         L.training_steps += 1
         update_actor = L.training_steps % ag.hp.policy_freq == 0
         L.prefetch_actor = update_actor  # phase_grads may start the actor forward early
+        self._pre_in, self._pre_out = self._target_prefetch_flags()
         if not self.use_graphs or self.iters < self.warmup_eager:
             self._eager(update_actor)
-        elif (update_actor, self._cur) not in self.graphs:
+        elif self._key(update_actor, True) not in self.graphs:
             self._capture(update_actor)
         else:
             self._replay(update_actor)
+        # the prefetch slots' state after this iteration (a replay runs no host code)
+        if self._pre_in or self._pre_out:
+            if not isinstance(L._pre_ready, list):
+                L._pre_ready = [False, False]
+            if self._pre_in:
+                L._pre_ready[self._cur] = False
+            if self._pre_out:
+                L._pre_ready[1 - self._cur] = True
+        L.pre_in = None
         if L.maybe_update_targets():
             ag.replay_buffer.reset_max_priority()
             ag.sync.max_(ag.replay_buffer._maxp)
@@ -853,6 +885,8 @@ class RefScheduleTrainer(VecTrainer):
         L.training_steps += 1
         update_actor = L.training_steps % ag.hp.policy_freq == 0
         L.prefetch_actor = update_actor
+        self._pre_in = self._pre_out = False
+        L.drop_prefetch()
         # both policy-update parities run eagerly once before their capture
         if not self.use_graphs or self._train_iters < max(2, self.warmup_eager):
             self._eager(update_actor, rollout=False)

@@ -824,7 +824,31 @@ class TD7Learner:
         wg_adam = enc_step and WGRAD_ADAM and tr.fuses_adam() and not self.sync.active
         self._enc_step_pending = False
         self._actor_fused_pre = False
-        if branch and TARGET_ON_MAIN:
+        pre = self.pre_in
+        self.pre_in = None
+        if pre is not None:
+            # the fixed embeddings and the target heads of this batch were
+            # computed at the end of the previous iteration (prefetch_targets)
+            if not self._pre_ready[pre]:
+                raise RuntimeError("phase_grads: no prefetched targets in slot %d" % pre)
+            self._pre_ready[pre] = False
+            zs, zsa, qt = self._pre_bufs[pre]
+            if branch:
+                side = stream("_side")
+                with torch.cuda.stream(side):
+                    tr.encoder(state, action, next_state)
+                    if enc_step:
+                        tr.wgrad_encoder(adam=wg_adam)
+                        if inline:
+                            self.sync.avg_(tr.enc_grad)
+                if self.prefetch_actor and self.actor_branch:
+                    aside = stream("_aside")
+                    with torch.cuda.stream(aside):
+                        tr.actor(0, state, zs)
+                    self._actor_fused_pre = True
+            else:
+                tr.encoder(state, action, next_state)
+        elif branch and TARGET_ON_MAIN:
             # the critic target chain (target_a -> target_b, the longest branch
             # before the critic) on the iteration's own stream, the fixed
             # embeddings beside it: the critic's join then waits on a branch
@@ -907,6 +931,58 @@ class TD7Learner:
         Q_target = ops.q_target(Q_heads, reward, not_done, hp.discount, self.min_target, self.max_target,
                                 self.max, self.min)
         return Q_target if pair is None else (Q_target, fixed_zsa)
+
+    # Cross-iteration prefetch of the critic's inputs (r04).  The fixed
+    # embeddings fixed_encoder.zs/zsa(s, a) and the target heads
+    # critic_target(s', actor_target(s') + noise, ...) of a batch read only the
+    # batch and nets that change at a target refresh (:284-293), so the
+    # trainer computes them for the NEXT batch right after sampling it, at the
+    # end of the current iteration -- beside that iteration's actor update --
+    # into one of two persistent slots; the next iteration's critic pass then
+    # starts at once.  The same launches on the same inputs in the same order
+    # (the target-noise stream included): bit-identical.  Never across a target
+    # refresh (the trainer does not prefetch before one; the refresh drops any
+    # prefetched slot), and Agent.train()'s own updates drop them too.
+    pre_in = None  # slot whose prefetched inputs the next phase_grads reads (set by the trainer)
+
+    def _pre_slot(self, slot, B):
+        bufs = getattr(self, "_pre_bufs", None)
+        if bufs is None or bufs[0][0].shape[0] != B:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("prefetch_targets: run once eagerly before graph capture")
+            Z = self.hp.zs_dim
+            f32 = dict(dtype=torch.float32, device=self.device)
+            self._pre_bufs = bufs = [(torch.empty((B, Z), **f32), torch.empty((B, Z), **f32),
+                                      torch.empty((B, 2), **f32)) for _ in range(2)]
+        return bufs[slot]
+
+    _pre_ready = (False, False)
+
+    def prefetch_ready(self, slot):
+        return bool(self._pre_ready[slot])
+
+    def drop_prefetch(self):
+        self._pre_ready = [False, False]
+
+    def prefetch_targets(self, state, action, next_state, slot):
+        """fixed(s, a) and the target heads of (s') for the batch in `slot`, on
+        the current stream (fixed on a branch beside the target chain)."""
+        if self.fused is None:
+            raise RuntimeError("prefetch_targets: the fused TD7 path only")
+        fz = self.fused
+        zs, zsa, qt = self._pre_slot(slot, state.shape[0])
+        cur = torch.cuda.current_stream(self.device)
+        st = getattr(self, "_pfside", None)
+        if st is None:
+            st = self._pfside = torch.cuda.Stream(device=self.device)
+        st.wait_stream(cur)
+        with torch.cuda.stream(st):
+            fz.fixed(state, action, out=(zs, zsa))
+        fz.target_heads(next_state, None, out=qt)
+        cur.wait_stream(st)
+        if not isinstance(self._pre_ready, list):
+            self._pre_ready = [False, False]
+        self._pre_ready[slot] = True
 
     def join_side(self):
         """Order the current stream after the encoder branch (end of an update)."""
@@ -1065,6 +1141,8 @@ class TD7Learner:
         """One TD7 gradient step on a sampled batch.  Returns the per-sample
         priorities |td|max.clamp(min_priority)^alpha (:262)."""
         self.training_steps += 1
+        self.drop_prefetch()  # prefetched inputs belong to the trainer's next batch, not this one
+        self.pre_in = None
         if update_actor is None:
             update_actor = self.training_steps % self.hp.policy_freq == 0
         # an eager update is self-contained: every branch it forks is joined
@@ -1096,6 +1174,7 @@ class TD7Learner:
         """:284-293; returns True when the targets were refreshed."""
         if self.training_steps % self.hp.target_update_rate != 0:
             return False
+        self.drop_prefetch()  # computed with the nets this refresh replaces
         for dst, src in ((self.actor_target, self.actor), (self.critic_target, self.critic),
                          (self.fixed_encoder_target, self.fixed_encoder), (self.fixed_encoder, self.encoder)):
             with torch.no_grad():

@@ -24,7 +24,9 @@ def test_graph_replay_matches_eager_bookkeeping():
     for _ in range(12):
         assert te.step() == tg.step()
     torch.cuda.synchronize()
-    assert len(tg.graphs) == 2  # policy_freq 2: parity and observation buffer alternate in lockstep
+    # policy_freq 2: parity and observation buffer alternate in lockstep (further keys:
+    # the target-prefetch variants around the target refreshes, target_update_rate 5)
+    assert len({k[:2] for k in tg.graphs}) == 2
     np.testing.assert_array_equal(ag_e.replay_buffer.size_s.cpu().numpy(), ag_g.replay_buffer.size_s.cpu().numpy())
     np.testing.assert_array_equal(ag_e.replay_buffer.ptr_s.cpu().numpy(), ag_g.replay_buffer.ptr_s.cpu().numpy())
     assert ag_g.learner.training_steps == 12
@@ -77,7 +79,7 @@ def test_graph_replay_matches_eager_with_policy_freq_3():
     tg, _, _ = _make(True, policy_freq=3)
     for _ in range(12):
         tg.step()
-    assert sorted(tg.graphs) == [(False, 0), (False, 1), (True, 0), (True, 1)]
+    assert sorted({k[:2] for k in tg.graphs}) == [(False, 0), (False, 1), (True, 0), (True, 1)]
 
 
 def test_pink_exploration_trainer_runs_in_graphs():
