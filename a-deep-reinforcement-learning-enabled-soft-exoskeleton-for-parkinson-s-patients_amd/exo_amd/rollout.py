@@ -341,13 +341,18 @@ class VecTrainer:
     def _prefetching(self):
         return self.prefetch_sample and self.overlap_rollout
 
-    # r04: with the next batch sampled at the end of an iteration, its fixed
-    # embeddings and target heads are computed right after it (beside the
-    # actor update of an actor iteration) into one of two persistent slots
-    # (TD7Learner.prefetch_targets); the next iteration's critic pass starts
-    # at once.  Not before a target refresh (the refresh changes those nets),
-    # not in the data-parallel three-graph layout.  EXO_TARGET_PREFETCH=0: off.
-    prefetch_targets = os.environ.get("EXO_TARGET_PREFETCH", "1") == "1"
+    # r04 (EXO_TARGET_PREFETCH=1, off by default): with the next batch sampled
+    # at the end of an iteration, its fixed embeddings and target heads are
+    # computed right after it (beside the actor update of an actor iteration)
+    # into one of two persistent slots (TD7Learner.prefetch_targets), and the
+    # next iteration's critic pass starts at once.  Not before a target
+    # refresh (the refresh changes those nets), not in the data-parallel
+    # three-graph layout.  Bit-identical, but measured slower (0.37-0.46 vs
+    # 0.30 ms per iteration, profiles/r04h_raw): the critic -> priority ->
+    # sample -> targets chain is as long as before, and the graph's four
+    # hardware queues put the actor passes behind the target chain instead of
+    # beside it ("TD7 fused").
+    prefetch_targets = os.environ.get("EXO_TARGET_PREFETCH", "0") == "1"
     _pre_in = _pre_out = False
 
     def _target_prefetch_flags(self):
@@ -387,10 +392,21 @@ class VecTrainer:
         if getattr(self, "_rollout_stream", None) is None:
             self._rollout_stream = torch.cuda.Stream(device=self.device)
         br = self._rollout_stream
-        br.wait_stream(cur)
-        with torch.cuda.stream(br):
-            self._rollout()
-        self._prio = ag.learner.phase_grads(*self._batch)
+        if self.td7_first:
+            # the same dependencies, the TD7 passes captured (and so dispatched)
+            # before the rollout branch: select_action's workgroups fill every
+            # CU, launched first they hold the update's first passes back
+            fork = torch.cuda.Event()
+            fork.record(cur)
+            self._prio = ag.learner.phase_grads(*self._batch)
+            br.wait_event(fork)
+            with torch.cuda.stream(br):
+                self._rollout()
+        else:
+            br.wait_stream(cur)
+            with torch.cuda.stream(br):
+                self._rollout()
+            self._prio = ag.learner.phase_grads(*self._batch)
         cur.wait_stream(br)
 
     # LAP.update_priority reads only the sampled indices and the new priorities
@@ -406,6 +422,12 @@ class VecTrainer:
     # with no cross-queue hand-off on the critical path (EXO_PRIO_BRANCH_ALL=1:
     # the branch in every iteration, the r02 layout)
     prio_branch_all = os.environ.get("EXO_PRIO_BRANCH_ALL", "0") == "1"
+    # capture order (r04, measured, off): EXO_TD7_FIRST (TD7 passes captured
+    # before the rollout branch: 0.324 vs 0.305 ms) / EXO_ACTOR_FIRST (actor
+    # passes before the priority branch: 0.303 vs 0.305, noise) --
+    # profiles/r04h_raw
+    td7_first = os.environ.get("EXO_TD7_FIRST", "0") == "1"
+    actor_first = os.environ.get("EXO_ACTOR_FIRST", "0") == "1"
 
     def _mid(self, update_actor, flat_grad=None, grad_scale=1.0, rollout=True):
         ag = self.agent
@@ -416,6 +438,17 @@ class VecTrainer:
             if getattr(self, "_prio_stream", None) is None:
                 self._prio_stream = torch.cuda.Stream(device=self.device)
             self._pside = self._prio_stream
+            if self.actor_first and update_actor:
+                # the same dependencies, the actor's passes captured before the
+                # priority branch (the graph's queues then take them first)
+                fork = torch.cuda.Event()
+                fork.record(cur)
+                ag.learner.phase_steps(flat_grad, grad_scale)
+                ag.learner.phase_actor_grads(self._batch[0], self._batch[1])
+                self._pside.wait_event(fork)
+                with torch.cuda.stream(self._pside):
+                    self._update_and_sample_next()
+                return
             self._pside.wait_stream(cur)
             with torch.cuda.stream(self._pside):
                 self._update_and_sample_next()
@@ -446,6 +479,7 @@ class VecTrainer:
             self._pside = None
         L = self.agent.learner
         L.join_side()  # the encoder branch's optimiser step
+        L.join_prefetch()  # the next batch's fixed pass
         # the deferred-join mode belongs to this iteration only: an update()
         # called later (Agent.train) must not leave work on the branch
         L.defer_side_join = False

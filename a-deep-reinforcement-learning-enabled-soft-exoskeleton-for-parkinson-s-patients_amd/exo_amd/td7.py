@@ -971,6 +971,10 @@ class TD7Learner:
             raise RuntimeError("prefetch_targets: the fused TD7 path only")
         fz = self.fused
         zs, zsa, qt = self._pre_slot(slot, state.shape[0])
+        # the fixed pass on a branch of its own beside the target chain, joined
+        # by the trainer at the end of the iteration (join_prefetch) -- not back
+        # into this stream: a fork joined inside a forked branch made
+        # hipStreamEndCapture crash (r04, tools/seg_bisect.py)
         cur = torch.cuda.current_stream(self.device)
         st = getattr(self, "_pfside", None)
         if st is None:
@@ -979,10 +983,18 @@ class TD7Learner:
         with torch.cuda.stream(st):
             fz.fixed(state, action, out=(zs, zsa))
         fz.target_heads(next_state, None, out=qt)
-        cur.wait_stream(st)
+        self._pf_open = True
         if not isinstance(self._pre_ready, list):
             self._pre_ready = [False, False]
         self._pre_ready[slot] = True
+
+    _pf_open = False
+
+    def join_prefetch(self):
+        """Order the current stream after prefetch_targets' fixed-pass branch."""
+        if self._pf_open:
+            torch.cuda.current_stream(self.device).wait_stream(self._pfside)
+            self._pf_open = False
 
     def join_side(self):
         """Order the current stream after the encoder branch (end of an update)."""
