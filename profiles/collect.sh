@@ -1,7 +1,8 @@
 #!/bin/bash
 # Collect the round's rocprofv3 evidence on the GPU box (run via gpurun):
 #   kernel stats of the default training bench, of the env-only bench, and the
-#   FETCH_SIZE / WRITE_SIZE PMC passes (separate runs) for the exo_step kernel.
+#   FETCH_SIZE / WRITE_SIZE PMC passes (separate runs) for the exo_step kernel,
+#   then the default bench (CPU baseline included) and configs[3] plain.
 # usage: bash profiles/collect.sh TAG
 set -euo pipefail
 TAG=${1:-r01}
@@ -17,7 +18,5 @@ timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex exo_step --o
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex exo_step --output-format csv -d $OUT/pmc_write -o run -- \
     python3 bench.py --mode env --steps 100 --warmup 10 --no-cpu-baseline > $OUT/pmc_write.log 2>&1
 timeout -k 10 400 python3 bench.py > $OUT/bench_default.log 2>&1
-timeout -k 10 200 python3 tools/dense_bench.py > $OUT/dense_bench.txt 2>&1
-timeout -k 10 200 python3 tools/fused_bench.py > $OUT/fused_bench.txt 2>&1
-if [ -x tools/stream_bench ]; then timeout -k 10 120 tools/stream_bench > $OUT/stream_bench.txt 2>&1; fi
+timeout -k 10 400 python3 bench.py --workload dr_sweep --steps 200 --warmup 20 --no-cpu-baseline --no-reference-schedule > $OUT/bench_dr.log 2>&1
 find $OUT -name "*.csv" | head -50
