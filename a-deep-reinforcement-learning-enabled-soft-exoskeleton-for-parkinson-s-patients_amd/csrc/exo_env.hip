@@ -518,47 +518,90 @@ __device__ __forceinline__ double pct_change(double v, double ref) { // nan_to_n
     return isfinite(x) ? x : 0.0;
 }
 
-__global__ void tremor_metrics_kernel(Dev S, const float *__restrict__ info, const uint8_t *__restrict__ stepped,
-                                      double L1, double L2, int disregard, float *__restrict__ metrics,
-                                      float *__restrict__ counters) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= S.N) return;
+// 8 lanes per env (r04; one thread per env before: 27 us per 4,096-env launch,
+// 16 workgroups, three serial DH chains of 7 fp64 sincos each per thread).
+// Lane j < 7 owns joint j: its two percent changes and the sines and cosines
+// of its angle in the three DH chains; lanes 0, 1, 2 then each multiply one
+// chain (the same expressions in the same order as dh_end_effector, the sines
+// and cosines fetched by shuffles) and lane 0 finishes the env.  Bit-identical
+// to the per-thread form.
+constexpr int TM_LANES = 8;
+__device__ __forceinline__ double shfl8(double v, int src) { return __shfl(v, src, TM_LANES); }
+
+__global__ __launch_bounds__(256) void tremor_metrics_kernel(Dev S, const float *__restrict__ info,
+                                                             const uint8_t *__restrict__ stepped, double L1, double L2,
+                                                             int disregard, float *__restrict__ metrics,
+                                                             float *__restrict__ counters) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    const int e = g / TM_LANES, j = g % TM_LANES;
+    if (e >= S.N) return;  // uniform over the env's 8 lanes
+    float *m = metrics + (size_t)e * 16;
     if (stepped && !stepped[e]) {  // a done env's row of the step is zeros (:201-203); counters untouched
-        float4 *m4 = reinterpret_cast<float4 *>(metrics + (size_t)e * 16);
-        for (int j = 0; j < 4; ++j) m4[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (j < 4) reinterpret_cast<float4 *>(m)[j] = make_float4(0.f, 0.f, 0.f, 0.f);
         return;
     }
     const float *in = info + (size_t)e * INFO;
-    double tr[7], ta[7];
-    for (int j = 0; j < 7; ++j) {
-        tr[j] = pct_change(in[7 + j], in[21 + j]);   // torque_val vs tremor_torque_val
-        ta[j] = pct_change(in[14 + j], in[28 + j]);  // ampl_val vs tremor_ampl_val
-    }
+    const int jj = j < 7 ? j : 6;  // lane 7 mirrors joint 6 (its values unused)
+    double tr = pct_change(in[7 + jj], in[21 + jj]);   // torque_val vs tremor_torque_val
+    double ta = pct_change(in[14 + jj], in[28 + jj]);  // ampl_val vs tremor_ampl_val
     // return_original_joint_angles at the post-step count: x, y, z, elbow y, elbow z, 0, 0 (degrees)
     const int cnt = S.counts[e];
     const double *imu = S.imu + (size_t)S.motion[e] * 5 * S.Lmax;
-    const int col[5] = {2, 3, 4, 0, 1};
-    double q0[7], q1[7], q2[7];
-    for (int j = 0; j < 7; ++j) {
-        const double o = j < 5 ? imu[col[j] * S.Lmax + cnt] * (PI / 180) : 0.0;
-        q0[j] = o;
-        q1[j] = (double)in[14 + j] * (PI / 180) + o;
-        q2[j] = (double)in[28 + j] * (PI / 180) + o;
+    const int colj = jj == 0 ? 2 : jj == 1 ? 3 : jj == 2 ? 4 : jj == 3 ? 0 : 1;
+    const double o = jj < 5 ? imu[colj * S.Lmax + cnt] * (PI / 180) : 0.0;
+    const double th0 = o, th1 = (double)in[14 + jj] * (PI / 180) + o, th2 = (double)in[28 + jj] * (PI / 180) + o;
+    const double c0 = cos(th0), s0 = sin(th0), c1 = cos(th1), s1 = sin(th1), c2 = cos(th2), s2 = sin(th2);
+    // lanes 0 / 1 / 2: the chain of q0 / q1 / q2 (dh_end_effector)
+    const int base = threadIdx.x & ~(TM_LANES - 1);
+    const double alpha[7] = {PI / 2, PI / 2, -PI / 2, PI / 2, PI / 2, PI / 2, PI / 2};
+    const double d[7] = {0, 0, L1, 0, L2, 0, 0};
+    double T[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        const double ck0 = shfl8(c0, k), sk0 = shfl8(s0, k), ck1 = shfl8(c1, k), sk1 = shfl8(s1, k);
+        const double ck2 = shfl8(c2, k), sk2 = shfl8(s2, k);
+        const double ct = j == 0 ? ck0 : j == 1 ? ck1 : ck2, st = j == 0 ? sk0 : j == 1 ? sk1 : sk2;
+        const double ca = cos(alpha[k]), sa = sin(alpha[k]);
+        const double A[12] = {ct, -st * ca, st * sa, 0.0, st, ct * ca, -ct * sa, 0.0, 0.0, sa, ca, d[k]};
+        double R[12];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                double v = T[i * 4 + 0] * A[0 * 4 + c] + T[i * 4 + 1] * A[1 * 4 + c] + T[i * 4 + 2] * A[2 * 4 + c];
+                if (c == 3) v += T[i * 4 + 3];
+                R[i * 4 + c] = v;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 12; ++i) T[i] = R[i];
     }
-    double p0[3], p1[3], p2[3];
-    dh_end_effector(q0, L1, L2, p0);
-    dh_end_effector(q1, L1, L2, p1);
-    dh_end_effector(q2, L1, L2, p2);
-    const double ds = sqrt((p1[0] - p0[0]) * (p1[0] - p0[0]) + (p1[1] - p0[1]) * (p1[1] - p0[1]) +
-                           (p1[2] - p0[2]) * (p1[2] - p0[2]));
-    const double du = sqrt((p2[0] - p0[0]) * (p2[0] - p0[0]) + (p2[1] - p0[1]) * (p2[1] - p0[1]) +
-                           (p2[2] - p0[2]) * (p2[2] - p0[2]));
+    (void)base;
+    const double px = T[3], py = T[7], pz = T[11];
+    const double p0x = shfl8(px, 0), p0y = shfl8(py, 0), p0z = shfl8(pz, 0);
+    const double p1x = shfl8(px, 1), p1y = shfl8(py, 1), p1z = shfl8(pz, 1);
+    const double p2x = shfl8(px, 2), p2y = shfl8(py, 2), p2z = shfl8(pz, 2);
+    // counters (before the disregard clamp, :172-184): torque reductions of axes 0..3
+    int neg = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) neg += shfl8(tr, k) < 0 ? 1 : 0;
+    if (disregard) { // :186-191
+        if (tr > 0) tr = 0;
+        if (ta > 0) ta = 0;
+    }
+    int nzc = 0;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) nzc += shfl8(tr, k) != 0.0 ? 1 : 0;
+    if (j < 7) {
+        m[j] = (float)tr;
+        m[7 + j] = (float)ta;
+    }
+    if (j != 0) return;
+    const double ds = sqrt((p1x - p0x) * (p1x - p0x) + (p1y - p0y) * (p1y - p0y) + (p1z - p0z) * (p1z - p0z));
+    const double du = sqrt((p2x - p0x) * (p2x - p0x) + (p2y - p0y) * (p2y - p0y) + (p2z - p0z) * (p2z - p0z));
     double total = (ds - du) / du * 100.0;
-    // counters (before the disregard clamp, :172-184)
     float *cn = counters + (size_t)e * 6;
-    int nonneg = 0, neg = 0;
-    for (int j = 0; j < 4; ++j) (tr[j] >= 0 ? nonneg : neg) += 1;
-    cn[0] += nonneg;
+    cn[0] += 4 - neg;
     cn[1] += neg;
     if (neg > 0) cn[2] += 1;
     if (total < 0) {
@@ -567,22 +610,9 @@ __global__ void tremor_metrics_kernel(Dev S, const float *__restrict__ info, con
     } else {
         cn[3] += 1;
     }
-    if (disregard) { // :186-191
-        for (int j = 0; j < 7; ++j) {
-            if (tr[j] > 0) tr[j] = 0;
-            if (ta[j] > 0) ta[j] = 0;
-        }
-        if (total > 0) total = 0;
-    }
-    float *m = metrics + (size_t)e * 16;
-    bool nz = false;
-    for (int j = 0; j < 7; ++j) {
-        m[j] = (float)tr[j];
-        m[7 + j] = (float)ta[j];
-        nz |= tr[j] != 0.0;
-    }
+    if (disregard && total > 0) total = 0;
     m[14] = (float)total;
-    m[15] = nz ? 1.f : 0.f;
+    m[15] = nzc ? 1.f : 0.f;
 }
 
 // Evaluation-script statistics (Simulation/Evaluate_control_performance.py:
@@ -1286,7 +1316,8 @@ int exo_tremor_metrics(exo_ctx *c, const float *info_dev, const uint8_t *stepped
     (void)hand_length; // the reference's DH table ends at the wrist (a = d = 0 for joints 6, 7)
     if (!c || !info_dev || !metrics_dev || !counters_dev) return EXO_EINVAL;
     DeviceGuard g(c->device);
-    hipLaunchKernelGGL(tremor_metrics_kernel, dim3((c->N + 255) / 256), dim3(256), 0, (hipStream_t)stream, c->S,
+    hipLaunchKernelGGL(tremor_metrics_kernel, dim3(((size_t)c->N * TM_LANES + 255) / 256), dim3(256), 0,
+                       (hipStream_t)stream, c->S,
                        info_dev, stepped_dev, humerus_length, forearm_length, disregard, metrics_dev, counters_dev);
     return check(c, hipGetLastError(), "exo_tremor_metrics");
 }

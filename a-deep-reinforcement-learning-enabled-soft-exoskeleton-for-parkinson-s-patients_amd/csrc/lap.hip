@@ -590,12 +590,26 @@ __device__ __forceinline__ void copy_rows(const lap_storage_desc &st, const floa
     }
 }
 
+// The training loop's per-step mask advance, optionally done by the insert's
+// last workgroup out (lap_store_batch_ref_fused_adv): every workgroup has read
+// the step's mask by then.  exo_active_advance_score's arithmetic: score +=
+// reward where the step's mask is set, k = min(k + 1, rows - 1), mask = table
+// row k, count = its population.
+struct MaskAdvance {
+    const uint8_t *table;  // nullptr: no advance
+    int rows;
+    long long *k;
+    uint8_t *active;
+    int32_t *count;
+    double *score;         // nullptr: no score
+};
+
 template <bool VEC>
 __global__ __launch_bounds__(UPD_THREADS) void lap_store_ref_fused_kernel(
     float *tree, const float *maxp, int cap, int levels, int capacity, int E, long long *ref, int32_t *ring_size,
     lap_storage_desc st, const float *state, const float *action, const float *next_state, const float *reward,
     const uint8_t *done, float action_scale, const int32_t *strata, const uint8_t *active, int n,
-    uint32_t *ticket) {
+    uint32_t *ticket, MaskAdvance adv) {
     const int s = blockIdx.x, part = blockIdx.y, K = gridDim.y;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     __shared__ int wsum[UPD_THREADS / 64];
@@ -727,15 +741,40 @@ __global__ __launch_bounds__(UPD_THREADS) void lap_store_ref_fused_kernel(
             propagate_span(T, cap, levels, capacity, (int)ptr0, cnt);
     }
     __syncthreads();
-    if (t == 0) {  // ref was read (and used) before this add: no fence needed
-        if (atomicAdd(ticket, 1u) == (uint32_t)(E * K - 1)) {  // every workgroup has read ref
-            const long long adv = mult_below(count0 + n_act, E) - m0;
-            const long long size = min(size0 + adv, (long long)capacity);
+    __shared__ int last;
+    if (t == 0) {  // ref and the mask were read (and used) before this add: no fence needed
+        last = atomicAdd(ticket, 1u) == (uint32_t)(E * K - 1);  // every workgroup has read them
+        if (last) {
+            const long long na = mult_below(count0 + n_act, E) - m0;
+            const long long size = min(size0 + na, (long long)capacity);
             for (int q = 0; q < E; ++q) ring_size[q] = (int32_t)size;
-            ref[0] = (ptr0 + adv) % capacity;
+            ref[0] = (ptr0 + na) % capacity;
             ref[1] = count0 + n_act;
             ref[2] = size;
             *ticket = 0u;
+        }
+    }
+    __syncthreads();
+    if (!last || !adv.table) return;
+    const long long k0 = *adv.k;
+    const long long kk = k0 + 1 < adv.rows ? k0 + 1 : adv.rows - 1;
+    int c = 0;
+    for (int e = t; e < n; e += UPD_THREADS) {
+        const uint8_t v = adv.table[(size_t)kk * n + e];
+        if (adv.score) adv.score[e] += adv.active[e] ? (double)reward[e] : 0.0;
+        adv.active[e] = v;
+        c += v != 0;
+    }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    __shared__ int wc[UPD_THREADS / 64];
+    if (lane == 0) wc[wv] = c;
+    __syncthreads();
+    if (t == 0) {
+        *adv.k = kk;
+        if (adv.count) {
+            int tot = 0;
+            for (int w = 0; w < UPD_THREADS / 64; ++w) tot += wc[w];
+            *adv.count = tot;
         }
     }
 }
@@ -1101,10 +1140,10 @@ int lap_store_batch_ref(const lap_tree_desc *t, const lap_storage_desc *st, int6
     return rc(hipGetLastError());
 }
 
-int lap_store_batch_ref_fused(const lap_tree_desc *t, const lap_storage_desc *st, int64_t *ref_dev,
-                              const float *state, const float *action, const float *next_state, const float *reward,
-                              const uint8_t *done, const int32_t *strata, const uint8_t *active, float action_scale,
-                              int32_t n, uint32_t *ticket_dev, void *stream) {
+static int store_ref_fused(const lap_tree_desc *t, const lap_storage_desc *st, int64_t *ref_dev,
+                           const float *state, const float *action, const float *next_state, const float *reward,
+                           const uint8_t *done, const int32_t *strata, const uint8_t *active, float action_scale,
+                           int32_t n, uint32_t *ticket_dev, const MaskAdvance &adv, void *stream) {
     if (!valid(t) || !st || !st->state || !st->action || !st->next_state || !st->reward || !st->not_done ||
         !st->size || st->state_dim <= 0 || st->action_dim <= 0 || !ref_dev || !state || !action || !next_state ||
         !reward || !done || !strata || !ticket_dev || n < 0 || action_scale == 0.0f)
@@ -1120,13 +1159,32 @@ int lap_store_batch_ref_fused(const lap_tree_desc *t, const lap_storage_desc *st
         hipLaunchKernelGGL(lap_store_ref_fused_kernel<true>, dim3(E, K), dim3(UPD_THREADS), 0, (hipStream_t)stream,
                            t->tree, t->max_priority, t->cap, levels_of(t), t->capacity, E, (long long *)ref_dev,
                            st->size, *st, state, action, next_state, reward, done, action_scale, strata, active, n,
-                           ticket_dev);
+                           ticket_dev, adv);
     else
         hipLaunchKernelGGL(lap_store_ref_fused_kernel<false>, dim3(E, K), dim3(UPD_THREADS), 0, (hipStream_t)stream,
                            t->tree, t->max_priority, t->cap, levels_of(t), t->capacity, E, (long long *)ref_dev,
                            st->size, *st, state, action, next_state, reward, done, action_scale, strata, active, n,
-                           ticket_dev);
+                           ticket_dev, adv);
     return rc(hipGetLastError());
+}
+
+int lap_store_batch_ref_fused(const lap_tree_desc *t, const lap_storage_desc *st, int64_t *ref_dev,
+                              const float *state, const float *action, const float *next_state, const float *reward,
+                              const uint8_t *done, const int32_t *strata, const uint8_t *active, float action_scale,
+                              int32_t n, uint32_t *ticket_dev, void *stream) {
+    return store_ref_fused(t, st, ref_dev, state, action, next_state, reward, done, strata, active, action_scale, n,
+                           ticket_dev, MaskAdvance{}, stream);
+}
+
+int lap_store_batch_ref_fused_adv(const lap_tree_desc *t, const lap_storage_desc *st, int64_t *ref_dev,
+                                  const float *state, const float *action, const float *next_state,
+                                  const float *reward, const uint8_t *done, const int32_t *strata, uint8_t *active,
+                                  float action_scale, int32_t n, uint32_t *ticket_dev, const uint8_t *table,
+                                  int32_t rows, int64_t *k_dev, int32_t *count_dev, double *score_dev, void *stream) {
+    if (!table || rows <= 0 || !k_dev || !active) return EXO_EINVAL;
+    return store_ref_fused(t, st, ref_dev, state, action, next_state, reward, done, strata, active, action_scale, n,
+                           ticket_dev, MaskAdvance{table, rows, (long long *)k_dev, active, count_dev, score_dev},
+                           stream);
 }
 
 int lap_sample_gather(const lap_tree_desc *t, const lap_storage_desc *st, const float *u, int32_t batch,

@@ -155,14 +155,16 @@ class LAP:
                                             nat.ptr(act), float(self.normalize_actions), n, nat.ptr(self._row_ws),
                                             self._stream()), "lap_store_batch")
 
-    def add_batch_ref(self, state, action, next_state, reward, done, strata, active=None):
+    def add_batch_ref(self, state, action, next_state, reward, done, strata, active=None, advance=None):
         """LAP.add (:49-63) for every active row in row order -- the training
         script's per-env loop over one vectorised step -- with the reference's
         shared pointer (ref_state, device-resident): env 0's first transition
         one slot behind the others, a done env's slot re-used by the next adds,
         one shared sampling size.  One kernel (lap_store_batch_ref_fused, r04;
         EXO_REF_INSERT_FUSED=0: the three launches of lap_store_batch_ref), no
-        host synchronisation."""
+        host synchronisation.  advance = (table, k, count, score): the
+        trainer's mask advance in the same launch (lap_store_batch_ref_fused_adv;
+        `active` is then advanced in place, the rewards added into score)."""
         n = state.shape[0]
         if self._ref_ws is None or self._ref_ws.numel() < 3 * n:
             # zeroed: its first word is the fused launch's ticket (left zero)
@@ -183,6 +185,16 @@ class LAP:
         act = None
         if active is not None:
             act = (active.view(torch.uint8) if active.dtype == torch.bool else active.to(torch.uint8)).contiguous()
+        if advance is not None:
+            if not self.ref_insert_fused or act is None or act.data_ptr() != active.data_ptr():
+                raise ValueError("add_batch_ref(advance=...): the fused insert and an in-place uint8/bool mask only")
+            table, k, count, score = advance
+            nat.check(nat.lib().lap_store_batch_ref_fused_adv(
+                ctypes.byref(self._desc), ctypes.byref(self._store), nat.ptr(self.ref_state), nat.ptr(st),
+                nat.ptr(ac), nat.ptr(nx), nat.ptr(rw), nat.ptr(dn), nat.ptr(sr), nat.ptr(act),
+                float(self.normalize_actions), n, nat.ptr(self._ref_ws), nat.ptr(table), table.shape[0], nat.ptr(k),
+                nat.ptr(count), nat.ptr(score), self._stream()), "lap_store_batch_ref_fused_adv")
+            return
         fn = "lap_store_batch_ref_fused" if self.ref_insert_fused else "lap_store_batch_ref"
         nat.check(getattr(nat.lib(), fn)(ctypes.byref(self._desc), ctypes.byref(self._store),
                                          nat.ptr(self.ref_state), nat.ptr(st), nat.ptr(ac), nat.ptr(nx),

@@ -750,6 +750,9 @@ class RefScheduleTrainer(VecTrainer):
         # the episode scores (:144) accumulated inside the mask advance launch;
         # EXO_REF_FUSED_SCORE=0: torch's where + add_ (2 launches per step)
         self.fused_score = os.environ.get("EXO_REF_FUSED_SCORE", "1") == "1"
+        # r04: that advance inside the replay insert's launch (its last
+        # workgroup out); EXO_REF_INSERT_ADVANCE=0: its own launch
+        self.insert_advance = os.environ.get("EXO_REF_INSERT_ADVANCE", "1") == "1"
         # the script's per-step tremor statistics (:149-205: exo_tremor_metrics
         # into a [round_len, N, 16] device record + per-env counters, 2
         # launches per step) and its per-round outputs (:213-317, round_stats()
@@ -844,6 +847,15 @@ class RefScheduleTrainer(VecTrainer):
         if not self.fused_score:
             self.score.add_(rew.where(self.active, 0.0))  # :144 (float32 into the float64 score, 2 launches)
         add = ag.replay_buffer.add_batch_ref if self.ref_replay else ag.replay_buffer.add_batch
+        rb = ag.replay_buffer
+        if (self.insert_advance and self.fused_score and self.ref_replay and not overlap and rb.ref_insert_fused
+                and self.active.dtype == torch.bool):
+            # the insert's last workgroup out advances the mask and adds the
+            # scores (:144), one launch for both (lap_store_batch_ref_fused_adv)
+            rb.add_batch_ref(obs, act, nobs, rew, done, self.strata, self.active,
+                             advance=(self._table_ext, self.k_dev, self.active_count, self.score))
+            self.last_actions = act
+            return
         if overlap:
             mask = self._act_prev[self._cur]
             mask.copy_(self.active)

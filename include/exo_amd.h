@@ -356,6 +356,20 @@ int lap_store_batch_ref_fused(const lap_tree_desc *t, const lap_storage_desc *st
                               const uint8_t *active_dev, float action_scale, int32_t n, uint32_t *ticket_dev,
                               void *stream);
 
+/* lap_store_batch_ref_fused plus the training loop's mask advance in the same
+ * launch (the reference-schedule rollout step, Simulation/
+ * Exoskeleton_agent_train.py:123-144): once every workgroup has read the
+ * step's mask, the last one out adds the step's rewards into the episode
+ * scores where the mask is set (score_dev, float64 [N], optional), advances
+ * the device step counter *k_dev = min(*k_dev + 1, rows - 1) and copies row
+ * *k_dev of the mask table (uint8 [rows][N]) into active (and its population
+ * into *count_dev, optional) -- exo_active_advance_score's arithmetic. */
+int lap_store_batch_ref_fused_adv(const lap_tree_desc *t, const lap_storage_desc *st, int64_t *ref_dev,
+                                  const float *state, const float *action, const float *next_state,
+                                  const float *reward, const uint8_t *done, const int32_t *strata, uint8_t *active,
+                                  float action_scale, int32_t n, uint32_t *ticket_dev, const uint8_t *table,
+                                  int32_t rows, int64_t *k_dev, int32_t *count_dev, double *score_dev, void *stream);
+
 /* LAP.sample (:65-111): batch draws per stratum (u_dev [n_strata][batch]),
  * indices -> idx_dev [n_strata][batch], the sampled rows gathered into
  * out_* [n_strata * batch][dim] (stratum-major). */

@@ -260,6 +260,46 @@ def test_fused_ref_insert_equals_three_launch_insert(E, C, N):
         np.testing.assert_array_equal(tr[s, 1:cap], tr[s, 2:2 * cap:2] + tr[s, 3:2 * cap:2])
 
 
+def test_fused_ref_insert_with_mask_advance_equals_two_launches():
+    """lap_store_batch_ref_fused_adv (the reference-schedule rollout's insert
+    with the trainer's mask advance and score accumulation in its last
+    workgroup out, r04) against lap_store_batch_ref_fused followed by
+    exo_active_advance_score: storage, trees, pointer, mask, step counter,
+    count and float64 scores bit for bit, past the table's last row."""
+    from exo_amd import _native as nat
+    E, C, N, rows = 8, 5000, 4100, 5
+    rng = np.random.default_rng(17)
+    a, b = _lap(E, C, 64), _lap(E, C, 64)
+    a.ref_insert_fused = b.ref_insert_fused = True
+    T = lambda x: torch.as_tensor(x, device="cuda")  # noqa: E731
+    table = T(rng.random((rows, N)) < 0.8).contiguous()
+    strata = T((np.arange(N) % E).astype(np.int32))
+    st_a = [table[0].clone(), torch.zeros(1, dtype=torch.int64, device="cuda"),
+            torch.zeros(1, dtype=torch.int32, device="cuda"), T(rng.normal(size=N))]
+    st_b = [x.clone() for x in st_a]
+    for step in range(rows + 2):
+        st = T(rng.normal(size=(N, 80)).astype(np.float32))
+        nx = T(rng.normal(size=(N, 80)).astype(np.float32))
+        ac = T(rng.uniform(-1, 1, (N, 7)).astype(np.float32))
+        rw = T(rng.normal(size=N).astype(np.float32))
+        dn = T(rng.random(N) < 0.05)
+        act_a, k_a, cnt_a, sc_a = st_a
+        a.add_batch_ref(st, ac, nx, rw, dn, strata, act_a)
+        nat.check(nat.lib().exo_active_advance_score(nat.ptr(table), rows, N, nat.ptr(k_a), nat.ptr(act_a),
+                                                     nat.ptr(cnt_a), nat.ptr(rw), nat.ptr(sc_a),
+                                                     nat.stream_ptr(torch.device("cuda", 0))), "advance")
+        act_b, k_b, cnt_b, sc_b = st_b
+        b.add_batch_ref(st, ac, nx, rw, dn, strata, act_b, advance=(table, k_b, cnt_b, sc_b))
+        torch.cuda.synchronize()
+        assert a.ref_pointer() == b.ref_pointer(), step
+        for name in ("state", "action", "next_state", "reward", "not_done"):
+            torch.testing.assert_close(getattr(b, name), getattr(a, name), rtol=0, atol=0)
+        torch.testing.assert_close(b._tree, a._tree, rtol=0, atol=0)
+        for x, y in zip(st_a, st_b):
+            assert torch.equal(x, y), step
+        assert int(k_b) == min(step + 1, rows - 1)
+
+
 @pytest.mark.parametrize("C,B,size", [(30_000, 128, 30_000), (30_000, 128, 17_001), (40, 16, 40), (250_000, 64, 99)])
 def test_update_and_sample_in_one_launch_equals_two(C, B, size):
     """lap_update_sample_rng (r04): LAP.update_priority then the next sample in
