@@ -156,9 +156,10 @@ def parse():
     if a.precision is None:
         a.precision = "fp16" if a.workload == "wide" else "bf16"
     if a.step_budget is None:
-        # configs[3]: 96 attempts per launch (profiles/r04d_raw: 25.3 M env-steps/s with async
-        # episodes at 96, 21.5 M at 160, 10.5 M unbudgeted)
-        a.step_budget = 96 if a.workload == "dr_sweep" and a.mode == "train" else 0
+        # configs[3]: 8 attempts per launch (profiles/r04o_raw, async episodes: 32.0 M
+        # env-steps/s at 8, 31.7 M at 16, 29.6 M at 32, 26.8 M at 64; r04d_raw: 25.3 M
+        # at 96, 21.5 M at 160, 10.5 M unbudgeted)
+        a.step_budget = 8 if a.workload == "dr_sweep" and a.mode == "train" else 0
     if a.episodes is None:
         # the vectorised trainer's own episodes: every env resets in place when its
         # episode ends (EXO_EPISODES=sync: the script's synchronous rounds)
