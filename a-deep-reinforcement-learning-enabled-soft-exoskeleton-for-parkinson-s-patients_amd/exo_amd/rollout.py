@@ -232,8 +232,6 @@ class VecTrainer:
             raise ValueError(f"exploration must be 'gaussian' or 'pink', not {exploration!r}")
         self.exploration = exploration
         self.k_dev = torch.zeros((1,), dtype=torch.int64, device=self.device)
-        self._act_next = torch.zeros((self.n, 7), dtype=torch.float32, device=self.device)
-        self._sel_ts = -1
         # budgeted env steps (env.set_step_budget, BASELINE configs[3]): a stiff
         # env's solve spans launches; the step mask then comes from the device
         # (exo_budget_advance: episode not over and no solve pending) and a
@@ -272,20 +270,12 @@ class VecTrainer:
     def _rollout(self):
         ag = self.agent
         obs = self.obs
-        pink = self.k_dev if self.exploration == "pink" else None
-        if self._sel_in:
-            act = self._act_next  # selected at the end of the previous iteration's rollout
-        else:
-            act = ag.select_action_batch(obs, timestep=pink, dec_count=self.active_count)
+        act = ag.select_action_batch(obs, timestep=self.k_dev if self.exploration == "pink" else None,
+                                     dec_count=self.active_count)
         nobs, rew, done, info = self.env.step(act, active=self.active, out=self._outs[self._cur],
                                               obs_cur=obs if self.budget else None)
         ag.replay_buffer.add_batch(obs, act, nobs, rew, done, self.strata, self.active)
         self._advance()
-        if self._sel_out:
-            # this iteration leaves the actor unchanged: the next step's actions
-            # (its observations, mask count and noise-stream position are final
-            # now) on this branch, off the next iteration's start
-            self._act_next.copy_(ag.select_action_batch(nobs, timestep=pink, dec_count=self.active_count))
         self.last_actions = act
 
     def _advance(self, rew=None, score=None):
@@ -550,26 +540,7 @@ class VecTrainer:
         self._join_prio()
 
     def _key(self, update_actor, rollout):
-        return ((update_actor, self._cur, self._pre_in, self._pre_out, self._sel_in, self._sel_out) if rollout
-                else ("train", update_actor))
-
-    # r04: the next step's select_action at the end of an iteration that does
-    # not update the actor (its weights are final for the next step then), on
-    # the rollout branch, into a persistent buffer; the next iteration starts
-    # with its env step and TD7 passes, without select_action's workgroups
-    # (every CU) in front of them.  Not before an episode-round reset (the
-    # observations are replaced) or across an Agent.train() (the actor may
-    # change).  The same launches in the same order: bit-identical.
-    # EXO_SELECT_AHEAD=0: off.
-    select_ahead = os.environ.get("EXO_SELECT_AHEAD", "1") == "1"
-    _sel_in = _sel_out = _sel_ready = False
-
-    def _select_flags(self, update_actor):
-        L = self.agent.learner
-        sel_in = self._sel_ready and self._sel_ts == L.training_steps - 1
-        nxt_round = self.episodes == "sync" and self.k + 1 >= self.round_len
-        sel_out = self.select_ahead and not update_actor and not nxt_round
-        return sel_in, sel_out
+        return (update_actor, self._cur, self._pre_in, self._pre_out) if rollout else ("train", update_actor)
 
     def _capture(self, update_actor, rollout=True):
         """Capture this parity's iteration (rollout=False: a training step
@@ -662,7 +633,6 @@ class VecTrainer:
         update_actor = L.training_steps % ag.hp.policy_freq == 0
         L.prefetch_actor = update_actor  # phase_grads may start the actor forward early
         self._pre_in, self._pre_out = self._target_prefetch_flags()
-        self._sel_in, self._sel_out = self._select_flags(update_actor)
         if not self.use_graphs or self.iters < self.warmup_eager:
             self._eager(update_actor)
         elif self._key(update_actor, True) not in self.graphs:
@@ -678,8 +648,6 @@ class VecTrainer:
             if self._pre_out:
                 L._pre_ready[1 - self._cur] = True
         L.pre_in = None
-        self._sel_ready, self._sel_ts = self._sel_out, L.training_steps
-        self._sel_in = self._sel_out = False
         if L.maybe_update_targets():
             ag.replay_buffer.reset_max_priority()
             ag.sync.max_(ag.replay_buffer._maxp)
