@@ -563,8 +563,13 @@ int td7f_select(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7
     if (actor[0].n_in != a.S || actor[1].n_in != a.Ha + a.Z || a.A > THIN_NC || a.S > NTH) return EXO_EINVAL;
     a.out = out;
     a.nz = noise_of(*noise);
-    const char *rt_env = getenv("EXO_SELECT_RT");  // read per call: tests switch it
-    const int RT = rt_env && rt_env[0] == '2' ? 2 : 1;
+    // 32-row tiles above 8,192 envs (more than two 16-row workgroups per CU:
+    // the weights are then streamed half as often; configs[3]'s 16,384 envs
+    // 0.452 vs 0.494 ms per iteration, profiles/r04q_raw); 16-row tiles below
+    // (4,096 envs: one workgroup per CU).  EXO_SELECT_RT=1|2 forces one (read
+    // per call: tests switch it).
+    const char *rt_env = getenv("EXO_SELECT_RT");
+    const int RT = rt_env && (rt_env[0] == '1' || rt_env[0] == '2') ? rt_env[0] - '0' : (n > 8192 ? 2 : 1);
     const int rows = RT * TR, hmax = std::max(enc[0].n_out, std::max(enc[1].n_out, std::max(a.Ha, actor[1].n_out)));
     Bump b(RT);
     a.X = b.r16(rows, ld16(a.S));
