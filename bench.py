@@ -146,6 +146,11 @@ def parse():
                     help="env-only launches timed with HIP events for the roofline line")
     ap.add_argument("--no-td7-variants", action="store_true",
                     help="skip the fp32-TD7 and 256-wide-alias sub-lines (configs[1] train mode)")
+    ap.add_argument("--step-clock", choices=["auto", "on", "off"], default="auto",
+                    help="configs[3] / [4]: device wall-clock kernels around every step launch inside the timed "
+                         "window (exo_set_step_clock; two extra launches on the rollout chain); auto = on with "
+                         "synchronous rounds only -- with async episodes the roofline launch is timed after the "
+                         "window on the loop's own state")
     ap.add_argument("--no-sync-rounds", action="store_true",
                     help="skip the synchronous-round comparison of the async-episode loop (configs[1])")
     ap.add_argument("--no-reference-schedule", action="store_true",
@@ -585,7 +590,9 @@ def main():
     # configs[3] / [4]: the env step inside the timed window itself -- device
     # wall-clock reads on the step's stream either side of every step launch,
     # captured into the trainer's graphs with it (exo_set_step_clock)
-    clock = env.set_step_clock() if (trainer is not None and args.workload != "configs1") else None
+    use_clock = trainer is not None and args.workload != "configs1" and (
+        args.step_clock == "on" or (args.step_clock == "auto" and args.episodes == "sync"))
+    clock = env.set_step_clock() if use_clock else None
     out = env.new_outputs(True)
     state = {"k": 0, "obs": env.reset() if trainer is None else None}  # the trainer resets its envs itself
     ev = []
@@ -775,7 +782,12 @@ def main():
             # freshly reset env stepped with U(-1, 1) actions is not what these
             # loops run, and the slowest domain-randomised env of a round sets
             # every launch of that round: profiles/r03_dr)
-            kern_ms, kern_active = window_clock[0], env_steps / args.steps
+            if window_clock is not None:
+                kern_ms, kern_active = window_clock[0], env_steps / args.steps
+            else:
+                # async episodes: no round whose stiffest env sets every launch;
+                # the loop's own launches timed right after the window
+                kern_ms, kern_active = loop_ms, loop_active
     # Whole-round rate, independent of where the K-iteration window falls in
     # the 344-step episode round: one round = round_len iterations (active
     # env-steps A_round = sum over k of the envs still running) + one reset.
@@ -877,7 +889,11 @@ def main():
                                               if args.workload == "configs1" else
                                               "the timed window's own step launches inside the graph-replayed "
                                               "training loop: device wall-clock reads either side of each launch "
-                                              "on its stream (exo_set_step_clock), averaged over the window")
+                                              "on its stream (exo_set_step_clock), averaged over the window"
+                                              if window_clock is not None else
+                                              "the loop's own step launches right after the timed window (its "
+                                              "policy, observations, masks and carried solves), eager, HIP events "
+                                              "(loop_workload); --step-clock on times them inside the window")
             if window_clock is not None:
                 res["roofline"]["window_step_clock"] = {"avg_ms": window_clock[0], "launches": window_clock[1],
                                                         "ms_per_iteration": elapsed / args.steps * 1e3}
