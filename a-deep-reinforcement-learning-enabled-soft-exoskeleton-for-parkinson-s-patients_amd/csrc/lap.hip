@@ -779,95 +779,6 @@ __global__ __launch_bounds__(UPD_THREADS) void lap_store_ref_fused_kernel(
     }
 }
 
-// r04: lap_store_batch (the per-stratum rings of the vectorised trainer) as
-// ONE launch, the layout of lap_store_ref_fused_kernel: grid (E strata) x (K
-// parts), every workgroup ranks its stratum's active rows (block scan per
-// chunk of STORE_CHUNK rows, ranks in env order), part 0 writes their leaves
-// (max_priority) at ring slot ptr + rank and recomputes the span's ancestors,
-// parts 1..K-1 copy ~64 rows each; the stratum's last part out (ticket
-// ws[s]) advances its ring.  Inactive rows are not copied
-// (lap_store_copy_kernel writes them to the trash row, which sampling never
-// reads).  The leaves, ancestors, slots and rows are those of the two
-// launches: bit-identical (tests/test_lap_gpu.py).
-template <bool VEC>
-__global__ __launch_bounds__(UPD_THREADS) void lap_store_fused_kernel(
-    float *tree, const float *maxp, int cap, int levels, int capacity, int32_t *ring_ptr, int32_t *ring_size,
-    lap_storage_desc st, const float *state, const float *action, const float *next_state, const float *reward,
-    const uint8_t *done, float action_scale, const int32_t *strata, const uint8_t *active, int n, int32_t *ws) {
-    const int s = blockIdx.x, part = blockIdx.y, K = gridDim.y;
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    const int KC = K > 1 ? K - 1 : 1, cpart = K > 1 ? part - 1 : 0;
-    __shared__ int wsum[UPD_THREADS / 64];
-    __shared__ int chunk_m;
-    __shared__ int32_t ri[STORE_CHUNK], sl[STORE_CHUNK];
-    float *T = stratum_tree(tree, s, cap);
-    const float p = *maxp;
-    const int ptr0 = ring_ptr[s];
-    int soff = 0;  // rows of stratum s ranked by earlier chunks
-    for (int base = 0; base < n; base += STORE_CHUNK) {
-        int cnt = 0;
-        bool g[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int i = base + 4 * t + k;
-            g[k] = i < n && strata[i] == s && (!active || active[i]);
-            cnt += g[k];
-        }
-        int incl = cnt;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int v = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += v;
-        }
-        if (lane == 63) wsum[wv] = incl;
-        __syncthreads();
-        if (t == 0) {
-            int acc = 0;
-            for (int k = 0; k < UPD_THREADS / 64; ++k) {
-                const int v = wsum[k];
-                wsum[k] = acc;
-                acc += v;
-            }
-            chunk_m = acc;
-        }
-        __syncthreads();
-        int j = wsum[wv] + incl - cnt;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (g[k]) {
-                const int slot = (ptr0 + soff + j) % capacity;
-                ri[j] = base + 4 * t + k;
-                sl[j] = slot;
-                if (part == 0) T[cap + slot] = p;
-                ++j;
-            }
-        }
-        __syncthreads();
-        const int m = chunk_m;
-        if (cpart >= 0) {
-            const int j0 = ((cpart - soff) % KC + KC) % KC;
-            copy_rows<VEC>(st, state, action, next_state, reward, done, action_scale, ri, sl, s, capacity, j0, KC, m,
-                           t, UPD_THREADS);
-        }
-        soff += m;
-        __syncthreads();
-    }
-    if (part == 0 && soff > 0) {
-        __shared__ float span_buf[2 * SPAN_LDS], span_edge[2 * SPAN_LEVELS];
-        const int c = min(soff, capacity);
-        if (!propagate_span_lds(T, cap, levels, capacity, ptr0, c, span_buf, span_edge))
-            propagate_span(T, cap, levels, capacity, ptr0, soff);
-    }
-    __syncthreads();
-    // the stratum's last part out advances its ring: every part ranked the same
-    // rows (soff), and each read the pointer (and used it) before its add
-    if (t == 0 && atomicAdd(ws + s, 1) == K - 1) {
-        ring_ptr[s] = (ptr0 + soff) % capacity;
-        ring_size[s] = min(ring_size[s] + soff, capacity);
-        ws[s] = 0;
-    }
-}
-
 __global__ __launch_bounds__(256) void lap_store_copy_kernel(lap_storage_desc st, const float *state,
                                                              const float *action, const float *next_state,
                                                              const float *reward, const uint8_t *done,
@@ -1205,31 +1116,6 @@ int lap_store_batch(const lap_tree_desc *t, const lap_storage_desc *st, const fl
     if (hipGetLastError() != hipSuccess) return EXO_EDEVICE;
     hipLaunchKernelGGL(lap_store_copy_kernel, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, *st, state,
                        action, next_state, reward, done, action_scale, n, row_ws);
-    return rc(hipGetLastError());
-}
-
-int lap_store_batch_fused(const lap_tree_desc *t, const lap_storage_desc *st, const float *state,
-                          const float *action, const float *next_state, const float *reward, const uint8_t *done,
-                          const int32_t *strata, const uint8_t *active, float action_scale, int32_t n, int32_t *ws_dev,
-                          void *stream) {
-    if (!valid(t) || !st || !st->state || !st->action || !st->next_state || !st->reward || !st->not_done ||
-        !st->ptr || !st->size || st->state_dim <= 0 || st->action_dim <= 0 || !state || !action || !next_state ||
-        !reward || !done || !strata || !ws_dev || n < 0 || action_scale == 0.0f)
-        return EXO_EINVAL;
-    if (n == 0) return EXO_OK;
-    const int E = t->n_strata;
-    const int K = 1 + std::max(1, std::min(15, (n + E * 64 - 1) / (E * 64)));
-    auto al16 = [](const void *p) { return ((uintptr_t)p & 15u) == 0; };
-    const bool vec = st->state_dim % 4 == 0 && al16(state) && al16(next_state) && al16(st->state) &&
-                     al16(st->next_state);
-    if (vec)
-        hipLaunchKernelGGL(lap_store_fused_kernel<true>, dim3(E, K), dim3(UPD_THREADS), 0, (hipStream_t)stream,
-                           t->tree, t->max_priority, t->cap, levels_of(t), t->capacity, st->ptr, st->size, *st, state,
-                           action, next_state, reward, done, action_scale, strata, active, n, ws_dev);
-    else
-        hipLaunchKernelGGL(lap_store_fused_kernel<false>, dim3(E, K), dim3(UPD_THREADS), 0, (hipStream_t)stream,
-                           t->tree, t->max_priority, t->cap, levels_of(t), t->capacity, st->ptr, st->size, *st, state,
-                           action, next_state, reward, done, action_scale, strata, active, n, ws_dev);
     return rc(hipGetLastError());
 }
 

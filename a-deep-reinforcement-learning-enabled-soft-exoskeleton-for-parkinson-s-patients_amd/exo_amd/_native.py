@@ -140,8 +140,6 @@ EXPORTS = {
     "lap_totals": (c_int32, [c_void_p, c_void_p, c_void_p]),
     "lap_store_batch": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_void_p, ctypes.c_float, c_int32, c_void_p, c_void_p]),
-    "lap_store_batch_fused": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                                        c_void_p, c_void_p, ctypes.c_float, c_int32, c_void_p, c_void_p]),
     "lap_store_batch_ref": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                       c_void_p, c_void_p, c_void_p, ctypes.c_float, c_int32, c_void_p, c_void_p]),
     "lap_store_batch_ref_fused": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -126,15 +126,10 @@ class LAP:
         self.count += 1
         self.size_s.fill_(self.size)
 
-    # r04: the ring insert as one launch (lap_store_batch_fused); EXO_LAP_STORE_FUSED=0:
-    # lap_store_batch's two
-    store_fused = os.environ.get("EXO_LAP_STORE_FUSED", "1") != "0"
-    _store_ws = None
-
     def add_batch(self, state, action, next_state, reward, done, strata, active=None):
         """One vectorised env step: row i goes to stratum strata[i] (int32 [N]) if
-        active[i] (bool/uint8 [N], default all) -- lap_store_batch_fused, one
-        kernel, no host synchronisation."""
+        active[i] (bool/uint8 [N], default all) -- lap_store_batch, two kernels,
+        no host synchronisation."""
         n = state.shape[0]
         if self._row_ws is None or self._row_ws.numel() < n:
             self._row_ws = torch.empty((n,), dtype=torch.int32, device=self.device)
@@ -155,15 +150,6 @@ class LAP:
         if active is not None:
             act = active.view(torch.uint8) if active.dtype == torch.bool else active.to(torch.uint8)
             act = act.contiguous()
-        if self.store_fused:
-            if self._store_ws is None:
-                self._store_ws = torch.zeros((self.num_envs,), dtype=torch.int32, device=self.device)  # tickets
-            nat.check(nat.lib().lap_store_batch_fused(ctypes.byref(self._desc), ctypes.byref(self._store),
-                                                      nat.ptr(st), nat.ptr(ac), nat.ptr(nx), nat.ptr(rw), nat.ptr(dn),
-                                                      nat.ptr(sr.contiguous()), nat.ptr(act),
-                                                      float(self.normalize_actions), n, nat.ptr(self._store_ws),
-                                                      self._stream()), "lap_store_batch_fused")
-            return
         nat.check(nat.lib().lap_store_batch(ctypes.byref(self._desc), ctypes.byref(self._store), nat.ptr(st),
                                             nat.ptr(ac), nat.ptr(nx), nat.ptr(rw), nat.ptr(dn), nat.ptr(sr.contiguous()),
                                             nat.ptr(act), float(self.normalize_actions), n, nat.ptr(self._row_ws),

@@ -332,15 +332,6 @@ int lap_store_batch(const lap_tree_desc *t, const lap_storage_desc *st, const fl
                     const uint8_t *done_dev, const int32_t *strata_dev, const uint8_t *active_dev, float action_scale,
                     int32_t n, int32_t *row_ws_dev, void *stream);
 
-/* lap_store_batch as ONE launch (r04): the same ring slots, leaves, ancestors
- * and copied rows (inactive rows are not copied to the trash row); ws_dev:
- * int32 [n_strata] tickets, zero-initialised by the caller once (the launch
- * leaves them zero). */
-int lap_store_batch_fused(const lap_tree_desc *t, const lap_storage_desc *st, const float *state,
-                          const float *action, const float *next_state, const float *reward, const uint8_t *done,
-                          const int32_t *strata, const uint8_t *active, float action_scale, int32_t n, int32_t *ws_dev,
-                          void *stream);
-
 /* LAP.add (Agent/TD7_buffer_multi_agent.py:49-63) called once per active env
  * of one vectorised step, in env order -- the training script's per-env loop
  * (Simulation/Exoskeleton_agent_train.py:139-142) -- with the reference's

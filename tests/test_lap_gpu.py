@@ -371,37 +371,6 @@ def test_wave_descent_and_subtree_rebuild_match_the_binary_tree():
         assert want.max() < size
 
 
-@pytest.mark.parametrize("E,C,N", [(8, 5000, 4096), (8, 30_000, 16_384), (3, 7000, 10_001)])
-def test_fused_ring_insert_equals_two_launches(E, C, N):
-    """lap_store_batch_fused (one launch, r04) against lap_store_batch (rank +
-    copy): ring slots, leaves, every tree node, ptr / size and the stored rows
-    (the trash row aside) bit for bit, with masks, several chunks and ring
-    wrap-around; non-integer priorities already in the trees."""
-    rng = np.random.default_rng(E * 7 + N)
-    a, b = _lap(E, C, 64), _lap(E, C, 64)
-    a.store_fused, b.store_fused = False, True
-    prio = rng.gamma(0.7, 2.0, (E, C)).astype(np.float32) + np.float32(1e-3)
-    for lap in (a, b):
-        _set_priorities(lap, prio)
-    T = lambda x: torch.as_tensor(x, device="cuda")  # noqa: E731
-    for step in range(5):
-        st = rng.normal(size=(N, 80)).astype(np.float32)
-        nx = rng.normal(size=(N, 80)).astype(np.float32)
-        ac = rng.uniform(-1, 1, (N, 7)).astype(np.float32)
-        rw = rng.normal(size=N).astype(np.float32)
-        dn = rng.random(N) < 0.05
-        strata = (np.arange(N) % E).astype(np.int32) if step % 2 == 0 else rng.integers(0, E, N).astype(np.int32)
-        active = rng.random(N) < [1.0, 0.7, 0.1, 0.95, 0.5][step]
-        for lap in (a, b):
-            lap.add_batch(T(st), T(ac), T(nx), T(rw), T(dn), T(strata), T(active))
-        torch.cuda.synchronize()
-        assert torch.equal(a.ptr_s, b.ptr_s) and torch.equal(a.size_s, b.size_s), step
-        for name in ("state", "action", "next_state", "reward", "not_done"):
-            torch.testing.assert_close(getattr(b, name)[:, :C], getattr(a, name)[:, :C], rtol=0, atol=0)
-        torch.testing.assert_close(b._tree, a._tree, rtol=0, atol=0)
-        assert int(b._store_ws.abs().sum()) == 0  # the tickets are left zero
-
-
 @pytest.mark.parametrize("C", [25_000, 5_000])
 def test_store_span_propagation_keeps_the_tree_exact(C):
     """lap_store_rank_kernel (r03d): a stratum's new slots are one ring span
