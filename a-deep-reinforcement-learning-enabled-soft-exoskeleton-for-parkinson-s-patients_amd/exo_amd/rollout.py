@@ -603,6 +603,53 @@ class VecTrainer:
             S.allreduce_flat(flat_a)
             g3.replay()
 
+    # Two iterations per graph replay (r04, EXO_PAIR_GRAPHS=1, one GPU): the
+    # iteration and the next one captured back to back into one graph (each
+    # joins all its branches before the next starts), so the GPU pays one
+    # graph launch per two iterations.  Only where no host work falls between
+    # them: no target refresh, no episode-round reset, no prefetch flags.
+    pair_graphs = os.environ.get("EXO_PAIR_GRAPHS", "0") == "1"
+    _pair_second = False
+
+    def _pair_ok(self):
+        L = self.agent.learner
+        return (self.pair_graphs and self.use_graphs and not self.dp and self.iters >= self.warmup_eager
+                and not (self._pre_in or self._pre_out)
+                and L.training_steps % L.hp.target_update_rate != 0
+                and (self.episodes == "async" or self.k + 1 < self.round_len))
+
+    def _pair_key(self, ua, ua2):
+        return ("pair", ua, ua2, self._cur)
+
+    def _run_pair(self, ua, ua2):
+        """This iteration and the next as one graph (captured on first use per
+        policy-update parities and observation buffer)."""
+        L = self.agent.learner
+        key = self._pair_key(ua, ua2)
+        g = self.graphs.get(key)
+        if g is None:
+            s = torch.cuda.Stream(device=self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            g = torch.cuda.CUDAGraph()
+            cur0 = self._cur
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s), ForkJoinAudit(s):
+                    for i, u in enumerate((ua, ua2)):
+                        L.prefetch_actor = u
+                        self._pre(True)
+                        self._mid(u, rollout=True)
+                        self._post(u)
+                        self._join_prio()
+                        if i == 0:
+                            self._cur ^= 1
+                            self.iters += 1  # the second half is never iteration 0
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            self._cur = cur0
+            self.iters -= 1
+            L.prefetch_actor = ua
+            self.graphs[key] = g
+        g.replay()
+
     # ------------------------------------------------------------- step
     def next_step_resets(self):
         """Whether the next step() starts a new episode round: after round_len
@@ -623,6 +670,10 @@ class VecTrainer:
         async episodes without a budget: every env, N)."""
         ag = self.agent
         L = ag.learner
+        if self._pair_second:  # its GPU work ran with the previous step's pair graph
+            self._pair_second = False
+            L.training_steps += 1
+            return self._step_tail()
         if self.next_step_resets():
             self.env.reset(obs_out=self.obs)
             self._round_start()
@@ -635,6 +686,12 @@ class VecTrainer:
         self._pre_in, self._pre_out = self._target_prefetch_flags()
         if not self.use_graphs or self.iters < self.warmup_eager:
             self._eager(update_actor)
+        elif (self._pair_ok() and self._key(update_actor, True) in self.graphs
+              and ((L.training_steps + 1) % ag.hp.policy_freq == 0, 1 - self._cur, False, False) in self.graphs):
+            # (both halves captured alone first: their warm-up created every
+            # buffer the pair capture needs)
+            self._run_pair(update_actor, (L.training_steps + 1) % ag.hp.policy_freq == 0)
+            self._pair_second = True
         elif self._key(update_actor, True) not in self.graphs:
             self._capture(update_actor)
         else:
@@ -648,6 +705,12 @@ class VecTrainer:
             if self._pre_out:
                 L._pre_ready[1 - self._cur] = True
         L.pre_in = None
+        return self._step_tail()
+
+    def _step_tail(self):
+        """Host bookkeeping after an iteration's GPU work."""
+        ag = self.agent
+        L = ag.learner
         if L.maybe_update_targets():
             ag.replay_buffer.reset_max_priority()
             ag.sync.max_(ag.replay_buffer._maxp)

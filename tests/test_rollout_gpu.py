@@ -116,3 +116,31 @@ def test_active_advance_saturates_and_copies_rows():
         assert torch.equal(act, table[want])
         if want != 2:  # the active count of the copied row (NULL: left alone)
             assert int(cnt) == int(table[want].sum())
+
+
+@pytest.mark.parametrize("episodes", ["sync", "async"])
+def test_pair_graphs_are_bit_identical(monkeypatch, episodes):
+    """EXO_PAIR_GRAPHS (two iterations per graph replay, r04): the same
+    launches in the same order -- weights, observations and replay rows bit
+    for bit against one graph per iteration, through target refreshes
+    (target_update_rate 5: single graphs around them)."""
+    from exo_amd.rollout import VecTrainer
+    res = []
+    for pair in (False, True):
+        monkeypatch.setattr(VecTrainer, "pair_graphs", pair)
+        monkeypatch.setenv("EXO_EPISODES", episodes)
+        tr, env, ag = _make(True, seed=4)
+        obs = []
+        for _ in range(17):
+            tr.step()
+            obs.append(tr.obs.clone())
+        torch.cuda.synchronize()
+        res.append((tr, obs, [p.detach().clone() for m in (ag.learner.actor, ag.learner.critic) for p in m.parameters()],
+                    ag.replay_buffer.state.clone()))
+    (t0, o0, w0, r0), (t1, o1, w1, r1) = res
+    for i, (a, b) in enumerate(zip(o0, o1)):
+        torch.testing.assert_close(b, a, rtol=0, atol=0, msg=f"iteration {i}")
+    for a, b in zip(w0, w1):
+        torch.testing.assert_close(b, a, rtol=0, atol=0)
+    torch.testing.assert_close(r1, r0, rtol=0, atol=0)
+    assert any(k[0] == "pair" for k in t1.graphs) and not any(k[0] == "pair" for k in t0.graphs)
