@@ -370,8 +370,11 @@ class VecTrainer:
         ag.learner.defer_side_join = ENC_STEP_BRANCH and (not self.dp or self.dp_inline)
         rb = ag.replay_buffer
         if not rollout:  # a training step alone (Agent.train): sample, then the gradients
-            self._batch = rb.sample()
-            self._ind = rb.ind
+            if self._train_pin:  # sampled by the burst's previous step (RefScheduleTrainer)
+                self._batch, self._ind = rb._slot(self._bslot)
+            else:
+                self._batch = rb.sample(self._bslot if self._train_pout else None)
+                self._ind = rb.ind
             self._prio = ag.learner.phase_grads(*self._batch)
             return
         slot = self._cur if self._prefetching() else None
@@ -465,7 +468,11 @@ class VecTrainer:
         (LAP.update_priority_and_sample).  The MAX all-reduce of max_priority
         (data parallel) follows; the sample does not read it."""
         rb = self.agent.replay_buffer
-        if self._prefetching() and self._mid_rollout:
+        if not self._mid_rollout and self._train_pout:
+            # a burst step with another after it: the next batch now, beside
+            # this step's optimiser steps (RefScheduleTrainer.train_step)
+            rb.update_priority_and_sample(self._prio, self._ind, 1 - self._bslot)
+        elif self._prefetching() and self._mid_rollout:
             rb.update_priority_and_sample(self._prio, self._ind, 1 - self._cur)
             if self._pre_out:
                 b = rb._slot(1 - self._cur)[0]
@@ -540,7 +547,15 @@ class VecTrainer:
         self._join_prio()
 
     def _key(self, update_actor, rollout):
-        return (update_actor, self._cur, self._pre_in, self._pre_out) if rollout else ("train", update_actor)
+        return ((update_actor, self._cur, self._pre_in, self._pre_out) if rollout
+                else ("train", update_actor, self._train_pin, self._train_pout, self._bslot))
+
+    # burst steps (RefScheduleTrainer.train_step): the next step's batch sampled
+    # at the end of the current one, into the other of two slots, when the
+    # burst has another step -- the sample leaves the head of every step
+    # (r04; bit-identical: the same update-then-sample order)
+    _train_pin = _train_pout = False
+    _bslot = 0
 
     def _capture(self, update_actor, rollout=True):
         """Capture this parity's iteration (rollout=False: a training step
@@ -816,6 +831,9 @@ class RefScheduleTrainer(VecTrainer):
         # r04: that advance inside the replay insert's launch (its last
         # workgroup out); EXO_REF_INSERT_ADVANCE=0: its own launch
         self.insert_advance = os.environ.get("EXO_REF_INSERT_ADVANCE", "1") == "1"
+        # the burst steps' next-batch prefetch (VecTrainer._key); EXO_BURST_PREFETCH=0: off
+        self.burst_prefetch = os.environ.get("EXO_BURST_PREFETCH", "1") == "1"
+        self._burst_i = 0
         # the script's per-step tremor statistics (:149-205: exo_tremor_metrics
         # into a [round_len, N, 16] device record + per-env counters, 2
         # launches per step) and its per-round outputs (:213-317, round_stats()
@@ -996,6 +1014,13 @@ class RefScheduleTrainer(VecTrainer):
         L.prefetch_actor = update_actor
         self._pre_in = self._pre_out = False
         L.drop_prefetch()
+        # the burst's position (maybe_train_and_checkpoint runs
+        # timesteps_since_update steps back to back, run_round zeroes _burst_i)
+        burst = int(ag.timesteps_since_update)
+        self._train_pin = self.burst_prefetch and self._burst_i > 0
+        self._train_pout = self.burst_prefetch and self._burst_i + 1 < burst
+        if self._train_pin:
+            self._bslot ^= 1
         # both policy-update parities run eagerly once before their capture
         if not self.use_graphs or self._train_iters < max(2, self.warmup_eager):
             self._eager(update_actor, rollout=False)
@@ -1004,6 +1029,8 @@ class RefScheduleTrainer(VecTrainer):
         else:
             self._replay(update_actor, rollout=False)
         L.prefetch_actor = False
+        self._burst_i += 1
+        self._train_pin = self._train_pout = False
         if L.maybe_update_targets():
             ag.replay_buffer.reset_max_priority()
             ag.sync.max_(ag.replay_buffer._maxp)
@@ -1035,6 +1062,7 @@ class RefScheduleTrainer(VecTrainer):
         ep_return = float(np.mean(self.score.cpu().numpy()))
         ep_timesteps = round(np.mean(self.ep_len))
         before, refreshed = L.training_steps, ag.checkpoint_refreshes
+        self._burst_i = 0
         ag.maybe_train_and_checkpoint(ep_timesteps, ep_return, train=self.train_step)
         burst = L.training_steps - before
         self.updates += burst
