@@ -8,9 +8,13 @@ One bench "step" (mode train, default) = one vectorised env step of all envs
 one TD7 train() grad step at batch 8 strata x 128 = 1024 -- the reference's
 ratio of one grad step per episode-round env step
 (Simulation/Exoskeleton_agent_train.py:208 trains round(mean(ep_len)) steps
-per round of max(ep_len) env steps).  Episodes are synchronous like the
-reference script: all envs reset together, done envs idle until the longest
-motion (344 steps) ends.  `value` counts ACTIVE env-steps only.
+per round of max(ep_len) env steps).  Episodes (r04): async by default --
+each env resets in place when its own episode ends, inside the timed
+iterations, so every launch steps every env (`--episodes sync`: the
+reference script's synchronous rounds, all envs reset together and done envs
+idle until the longest motion, 344 steps, ends; reported beside the async
+line as `sync_rounds`).  `value` counts ACTIVE env-steps only, over the timed
+window's wall time.
 
 mode env: the env alone (random actions), for the sim-kernel roofline.
 
