@@ -883,13 +883,24 @@ __global__ __launch_bounds__(256) void lap_sample_gather_kernel(const float *tre
 // s * batch + b of call *counter, as lap_sample_gather_kernel) descend with
 // the nodes below TOPN read from LDS, and the workgroup gathers their rows.
 // The same sums and comparisons: bit-identical to the two launches.
+// TdPrio (lap_update_sample_td): the priorities computed here from the critic
+// pass's |td| of both heads, prio = max(|td0|, |td1|, min_priority)^alpha
+// (TD7_multi_agent.py:259, the expression td7f_wgrad evaluates), so the update
+// need not wait for the weight-gradient launch; written to `out` if non-null.
+struct TdPrio {
+    const float *td;  // [B][2]; nullptr: the priorities are given (prio)
+    float alpha, minp;
+    float *out;
+};
+
 __global__ __launch_bounds__(UPD_THREADS) void lap_update_sample_kernel(float *tree, float *maxp, int cap, int levels,
                                                                         int capacity, const int32_t *idx_in,
                                                                         const float *prio, int batch,
                                                                         const int32_t *size, lap_storage_desc st,
                                                                         SampleRng rng, int32_t *idx_out,
                                                                         float *o_state, float *o_action, float *o_next,
-                                                                        float *o_reward, float *o_not_done) {
+                                                                        float *o_reward, float *o_not_done,
+                                                                        TdPrio tp) {
     const int s = blockIdx.x;
     float *T = stratum_tree(tree, s, cap);
     const int32_t *I = idx_in + (size_t)s * batch;
@@ -911,8 +922,16 @@ __global__ __launch_bounds__(UPD_THREADS) void lap_update_sample_kernel(float *t
             bool last = true;
             for (int k = threadIdx.x + 1; k < nb; ++k) last &= (li[k] != me);
             for (int b2 = b0 + nb; b2 < batch; ++b2) last &= (I[b2] != me);
-            if (last) T[cap + me] = P[b];
-            mx = fmaxf(mx, P[b]);
+            float pb;
+            if (tp.td) {
+                const long d = (long)s * batch + b;
+                pb = powf(fmaxf(fmaxf(tp.td[2 * d], tp.td[2 * d + 1]), tp.minp), tp.alpha);
+                if (tp.out) tp.out[d] = pb;
+            } else {
+                pb = P[b];
+            }
+            if (last) T[cap + me] = pb;
+            mx = fmaxf(mx, pb);
         }
     }
     for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
@@ -1210,7 +1229,22 @@ int lap_update_sample_rng(const lap_tree_desc *t, const lap_storage_desc *st, co
     hipLaunchKernelGGL(lap_update_sample_kernel, dim3(t->n_strata), dim3(UPD_THREADS), 0, (hipStream_t)stream,
                        t->tree, t->max_priority, t->cap, levels_of(t), t->capacity, idx_in, prio, batch, st->size,
                        *st, SampleRng{seed, tag, counter, ticket}, idx_out, out_state, out_action, out_next_state,
-                       out_reward, out_not_done);
+                       out_reward, out_not_done, TdPrio{nullptr, 0.f, 0.f, nullptr});
+    return rc(hipGetLastError());
+}
+
+int lap_update_sample_td(const lap_tree_desc *t, const lap_storage_desc *st, const int32_t *idx_in, const float *td,
+                         float alpha, float min_priority, float *prio_out, int32_t batch, uint64_t seed, uint32_t tag,
+                         unsigned long long *counter, uint32_t *ticket, int32_t *idx_out, float *out_state,
+                         float *out_action, float *out_next_state, float *out_reward, float *out_not_done,
+                         void *stream) {
+    if (!valid(t) || !st || !st->size || !idx_in || !td || !counter || !ticket || !idx_out || batch <= 0 ||
+        batch > UPD_THREADS || !out_state || !out_action || !out_next_state || !out_reward || !out_not_done)
+        return EXO_EINVAL;
+    hipLaunchKernelGGL(lap_update_sample_kernel, dim3(t->n_strata), dim3(UPD_THREADS), 0, (hipStream_t)stream,
+                       t->tree, t->max_priority, t->cap, levels_of(t), t->capacity, idx_in, (const float *)nullptr,
+                       batch, st->size, *st, SampleRng{seed, tag, counter, ticket}, idx_out, out_state, out_action,
+                       out_next_state, out_reward, out_not_done, TdPrio{td, alpha, min_priority, prio_out});
     return rc(hipGetLastError());
 }
 

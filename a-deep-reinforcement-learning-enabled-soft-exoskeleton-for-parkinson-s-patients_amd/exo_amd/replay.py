@@ -283,6 +283,22 @@ class LAP:
         self.ind = idx
         return batch
 
+    def update_priority_and_sample_td(self, td, alpha, min_priority, ind, slot, prio_out=None):
+        """update_priority_and_sample with the priorities computed in the launch
+        from the critic pass's |td| [B, 2] (lap_update_sample_td): the same
+        values as td7f_wgrad's, so the update needs only the critic pass."""
+        if not (self.device_rng and self.batch_size <= 1024):
+            raise RuntimeError("update_priority_and_sample_td: the device RNG and batch <= 1024 only")
+        batch, idx = self._slot(slot)
+        r = self._rng
+        nat.check(nat.lib().lap_update_sample_td(ctypes.byref(self._desc), ctypes.byref(self._store), nat.ptr(ind),
+                                                 nat.ptr(td), float(alpha), float(min_priority), nat.ptr(prio_out),
+                                                 ind.shape[1], r.seed, r.tag, r.counter_ptr, r.ticket_ptr,
+                                                 nat.ptr(idx), *[nat.ptr(t) for t in batch], self._stream()),
+                  "lap_update_sample_td")
+        self.ind = idx
+        return batch
+
     def reset_max_priority(self):
         nat.check(nat.lib().lap_reset_max(ctypes.byref(self._desc), self._stream()), "lap_reset_max")
 

@@ -395,21 +395,27 @@ class VecTrainer:
         if getattr(self, "_rollout_stream", None) is None:
             self._rollout_stream = torch.cuda.Stream(device=self.device)
         br = self._rollout_stream
-        if self.td7_first:
-            # the same dependencies, the TD7 passes captured (and so dispatched)
-            # before the rollout branch: select_action's workgroups fill every
-            # CU, launched first they hold the update's first passes back
-            fork = torch.cuda.Event()
-            fork.record(cur)
-            self._prio = ag.learner.phase_grads(*self._batch)
-            br.wait_event(fork)
-            with torch.cuda.stream(br):
-                self._rollout()
-        else:
-            br.wait_stream(cur)
-            with torch.cuda.stream(br):
-                self._rollout()
-            self._prio = ag.learner.phase_grads(*self._batch)
+        br.wait_stream(cur)
+        with torch.cuda.stream(br):
+            self._rollout()
+        self._us_done = False
+        if self._us_after_critic():
+            # the priority update + next sample on its branch as soon as the
+            # critic pass has written |td| (beside the weight gradients and the
+            # optimiser steps); it also needs this iteration's inserts
+            def fork(td, cur=cur, br=br):
+                L = ag.learner
+                ps = self._prio_stream_get()
+                ps.wait_stream(cur)
+                ps.wait_stream(br)
+                with torch.cuda.stream(ps):
+                    ag.replay_buffer.update_priority_and_sample_td(td, L.hp.alpha, L.hp.min_priority, self._ind,
+                                                                   1 - self._cur)
+                self._pside = ps
+                self._us_done = True
+            ag.learner.after_critic = fork
+        self._prio = ag.learner.phase_grads(*self._batch)
+        ag.learner.after_critic = None
         cur.wait_stream(br)
 
     # LAP.update_priority reads only the sampled indices and the new priorities
@@ -425,33 +431,40 @@ class VecTrainer:
     # with no cross-queue hand-off on the critical path (EXO_PRIO_BRANCH_ALL=1:
     # the branch in every iteration, the r02 layout)
     prio_branch_all = os.environ.get("EXO_PRIO_BRANCH_ALL", "0") == "1"
-    # capture order (r04, measured, off): EXO_TD7_FIRST (TD7 passes captured
-    # before the rollout branch: 0.324 vs 0.305 ms) / EXO_ACTOR_FIRST (actor
-    # passes before the priority branch: 0.303 vs 0.305, noise) --
-    # profiles/r04h_raw
-    td7_first = os.environ.get("EXO_TD7_FIRST", "0") == "1"
-    actor_first = os.environ.get("EXO_ACTOR_FIRST", "0") == "1"
+
+    # r04: the priority update + next sample from the critic pass's |td|
+    # (LAP.update_priority_and_sample_td) right after the critic pass, on its
+    # branch, instead of after the weight-gradient launch; one GPU, prefetching
+    # trainer only.  EXO_US_AFTER_CRITIC=0: after the weight gradients.
+    us_after_critic = os.environ.get("EXO_US_AFTER_CRITIC", "1") == "1"
+    _us_done = False
+
+    def _us_after_critic(self):
+        L = self.agent.learner
+        rb = self.agent.replay_buffer
+        return (self.us_after_critic and not self.dp and self._prefetching() and not self._pre_out
+                and L.fused is not None and rb.device_rng and rb.batch_size <= 1024)
+
+    def _prio_stream_get(self):
+        if getattr(self, "_prio_stream", None) is None:
+            self._prio_stream = torch.cuda.Stream(device=self.device)
+        return self._prio_stream
 
     def _mid(self, update_actor, flat_grad=None, grad_scale=1.0, rollout=True):
         ag = self.agent
-        self._pside = None
         self._mid_rollout = rollout
+        if self._us_done:  # the priority update already runs on its branch (_pre)
+            self._us_done = False
+            ag.learner.phase_steps(flat_grad, grad_scale)
+            if update_actor:
+                ag.learner.phase_actor_grads(self._batch[0], self._batch[1])
+            return
+        self._pside = None
         if self.prio_branch and not self.dp and (update_actor or self.prio_branch_all):
             cur = torch.cuda.current_stream(self.device)
             if getattr(self, "_prio_stream", None) is None:
                 self._prio_stream = torch.cuda.Stream(device=self.device)
             self._pside = self._prio_stream
-            if self.actor_first and update_actor:
-                # the same dependencies, the actor's passes captured before the
-                # priority branch (the graph's queues then take them first)
-                fork = torch.cuda.Event()
-                fork.record(cur)
-                ag.learner.phase_steps(flat_grad, grad_scale)
-                ag.learner.phase_actor_grads(self._batch[0], self._batch[1])
-                self._pside.wait_event(fork)
-                with torch.cuda.stream(self._pside):
-                    self._update_and_sample_next()
-                return
             self._pside.wait_stream(cur)
             with torch.cuda.stream(self._pside):
                 self._update_and_sample_next()

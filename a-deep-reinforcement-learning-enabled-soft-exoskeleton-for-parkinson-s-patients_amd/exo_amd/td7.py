@@ -894,6 +894,9 @@ class TD7Learner:
             if branch:
                 cur.wait_stream(tside)
         tr.critic(state, action, zs, zsa, qt, reward, not_done)
+        hook, self.after_critic = self.after_critic, None
+        if hook is not None:  # the trainer's priority update, from |td| (VecTrainer._fork_update_sample)
+            hook(tr.td)
         if enc_step:
             priority = tr.wgrad_critic(adam=wg_adam)
             self._enc_step_pending = True
@@ -944,6 +947,7 @@ class TD7Learner:
     # refresh (the trainer does not prefetch before one; the refresh drops any
     # prefetched slot), and Agent.train()'s own updates drop them too.
     pre_in = None  # slot whose prefetched inputs the next phase_grads reads (set by the trainer)
+    after_critic = None  # called with the critic pass's |td| right after it (set by the trainer)
 
     def _pre_slot(self, slot, B):
         bufs = getattr(self, "_pre_bufs", None)

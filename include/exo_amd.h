@@ -385,6 +385,19 @@ int lap_update_sample_rng(const lap_tree_desc *t, const lap_storage_desc *st, co
                           unsigned long long *counter_dev, uint32_t *ticket_dev, int32_t *idx_dev, float *out_state,
                           float *out_action, float *out_next_state, float *out_reward, float *out_not_done,
                           void *stream);
+
+/* lap_update_sample_rng with the priorities computed in the launch from the
+ * critic pass's |td| of both heads (td [B][2], B = n_strata x batch):
+ * prio = max(|td0|, |td1|, min_priority)^alpha (TD7_multi_agent.py:259, the
+ * expression td7f_wgrad writes), also stored in prio_out if non-NULL -- the
+ * priority update then depends on the critic pass only, not on the weight
+ * gradients that follow it.  Bit-identical to td7f_wgrad's priorities +
+ * lap_update_sample_rng. */
+int lap_update_sample_td(const lap_tree_desc *t, const lap_storage_desc *st, const int32_t *idx_in, const float *td,
+                         float alpha, float min_priority, float *prio_out, int32_t batch, uint64_t seed, uint32_t tag,
+                         unsigned long long *counter, uint32_t *ticket, int32_t *idx_out, float *out_state,
+                         float *out_action, float *out_next_state, float *out_reward, float *out_not_done,
+                         void *stream);
 /* lap_sample_gather with the uniforms drawn inside the kernel (Philox4x32-10,
  * key seed, counter words (draw index, call, tag)); *counter_dev (the call
  * number) advances by one per launch, ticket_dev: one uint32, zero at the first

@@ -58,16 +58,3 @@ def test_agent_train_drops_prefetched_inputs(monkeypatch):
     tr.step()
     torch.cuda.synchronize()
     assert all(torch.isfinite(p).all() for p in L.critic.parameters())
-
-
-@pytest.mark.parametrize("order", ["td7_first", "actor_first"])
-def test_capture_order_does_not_change_training(monkeypatch, order):
-    """EXO_TD7_FIRST / EXO_ACTOR_FIRST capture the same dependencies in another
-    order (which the graph's queues take first): the same weights bit for bit."""
-    from exo_amd.rollout import VecTrainer
-    _, w_ref = _run(False, 12, monkeypatch)
-    monkeypatch.setattr(VecTrainer, order, True)
-    _, w = _run(False, 12, monkeypatch)
-    for n in w_ref:
-        for a, b in zip(w_ref[n], w[n]):
-            torch.testing.assert_close(a, b, rtol=0, atol=0)

@@ -71,3 +71,24 @@ def test_fused_priority_update_and_next_sample_does_not_change_training(monkeypa
         outs.append((_params(a), a.replay_buffer._tree.clone()))
     _assert_same(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
+
+
+def test_priority_update_after_the_critic_pass_does_not_change_training(monkeypatch):
+    """LAP.update_priority_and_sample_td forked right after the critic pass
+    (priorities from its |td|, r04) against the update after the weight-
+    gradient launch (td7f_wgrad's priorities): the same weights, replay trees
+    and batches bit for bit."""
+    import exo_amd.rollout as rollout
+    monkeypatch.setattr(rollout.VecTrainer, "us_after_critic", False)
+    t1, a1 = _make(seed=9)
+    for _ in range(10):
+        t1.step()
+    torch.cuda.synchronize()
+    ref, tree_ref = _params(a1), a1.replay_buffer._tree.clone()
+    monkeypatch.setattr(rollout.VecTrainer, "us_after_critic", True)
+    t2, a2 = _make(seed=9)
+    for _ in range(10):
+        t2.step()
+    torch.cuda.synchronize()
+    _assert_same(_params(a2), ref)
+    assert torch.equal(a2.replay_buffer._tree, tree_ref)
