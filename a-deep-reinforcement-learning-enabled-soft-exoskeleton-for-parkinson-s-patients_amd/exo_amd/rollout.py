@@ -435,8 +435,8 @@ class VecTrainer:
     # r04: the priority update + next sample from the critic pass's |td|
     # (LAP.update_priority_and_sample_td) right after the critic pass, on its
     # branch, instead of after the weight-gradient launch; one GPU, prefetching
-    # trainer only.  EXO_US_AFTER_CRITIC=0: after the weight gradients.
-    us_after_critic = os.environ.get("EXO_US_AFTER_CRITIC", "1") == "1"
+    # trainer only.  Off until measured (EXO_US_AFTER_CRITIC=1: on).
+    us_after_critic = os.environ.get("EXO_US_AFTER_CRITIC", "0") == "1"
     _us_done = False
 
     def _us_after_critic(self):
@@ -844,8 +844,8 @@ class RefScheduleTrainer(VecTrainer):
         # r04: that advance inside the replay insert's launch (its last
         # workgroup out); EXO_REF_INSERT_ADVANCE=0: its own launch
         self.insert_advance = os.environ.get("EXO_REF_INSERT_ADVANCE", "1") == "1"
-        # the burst steps' next-batch prefetch (VecTrainer._key); EXO_BURST_PREFETCH=0: off
-        self.burst_prefetch = os.environ.get("EXO_BURST_PREFETCH", "1") == "1"
+        # the burst steps' next-batch prefetch (VecTrainer._key); off until measured (EXO_BURST_PREFETCH=1)
+        self.burst_prefetch = os.environ.get("EXO_BURST_PREFETCH", "0") == "1"
         self._burst_i = 0
         # the script's per-step tremor statistics (:149-205: exo_tremor_metrics
         # into a [round_len, N, 16] device record + per-env counters, 2
