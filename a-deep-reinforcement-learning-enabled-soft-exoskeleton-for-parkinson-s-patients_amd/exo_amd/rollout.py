@@ -560,8 +560,11 @@ class VecTrainer:
         self._join_prio()
 
     def _key(self, update_actor, rollout):
-        return ((update_actor, self._cur, self._pre_in, self._pre_out) if rollout
-                else ("train", update_actor, self._train_pin, self._train_pout, self._bslot))
+        if rollout:
+            return update_actor, self._cur, self._pre_in, self._pre_out
+        if self._train_pin or self._train_pout:
+            return "train", update_actor, self._train_pin, self._train_pout, self._bslot
+        return "train", update_actor
 
     # burst steps (RefScheduleTrainer.train_step): the next step's batch sampled
     # at the end of the current one, into the other of two slots, when the

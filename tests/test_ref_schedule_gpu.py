@@ -277,3 +277,33 @@ def test_fused_score_matches_torch_where_add():
     for x, y in zip(outs[0][0], outs[1][0]):
         torch.testing.assert_close(x, y, rtol=0, atol=0)
     assert outs[0][1] == outs[1][1]
+
+
+def test_burst_prefetch_is_bit_identical(monkeypatch):
+    """RefScheduleTrainer.burst_prefetch (r04): each burst step samples the
+    next step's batch at its end (update + sample in one launch) -- the same
+    launches in the same order as sampling at the start of every step: the
+    nets, trees, replay and decision trace bit for bit."""
+    from exo_amd import VecExoskeletonEnv
+    from exo_amd.rollout import RefScheduleTrainer
+    from exo_amd.td7 import Agent
+    out = []
+    for on in ("0", "1"):
+        monkeypatch.setenv("EXO_BURST_PREFETCH", on)
+        torch.manual_seed(0)
+        env = VecExoskeletonEnv(64, seed=5)
+        agent = Agent(80, 7, 1, learning_steps=100000, env_num=E, buffer_size=2 * BUF, precision="bf16", n_envs=64)
+        tr = RefScheduleTrainer(env, agent, warmup=1)
+        for _ in range(3):
+            tr.run_round()
+        torch.cuda.synchronize()
+        L = agent.learner
+        out.append(([p.detach().clone() for m in (L.actor, L.critic, L.encoder) for p in m.parameters()],
+                    agent.replay_buffer._tree.clone(), [dict(t) for t in tr.trace], tr))
+    (w0, t0, d0, tr0), (w1, t1, d1, tr1) = out
+    for a, b in zip(w0, w1):
+        torch.testing.assert_close(b, a, rtol=0, atol=0)
+    torch.testing.assert_close(t1, t0, rtol=0, atol=0)
+    assert d0 == d1
+    assert any(len(k) == 5 for k in tr1.graphs if k[0] == "train")
+    assert not any(len(k) == 5 for k in tr0.graphs if k[0] == "train")
