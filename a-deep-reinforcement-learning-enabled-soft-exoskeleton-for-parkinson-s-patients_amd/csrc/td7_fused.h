@@ -48,12 +48,24 @@ constexpr int NTH = 64 * NW * NKG;  // threads per workgroup (2 waves per SIMD)
 constexpr int PD = TD7F_PD;    // k-steps of weight loads in flight per wave (k-steps are padded to multiples)
 constexpr int TR = 16;         // rows of one MFMA row tile
 
-enum Prec : int { PREC_BF16 = 1, PREC_F16 = 2 };
+enum Prec : int { PREC_BF16 = 1, PREC_F16 = 2, PREC_F32 = 3 };
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_ELU = 2, ACT_TANH = 3 };
 
+// The MFMA operand type.  Every operand -- a packed weight block, a k-step of
+// an LDS image row, a weight-gradient fragment -- is 16 bytes per lane and 64
+// bytes per row per k-step whatever the type: 32 16-bit values (one
+// v_mfma_f32_16x16x32_{bf16,f16}) or 16 fp32 values (SUB = 4 chained
+// v_mfma_f32_16x16x4_f32, lane l's k = 4 (l >> 4) + j in sub-step j: the same
+// k-permutation on both operands, so the sum is over the same 16 products).
+// Image geometry is kept in 16-bit units (R16.ld), an fp32 element being two
+// of them, so the GEMM core and the LDS layout code are shared.
 template <int P> struct Ty;
-template <> struct Ty<PREC_BF16> {
-    static __device__ __forceinline__ floatx4 mfma(u32x4 a, u32x4 b, floatx4 c) {
+struct Ty16 {
+    using E = uint16_t;
+    static constexpr int EB = 2, KD = 32, SUB = 1;
+};
+template <> struct Ty<PREC_BF16> : Ty16 {
+    static __device__ __forceinline__ floatx4 mfma(u32x4 a, u32x4 b, floatx4 c, int = 0) {
         return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
                                                        c, 0, 0, 0);
     }
@@ -62,8 +74,8 @@ template <> struct Ty<PREC_BF16> {
     // gradient operands are rounded unscaled (bf16 has fp32's exponent range)
     static constexpr float gs = 1.f;
 };
-template <> struct Ty<PREC_F16> {
-    static __device__ __forceinline__ floatx4 mfma(u32x4 a, u32x4 b, floatx4 c) {
+template <> struct Ty<PREC_F16> : Ty16 {
+    static __device__ __forceinline__ floatx4 mfma(u32x4 a, u32x4 b, floatx4 c, int = 0) {
         return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(halfx8, a), __builtin_bit_cast(halfx8, b), c,
                                                       0, 0, 0);
     }
@@ -73,6 +85,19 @@ template <> struct Ty<PREC_F16> {
     // td7_dense convention, td7_dense_kernels.h grad_scale) and the
     // accumulators by 2^-10 after: exact, keeps ~1e-6 gradients normal
     static constexpr float gs = 1024.f;
+};
+// fp32 operands (the reference's precision, Agent/TD7_multi_agent.py:211-293):
+// exact products, fp32 accumulation; sub-step j of a 16-deep k-step
+template <> struct Ty<PREC_F32> {
+    using E = float;
+    static constexpr int EB = 4, KD = 16, SUB = 4;
+    static __device__ __forceinline__ floatx4 mfma(u32x4 a, u32x4 b, floatx4 c, int j) {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(__builtin_bit_cast(float, a[j]), __builtin_bit_cast(float, b[j]), c,
+                                                    0, 0, 0);
+    }
+    static __device__ __forceinline__ float bits(float v) { return v; }
+    static __device__ __forceinline__ float val(float b) { return b; }
+    static constexpr float gs = 1.f;
 };
 
 // ELU's negative branch as exp(x) - 1 (v_exp_f32): within ~1e-7 of expm1f,
@@ -222,11 +247,13 @@ __device__ __forceinline__ void gemm(char *lds, int a_off, int lda, const GDesc 
                     an[r] = *(const u32x4 *)(ap + (r * TR * lda + 32 * (s + 1)) * 2);
                 }
 #pragma unroll
-                for (int i = 0; i < TH; ++i) {
+                for (int j = 0; j < Ty<P>::SUB; ++j)
 #pragma unroll
-                    for (int r = 0; r < RT; ++r) acc[r][i] = Ty<P>::mfma(R[p][i], x[r], acc[r][i]);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
+                    for (int i = 0; i < TH; ++i) {
+#pragma unroll
+                        for (int r = 0; r < RT; ++r) acc[r][i] = Ty<P>::mfma(R[p][i], x[r], acc[r][i], j);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
 #pragma unroll
                 for (int i = 0; i < TH; ++i) {
                     R[p][i] = ldg(bp[i] + (s + PD) * 64);
@@ -248,11 +275,13 @@ __device__ __forceinline__ void gemm(char *lds, int a_off, int lda, const GDesc 
                 if (p + 1 < PD) an[r] = *(const u32x4 *)(ap + (r * TR * lda + 32 * (s + 1)) * 2);
             }
 #pragma unroll
-            for (int i = 0; i < TH; ++i) {
+            for (int j = 0; j < Ty<P>::SUB; ++j)
 #pragma unroll
-                for (int r = 0; r < RT; ++r) acc[r][i] = Ty<P>::mfma(R[p][i], x[r], acc[r][i]);
-                __builtin_amdgcn_sched_barrier(0);
-            }
+                for (int i = 0; i < TH; ++i) {
+#pragma unroll
+                    for (int r = 0; r < RT; ++r) acc[r][i] = Ty<P>::mfma(R[p][i], x[r], acc[r][i], j);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
             if (ne > nb) {
 #pragma unroll
                 for (int i = 0; i < TH; ++i) {
@@ -314,6 +343,17 @@ __device__ __forceinline__ u32x2 pack4(const float (&v)[4]) {
     return u32x2{(uint32_t)Ty<P>::bits(v[0]) | ((uint32_t)Ty<P>::bits(v[1]) << 16),
                  (uint32_t)Ty<P>::bits(v[2]) | ((uint32_t)Ty<P>::bits(v[3]) << 16)};
 }
+// element `col` of row `row` of an operand image (R16.ld in 16-bit units)
+template <int P>
+__device__ __forceinline__ typename Ty<P>::E *pe(char *lds, R16 r, int row, int col) {
+    return (typename Ty<P>::E *)(lds + r.off + row * r.ld * 2) + col;
+}
+// 4 consecutive elements (col % 4 == 0): one 8-byte (16-bit) or 16-byte (fp32) LDS store
+template <int P>
+__device__ __forceinline__ void put4(char *lds, R16 r, int row, int col, const float (&v)[4]) {
+    if constexpr (Ty<P>::EB == 4) *(floatx4 *)pe<P>(lds, r, row, col) = floatx4{v[0], v[1], v[2], v[3]};
+    else *(u32x2 *)pe<P>(lds, r, row, col) = pack4<P>(v);
+}
 
 // Forward epilogue of an MFMA layer (N % 4 == 0): v = act(acc + b) for the
 // owned columns n < N, written to any of: 16-bit LDS image (column col0 + n),
@@ -334,7 +374,7 @@ __device__ __forceinline__ void epi_fwd(char *lds, const floatx4 (&acc)[RT][TH],
             float v[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = act_fwd(act, acc[r][i][e] + b[e]);
-            if (o16.off >= 0) *(u32x2 *)p16(lds, o16, row, col0 + n) = pack4<P>(v);
+            if (o16.off >= 0) put4<P>(lds, o16, row, col0 + n, v);
             if (o32.off >= 0) *(floatx4 *)p32(lds, o32, row, n) = floatx4{v[0], v[1], v[2], v[3]};
             if (g && row0 + row < nrows) stg((floatx4 *)(g + (long)(row0 + row) * gld + n), floatx4{v[0], v[1], v[2], v[3]});
         }
@@ -377,7 +417,7 @@ __device__ __forceinline__ void epi_bwd(char *lds, const floatx4 (&acc)[RT][TH],
                 if (o32.off >= 0) *(floatx4 *)p32(lds, o32, row, m) = floatx4{v[0], v[1], v[2], v[3]};
                 if (o16.off >= 0) {
                     float s[4] = {v[0] * Ty<P>::gs, v[1] * Ty<P>::gs, v[2] * Ty<P>::gs, v[3] * Ty<P>::gs};
-                    *(u32x2 *)p16(lds, o16, row, m) = pack4<P>(s);
+                    put4<P>(lds, o16, row, m, s);
                 }
                 if (g && row0 + row < nrows) stg((floatx4 *)(g + (long)(row0 + row) * gld + m), floatx4{v[0], v[1], v[2], v[3]});
             }
@@ -394,23 +434,8 @@ __device__ __forceinline__ void epi_bwd(char *lds, const floatx4 (&acc)[RT][TH],
 
 // Thin GEMMs on the VALU (an output width or a reduction too narrow for a
 // 16-wide MFMA tile: the N = 1 / 7 heads, the 7-wide action windows of the
-// backward).  stage_thin copies the ncols x K weight slice w(j, k) =
-// W[(j0 + j) * ldw + k] (trans = false) or W[k * ldw + j0 + j] (trans = true)
-// of the fp32 master weights into the LDS region wl [ncols][K], rounded to the
-// MFMA operand type (the operands the per-layer kernels use) -- at kernel start,
-// off the critical path (no barrier: the kernel's first one covers it).
-// rows j >= ncols of the region (up to nc_pad) are zero-filled (thin's NC).
-template <int P>
-__device__ __forceinline__ void stage_thin(char *lds, R32 wl, const float *W, long ldw, int j0, bool trans, int ncols,
-                                           int K, int nc_pad) {
-#pragma unroll 4
-    for (int idx = threadIdx.x; idx < nc_pad * K; idx += NTH) {
-        const int j = idx / K, k = idx - j * K;
-        float w = 0.f;
-        if (j < ncols) w = ldg(trans ? W + (long)k * ldw + j0 + j : W + (long)(j0 + j) * ldw + k);
-        *p32(lds, wl, j, k) = Ty<P>::val(Ty<P>::bits(w));
-    }
-}
+// backward), their weight slices staged in LDS at kernel start (thin_issue /
+// thin_put), rounded to the MFMA operand type.
 // out[row][j] = scale * sum_{k < K} X[row][xc0 + k] wl[j][k] for j < ncols <= NC
 // (raw sums to the fp32 LDS region out; wl holds NC rows, zero past ncols),
 // 16 rows: one pass, a thread per (row, k-slice of NTH / 16) accumulating all
@@ -425,7 +450,7 @@ __device__ __forceinline__ void thin(char *lds, R16 in, int xc0, int K, R32 wl, 
     for (int j = 0; j < NC; ++j) acc[j] = 0.f;
 #pragma unroll 2
     for (int k = sl; k < K; k += KS) {
-        const float x = Ty<P>::val(*p16(lds, in, row, xc0 + k));
+        const float x = Ty<P>::val(*pe<P>(lds, in, row, xc0 + k));
 #pragma unroll
         for (int j = 0; j < NC; ++j) acc[j] += x * *p32(lds, wl, j, k);
     }
@@ -455,60 +480,13 @@ __device__ __forceinline__ void make_dp(char *lds, R32 dy, int N, int act, const
             if (row0 + r >= nrows) v = 0.f;
             else if (act != ACT_NONE) v *= act_grad(act, ldg(y + (long)(row0 + r) * yld + n));
             *p32(lds, dy, r, n) = v;
-            *p16(lds, o16, r, n) = Ty<P>::bits(v * Ty<P>::gs);
+            *pe<P>(lds, o16, r, n) = Ty<P>::bits(v * Ty<P>::gs);
             cs += v;
         }
         if (part) stg(part + n, cs);
     }
 }
 
-// Rows of a global matrix into a 16-bit LDS image: dst[row][col0 + c] for
-// c < ncols from src[(row0+row) * sld + c] (fp32 or 16-bit), zero past nrows.
-template <int P>
-__device__ __forceinline__ void load_rows(char *lds, R16 dst, int col0, const float *src, long sld, int ncols,
-                                          int rows, int row0, int nrows) {
-    if (ncols % 4 == 0 && sld % 4 == 0 && col0 % 4 == 0) {  // 16-byte loads, 8-byte LDS stores
-        const int nq = ncols / 4;
-#pragma unroll 4
-        for (int k = threadIdx.x; k < rows * nq; k += NTH) {
-            const int row = k / nq, c = 4 * (k - row * nq);
-            const floatx4 v = (row0 + row < nrows) ? ldg((const floatx4 *)(src + (long)(row0 + row) * sld + c))
-                                                    : floatx4{0.f, 0.f, 0.f, 0.f};
-            const float f[4] = {v[0], v[1], v[2], v[3]};
-            *(u32x2 *)p16(lds, dst, row, col0 + c) = pack4<P>(f);
-        }
-        return;
-    }
-    for (int k = threadIdx.x; k < rows * ncols; k += NTH) {
-        const int row = k / ncols, c = k - row * ncols;
-        const float v = (row0 + row < nrows) ? ldg(src + (long)(row0 + row) * sld + c) : 0.f;
-        *p16(lds, dst, row, col0 + c) = Ty<P>::bits(v);
-    }
-}
-__device__ __forceinline__ void load_rows16(char *lds, R16 dst, int col0, const uint16_t *src, long sld, int ncols,
-                                            int rows, int row0, int nrows) {
-    if (ncols % 8 == 0 && sld % 8 == 0 && col0 % 8 == 0 && dst.ld % 8 == 0) {  // 16-byte loads and stores
-        const int nq = ncols / 8;
-        for (int k = threadIdx.x; k < rows * nq; k += NTH) {
-            const int row = k / nq, c = 8 * (k - row * nq);
-            *(u32x4 *)p16(lds, dst, row, col0 + c) = (row0 + row < nrows)
-                                                          ? ldg((const u32x4 *)(src + (long)(row0 + row) * sld + c))
-                                                          : u32x4{0u, 0u, 0u, 0u};
-        }
-        return;
-    }
-    for (int k = threadIdx.x; k < rows * ncols; k += NTH) {
-        const int row = k / ncols, c = k - row * ncols;
-        *p16(lds, dst, row, col0 + c) = (row0 + row < nrows) ? ldg(src + (long)(row0 + row) * sld + c) : (uint16_t)0;
-    }
-}
-__device__ __forceinline__ void load_rows32(char *lds, R32 dst, const float *src, long sld, int ncols, int rows,
-                                            int row0, int nrows) {
-    for (int k = threadIdx.x; k < rows * ncols; k += NTH) {
-        const int row = k / ncols, c = k - row * ncols;
-        *p32(lds, dst, row, c) = (row0 + row < nrows) ? ldg(src + (long)(row0 + row) * sld + c) : 0.f;
-    }
-}
 // 16-bit LDS image rows -> global [row0+row][c] (same element type)
 __device__ __forceinline__ void store_rows16(char *lds, R16 src, int col0, uint16_t *dst, long dld, int ncols,
                                              int rows, int row0, int nrows) {
@@ -552,7 +530,7 @@ __device__ __forceinline__ void row_put16(char *lds, const RowStage &s, R16 dst,
     if ((int)threadIdx.x < ncols)
 #pragma unroll
         for (int r = 0; r < TR; ++r)
-            *p16(lds, dst, r, col0 + threadIdx.x) = Ty<P>::bits(row0 + r < nrows ? s.v[r] * scale : 0.f);
+            *pe<P>(lds, dst, r, col0 + threadIdx.x) = Ty<P>::bits(row0 + r < nrows ? s.v[r] * scale : 0.f);
 }
 __device__ __forceinline__ void row_put32(char *lds, const RowStage &s, R32 dst, int ncols, int row0, int nrows) {
     if ((int)threadIdx.x < ncols)
@@ -610,14 +588,34 @@ __device__ __forceinline__ void thin_put(char *lds, const ThinStage<NC> &s, R32 
 // (16-bit units, ld = padded batch), so that td7f_wgrad's 16 x 32 fragment of a
 // k-step is one contiguous 1 KiB block (one full-line 16-byte load per lane).
 // blk8 -> the 8 batch rows r..r+7 (r % 8 == 0) of operand row c.
+// fp32 operands: k-steps of 16 batch rows, the 4 rows r..r+3 (r % 4 == 0) of
+// operand row c at blk4 (the same 1 KiB block per fragment, 16 bytes per lane).
 __device__ __forceinline__ uint16_t *blk8(uint16_t *base, long ld, int c, int r) {
     return base + ((long)(c >> 4) * (ld >> 5) + (r >> 5)) * 512 + ((c & 15) + 16 * ((r & 31) >> 3)) * 8;
+}
+__device__ __forceinline__ float *blk4(float *base, long ld, int c, int r) {
+    return base + ((long)(c >> 4) * (ld >> 4) + (r >> 4)) * 256 + ((c & 15) + 16 * ((r & 15) >> 2)) * 4;
 }
 
 // The layer input for the weight gradient from the LDS image (columns col0 + c,
 // c < ncols), 16 rows per call (row0 % 16 == 0), in the blocked layout above.
-__device__ __forceinline__ void save_xt(char *lds, R16 src, int col0, int ncols, uint16_t *xt, long ld, int rows,
+template <int P>
+__device__ __forceinline__ void save_xt(char *lds, R16 src, int col0, int ncols, void *xt_, long ld, int rows,
                                         int row0) {
+    if constexpr (P == PREC_F32) {  // a thread per (column, 16 rows): 4 x 16-byte stores
+        float *xt = (float *)xt_;
+        for (int k = threadIdx.x; k < ncols * (rows / TR); k += NTH) {
+            const int c = k % ncols, rb = (k / ncols) * TR;
+            float v[TR];
+#pragma unroll
+            for (int j = 0; j < TR; ++j) v[j] = *pe<P>(lds, src, rb + j, col0 + c);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                stg((floatx4 *)blk4(xt, ld, c, row0 + rb + 4 * q), floatx4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]});
+        }
+        return;
+    }
+    uint16_t *xt = (uint16_t *)xt_;
     if (col0 % 2 == 0 && src.ld % 2 == 0) {  // column pairs: 32-bit LDS reads
         for (int k = threadIdx.x; k < ((ncols + 1) / 2) * (rows / TR); k += NTH) {
             const int c = 2 * (k % ((ncols + 1) / 2)), rb = (k / ((ncols + 1) / 2)) * TR;
@@ -667,9 +665,9 @@ __device__ __forceinline__ void norm_fwd(char *lds, R32 h, int N, int rows, floa
     const float m = acc / N, s = fmaxf(m, eps);
     for (int n = j0; n < N; n += tpr) {
         const float v = *p32(lds, h, row, n) / s;
-        const uint16_t b = Ty<P>::bits(v);
-        if (o16.off >= 0) *p16(lds, o16, row, col0 + n) = b;
-        if (o16b.off >= 0) *p16(lds, o16b, row, col0b + n) = b;
+        const auto b = Ty<P>::bits(v);
+        if (o16.off >= 0) *pe<P>(lds, o16, row, col0 + n) = b;
+        if (o16b.off >= 0) *pe<P>(lds, o16b, row, col0b + n) = b;
         if (o32.off >= 0) *p32(lds, o32, row, n) = v;
         if (g && row0 + row < nrows) stg(g + (long)(row0 + row) * gld + n, v);
     }
@@ -685,7 +683,7 @@ __device__ __forceinline__ void norm_fwd(char *lds, R32 h, int N, int rows, floa
 // dP^T in HBM and the bias-gradient column partials.  16 rows.
 template <int P>
 __device__ __forceinline__ void norm_bwd(char *lds, R32 dy, R32 h, const float *mean, int N, float eps, float *dot,
-                                         R16 o16, uint16_t *dpt, long dpt_ld, float *part, int row0, int nrows) {
+                                         R16 o16, void *dpt, long dpt_ld, float *part, int row0, int nrows) {
     {
         constexpr int tpr = NTH / TR;
         const int row = threadIdx.x / tpr, j0 = threadIdx.x % tpr;
@@ -698,6 +696,7 @@ __device__ __forceinline__ void norm_bwd(char *lds, R32 dy, R32 h, const float *
     for (int n = threadIdx.x; n < N; n += NTH) {
         float csum = 0.f;
         uint32_t v[8];
+        float f[TR];
 #pragma unroll
         for (int r = 0; r < TR; ++r) {
             const float m = mean[r];
@@ -712,14 +711,24 @@ __device__ __forceinline__ void norm_bwd(char *lds, R32 dy, R32 h, const float *
             }
             if (row0 + r >= nrows) gx = 0.f;
             csum += gx;
-            const uint16_t hb = Ty<P>::bits(gx * Ty<P>::gs);
-            *p16(lds, o16, r, n) = hb;
-            if (r & 1) v[r >> 1] |= (uint32_t)hb << 16;
-            else v[r >> 1] = hb;
+            const auto hb = Ty<P>::bits(gx * Ty<P>::gs);
+            *pe<P>(lds, o16, r, n) = hb;
+            if constexpr (P == PREC_F32) {
+                f[r] = hb;
+            } else {
+                if (r & 1) v[r >> 1] |= (uint32_t)hb << 16;
+                else v[r >> 1] = hb;
+            }
         }
         if (dpt) {
-            stg((u32x4 *)blk8(dpt, dpt_ld, n, row0), u32x4{v[0], v[1], v[2], v[3]});
-            stg((u32x4 *)blk8(dpt, dpt_ld, n, row0 + 8), u32x4{v[4], v[5], v[6], v[7]});
+            if constexpr (P == PREC_F32) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    stg((floatx4 *)blk4((float *)dpt, dpt_ld, n, row0 + 4 * q), floatx4{f[4 * q], f[4 * q + 1], f[4 * q + 2], f[4 * q + 3]});
+            } else {
+                stg((u32x4 *)blk8((uint16_t *)dpt, dpt_ld, n, row0), u32x4{v[0], v[1], v[2], v[3]});
+                stg((u32x4 *)blk8((uint16_t *)dpt, dpt_ld, n, row0 + 8), u32x4{v[4], v[5], v[6], v[7]});
+            }
         }
         if (part) stg(part + n, csum);
     }
@@ -840,9 +849,9 @@ __device__ __forceinline__ void noise_rows(char *lds, R32 a, int A, int rows, in
             v = fminf(fmaxf(*p32(lds, a, row, c) + e, -1.0f), 1.0f) * nz.scale;
             if (out) stg(out + i, v);
         }
-        const uint16_t b = Ty<P>::bits(v);
-        if (o1.off >= 0) *p16(lds, o1, row, c1 + c) = b;
-        if (o2.off >= 0) *p16(lds, o2, row, c2 + c) = b;
+        const auto b = Ty<P>::bits(v);
+        if (o1.off >= 0) *pe<P>(lds, o1, row, c1 + c) = b;
+        if (o2.off >= 0) *pe<P>(lds, o2, row, c2 + c) = b;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -857,9 +866,12 @@ __device__ __forceinline__ void noise_rows(char *lds, R32 a, int A, int rows, in
 
 // ---------------------------------------------------------------- host helpers
 inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
-inline int ks_of(int k) { return round_up((k + 31) / 32, PD); }
-// 16-bit operand image of an n-wide input: every k-step the gemm reads, +16 (bank spread)
-inline int ld16(int n) { return ks_of(n) * 32 + 16; }
+// k per k-step of the operand type (Ty<P>::KD)
+inline int kd_of(int prec) { return prec == PREC_F32 ? 16 : 32; }
+inline int ks_of(int k, int kd = 32) { return round_up((k + kd - 1) / kd, PD); }
+// operand image of an n-wide input in 16-bit units (64 bytes per k-step the
+// gemm reads, +32 bytes of bank spread)
+inline int ld16(int n, int kd = 32) { return ks_of(n, kd) * 32 + 16; }
 
 struct Bump {
     int off;
@@ -914,10 +926,12 @@ int launch(K kernel, dim3 grid, int lds, A args, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 
-#define DISPATCH(PREC, TH, KERNEL, ...)                                                       \
-    ((PREC) == PREC_BF16 ? ((TH) == 5 ? launch(KERNEL<PREC_BF16, 5>, __VA_ARGS__)             \
-                                      : launch(KERNEL<PREC_BF16, 4>, __VA_ARGS__))            \
-                         : ((TH) == 5 ? launch(KERNEL<PREC_F16, 5>, __VA_ARGS__)              \
-                                      : launch(KERNEL<PREC_F16, 4>, __VA_ARGS__)))
+#define DISPATCH(PREC, TH, KERNEL, ...)                                                                 \
+    ((PREC) == PREC_BF16  ? ((TH) == 5 ? launch(KERNEL<PREC_BF16, 5>, __VA_ARGS__)                      \
+                                       : launch(KERNEL<PREC_BF16, 4>, __VA_ARGS__))                     \
+     : (PREC) == PREC_F16 ? ((TH) == 5 ? launch(KERNEL<PREC_F16, 5>, __VA_ARGS__)                       \
+                                       : launch(KERNEL<PREC_F16, 4>, __VA_ARGS__))                      \
+                          : ((TH) == 5 ? launch(KERNEL<PREC_F32, 5>, __VA_ARGS__)                       \
+                                       : launch(KERNEL<PREC_F32, 4>, __VA_ARGS__)))
 
 }  // namespace td7f

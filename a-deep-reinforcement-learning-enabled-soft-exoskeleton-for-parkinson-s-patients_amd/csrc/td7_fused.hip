@@ -47,9 +47,45 @@ __device__ __forceinline__ float w_at(const PackJob &J, int n, int c) {
     const float x = ldg(J.w + (long)(ok ? n : 0) * J.ld + (ok ? c : 0));
     return ok ? x : 0.f;
 }
+// fp32 (Ty<PREC_F32>: 16-deep k-steps): a forward item is 4 consecutive inputs
+// W[16t + (l&15)][16s + 4(l>>4) + j], a dX item W[16s + 4(l>>4) + j][16t + (l&15)], j < 4
+__device__ __forceinline__ void pack_item_f32(const PackJob &J, long k, long nf, bool vec) {
+    const int l = (int)(k & 63);
+    float x[4];
+    u32x4 *dst;
+    if (k < nf) {
+        const long blk = k >> 6;
+        const int t = (int)(blk / J.ksf), s = (int)(blk % J.ksf);
+        const int n = 16 * t + (l & 15), k0 = 16 * s + 4 * (l >> 4);
+        if (vec && n < J.N && k0 + 4 <= J.K) {
+            const floatx4 a0 = ldg((const floatx4 *)(J.w + (long)n * J.ld + k0));
+            x[0] = a0[0], x[1] = a0[1], x[2] = a0[2], x[3] = a0[3];
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) x[j] = w_at<PREC_F32>(J, n, k0 + j);
+        }
+        dst = J.wf + k;
+    } else {
+        const long blk = (k - nf) >> 6;
+        const int t = (int)(blk / J.ksb), s = (int)(blk % J.ksb);
+        const int c = 16 * t + (l & 15), n0 = 16 * s + 4 * (l >> 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[j] = w_at<PREC_F32>(J, n0 + j, c);
+        dst = J.wb + (k - nf);
+    }
+    stg(dst, __builtin_bit_cast(u32x4, floatx4{x[0], x[1], x[2], x[3]}));
+}
+
 template <int P>
 __global__ __launch_bounds__(256) void pack_kernel(PackArgs a) {
     const PackJob J = a.j[blockIdx.y];
+    if constexpr (P == PREC_F32) {
+        const long nf = (long)J.ntf * J.ksf * 64, total = nf + (long)J.ntb * J.ksb * 64;
+        const bool vec = (J.ld % 4) == 0 && (reinterpret_cast<uintptr_t>(J.w) & 15) == 0;
+        for (long k = (long)blockIdx.x * 256 + threadIdx.x; k < total; k += (long)gridDim.x * 256)
+            pack_item_f32(J, k, nf, vec);
+        return;
+    }
     const long nf = (long)J.ntf * J.ksf * 64, total = nf + (long)J.ntb * J.ksb * 64;
     const bool vec = (J.ld % 4) == 0 && (reinterpret_cast<uintptr_t>(J.w) & 15) == 0;
     for (long k = (long)blockIdx.x * 256 + threadIdx.x; k < total; k += (long)gridDim.x * 256) {
@@ -186,6 +222,31 @@ __global__ __launch_bounds__(256) void adam_pack_kernel(AdamPackArgs a) {
 #pragma unroll
             for (int jj = 0; jj < 8; ++jj) x[jj] = jj < ne ? pp[jj] : 0.f;
         }
+        if constexpr (P == PREC_F32) {
+            // two forward items (columns c0.. and c0 + 4..) and, after the
+            // exchange, two dX items (rows n0.. and n0 + 4..) per lane
+            __shared__ float tf[32][8][8];
+            if (rv)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int c = c0 + 4 * h;
+                    stg(J.wf + ((long)(n >> 4) * J.ksf + (c >> 4)) * 64 + (n & 15) + 16 * ((c & 15) >> 2),
+                        __builtin_bit_cast(u32x4, floatx4{x[4 * h], x[4 * h + 1], x[4 * h + 2], x[4 * h + 3]}));
+                }
+            const int slot = threadIdx.x >> 3;
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) tf[slot][r][jj] = x[jj];
+            __syncthreads();
+            const int c = c0 + r;
+            if (J.wb && n0 < J.N && c < J.K)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int nn = n0 + 4 * h;
+                    stg(J.wb + ((long)(c >> 4) * J.ksb + (nn >> 4)) * 64 + (c & 15) + 16 * ((nn & 15) >> 2),
+                        __builtin_bit_cast(u32x4, floatx4{tf[slot][4 * h][r], tf[slot][4 * h + 1][r],
+                                                          tf[slot][4 * h + 2][r], tf[slot][4 * h + 3][r]}));
+                }
+        } else {
         uint32_t w[4];
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj)
@@ -204,6 +265,7 @@ __global__ __launch_bounds__(256) void adam_pack_kernel(AdamPackArgs a) {
             for (int jj = 0; jj < 4; ++jj) d[jj] = (uint32_t)T[16 * jj + r] | ((uint32_t)T[16 * jj + 8 + r] << 16);
             stg(J.wb + ((long)(c >> 4) * J.ksb + (n0 >> 5)) * 64 + (c & 15) + 16 * ((n0 & 31) >> 3),
                 u32x4{d[0], d[1], d[2], d[3]});
+        }
         }
     } else if (a.nseg > 0) {
         const int pb = b - a.jb[a.njobs], npb = gridDim.x - a.jb[a.njobs];
@@ -319,7 +381,7 @@ struct TargetArgs {
     const float *ns;  // next_state [B][S]
     int B, S, A, Z, Ha, Hc;
     Noise nz;
-    uint16_t *img;  // [B][2Z + A]: zsa | zs | next_action
+    void *img;      // [B][round_up(2Z + A, 8)] operand type: zsa | zs | next_action
     float *qt;      // [B][2]
     R16 X, H1, H2, CATA, CATZ, OUT, CAT;
     R32 F, TW;
@@ -365,10 +427,13 @@ __global__ __launch_bounds__(NTH) void target_a_kernel(TargetArgs a) {
     // zs into OUT[:, Z:2Z] (from CATZ[:, 0:Z])
     for (int k = threadIdx.x; k < rows * Z; k += NTH) {
         const int row = k / Z, c = k - row * Z;
-        *p16(lds, a.OUT, row, Z + c) = *p16(lds, a.CATZ, row, c);
+        *pe<P>(lds, a.OUT, row, Z + c) = *pe<P>(lds, a.CATZ, row, c);
     }
     __syncthreads();
-    store_rows16(lds, a.OUT, 0, a.img, (2 * Z + a.A + 7) / 8 * 8, (2 * Z + a.A + 7) / 8 * 8, rows, row0, B);
+    // raw 16-bit copy of the image rows (an fp32 element is two 16-bit units)
+    constexpr int EH = Ty<P>::EB / 2;
+    const int ild = (2 * Z + a.A + 7) / 8 * 8 * EH;
+    store_rows16(lds, a.OUT, 0, (uint16_t *)a.img, ild, ild, rows, row0, B);
 }
 
 template <int P, int TH>
@@ -381,18 +446,35 @@ __global__ __launch_bounds__(NTH) void target_b_kernel(TargetArgs a) {
     int si = 0;
     FSTAMP(si);
     RowStage sn;
-    Row16Stage sa, sc;
     ThinStage<1> tw;
     row_issue(sn, a.ns, a.S, a.S, row0, B);
-    row16_issue(sa, a.img + 2 * Z, ild, a.A, row0, B);
-    row16_issue(sc, a.img, ild, 2 * Z, row0, B);
+    // fp32: zsa, zs and the action as three fp32 row stages (column per thread);
+    // 16-bit: zsa | zs and the action as column pairs
+    [[maybe_unused]] RowStage fa, fz0, fz1;
+    [[maybe_unused]] Row16Stage sa, sc;
+    if constexpr (P == PREC_F32) {
+        const float *img = (const float *)a.img;
+        row_issue(fa, img + 2 * Z, ild, a.A, row0, B);
+        row_issue(fz0, img, ild, Z, row0, B);
+        row_issue(fz1, img + Z, ild, Z, row0, B);
+    } else {
+        const uint16_t *img = (const uint16_t *)a.img;
+        row16_issue(sa, img + 2 * Z, ild, a.A, row0, B);
+        row16_issue(sc, img, ild, 2 * Z, row0, B);
+    }
     thin_issue(tw, cr[6].w, cr[6].ldw, 0, false, 1, cr[6].K);
     RING_START(cr[0]);
     zero_lds(lds, a.lds_b);
     __syncthreads();
     row_put16<P>(lds, sn, a.X, 0, a.S, row0, B);
-    row16_put(lds, sa, a.X, a.S, a.A, row0, B);
-    row16_put(lds, sc, a.CAT, a.Hc, 2 * Z, row0, B);
+    if constexpr (P == PREC_F32) {
+        row_put16<P>(lds, fa, a.X, a.S, a.A, row0, B);
+        row_put16<P>(lds, fz0, a.CAT, a.Hc, Z, row0, B);
+        row_put16<P>(lds, fz1, a.CAT, a.Hc + Z, Z, row0, B);
+    } else {
+        row16_put(lds, sa, a.X, a.S, a.A, row0, B);
+        row16_put(lds, sc, a.CAT, a.Hc, 2 * Z, row0, B);
+    }
     thin_put<P>(lds, tw, a.TW, 1, cr[6].K);
     __syncthreads();
     // critic_target(s', a', zsa, zs) head h (:109-140): AvgL1Norm(q0(sa)) | zsa | zs -> q1 -> q2 -> q3
@@ -447,6 +529,8 @@ __global__ __launch_bounds__(NTH) void fixed_kernel(FixedArgs a) {
 
 using namespace td7f;
 
+static bool prec_ok(int p) { return p == PREC_BF16 || p == PREC_F16 || p == PREC_F32; }
+
 extern "C" {
 
 #ifdef EXO_STAMPS
@@ -456,14 +540,15 @@ int td7f_debug_set_stamps(unsigned long long *buf) {
 #endif
 
 int td7f_pack(int32_t prec, int32_t njobs, const td7f_pack_job *jobs, void *stream) {
-    if ((prec != PREC_BF16 && prec != PREC_F16) || njobs <= 0 || njobs > TD7F_MAX_PACK || !jobs) return EXO_EINVAL;
+    if (!prec_ok(prec) || njobs <= 0 || njobs > TD7F_MAX_PACK || !jobs) return EXO_EINVAL;
+    const int kd = kd_of(prec);
     PackArgs a{};
     a.njobs = njobs;
     a.start[0] = 0;
     for (int q = 0; q < njobs; ++q) {
         const td7f_pack_job &J = jobs[q];
-        if (!J.w || !J.wf || J.n_out <= 0 || J.n_in <= 0 || J.ld < J.n_in || J.ksf * 32 < J.n_in ||
-            J.ntf * 16 < J.n_out || (J.wb && (J.ksb * 32 < J.n_out || J.ntb * 16 < J.n_in)))
+        if (!J.w || !J.wf || J.n_out <= 0 || J.n_in <= 0 || J.ld < J.n_in || J.ksf * kd < J.n_in ||
+            J.ntf * 16 < J.n_out || (J.wb && (J.ksb * kd < J.n_out || J.ntb * 16 < J.n_in)))
             return EXO_EINVAL;
         a.j[q] = PackJob{J.w, (long)J.ld, J.n_out, J.n_in, (u32x4 *)J.wf, (u32x4 *)J.wb, J.ksf, J.ntf,
                          J.wb ? J.ksb : 0, J.wb ? J.ntb : 0};
@@ -474,8 +559,10 @@ int td7f_pack(int32_t prec, int32_t njobs, const td7f_pack_job *jobs, void *stre
     const dim3 grid((unsigned)std::min<long>(1024, (most + 255) / 256), (unsigned)njobs);
     if (prec == PREC_BF16)
         hipLaunchKernelGGL(pack_kernel<PREC_BF16>, grid, dim3(256), 0, (hipStream_t)stream, a);
-    else
+    else if (prec == PREC_F16)
         hipLaunchKernelGGL(pack_kernel<PREC_F16>, grid, dim3(256), 0, (hipStream_t)stream, a);
+    else
+        hipLaunchKernelGGL(pack_kernel<PREC_F32>, grid, dim3(256), 0, (hipStream_t)stream, a);
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 
@@ -484,10 +571,11 @@ int td7f_adam_pack(int32_t prec, int32_t nopt, float *const *p, float *const *m,
                    const float *weight_decay, int32_t nseg, const float *const *g, const int64_t *off, const int32_t *n,
                    const int32_t *opt, int32_t njobs, const td7f_pack_job *jobs, const int32_t *job_seg,
                    uint32_t *ticket, void *stream) {
-    if ((prec != PREC_BF16 && prec != PREC_F16) || nopt <= 0 || nopt > TD7_ADAM_MAX_OPT || nseg <= 0 ||
+    if (!prec_ok(prec) || nopt <= 0 || nopt > TD7_ADAM_MAX_OPT || nseg <= 0 ||
         nseg > TD7_ADAM_MAX_SEG || njobs < 0 || njobs > TD7F_MAX_ADAM_PACK || (njobs && (!jobs || !job_seg)) ||
         !ticket)
         return EXO_EINVAL;
+    const int kd = kd_of(prec);
     AdamPackArgs a{};
     a.nopt = nopt;
     a.ticket = ticket;
@@ -505,7 +593,7 @@ int td7f_adam_pack(int32_t prec, int32_t nopt, float *const *p, float *const *m,
         const td7f_pack_job &J = jobs[q];
         const int k = job_seg[q];
         if (k < 0 || k >= nseg || !J.w || !J.wf || J.n_out <= 0 || J.n_in <= 0 || J.ld != J.n_in ||
-            J.ksf * 32 < J.n_in || J.ntf * 16 < J.n_out || (J.wb && (J.ksb * 32 < J.n_out || J.ntb * 16 < J.n_in)))
+            J.ksf * kd < J.n_in || J.ntf * 16 < J.n_out || (J.wb && (J.ksb * kd < J.n_out || J.ntb * 16 < J.n_in)))
             return EXO_EINVAL;
         const int o = opt[k];
         const long e = (long)(J.w - p[o]), sz = (long)J.n_out * J.n_in;
@@ -537,15 +625,17 @@ int td7f_adam_pack(int32_t prec, int32_t nopt, float *const *p, float *const *m,
     if (grid == 0) return EXO_OK;
     if (prec == PREC_BF16)
         hipLaunchKernelGGL(adam_pack_kernel<PREC_BF16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
-    else
+    else if (prec == PREC_F16)
         hipLaunchKernelGGL(adam_pack_kernel<PREC_F16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
+    else
+        hipLaunchKernelGGL(adam_pack_kernel<PREC_F32>, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 
 int td7f_select(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7f_lin *actor, const float *obs,
                 int32_t n, const td7f_noise *noise, float *out, void *stream) {
-    if ((prec != PREC_BF16 && prec != PREC_F16) || !act || !enc || !actor || !obs || !noise || !out || n <= 0)
-        return EXO_EINVAL;
+    if (!prec_ok(prec) || !act || !enc || !actor || !obs || !noise || !out || n <= 0) return EXO_EINVAL;
+    const int kd = kd_of(prec);
     td7f_lin all[7] = {enc[0], enc[1], enc[2], actor[0], actor[1], actor[2], actor[3]};
     const int th = th_of(all, 7);
     if (th != 4 && th != 5) return EXO_EINVAL;
@@ -569,24 +659,29 @@ int td7f_select(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7
     // (4,096 envs: one workgroup per CU).  EXO_SELECT_RT=1|2 forces one (read
     // per call: tests switch it).
     const char *rt_env = getenv("EXO_SELECT_RT");
-    const int RT = rt_env && (rt_env[0] == '1' || rt_env[0] == '2') ? rt_env[0] - '0' : (n > 8192 ? 2 : 1);
+    // (fp32: 16-row tiles only -- a 32-row tile's fp32 images exceed the LDS)
+    const int RT = prec == PREC_F32 ? 1
+                   : rt_env && (rt_env[0] == '1' || rt_env[0] == '2') ? rt_env[0] - '0' : (n > 8192 ? 2 : 1);
     const int rows = RT * TR, hmax = std::max(enc[0].n_out, std::max(enc[1].n_out, std::max(a.Ha, actor[1].n_out)));
     Bump b(RT);
-    a.X = b.r16(rows, ld16(a.S));
-    a.H1 = b.r16(rows, ld16(hmax));
-    a.H2 = b.r16(rows, ld16(hmax));
+    a.X = b.r16(rows, ld16(a.S, kd));
+    a.H1 = b.r16(rows, ld16(hmax, kd));
+    a.H2 = b.r16(rows, ld16(hmax, kd));
     const int fld = std::max(std::max(a.Z, a.Ha), 16);
     if (rows * fld * 4 <= a.H2.off + rows * a.H2.ld * 2 - a.H1.off) {
         a.F = R32{a.H1.off, fld};  // overlays H1 | H2 (both dead whenever F is written)
     } else {
         a.F = b.r32(rows, fld);
     }
-    a.CAT = b.r16(rows, ld16(a.Ha + a.Z));
+    a.CAT = b.r16(rows, ld16(a.Ha + a.Z, kd));
     a.TW = b.r32(THIN_NC, actor[3].n_in);
     a.FT = b.r32(rows, 16);
     a.lds_bytes = b.off;
     const dim3 grid((n + rows - 1) / rows);
     const hipStream_t st = (hipStream_t)stream;
+    if (prec == PREC_F32)
+        return th == 5 ? launch(select_kernel<PREC_F32, 5, 1>, grid, b.off, a, st)
+                       : launch(select_kernel<PREC_F32, 4, 1>, grid, b.off, a, st);
     if (RT == 2)
         return prec == PREC_BF16 ? (th == 5 ? launch(select_kernel<PREC_BF16, 5, 2>, grid, b.off, a, st)
                                             : launch(select_kernel<PREC_BF16, 4, 2>, grid, b.off, a, st))
@@ -599,11 +694,11 @@ int td7f_select(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7
 }
 
 int td7f_target(int32_t prec, const int32_t *act, const td7f_lin *tenc, const td7f_lin *tactor,
-                const td7f_lin *tcritic, const float *ns, int32_t B, const td7f_noise *noise, uint16_t *img,
+                const td7f_lin *tcritic, const float *ns, int32_t B, const td7f_noise *noise, void *img,
                 float *qt, void *stream) {
-    if ((prec != PREC_BF16 && prec != PREC_F16) || !act || !tenc || !tactor || !tcritic || !ns || !noise || !img ||
-        !qt || B <= 0)
+    if (!prec_ok(prec) || !act || !tenc || !tactor || !tcritic || !ns || !noise || !img || !qt || B <= 0)
         return EXO_EINVAL;
+    const int kd = kd_of(prec), eh = prec == PREC_F32 ? 2 : 1;
     td7f_lin all[18];
     for (int i = 0; i < 6; ++i) all[i] = tenc[i];
     for (int i = 0; i < 4; ++i) all[6 + i] = tactor[i];
@@ -635,18 +730,31 @@ int td7f_target(int32_t prec, const int32_t *act, const td7f_lin *tenc, const td
     int hmax = 0;
     for (int i = 0; i < 18; ++i) hmax = std::max(hmax, all[i].n_out);
     Bump ba(1);
-    a.X = ba.r16(rows, ld16(a.S + a.A));
-    a.H1 = ba.r16(rows, ld16(hmax));
-    a.H2 = ba.r16(rows, ld16(hmax));
-    a.CATA = ba.r16(rows, ld16(a.Ha + a.Z));
-    a.CATZ = ba.r16(rows, ld16(a.Z + a.A));
-    a.OUT = ba.r16(rows, round_up(2 * a.Z + a.A, 8));  // == the image row (16-byte stores)
-    a.F = ba.r32(rows, std::max(hmax, 16));
+    a.X = ba.r16(rows, ld16(a.S + a.A, kd));
+    a.H1 = ba.r16(rows, ld16(hmax, kd));
+    a.H2 = ba.r16(rows, ld16(hmax, kd));
+    a.CATA = ba.r16(rows, ld16(a.Ha + a.Z, kd));
+    a.CATZ = ba.r16(rows, ld16(a.Z + a.A, kd));
+    const int old = eh * round_up(2 * a.Z + a.A, 8);  // == the image row (16-byte stores)
+    const int fld = std::max(hmax, 16);
+    if (prec == PREC_F32) {
+        // fp32 images: OUT overlays CATA (dead once actor_target's l1 has read
+        // it; OUT is first written by the noise after l3) and F overlays
+        // H1 | H2 (dead whenever F is written; the thin l3 writes F's first
+        // columns only, inside H1, while it reads H2)
+        a.OUT = R16{a.CATA.off, old};
+        a.F = R32{a.H1.off, fld};
+        if (rows * old * 2 > rows * a.CATA.ld * 2 || rows * fld * 4 > a.H2.off + rows * a.H2.ld * 2 - a.H1.off)
+            return EXO_EINVAL;
+    } else {
+        a.OUT = ba.r16(rows, old);
+        a.F = ba.r32(rows, fld);
+    }
     a.TW = ba.r32(THIN_NC, tactor[3].n_in);
     a.lds_a = ba.off;
     Bump bb(1);
-    const R16 Xb = bb.r16(rows, ld16(a.S + a.A)), H1b = bb.r16(rows, ld16(hmax)), H2b = bb.r16(rows, ld16(hmax));
-    const R16 CATb = bb.r16(rows, ld16(a.Hc + 2 * a.Z));
+    const R16 Xb = bb.r16(rows, ld16(a.S + a.A, kd)), H1b = bb.r16(rows, ld16(hmax, kd)), H2b = bb.r16(rows, ld16(hmax, kd));
+    const R16 CATb = bb.r16(rows, ld16(a.Hc + 2 * a.Z, kd));
     const R32 Fb = bb.r32(rows, std::max(hmax, 16));
     const R32 TWb = bb.r32(1, tcritic[6].n_in);
     a.lds_b = bb.off;
@@ -665,8 +773,8 @@ int td7f_target(int32_t prec, const int32_t *act, const td7f_lin *tenc, const td
 
 int td7f_fixed(int32_t prec, const int32_t *act, const td7f_lin *fenc, const float *s, const float *action,
                int32_t B, float *zs, float *zsa, void *stream) {
-    if ((prec != PREC_BF16 && prec != PREC_F16) || !act || !fenc || !s || !action || !zs || !zsa || B <= 0)
-        return EXO_EINVAL;
+    if (!prec_ok(prec) || !act || !fenc || !s || !action || !zs || !zsa || B <= 0) return EXO_EINVAL;
+    const int kd = kd_of(prec);
     const int th = th_of(fenc, 6);
     if (th != 4 && th != 5) return EXO_EINVAL;
     FixedArgs a{};
@@ -685,10 +793,10 @@ int td7f_fixed(int32_t prec, const int32_t *act, const td7f_lin *fenc, const flo
     int hmax = 0;
     for (int i = 0; i < 6; ++i) hmax = std::max(hmax, fenc[i].n_out);
     Bump b(1);
-    a.X = b.r16(rows, ld16(a.S));
-    a.H1 = b.r16(rows, ld16(hmax));
-    a.H2 = b.r16(rows, ld16(hmax));
-    a.CATZ = b.r16(rows, ld16(a.Z + a.A));
+    a.X = b.r16(rows, ld16(a.S, kd));
+    a.H1 = b.r16(rows, ld16(hmax, kd));
+    a.H2 = b.r16(rows, ld16(hmax, kd));
+    a.CATZ = b.r16(rows, ld16(a.Z + a.A, kd));
     a.F = b.r32(rows, std::max(hmax, 16));
     a.lds_bytes = b.off;
     return DISPATCH(prec, th, fixed_kernel, dim3((B + rows - 1) / rows), b.off, a, (hipStream_t)stream);

@@ -30,8 +30,8 @@ namespace td7f {
 
 // Transposed operands of one layer's weight gradient (row stride ld = padded batch).
 struct XT {
-    uint16_t *x;   // X^T  [K][ld]
-    uint16_t *dp;  // dP^T [N][ld] (x gs)
+    void *x;   // X^T  [K][ld] (operand type, fragment blocks: td7_fused.h blk8 / blk4)
+    void *dp;  // dP^T [N][ld] (x gs)
     float *part;   // [row tiles][N] fp32 column sums of dP
 };
 
@@ -113,13 +113,13 @@ __global__ __launch_bounds__(NTH) void critic_kernel(CriticArgs a) {
     layer_fwd<P, 1, TH>(lds, R, a.X, cr[0], &cr[2], ACT_NONE, NO16, 0, a.H0, nullptr, 0, row0, B, si);
     norm_fwd<P>(lds, a.H0, Hc, TR, 1e-8f, a.CAT, 0, NO16, 0, NO32, nullptr, 0, mean, nullptr, row0, B);
     __syncthreads();
-    save_xt(lds, a.X, 0, a.S + a.A, xt[0].x, a.ld, TR, row0);
-    save_xt(lds, a.CAT, 0, Hc + 2 * Z, xt[2].x, a.ld, TR, row0);
+    save_xt<P>(lds, a.X, 0, a.S + a.A, xt[0].x, a.ld, TR, row0);
+    save_xt<P>(lds, a.CAT, 0, Hc + 2 * Z, xt[2].x, a.ld, TR, row0);
     layer_fwd<P, 1, TH>(lds, R, a.CAT, cr[2], &cr[4], a.act, a.H1, 0, NO32, y1, Hc, row0, B, si);
     const GDesc b3 = bwd_of(cr[6], 0);
     layer_fwd<P, 1, TH>(lds, R, a.H1, cr[4], &b3, a.act, a.H2, 0, NO32, y2, Hc, row0, B, si);
-    save_xt(lds, a.H1, 0, Hc, xt[4].x, a.ld, TR, row0);
-    save_xt(lds, a.H2, 0, Hc, xt[6].x, a.ld, TR, row0);
+    save_xt<P>(lds, a.H1, 0, Hc, xt[4].x, a.ld, TR, row0);
+    save_xt<P>(lds, a.H2, 0, Hc, xt[6].x, a.ld, TR, row0);
     layer_thin_fwd<P, 1>(lds, a.H2, cr[6], a.TW, ACT_NONE, a.F, TR, nullptr, 0, row0, B, si);
     // Q_target (:241-246) and the LAP-Huber gradient (:257-259) of this head
     if (threadIdx.x < TR) {
@@ -146,15 +146,15 @@ __global__ __launch_bounds__(NTH) void critic_kernel(CriticArgs a) {
     // backward (:260-262): q3 -> q2 -> q1 (the q window) -> AvgL1Norm -> q0's dP
     make_dp<P>(lds, a.F, 1, ACT_NONE, nullptr, 0, a.DP1, xt[6].part + (long)tile * 1, row0, B);
     __syncthreads();
-    save_xt(lds, a.DP1, 0, 1, xt[6].dp, a.ld, TR, row0);
+    save_xt<P>(lds, a.DP1, 0, 1, xt[6].dp, a.ld, TR, row0);
     const GDesc nx1 = bwd_of(cr[4], 0);
     layer_bwd<P, TH>(lds, R, a.DP1, cr[6], 0, Hc, &nx1, a.act, y2, Hc, NO32, nullptr, 0, a.DP0,
                      xt[4].part + (long)tile * Hc, row0, B, si);
-    save_xt(lds, a.DP0, 0, Hc, xt[4].dp, a.ld, TR, row0);
+    save_xt<P>(lds, a.DP0, 0, Hc, xt[4].dp, a.ld, TR, row0);
     const GDesc nx2 = bwd_of(cr[2], 0);
     layer_bwd<P, TH>(lds, R, a.DP0, cr[4], 0, Hc, &nx2, a.act, y1, Hc, NO32, nullptr, 0, a.DP1,
                      xt[2].part + (long)tile * Hc, row0, B, si);
-    save_xt(lds, a.DP1, 0, Hc, xt[2].dp, a.ld, TR, row0);
+    save_xt<P>(lds, a.DP1, 0, Hc, xt[2].dp, a.ld, TR, row0);
     layer_bwd<P, TH>(lds, R, a.DP1, cr[2], 0, Hc, nullptr, ACT_NONE, nullptr, 0, a.DY, nullptr, 0, NO16, nullptr,
                      row0, B, si);
     norm_bwd<P>(lds, a.DY, a.H0, mean, Hc, 1e-8f, dot, a.DP0, xt[0].dp, a.ld, xt[0].part + (long)tile * Hc,
@@ -238,20 +238,20 @@ __global__ __launch_bounds__(NTH) void encoder_kernel(EncoderArgs a) {
     // zs = encoder.zs(state) (:222), pred_zs = encoder.zsa(zs, action) (:223)
     row_put16<P>(lds, ss, a.X, 0, a.S, row0, B);
     __syncthreads();
-    save_xt(lds, a.X, 0, a.S, a.xt[0].x, ld, TR, row0);
+    save_xt<P>(lds, a.X, 0, a.S, a.xt[0].x, ld, TR, row0);
     layer_fwd<P, 1, TH>(lds, R, a.X, a.e[0], &a.e[1], a.act, a.H1, 0, NO32, a.y0, He, row0, B, si);
-    save_xt(lds, a.H1, 0, He, a.xt[1].x, ld, TR, row0);
+    save_xt<P>(lds, a.H1, 0, He, a.xt[1].x, ld, TR, row0);
     layer_fwd<P, 1, TH>(lds, R, a.H1, a.e[1], &a.e[2], a.act, a.H2, 0, NO32, a.y1, He, row0, B, si);
-    save_xt(lds, a.H2, 0, He, a.xt[2].x, ld, TR, row0);
+    save_xt<P>(lds, a.H2, 0, He, a.xt[2].x, ld, TR, row0);
     layer_fwd<P, 1, TH>(lds, R, a.H2, a.e[2], &a.e[3], ACT_NONE, NO16, 0, a.H3, nullptr, 0, row0, B, si);
     norm_fwd<P>(lds, a.H3, Z, TR, 1e-8f, a.CATZ, 0, NO16, 0, NO32, nullptr, 0, mean, nullptr, row0, B);
     __syncthreads();
-    save_xt(lds, a.CATZ, 0, Z + a.A, a.xt[3].x, ld, TR, row0);
+    save_xt<P>(lds, a.CATZ, 0, Z + a.A, a.xt[3].x, ld, TR, row0);
     layer_fwd<P, 1, TH>(lds, R, a.CATZ, a.e[3], &a.e[4], a.act, a.H1, 0, NO32, a.y2, He, row0, B, si);
-    save_xt(lds, a.H1, 0, He, a.xt[4].x, ld, TR, row0);
+    save_xt<P>(lds, a.H1, 0, He, a.xt[4].x, ld, TR, row0);
     const GDesc b6 = bwd_of(a.e[5], 0);
     layer_fwd<P, 1, TH>(lds, R, a.H1, a.e[4], &a.e[5], a.act, a.H2, 0, NO32, a.y3, He, row0, B, si);
-    save_xt(lds, a.H2, 0, He, a.xt[5].x, ld, TR, row0);
+    save_xt<P>(lds, a.H2, 0, He, a.xt[5].x, ld, TR, row0);
     layer_fwd<P, 1, TH>(lds, R, a.H2, a.e[5], &b6, ACT_NONE, NO16, 0, a.DY, nullptr, 0, row0, B, si);
     if (split) {  // next_zs from this tile's producer
         if (threadIdx.x == 0) {
@@ -277,15 +277,15 @@ __global__ __launch_bounds__(NTH) void encoder_kernel(EncoderArgs a) {
     __syncthreads();
     make_dp<P>(lds, a.DY, Z, ACT_NONE, nullptr, 0, a.DP0, a.xt[5].part + (long)tile * Z, row0, B);
     __syncthreads();
-    save_xt(lds, a.DP0, 0, Z, a.xt[5].dp, ld, TR, row0);
+    save_xt<P>(lds, a.DP0, 0, Z, a.xt[5].dp, ld, TR, row0);
     const GDesc nx3 = bwd_of(a.e[4], 0);
     layer_bwd<P, TH>(lds, R, a.DP0, a.e[5], 0, He, &nx3, a.act, a.y3, He, NO32, nullptr, 0, a.DP1,
                      a.xt[4].part + (long)tile * He, row0, B, si);
-    save_xt(lds, a.DP1, 0, He, a.xt[4].dp, ld, TR, row0);
+    save_xt<P>(lds, a.DP1, 0, He, a.xt[4].dp, ld, TR, row0);
     const GDesc nx4 = bwd_of(a.e[3], 0);
     layer_bwd<P, TH>(lds, R, a.DP1, a.e[4], 0, He, &nx4, a.act, a.y2, He, NO32, nullptr, 0, a.DP0,
                      a.xt[3].part + (long)tile * He, row0, B, si);
-    save_xt(lds, a.DP0, 0, He, a.xt[3].dp, ld, TR, row0);
+    save_xt<P>(lds, a.DP0, 0, He, a.xt[3].dp, ld, TR, row0);
     const GDesc nx5 = bwd_of(a.e[2], 0);
     // d zs from the zs columns of zsa1's input, then AvgL1Norm backward
     layer_bwd<P, TH>(lds, R, a.DP0, a.e[3], 0, Z, &nx5, ACT_NONE, nullptr, 0, a.NZ, nullptr, 0, NO16, nullptr, row0, B,
@@ -295,10 +295,10 @@ __global__ __launch_bounds__(NTH) void encoder_kernel(EncoderArgs a) {
     const GDesc nx6 = bwd_of(a.e[1], 0);
     layer_bwd<P, TH>(lds, R, a.DP1, a.e[2], 0, He, &nx6, a.act, a.y1, He, NO32, nullptr, 0, a.DP0,
                      a.xt[1].part + (long)tile * He, row0, B, si);
-    save_xt(lds, a.DP0, 0, He, a.xt[1].dp, ld, TR, row0);
+    save_xt<P>(lds, a.DP0, 0, He, a.xt[1].dp, ld, TR, row0);
     layer_bwd<P, TH>(lds, R, a.DP0, a.e[1], 0, He, nullptr, a.act, a.y0, He, NO32, nullptr, 0, a.DP1,
                      a.xt[0].part + (long)tile * He, row0, B, si);
-    save_xt(lds, a.DP1, 0, He, a.xt[0].dp, ld, TR, row0);
+    save_xt<P>(lds, a.DP1, 0, He, a.xt[0].dp, ld, TR, row0);
 }
 
 // ---------------------------------------------------------------- actor update
@@ -346,16 +346,16 @@ __global__ __launch_bounds__(NTH) void actor_a_kernel(ActorArgs a) {
     layer_fwd<P, 1, TH>(lds, R, a.X, a.ac[0], &a.ac[1], ACT_NONE, NO16, 0, a.H0, a.h0, Ha, row0, B, si);
     norm_fwd<P>(lds, a.H0, Ha, TR, 1e-8f, a.CATA, 0, NO16, 0, NO32, nullptr, 0, nullptr, a.mean0, row0, B);
     __syncthreads();
-    save_xt(lds, a.X, 0, a.S, a.xt[0].x, ld, TR, row0);
-    save_xt(lds, a.CATA, 0, Ha + Z, a.xt[1].x, ld, TR, row0);
+    save_xt<P>(lds, a.X, 0, a.S, a.xt[0].x, ld, TR, row0);
+    save_xt<P>(lds, a.CATA, 0, Ha + Z, a.xt[1].x, ld, TR, row0);
     layer_fwd<P, 1, TH>(lds, R, a.CATA, a.ac[1], &a.ac[2], a.act_actor, a.H1, 0, NO32, a.ya[0], Ha, row0, B, si);
     layer_fwd<P, 1, TH>(lds, R, a.H1, a.ac[2], &a.fe[3], a.act_actor, a.H2, 0, NO32, a.ya[1], Ha, row0, B, si);
-    save_xt(lds, a.H1, 0, Ha, a.xt[2].x, ld, TR, row0);
-    save_xt(lds, a.H2, 0, Ha, a.xt[3].x, ld, TR, row0);
+    save_xt<P>(lds, a.H1, 0, Ha, a.xt[2].x, ld, TR, row0);
+    save_xt<P>(lds, a.H2, 0, Ha, a.xt[3].x, ld, TR, row0);
     layer_thin_fwd<P, THIN_NC>(lds, a.H2, a.ac[3], a.TW, ACT_TANH, a.F, TR, a.act_out, a.A, row0, B, si);
     for (int k = threadIdx.x; k < TR * a.A; k += NTH) {
         const int r = k / a.A, c = k - r * a.A;
-        *p16(lds, a.CATZ, r, Z + c) = Ty<P>::bits(*p32(lds, a.F, r, c));
+        *pe<P>(lds, a.CATZ, r, Z + c) = Ty<P>::bits(*p32(lds, a.F, r, c));
     }
     __syncthreads();
     // fixed_encoder.zsa(fixed_zs, actor) (:269)
@@ -388,13 +388,15 @@ __global__ __launch_bounds__(NTH) void actor_b_kernel(ActorArgs a) {
     row_put16<P>(lds, sa, a.X, a.S, a.A, row0, B);
     row_put16<P>(lds, sz, a.CAT, Hc, Z, row0, B);
     row_put16<P>(lds, szs, a.CAT, Hc + Z, Z, row0, B);
-    thin_put<P>(lds, tw, a.TW, a.A, Hc);
+    if constexpr (P != PREC_F32) thin_put<P>(lds, tw, a.TW, a.A, Hc);
     __syncthreads();
     // Q = critic(state, actor, zsa, zs) with the updated critic (:270)
     layer_fwd<P, 1, TH>(lds, R, a.X, cr[0], &cr[2], ACT_NONE, NO16, 0, a.H0, nullptr, 0, row0, B, si);
     norm_fwd<P>(lds, a.H0, Hc, TR, 1e-8f, a.CAT, 0, NO16, 0, NO32, nullptr, 0, mean, nullptr, row0, B);
     __syncthreads();
     layer_fwd<P, 1, TH>(lds, R, a.CAT, cr[2], &cr[4], a.act_critic, a.H1, 0, NO32, y1, Hc, row0, B, si);
+    // (fp32: the thin weights' region lies in CAT, dead from here on)
+    if constexpr (P == PREC_F32) thin_put<P>(lds, tw, a.TW, a.A, Hc);
     const GDesc b3 = bwd_of(cr[6], 0);
     layer_fwd<P, 1, TH>(lds, R, a.H1, cr[4], &b3, a.act_critic, a.H2, 0, NO32, y2, Hc, row0, B, si);
     // d(-Q.mean())/dQ (:272): the constant -1/(2B) on every live row
@@ -477,15 +479,15 @@ __global__ __launch_bounds__(NTH) void actor_c_kernel(ActorArgs a) {
     __syncthreads();
     make_dp<P>(lds, a.F, A, ACT_NONE, nullptr, 0, a.DP1, a.xt[3].part + (long)tile * A, row0, B);
     __syncthreads();
-    save_xt(lds, a.DP1, 0, A, a.xt[3].dp, ld, TR, row0);
+    save_xt<P>(lds, a.DP1, 0, A, a.xt[3].dp, ld, TR, row0);
     const GDesc nx12 = bwd_of(a.ac[2], 0);
     layer_bwd<P, TH>(lds, R, a.DP1, a.ac[3], 0, Ha, &nx12, a.act_actor, a.ya[1], Ha, NO32, nullptr, 0, a.DP0,
                      a.xt[2].part + (long)tile * Ha, row0, B, si);
-    save_xt(lds, a.DP0, 0, Ha, a.xt[2].dp, ld, TR, row0);
+    save_xt<P>(lds, a.DP0, 0, Ha, a.xt[2].dp, ld, TR, row0);
     const GDesc nx13 = bwd_of(a.ac[1], 0);
     layer_bwd<P, TH>(lds, R, a.DP0, a.ac[2], 0, Ha, &nx13, a.act_actor, a.ya[0], Ha, NO32, nullptr, 0, a.DP1,
                      a.xt[1].part + (long)tile * Ha, row0, B, si);
-    save_xt(lds, a.DP1, 0, Ha, a.xt[1].dp, ld, TR, row0);
+    save_xt<P>(lds, a.DP1, 0, Ha, a.xt[1].dp, ld, TR, row0);
     layer_bwd<P, TH>(lds, R, a.DP1, a.ac[1], 0, Ha, nullptr, ACT_NONE, nullptr, 0, a.DY, nullptr, 0, NO16, nullptr,
                      row0, B, si);
     FSTAMP(si);
@@ -502,7 +504,7 @@ __global__ __launch_bounds__(NTH) void actor_c_kernel(ActorArgs a) {
 // are 16-byte loads of the transposed operands (rows r contiguous), PD2
 // k-steps of 32 rows in flight.
 struct WgJob {
-    const uint16_t *dp, *x;
+    const char *dp, *x;  // operand-type fragment blocks (td7_fused.h blk8 / blk4)
     const float *part;
     float *dw, *db;
     int N, K, tiles_k, ntiles_rows;  // tiles_k = ceil(K / 64); row tiles of part
@@ -577,14 +579,16 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs a) {
             bp = ldg(o.p + i), bm = ldg(o.m + i), bv = ldg(o.v + i);
         }
     }
-    // the operands are in fragment blocks (td7_fused.h blk8): the 16 x 32
-    // fragment of operand rows g*16.. and k-step s is the 1 KiB block g * (ld/32) + s;
-    // they are padded to multiples of 64 rows (zeros), so every load is in range
-    const uint16_t *ap[2], *bp2[2];
+    // the operands are in fragment blocks (td7_fused.h blk8 / blk4): the
+    // fragment of operand rows g*16.. and k-step s (KD batch rows) is the 1 KiB
+    // block g * (ld / KD) + s; they are padded to multiples of 64 rows (zeros),
+    // so every load is in range
+    constexpr int KD = Ty<P>::KD;
+    const char *ap[2], *bp2[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-        ap[u] = J.dp + (long)((wn + 16 * u) >> 4) * (ld >> 5) * 512 + lane * 8;
-        bp2[u] = J.x + (long)((wk + 16 * u) >> 4) * (ld >> 5) * 512 + lane * 8;
+        ap[u] = J.dp + ((long)((wn + 16 * u) >> 4) * (ld / KD)) * 1024 + lane * 16;
+        bp2[u] = J.x + ((long)((wk + 16 * u) >> 4) * (ld / KD)) * 1024 + lane * 16;
     }
     floatx4 acc[2][2];
 #pragma unroll
@@ -593,14 +597,14 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs a) {
         for (int v = 0; v < 2; ++v) acc[u][v] = floatx4{0.f, 0.f, 0.f, 0.f};
     // rows is a multiple of 32 PD2 (the host pads the operands with zero columns):
     // PD2 k-steps of loads in flight, issue order pinned as in gemm
-    const int ns = a.rows / 32;
+    const int ns = a.rows / KD;
     u32x4 fa[PD2][2], fb[PD2][2];
 #pragma unroll
     for (int p = 0; p < PD2; ++p)
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            fa[p][u] = ldg((const u32x4 *)(ap[u] + 512 * p));
-            fb[p][u] = ldg((const u32x4 *)(bp2[u] + 512 * p));
+            fa[p][u] = ldg((const u32x4 *)(ap[u] + 1024 * p));
+            fb[p][u] = ldg((const u32x4 *)(bp2[u] + 1024 * p));
             __builtin_amdgcn_sched_barrier(0);
         }
     int s0 = 0;
@@ -609,14 +613,16 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs a) {
         for (int p = 0; p < PD2; ++p) {
             const int s = s0 + p;
 #pragma unroll
-            for (int u = 0; u < 2; ++u)
+            for (int j = 0; j < Ty<P>::SUB; ++j)
 #pragma unroll
-                for (int v = 0; v < 2; ++v) acc[u][v] = Ty<P>::mfma(fa[p][u], fb[p][v], acc[u][v]);
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int v = 0; v < 2; ++v) acc[u][v] = Ty<P>::mfma(fa[p][u], fb[p][v], acc[u][v], j);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
-                fa[p][u] = ldg((const u32x4 *)(ap[u] + 512 * (s + PD2)));
-                fb[p][u] = ldg((const u32x4 *)(bp2[u] + 512 * (s + PD2)));
+                fa[p][u] = ldg((const u32x4 *)(ap[u] + 1024L * (s + PD2)));
+                fb[p][u] = ldg((const u32x4 *)(bp2[u] + 1024L * (s + PD2)));
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -624,11 +630,14 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs a) {
 #pragma unroll
     for (int p = 0; p < PD2; ++p)
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
+        for (int j = 0; j < Ty<P>::SUB; ++j)
 #pragma unroll
-            for (int v = 0; v < 2; ++v) acc[u][v] = Ty<P>::mfma(fa[p][u], fb[p][v], acc[u][v]);
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int v = 0; v < 2; ++v) acc[u][v] = Ty<P>::mfma(fa[p][u], fb[p][v], acc[u][v], j);
     // C[n][k]: lane holds n = 16u + 4(lane >> 4) + e, k = 16v + (lane & 15)
-    __shared__ alignas(16) uint16_t T[ADAM ? 64 : 1][72];  // the tile's updated 16-bit weights (rows padded to 144 B)
+    // the tile's updated weights in the operand type (rows padded to 144 / 272 B)
+    __shared__ alignas(16) typename Ty<P>::E T[ADAM ? 64 : 1][Ty<P>::EB == 4 ? 68 : 72];
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -647,7 +656,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs a) {
                         const long i = J.w_off + (long)n * J.K + k;
                         stg(o.p + i, pp[u][v][e]), stg(o.m + i, mm[u][v][e]), stg(o.v + i, vv[u][v][e]);
                     }
-                    T[n - n0][k - k0] = ok ? Ty<P>::bits(pp[u][v][e]) : (uint16_t)0;
+                    T[n - n0][k - k0] = Ty<P>::bits(ok ? pp[u][v][e] : 0.f);
                 }
             }
         }
@@ -673,7 +682,31 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs a) {
             }
         }
     }
-    if constexpr (ADAM) {
+    if constexpr (ADAM && P == PREC_F32) {
+        __syncthreads();
+        // 64 rows x 16 forward items (4 inputs of one output row) and 64 columns
+        // x 16 dX items (4 output rows of one input column): four of each per thread
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            const int i = threadIdx.x + 256 * h;
+            const int r = i >> 4, c = 4 * (i & 15);
+            const int n = n0 + r, k = k0 + c;
+            if (n < J.N && k < J.K)
+                stg(J.wf + ((long)(n >> 4) * J.ksf + (k >> 4)) * 64 + (n & 15) + 16 * ((k & 15) >> 2),
+                    *(const u32x4 *)&T[r][c]);
+        }
+        if (J.wb) {
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                const int i = threadIdx.x + 256 * h;
+                const int c = i & 63, r4 = 4 * (i >> 6);
+                const int n = n0 + r4, k = k0 + c;
+                if (n < J.N && k < J.K)
+                    stg(J.wb + ((long)(k >> 4) * J.ksb + (n >> 4)) * 64 + (k & 15) + 16 * ((n & 15) >> 2),
+                        __builtin_bit_cast(u32x4, floatx4{T[r4][c], T[r4 + 1][c], T[r4 + 2][c], T[r4 + 3][c]}));
+            }
+        }
+    } else if constexpr (ADAM) {
         __syncthreads();
         // 64 rows x 8 forward items (8 inputs of one output row) and 64 columns
         // x 8 dX items (8 output rows of one input column): two of each per thread
@@ -721,13 +754,24 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs a) {
 
 using namespace td7f;
 
-static XT xt_of(const td7f_xt &x) { return XT{(uint16_t *)x.x, (uint16_t *)x.dp, x.part}; }
+static XT xt_of(const td7f_xt &x) { return XT{x.x, x.dp, x.part}; }
 
-static bool prec_ok(int p) { return p == PREC_BF16 || p == PREC_F16; }
+static bool prec_ok(int p) { return p == PREC_BF16 || p == PREC_F16 || p == PREC_F32; }
 static bool xt_ok(const td7f_xt *xt, int n) {
     for (int i = 0; i < n; ++i)
         if (!xt[i].x || !xt[i].dp || !xt[i].part) return false;
     return true;
+}
+// fp32 layouts: two 16-row dP images of row stride ld inside the image region r
+static bool alias_pair(R16 r, int ld, R16 &d0, R16 &d1) {
+    d0 = R16{r.off, ld};
+    d1 = R16{r.off + round_up(TR * ld * 2, 16), ld};
+    return d1.off + TR * ld * 2 <= r.off + TR * r.ld * 2;
+}
+// a 16-row fp32 region of n columns over the adjacent images a | b
+static bool alias32(R16 a, R16 b, int n, R32 &d) {
+    d = R32{a.off, n};
+    return a.off + TR * n * 4 <= b.off + TR * b.ld * 2;
 }
 static bool wb_ok(const td7f_lin *l, int n) {
     for (int i = 0; i < n; ++i)
@@ -770,15 +814,24 @@ int td7f_critic(int32_t prec, const int32_t *act, const td7f_lin *critic, const 
         g.Z * 2 + g.Hc != critic[2].n_in || g.Hc % 16)
         return EXO_EINVAL;
     g.td = td; g.q = q; g.y1 = y1; g.y2 = y2; g.ld = ld;
+    const int kd = kd_of(prec);
     Bump b(1);
-    g.X = b.r16(TR, ld16(S + A));
-    g.CAT = b.r16(TR, ld16(g.Hc + 2 * g.Z));
-    g.H1 = b.r16(TR, ld16(g.Hc));
-    g.H2 = b.r16(TR, ld16(g.Hc));
-    g.DP0 = b.r16(TR, ld16(g.Hc));
-    g.DP1 = b.r16(TR, ld16(g.Hc));
+    g.X = b.r16(TR, ld16(S + A, kd));
+    g.CAT = b.r16(TR, ld16(g.Hc + 2 * g.Z, kd));
+    g.H1 = b.r16(TR, ld16(g.Hc, kd));
+    g.H2 = b.r16(TR, ld16(g.Hc, kd));
+    if (prec == PREC_F32) {
+        // fp32 images: the backward's dP images overlay CAT and its fp32 dY
+        // overlays H1 | H2 -- all four are dead once the forward has read them
+        // (act' comes from the fp32 activations in HBM); leftover values in
+        // the padding columns are finite and meet zero weights
+        if (!alias_pair(g.CAT, ld16(g.Hc, kd), g.DP0, g.DP1) || !alias32(g.H1, g.H2, g.Hc, g.DY)) return EXO_EINVAL;
+    } else {
+        g.DP0 = b.r16(TR, ld16(g.Hc));
+        g.DP1 = b.r16(TR, ld16(g.Hc));
+    }
     g.H0 = b.r32(TR, g.Hc);
-    g.DY = b.r32(TR, g.Hc);
+    if (prec != PREC_F32) g.DY = b.r32(TR, g.Hc);
     g.F = b.r32(TR, 16);
     g.TW = b.r32(1, g.Hc);
     const R32 sm = b.r32(1, 2 * TR);
@@ -816,14 +869,21 @@ int td7f_encoder(int32_t prec, const int32_t *act, const td7f_lin *enc, const fl
         return EXO_EINVAL;
     g.mse_scale = 2.0f / ((float)B * (float)g.Z);
     g.ld = ld;
-    const int w = std::max(g.Z, g.He);
+    const int w = std::max(g.Z, g.He), kd = kd_of(prec);
     Bump b(1);
-    g.X = b.r16(TR, ld16(g.S));
-    g.H1 = b.r16(TR, ld16(g.He));
-    g.H2 = b.r16(TR, ld16(g.He));
-    g.CATZ = b.r16(TR, ld16(g.Z + g.A));
-    g.DP0 = b.r16(TR, ld16(w));
-    g.DP1 = b.r16(TR, ld16(w));
+    g.X = b.r16(TR, ld16(g.S, kd));
+    g.H1 = b.r16(TR, ld16(g.He, kd));
+    g.H2 = b.r16(TR, ld16(g.He, kd));
+    g.CATZ = b.r16(TR, ld16(g.Z + g.A, kd));
+    if (prec == PREC_F32 && ld16(w, kd) <= g.H1.ld) {
+        // fp32: the backward's dP images overlay H1 / H2 (dead once zsa3's
+        // forward has read H2; act' comes from the activations in HBM)
+        g.DP0 = R16{g.H1.off, ld16(w, kd)};
+        g.DP1 = R16{g.H2.off, ld16(w, kd)};
+    } else {
+        g.DP0 = b.r16(TR, ld16(w, kd));
+        g.DP1 = b.r16(TR, ld16(w, kd));
+    }
     g.H3 = b.r32(TR, g.Z);
     g.NZ = b.r32(TR, w);
     g.DY = b.r32(TR, w);
@@ -879,31 +939,40 @@ int td7f_actor(int32_t prec, int32_t phase, const int32_t *act, const td7f_lin *
         g.yc[i] = u.yc[i];
     }
     g.da = u.da; g.dzsa = u.dzsa; g.ld = ld;
-    const int hmax = std::max(g.Ha, std::max(g.He, g.Hc));
+    const int hmax = std::max(g.Ha, std::max(g.He, g.Hc)), kd = kd_of(prec);
     Bump b(1);
     if (phase == 0) {
-        g.X = b.r16(TR, ld16(g.S));
-        g.CATA = b.r16(TR, ld16(g.Ha + g.Z));
-        g.CATZ = b.r16(TR, ld16(g.Z + g.A));
-        g.H1 = b.r16(TR, ld16(hmax));
-        g.H2 = b.r16(TR, ld16(hmax));
+        g.X = b.r16(TR, ld16(g.S, kd));
+        g.CATA = b.r16(TR, ld16(g.Ha + g.Z, kd));
+        g.CATZ = b.r16(TR, ld16(g.Z + g.A, kd));
+        g.H1 = b.r16(TR, ld16(hmax, kd));
+        g.H2 = b.r16(TR, ld16(hmax, kd));
         g.H0 = b.r32(TR, g.Ha);
         g.F = b.r32(TR, 16);
         g.TW = b.r32(THIN_NC, g.Ha);
     } else if (phase == 1) {
-        g.X = b.r16(TR, ld16(g.S + g.A));
-        g.CAT = b.r16(TR, ld16(g.Hc + 2 * g.Z));
-        g.H1 = b.r16(TR, ld16(g.Hc));
-        g.H2 = b.r16(TR, ld16(g.Hc));
-        g.DP0 = b.r16(TR, ld16(g.Hc));
-        g.DP1 = b.r16(TR, ld16(g.Hc));
+        g.X = b.r16(TR, ld16(g.S + g.A, kd));
+        g.CAT = b.r16(TR, ld16(g.Hc + 2 * g.Z, kd));
+        g.H1 = b.r16(TR, ld16(g.Hc, kd));
+        g.H2 = b.r16(TR, ld16(g.Hc, kd));
+        if (prec == PREC_F32) {
+            // fp32 (as td7f_critic): dP images and the thin weights (staged
+            // after q1's forward) in CAT, dY over H1 | H2
+            if (!alias_pair(g.CAT, ld16(g.Hc, kd), g.DP0, g.DP1) || !alias32(g.H1, g.H2, g.Hc, g.DY)) return EXO_EINVAL;
+            const int tw = g.DP1.off + round_up(TR * g.DP1.ld * 2, 16);
+            g.TW = R32{tw, g.Hc};
+            if (tw + THIN_NC * g.Hc * 4 > g.CAT.off + TR * g.CAT.ld * 2) return EXO_EINVAL;
+        } else {
+            g.DP0 = b.r16(TR, ld16(g.Hc));
+            g.DP1 = b.r16(TR, ld16(g.Hc));
+        }
         g.H0 = b.r32(TR, g.Hc);
-        g.DY = b.r32(TR, g.Hc);
+        if (prec != PREC_F32) g.DY = b.r32(TR, g.Hc);
         g.F = b.r32(TR, 16);
-        g.TW = b.r32(THIN_NC, g.Hc);
+        if (prec != PREC_F32) g.TW = b.r32(THIN_NC, g.Hc);
     } else {
-        g.DP0 = b.r16(TR, ld16(std::max(hmax, g.Z)));
-        g.DP1 = b.r16(TR, ld16(std::max(hmax, g.Z)));
+        g.DP0 = b.r16(TR, ld16(std::max(hmax, g.Z), kd));
+        g.DP1 = b.r16(TR, ld16(std::max(hmax, g.Z), kd));
         g.H0 = b.r32(TR, g.Ha);
         g.DY = b.r32(TR, g.Ha);
         g.F = b.r32(TR, 16);
@@ -932,8 +1001,8 @@ static int wgrad_args(int32_t prec, int32_t njobs, const td7f_wg_job *jobs, int6
         const td7f_wg_job &J = jobs[q];
         if (!J.dp || !J.x || !J.dw || J.n <= 0 || J.k <= 0 || (J.db && (!J.part || J.row_tiles <= 0))) return EXO_EINVAL;
         WgJob &w = g.j[q];
-        w.dp = (const uint16_t *)J.dp;
-        w.x = (const uint16_t *)J.x;
+        w.dp = (const char *)J.dp;
+        w.x = (const char *)J.x;
         w.part = J.part;
         w.dw = J.dw;
         w.db = J.db;
@@ -961,7 +1030,8 @@ int td7f_wgrad(int32_t prec, int32_t njobs, const td7f_wg_job *jobs, int64_t ld,
     const hipStream_t st = (hipStream_t)stream;
     const dim3 grid(g.total + (prio ? 1 : 0));
     if (prec == PREC_BF16) hipLaunchKernelGGL((wgrad_kernel<PREC_BF16, false>), grid, dim3(256), 0, st, g);
-    else hipLaunchKernelGGL((wgrad_kernel<PREC_F16, false>), grid, dim3(256), 0, st, g);
+    else if (prec == PREC_F16) hipLaunchKernelGGL((wgrad_kernel<PREC_F16, false>), grid, dim3(256), 0, st, g);
+    else hipLaunchKernelGGL((wgrad_kernel<PREC_F32, false>), grid, dim3(256), 0, st, g);
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 
@@ -985,7 +1055,7 @@ int td7f_wgrad_adam(int32_t prec, int32_t njobs, const td7f_wg_job *jobs, int64_
         const td7f_wg_job &J = jobs[q];
         // every layer: weight, bias (its gradient db required) and forward operand
         if (A.opt < 0 || A.opt >= nopt || A.w_off < 0 || A.b_off < 0 || !J.db || !A.wf ||
-            A.ksf * 32 < J.k || (A.wb && A.ksb * 32 < J.n))
+            A.ksf * kd_of(prec) < J.k || (A.wb && A.ksb * kd_of(prec) < J.n))
             return EXO_EINVAL;
         WgJob &w = g.j[q];
         w.w_off = A.w_off;
@@ -999,7 +1069,8 @@ int td7f_wgrad_adam(int32_t prec, int32_t njobs, const td7f_wg_job *jobs, int64_
     const hipStream_t st = (hipStream_t)stream;
     const dim3 grid(g.total + (prio ? 1 : 0));
     if (prec == PREC_BF16) hipLaunchKernelGGL((wgrad_kernel<PREC_BF16, true>), grid, dim3(256), 0, st, g);
-    else hipLaunchKernelGGL((wgrad_kernel<PREC_F16, true>), grid, dim3(256), 0, st, g);
+    else if (prec == PREC_F16) hipLaunchKernelGGL((wgrad_kernel<PREC_F16, true>), grid, dim3(256), 0, st, g);
+    else hipLaunchKernelGGL((wgrad_kernel<PREC_F32, true>), grid, dim3(256), 0, st, g);
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 

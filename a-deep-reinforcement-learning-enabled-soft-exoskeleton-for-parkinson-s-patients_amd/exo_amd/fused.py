@@ -1,10 +1,12 @@
 """Row-tile-fused TD7 networks on the GPU (csrc/td7_fused.hip): the host side.
 
-With bf16 / fp16 MFMA operands the TD7 nets of Agent/TD7_multi_agent.py:61-140
-run as whole-network launches (one workgroup per 16 rows, activations in LDS)
-instead of one launch per Linear.  Their weights are read from packed 16-bit
-copies in MFMA-fragment order (PackedLinear), refreshed by td7f_pack after every
-change of the fp32 master weights (optimiser steps, target refreshes, loads).
+With bf16 / fp16 MFMA operands -- and, behind EXO_FUSED_F32=1, exact fp32
+ones (v_mfma_f32_16x16x4_f32, the reference's precision) -- the TD7 nets of
+Agent/TD7_multi_agent.py:61-140 run as whole-network launches (one workgroup
+per 16 rows, activations in LDS) instead of one launch per Linear.  Their
+weights are read from packed copies in MFMA-fragment order (PackedLinear),
+refreshed by td7f_pack after every change of the fp32 master weights
+(optimiser steps, target refreshes, loads).
 
 FusedNets owns the packed copies of every net the update reads and the
 launch wrappers; TD7Learner routes its passes here when `fused` is on.
@@ -21,15 +23,24 @@ PD = 5  # include/exo_amd.h TD7F_PD
 NW = 4  # waves per fused workgroup (csrc/td7_fused.h)
 MAX_PACK = 32
 MAX_ADAM_PACK = 16  # include/exo_amd.h TD7F_MAX_ADAM_PACK
-PREC = {"bf16": 1, "fp16": 2}
+PREC = {"bf16": 1, "fp16": 2, "fp32": 3}
+# inputs per k-step (64 bytes of a row): 32 16-bit or 16 fp32 operands
+KD = {1: 32, 2: 32, 3: 16}
+# the fp32 fused path (csrc/td7_fused.h Ty<PREC_F32>); EXO_FUSED_F32=1 turns it on
+FUSED_F32 = os.environ.get("EXO_FUSED_F32", "0") == "1"
 
 
 TD7FLin, TD7FPackJob, TD7FNoise = nat.TD7FLin, nat.TD7FPackJob, nat.TD7FNoise
 
 
-def _ks(k):
-    """k-steps of a packed operand: ceil(k / 32) rounded up to TD7F_PD."""
-    return -(-(-(-k // 32)) // PD) * PD
+def _ks(k, kd=32):
+    """k-steps of a packed operand: ceil(k / kd) rounded up to TD7F_PD."""
+    return -(-(-(-k // kd)) // PD) * PD
+
+
+def _etype(prec):
+    """torch dtype of an operand-type buffer (bit storage)."""
+    return torch.float32 if prec == 3 else torch.int16
 
 
 def _tiles(n):
@@ -39,18 +50,20 @@ def _tiles(n):
 
 
 class PackedLinear:
-    """The 16-bit packed operands of one Linear W [N, K] (a view of the fp32
-    master weight; one head of a stacked critic layer is a slice): the forward
-    operand and, with bwd=True, the dX operand."""
+    """The packed operands of one Linear W [N, K] (a view of the fp32 master
+    weight; one head of a stacked critic layer is a slice) in the operand type
+    of prec: the forward operand and, with bwd=True, the dX operand (16 bytes
+    per lane per 64-lane block either way)."""
 
-    def __init__(self, weight, bias, bwd):
+    def __init__(self, weight, bias, bwd, prec=1):
         N, K = weight.shape
         dev = weight.device
+        kd = KD[prec]
         self.weight, self.bias = weight, bias
         self.N, self.K = N, K
-        self.ksf, self.ntf = _ks(K), _tiles(N)
+        self.ksf, self.ntf = _ks(K, kd), _tiles(N)
         self.wf = torch.zeros(self.ntf * self.ksf * 64 * 8, dtype=torch.int16, device=dev)
-        self.ksb = _ks(N) if bwd else 0
+        self.ksb = _ks(N, kd) if bwd else 0
         self.ntb = -(-(-(-K // 16)) // NW) * NW if bwd else 0
         self.wb = torch.zeros(self.ntb * self.ksb * 64 * 8, dtype=torch.int16, device=dev) if bwd else None
         assert weight.stride(1) == 1
@@ -72,7 +85,7 @@ class PackedNet:
     """Packed copies of a set of Linears, refreshed together by one td7f_pack launch."""
 
     def __init__(self, layers, prec, bwd=False):
-        self.layers = [PackedLinear(w, b, bwd) for w, b in layers]
+        self.layers = [PackedLinear(w, b, bwd, prec) for w, b in layers]
         self.prec = prec
         self.array = _lin_array(self.layers)
 
@@ -116,14 +129,16 @@ def critic_layers(critic):
 
 
 def supported(learner):
-    """The fused path applies: GPU, bf16/fp16 operands, the reference's
-    activations, and every hidden width (zs_dim, enc_hdim, critic_hdim,
-    actor_hdim) a multiple of 4 in 241..320 -- 16-wide tiles per wave of 4 or 5
-    (NW = 4 waves), all widths in the same tile class.  Anything else (the
-    wide configuration, fp32 operands, widths below 241) runs the per-layer
-    kernels."""
+    """The fused path applies: GPU, bf16/fp16 operands (fp32 with
+    EXO_FUSED_F32=1), the reference's activations, and every hidden width
+    (zs_dim, enc_hdim, critic_hdim, actor_hdim) a multiple of 4 in 241..320 --
+    16-wide tiles per wave of 4 or 5 (NW = 4 waves), all widths in the same
+    tile class.  Anything else (the wide configuration, widths below 241)
+    runs the per-layer kernels."""
     hp = learner.hp
     if learner.device.type != "cuda" or learner.precision not in PREC:
+        return False
+    if learner.precision == "fp32" and not FUSED_F32:
         return False
     acts = [ops.act_code(f) for f in (hp.enc_activ, hp.actor_activ, hp.critic_activ)]
     if any(a is None or a == ops.ACT_CODES["tanh"] for a in acts):
@@ -266,7 +281,7 @@ class FusedNets:
         if buf is None or buf.shape[0] < B:
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("FusedNets.target: run once eagerly before graph capture")
-            buf = self._tgt_img = torch.empty((B, -(-(2 * Z + A) // 8) * 8), dtype=torch.int16, device=self.dev)
+            buf = self._tgt_img = torch.empty((B, -(-(2 * Z + A) // 8) * 8), dtype=_etype(self.prec), device=self.dev)
         return buf
 
     @torch.no_grad()
@@ -307,13 +322,14 @@ class FusedNets:
 
 
 class XTBuffers:
-    """The transposed 16-bit weight-gradient operands of one Linear (include/exo_amd.h td7f_xt)."""
+    """The transposed weight-gradient operands of one Linear in the operand
+    type (include/exo_amd.h td7f_xt)."""
 
-    def __init__(self, N, K, B, ld, dev):
+    def __init__(self, N, K, B, ld, dev, prec=1):
         r64 = lambda n: -(-n // 64) * 64  # noqa: E731
         self.N, self.K = N, K
-        self.x = torch.zeros((r64(K), ld), dtype=torch.int16, device=dev)
-        self.dp = torch.zeros((r64(N), ld), dtype=torch.int16, device=dev)
+        self.x = torch.zeros((r64(K), ld), dtype=_etype(prec), device=dev)
+        self.dp = torch.zeros((r64(N), ld), dtype=_etype(prec), device=dev)
         self.part = torch.zeros((-(-B // 16), N), dtype=torch.float32, device=dev)
         self.c = nat.TD7FXT(self.x.data_ptr(), self.dp.data_ptr(), self.part.data_ptr())
 
@@ -347,9 +363,10 @@ class FusedTrain:
         S = L.actor.l0.in_features
         self.S, self.A = S, A
         f32 = dict(dtype=torch.float32, device=dev)
-        self.xt_enc = [XTBuffers(pl.N, pl.K, B, self.ld, dev) for pl in nets.nets["encoder"].layers]
-        self.xt_critic = [XTBuffers(pl.N, pl.K, B, self.ld, dev) for pl in nets.nets["critic"].layers]
-        self.xt_actor = [XTBuffers(pl.N, pl.K, B, self.ld, dev) for pl in nets.nets["actor"].layers]
+        p = nets.prec
+        self.xt_enc = [XTBuffers(pl.N, pl.K, B, self.ld, dev, p) for pl in nets.nets["encoder"].layers]
+        self.xt_critic = [XTBuffers(pl.N, pl.K, B, self.ld, dev, p) for pl in nets.nets["critic"].layers]
+        self.xt_actor = [XTBuffers(pl.N, pl.K, B, self.ld, dev, p) for pl in nets.nets["actor"].layers]
         self.y_enc = [torch.empty((B, He), **f32) for _ in range(4)]
         self.y_critic = [torch.empty((2, B, Hc), **f32) for _ in range(2)]
         self.td = torch.zeros((B, 2), **f32)

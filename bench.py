@@ -520,17 +520,25 @@ def dp_layout(trainer):
 
 def td7_variants(env, dev, args, iters=60, warmup=8):
     """Sub-lines next to the bf16 headline (configs[1]): the same training
-    iteration with exact fp32 TD7 (the reference's precision) and with the
+    iteration with exact fp32 TD7 (the reference's precision) -- per-layer
+    kernels and the row-tile-fused passes with fp32 operands -- and with the
     256-wide alias of BASELINE configs[1]'s "256-wide MLPs" wording, each on a
     fresh graph-replayed trainer over the same envs: ms per iteration."""
+    from exo_amd import fused
     from exo_amd.rollout import VecTrainer
     from exo_amd.td7 import Agent, Hyperparameters
     out = {}
-    for name, hp, prec in (("fp32_300_320", Hyperparameters(), "fp32"),
-                           ("bf16_alias256", Hyperparameters(zs_dim=256, enc_hdim=256, critic_hdim=256,
-                                                             actor_hdim=256), "bf16")):
+    f0 = fused.FUSED_F32
+    for name, hp, prec, f32 in (("fp32_300_320", Hyperparameters(), "fp32", False),
+                                ("fp32_fused_300_320", Hyperparameters(), "fp32", True),
+                                ("bf16_alias256", Hyperparameters(zs_dim=256, enc_hdim=256, critic_hdim=256,
+                                                                  actor_hdim=256), "bf16", False)):
         torch.manual_seed(1)
-        ag = Agent(80, 7, 1, env_num=8, hp=hp, device=dev, precision=prec, n_envs=env.n, graph_safe=True)
+        fused.FUSED_F32 = f32
+        try:
+            ag = Agent(80, 7, 1, env_num=8, hp=hp, device=dev, precision=prec, n_envs=env.n, graph_safe=True)
+        finally:
+            fused.FUSED_F32 = f0
         tr = VecTrainer(env, ag, use_graphs=True)
         for _ in range(warmup):
             tr.step()
@@ -540,6 +548,7 @@ def td7_variants(env, dev, args, iters=60, warmup=8):
             tr.step()
         torch.cuda.synchronize()
         out[name] = {"ms_per_iteration": (time.perf_counter() - t0) / iters * 1e3, "precision": prec,
+                     "fused": ag.learner.fused is not None,
                      "widths": [hp.zs_dim, hp.enc_hdim, hp.critic_hdim, hp.actor_hdim], "iterations": iters}
         del tr, ag
     return out

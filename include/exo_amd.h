@@ -573,17 +573,19 @@ int td7_dense_bwd_weight(const float *dy_dev, long dysg, long lddy, const float 
                          int32_t m, int32_t n, int32_t k, int32_t act, void *stream);
 
 /* ---------------------------------------------------------------------------
- * Row-tile-fused TD7 networks (csrc/td7_fused.hip), bf16 / fp16 MFMA operands
- * (prec 1 / 2).  One workgroup owns 16 (select: 32) rows and runs a whole
- * network pass of Agent/TD7_multi_agent.py on them with the activations in
- * LDS; weights are read from packed 16-bit copies (td7f_pack, refreshed after
- * every optimiser step / target copy).  Widths: hidden <= 320, inputs <= 1,008. */
+ * Row-tile-fused TD7 networks (csrc/td7_fused.hip), bf16 / fp16 / fp32 MFMA
+ * operands (prec 1 / 2 / 3).  One workgroup owns 16 (select: 32) rows and runs
+ * a whole network pass of Agent/TD7_multi_agent.py on them with the
+ * activations in LDS; weights are read from packed copies in the operand type
+ * (td7f_pack, refreshed after every optimiser step / target copy).  Widths:
+ * hidden <= 320, inputs <= 1,008.  A k-step is 32 inputs of a 16-bit operand
+ * or 16 of an fp32 one (64 bytes per row either way): "kd" below. */
 #define TD7F_PD 5          /* k-steps of weight loads in flight; packed k-steps are multiples of it */
 #define TD7F_MAX_PACK 32
 
 /* One nn.Linear: packed operands + fp32 bias.  ksf = k-steps of the forward
- * operand (ceil(n_in/32) rounded up to TD7F_PD), ksb = k-steps of the dX
- * operand (ceil(n_out/32) rounded up to TD7F_PD). */
+ * operand (ceil(n_in/kd) rounded up to TD7F_PD), ksb = k-steps of the dX
+ * operand (ceil(n_out/kd) rounded up to TD7F_PD). */
 typedef struct {
     const void *wf;
     const void *wb;
@@ -646,21 +648,21 @@ int td7f_select(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7
  * next_action = actor_target(s', zs) + clipped noise, fixed_target_zsa and both
  * heads of critic_target -> qt_dev [B][2].  tenc: zs1..zs3, zsa1..zsa3;
  * tcritic: [layer][head] (8).  tgt_img_dev: [B][round_up(2 zs_dim + A, 8)]
- * 16-bit scratch ([zsa | zs | next_action] per row). */
+ * scratch in the operand type ([zsa | zs | next_action] per row). */
 int td7f_target(int32_t prec, const int32_t *act, const td7f_lin *tenc, const td7f_lin *tactor,
                 const td7f_lin *tcritic, const float *next_state_dev, int32_t B, const td7f_noise *noise,
-                uint16_t *tgt_img_dev, float *qt_dev, void *stream);
+                void *tgt_img_dev, float *qt_dev, void *stream);
 /* fixed_zs = fixed_encoder.zs(state), fixed_zsa = fixed_encoder.zsa(fixed_zs,
  * action) (TD7_multi_agent.py:248-249) -> fp32 [B][zs_dim] each. */
 int td7f_fixed(int32_t prec, const int32_t *act, const td7f_lin *fenc, const float *state_dev,
                const float *action_dev, int32_t B, float *zs_dev, float *zsa_dev, void *stream);
 
 /* The gradient passes (csrc/td7_fused_train.hip).  Each leaves, per trained
- * layer, the transposed 16-bit operands of its weight gradient -- the layer
- * input X^T [round_up(n_in, 64)][ld] and dP^T = (dY act'(Y))^T [round_up(n_out,
- * 64)][ld] (x 1024 at fp16), ld = the batch padded to 256, stored in 1 KiB
- * MFMA-fragment blocks of 16 operand rows x 32 batch rows (csrc/td7_fused.h
- * blk8), padding zero -- and fp32 column sums of dP per 16-row tile (part
+ * layer, the transposed operands of its weight gradient (operand type) -- the
+ * layer input X^T [round_up(n_in, 64)][ld] and dP^T = (dY act'(Y))^T
+ * [round_up(n_out, 64)][ld] (x 1024 at fp16), ld = the batch padded to 256,
+ * stored in 1 KiB MFMA-fragment blocks of 16 operand rows x kd batch rows
+ * (csrc/td7_fused.h blk8 / blk4), padding zero -- and fp32 column sums of dP per 16-row tile (part
  * [ceil(B/16)][n_out]); td7f_wgrad turns them into dW and db. */
 typedef struct {
     void *x;

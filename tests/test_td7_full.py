@@ -71,12 +71,19 @@ def _cpu_learner(name="td7_full"):
     return TD7Learner(80, 7, hp, learning_steps=TD7_FULL_LEARNING_STEPS, device="cpu", fused_adam=False)
 
 
-def _learner(device, precision="fp32", golden="td7_full"):
+def _learner(device, precision="fp32", golden="td7_full", fused_f32=False):
     L = _cpu_learner(golden)
     if device == "cpu":
         L2 = L
     else:
-        L2 = TD7Learner(80, 7, L.hp, learning_steps=TD7_FULL_LEARNING_STEPS, device=device, precision=precision)
+        from exo_amd import fused
+        f0 = fused.FUSED_F32
+        fused.FUSED_F32 = fused_f32  # read when the learner builds its fused nets
+        try:
+            L2 = TD7Learner(80, 7, L.hp, learning_steps=TD7_FULL_LEARNING_STEPS, device=device, precision=precision)
+        finally:
+            fused.FUSED_F32 = f0
+        assert (L2.fused is not None) == (fused_f32 or precision != "fp32") or golden != "td7_full"
         for name in ("actor", "critic", "encoder", "actor_target", "critic_target", "fixed_encoder",
                      "fixed_encoder_target"):
             getattr(L2, name).load_state_dict(getattr(L, name).state_dict())
@@ -256,11 +263,11 @@ def _free_run(golden):
     return _EXACT[golden]
 
 
-def _run(device, precision="fp32", golden="td7_full"):
+def _run(device, precision="fp32", golden="td7_full", fused_f32=False):
     g = _golden(golden)
     free = _free_run(golden)
     tol = TOL[precision]
-    L = _learner(device, precision, golden)
+    L = _learner(device, precision, golden, fused_f32)
     X = _f64_learner(golden)  # teacher-forced restatement, reloaded from L before every phase
     rounding = _rounded_matmuls(ROUND[precision]) if ROUND[precision] is not None else None
     init = {}
@@ -365,6 +372,15 @@ def test_three_train_steps_at_bench_shape_gpu(precision):
     shape, exact fp32 MFMA and the bench's bf16 operands."""
     rep = _run("cuda", precision)
     print(precision, {k: f"{v:.2e}" for k, v in rep.items() if not isinstance(v, tuple)})
+
+
+@pytest.mark.gpu
+def test_three_train_steps_at_bench_shape_gpu_fused_fp32():
+    """The row-tile-fused passes with exact fp32 operands (EXO_FUSED_F32,
+    csrc/td7_fused.h Ty<PREC_F32>: v_mfma_f32_16x16x4_f32, fp32 images and
+    weight-gradient operands) against the same golden at the fp32 bounds."""
+    rep = _run("cuda", "fp32", fused_f32=True)
+    print("fp32 fused", {k: f"{v:.2e}" for k, v in rep.items() if not isinstance(v, tuple)})
 
 
 @pytest.mark.gpu
