@@ -91,9 +91,11 @@ template <> struct Ty<PREC_F16> : Ty16 {
 template <> struct Ty<PREC_F32> {
     using E = float;
     static constexpr int EB = 4, KD = 16, SUB = 4;
+    // (the vectors are bit-cast whole, then indexed: bit_cast(float, a[j]) of a
+    // u32x4 element compiled to a[0] for every j -- tools/mfma_f32_probe.hip)
     static __device__ __forceinline__ floatx4 mfma(u32x4 a, u32x4 b, floatx4 c, int j) {
-        return __builtin_amdgcn_mfma_f32_16x16x4f32(__builtin_bit_cast(float, a[j]), __builtin_bit_cast(float, b[j]), c,
-                                                    0, 0, 0);
+        const floatx4 af = __builtin_bit_cast(floatx4, a), bf = __builtin_bit_cast(floatx4, b);
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(af[j], bf[j], c, 0, 0, 0);
     }
     static __device__ __forceinline__ float bits(float v) { return v; }
     static __device__ __forceinline__ float val(float b) { return b; }

@@ -1,7 +1,7 @@
 """Row-tile-fused TD7 networks on the GPU (csrc/td7_fused.hip): the host side.
 
-With bf16 / fp16 MFMA operands -- and, behind EXO_FUSED_F32=1, exact fp32
-ones (v_mfma_f32_16x16x4_f32, the reference's precision) -- the TD7 nets of
+With bf16 / fp16 MFMA operands -- and exact fp32 ones (v_mfma_f32_16x16x4_f32,
+the reference's precision; EXO_FUSED_F32=0 keeps fp32 per layer) -- the TD7 nets of
 Agent/TD7_multi_agent.py:61-140 run as whole-network launches (one workgroup
 per 16 rows, activations in LDS) instead of one launch per Linear.  Their
 weights are read from packed copies in MFMA-fragment order (PackedLinear),
@@ -26,8 +26,10 @@ MAX_ADAM_PACK = 16  # include/exo_amd.h TD7F_MAX_ADAM_PACK
 PREC = {"bf16": 1, "fp16": 2, "fp32": 3}
 # inputs per k-step (64 bytes of a row): 32 16-bit or 16 fp32 operands
 KD = {1: 32, 2: 32, 3: 16}
-# the fp32 fused path (csrc/td7_fused.h Ty<PREC_F32>); EXO_FUSED_F32=1 turns it on
-FUSED_F32 = os.environ.get("EXO_FUSED_F32", "0") == "1"
+# the fp32 fused path (csrc/td7_fused.h Ty<PREC_F32>): 0.50 vs 0.79 ms per
+# configs[1] iteration per layer, parity-tested against the reference golden at
+# the fp32 bounds (tests/test_td7_full.py); EXO_FUSED_F32=0 runs fp32 per layer
+FUSED_F32 = os.environ.get("EXO_FUSED_F32", "1") == "1"
 
 
 TD7FLin, TD7FPackJob, TD7FNoise = nat.TD7FLin, nat.TD7FPackJob, nat.TD7FNoise
@@ -129,8 +131,8 @@ def critic_layers(critic):
 
 
 def supported(learner):
-    """The fused path applies: GPU, bf16/fp16 operands (fp32 with
-    EXO_FUSED_F32=1), the reference's activations, and every hidden width
+    """The fused path applies: GPU, bf16/fp16/fp32 operands (fp32 unless
+    EXO_FUSED_F32=0), the reference's activations, and every hidden width
     (zs_dim, enc_hdim, critic_hdim, actor_hdim) a multiple of 4 in 241..320 --
     16-wide tiles per wave of 4 or 5 (NW = 4 waves), all widths in the same
     tile class.  Anything else (the wide configuration, widths below 241)

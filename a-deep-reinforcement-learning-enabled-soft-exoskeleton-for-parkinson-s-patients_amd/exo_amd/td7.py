@@ -578,9 +578,9 @@ class TD7Learner:
         self._device_rng = os.environ.get("EXO_DEVICE_RNG", "1") != "0"
         self._noise_rng = ops.DeviceRNG(self.device, 1) if self.device.type == "cuda" else None
         self._explore_rng = ops.DeviceRNG(self.device, 2) if self.device.type == "cuda" else None
-        # bf16/fp16 on the GPU: whole-network fused launches (exo_amd/fused.py,
-        # csrc/td7_fused.hip) over packed 16-bit weight copies; EXO_TD7_FUSED=0
-        # keeps the per-layer kernels
+        # on the GPU: whole-network fused launches (exo_amd/fused.py,
+        # csrc/td7_fused.hip) over packed weight copies in the operand type
+        # (bf16 / fp16 / fp32); EXO_TD7_FUSED=0 keeps the per-layer kernels
         self.fused = None
         if os.environ.get("EXO_TD7_FUSED", "1") != "0" and self._device_rng:
             from . import fused as _fused

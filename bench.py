@@ -520,8 +520,9 @@ def dp_layout(trainer):
 
 def td7_variants(env, dev, args, iters=60, warmup=8):
     """Sub-lines next to the bf16 headline (configs[1]): the same training
-    iteration with exact fp32 TD7 (the reference's precision) -- per-layer
-    kernels and the row-tile-fused passes with fp32 operands -- and with the
+    iteration with exact fp32 TD7 (the reference's precision) -- the
+    row-tile-fused passes with fp32 operands (the default) and the per-layer
+    kernels (EXO_FUSED_F32=0) -- and with the
     256-wide alias of BASELINE configs[1]'s "256-wide MLPs" wording, each on a
     fresh graph-replayed trainer over the same envs: ms per iteration."""
     from exo_amd import fused
@@ -529,8 +530,8 @@ def td7_variants(env, dev, args, iters=60, warmup=8):
     from exo_amd.td7 import Agent, Hyperparameters
     out = {}
     f0 = fused.FUSED_F32
-    for name, hp, prec, f32 in (("fp32_300_320", Hyperparameters(), "fp32", False),
-                                ("fp32_fused_300_320", Hyperparameters(), "fp32", True),
+    for name, hp, prec, f32 in (("fp32_300_320", Hyperparameters(), "fp32", True),
+                                ("fp32_per_layer_300_320", Hyperparameters(), "fp32", False),
                                 ("bf16_alias256", Hyperparameters(zs_dim=256, enc_hdim=256, critic_hdim=256,
                                                                   actor_hdim=256), "bf16", False)):
         torch.manual_seed(1)
