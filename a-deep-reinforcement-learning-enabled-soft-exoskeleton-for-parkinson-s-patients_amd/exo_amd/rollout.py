@@ -829,11 +829,14 @@ class RefScheduleTrainer(VecTrainer):
         # 4,096-env rollout round, profiles/r03_refsched_raw): the select_action
         # workgroups hold every CU, so the overlapped insert kernels wait for
         # CUs (lap_add 9 -> 34 us) and the next env step waits for them
-        # EXO_REF_ROUND_GRAPH=2 (round_graph="serial"): the round graph with each
-        # step's insert in line (no branch), so the only change from the per-step
-        # replays is one graph launch per round instead of one per step
-        if round_graph is None:  # EXO_REF_ROUND_GRAPH=1: the round graph
-            round_graph = {"1": True, "2": "serial"}.get(os.environ.get("EXO_REF_ROUND_GRAPH", "0"), False)
+        # EXO_REF_ROUND_GRAPH=2 (round_graph="serial", the default since r04):
+        # the round graph with each step's insert in line (no branch), so the
+        # only change from the per-step replays is one graph launch per round
+        # instead of one per step -- with the one-launch insert + mask advance
+        # 28.80 vs 29.19-29.27 ms per 4,096-env rollout round
+        # (profiles/r04v_raw); EXO_REF_ROUND_GRAPH=0: per-step replays
+        if round_graph is None:  # EXO_REF_ROUND_GRAPH=1: the branch-overlapped round graph
+            round_graph = {"1": True, "2": "serial"}.get(os.environ.get("EXO_REF_ROUND_GRAPH", "2"), False)
         self.round_graph = bool(round_graph)
         self.round_overlap = round_graph != "serial"
         self._ins_stream = None
@@ -847,8 +850,9 @@ class RefScheduleTrainer(VecTrainer):
         # r04: that advance inside the replay insert's launch (its last
         # workgroup out); EXO_REF_INSERT_ADVANCE=0: its own launch
         self.insert_advance = os.environ.get("EXO_REF_INSERT_ADVANCE", "1") == "1"
-        # the burst steps' next-batch prefetch (VecTrainer._key); off until measured (EXO_BURST_PREFETCH=1)
-        self.burst_prefetch = os.environ.get("EXO_BURST_PREFETCH", "0") == "1"
+        # the burst steps' next-batch prefetch (VecTrainer._key): 74.7 vs
+        # 75.3-75.7 ms per 283-step burst (profiles/r04v_raw); EXO_BURST_PREFETCH=0: off
+        self.burst_prefetch = os.environ.get("EXO_BURST_PREFETCH", "1") == "1"
         self._burst_i = 0
         # the script's per-step tremor statistics (:149-205: exo_tremor_metrics
         # into a [round_len, N, 16] device record + per-env counters, 2
