@@ -851,8 +851,12 @@ class RefScheduleTrainer(VecTrainer):
         # workgroup out); EXO_REF_INSERT_ADVANCE=0: its own launch
         self.insert_advance = os.environ.get("EXO_REF_INSERT_ADVANCE", "1") == "1"
         # the burst steps' next-batch prefetch (VecTrainer._key): 74.7 vs
-        # 75.3-75.7 ms per 283-step burst (profiles/r04v_raw); EXO_BURST_PREFETCH=0: off
-        self.burst_prefetch = os.environ.get("EXO_BURST_PREFETCH", "1") == "1"
+        # 75.3-75.7 ms per 283-step burst (profiles/r04v_raw), bit-identical,
+        # but OFF: with it on, the full default bench segfaulted in the first
+        # graph replay of the trainer that runs after this one (sync_rounds,
+        # host side, inside hipGraphLaunch; profiles/r04seg_raw); off, the same
+        # bench runs clean.  EXO_BURST_PREFETCH=1 turns it on.
+        self.burst_prefetch = os.environ.get("EXO_BURST_PREFETCH", "0") == "1"
         self._burst_i = 0
         # the script's per-step tremor statistics (:149-205: exo_tremor_metrics
         # into a [round_len, N, 16] device record + per-env counters, 2
