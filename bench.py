@@ -740,6 +740,17 @@ def main():
             n = int(active_per_k.sum())
         return float(dt), n, its
 
+    # RCCL settle (data parallel on RCCL only): untimed iterations of the same
+    # trainer BEFORE the W warm-up steps.  The first RCCL process on a fresh box
+    # ran its first few hundred in-graph iterations at 0.45-0.53 ms instead of
+    # 0.32-0.33 (5 of 6 boxes; later processes and later trainers in the same
+    # process fast); 2,000 iterations of activity end it, idling does not
+    # (profiles/r04rccl_raw).  Reported as dist_settle_iterations.
+    settle = 0
+    if dist_on and backend == "nccl" and trainer is not None:
+        settle = int(os.environ.get("EXO_DIST_SETTLE_ITERS", "2000"))
+        for _ in range(settle):
+            one_step(False)
     for _ in range(args.warmup):
         one_step(False)
     torch.cuda.synchronize()
@@ -858,7 +869,7 @@ def main():
             "metric": "env steps/sec (batched exo sim) + TD7 grad-steps/sec at 1/2/4/8 MI355X",
             "value": round_value,
             "unit": "env-steps/s",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "dist_settle_iterations": settle,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f64" if agent is None else f"f64 sim + {args.precision} TD7",
