@@ -19,7 +19,10 @@ window's wall time.
 mode env: the env alone (random actions), for the sim-kernel roofline.
 
 Multi-GPU: one process per GPU (torchrun); envs shard with no exchange,
-TD7 gradients are all-reduced over RCCL (weak scaling).
+TD7 gradients are all-reduced over RCCL (weak scaling).  On RCCL the trainer
+first runs 2,000 untimed settle iterations, then the W warm-up steps
+(`dist_settle_iterations` in the line; DESIGN.md 7: the first RCCL process on
+a fresh box runs its first few hundred iterations ~45 % slow).
 """
 import argparse
 import json
