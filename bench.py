@@ -380,6 +380,24 @@ def fused_critic_timing(agent, reps=20, replays=10):
 REFERENCE_ENV_STEPS_PER_UPDATE = 2257 / 283
 
 
+def _release(tr):
+    """Drop a finished phase's graphs now, with the device idle (the caller
+    then deletes the trainer / agent and calls _collect): graph and memory-pool
+    teardown never runs inside a later phase's stream capture."""
+    torch.cuda.synchronize()
+    for name in ("graphs", "_round_graphs"):
+        g = getattr(tr, name, None)
+        if isinstance(g, dict):
+            g.clear()
+    torch.cuda.synchronize()
+
+
+def _collect():
+    import gc
+    gc.collect()
+    torch.cuda.synchronize()
+
+
 def sync_rounds(env, dev, args, hp, group=None, warm=40):
     """The same training loop with the script's synchronous episode rounds
     (VecTrainer episodes="sync": every env resets when the longest motion ends,
@@ -419,6 +437,9 @@ def sync_rounds(env, dev, args, hp, group=None, warm=40):
         dist.all_reduce(v, op=dist.ReduceOp.SUM, group=group)
         v[0] = dt[0]
     sec, total = float(v[0]), float(v[1])
+    _release(tr)
+    del tr, ag
+    _collect()
     return {"value": total / sec, "seconds": sec, "iterations": its, "ms_per_iteration": sec / its * 1e3,
             "active_env_steps": total,
             "note": "VecTrainer(episodes='sync'): one whole round incl. its reset, timed end to end after "
@@ -510,8 +531,14 @@ def reference_schedule(env, dev, args, hp, rounds=3, warm_rounds=3, group=None):
         "last_round": st,
         "note": "Exoskeleton_agent_train.py:149-205 per rollout step (exo_tremor_metrics + a row of the round's "
                 "device record, 2 launches) and :213-317 per round (one host sync), RefScheduleTrainer(stats=True)"}
-    ag.maybe_train_and_checkpoint = orig
+    # the timing wrapper removed (not re-assigned: an instance attribute holding
+    # the bound method would tie the agent into a reference cycle), then the
+    # trainer, its graphs and the agent freed HERE, not by a later garbage
+    # collection that could land inside the next phase's graph capture
+    del ag.maybe_train_and_checkpoint
+    _release(tr)
     del tr, ag
+    _collect()
     return out
 
 
@@ -554,7 +581,9 @@ def td7_variants(env, dev, args, iters=60, warmup=8):
         out[name] = {"ms_per_iteration": (time.perf_counter() - t0) / iters * 1e3, "precision": prec,
                      "fused": ag.learner.fused is not None,
                      "widths": [hp.zs_dim, hp.enc_hdim, hp.critic_hdim, hp.actor_hdim], "iterations": iters}
+        _release(tr)
         del tr, ag
+        _collect()
     return out
 
 
