@@ -129,3 +129,37 @@ def test_select_action_matches_per_layer(precision, width, n, rt, monkeypatch):
     assert _rel(out, ref) < _tol(precision), _rel(out, ref)
     # actions saturate at +-1 identically where the noise dominates
     assert float((out - ref).abs().max()) < (1e-4 if precision == "fp32" else 0.05)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_fused_trainer_graph_replay_equals_eager(precision):
+    """The graph-replayed training loop on the fused passes (fp32 operands:
+    the drop-in default; bf16: the bench) trains the nets bit-identically to
+    the same loop run eagerly -- both policy-update parities, a target refresh
+    (target_update_rate 5), the bench's widths."""
+    from exo_amd import VecExoskeletonEnv, fused
+    from exo_amd.rollout import VecTrainer
+    from exo_amd.td7 import Agent
+    out = []
+    for graphs in (False, True):
+        torch.manual_seed(7)
+        hp = Hyperparameters(batch_size=32, target_update_rate=5)
+        env = VecExoskeletonEnv(64, seed=7)
+        f0 = fused.FUSED_F32
+        fused.FUSED_F32 = True
+        try:
+            ag = Agent(80, 7, 1, hp=hp, env_num=8, precision=precision, n_envs=64, buffer_size=8192,
+                       graph_safe=graphs)
+        finally:
+            fused.FUSED_F32 = f0
+        assert ag.learner.fused is not None
+        tr = VecTrainer(env, ag, use_graphs=graphs)
+        for _ in range(12):
+            tr.step()
+        torch.cuda.synchronize()
+        out.append([p.detach().clone() for m in (ag.learner.actor, ag.learner.critic, ag.learner.encoder)
+                    for p in m.parameters()])
+        if graphs:
+            assert tr.graphs, "the graph-replayed trainer captured no graph"
+    for a, b in zip(*out):
+        torch.testing.assert_close(b, a, rtol=0, atol=0)
