@@ -4,11 +4,12 @@
 // (encoder zs/zsa, actor, twin critic) over B = 8 x 128 rows whose widths are
 // 300-320.  Layer-per-launch, every GEMM is latency bound (M = 1,024, N <= 320)
 // and the graph holds ~53 of them.  Here a workgroup owns 16 rows and runs a
-// whole network on them: activations stay in LDS (bf16/fp16, the MFMA operand
-// format), each wave streams its column tiles of every weight matrix straight
-// from L2 into registers in a pre-packed fragment order (one 1 KiB contiguous
-// block per 16-column tile and 32-deep k-step, written by td7_pack_weights),
-// and v_mfma_f32_16x16x32_{bf16,f16} accumulates in fp32.  Bias, activation,
+// whole network on them: activations stay in LDS (bf16 / fp16 / fp32, the MFMA
+// operand format), each wave streams its column tiles of every weight matrix
+// straight from L2 into registers in a pre-packed fragment order (one 1 KiB
+// contiguous block per 16-column tile and k-step -- 32 16-bit or 16 fp32
+// inputs -- written by td7f_pack), and v_mfma_f32_16x16x32_{bf16,f16} (fp32:
+// 4 x v_mfma_f32_16x16x4_f32 per k-step) accumulates in fp32.  Bias, activation,
 // AvgL1Norm, losses, noise and the backward's act' are fused epilogues; the
 // backward chains (dX) run in the same launch and leave the per-layer
 // gradient operands dP = dY act'(Y) (and the layer inputs X) transposed in
