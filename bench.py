@@ -20,7 +20,7 @@ mode env: the env alone (random actions), for the sim-kernel roofline.
 
 Multi-GPU: one process per GPU (torchrun); envs shard with no exchange,
 TD7 gradients are all-reduced over RCCL (weak scaling).  On RCCL the trainer
-first runs 2,000 untimed settle iterations, then the W warm-up steps
+first runs 3,000 untimed settle iterations, then the W warm-up steps
 (`dist_settle_iterations` in the line; DESIGN.md 7: the first RCCL process on
 a fresh box runs its first few hundred iterations ~45 % slow).
 """
@@ -777,10 +777,11 @@ def main():
     # ran its first few hundred in-graph iterations at 0.45-0.53 ms instead of
     # 0.32-0.33 (5 of 6 boxes; later processes and later trainers in the same
     # process fast); 2,000 iterations of activity end it, idling does not
-    # (profiles/r04rccl_raw).  Reported as dist_settle_iterations.
+    # (profiles/r04rccl_raw); 3,000 for margin.  Reported as
+    # dist_settle_iterations.
     settle = 0
     if dist_on and backend == "nccl" and trainer is not None:
-        settle = int(os.environ.get("EXO_DIST_SETTLE_ITERS", "2000"))
+        settle = int(os.environ.get("EXO_DIST_SETTLE_ITERS", "3000"))
         for _ in range(settle):
             one_step(False)
     for _ in range(args.warmup):
