@@ -748,7 +748,27 @@ def main():
         8(d) config 2 "whole rounds"): after the window, iterate untimed to the
         round boundary, then time exactly round_len iterations -- the first
         runs the episode reset -- bracketed by barrier + synchronize, max over
-        ranks.  Returns (seconds, active env-steps of this rank)."""
+        ranks.  Returns (seconds, active env-steps of this rank).  Async episodes:
+        there is no round boundary (every env resets in place when its own
+        episode ends), so exactly round_len (344) consecutive iterations, their
+        in-place resets included, are timed the same way."""
+        if trainer.episodes == "async":
+            torch.cuda.synchronize()
+            if dist_on:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            n = 0
+            for _ in range(round_len):
+                n += trainer.step()
+            torch.cuda.synchronize()
+            if dist_on:
+                dist.barrier()
+            torch.cuda.synchronize()
+            dt = torch.tensor([time.perf_counter() - t], device=dev, dtype=torch.float64)
+            if dist_on:
+                dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+            return float(dt), n, round_len
         while not trainer.next_step_resets():
             trainer.step()
         torch.cuda.synchronize()
@@ -814,7 +834,7 @@ def main():
         env.set_step_clock(False)
     # async episodes: no rounds (every env resets in place inside the timed
     # iterations), the window itself is the whole-job rate
-    measured_round = measured_round_timing() if trainer is not None and not async_eps else None
+    measured_round = measured_round_timing() if trainer is not None else None
     reset_ms = reset_timing()
     loop_kern_ms = None
     if ev:  # env mode: the timed launches themselves
@@ -930,8 +950,10 @@ def main():
             "measured_round": ({"seconds": measured_round[0], "iterations": measured_round[2],
                                 "active_env_steps_per_rank": measured_round[1],
                                 "value_over_measured": round_value / (world * measured_round[1] / measured_round[0]),
-                                "note": "one whole episode round (reset + round_len graph-replayed iterations) "
-                                        "timed end to end after the window, max over ranks"}
+                                "note": "one whole episode round timed end to end after the window, max over "
+                                        "ranks: sync episodes the reset + round_len graph-replayed iterations, "
+                                        "async episodes round_len consecutive iterations with their in-place "
+                                        "resets"}
                                if measured_round else None),
             "env_kernel_env_steps_per_sec": active_avg / (kern_ms * 1e-3),
             "roofline": {"kernel": ("exo_step_rp_kernel" if N <= 16384 else "exo_step_kernel")
