@@ -829,7 +829,7 @@ __device__ __forceinline__ void zero_lds(char *lds, int bytes) {
 // workgroup, which advances sigma and the call counter.
 template <int P>
 __device__ __forceinline__ void noise_rows(char *lds, R32 a, int A, int rows, int row0, int nrows, const Noise &nz,
-                                           float *out, R16 o1, int c1, R16 o2, int c2) {
+                                           float *out, R16 o1, int c1, R16 o2, int c2, bool ticket = true) {
     const float sg = ldg(nz.sigma);
     const unsigned long long call = ldg(nz.counter);
     for (int k = threadIdx.x; k < rows * A; k += NTH) {
@@ -857,7 +857,7 @@ __device__ __forceinline__ void noise_rows(char *lds, R32 a, int A, int rows, in
         if (o2.off >= 0) *pe<P>(lds, o2, row, c2 + c) = b;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (ticket && threadIdx.x == 0) {
         __threadfence();
         if (atomicAdd(nz.ticket, 1u) == gridDim.x * gridDim.y - 1) {
             *nz.sigma = sg - (nz.dec_count ? nz.sigma_dec * (float)*nz.dec_count : nz.sigma_dec);

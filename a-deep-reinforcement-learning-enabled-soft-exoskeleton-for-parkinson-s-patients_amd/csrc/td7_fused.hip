@@ -313,6 +313,7 @@ struct SelectArgs {
     R16 X, H1, H2, CAT;
     R32 F, TW, FT;
     int lds_bytes;
+    int tile0, ticket;  // fp32 chunked launches: first row tile; 1 = take the noise ticket
 };
 
 #define RING_START(first)      \
@@ -322,11 +323,18 @@ struct SelectArgs {
 __device__ __forceinline__ R16 rows_of(R16 r, int t) { return R16{r.off + t * TR * r.ld * 2, r.ld}; }
 __device__ __forceinline__ R32 rows_of(R32 r, int t) { return R32{r.off + t * TR * r.ld * 4, r.ld}; }
 
+// Row tiles tile0 + blockIdx.x: td7f_select may cover the tiles with several
+// launches of at most its workgroup cap each (the same per-row arithmetic and
+// Philox elements); only the last launch takes the noise ticket, so sigma and
+// the call counter advance once, after every tile has drawn.
 template <int P, int TH, int RT>
 __global__ __launch_bounds__(NTH) void select_kernel(SelectArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     constexpr int rows = RT * TR;
-    const int row0 = blockIdx.x * rows;
+    // (the chunked launches are fp32-only: the 16-bit kernels keep blockIdx.x)
+    int row0;
+    if constexpr (P == PREC_F32) row0 = (a.tile0 + blockIdx.x) * rows;
+    else row0 = blockIdx.x * rows;
     int si = 0;
     FSTAMP(si);
     RowStage so[RT];
@@ -371,7 +379,8 @@ __global__ __launch_bounds__(NTH) void select_kernel(SelectArgs a) {
         }
         __syncthreads();
     }
-    noise_rows<P>(lds, a.FT, a.A, rows, row0, a.n, a.nz, a.out, NO16, 0, NO16, 0);
+    if constexpr (P == PREC_F32) noise_rows<P>(lds, a.FT, a.A, rows, row0, a.n, a.nz, a.out, NO16, 0, NO16, 0, a.ticket != 0);
+    else noise_rows<P>(lds, a.FT, a.A, rows, row0, a.n, a.nz, a.out, NO16, 0, NO16, 0);
 }
 
 // ---------------------------------------------------------------- critic target chain
@@ -677,8 +686,28 @@ int td7f_select(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7
     a.TW = b.r32(THIN_NC, actor[3].n_in);
     a.FT = b.r32(rows, 16);
     a.lds_bytes = b.off;
-    const dim3 grid((n + rows - 1) / rows);
+    // fp32 workgroup cap (EXO_SELECT_WG_CAP, read per call; 0 = all tiles in
+    // one launch; default 128): the tiles in launches of at most cap
+    // workgroups back to back, leaving CUs to the fused passes that run beside
+    // select_action -- 0.488-0.491 vs 0.493-0.499 ms per fp32 iteration at
+    // 4,096 envs (64: 0.525; profiles/r04sc_raw)
+    const char *cap_env = getenv("EXO_SELECT_WG_CAP");
+    const int ntiles = (n + rows - 1) / rows, cap = cap_env ? atoi(cap_env) : 128;
     const hipStream_t st = (hipStream_t)stream;
+    if (prec == PREC_F32 && cap > 0 && cap < ntiles) {
+        for (int t0 = 0; t0 < ntiles; t0 += cap) {
+            a.tile0 = t0;
+            a.ticket = t0 + cap >= ntiles;
+            const dim3 g(std::min(cap, ntiles - t0));
+            const int rc = th == 5 ? launch(select_kernel<PREC_F32, 5, 1>, g, b.off, a, st)
+                                   : launch(select_kernel<PREC_F32, 4, 1>, g, b.off, a, st);
+            if (rc != EXO_OK) return rc;
+        }
+        return EXO_OK;
+    }
+    a.tile0 = 0;
+    a.ticket = 1;
+    const dim3 grid(ntiles);
     if (prec == PREC_F32)
         return th == 5 ? launch(select_kernel<PREC_F32, 5, 1>, grid, b.off, a, st)
                        : launch(select_kernel<PREC_F32, 4, 1>, grid, b.off, a, st);

@@ -163,3 +163,26 @@ def test_fused_trainer_graph_replay_equals_eager(precision):
             assert tr.graphs, "the graph-replayed trainer captured no graph"
     for a, b in zip(*out):
         torch.testing.assert_close(b, a, rtol=0, atol=0)
+
+
+def test_fp32_select_in_capped_launches_equals_one_launch(monkeypatch):
+    """td7f_select with a workgroup cap (EXO_SELECT_WG_CAP: the row tiles in
+    back-to-back launches of at most cap workgroups, fp32): the same actions
+    bit for bit, exploration_noise decremented once and the Philox call
+    counter advanced once -- by the last launch's ticket."""
+    L = _learner("fp32", None)
+    obs, _ = _inputs(4096, 4)
+    rng = L._explore_rng
+    st0, sig0 = rng.state.clone(), float(L.exploration_noise_t)
+    outs, states, sigmas = [], [], []
+    for cap in ("0", "100"):  # 256 tiles: one launch / launches of 100, 100, 56
+        monkeypatch.setenv("EXO_SELECT_WG_CAP", cap)
+        rng.state.copy_(st0)
+        L.exploration_noise_t.fill_(sig0)
+        outs.append(L.fused.select(obs, scale=1.0))
+        torch.cuda.synchronize()
+        states.append(rng.state.clone())
+        sigmas.append(float(L.exploration_noise_t))
+    torch.testing.assert_close(outs[1], outs[0], rtol=0, atol=0)
+    assert torch.equal(states[0], states[1]) and not torch.equal(states[0], st0)
+    assert sigmas[0] == sigmas[1] < sig0
