@@ -331,9 +331,10 @@ template <int P, int TH, int RT>
 __global__ __launch_bounds__(NTH) void select_kernel(SelectArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     constexpr int rows = RT * TR;
-    // (the chunked launches are fp32-only: the 16-bit kernels keep blockIdx.x)
+    // (chunked launches for the 16-row kernels only: the 32-row ones keep
+    // blockIdx.x -- their register allocation spills otherwise)
     int row0;
-    if constexpr (P == PREC_F32) row0 = (a.tile0 + blockIdx.x) * rows;
+    if constexpr (RT == 1) row0 = (a.tile0 + blockIdx.x) * rows;
     else row0 = blockIdx.x * rows;
     int si = 0;
     FSTAMP(si);
@@ -379,7 +380,7 @@ __global__ __launch_bounds__(NTH) void select_kernel(SelectArgs a) {
         }
         __syncthreads();
     }
-    if constexpr (P == PREC_F32) noise_rows<P>(lds, a.FT, a.A, rows, row0, a.n, a.nz, a.out, NO16, 0, NO16, 0, a.ticket != 0);
+    if constexpr (RT == 1) noise_rows<P>(lds, a.FT, a.A, rows, row0, a.n, a.nz, a.out, NO16, 0, NO16, 0, a.ticket != 0);
     else noise_rows<P>(lds, a.FT, a.A, rows, row0, a.n, a.nz, a.out, NO16, 0, NO16, 0);
 }
 
@@ -686,21 +687,29 @@ int td7f_select(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7
     a.TW = b.r32(THIN_NC, actor[3].n_in);
     a.FT = b.r32(rows, 16);
     a.lds_bytes = b.off;
-    // fp32 workgroup cap (EXO_SELECT_WG_CAP, read per call; 0 = all tiles in
-    // one launch; default 128): the tiles in launches of at most cap
-    // workgroups back to back, leaving CUs to the fused passes that run beside
-    // select_action -- 0.488-0.491 vs 0.493-0.499 ms per fp32 iteration at
-    // 4,096 envs (64: 0.525; profiles/r04sc_raw)
+    // workgroup cap (EXO_SELECT_WG_CAP, read per call; unset / 0 = all tiles
+    // in one launch): the tiles in launches of at most cap workgroups back to
+    // back, leaving CUs to the fused passes that run beside select_action in
+    // the training loop -- fp32 at 4,096 envs, cap 128: 0.488-0.491 vs
+    // 0.493-0.499 ms per iteration (64: 0.525; profiles/r04sc_raw)
+    // (16-row tiles only; the caller sets it per call: exo_amd.fused.select's
+    // wg_cap, which the training loop passes and the reference schedule's
+    // rollout -- select_action on its critical chain -- does not)
     const char *cap_env = getenv("EXO_SELECT_WG_CAP");
-    const int ntiles = (n + rows - 1) / rows, cap = cap_env ? atoi(cap_env) : 128;
+    const int ntiles = (n + rows - 1) / rows;
+    const int cap = cap_env ? atoi(cap_env) : 0;
     const hipStream_t st = (hipStream_t)stream;
-    if (prec == PREC_F32 && cap > 0 && cap < ntiles) {
+    if (RT == 1 && cap > 0 && cap < ntiles) {
         for (int t0 = 0; t0 < ntiles; t0 += cap) {
             a.tile0 = t0;
             a.ticket = t0 + cap >= ntiles;
             const dim3 g(std::min(cap, ntiles - t0));
-            const int rc = th == 5 ? launch(select_kernel<PREC_F32, 5, 1>, g, b.off, a, st)
-                                   : launch(select_kernel<PREC_F32, 4, 1>, g, b.off, a, st);
+            const int rc = prec == PREC_F32 ? (th == 5 ? launch(select_kernel<PREC_F32, 5, 1>, g, b.off, a, st)
+                                                       : launch(select_kernel<PREC_F32, 4, 1>, g, b.off, a, st))
+                           : prec == PREC_BF16 ? (th == 5 ? launch(select_kernel<PREC_BF16, 5, 1>, g, b.off, a, st)
+                                                          : launch(select_kernel<PREC_BF16, 4, 1>, g, b.off, a, st))
+                                               : (th == 5 ? launch(select_kernel<PREC_F16, 5, 1>, g, b.off, a, st)
+                                                          : launch(select_kernel<PREC_F16, 4, 1>, g, b.off, a, st));
             if (rc != EXO_OK) return rc;
         }
         return EXO_OK;

@@ -267,11 +267,22 @@ class VecTrainer:
             graph_reductions_ok(self.device)
 
     # ----------------------------------------------------------- pieces
+    # select_action's workgroups per launch in this loop (td7f_select's cap):
+    # here it runs beside the iteration's fused passes, off the critical
+    # chain, so with fp32 operands it takes at most 128 CUs at a time (0.488-
+    # 0.491 vs 0.493-0.499 ms per iteration at 4,096 envs, profiles/r04sc_raw);
+    # EXO_LOOP_SELECT_CAP overrides (0: one launch)
+    def _select_cap(self):
+        env = os.environ.get("EXO_LOOP_SELECT_CAP")
+        if env is not None:
+            return int(env)
+        return 128 if self.agent.learner.precision == "fp32" else None
+
     def _rollout(self):
         ag = self.agent
         obs = self.obs
         act = ag.select_action_batch(obs, timestep=self.k_dev if self.exploration == "pink" else None,
-                                     dec_count=self.active_count)
+                                     dec_count=self.active_count, wg_cap=self._select_cap())
         nobs, rew, done, info = self.env.step(act, active=self.active, out=self._outs[self._cur],
                                               obs_cur=obs if self.budget else None)
         ag.replay_buffer.add_batch(obs, act, nobs, rew, done, self.strata, self.active)

@@ -1320,7 +1320,8 @@ class Agent:
         return self.noise_dev
 
     @torch.no_grad()
-    def select_action_batch(self, obs, use_checkpoint=False, use_exploration=True, timestep=None, dec_count=None):
+    def select_action_batch(self, obs, use_checkpoint=False, use_exploration=True, timestep=None, dec_count=None,
+                            wg_cap=None):
         """Device-resident batched actions for the vectorised loop (no host sync).
         timestep (int64 device tensor [1]): Pink-noise exploration -- column
         `timestep` of the episode's noise (init_episode_noise_device) is added
@@ -1336,7 +1337,7 @@ class Agent:
         fz = self.learner.fused
         if fz is not None and use_exploration and timestep is None and not use_checkpoint and obs.is_cuda:
             # zs, actor and the noise in one launch
-            return fz.select(obs, scale=self.max_action, dec_count=dec_count, world=self.sync.world)
+            return fz.select(obs, scale=self.max_action, dec_count=dec_count, world=self.sync.world, wg_cap=wg_cap)
         a = self.learner.act(obs, use_checkpoint)
         if use_exploration and timestep is not None:
             col = self.noise_dev.index_select(1, timestep).t()           # [1, action_dim]
