@@ -1,12 +1,15 @@
 // exo_env.hip -- vectorised exoskeleton environment for MI355X (gfx950).
 //
 // Kernels
-//   exo_reset_kernel : one wavefront per env.  Lanes sweep the tremor samples
-//                      (generate_parkinson_tremor.py:31-73), the domain-
+//   exo_reset_kernel : 16 envs per 256-thread workgroup, 16 threads per env.
+//                      They sweep the tremor samples (generate_parkinson_
+//                      tremor.py:31-73; coalesced table stores), the domain-
 //                      randomised matrices (Exoskeleton_env.py:208-210) and the
-//                      dummy shift (Exoskeleton_sim_pybullet.py:98-107); lane 0
-//                      inverts the two diagonal blocks of I and packs the reset
-//                      observation (Exoskeleton_env.py:220-254).
+//                      dummy shift (Exoskeleton_sim_pybullet.py:98-107); one
+//                      thread per env inverts the two diagonal blocks of I and
+//                      packs the reset observation (Exoskeleton_env.py:220-254).
+//                      exo_reset_list_kernel: the same with one wavefront per
+//                      listed env (async episodes' short lists).
 //   exo_step_kernel  : two lanes per env.  Both lanes run the kinematics and
 //                      torque model (Exoskeleton_env.py:369-406); lane 0 solves
 //                      the actuated joint ODE, lane 1 the tremor-only ODE
@@ -84,124 +87,171 @@ __device__ void invert(double *a /* n*n, destroyed */, double *inv) {
 //   17+8L: I noise (49), D noise (49), S noise (49), 164+8L: shift (42),
 //   206+8L: shoulder force scale, elbow force scale.
 // ---------------------------------------------------------------------------
-// One env's reset by one wavefront (block of 64); draws: its injected stream or
-// nullptr (Philox).
-__device__ void reset_one(const Dev &S, const Urdf &U, int e, const double *draws, uint64_t seed, float *obs) {
+// The resets of EPW envs by one workgroup of EPW x TS threads: thread
+// (el = tid % EPW, tl = tid / EPW) works for env slot el and sweeps its tremor
+// samples t = tl, tl + TS, ...  With EPW = 16 the 16 threads of a (sample,
+// axis) store 16 consecutive envs' values -- one whole 128-byte line of the
+// [Lmax][7][N] tremor table per store instruction -- where one wavefront per
+// env stored each value to a line of its own (r05: 275 us per 4,096-env reset,
+// the line-scattered stores).  The arithmetic of every value is the one-env
+// sequence of the reference (numpy order, no contraction), so the tables are
+// bit-identical to the per-env kernel's.  e < 0: an idle slot (it joins the
+// barriers, stores nothing).  draws: the slot's injected stream or nullptr
+// (Philox).
+template <int EPW, int TS>
+__device__ void reset_group(const Dev &S, const Urdf &U, int e, const double *draws, uint64_t seed, float *obs) {
     // numpy evaluates every expression of the reset without fused multiply-add;
     // keep the rounding identical (bit-exact D, S, shift and force scales).
 #pragma clang fp contract(off)
-    const int lane = threadIdx.x;
-    if (S.pend && lane == 0) S.pend[e] = 0;  // a solve still carried by a budgeted step is dropped
-    const int N = S.N, L = S.L[e], seq = S.seq[e];
-    const uint32_t ep = S.episode[e];
-    const Draws D{draws, seed, (uint32_t)e, ep};
+    constexpr int NT = EPW * TS, NW = NT / 64;
+    static_assert(NT % 64 == 0 && 64 % EPW == 0, "whole wavefronts, a slot's threads spread over lanes");
+    const int el = threadIdx.x % EPW, tl = threadIdx.x / EPW, w = threadIdx.x / 64;
+    const bool on = e >= 0;
+    const int ee = on ? e : 0;
+    if (on && tl == 0 && S.pend) S.pend[e] = 0;  // a solve still carried by a budgeted step is dropped
+    const int N = S.N, L = on ? S.L[ee] : 0, seq = S.seq[ee];
+    const uint32_t ep = S.episode[ee];
+    const Draws D{draws, seed, (uint32_t)ee, ep};
 
-    __shared__ double sI[49], sD[49], sS[49], sShift[42], sTrem[3][4], sInv[NINV];
+    __shared__ double sA[EPW][14], sMn[NW][EPW][7], sMx[NW][EPW][7];
+    __shared__ double sI[EPW][49], sD[EPW][49], sS[EPW][49], sShift[EPW][42], sTrem[EPW][3][4], sInv[EPW][NINV];
 
     // ---- tremor (generate_parkinson_tremor.py:5-28, :31-73) -------------
-    const double amp0 = cfg(S, C_AMP0, e), amp1 = cfg(S, C_AMP1, e);
-    const double mag = amp0 + (D(0) * (amp1 - amp0)); // :198-199
-    const double h1a = cfg(S, C_H1A, e), h1b = cfg(S, C_H1B, e), h2a = cfg(S, C_H2A, e), h2b = cfg(S, C_H2B, e);
-    const double f1 = h1a + (h1b - h1a) * D(1);
-    const double f2 = h2a + (h2b - h2a) * D(2);
+    const double amp0 = cfg(S, C_AMP0, ee), amp1 = cfg(S, C_AMP1, ee);
+    const double h1a = cfg(S, C_H1A, ee), h1b = cfg(S, C_H1B, ee), h2a = cfg(S, C_H2A, ee), h2b = cfg(S, C_H2B, ee);
+    double mag = 0, f1 = 0, f2 = 0;
+    if (on) {
+        mag = amp0 + (D(0) * (amp1 - amp0)); // :198-199
+        f1 = h1a + (h1b - h1a) * D(1);
+        f2 = h2a + (h2b - h2a) * D(2);
+    }
     const double stop = L * DT, step = stop / (L - 1); // np.linspace(0, L*dt, L)
     const double w1 = 2 * PI * f1, w2 = 2 * PI * f2;
-    double a1[7], a2[7];
+    // the 14 amplitudes, one pow per thread of the slot
+    for (int j = tl; j < 14; j += TS) {
+        const int i = j % 7, b = 3 + L + i * (L + 2);
+        sA[el][j] = !on ? 0.0
+                    : j < 7 ? pow(10.0, (-5.0 + (0.0 - (-5.0)) * D(b)) / 20)
+                            : pow(10.0, (-20.0 + (-10.0 - (-20.0)) * D(b + 1)) / 20);
+    }
+    __syncthreads();
+    double a1[7], a2[7], mn[7], mx[7];
 #pragma unroll
     for (int i = 0; i < 7; ++i) {
-        const int b = 3 + L + i * (L + 2);
-        a1[i] = pow(10.0, (-5.0 + (0.0 - (-5.0)) * D(b)) / 20);
-        a2[i] = pow(10.0, (-20.0 + (-10.0 - (-20.0)) * D(b + 1)) / 20);
+        a1[i] = sA[el][i];
+        a2[i] = sA[el][7 + i];
+        mn[i] = INFINITY;
+        mx[i] = -INFINITY;
     }
-    double wv1[T_PER_LANE], wv2[T_PER_LANE], nz[T_PER_LANE];
-    double mn[7], mx[7];
+    for (int t = tl; t < L; t += TS) {
+        const double tt = (t == L - 1) ? stop : t * step;
+        const double wv1 = sin(w1 * tt), wv2 = sin(w2 * tt), nz = D(3 + t) * 0.001;
 #pragma unroll
-    for (int i = 0; i < 7; ++i) { mn[i] = INFINITY; mx[i] = -INFINITY; }
+        for (int i = 0; i < 7; ++i) {
+            const double acc = (a1[i] * wv1 + a2[i] * wv2 + nz) * (double)((seq >> i) & 1);
+            mn[i] = fmin(mn[i], acc);
+            mx[i] = fmax(mx[i], acc);
+        }
+    }
+    // min / max over the slot's threads: lanes EPW apart in a wavefront, then
+    // the wavefronts through LDS (fmin / fmax are exact: any order)
 #pragma unroll
-    for (int k = 0; k < T_PER_LANE; ++k) {
-        const int t = lane + 64 * k;
-        if (t < L) {
-            const double tt = (t == L - 1) ? stop : t * step;
-            wv1[k] = sin(w1 * tt);
-            wv2[k] = sin(w2 * tt);
-            nz[k] = D(3 + t) * 0.001;
+    for (int i = 0; i < 7; ++i) {
+#pragma unroll
+        for (int o = EPW; o < 64; o <<= 1) {
+            mn[i] = fmin(mn[i], __shfl_xor(mn[i], o, 64));
+            mx[i] = fmax(mx[i], __shfl_xor(mx[i], o, 64));
+        }
+    }
+    if (NW > 1) {
+        if ((threadIdx.x & 63) < EPW) {
 #pragma unroll
             for (int i = 0; i < 7; ++i) {
-                const double acc = (a1[i] * wv1[k] + a2[i] * wv2[k] + nz[k]) * (double)((seq >> i) & 1);
-                mn[i] = fmin(mn[i], acc);
-                mx[i] = fmax(mx[i], acc);
+                sMn[w][el][i] = mn[i];
+                sMx[w][el][i] = mx[i];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 7; ++i) {
+            mn[i] = sMn[0][el][i];
+            mx[i] = sMx[0][el][i];
+#pragma unroll
+            for (int v = 1; v < NW; ++v) {
+                mn[i] = fmin(mn[i], sMn[v][el][i]);
+                mx[i] = fmax(mx[i], sMx[v][el][i]);
             }
         }
     }
-#pragma unroll
-    for (int i = 0; i < 7; ++i) { mn[i] = wave_min(mn[i]); mx[i] = wave_max(mx[i]); }
     // joint_max_values (:59): the shipped table unless exo_set_tremor_model chose another
+    for (int t = tl; t < L; t += TS) {
+        const double tt = (t == L - 1) ? stop : t * step;
+        const double wv1 = sin(w1 * tt), wv2 = sin(w2 * tt), nz = D(3 + t) * 0.001;
 #pragma unroll
-    for (int k = 0; k < T_PER_LANE; ++k) {
-        const int t = lane + 64 * k;
-        if (t < L) {
-#pragma unroll
-            for (int i = 0; i < 7; ++i) {
-                const double acc = (a1[i] * wv1[k] + a2[i] * wv2[k] + nz[k]) * (double)((seq >> i) & 1);
-                double v = (-1 + 2 * (acc - mn[i]) / (mx[i] - mn[i])) * (S.tjmax[i] * mag);
-                if (!isfinite(v)) v = 0.0; // np.nan_to_num (:67)
-                // np.random.choice([-1, 1], L) per sample (:70); the diagnostic
-                // models use the axis's first sign draw for every sample, or none
-                const int ts = S.tsign == EXO_TREMOR_SIGN_PER_AXIS ? 0 : t;
-                const double sgn = (S.tsign != EXO_TREMOR_SIGN_NONE && D(3 + L + i * (L + 2) + 2 + ts) < 0.5) ? -1.0
-                                                                                                                : 1.0;
-                v *= sgn;
-                S.tremor[((size_t)t * 7 + i) * N + e] = v;
-                if (t < 3 && i < 4) sTrem[t][i] = v;
-            }
+        for (int i = 0; i < 7; ++i) {
+            const double acc = (a1[i] * wv1 + a2[i] * wv2 + nz) * (double)((seq >> i) & 1);
+            double v = (-1 + 2 * (acc - mn[i]) / (mx[i] - mn[i])) * (S.tjmax[i] * mag);
+            if (!isfinite(v)) v = 0.0; // np.nan_to_num (:67)
+            // np.random.choice([-1, 1], L) per sample (:70); the diagnostic
+            // models use the axis's first sign draw for every sample, or none
+            const int ts = S.tsign == EXO_TREMOR_SIGN_PER_AXIS ? 0 : t;
+            const double sgn = (S.tsign != EXO_TREMOR_SIGN_NONE && D(3 + L + i * (L + 2) + 2 + ts) < 0.5) ? -1.0
+                                                                                                            : 1.0;
+            v *= sgn;
+            S.tremor[((size_t)t * 7 + i) * N + e] = v;
+            if (t < 3 && i < 4) sTrem[el][t][i] = v;
         }
     }
 
     // ---- domain-randomised matrices (domain_randomization_...py:4-27) ----
-    const double mf = cfg(S, C_MATF, e);
+    const double mf = cfg(S, C_MATF, ee);
     const int pI = 17 + 8 * L;
-    if (lane < 49) {
-        const int r = lane / 7, c = lane % 7, tr = c * 7 + r;
-        double n0, n1, s;
-        n0 = -mf + (mf - (-mf)) * D(pI + lane); n1 = -mf + (mf - (-mf)) * D(pI + tr);
-        s = (n0 + n1) / 2; sI[lane] = I0[lane] + s * I0[lane];
-        n0 = -mf + (mf - (-mf)) * D(pI + 49 + lane); n1 = -mf + (mf - (-mf)) * D(pI + 49 + tr);
-        s = (n0 + n1) / 2; sD[lane] = D0[lane] + s * D0[lane];
-        n0 = -mf + (mf - (-mf)) * D(pI + 98 + lane); n1 = -mf + (mf - (-mf)) * D(pI + 98 + tr);
-        s = (n0 + n1) / 2; sS[lane] = S0[lane] + s * S0[lane];
-    }
-    const double sr = cfg(S, C_SHIFT, e);
-    if (lane < 42) {
-        const double v = -sr + (sr - (-sr)) * D(pI + 147 + lane);
-        sShift[lane] = v;
-        S.shift[(size_t)lane * N + e] = v;
+    if (on) {
+        for (int j = tl; j < 49; j += TS) {
+            const int r = j / 7, c = j % 7, tr = c * 7 + r;
+            double n0, n1, s;
+            n0 = -mf + (mf - (-mf)) * D(pI + j); n1 = -mf + (mf - (-mf)) * D(pI + tr);
+            s = (n0 + n1) / 2; sI[el][j] = I0[j] + s * I0[j];
+            n0 = -mf + (mf - (-mf)) * D(pI + 49 + j); n1 = -mf + (mf - (-mf)) * D(pI + 49 + tr);
+            s = (n0 + n1) / 2; sD[el][j] = D0[j] + s * D0[j];
+            n0 = -mf + (mf - (-mf)) * D(pI + 98 + j); n1 = -mf + (mf - (-mf)) * D(pI + 98 + tr);
+            s = (n0 + n1) / 2; sS[el][j] = S0[j] + s * S0[j];
+        }
+        const double sr = cfg(S, C_SHIFT, ee);
+        for (int j = tl; j < 42; j += TS) {
+            const double v = -sr + (sr - (-sr)) * D(pI + 147 + j);
+            sShift[el][j] = v;
+            S.shift[(size_t)j * N + e] = v;
+        }
     }
     __syncthreads();
-    if (lane < NSYM) { // the upper-triangle non-zeros of D and S
-        int r = 0, c = 0;
+    if (on) {
+        for (int k = tl; k < NSYM; k += TS) { // the upper-triangle non-zeros of D and S
+            int r = 0, c = 0;
 #pragma unroll
-        for (int k = 0; k < NSYM; ++k)
-            if (k == lane) { r = SYM_R[k]; c = SYM_C[k]; }
-        S.dnz[(size_t)lane * N + e] = sD[r * 7 + c];
-        S.snz[(size_t)lane * N + e] = sS[r * 7 + c];
-    }
-    if (lane == 0) {
-        double a3[9], i3[9], a4[16], i4[16];
-        for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j) a3[i * 3 + j] = sI[B1[i] * 7 + B1[j]];
-        for (int i = 0; i < 4; ++i)
-            for (int j = 0; j < 4; ++j) a4[i * 4 + j] = sI[B2[i] * 7 + B2[j]];
-        invert<3>(a3, i3);
-        invert<4>(a4, i4);
-        for (int i = 0; i < 3; ++i)
-            for (int j = i; j < 3; ++j) sInv[B1U[i][j]] = i3[i * 3 + j];
-        for (int i = 0; i < 4; ++i)
-            for (int j = i; j < 4; ++j) sInv[B2U[i][j]] = i4[i * 4 + j];
+            for (int q = 0; q < NSYM; ++q)
+                if (q == k) { r = SYM_R[q]; c = SYM_C[q]; }
+            S.dnz[(size_t)k * N + e] = sD[el][r * 7 + c];
+            S.snz[(size_t)k * N + e] = sS[el][r * 7 + c];
+        }
+        if (tl == 0) {
+            double a3[9], i3[9], a4[16], i4[16];
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) a3[i * 3 + j] = sI[el][B1[i] * 7 + B1[j]];
+            for (int i = 0; i < 4; ++i)
+                for (int j = 0; j < 4; ++j) a4[i * 4 + j] = sI[el][B2[i] * 7 + B2[j]];
+            invert<3>(a3, i3);
+            invert<4>(a4, i4);
+            for (int i = 0; i < 3; ++i)
+                for (int j = i; j < 3; ++j) sInv[el][B1U[i][j]] = i3[i * 3 + j];
+            for (int i = 0; i < 4; ++i)
+                for (int j = i; j < 4; ++j) sInv[el][B2U[i][j]] = i4[i * 4 + j];
+        }
     }
     __syncthreads();
-    if (lane < NINV) S.iinv[(size_t)lane * N + e] = sInv[lane];
-
-    if (lane != 0) return;
+    if (!on) return;
+    for (int k = tl; k < NINV; k += TS) S.iinv[(size_t)k * N + e] = sInv[el][k];
+    if (tl != 0) return;
     // ---- actuator force scale (:216-217) --------------------------------
     const double ar = cfg(S, C_ACTR, e), lo = 1 - ar, hi = 1 + ar;
     const double maxS = cfg(S, C_MAXS0, e) * (lo + (hi - lo) * D(pI + 189));
@@ -228,12 +278,12 @@ __device__ void reset_one(const Dev &S, const Urdf &U, int e, const double *draw
 #pragma unroll
     for (int t = 0; t < 3; ++t)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) ob[14 + t * 4 + i] = (float)(sTrem[t][i] / tn[i]);
+        for (int i = 0; i < 4; ++i) ob[14 + t * 4 + i] = (float)(sTrem[el][t][i] / tn[i]);
 #pragma unroll
     for (int j = 0; j < 7; ++j)
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
-            const double p = act[2 * j + 1][a] + sShift[(2 * j + 1) * 3 + a];
+            const double p = act[2 * j + 1][a] + sShift[el][(2 * j + 1) * 3 + a];
             const double rc = (j < 2) ? refc[3 + a] : refc[a];
             const double rn = (j < 2) ? ref[3 + a] : ref[a];
             ob[26 + j * 3 + a] = (float)(p - rc);
@@ -253,24 +303,34 @@ __device__ void reset_one(const Dev &S, const Urdf &U, int e, const double *draw
     }
 }
 
-// reset (Exoskeleton_env.py:473-478 -> initialize_movement, :193-254): one
-// wavefront per env -- every env, the envs of a mask, or listed envs with
-// their injected draw streams
-__global__ __launch_bounds__(64) void exo_reset_kernel(Dev S, Urdf U, const uint8_t *mask, const int32_t *ids,
-                                                       const double *draws, int draw_stride, uint64_t seed,
-                                                       float *obs) {
-    const int e = ids ? ids[blockIdx.x] : (int)blockIdx.x;
-    if (e >= S.N) return;
-    if (!ids && mask && !mask[e]) return;
-    reset_one(S, U, e, draws ? draws + (size_t)blockIdx.x * draw_stride : nullptr, seed, obs);
+// bulk resets (exo_reset, exo_reset_from_draws; Exoskeleton_env.py:473-478 ->
+// initialize_movement, :193-254): 16 envs per 256-thread workgroup -- every
+// env (slot = env index; mask: those set), or the n listed envs with their
+// injected draw streams
+constexpr int RESET_EPW = 16, RESET_TS = 16;
+__global__ __launch_bounds__(RESET_EPW *RESET_TS) void exo_reset_kernel(Dev S, Urdf U, const uint8_t *mask,
+                                                                        const int32_t *ids, int n,
+                                                                        const double *draws, int draw_stride,
+                                                                        uint64_t seed, float *obs) {
+    const int slot = blockIdx.x * RESET_EPW + (int)threadIdx.x % RESET_EPW;
+    int e = -1;
+    if (ids) {
+        if (slot < n) e = ids[slot];
+    } else if (slot < S.N && !(mask && !mask[slot])) {
+        e = slot;
+    }
+    reset_group<RESET_EPW, RESET_TS>(S, U, e, draws && slot < n ? draws + (size_t)slot * draw_stride : nullptr,
+                                     seed, obs);
 }
 
-// the envs listed in ids[0 .. *n_ids) (exo_episode_advance's compacted list):
-// a small fixed grid, each wavefront taking every gridDim.x-th listed env
+// the envs listed in ids[0 .. *n_ids) (exo_episode_advance's compacted list,
+// a dozen envs per iteration at 4,096 envs): one wavefront per env as the
+// latency of a short list wants, a small fixed grid, each wavefront taking
+// every gridDim.x-th listed env
 __global__ __launch_bounds__(64) void exo_reset_list_kernel(Dev S, Urdf U, const int32_t *ids,
                                                             const int32_t *n_ids, uint64_t seed, float *obs) {
     const int n = *n_ids;
-    for (int k = blockIdx.x; k < n; k += gridDim.x) reset_one(S, U, ids[k], nullptr, seed, obs);
+    for (int k = blockIdx.x; k < n; k += gridDim.x) reset_group<1, 64>(S, U, ids[k], nullptr, seed, obs);
 }
 
 // ---------------------------------------------------------------------------
@@ -861,8 +921,9 @@ int exo_create(const exo_env_config *cfgs, int32_t n_envs, const double *motion_
 int exo_reset(exo_ctx *c, const uint8_t *mask_dev, float *obs_dev, void *stream) {
     if (!c) return EXO_EINVAL;
     DeviceGuard g(c->device);
-    hipLaunchKernelGGL(exo_reset_kernel, dim3(c->N), dim3(64), 0, (hipStream_t)stream, c->S, c->U, mask_dev,
-                       (const int32_t *)nullptr, (const double *)nullptr, 0, c->seed, obs_dev);
+    hipLaunchKernelGGL(exo_reset_kernel, dim3((c->N + RESET_EPW - 1) / RESET_EPW), dim3(RESET_EPW * RESET_TS), 0,
+                       (hipStream_t)stream, c->S, c->U, mask_dev, (const int32_t *)nullptr, 0,
+                       (const double *)nullptr, 0, c->seed, obs_dev);
     return check(c, hipGetLastError(), "exo_reset");
 }
 
@@ -883,8 +944,8 @@ int exo_reset_from_draws(exo_ctx *c, const int32_t *env_ids_host, int32_t n, con
     hipError_t e = hipMemcpyAsync(ids, env_ids_host, n * 4, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(dr, draws_host, (size_t)n * stride * 8, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(exo_reset_kernel, dim3(n), dim3(64), 0, s, c->S, c->U, (const uint8_t *)nullptr, ids, dr,
-                           stride, c->seed, obs_dev);
+        hipLaunchKernelGGL(exo_reset_kernel, dim3((n + RESET_EPW - 1) / RESET_EPW), dim3(RESET_EPW * RESET_TS), 0,
+                           s, c->S, c->U, (const uint8_t *)nullptr, ids, n, dr, stride, c->seed, obs_dev);
         e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipStreamSynchronize(s);

@@ -643,8 +643,9 @@ int td7f_adam_pack(int32_t prec, int32_t nopt, float *const *p, float *const *m,
 }
 
 int td7f_select(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7f_lin *actor, const float *obs,
-                int32_t n, const td7f_noise *noise, float *out, void *stream) {
-    if (!prec_ok(prec) || !act || !enc || !actor || !obs || !noise || !out || n <= 0) return EXO_EINVAL;
+                int32_t n, const td7f_noise *noise, float *out, int32_t wg_cap, void *stream) {
+    if (!prec_ok(prec) || !act || !enc || !actor || !obs || !noise || !out || n <= 0 || wg_cap < 0)
+        return EXO_EINVAL;
     const int kd = kd_of(prec);
     td7f_lin all[7] = {enc[0], enc[1], enc[2], actor[0], actor[1], actor[2], actor[3]};
     const int th = th_of(all, 7);
@@ -687,17 +688,17 @@ int td7f_select(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7
     a.TW = b.r32(THIN_NC, actor[3].n_in);
     a.FT = b.r32(rows, 16);
     a.lds_bytes = b.off;
-    // workgroup cap (EXO_SELECT_WG_CAP, read per call; unset / 0 = all tiles
-    // in one launch): the tiles in launches of at most cap workgroups back to
+    // workgroup cap (wg_cap; EXO_SELECT_WG_CAP overrides it when set; 0 = all
+    // tiles in one launch): the tiles in launches of at most cap workgroups back to
     // back, leaving CUs to the fused passes that run beside select_action in
     // the training loop -- fp32 at 4,096 envs, cap 128: 0.488-0.491 vs
     // 0.493-0.499 ms per iteration (64: 0.525; profiles/r04sc_raw)
-    // (16-row tiles only; the caller sets it per call: exo_amd.fused.select's
-    // wg_cap, which the training loop passes and the reference schedule's
-    // rollout -- select_action on its critical chain -- does not)
+    // (16-row tiles only; exo_amd.fused.select's wg_cap, which the training
+    // loop passes and the reference schedule's rollout -- select_action on
+    // its critical chain -- does not)
     const char *cap_env = getenv("EXO_SELECT_WG_CAP");
     const int ntiles = (n + rows - 1) / rows;
-    const int cap = cap_env ? atoi(cap_env) : 0;
+    const int cap = cap_env ? atoi(cap_env) : wg_cap;
     const hipStream_t st = (hipStream_t)stream;
     if (RT == 1 && cap > 0 && cap < ntiles) {
         for (int t0 = 0; t0 < ntiles; t0 += cap) {
@@ -779,11 +780,11 @@ int td7f_target(int32_t prec, const int32_t *act, const td7f_lin *tenc, const td
         // fp32 images: OUT overlays CATA (dead once actor_target's l1 has read
         // it; OUT is first written by the noise after l3) and F overlays
         // H1 | H2 (dead whenever F is written; the thin l3 writes F's first
-        // columns only, inside H1, while it reads H2)
-        a.OUT = R16{a.CATA.off, old};
-        a.F = R32{a.H1.off, fld};
-        if (rows * old * 2 > rows * a.CATA.ld * 2 || rows * fld * 4 > a.H2.off + rows * a.H2.ld * 2 - a.H1.off)
-            return EXO_EINVAL;
+        // columns only, inside H1, while it reads H2); a region the overlay
+        // does not fit (zs_dim well above actor_hdim, or a narrow hidden
+        // width) gets its own bytes instead, as in the 16-bit images
+        a.OUT = old <= a.CATA.ld ? R16{a.CATA.off, old} : ba.r16(rows, old);
+        a.F = rows * fld * 4 <= a.H2.off + rows * a.H2.ld * 2 - a.H1.off ? R32{a.H1.off, fld} : ba.r32(rows, fld);
     } else {
         a.OUT = ba.r16(rows, old);
         a.F = ba.r32(rows, fld);

@@ -271,21 +271,10 @@ class FusedNets:
         else:
             nz = self._noise(L._explore_rng, L.exploration_noise_t, dec * n, 0.0, scale)
         fe, ac = self.nets["fixed_encoder"].layers, self.nets["actor"].layers
-        # wg_cap: at most this many workgroups per launch (td7f_select reads
-        # EXO_SELECT_WG_CAP per call; set only around this call)
-        prev = os.environ.get("EXO_SELECT_WG_CAP")
-        if wg_cap is not None:
-            os.environ["EXO_SELECT_WG_CAP"] = str(int(wg_cap))
-        try:
-            nat.check(nat.lib().td7f_select(self.prec, self.act, _lin_array(fe[:3]), self.nets["actor"].array,
-                                            nat.ptr(obs), n, ctypes.byref(nz), nat.ptr(out),
-                                            nat.stream_ptr(obs.device)), "td7f_select")
-        finally:
-            if wg_cap is not None:
-                if prev is None:
-                    del os.environ["EXO_SELECT_WG_CAP"]
-                else:
-                    os.environ["EXO_SELECT_WG_CAP"] = prev
+        # wg_cap: at most this many workgroups per launch (None / 0: one launch)
+        nat.check(nat.lib().td7f_select(self.prec, self.act, _lin_array(fe[:3]), self.nets["actor"].array,
+                                        nat.ptr(obs), n, ctypes.byref(nz), nat.ptr(out), int(wg_cap or 0),
+                                        nat.stream_ptr(obs.device)), "td7f_select")
         return out
 
     def _img(self, B):

@@ -788,7 +788,11 @@ class RefScheduleTrainer(VecTrainer):
       update, target refresh every 250 steps), and refreshes the policy
       checkpoint by the reference's rule (TD7_multi_agent.py:296-325);
     * the warm-up switch after the round (:210-211): steps_count counts active
-      env-steps over all data-parallel ranks.
+      env-steps over all data-parallel ranks;
+    * save_prefix (the script's agent.save("AGENT_NNS/test_agent") after every
+      round, :290): Agent.save(save_prefix) once per round, its 8 files, on
+      rank 0 of a data-parallel run (the replicas are identical); the host
+      time it takes is summed in save_seconds.  None (the default): no save.
 
     One rollout step = select / uniform actions -> exo_step -> score -> replay
     insert -> next active mask, replayed from a captured graph per (random,
@@ -800,7 +804,8 @@ class RefScheduleTrainer(VecTrainer):
     from injected draw streams) instead of exo_reset."""
 
     def __init__(self, env, agent, warmup=25_000, strata=None, use_graphs=True, ref_replay=True,
-                 action_source=None, reset_source=None, warmup_eager=2, round_graph=None, stats=None):
+                 action_source=None, reset_source=None, warmup_eager=2, round_graph=None, stats=None,
+                 save_prefix=None):
         if getattr(env, "step_budget", 0):
             raise ValueError("RefScheduleTrainer steps the script's synchronous episodes: no step budget")
         super().__init__(env, agent, strata=strata, use_graphs=use_graphs, warmup_eager=warmup_eager,
@@ -876,6 +881,9 @@ class RefScheduleTrainer(VecTrainer):
         self.stats = (os.environ.get("EXO_REF_STATS", "0") == "1") if stats is None else bool(stats)
         self.round_stats = []
         self._stat_bufs = None
+        self.save_prefix = save_prefix
+        self.saves = 0
+        self.save_seconds = 0.0
 
     # ------------------------------------------------------------ rollout
     def _seen_eager(self, random):
@@ -1072,6 +1080,18 @@ class RefScheduleTrainer(VecTrainer):
         self._train_iters += 1
 
     # -------------------------------------------------------------- round
+    def save_round(self):
+        """:290 -- agent.save(prefix) after the round (rank 0 only when data
+        parallel).  Agent.save copies every tensor to the host, which orders it
+        after the round's burst on the device."""
+        import time
+        if self.agent.sync.rank != 0:
+            return
+        t = time.perf_counter()
+        self.agent.save(self.save_prefix)
+        self.save_seconds += time.perf_counter() - t
+        self.saves += 1
+
     def run_round(self):
         """One episode round (:111-211); returns (active env-steps of this
         rank, training steps of the burst)."""
@@ -1106,6 +1126,8 @@ class RefScheduleTrainer(VecTrainer):
             self.allow_train = True
         if self.stats:
             self.round_stats.append(self.compute_round_stats())
+        if self.save_prefix is not None:
+            self.save_round()
         self.rounds += 1
         self.trace.append(dict(round=self.rounds, random_actions=random, ep_return=ep_return,
                                ep_timesteps=ep_timesteps, training_steps=L.training_steps,

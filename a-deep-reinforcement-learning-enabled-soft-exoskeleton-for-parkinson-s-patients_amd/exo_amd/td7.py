@@ -445,20 +445,40 @@ class GradSync:
         return self._capture_ok
 
     def _capture_selftest(self, device, replays=3):
-        x = torch.zeros(1024, device=device)
+        """The iteration's collective pattern (VecTrainer._inline) captured and
+        replayed at this world size: an AVG on a forked branch (the encoder
+        bucket), an AVG on the capture stream (the critic bucket), a MAX on a
+        second branch forked after it (max_priority), an AVG on the capture
+        stream again (the actor bucket), each branch joined at the end -- so a
+        cross-stream ordering the runtime or RCCL mishandles at world > 1
+        shows here, before any training graph is captured."""
+        xe = torch.zeros(4096, device=device)
+        xc = torch.zeros(1024, device=device)
+        xa = torch.zeros(256, device=device)
         y = torch.zeros(1, device=device)
-        self.avg_(x)  # eager first: communicator set up outside the capture
+        self.avg_(xe)  # eager first: communicator set up outside the capture
         dist.all_reduce(y, op=dist.ReduceOp.MAX, group=self.group)
         cur = torch.cuda.current_stream(device)
         s = torch.cuda.Stream(device=device)
+        side, prio = torch.cuda.Stream(device=device), torch.cuda.Stream(device=device)
         s.wait_stream(cur)
         g = torch.cuda.CUDAGraph()
         captured = True
         try:
             with torch.cuda.stream(s):
                 with torch.cuda.graph(g, stream=s):
-                    self.avg_(x)
-                    dist.all_reduce(y, op=dist.ReduceOp.MAX, group=self.group)
+                    side.wait_stream(s)
+                    with torch.cuda.stream(side):
+                        xe.mul_(2.0)
+                        self.avg_(xe)
+                    xc.add_(1.0)
+                    self.avg_(xc)
+                    prio.wait_stream(s)
+                    with torch.cuda.stream(prio):
+                        dist.all_reduce(y, op=dist.ReduceOp.MAX, group=self.group)
+                    self.avg_(xa)
+                    s.wait_stream(side)
+                    s.wait_stream(prio)
         except Exception:
             captured = False
         cur.wait_stream(s)
@@ -469,12 +489,17 @@ class GradSync:
             return False
         ok = True
         for k in range(replays):
-            x.fill_(float(self.rank + 1 + k))
+            r = float(self.rank + 1 + k)
+            xe.fill_(r)
+            xc.fill_(r)
+            xa.fill_(r)
             y.fill_(float(self.rank + 2 * k))
             g.replay()
             torch.cuda.synchronize(device)
-            want = (self.world + 1) / 2.0 + k
-            ok = ok and bool((x - want).abs().max() <= 1e-5 * want) and float(y) == self.world - 1 + 2 * k
+            want = (self.world + 1) / 2.0 + k  # the mean of rank + 1 + k
+            ok = (ok and bool((xe - 2 * want).abs().max() <= 2e-5 * want)
+                  and bool((xc - (want + 1)).abs().max() <= 1e-5 * (want + 1))
+                  and bool((xa - want).abs().max() <= 1e-5 * want) and float(y) == self.world - 1 + 2 * k)
         del g
         return ok
 

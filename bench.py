@@ -509,6 +509,17 @@ def reference_schedule(env, dev, args, hp, rounds=3, warm_rounds=3, group=None):
            "note": "Exoskeleton_agent_train.py:110-211 on the device: warm-up 25,000 env-steps of uniform actions, "
                    "then select_action with Gaussian exploration; per round round(mean(ep_len)) = 283 "
                    "graph-replayed Agent.train steps and the policy-checkpoint rule (TD7_multi_agent.py:296-325)"}
+    # the script's per-round agent.save (:290; RefScheduleTrainer(save_prefix=)):
+    # its host cost per round, timed apart (3 saves of the 8 files into a
+    # temporary directory, rank 0)
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        tr.save_prefix = os.path.join(d, "test_agent")
+        for _ in range(3):
+            tr.save_round()
+        tr.save_prefix = None
+    if tr.saves:
+        out["save_ms_per_round"] = tr.save_seconds / tr.saves * 1e3
     # the script's per-step tremor statistics (:149-205) and per-round outputs
     # (:213-317) on the device (RefScheduleTrainer(stats=True)): one round to
     # capture the rollout graphs with them, then rounds timed as above

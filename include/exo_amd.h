@@ -641,11 +641,12 @@ int td7f_adam_pack(int32_t prec, int32_t nopt, float *const *p_dev, float *const
                    const int32_t *job_seg, uint32_t *ticket_dev, void *stream);
 /* Agent.select_action_batch (TD7_multi_agent.py:192-209 batched): actor(obs,
  * fixed_encoder.zs(obs)) + Gaussian exploration noise -> act_out [n][A].
- * enc: zs1..zs3, actor: l0..l3.  EXO_SELECT_WG_CAP (read per call, 16-row
- * tiles): at most that many workgroups per launch, the tiles in back-to-back
- * launches (same results; the noise state advances once). */
+ * enc: zs1..zs3, actor: l0..l3.  wg_cap > 0 (16-row tiles): at most that
+ * many workgroups per launch, the tiles in back-to-back launches (same
+ * results; the noise state advances once); 0: one launch.  The environment
+ * variable EXO_SELECT_WG_CAP, when set, overrides wg_cap (experiments). */
 int td7f_select(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7f_lin *actor, const float *obs_dev,
-                int32_t n, const td7f_noise *noise, float *act_out_dev, void *stream);
+                int32_t n, const td7f_noise *noise, float *act_out_dev, int32_t wg_cap, void *stream);
 /* The critic target chain (TD7_multi_agent.py:233-241): fixed_target_zs(s'),
  * next_action = actor_target(s', zs) + clipped noise, fixed_target_zsa and both
  * heads of critic_target -> qt_dev [B][2].  tenc: zs1..zs3, zsa1..zsa3;

@@ -166,7 +166,7 @@ def test_fused_trainer_graph_replay_equals_eager(precision):
 
 
 def test_fp32_select_in_capped_launches_equals_one_launch(monkeypatch):
-    """td7f_select with a workgroup cap (EXO_SELECT_WG_CAP: the row tiles in
+    """td7f_select with a workgroup cap (wg_cap: the row tiles in
     back-to-back launches of at most cap workgroups, fp32): the same actions
     bit for bit, exploration_noise decremented once and the Philox call
     counter advanced once -- by the last launch's ticket."""
@@ -175,11 +175,11 @@ def test_fp32_select_in_capped_launches_equals_one_launch(monkeypatch):
     rng = L._explore_rng
     st0, sig0 = rng.state.clone(), float(L.exploration_noise_t)
     outs, states, sigmas = [], [], []
-    for cap in ("0", "100"):  # 256 tiles: one launch / launches of 100, 100, 56
-        monkeypatch.setenv("EXO_SELECT_WG_CAP", cap)
+    monkeypatch.delenv("EXO_SELECT_WG_CAP", raising=False)
+    for cap in (0, 100):  # 256 tiles: one launch / launches of 100, 100, 56
         rng.state.copy_(st0)
         L.exploration_noise_t.fill_(sig0)
-        outs.append(L.fused.select(obs, scale=1.0))
+        outs.append(L.fused.select(obs, scale=1.0, wg_cap=cap))
         torch.cuda.synchronize()
         states.append(rng.state.clone())
         sigmas.append(float(L.exploration_noise_t))

@@ -307,3 +307,35 @@ def test_burst_prefetch_is_bit_identical(monkeypatch):
     assert d0 == d1
     assert any(len(k) == 5 for k in tr1.graphs if k[0] == "train")
     assert not any(len(k) == 5 for k in tr0.graphs if k[0] == "train")
+
+
+def test_per_round_save_reloads_to_the_trainers_weights(tmp_path):
+    """RefScheduleTrainer(save_prefix=...): agent.save(prefix) after every
+    round (Exoskeleton_agent_train.py:290, TD7_multi_agent.py:330-345); the 8
+    files of the last round, loaded into a fresh Agent (weights_only), hold the
+    trainer's live nets, optimiser moments and checkpoint nets."""
+    from exo_amd import VecExoskeletonEnv
+    from exo_amd.rollout import RefScheduleTrainer
+    from exo_amd.td7 import Agent
+    torch.manual_seed(0)
+    N = 64
+    env = VecExoskeletonEnv(N, seed=5)
+    agent = Agent(80, 7, 1, learning_steps=100000, env_num=E, buffer_size=2 * BUF, precision="bf16", n_envs=N)
+    prefix = str(tmp_path / "test_agent")
+    tr = RefScheduleTrainer(env, agent, warmup=1, save_prefix=prefix)
+    for _ in range(2):
+        tr.run_round()
+    torch.cuda.synchronize()
+    assert tr.saves == 2 and tr.save_seconds > 0
+    assert all(os.path.exists(prefix + s) for s in Agent.SUFFIXES)
+    fresh = Agent(80, 7, 1, learning_steps=100000, env_num=E, buffer_size=2 * BUF, precision="bf16", n_envs=N)
+    fresh.load(prefix)
+    La, Lb = agent.learner, fresh.learner
+    for name in ("actor", "critic", "encoder", "checkpoint_actor", "checkpoint_encoder"):
+        for p, q in zip(getattr(La, name).parameters(), getattr(Lb, name).parameters()):
+            torch.testing.assert_close(q, p, rtol=0, atol=0, msg=name)
+    for opt in ("actor_optimizer", "critic_optimizer", "encoder_optimizer"):
+        torch.testing.assert_close(getattr(Lb, opt).m, getattr(La, opt).m, rtol=0, atol=0)
+        torch.testing.assert_close(getattr(Lb, opt).v, getattr(La, opt).v, rtol=0, atol=0)
+        assert float(getattr(Lb, opt)._step) == float(getattr(La, opt)._step) == La.training_steps // (
+            2 if opt == "actor_optimizer" else 1)

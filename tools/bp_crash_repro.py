@@ -10,8 +10,54 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
                                 "a-deep-reinforcement-learning-enabled-soft-exoskeleton-for-parkinson-s-patients_amd"))
 import torch  # noqa: E402
 
+# diagnostics (r05): a native SIGSEGV backtrace with per-library offsets
+import ctypes  # noqa: E402
+import faulthandler  # noqa: E402
+import traceback  # noqa: E402
+
+faulthandler.enable()
+_tr = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_segv_trace.so")
+if os.path.exists(_tr):
+    ctypes.CDLL(_tr).segv_trace_install()
+
+
+def _bisect_switches():
+    """r05 bisection of the two r05 changes that made the crash go away:
+    "r04reset" loads a library built with round 4's reset kernels (one
+    wavefront per env, 2,112 B/lane of scratch), made from the r04 source:
+      git show b3aefae:<pkg>/csrc/exo_env.hip > tools/_bisect/exo_env_r04.hip
+      (cd <pkg>/csrc && hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC
+       -I../../include -I. -c ../../tools/_bisect/exo_env_r04.hip -o ../../tools/_bisect/exo_env_r04.o &&
+       hipcc --offload-arch=gfx950 -shared -fPIC -o ../../tools/_bisect/libexo_amd_r04reset.so
+       ../../tools/_bisect/exo_env_r04.o <every other ../exo_amd/_lib/*.o>)
+    "r04select" passes the select workgroup cap by setting EXO_SELECT_WG_CAP
+    in os.environ around every td7f_select call, as round 4 did."""
+    import exo_amd._native as nat
+    from exo_amd import fused
+    if "r04reset" in sys.argv:
+        nat.LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_bisect", "libexo_amd_r04reset.so")
+        print("library", nat.LIB_PATH, flush=True)
+    if "r04select" in sys.argv:
+        orig = fused.FusedNets.select
+
+        def select(self, obs, scale=1.0, dec_count=None, world=1, wg_cap=None):
+            prev = os.environ.get("EXO_SELECT_WG_CAP")
+            if wg_cap is not None:
+                os.environ["EXO_SELECT_WG_CAP"] = str(int(wg_cap))
+            try:
+                return orig(self, obs, scale, dec_count, world, None)
+            finally:
+                if wg_cap is not None:
+                    if prev is None:
+                        del os.environ["EXO_SELECT_WG_CAP"]
+                    else:
+                        os.environ["EXO_SELECT_WG_CAP"] = prev
+        fused.FusedNets.select = select
+        print("select cap through os.environ", flush=True)
+
 
 def main():
+    _bisect_switches()
     from exo_amd import VecExoskeletonEnv
     from exo_amd.rollout import RefScheduleTrainer, VecTrainer
     from exo_amd.td7 import Agent, Hyperparameters
