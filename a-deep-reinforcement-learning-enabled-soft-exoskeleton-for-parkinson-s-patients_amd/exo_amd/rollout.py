@@ -56,6 +56,26 @@ def graph_reductions_ok(device, rows=1024, cols=300, replays=3):
     return True
 
 
+# Graphs of finished trainers kept alive until the process ends (retire_graphs).
+_RETIRED = []
+
+
+def retire_graphs(trainer):
+    """Move a finished trainer's captured graphs to a process-wide keep-alive
+    list instead of destroying them.  Every graph exec owns up to 4 runtime
+    streams spread over the GPU_MAX_HW_QUEUES = 4 hardware queues; destroying
+    execs frees them unevenly, after which the HIP runtime (ROCm 7.0 CLR,
+    first-launch stream assignment of a graph exec) can place two of a new
+    exec's streams on the launch stream's queue, skip both and read past its
+    stream array -- the round-4 segfault in hipGraphLaunch (DESIGN.md 4,
+    "The graph-replay crash").  Call with the device idle."""
+    for name in ("graphs", "_round_graphs"):
+        g = getattr(trainer, name, None)
+        if isinstance(g, dict) and g:
+            _RETIRED.append(dict(g))
+            g.clear()
+
+
 def _np_median(x):
     """numpy's median of a 1-D tensor (the mean of the two middle values for
     an even count; torch.median returns the lower one)."""

@@ -36,6 +36,10 @@ sys.path.insert(0, PKG)
 
 # before the HIP runtime initialises (see exo_amd/__init__.py)
 os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+# the reference schedule's burst steps sample the next batch at their end
+# (RefScheduleTrainer.burst_prefetch; 74.5 vs 75.6 ms per burst): on here,
+# where every finished phase's graphs are retired (_release), not destroyed
+os.environ.setdefault("EXO_BURST_PREFETCH", "1")
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -381,14 +385,16 @@ REFERENCE_ENV_STEPS_PER_UPDATE = 2257 / 283
 
 
 def _release(tr):
-    """Drop a finished phase's graphs now, with the device idle (the caller
-    then deletes the trainer / agent and calls _collect): graph and memory-pool
-    teardown never runs inside a later phase's stream capture."""
+    """Retire a finished phase's graphs with the device idle: moved to the
+    process-wide keep-alive list (exo_amd.rollout.retire_graphs), not destroyed.
+    Destroying graph execs releases their runtime streams unevenly over the
+    4 hardware queues, and the HIP runtime's first-launch stream assignment
+    of a later graph then over-reads its stream array when two of its streams
+    share the launch stream's queue -- the round-4 segfault in hipGraphLaunch
+    ("The graph-replay crash")."""
+    from exo_amd.rollout import retire_graphs
     torch.cuda.synchronize()
-    for name in ("graphs", "_round_graphs"):
-        g = getattr(tr, name, None)
-        if isinstance(g, dict):
-            g.clear()
+    retire_graphs(tr)
     torch.cuda.synchronize()
 
 
@@ -504,6 +510,7 @@ def reference_schedule(env, dev, args, hp, rounds=3, warm_rounds=3, group=None):
            "env_steps_per_round": env_steps / rounds, "rounds_timed": rounds,
            "env_steps_per_grad_step": env_steps / max(updates, 1),
            "checkpoint_refreshes": ag.checkpoint_refreshes, "replay": "reference shared pointer (add_batch_ref)",
+           "burst_prefetch": tr.burst_prefetch,
            "n_gpus": dist.get_world_size(group) if group is not None else 1,
            "dp_layout": dp_layout(tr) if group is not None else None,
            "note": "Exoskeleton_agent_train.py:110-211 on the device: warm-up 25,000 env-steps of uniform actions, "
@@ -1098,4 +1105,10 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    import faulthandler
+    faulthandler.enable()  # a host-side crash prints its Python stack
+    if os.environ.get("EXO_BENCH_STREAM") == "high":  # r05 experiment: every launch from a high-priority stream
+        with torch.cuda.stream(torch.cuda.Stream(priority=-1)):
+            main()
+    else:
+        main()

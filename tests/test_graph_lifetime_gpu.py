@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 
 def test_trainer_after_async_trainer_and_burst_prefetch_stats_rounds(monkeypatch):
     from exo_amd import VecExoskeletonEnv
-    from exo_amd.rollout import RefScheduleTrainer, VecTrainer
+    from exo_amd.rollout import RefScheduleTrainer, VecTrainer, retire_graphs
     from exo_amd.td7 import Agent, Hyperparameters
     monkeypatch.setenv("EXO_BURST_PREFETCH", "1")
     dev = torch.device("cuda", 0)
@@ -45,6 +45,7 @@ def test_trainer_after_async_trainer_and_burst_prefetch_stats_rounds(monkeypatch
     torch.cuda.synchronize()
     assert any(k[0] == "train" and len(k) == 5 for k in tr1.graphs)  # prefetching burst graphs were replayed
     assert len(tr1.round_stats) == 3
+    retire_graphs(tr1)  # the mitigation: its graph execs stay alive (exo_amd.rollout.retire_graphs)
     del tr1, ag1
     torch.cuda.synchronize()
     ag2 = agent()

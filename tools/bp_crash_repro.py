@@ -93,6 +93,10 @@ def main():
     torch.cuda.synchronize()
     keys = sorted(map(str, tr.graphs))
     print("ref trainer graph keys:", keys, flush=True)
+    if "retire" in sys.argv:  # r05 mitigation: keep the finished trainer's graph execs alive
+        from exo_amd.rollout import retire_graphs
+        retire_graphs(tr)
+        print("graphs retired", flush=True)
     del tr, ag
     import gc
     gc.collect()
