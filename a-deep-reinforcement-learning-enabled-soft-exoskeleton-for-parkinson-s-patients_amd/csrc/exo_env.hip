@@ -307,7 +307,7 @@ __device__ void reset_group(const Dev &S, const Urdf &U, int e, const double *dr
 // initialize_movement, :193-254): 16 envs per 256-thread workgroup -- every
 // env (slot = env index; mask: those set), or the n listed envs with their
 // injected draw streams
-constexpr int RESET_EPW = 16, RESET_TS = 16;
+constexpr int RESET_EPW = 16, RESET_TS = 32;
 __global__ __launch_bounds__(RESET_EPW *RESET_TS) void exo_reset_kernel(Dev S, Urdf U, const uint8_t *mask,
                                                                         const int32_t *ids, int n,
                                                                         const double *draws, int draw_stride,

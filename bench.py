@@ -974,6 +974,7 @@ def main():
                                         "resets"}
                                if measured_round else None),
             "env_kernel_env_steps_per_sec": active_avg / (kern_ms * 1e-3),
+            "reset_kernel_ms": reset_ms,  # one reset of every env (exo_reset_kernel), HIP events
             "roofline": {"kernel": ("exo_step_rp_kernel" if N <= 16384 else "exo_step_kernel")
                                    + (" + exo_multibody_kernel" if args.physics == "multibody" else ""), "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

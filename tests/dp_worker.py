@@ -41,6 +41,11 @@ def main():
     ap.add_argument("--iters", type=int, default=16)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--precision", default="bf16")
+    ap.add_argument("--no-noise", action="store_true",
+                    help="exploration and target-policy noise 0 (the full-loop comparison with one process)")
+    ap.add_argument("--dump", action="store_true",
+                    help="vec: save the sampled indices of every iteration and the final nets / trees")
     a = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("EXO_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
@@ -58,14 +63,25 @@ def main():
     env = VecExoskeletonEnv(a.envs, seed=1000 + rank, device=dev)
     out = {"rank": rank, "world": world}
     if a.mode == "vec":
-        agent = Agent(80, 7, 1, env_num=8, hp=Hyperparameters(), device=dev, precision="bf16", n_envs=a.envs,
+        hp = Hyperparameters(exploration_noise=0.0, target_policy_noise=0.0) if a.no_noise else Hyperparameters()
+        agent = Agent(80, 7, 1, env_num=8, hp=hp, device=dev, precision=a.precision, n_envs=a.envs,
                       process_group=dist.group.WORLD, graph_safe=True,
                       buffer_size=max(8192, a.iters * a.envs // 8))
         tr = VecTrainer(env, agent)
         out["dp_inline"] = tr.dp_inline
+        inds = []
         for _ in range(a.iters):
             tr.step()
+            if a.dump:  # the batch sampled for the next iteration: its slot is the new observation parity
+                inds.append(agent.replay_buffer._slot(tr._cur)[1].cpu().clone())
         torch.cuda.synchronize()
+        if a.dump:
+            L = agent.learner
+            torch.save({"ind": torch.stack(inds), "tree": agent.replay_buffer._tree.cpu(),
+                        "maxp": agent.replay_buffer._maxp.cpu(),
+                        **{f"{n}.{k}": v.detach().cpu() for n in ("actor", "critic", "encoder")
+                           for k, v in getattr(L, n).state_dict().items()}},
+                       os.path.join(a.out, f"final_r{rank}.pt"))
         rb = agent.replay_buffer
         per = a.envs // 8
         envs = sorted({e % a.envs for e in SAMPLE})

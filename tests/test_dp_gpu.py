@@ -206,3 +206,100 @@ def test_rccl_inline_layout_is_bit_identical_to_the_one_gpu_graph(monkeypatch):
                 torch.testing.assert_close(y, x, rtol=0, atol=0, msg=f"tensor {i} (capture={capture})")
     finally:
         dist.destroy_process_group()
+
+
+def _single_process_two_shards(iters, precision, envs=4096):
+    """ONE process stepping both ranks' envs (2 x 4,096 = 8,192: env seeds 1000
+    and 1001) and training on the concatenation of the two ranks' batches,
+    in VecTrainer's order (iteration 0: rollout, then the batch; later ones:
+    the batch sampled at the end of the previous iteration, then the rollout;
+    the update; the priority update + next sample per shard; the global
+    max_priority).  Each shard keeps its rank's replay (8 strata) and sampling
+    stream (torch seed 7 + rank, folded with the rank, as tests/dp_worker.py
+    and Agent do); exploration and target-policy noise are 0, so those
+    streams draw nothing that matters.  Returns the learner, both replays and
+    the per-iteration sampled indices."""
+    from exo_amd import VecExoskeletonEnv
+    from exo_amd.td7 import Agent, Hyperparameters
+    hp = Hyperparameters(exploration_noise=0.0, target_policy_noise=0.0)
+    shards = []
+    for r in range(2):
+        torch.manual_seed(7 + r)
+        env = VecExoskeletonEnv(envs, seed=1000 + r)
+        env.set_step_variant("rows_shared")  # VecTrainer's shape beside the TD7 passes
+        ag = Agent(80, 7, 1, env_num=8, hp=hp, precision=precision, n_envs=envs,
+                   buffer_size=max(8192, iters * envs // 8))
+        ag.replay_buffer._rng.fold(r)
+        ag.learner._explore_rng.fold(r)
+        strata = torch.as_tensor(env.motions % 8, dtype=torch.int32, device=env.device)
+        shards.append((env, ag, strata, [env.reset()]))
+    L = shards[0][1].learner  # rank 0's initial weights are the ones the data-parallel run broadcasts
+    inds = []
+
+    def rollout():
+        for env, ag, strata, obs in shards:
+            act = L_select(ag, obs[0])
+            nobs, rew, done, _ = env.step(act)
+            nobs = nobs.clone()
+            ag.replay_buffer.add_batch(obs[0], act, nobs, rew, done, strata)
+            obs[0] = nobs
+
+    def L_select(ag, o):  # the shard's own agent object, the shared weights
+        ag.learner = L
+        return ag.select_action_batch(o)
+
+    for it in range(iters):
+        if it == 0:
+            rollout()
+            batches = [sh[1].replay_buffer.sample(0) for sh in shards]
+            batches = [tuple(t.clone() for t in b) for b in batches]
+            idx = [sh[1].replay_buffer.ind.clone() for sh in shards]
+        else:
+            rollout()
+        cat = [torch.cat([b[k] for b in batches]) for k in range(5)]
+        prio = L.update(*cat).reshape(2, -1)
+        nxt = []
+        for r, (env, ag, strata, obs) in enumerate(shards):
+            rb = ag.replay_buffer
+            b = rb.update_priority_and_sample(prio[r], idx[r], slot=1)
+            nxt.append((tuple(t.clone() for t in b), rb.ind.clone()))
+        m = torch.maximum(shards[0][1].replay_buffer._maxp, shards[1][1].replay_buffer._maxp)
+        for sh in shards:
+            sh[1].replay_buffer._maxp.copy_(m)
+        batches = [n[0] for n in nxt]
+        idx = [n[1] for n in nxt]
+        inds.append([i.cpu() for i in idx])
+    torch.cuda.synchronize()
+    return L, [sh[1].replay_buffer for sh in shards], inds
+
+
+def test_data_parallel_full_loop_matches_one_process(tmp_path):
+    """the data-parallel training loop itself (VecTrainer on
+    2 gloo ranks x 4,096 envs, fp32 TD7, graph-replayed, the gradient buckets
+    averaged) against one process that steps both ranks' 8,192 envs and
+    trains on the concatenated batches (_single_process_two_shards).  Every
+    iteration's sampled indices must agree exactly (the LAP descent over the
+    shard's priorities: a priority off by more than the rounding would move
+    one), the final weights within tests/test_dp_bench_gpu.py's fp32 bounds
+    and the two shards' priority trees within fp32 rounding."""
+    iters = 12
+    outs = _run_workers(tmp_path, 2, "vec", ["--envs", "4096", "--iters", str(iters), "--precision", "fp32",
+                                             "--no-noise", "--dump"])
+    assert outs[0]["checksums"] == outs[1]["checksums"]
+    d = [torch.load(os.path.join(tmp_path, f"final_r{r}.pt"), weights_only=True) for r in range(2)]
+    L, rbs, inds = _single_process_two_shards(iters, "fp32")
+    for r in range(2):
+        for it in range(iters):
+            assert torch.equal(d[r]["ind"][it], inds[it][r]), f"rank {r} iteration {it}: sampled indices differ"
+        torch.testing.assert_close(rbs[r]._tree.cpu(), d[r]["tree"], rtol=1e-5, atol=1e-6)
+        assert float(rbs[r]._maxp) == float(d[r]["maxp"]) or abs(float(rbs[r]._maxp) - float(d[r]["maxp"])) < 1e-5
+    rtol, atol = 2e-5, 2e-6
+    outliers = total = 0
+    for n in ("actor", "critic", "encoder"):
+        for k, v in getattr(L, n).state_dict().items():
+            a, b = d[0][f"{n}.{k}"].double().numpy(), v.detach().cpu().double().numpy()
+            bad = np.abs(a - b) > atol + rtol * np.abs(b)
+            total += a.size
+            outliers += int(bad.sum())
+            assert not bad.any() or np.abs(a - b)[bad].max() <= 2 * 3e-4 * iters, f"{n}.{k}"
+    assert outliers <= 1e-3 * total, f"{outliers} of {total} entries outside rtol {rtol} / atol {atol}"
