@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 
 #include "philox.h"
@@ -38,11 +39,13 @@ __device__ __forceinline__ float *stratum_tree(float *tree, int s, int cap) { re
 // fewer -- and the recomputed nodes [1, TOPN/2) are written back.  The same
 // additions in the same order: the sums are bit-identical.
 constexpr int TOPN = 8192;
-// top: the caller's LDS array of TOPN floats; on return (true) it holds the
-// final nodes [1, min(TOPN, 2 cap)) (false: no level was staged, T holds them)
+// top: the caller's LDS array of NTOP floats; on return (true) it holds the
+// final nodes [1, min(NTOP, 2 cap)) (false: no level was staged, T holds them).
+// The staging loads are all issued before their LDS stores (one round trip).
+template <int NTOP = TOPN>
 __device__ bool propagate_top(float *T, int cap, int levels, const int32_t *slot, int n, float *top) {
     int lv = 1;
-    for (; lv <= levels && ((2 * cap) >> lv) > TOPN / 2; ++lv) {
+    for (; lv <= levels && ((2 * cap) >> lv) > NTOP / 2; ++lv) {
         __syncthreads();
         for (int k = threadIdx.x; k < n; k += blockDim.x) {
             const int node = (cap + slot[k]) >> lv;
@@ -51,8 +54,23 @@ __device__ bool propagate_top(float *T, int cap, int levels, const int32_t *slot
     }
     __syncthreads();
     if (lv > levels) return false;
-    const int lim = min(TOPN, 2 * cap);
-    for (int i = threadIdx.x; i < lim; i += blockDim.x) top[i] = T[i];
+    const int lim = min(NTOP, 2 * cap);
+    if (blockDim.x == UPD_THREADS) {
+        constexpr int PER = NTOP / UPD_THREADS;
+        float v[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int i = threadIdx.x + j * UPD_THREADS;
+            v[j] = i < lim ? T[i] : 0.0f;
+        }
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int i = threadIdx.x + j * UPD_THREADS;
+            if (i < lim) top[i] = v[j];
+        }
+    } else {
+        for (int i = threadIdx.x; i < lim; i += blockDim.x) top[i] = T[i];
+    }
     for (; lv <= levels; ++lv) {
         __syncthreads();
         for (int k = threadIdx.x; k < n; k += blockDim.x) {
@@ -61,7 +79,7 @@ __device__ bool propagate_top(float *T, int cap, int levels, const int32_t *slot
         }
     }
     __syncthreads();
-    const int wb = min(TOPN / 2, cap);
+    const int wb = min(NTOP / 2, cap);
     for (int i = 1 + threadIdx.x; i < wb; i += blockDim.x) T[i] = top[i];
     __syncthreads();
     return true;
@@ -207,19 +225,86 @@ __global__ __launch_bounds__(UPD_THREADS) void lap_add_kernel(float *tree, const
 // quirk (:59-61) strata 1..E-1 hold their newest transition at slot == size,
 // outside that prefix -- so the draw is scaled by the prefix total, not the
 // root.  One root-to-leaf walk towards leaf sz adding every left sibling.
-__device__ __forceinline__ float prefix_total(const float *T, int cap, int levels, int sz) {
-    if (sz >= cap) return T[1];
-    float acc = 0.0f;
-    int node = 1;
-    for (int lv = levels - 1; lv >= 0; --lv) {
-        if ((sz >> lv) & 1) {
-            acc += T[2 * node];
-            node = 2 * node + 1;
-        } else {
-            node = 2 * node;
+// The walk's nodes depend on sz alone (step j visits (1 << j) | sz >> (levels
+// - j)): every addend is loaded first, independently, and then added in the
+// walk's order (an unset bit adds +0: the same sum) -- one memory round trip
+// instead of one per level.  at(node): the tree accessor.
+constexpr int MAXLV = 24;  // levels of a stratum tree (capacity <= 2^24)
+template <class At>
+__device__ __forceinline__ float prefix_sum(At at, int cap, int levels, int sz) {
+    if (sz >= cap) return at(1);
+    float v[MAXLV];
+#pragma unroll
+    for (int j = 0; j < MAXLV; ++j) {
+        v[j] = 0.0f;
+        if (j < levels) {
+            const int lv = levels - 1 - j;
+            const float x = at(2 * ((1 << j) | (sz >> (lv + 1))));
+            v[j] = ((sz >> lv) & 1) ? x : 0.0f;
         }
     }
+    float acc = 0.0f;
+#pragma unroll
+    for (int j = 0; j < MAXLV; ++j)
+        if (j < levels) acc += v[j];
     return acc;
+}
+__device__ __forceinline__ float prefix_total(const float *T, int cap, int levels, int sz) {
+    return prefix_sum([T](int n) { return T[n]; }, cap, levels, sz);
+}
+
+__device__ __forceinline__ float sel4(int r, float a, float b, float c, float d) {
+    return r == 0 ? a : r == 1 ? b : r == 2 ? c : d;
+}
+
+// The descent from `node` at level lv to a leaf: at every level go left when
+// val <= left (or the right subtree is empty), else subtract left and go
+// right.  The children of the next (up to) three levels are read together --
+// 2 + 4 + 8 nodes at 2n, 4n, 8n -- and the three choices made from registers:
+// the same comparisons and subtractions as the one-level walk, a third of its
+// dependent memory round trips.  Returns the leaf node.
+template <class At>
+__device__ __forceinline__ int descend_from(At at, float val, int node, int lv, int levels) {
+    while (lv < levels) {
+        const int k = levels - lv >= 3 ? 3 : levels - lv;
+        const int n1 = 2 * node, n2 = 4 * node, n3 = 8 * node;
+        const float a0 = at(n1), a1 = at(n1 + 1);
+        float b0 = 0.f, b1 = 0.f, b2 = 0.f, b3 = 0.f, c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
+        float c4 = 0.f, c5 = 0.f, c6 = 0.f, c7 = 0.f;
+        if (k >= 2) b0 = at(n2), b1 = at(n2 + 1), b2 = at(n2 + 2), b3 = at(n2 + 3);
+        if (k >= 3) {
+            c0 = at(n3), c1 = at(n3 + 1), c2 = at(n3 + 2), c3 = at(n3 + 3);
+            c4 = at(n3 + 4), c5 = at(n3 + 5), c6 = at(n3 + 6), c7 = at(n3 + 7);
+        }
+        int r;
+        if (val <= a0 || a1 <= 0.0f) {
+            r = 0;
+        } else {
+            val -= a0;
+            r = 1;
+        }
+        if (k >= 2) {
+            const float l = r ? b2 : b0, rt = r ? b3 : b1;
+            if (val <= l || rt <= 0.0f) {
+                r = 2 * r;
+            } else {
+                val -= l;
+                r = 2 * r + 1;
+            }
+            if (k >= 3) {
+                const float l3 = sel4(r, c0, c2, c4, c6), r3 = sel4(r, c1, c3, c5, c7);
+                if (val <= l3 || r3 <= 0.0f) {
+                    r = 2 * r;
+                } else {
+                    val -= l3;
+                    r = 2 * r + 1;
+                }
+            }
+        }
+        node = (node << k) + r;
+        lv += k;
+    }
+    return node;
 }
 
 // LAP.sample (:75-78): idx = searchsorted_left(cumsum(p[:size]), u * total)
@@ -230,17 +315,8 @@ __global__ void lap_sample_kernel(const float *tree, int cap, int levels, const 
     if (b >= batch) return;
     const float *T = tree + (size_t)s * 2 * cap;
     const int sz = size[s];
-    float val = u[(size_t)s * batch + b] * prefix_total(T, cap, levels, sz);
-    int node = 1;
-    for (int lv = 0; lv < levels; ++lv) {
-        const float left = T[2 * node], right = T[2 * node + 1];
-        if (val <= left || right <= 0.0f) {
-            node = 2 * node;
-        } else {
-            val -= left;
-            node = 2 * node + 1;
-        }
-    }
+    const float val = u[(size_t)s * batch + b] * prefix_total(T, cap, levels, sz);
+    const int node = descend_from([T](int n) { return T[n]; }, val, 1, 0, levels);
     int i = node - cap;
     if (i >= sz) i = sz > 0 ? sz - 1 : 0;
     idx[(size_t)s * batch + b] = i;
@@ -808,17 +884,8 @@ __device__ __forceinline__ void sample_descend(const float *tree, int cap, int l
     const int s = d / batch;
     const float *T = tree + (size_t)s * 2 * cap;
     const int sz = size[s];
-    float val = ud * prefix_total(T, cap, levels, sz);
-    int node = 1;
-    for (int lv = 0; lv < levels; ++lv) {
-        const float left = T[2 * node], right = T[2 * node + 1];
-        if (val <= left || right <= 0.0f) {
-            node = 2 * node;
-        } else {
-            val -= left;
-            node = 2 * node + 1;
-        }
-    }
+    const float val = ud * prefix_total(T, cap, levels, sz);
+    const int node = descend_from([T](int n) { return T[n]; }, val, 1, 0, levels);
     int i = node - cap;
     if (i >= sz) i = sz > 0 ? sz - 1 : 0;
     if (lane == 0) idx[d] = i;
@@ -874,6 +941,79 @@ __global__ __launch_bounds__(256) void lap_sample_gather_kernel(const float *tre
 }
 
 
+// The top of a stratum tree lap_update_sample stages in LDS (r05 A/B at the
+// bench's shape, tools/lap_bench.py: 32,768 nodes -- 128 KB, 3 global levels
+// left instead of 6 -- 23.9 us per launch against 21.8 with 8,192: staging
+// 128 KB costs more than the three level sweeps it saves)
+#ifndef LAP_TOPN_US
+#define LAP_TOPN_US 8192
+#endif
+constexpr int TOPN_US = LAP_TOPN_US;
+
+// The sampled rows gathered by their own launch (r05): lap_update_sample's
+// stratum workgroups stop at the indices, and DRAWS draws per 256-thread
+// workgroup here copy state, next_state (float4 where aligned), action,
+// reward and not_done -- 64 workgroups for the bench's 8 x 128 batch instead
+// of the 8 that ran the update (9.7 of its 24.7 us, r05g).
+constexpr int GATHER_DRAWS = 16;
+__global__ __launch_bounds__(256) void lap_gather_kernel(lap_storage_desc st, int capacity, const int32_t *idx,
+                                                         int batch, int total, float *o_state, float *o_action,
+                                                         float *o_next, float *o_reward, float *o_not_done) {
+    const int sd = st.state_dim, ad = st.action_dim;
+    const bool v4 = (sd & 3) == 0 && ((reinterpret_cast<uintptr_t>(st.state) | reinterpret_cast<uintptr_t>(st.next_state) |
+                                       reinterpret_cast<uintptr_t>(o_state) | reinterpret_cast<uintptr_t>(o_next)) & 15) == 0;
+    const int sv = v4 ? sd / 4 : sd, per = 2 * sv + ad + 2;
+    const int d0 = blockIdx.x * GATHER_DRAWS;
+    const int nd = min(GATHER_DRAWS, total - d0);
+    const int items = nd * per;
+    constexpr int GU = 4;
+    for (int it0 = threadIdx.x; it0 < items; it0 += GU * 256) {
+        float4 v[GU];
+        float *dst[GU];
+        bool wide[GU];
+#pragma unroll
+        for (int u = 0; u < GU; ++u) {
+            const int it = it0 + u * 256;
+            dst[u] = nullptr;
+            wide[u] = false;
+            if (it >= items) continue;
+            const int q = it / per, c = it - q * per;
+            const long d = d0 + q;
+            const long row = (long)(d / batch) * (capacity + 1) + idx[d];
+            if (c < 2 * sv) {
+                const bool nx = c >= sv;
+                const int e = nx ? c - sv : c;
+                const float *src = (nx ? st.next_state : st.state) + row * sd;
+                float *o = (nx ? o_next : o_state) + d * sd;
+                if (v4) {
+                    v[u] = ld4(src + 4 * e);
+                    dst[u] = o + 4 * e;
+                    wide[u] = true;
+                } else {
+                    v[u].x = src[e];
+                    dst[u] = o + e;
+                }
+            } else if (c < 2 * sv + ad) {
+                const int e = c - 2 * sv;
+                v[u].x = st.action[row * ad + e];
+                dst[u] = o_action + d * ad + e;
+            } else if (c == 2 * sv + ad) {
+                v[u].x = st.reward[row];
+                dst[u] = o_reward + d;
+            } else {
+                v[u].x = st.not_done[row];
+                dst[u] = o_not_done + d;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < GU; ++u) {
+            if (!dst[u]) continue;
+            if (wide[u]) st4(dst[u], v[u]);
+            else *dst[u] = v[u].x;
+        }
+    }
+}
+
 // LAP.update_priority (:113-117) and the NEXT LAP.sample (:65-111) as ONE
 // launch (r04: lap_update_kernel + lap_sample_gather_kernel were 32 us plus a
 // queue hand-off at the end of every critic-only iteration).  One workgroup
@@ -900,14 +1040,14 @@ __global__ __launch_bounds__(UPD_THREADS) void lap_update_sample_kernel(float *t
                                                                         SampleRng rng, int32_t *idx_out,
                                                                         float *o_state, float *o_action, float *o_next,
                                                                         float *o_reward, float *o_not_done,
-                                                                        TdPrio tp) {
+                                                                        TdPrio tp, bool gather) {
     const int s = blockIdx.x;
     float *T = stratum_tree(tree, s, cap);
     const int32_t *I = idx_in + (size_t)s * batch;
     const float *P = prio + (size_t)s * batch;
     __shared__ float red[UPD_THREADS / 64];
     __shared__ int32_t li[UPD_THREADS];
-    __shared__ float top[TOPN];
+    __shared__ float top[TOPN_US];
     __shared__ int32_t pick[UPD_THREADS];
     const unsigned long long call = *rng.counter;  // read before any workgroup can take the ticket
     float mx = 0.0f;
@@ -936,38 +1076,26 @@ __global__ __launch_bounds__(UPD_THREADS) void lap_update_sample_kernel(float *t
     }
     for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
-    const bool staged = propagate_top(T, cap, levels, I, batch, top);
+    const bool staged = propagate_top<TOPN_US>(T, cap, levels, I, batch, top);
     if (threadIdx.x == 0) {
         for (int w = 1; w < (int)(blockDim.x >> 6); ++w) mx = fmaxf(mx, red[w]);
         atomicMax(reinterpret_cast<int *>(maxp), __float_as_int(mx));
     }
     // ---- the next batch of this stratum
-    const int lim = staged ? min(TOPN, 2 * cap) : 0;
+    const int lim = staged ? min(TOPN_US, 2 * cap) : 0;
     auto node_at = [&](int node) { return node < lim ? top[node] : T[node]; };
     const int sz = size[s];
+    const float tot = prefix_sum(node_at, cap, levels, sz);
     for (int b = threadIdx.x; b < batch; b += UPD_THREADS) {
         const int d = s * batch + b;
         uint32_t r[4];
         philox_block(rng.seed, rng.tag, call, (uint32_t)d, r);
-        float tot;
-        if (sz >= cap) {
-            tot = node_at(1);
-        } else {  // prefix_total
-            tot = 0.0f;
-            int node = 1;
-            for (int lv = levels - 1; lv >= 0; --lv) {
-                if ((sz >> lv) & 1) {
-                    tot += node_at(2 * node);
-                    node = 2 * node + 1;
-                } else {
-                    node = 2 * node;
-                }
-            }
-        }
         float val = u01_open_hi(r[0]) * tot;
-        int node = 1;
-        for (int lv = 0; lv < levels; ++lv) {
-            const float left = node_at(2 * node), right = node_at(2 * node + 1);
+        // the staged top levels from LDS one level at a time, the rest (below
+        // TOPN) three levels per round trip
+        int node = 1, lv = 0;
+        for (; lv < levels && 2 * node + 1 < lim; ++lv) {
+            const float left = top[2 * node], right = top[2 * node + 1];
             if (val <= left || right <= 0.0f) {
                 node = 2 * node;
             } else {
@@ -975,12 +1103,20 @@ __global__ __launch_bounds__(UPD_THREADS) void lap_update_sample_kernel(float *t
                 node = 2 * node + 1;
             }
         }
+        node = descend_from([T](int n) { return T[n]; }, val, node, lv, levels);
         int i = node - cap;
         if (i >= sz) i = sz > 0 ? sz - 1 : 0;
         idx_out[d] = i;
         if (b < UPD_THREADS) pick[b] = i;
     }
     __syncthreads();
+    if (!gather) {  // the rows follow in lap_gather_kernel; the call counter's ticket below
+        if (threadIdx.x == 0 && atomicAdd(rng.ticket, 1u) == gridDim.x - 1) {
+            *rng.counter = call + 1ull;
+            *rng.ticket = 0u;
+        }
+        return;
+    }
     // gather: (draw, item) over the workgroup, items = state, next_state (float4
     // where the rows are 16-byte aligned), action, reward, not_done; GU items
     // per thread loaded before any is stored (the stores may alias the loads as
@@ -1052,6 +1188,27 @@ int levels_of(const lap_tree_desc *t) {
     int lv = 0;
     while ((1 << lv) < t->cap) ++lv;
     return lv;
+}
+
+// lap_update_sample's rows gathered by lap_gather_kernel (EXO_LAP_GATHER_SPLIT=0:
+// by the update's own stratum workgroups, the r04 layout)
+bool gather_split() {
+    static const bool on = [] {
+        const char *e = getenv("EXO_LAP_GATHER_SPLIT");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+int gather_after(const lap_tree_desc *t, const lap_storage_desc *st, int batch, const int32_t *idx, float *o_state,
+                 float *o_action, float *o_next, float *o_reward, float *o_not_done, void *stream) {
+    if (hipGetLastError() != hipSuccess) return EXO_EDEVICE;
+    if (!gather_split()) return EXO_OK;
+    const int total = t->n_strata * batch;
+    hipLaunchKernelGGL(lap_gather_kernel, dim3((total + GATHER_DRAWS - 1) / GATHER_DRAWS), dim3(256), 0,
+                       (hipStream_t)stream, *st, t->capacity, idx, batch, total, o_state, o_action, o_next, o_reward,
+                       o_not_done);
+    return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
 }
 
 bool valid(const lap_tree_desc *t) {
@@ -1229,8 +1386,8 @@ int lap_update_sample_rng(const lap_tree_desc *t, const lap_storage_desc *st, co
     hipLaunchKernelGGL(lap_update_sample_kernel, dim3(t->n_strata), dim3(UPD_THREADS), 0, (hipStream_t)stream,
                        t->tree, t->max_priority, t->cap, levels_of(t), t->capacity, idx_in, prio, batch, st->size,
                        *st, SampleRng{seed, tag, counter, ticket}, idx_out, out_state, out_action, out_next_state,
-                       out_reward, out_not_done, TdPrio{nullptr, 0.f, 0.f, nullptr});
-    return rc(hipGetLastError());
+                       out_reward, out_not_done, TdPrio{nullptr, 0.f, 0.f, nullptr}, !gather_split());
+    return gather_after(t, st, batch, idx_out, out_state, out_action, out_next_state, out_reward, out_not_done, stream);
 }
 
 int lap_update_sample_td(const lap_tree_desc *t, const lap_storage_desc *st, const int32_t *idx_in, const float *td,
@@ -1244,8 +1401,9 @@ int lap_update_sample_td(const lap_tree_desc *t, const lap_storage_desc *st, con
     hipLaunchKernelGGL(lap_update_sample_kernel, dim3(t->n_strata), dim3(UPD_THREADS), 0, (hipStream_t)stream,
                        t->tree, t->max_priority, t->cap, levels_of(t), t->capacity, idx_in, (const float *)nullptr,
                        batch, st->size, *st, SampleRng{seed, tag, counter, ticket}, idx_out, out_state, out_action,
-                       out_next_state, out_reward, out_not_done, TdPrio{td, alpha, min_priority, prio_out});
-    return rc(hipGetLastError());
+                       out_next_state, out_reward, out_not_done, TdPrio{td, alpha, min_priority, prio_out},
+                       !gather_split());
+    return gather_after(t, st, batch, idx_out, out_state, out_action, out_next_state, out_reward, out_not_done, stream);
 }
 
 int lap_sample_gather_rng(const lap_tree_desc *t, const lap_storage_desc *st, uint64_t seed, uint32_t tag,
