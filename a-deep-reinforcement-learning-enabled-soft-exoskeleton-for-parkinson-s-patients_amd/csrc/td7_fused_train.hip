@@ -80,6 +80,12 @@ struct CriticArgs {
     R32 H0, DY, F, TW;
     int small_off;     // 2 x 16 floats: row means, row dots
     int lds_bytes;
+    // phase (td7f_critic_phase): 0 the whole pass; 1 the forward alone, its
+    // state for the backward stored -- Q [2][Bp], the pre-norm q0 output H0
+    // [2][Bp][Hc] and the row means [2][Bp] (Bp = B padded to 16 rows); 2 the
+    // loss and the backward from that state
+    int phase;
+    float *qs, *h0s, *ms;
 };
 
 template <int P, int TH>
@@ -92,6 +98,35 @@ __global__ __launch_bounds__(NTH) void critic_kernel(CriticArgs a) {
     float *y1 = a.y1 + (long)h * B * Hc, *y2 = a.y2 + (long)h * B * Hc;
     int si = 0;
     FSTAMP(si);
+    u32x4 R[PD][TH];
+    const long Bp = (long)gridDim.x * TR;
+    if (a.phase == 2) {
+        // the forward's state back into LDS (the same fp32 values), the ring
+        // filled with q3's first backward k-steps as the forward's tail left it
+        constexpr int PER = TR * 320 / NTH;  // H0 values per thread (Hc <= 320)
+        const float *h0 = a.h0s + ((long)h * Bp + row0) * Hc;
+        float v[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int i = threadIdx.x + j * NTH;
+            v[j] = i < TR * Hc ? ldg(h0 + i) : 0.f;
+        }
+        const float qv = threadIdx.x < TR ? ldg(a.qs + h * Bp + row0 + threadIdx.x) : 0.f;
+        const float mv = threadIdx.x < TR ? ldg(a.ms + h * Bp + row0 + threadIdx.x) : 0.f;
+        ring_fill(R, bwd_of(cr[6], 0));
+        zero_lds(lds, a.lds_bytes);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int i = threadIdx.x + j * NTH;
+            if (i < TR * Hc) *p32(lds, a.H0, i / Hc, i % Hc) = v[j];
+        }
+        if (threadIdx.x < TR) {
+            *p32(lds, a.F, threadIdx.x, 0) = qv;
+            mean[threadIdx.x] = mv;
+        }
+        __syncthreads();
+    } else {
     RowStage ss, sa, sz, szs;
     ThinStage<1> tw;
     row_issue(ss, a.s, a.S, a.S, row0, B);
@@ -99,7 +134,6 @@ __global__ __launch_bounds__(NTH) void critic_kernel(CriticArgs a) {
     row_issue(sz, a.zsa, Z, Z, row0, B);
     row_issue(szs, a.zs, Z, Z, row0, B);
     thin_issue(tw, cr[6].w, cr[6].ldw, 0, false, 1, cr[6].K);
-    u32x4 R[PD][TH];
     ring_fill(R, fwd_of(cr[0]));
     zero_lds(lds, a.lds_bytes);
     __syncthreads();
@@ -121,6 +155,17 @@ __global__ __launch_bounds__(NTH) void critic_kernel(CriticArgs a) {
     save_xt<P>(lds, a.H1, 0, Hc, xt[4].x, a.ld, TR, row0);
     save_xt<P>(lds, a.H2, 0, Hc, xt[6].x, a.ld, TR, row0);
     layer_thin_fwd<P, 1>(lds, a.H2, cr[6], a.TW, ACT_NONE, a.F, TR, nullptr, 0, row0, B, si);
+    if (a.phase == 1) {  // the state the backward launch needs, then done
+        __syncthreads();
+        float *h0 = a.h0s + ((long)h * Bp + row0) * Hc;
+        for (int i = threadIdx.x; i < TR * Hc; i += NTH) stg(h0 + i, *p32(lds, a.H0, i / Hc, i % Hc));
+        if (threadIdx.x < TR) {
+            stg(a.qs + h * Bp + row0 + threadIdx.x, *p32(lds, a.F, threadIdx.x, 0));
+            stg(a.ms + h * Bp + row0 + threadIdx.x, mean[threadIdx.x]);
+        }
+        return;
+    }
+    }
     // Q_target (:241-246) and the LAP-Huber gradient (:257-259) of this head
     if (threadIdx.x < TR) {
         const int r = threadIdx.x, b = row0 + r;
@@ -792,9 +837,19 @@ int td7f_critic(int32_t prec, const int32_t *act, const td7f_lin *critic, const 
                 float discount, const float *lo, const float *hi, float *run_max, float *run_min, int32_t B,
                 int32_t S, int32_t A, float *td, float *q, float *y1, float *y2, const td7f_xt *xt, int64_t ld,
                 void *stream) {
+    return td7f_critic_phase(0, prec, act, critic, s, a, zs, zsa, qt, reward, not_done, discount, lo, hi, run_max,
+                             run_min, B, S, A, td, q, y1, y2, xt, ld, nullptr, nullptr, nullptr, stream);
+}
+
+int td7f_critic_phase(int32_t phase, int32_t prec, const int32_t *act, const td7f_lin *critic, const float *s,
+                      const float *a, const float *zs, const float *zsa, const float *qt, const float *reward,
+                      const float *not_done, float discount, const float *lo, const float *hi, float *run_max,
+                      float *run_min, int32_t B, int32_t S, int32_t A, float *td, float *q, float *y1, float *y2,
+                      const td7f_xt *xt, int64_t ld, float *q_ws, float *h0_ws, float *mean_ws, void *stream) {
     if (!prec_ok(prec) || !act || !critic || !s || !a || !zs || !zsa || !qt || !reward || !not_done || !lo || !hi ||
         !run_max || !run_min || !td || !y1 || !y2 || !xt || B <= 0 || S <= 0 || S > NTH || A <= 0 || A > THIN_NC || ld < B || ld % 32)
         return EXO_EINVAL;
+    if (phase < 0 || phase > 2 || (phase != 0 && (!q_ws || !h0_ws || !mean_ws))) return EXO_EINVAL;
     const int th = th_of(critic, 8);
     if ((th != 4 && th != 5) || !wb_ok(critic, 8) || !xt_ok(xt, 8)) return EXO_EINVAL;
     CriticArgs g{};
@@ -811,9 +866,11 @@ int td7f_critic(int32_t prec, const int32_t *act, const td7f_lin *critic, const 
     g.Hc = critic[0].n_out;
     g.Z = (critic[2].n_in - g.Hc) / 2;
     if (critic[0].n_in != S + A || critic[4].n_in != g.Hc || critic[6].n_in != g.Hc || critic[6].n_out != 1 ||
-        g.Z * 2 + g.Hc != critic[2].n_in || g.Hc % 16)
+        g.Z * 2 + g.Hc != critic[2].n_in || g.Hc % 16 || g.Hc > 320)
         return EXO_EINVAL;
     g.td = td; g.q = q; g.y1 = y1; g.y2 = y2; g.ld = ld;
+    g.phase = phase;
+    g.qs = q_ws; g.h0s = h0_ws; g.ms = mean_ws;
     const int kd = kd_of(prec);
     Bump b(1);
     g.X = b.r16(TR, ld16(S + A, kd));

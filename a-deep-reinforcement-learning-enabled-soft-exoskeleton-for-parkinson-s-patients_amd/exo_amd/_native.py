@@ -226,6 +226,9 @@ EXPORTS = {
                              c_void_p]),
     "td7f_critic": (c_int32, [c_int32, P(c_int32), P(TD7FLin)] + [c_void_p] * 7 + [ctypes.c_float]
                     + [c_void_p] * 4 + [c_int32] * 3 + [c_void_p] * 4 + [P(TD7FXT), ctypes.c_int64, c_void_p]),
+    "td7f_critic_phase": (c_int32, [c_int32, c_int32, P(c_int32), P(TD7FLin)] + [c_void_p] * 7 + [ctypes.c_float]
+                          + [c_void_p] * 4 + [c_int32] * 3 + [c_void_p] * 4
+                          + [P(TD7FXT), ctypes.c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
     "td7f_encoder": (c_int32, [c_int32, P(c_int32), P(TD7FLin), c_void_p, c_void_p, c_void_p, c_int32, P(c_void_p),
                                P(TD7FXT), ctypes.c_int64, c_void_p, c_void_p, c_void_p]),
     "td7f_actor": (c_int32, [c_int32, c_int32, P(c_int32), P(TD7FLin), P(TD7FLin), P(TD7FLin), c_void_p, c_void_p,

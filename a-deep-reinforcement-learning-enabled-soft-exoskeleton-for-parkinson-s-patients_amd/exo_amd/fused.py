@@ -374,6 +374,12 @@ class FusedTrain:
         self.y_critic = [torch.empty((2, B, Hc), **f32) for _ in range(2)]
         self.td = torch.zeros((B, 2), **f32)
         self.q = torch.zeros((B, 2), **f32)
+        # the critic pass split in two launches (critic(phase=1 / 2)): the
+        # forward's state for the backward -- Q, q0's pre-norm output, row means
+        bp = -(-B // 16) * 16
+        self.crit_q = torch.zeros((2, bp), **f32)
+        self.crit_h0 = torch.zeros((2, bp, Hc), **f32)
+        self.crit_mean = torch.zeros((2, bp), **f32)
         self.prio = torch.zeros((B,), **f32)
         self.act_out = torch.zeros((B, A), **f32)
         self.zsa_out = torch.zeros((B, Z), **f32)
@@ -479,15 +485,20 @@ class FusedTrain:
                                          nat.ptr(next_state), self.B, self.ptrs_y_enc, self._xts(self.xt_enc), self.ld,
                                          nat.ptr(nz), nat.ptr(fl), nat.stream_ptr(state.device)), "td7f_encoder")
 
-    def critic(self, state, action, zs, zsa, qt, reward, not_done):
+    def critic(self, state, action, zs, zsa, qt, reward, not_done, phase=0):
+        """td7f_critic_phase: 0 the whole critic pass; 1 its forward alone (needs
+        no qt: it runs beside the target chain); 2 the loss and the backward
+        from phase 1's stored state -- phases 1 + 2 == phase 0 bit for bit."""
         fz, L = self.nets, self.L
-        fz.refresh("critic")
-        nat.check(nat.lib().td7f_critic(
-            fz.prec, fz.act, fz.nets["critic"].array, nat.ptr(state), nat.ptr(action), nat.ptr(zs), nat.ptr(zsa),
-            nat.ptr(qt), nat.ptr(reward), nat.ptr(not_done), float(L.hp.discount), nat.ptr(L.min_target),
-            nat.ptr(L.max_target), nat.ptr(L.max), nat.ptr(L.min), self.B, self.S, self.A, nat.ptr(self.td),
-            nat.ptr(self.q), nat.ptr(self.y_critic[0]), nat.ptr(self.y_critic[1]), self._xts(self.xt_critic), self.ld,
-            nat.stream_ptr(state.device)), "td7f_critic")
+        if phase != 2:
+            fz.refresh("critic")
+        nat.check(nat.lib().td7f_critic_phase(
+            int(phase), fz.prec, fz.act, fz.nets["critic"].array, nat.ptr(state), nat.ptr(action), nat.ptr(zs),
+            nat.ptr(zsa), nat.ptr(qt), nat.ptr(reward), nat.ptr(not_done), float(L.hp.discount),
+            nat.ptr(L.min_target), nat.ptr(L.max_target), nat.ptr(L.max), nat.ptr(L.min), self.B, self.S, self.A,
+            nat.ptr(self.td), nat.ptr(self.q), nat.ptr(self.y_critic[0]), nat.ptr(self.y_critic[1]),
+            self._xts(self.xt_critic), self.ld, nat.ptr(self.crit_q), nat.ptr(self.crit_h0), nat.ptr(self.crit_mean),
+            nat.stream_ptr(state.device)), "td7f_critic_phase")
 
     def wgrad_encoder_critic(self):
         """Every encoder and critic weight/bias gradient (one launch) and the LAP priorities."""

@@ -74,6 +74,9 @@ def retire_graphs(trainer):
         if isinstance(g, dict) and g:
             _RETIRED.append(dict(g))
             g.clear()
+    if trainer.__dict__.get("_refresh_graph") is not None:
+        _RETIRED.append(trainer._refresh_graph)
+        trainer._refresh_graph = None
 
 
 def _np_median(x):
@@ -647,6 +650,8 @@ class VecTrainer:
                 parts = [g1, g2, g3, flat_c, flat_a]
         torch.cuda.current_stream(self.device).wait_stream(s)
         self.graphs[self._key(update_actor, rollout)] = parts
+        if self.dp_inline and self._refresh_graph is None:
+            self._capture_refresh()
         # capture records but does not execute: run the iteration now
         self._replay(update_actor, rollout)
 
@@ -769,13 +774,56 @@ class VecTrainer:
         L.pre_in = None
         return self._step_tail()
 
+    # The target refresh every target_update_rate steps (:284-293, plus the LAP
+    # max_priority reset, :119-120) with the collectives of data parallelism
+    # (the Q bounds and max_priority MAX-reduced): on RCCL with the collectives
+    # captured in the iteration graphs it is itself replayed from a graph
+    # captured at the first refresh, so no eager collective follows the
+    # captured ones -- the first such eager all-reduce of a process cost 96 ms
+    # (31-35 ms in later processes) of host time, GPU idle, at training step
+    # 250: the first RCCL process's slow mode of r04 (profiles/r05rccl_raw).
+    _refresh_graph = None
+
+    def _refresh_targets(self):
+        ag = self.agent
+        L = ag.learner
+        if L.training_steps % L.hp.target_update_rate != 0:
+            return False
+        if not (self.dp_inline and self.use_graphs):
+            L.maybe_update_targets()
+            ag.replay_buffer.reset_max_priority()
+            ag.sync.max_(ag.replay_buffer._maxp)
+            return True
+        L.drop_prefetch()
+        if self._refresh_graph is None:
+            self._capture_refresh()
+        self._refresh_graph.replay()
+        return True
+
+    def _capture_refresh(self):
+        """Record (not run) the refresh graph.  Captured with the first
+        iteration graphs, not at the first refresh inside a timed window: the
+        capture of its collectives itself cost ~60 ms there (r05).  Thread-
+        local capture mode: the process group's watchdog thread queries its
+        events meanwhile (a global-mode capture failed it once with
+        hipErrorStreamCaptureUnsupported)."""
+        ag, L = self.agent, self.agent.learner
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"), ForkJoinAudit(s):
+                L.update_targets_device()
+                ag.replay_buffer.reset_max_priority()
+                ag.sync.max_(ag.replay_buffer._maxp)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        self._refresh_graph = g
+
     def _step_tail(self):
         """Host bookkeeping after an iteration's GPU work."""
         ag = self.agent
         L = ag.learner
-        if L.maybe_update_targets():
-            ag.replay_buffer.reset_max_priority()
-            ag.sync.max_(ag.replay_buffer._maxp)
+        self._refresh_targets()
         if self.budget:
             n_active = 0
         elif self.episodes == "async":
@@ -1094,9 +1142,7 @@ class RefScheduleTrainer(VecTrainer):
         L.prefetch_actor = False
         self._burst_i += 1
         self._train_pin = self._train_pout = False
-        if L.maybe_update_targets():
-            ag.replay_buffer.reset_max_priority()
-            ag.sync.max_(ag.replay_buffer._maxp)
+        self._refresh_targets()
         self._train_iters += 1
 
     # -------------------------------------------------------------- round

@@ -39,6 +39,14 @@ from .ops import avg_l1_norm
 # on a branch that finished early -- measured 307 vs 304 us per iteration
 # (profiles/r03_sched_raw/ab.txt); EXO_TD7_TARGET_ON_MAIN=1 turns it on
 TARGET_ON_MAIN = os.environ.get("EXO_TD7_TARGET_ON_MAIN", "0") == "1"
+# r05: the fused critic pass as two launches, the forward (Q, which needs only
+# the batch and the fixed embeddings) on the fixed embeddings' stream beside
+# the target chain, the loss and backward once the target heads are in
+# (td7f_critic_phase, bit-identical to one launch).  Measured slower, so off:
+# 0.318-0.319 vs 0.296-0.303 ms per bf16 iteration, 0.510-0.513 vs 0.487-0.491
+# fp32 (profiles/r05m_raw) -- its 128 workgroups take CUs from the target chain
+# it runs beside.  EXO_CRITIC_SPLIT=1 turns it on.
+CRITIC_SPLIT = os.environ.get("EXO_CRITIC_SPLIT", "0") == "1"
 # fused optimiser step + weight repack (td7f_adam_pack); EXO_ADAM_PACK=0: two launches
 ADAM_PACK = os.environ.get("EXO_ADAM_PACK", "1") != "0"
 # graph-replayed trainer on one GPU, fused: the encoder's weight gradients and
@@ -849,6 +857,7 @@ class TD7Learner:
         wg_adam = enc_step and WGRAD_ADAM and tr.fuses_adam() and not self.sync.active
         self._enc_step_pending = False
         self._actor_fused_pre = False
+        critic_phase = 0
         pre = self.pre_in
         self.pre_in = None
         if pre is not None:
@@ -916,9 +925,13 @@ class TD7Learner:
                 with torch.cuda.stream(aside):
                     tr.actor(0, state, zs)
                 self._actor_fused_pre = True
+            if branch and CRITIC_SPLIT:
+                # the critic's forward now, beside the target chain
+                tr.critic(state, action, zs, zsa, qt, reward, not_done, phase=1)
+                critic_phase = 2
             if branch:
                 cur.wait_stream(tside)
-        tr.critic(state, action, zs, zsa, qt, reward, not_done)
+        tr.critic(state, action, zs, zsa, qt, reward, not_done, phase=critic_phase)
         hook, self.after_critic = self.after_critic, None
         if hook is not None:  # the trainer's priority update, from |td| (VecTrainer._fork_update_sample)
             hook(tr.td)
@@ -1216,6 +1229,14 @@ class TD7Learner:
         if self.training_steps % self.hp.target_update_rate != 0:
             return False
         self.drop_prefetch()  # computed with the nets this refresh replaces
+        self.update_targets_device()
+        return True
+
+    def update_targets_device(self):
+        """The refresh's device work (:284-293): the target and fixed nets
+        copied, repacked, the Q bounds MAX-reduced over data-parallel ranks
+        and made the new target bounds -- no host synchronisation, so a
+        trainer can capture it into a graph (VecTrainer._refresh_targets)."""
         for dst, src in ((self.actor_target, self.actor), (self.critic_target, self.critic),
                          (self.fixed_encoder_target, self.fixed_encoder), (self.fixed_encoder, self.encoder)):
             with torch.no_grad():
@@ -1225,7 +1246,6 @@ class TD7Learner:
         self.sync_bounds()
         self.max_target.copy_(self.max)
         self.min_target.copy_(self.min)
-        return True
 
     @torch.no_grad()
     def act(self, state, use_checkpoint=False):

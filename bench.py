@@ -20,9 +20,9 @@ mode env: the env alone (random actions), for the sim-kernel roofline.
 
 Multi-GPU: one process per GPU (torchrun); envs shard with no exchange,
 TD7 gradients are all-reduced over RCCL (weak scaling).  On RCCL the trainer
-first runs 3,000 untimed settle iterations, then the W warm-up steps
-(`dist_settle_iterations` in the line; DESIGN.md 7: the first RCCL process on
-a fresh box runs its first few hundred iterations ~45 % slow).
+replays the iterations with the collectives captured in the graphs, the
+target refresh included (`dp_layout` and `dist_settle_iterations` -- 0 by
+default since r05 -- in the line).
 """
 import argparse
 import json
@@ -811,15 +811,17 @@ def main():
         return float(dt), n, its
 
     # RCCL settle (data parallel on RCCL only): untimed iterations of the same
-    # trainer BEFORE the W warm-up steps.  The first RCCL process on a fresh box
-    # ran its first few hundred in-graph iterations at 0.45-0.53 ms instead of
-    # 0.32-0.33 (5 of 6 boxes; later processes and later trainers in the same
-    # process fast); 2,000 iterations of activity end it, idling does not
-    # (profiles/r04rccl_raw); 3,000 for margin.  Reported as
-    # dist_settle_iterations.
+    # trainer BEFORE the W warm-up steps.  r04 ran 3,000 of them to hide the
+    # first RCCL process's slow mode; r05 found its cause -- the first eager
+    # all-reduce after the captured ones (the target refresh at training step
+    # 250) cost 96 ms of host time with the GPU idle, 31-35 ms in later
+    # processes -- and replays the refresh from a graph captured with the
+    # iteration graphs (VecTrainer._refresh_targets; DESIGN.md 7,
+    # profiles/r05rccl_raw), so the default is now 0.  Reported as
+    # dist_settle_iterations (EXO_DIST_SETTLE_ITERS sets it).
     settle = 0
     if dist_on and backend == "nccl" and trainer is not None:
-        settle = int(os.environ.get("EXO_DIST_SETTLE_ITERS", "3000"))
+        settle = int(os.environ.get("EXO_DIST_SETTLE_ITERS", "0"))
         for _ in range(settle):
             one_step(False)
     for _ in range(args.warmup):

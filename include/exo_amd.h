@@ -684,6 +684,18 @@ int td7f_critic(int32_t prec, const int32_t *act, const td7f_lin *critic, const 
                 float *run_max_dev, float *run_min_dev, int32_t B, int32_t state_dim, int32_t action_dim,
                 float *td_dev, float *q_dev, float *y1_dev, float *y2_dev, const td7f_xt *xt, int64_t ld,
                 void *stream);
+/* td7f_critic in two launches (the same results bit for bit): phase 1 the
+ * critic forward (it needs only the batch and the fixed embeddings, so the
+ * trainer runs it beside the target chain), storing Q, the pre-norm q0
+ * output and the row means into q_ws [2][Bp], h0_ws [2][Bp][hdim], mean_ws
+ * [2][Bp] (Bp = B rounded up to 16); phase 2 the loss from qt and the whole
+ * backward from that state.  phase 0 = td7f_critic (workspaces unused). */
+int td7f_critic_phase(int32_t phase, int32_t prec, const int32_t *act, const td7f_lin *critic, const float *s_dev,
+                      const float *a_dev, const float *zs_dev, const float *zsa_dev, const float *qt_dev,
+                      const float *reward_dev, const float *not_done_dev, float discount, const float *lo_dev,
+                      const float *hi_dev, float *run_max_dev, float *run_min_dev, int32_t B, int32_t state_dim,
+                      int32_t action_dim, float *td_dev, float *q_dev, float *y1_dev, float *y2_dev,
+                      const td7f_xt *xt, int64_t ld, float *q_ws, float *h0_ws, float *mean_ws, void *stream);
 /* Encoder update (TD7_multi_agent.py:219-228): zs(s') (no grad), zs(s),
  * zsa(zs, a), d mse / d pred and the dX chain of all six layers.  y: four
  * [B][enc_hdim] fp32 scratch buffers (zs1, zs2, zsa1, zsa2 activations).

@@ -169,11 +169,13 @@ def test_rccl_inline_layout_is_bit_identical_to_the_one_gpu_graph(monkeypatch):
     and actor buckets and the MAX of max_priority inside it.  At world 1 every
     collective is the identity, so the run must equal the one-GPU graph bit
     for bit -- weights, optimiser moments, replay trees -- and so must the
-    eager-collective three-graph layout (EXO_DP_CAPTURE=0)."""
+    eager-collective three-graph layout (EXO_DP_CAPTURE=0).  Targets refresh
+    every 5 steps: the in-graph layout replays the refresh (copies, repack,
+    MAX-reduced bounds and max_priority) from its own captured graph."""
     import torch.distributed as dist
     from exo_amd import VecExoskeletonEnv
     from exo_amd.rollout import VecTrainer
-    from exo_amd.td7 import Agent
+    from exo_amd.td7 import Agent, Hyperparameters
 
     def run(group, capture="1"):
         monkeypatch.setenv("EXO_FORCE_DIST", "1" if group is not None else "0")
@@ -181,7 +183,7 @@ def test_rccl_inline_layout_is_bit_identical_to_the_one_gpu_graph(monkeypatch):
         torch.manual_seed(11)
         env = VecExoskeletonEnv(512, seed=21)
         ag = Agent(80, 7, 1, env_num=8, precision="bf16", n_envs=512, process_group=group, graph_safe=True,
-                   buffer_size=8192)
+                   buffer_size=8192, hp=Hyperparameters(target_update_rate=5))
         tr = VecTrainer(env, ag)
         for _ in range(14):
             tr.step()
@@ -202,6 +204,7 @@ def test_rccl_inline_layout_is_bit_identical_to_the_one_gpu_graph(monkeypatch):
             assert tr.dp and tr.dp_inline is inline
             if inline:
                 assert all(len(parts) == 1 for parts in tr.graphs.values())
+                assert tr._refresh_graph is not None
             for i, (x, y) in enumerate(zip(ref, st)):
                 torch.testing.assert_close(y, x, rtol=0, atol=0, msg=f"tensor {i} (capture={capture})")
     finally:

@@ -186,3 +186,36 @@ def test_fp32_select_in_capped_launches_equals_one_launch(monkeypatch):
     torch.testing.assert_close(outs[1], outs[0], rtol=0, atol=0)
     assert torch.equal(states[0], states[1]) and not torch.equal(states[0], st0)
     assert sigmas[0] == sigmas[1] < sig0
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+def test_critic_split_launches_equal_one_launch(monkeypatch, precision):
+    """td7f_critic_phase (r05): the critic pass as a forward launch beside the
+    target chain and a loss + backward launch after it (EXO_CRITIC_SPLIT) --
+    the graph-replayed training loop with it and without it: every weight,
+    optimiser moment, replay priority and Q bound bit for bit."""
+    from exo_amd import VecExoskeletonEnv, fused, td7
+    from exo_amd.rollout import VecTrainer
+    from exo_amd.td7 import Agent
+    out = []
+    for split in (False, True):
+        monkeypatch.setattr(td7, "CRITIC_SPLIT", split)
+        torch.manual_seed(7)
+        env = VecExoskeletonEnv(256, seed=7)
+        f0 = fused.FUSED_F32
+        fused.FUSED_F32 = True
+        try:
+            ag = Agent(80, 7, 1, env_num=8, precision=precision, n_envs=256, buffer_size=8192, graph_safe=True)
+        finally:
+            fused.FUSED_F32 = f0
+        tr = VecTrainer(env, ag)
+        for _ in range(10):
+            tr.step()
+        torch.cuda.synchronize()
+        L = ag.learner
+        st = [p.detach().clone() for m in (L.actor, L.critic, L.encoder) for p in m.parameters()]
+        st += [getattr(L, o).m.clone() for o in ("actor_optimizer", "critic_optimizer", "encoder_optimizer")]
+        st += [ag.replay_buffer._tree.clone(), L.max.clone(), L.min.clone()]
+        out.append(st)
+    for i, (a, b) in enumerate(zip(*out)):
+        torch.testing.assert_close(b, a, rtol=0, atol=0, msg=f"tensor {i}")

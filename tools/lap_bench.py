@@ -61,7 +61,18 @@ def main():
 
     def smp():
         rb.sample(1)
-    for name, f in (("update + sample (one launch)", upd_sample), ("update alone", upd), ("sample + gather", smp)):
+    # the reference schedule's per-step insert (shared pointer) with the mask advance, on a second buffer
+    rb2 = LAP(80, 7, dev, 8, 250_000, 128)
+    table = torch.ones((345, n), dtype=torch.bool, device=dev)
+    k = torch.zeros((1,), dtype=torch.int64, device=dev)
+    active = torch.ones(n, dtype=torch.bool, device=dev)
+    count = torch.zeros((1,), dtype=torch.int32, device=dev)
+    score = torch.zeros(n, dtype=torch.float64, device=dev)
+
+    def ref_insert():
+        rb2.add_batch_ref(obs, act, obs, rew, done, strata, active, advance=(table, k, count, score))
+    for name, f in (("update + sample (one launch)", upd_sample), ("update alone", upd), ("sample + gather", smp),
+                    ("ref insert + mask advance", ref_insert)):
         print(f"{name:32s} {timed(f):8.2f} us", flush=True)
 
 
