@@ -957,6 +957,177 @@ __global__ __launch_bounds__(256) void lap_sample_gather_kernel(const float *tre
 #endif
 constexpr int TOPN_US = LAP_TOPN_US;
 
+// ---------------------------------------------------------------- planned reference inserts
+// The reference schedule's rollout inserts (lap_store_batch_ref_fused_adv per
+// step: 18.5 us of its ~80 us per 4,096-env step, r05 lap_bench) planned for
+// a whole episode round at its start (r05).  Which envs run at each step of
+// a synchronous round is fixed by the motion lengths (the trainer's mask
+// table), so the shared pointer's slot of every add of the round -- and
+// which adds a later same-slot add of the same stratum overwrites -- follow
+// from the pointer at the round start alone: lap_ref_plan writes
+// plan[k][e] = the slot env e's step-k transition lands in (-1: inactive or
+// overwritten).  A step is then one elementwise launch (lap_ref_step: the
+// row copies, the scores, the next mask) with no scan, ticket or tree work,
+// and lap_ref_commit writes the round's leaves (max_priority: constant over a
+// rollout, nothing trains during it), recomputes the round's ring span once
+// and advances the pointer and sizes.  The same rows, leaves, sums, pointer
+// and sizes as the per-step inserts: a slot written twice in a round is
+// written by the later add either way, an ancestor's last recomputation sees
+// its children's final values either way.
+
+// pass 1: rank of every active env within its step (block scan per step row),
+// add index c = offs[k] + rank, stratum_of_add[c]; plan[k][e] = c or -1
+__global__ __launch_bounds__(UPD_THREADS) void lap_ref_plan_scan_kernel(const uint8_t *table, int n,
+                                                                        const int32_t *strata, int E,
+                                                                        const long long *offs, int32_t *add_s,
+                                                                        int32_t *plan) {
+    const int k = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    __shared__ int wsum[UPD_THREADS / 64];
+    __shared__ int chunk_total;
+    const uint8_t *A = table + (size_t)k * n;
+    int32_t *P = plan + (size_t)k * n;
+    long long offset = offs[k];
+    for (int base = 0; base < n; base += STORE_CHUNK) {
+        int f[4], sk[4], cnt = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int i = base + 4 * t + j;
+            sk[j] = i < n ? strata[i] : -1;
+            f[j] = (i < n && sk[j] >= 0 && sk[j] < E && A[i]) ? 1 : 0;
+            cnt += f[j];
+        }
+        int incl = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += v;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        if (t == 0) {
+            int acc = 0;
+            for (int q = 0; q < UPD_THREADS / 64; ++q) {
+                const int v = wsum[q];
+                wsum[q] = acc;
+                acc += v;
+            }
+            chunk_total = acc;
+        }
+        __syncthreads();
+        long long c = offset + wsum[wv] + incl - cnt;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int i = base + 4 * t + j;
+            if (i >= n) continue;
+            if (f[j]) {
+                add_s[c] = sk[j];
+                P[i] = (int32_t)c;
+                ++c;
+            } else {
+                P[i] = -1;
+            }
+        }
+        offset += chunk_total;
+        __syncthreads();
+    }
+}
+
+// pass 2: add c -> its slot, or -1 when a later add of its slot group (the
+// adds sharing ceil((count0 + c) / E)) has the same stratum
+__global__ __launch_bounds__(256) void lap_ref_plan_slots_kernel(int32_t *plan, long long entries,
+                                                                 const int32_t *add_s, long long total,
+                                                                 const long long *ref, int E, int capacity) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= entries) return;
+    const int c = plan[i];
+    if (c < 0) return;
+    const long long ptr0 = ref[0], count0 = ref[1];
+    const long long m0 = mult_below(count0, E), mr = mult_below(count0 + c, E);
+    const long long qend = min(mr * E - count0, total - 1);
+    const int s = add_s[c];
+    bool win = true;
+    for (long long q = c + 1; q <= qend; ++q) win &= add_s[q] != s;
+    long long v = ptr0 + (mr - m0);
+    if (v >= capacity) v -= capacity;
+    if (v >= capacity) v %= capacity;
+    plan[i] = win ? (int32_t)v : -1;
+}
+
+// one step of the planned round: env e's transition to its slot, the episode
+// score (:144) and the next mask -- one wavefront per env, 4 per workgroup.
+// The step index lives in kk[par] (the trainers' observation parity); the
+// launch writes k + 1 to kk[par ^ 1] (and *k_dev), so no workgroup reads a
+// counter another one advances.
+__global__ __launch_bounds__(256) void lap_ref_step_kernel(lap_storage_desc st, const int32_t *plan, int rows, int n,
+                                                           long long *kk, int par, long long *k_dev,
+                                                           const int32_t *strata, int capacity, const float *state,
+                                                           const float *action, const float *next_state,
+                                                           const float *reward, const uint8_t *done,
+                                                           float action_scale, const uint8_t *table,
+                                                           uint8_t *active, int32_t *count,
+                                                           const int32_t *counts_table, double *score) {
+    const long long k = kk[par];
+    const long long k1 = k + 1 < rows ? k + 1 : rows - 1;
+    const int e = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        kk[par ^ 1] = k1;
+        if (k_dev) *k_dev = k1;
+        if (count) *count = counts_table[k1];
+    }
+    if (e >= n) return;
+    const int slot = k < rows ? plan[(size_t)k * n + e] : -1;
+    if (slot >= 0) {
+        const long r = (long)strata[e] * (capacity + 1) + slot;
+        const int sd = st.state_dim, ad = st.action_dim;
+        for (int q = lane; q < sd; q += 64) {
+            st.state[r * sd + q] = state[(long)e * sd + q];
+            st.next_state[r * sd + q] = next_state[(long)e * sd + q];
+        }
+        for (int q = lane; q < ad; q += 64) st.action[r * ad + q] = action[(long)e * ad + q] / action_scale;
+        if (lane == 0) {
+            st.reward[r] = reward[e];
+            st.not_done[r] = 1.0f - (done[e] ? 1.0f : 0.0f);
+        }
+    }
+    if (lane == 0) {
+        if (score) score[e] += active[e] ? (double)reward[e] : 0.0;
+        active[e] = table[(size_t)k1 * n + e];
+    }
+}
+
+// the round's leaves (max_priority) at every planned slot
+__global__ __launch_bounds__(256) void lap_ref_commit_leaves_kernel(const int32_t *plan, long long entries, int n,
+                                                                    const int32_t *strata, float *tree, int cap,
+                                                                    const float *maxp) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= entries) return;
+    const int slot = plan[i];
+    if (slot < 0) return;
+    stratum_tree(tree, strata[i % n], cap)[cap + slot] = *maxp;
+}
+
+// the round's ring span recomputed per stratum (one workgroup each)
+__global__ __launch_bounds__(UPD_THREADS) void lap_ref_commit_tree_kernel(float *tree, int cap, int levels,
+                                                                          int capacity, const long long *ref,
+                                                                          long long total, int E) {
+    const long long ptr0 = ref[0], count0 = ref[1];
+    const long long adv = mult_below(count0 + total, E) - mult_below(count0, E);
+    if (adv <= 0) return;
+    propagate_span(stratum_tree(tree, blockIdx.x, cap), cap, levels, capacity, (int)ptr0,
+                   (int)min(adv, (long long)capacity));
+}
+
+// the pointer and sizes after the round
+__global__ void lap_ref_commit_ref_kernel(long long *ref, long long total, int E, int capacity, int32_t *ring_size) {
+    const long long ptr0 = ref[0], count0 = ref[1], size0 = ref[2];
+    const long long adv = mult_below(count0 + total, E) - mult_below(count0, E);
+    const long long size = min(size0 + adv, (long long)capacity);
+    for (int s = 0; s < E; ++s) ring_size[s] = (int32_t)size;
+    ref[0] = (ptr0 + adv) % capacity;
+    ref[1] = count0 + total;
+    ref[2] = size;
+}
+
 // The sampled rows gathered by their own launch (r05): lap_update_sample's
 // stratum workgroups stop at the indices, and DRAWS draws per 256-thread
 // workgroup here copy state, next_state (float4 where aligned), action,
@@ -1424,6 +1595,56 @@ int lap_sample_gather_rng(const lap_tree_desc *t, const lap_storage_desc *st, ui
     hipLaunchKernelGGL(lap_sample_gather_kernel, dim3((total + 3) / 4), dim3(256), 0, (hipStream_t)stream, t->tree,
                        t->cap, levels_of(t), t->capacity, nullptr, st->size, batch, total, idx, *st, out_state,
                        out_action, out_next_state, out_reward, out_not_done, SampleRng{seed, tag, counter, ticket});
+    return rc(hipGetLastError());
+}
+
+
+// ---------------------------------------------------------------- planned reference inserts (C ABI)
+int lap_ref_plan(const lap_tree_desc *t, const int64_t *ref_dev, const uint8_t *table_dev, int32_t rows, int32_t n,
+                 const int32_t *strata_dev, const int64_t *offs_dev, int64_t total, int32_t *add_ws_dev,
+                 int32_t *plan_dev, void *stream) {
+    if (!valid(t) || !ref_dev || !table_dev || rows <= 0 || n <= 0 || !strata_dev || !offs_dev || total < 0 ||
+        (total > 0 && !add_ws_dev) || !plan_dev)
+        return EXO_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(lap_ref_plan_scan_kernel, dim3(rows), dim3(UPD_THREADS), 0, s, table_dev, n, strata_dev,
+                       t->n_strata, (const long long *)offs_dev, add_ws_dev, plan_dev);
+    if (hipGetLastError() != hipSuccess) return EXO_EDEVICE;
+    const long long entries = (long long)rows * n;
+    hipLaunchKernelGGL(lap_ref_plan_slots_kernel, dim3((unsigned)((entries + 255) / 256)), dim3(256), 0, s, plan_dev,
+                       entries, add_ws_dev, (long long)total, (const long long *)ref_dev, t->n_strata, t->capacity);
+    return rc(hipGetLastError());
+}
+
+int lap_ref_step(const lap_tree_desc *t, const lap_storage_desc *st, const int32_t *plan_dev, int32_t rows,
+                 int32_t n, int64_t *kk_dev, int32_t par, int64_t *k_dev, const int32_t *strata_dev,
+                 const float *state, const float *action, const float *next_state, const float *reward,
+                 const uint8_t *done, float action_scale, const uint8_t *table_dev, uint8_t *active_dev,
+                 int32_t *count_dev, const int32_t *counts_table_dev, double *score_dev, void *stream) {
+    if (!valid(t) || !st || !st->state || !st->action || !st->next_state || !st->reward || !st->not_done ||
+        !plan_dev || rows <= 0 || n <= 0 || !kk_dev || (par != 0 && par != 1) || !strata_dev || !state || !action ||
+        !next_state || !reward || !done || action_scale == 0.0f || !table_dev || !active_dev ||
+        (count_dev && !counts_table_dev))
+        return EXO_EINVAL;
+    hipLaunchKernelGGL(lap_ref_step_kernel, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, *st, plan_dev,
+                       rows, n, (long long *)kk_dev, par, (long long *)k_dev, strata_dev, t->capacity, state, action,
+                       next_state, reward, done, action_scale, table_dev, active_dev, count_dev, counts_table_dev,
+                       score_dev);
+    return rc(hipGetLastError());
+}
+
+int lap_ref_commit(const lap_tree_desc *t, const lap_storage_desc *st, int64_t *ref_dev, const int32_t *plan_dev,
+                   int32_t rows, int32_t n, const int32_t *strata_dev, int64_t total, void *stream) {
+    if (!valid(t) || !st || !st->size || !ref_dev || !plan_dev || rows <= 0 || n <= 0 || !strata_dev || total < 0)
+        return EXO_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    const long long entries = (long long)rows * n;
+    hipLaunchKernelGGL(lap_ref_commit_leaves_kernel, dim3((unsigned)((entries + 255) / 256)), dim3(256), 0, s,
+                       plan_dev, entries, n, strata_dev, t->tree, t->cap, t->max_priority);
+    hipLaunchKernelGGL(lap_ref_commit_tree_kernel, dim3(t->n_strata), dim3(UPD_THREADS), 0, s, t->tree, t->cap,
+                       levels_of(t), t->capacity, (const long long *)ref_dev, (long long)total, t->n_strata);
+    hipLaunchKernelGGL(lap_ref_commit_ref_kernel, dim3(1), dim3(1), 0, s, (long long *)ref_dev, (long long)total,
+                       t->n_strata, t->capacity, st->size);
     return rc(hipGetLastError());
 }
 

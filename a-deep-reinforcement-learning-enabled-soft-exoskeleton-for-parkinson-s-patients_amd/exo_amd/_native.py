@@ -147,6 +147,12 @@ EXPORTS = {
                                             c_void_p]),
     "lap_store_batch_ref_fused_adv": (c_int32, [c_void_p] * 10 + [ctypes.c_float, c_int32, c_void_p, c_void_p,
                                                                  c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "lap_ref_plan": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p, ctypes.c_int64,
+                               c_void_p, c_void_p, c_void_p]),
+    "lap_ref_step": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_int32, c_void_p, c_void_p]
+                     + [c_void_p] * 5 + [ctypes.c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "lap_ref_commit": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, ctypes.c_int64,
+                                 c_void_p]),
     "lap_update_sample_rng": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, ctypes.c_uint64,
                                         ctypes.c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_void_p, c_void_p, c_void_p]),

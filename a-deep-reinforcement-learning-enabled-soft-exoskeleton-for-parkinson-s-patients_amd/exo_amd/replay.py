@@ -202,6 +202,47 @@ class LAP:
                                          float(self.normalize_actions), n, nat.ptr(self._ref_ws),
                                          self._stream()), fn)
 
+    # ----------------------------------------------- planned reference inserts
+    # (lap_ref_plan / lap_ref_step / lap_ref_commit, csrc/lap.hip): a whole
+    # synchronous episode round of add_batch_ref calls planned at its start --
+    # the steps' envs come from a fixed mask table -- so a step is one
+    # elementwise launch and the tree is updated once, at ref_commit.  Bit
+    # for bit the per-step inserts' rows, leaves, sums, pointer and sizes,
+    # provided nothing reads the tree between ref_plan and ref_commit.
+    def ref_plan(self, table, strata, offs, total, plan):
+        """plan[k][e] (int32 [rows][n]) for the mask table rows (uint8/bool
+        [rows][n]); offs: int64 device [rows], the adds before each row."""
+        rows, n = table.shape
+        if getattr(self, "_ref_add_ws", None) is None or self._ref_add_ws.numel() < max(int(total), 1):
+            self._ref_add_ws = torch.empty((max(int(total), 1),), dtype=torch.int32, device=self.device)
+        tb = table.view(torch.uint8) if table.dtype == torch.bool else table
+        sr = (strata if strata.dtype == torch.int32 else strata.to(torch.int32)).contiguous()
+        nat.check(nat.lib().lap_ref_plan(ctypes.byref(self._desc), nat.ptr(self.ref_state), nat.ptr(tb), rows, n,
+                                         nat.ptr(sr), nat.ptr(offs), int(total), nat.ptr(self._ref_add_ws),
+                                         nat.ptr(plan), self._stream()), "lap_ref_plan")
+
+    def ref_step(self, plan, table, kk, par, state, action, next_state, reward, done, strata, active,
+                 k_dev=None, count=None, counts_table=None, score=None):
+        """One step of a planned round (see ref_plan): the transitions to their
+        planned slots, score += reward where active, the next mask in place."""
+        rows, n = plan.shape
+        tb = table.view(torch.uint8) if table.dtype == torch.bool else table
+        dn = done.view(torch.uint8) if done.dtype == torch.bool else done.to(torch.uint8)
+        act = active.view(torch.uint8) if active.dtype == torch.bool else active
+        nat.check(nat.lib().lap_ref_step(
+            ctypes.byref(self._desc), ctypes.byref(self._store), nat.ptr(plan), rows, n, nat.ptr(kk), int(par),
+            nat.ptr(k_dev), nat.ptr(strata), nat.ptr(state.contiguous()), nat.ptr(action.contiguous()),
+            nat.ptr(next_state.contiguous()), nat.ptr(reward.contiguous()), nat.ptr(dn.contiguous()),
+            float(self.normalize_actions), nat.ptr(tb), nat.ptr(act), nat.ptr(count), nat.ptr(counts_table),
+            nat.ptr(score), self._stream()), "lap_ref_step")
+
+    def ref_commit(self, plan, strata, total):
+        """The end of a planned round: leaves, the round's span, the pointer."""
+        rows, n = plan.shape
+        nat.check(nat.lib().lap_ref_commit(ctypes.byref(self._desc), ctypes.byref(self._store),
+                                           nat.ptr(self.ref_state), nat.ptr(plan), rows, n, nat.ptr(strata),
+                                           int(total), self._stream()), "lap_ref_commit")
+
     def ref_pointer(self):
         """(ptr, count, size) of add_batch_ref (host sync)."""
         return tuple(int(v) for v in self.ref_state.cpu())

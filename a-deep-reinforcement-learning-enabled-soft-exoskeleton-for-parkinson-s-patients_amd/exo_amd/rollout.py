@@ -952,8 +952,31 @@ class RefScheduleTrainer(VecTrainer):
         self.save_prefix = save_prefix
         self.saves = 0
         self.save_seconds = 0.0
+        # r05: the round's inserts planned at its start (LAP.ref_plan: the
+        # steps' envs come from the mask table, so every add's slot follows
+        # from the pointer at the round start), one elementwise launch per
+        # step (LAP.ref_step: rows, scores, next mask) and the tree updated
+        # once at the end (LAP.ref_commit) -- bit for bit the per-step fused
+        # inserts (the branch-overlapped round graph, EXO_REF_ROUND_GRAPH=1,
+        # keeps those).  EXO_REF_PLANNED=0: the per-step inserts.
+        self.planned = os.environ.get("EXO_REF_PLANNED", "1") == "1" and ref_replay
+        if self.planned:
+            rows = self._table_ext.shape[0]
+            counts = self._table_ext.sum(1).to(torch.int64)
+            self._offs = torch.cumsum(counts, 0) - counts           # adds before each row
+            self._plan_total = int(counts.sum())
+            self._counts_tab = counts.to(torch.int32)
+            self._plan = torch.full((rows, self.n), -1, dtype=torch.int32, device=dev)
+            self._kk = torch.zeros((2,), dtype=torch.int64, device=dev)
 
     # ------------------------------------------------------------ rollout
+    def _use_plan(self):
+        """The planned inserts (ref_plan / ref_step / ref_commit) this round:
+        the reference pointer with the score in the insert launch, not the
+        branch-overlapped round graph."""
+        return (self.planned and self.ref_replay and self.fused_score and self.active.dtype == torch.bool
+                and not (self.round_graph and self.round_overlap))
+
     def _seen_eager(self, random):
         """A round graph is captured only after a per-step round of the same
         kind (random / policy) allocated its buffers."""
@@ -1040,6 +1063,12 @@ class RefScheduleTrainer(VecTrainer):
             self.score.add_(rew.where(self.active, 0.0))  # :144 (float32 into the float64 score, 2 launches)
         add = ag.replay_buffer.add_batch_ref if self.ref_replay else ag.replay_buffer.add_batch
         rb = ag.replay_buffer
+        if self._use_plan():  # the round's planned slots; score, next mask and count in the same launch
+            rb.ref_step(self._plan, self._table_ext, self._kk, self._cur, obs, act, nobs, rew, done, self.strata,
+                        self.active, k_dev=self.k_dev, count=self.active_count, counts_table=self._counts_tab,
+                        score=self.score)
+            self.last_actions = act
+            return
         if (self.insert_advance and self.fused_score and self.ref_replay and not overlap and rb.ref_insert_fused
                 and self.active.dtype == torch.bool):
             # the insert's last workgroup out advances the mask and adds the
@@ -1170,6 +1199,10 @@ class RefScheduleTrainer(VecTrainer):
         self._round_start()
         if self.stats:
             self._stats_buffers()[2].zero_()  # the round's counters (:117-121)
+        plan = self._use_plan()
+        if plan:
+            self._kk.zero_()
+            ag.replay_buffer.ref_plan(self._table_ext, self.strata, self._offs, self._plan_total, self._plan)
         random = not self.allow_train
         if (self.round_graph and self.use_graphs and self.action_source is None
                 and self._roll_iters >= max(self.warmup_eager, 1) and self._seen_eager(random)):
@@ -1178,6 +1211,8 @@ class RefScheduleTrainer(VecTrainer):
             for _ in range(self.round_len):
                 self._roll_step(random)
                 self._eager_kinds.add((bool(random), self.stats))
+        if plan:
+            ag.replay_buffer.ref_commit(self._plan, self.strata, self._plan_total)
         self.resets += 1
         # :208 -- the host sees one value per round: the mean episode return
         ep_return = float(np.mean(self.score.cpu().numpy()))

@@ -370,6 +370,38 @@ int lap_store_batch_ref_fused_adv(const lap_tree_desc *t, const lap_storage_desc
                                   float action_scale, int32_t n, uint32_t *ticket_dev, const uint8_t *table,
                                   int32_t rows, int64_t *k_dev, int32_t *count_dev, double *score_dev, void *stream);
 
+/* The reference-schedule rollout's inserts planned per episode round (r05;
+ * the same rows, leaves, sums, pointer and sizes as calling
+ * lap_store_batch_ref_fused_adv at every step, bit for bit, provided the tree
+ * is not read before lap_ref_commit -- the rollout trains nothing):
+ * lap_ref_plan: for the mask table rows [0, rows) of the round (uint8
+ * [rows][n], table_dev, the envs running at each step) and offs_dev (int64
+ * [rows]: the adds before each step, i.e. the exclusive prefix sums of the
+ * rows' active counts; total = all the round's adds), plan_dev[k][e] = the
+ * slot env e's step-k add writes, -1 when it is inactive or a later add of
+ * its slot group has its stratum (overwritten).  add_ws_dev: total int32.
+ * ref_dev is read (the pointer at the round start), not changed. */
+int lap_ref_plan(const lap_tree_desc *t, const int64_t *ref_dev, const uint8_t *table_dev, int32_t rows, int32_t n,
+                 const int32_t *strata_dev, const int64_t *offs_dev, int64_t total, int32_t *add_ws_dev,
+                 int32_t *plan_dev, void *stream);
+/* One rollout step of a planned round: every env with plan[k][e] >= 0 stores
+ * its transition there (action / action_scale, not_done = 1 - done); then
+ * score_dev[e] += reward where active[e] (optional), active = table row k + 1
+ * (saturating at rows - 1), *count_dev = counts_table_dev[k + 1] (optional).
+ * k = kk_dev[par]; the launch writes k + 1 into kk_dev[par ^ 1] and *k_dev
+ * (optional), so consecutive steps alternate par. */
+int lap_ref_step(const lap_tree_desc *t, const lap_storage_desc *st, const int32_t *plan_dev, int32_t rows,
+                 int32_t n, int64_t *kk_dev, int32_t par, int64_t *k_dev, const int32_t *strata_dev,
+                 const float *state, const float *action, const float *next_state, const float *reward,
+                 const uint8_t *done, float action_scale, const uint8_t *table_dev, uint8_t *active_dev,
+                 int32_t *count_dev, const int32_t *counts_table_dev, double *score_dev, void *stream);
+/* The end of a planned round: the leaves of every planned slot set to
+ * max_priority, the round's ring span recomputed in every stratum, the shared
+ * pointer {ptr, count, size} advanced by the round's `total` adds and every
+ * stratum's sampling size set. */
+int lap_ref_commit(const lap_tree_desc *t, const lap_storage_desc *st, int64_t *ref_dev, const int32_t *plan_dev,
+                   int32_t rows, int32_t n, const int32_t *strata_dev, int64_t total, void *stream);
+
 /* LAP.sample (:65-111): batch draws per stratum (u_dev [n_strata][batch]),
  * indices -> idx_dev [n_strata][batch], the sampled rows gathered into
  * out_* [n_strata * batch][dim] (stratum-major). */

@@ -230,13 +230,18 @@ def test_round_graph_rollout_matches_per_step_rollout():
             scores.append(tr.score.clone())
         torch.cuda.synchronize()
         rb = agent.replay_buffer
-        # (_u: the host-RNG sampling scratch, unused and uninitialised with the device RNG)
-        st = {k: v.detach().clone() for k, v in rb.__dict__.items() if isinstance(v, torch.Tensor) and k != "_u"}
+        # (_u: the host-RNG sampling scratch, unused and uninitialised with the
+        # device RNG; _ref_ws / _ref_add_ws: the per-step and the planned
+        # inserts' scratch -- the branch-overlapped round graph (rg True) keeps
+        # the per-step inserts, the others plan the round, r05)
+        st = {k: v.detach().clone() for k, v in rb.__dict__.items()
+              if isinstance(v, torch.Tensor) and k not in ("_u", "_ref_ws", "_ref_add_ws")}
         w = [p.detach().clone() for m in (agent.learner.actor, agent.learner.critic, agent.learner.encoder)
              for p in m.parameters()]
         obs = tr.obs.clone()
         outs.append((st, w, scores, obs, [t["training_steps"] for t in tr.trace]))
         assert [t["random_actions"] for t in tr.trace] == [True] * 3 + [False] * 3
+        assert tr._use_plan() == (rg is not True)
         if rg:
             assert {k[:2] for k in tr._round_graphs} == {("round", True), ("round", False)}
     a = outs[0]
