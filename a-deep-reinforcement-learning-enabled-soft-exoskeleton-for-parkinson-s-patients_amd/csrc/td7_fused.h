@@ -920,9 +920,16 @@ inline int th_of(const td7f_lin *ls, int n) {
 
 constexpr int LDS_MAX = 160 * 1024;
 
+// Plan-only mode (td7f_probe, per host thread): launch() checks a pass's LDS
+// plan and returns without launching, so the host can test a network shape
+// once when it builds the fused passes (exo_amd.fused.FusedNets) instead of
+// failing at the first call of a pass whose images do not fit.
+extern thread_local bool td7f_probe_mode;
+
 template <typename K, typename A>
 int launch(K kernel, dim3 grid, int lds, A args, hipStream_t st) {
     if (lds > LDS_MAX) return EXO_EINVAL;
+    if (td7f_probe_mode) return EXO_OK;
     if (hipFuncSetAttribute((const void *)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
         return EXO_EDEVICE;
     hipLaunchKernelGGL(kernel, grid, dim3(NTH), lds, st, args);

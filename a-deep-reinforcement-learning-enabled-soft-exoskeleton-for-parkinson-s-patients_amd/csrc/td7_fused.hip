@@ -535,6 +535,7 @@ __global__ __launch_bounds__(NTH) void fixed_kernel(FixedArgs a) {
 }
 
 // ---------------------------------------------------------------- host side
+thread_local bool td7f_probe_mode = false;
 }  // namespace td7f
 
 using namespace td7f;
@@ -640,6 +641,11 @@ int td7f_adam_pack(int32_t prec, int32_t nopt, float *const *p, float *const *m,
     else
         hipLaunchKernelGGL(adam_pack_kernel<PREC_F32>, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
+}
+
+int td7f_probe(int32_t on) {
+    td7f::td7f_probe_mode = on != 0;
+    return EXO_OK;
 }
 
 int td7f_select(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7f_lin *actor, const float *obs,
@@ -768,22 +774,28 @@ int td7f_target(int32_t prec, const int32_t *act, const td7f_lin *tenc, const td
     const int rows = TR;
     int hmax = 0;
     for (int i = 0; i < 18; ++i) hmax = std::max(hmax, all[i].n_out);
-    Bump ba(1);
-    a.X = ba.r16(rows, ld16(a.S + a.A, kd));
-    a.H1 = ba.r16(rows, ld16(hmax, kd));
-    a.H2 = ba.r16(rows, ld16(hmax, kd));
-    a.CATA = ba.r16(rows, ld16(a.Ha + a.Z, kd));
-    a.CATZ = ba.r16(rows, ld16(a.Z + a.A, kd));
     const int old = eh * round_up(2 * a.Z + a.A, 8);  // == the image row (16-byte stores)
     const int fld = std::max(hmax, 16);
+    // fp32 with an OUT row wider than CATA's (zs_dim well above actor_hdim):
+    // X and CATA side by side, OUT over both (below)
+    const bool wide_out = prec == PREC_F32 && old > ld16(a.Ha + a.Z, kd);
+    Bump ba(1);
+    a.X = ba.r16(rows, ld16(a.S + a.A, kd));
+    if (wide_out) a.CATA = ba.r16(rows, ld16(a.Ha + a.Z, kd));
+    a.H1 = ba.r16(rows, ld16(hmax, kd));
+    a.H2 = ba.r16(rows, ld16(hmax, kd));
+    if (!wide_out) a.CATA = ba.r16(rows, ld16(a.Ha + a.Z, kd));
+    a.CATZ = ba.r16(rows, ld16(a.Z + a.A, kd));
     if (prec == PREC_F32) {
         // fp32 images: OUT overlays CATA (dead once actor_target's l1 has read
-        // it; OUT is first written by the noise after l3) and F overlays
-        // H1 | H2 (dead whenever F is written; the thin l3 writes F's first
-        // columns only, inside H1, while it reads H2); a region the overlay
-        // does not fit (zs_dim well above actor_hdim, or a narrow hidden
-        // width) gets its own bytes instead, as in the 16-bit images
-        a.OUT = old <= a.CATA.ld ? R16{a.CATA.off, old} : ba.r16(rows, old);
+        // it; OUT is first written by the noise after l3) -- or, wider than
+        // CATA's rows, X | CATA (X is dead after actor_target's l0, before
+        // l1) -- and F overlays H1 | H2 (dead whenever F is written; the thin
+        // l3 writes F's first columns only, inside H1, while it reads H2); a
+        // region no overlay fits gets its own bytes, as in the 16-bit images
+        if (!wide_out) a.OUT = R16{a.CATA.off, old};
+        else if (rows * old * 2 <= a.CATA.off + rows * a.CATA.ld * 2 - a.X.off) a.OUT = R16{a.X.off, old};
+        else a.OUT = ba.r16(rows, old);
         a.F = rows * fld * 4 <= a.H2.off + rows * a.H2.ld * 2 - a.H1.off ? R32{a.H1.off, fld} : ba.r32(rows, fld);
     } else {
         a.OUT = ba.r16(rows, old);

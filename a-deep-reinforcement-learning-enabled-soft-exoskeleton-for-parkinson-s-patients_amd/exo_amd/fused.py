@@ -150,6 +150,10 @@ def supported(learner):
     return all(49 <= w <= 320 and w % 4 == 0 for w in widths) and len(th) == 1 and th <= {4, 5}
 
 
+class PlanError(RuntimeError):
+    """A network shape the fused passes' shared-memory plan cannot hold."""
+
+
 class FusedNets:
     """Packed copies of every TD7 net plus the fused launches of one learner."""
 
@@ -162,6 +166,54 @@ class FusedNets:
         self.act = (ctypes.c_int32 * 3)(ops.act_code(hp.enc_activ), ops.act_code(hp.actor_activ),
                                         ops.act_code(hp.critic_activ))
         self._build()
+        self.probe()
+
+    @torch.no_grad()
+    def probe(self):
+        """Every fused pass once in plan-only mode (td7f_probe: arguments and
+        the LDS plan checked, nothing launched) at the row counts whose plans
+        differ (select's 16- and 32-row tiles), when the learner builds its
+        passes instead of at the first call of a pass that cannot run (ADVICE
+        r4: fp32 with zs_dim well above actor_hdim).  An inference pass
+        (select_action, the target heads, the fixed embeddings) that does not
+        fit raises PlanError: the learner keeps the per-layer kernels.  A
+        gradient pass that does not (the actor passes need hidden widths in
+        multiples of 16: the Pink agent's 300-wide actor) leaves train_ok
+        False: fused inference, per-layer update (TD7Learner.fused_train)."""
+        L, dev = self.L, self.dev
+        S, A = L.actor.l0.in_features, L.actor.l3.out_features
+        B = 16
+        # FusedTrain points the parameters' .grad at its own buffers: restored after
+        params = [p for m in (L.encoder, L.critic, L.actor) for p in m.parameters()]
+        grads = [p.grad for p in params]
+        f32 = dict(dtype=torch.float32, device=dev)
+        lib = nat.lib()
+        lib.td7f_probe(1)
+        self.train_ok = False
+        try:
+            s, a = torch.zeros((B, S), **f32), torch.zeros((B, A), **f32)
+            try:
+                for n in (B, 8200):
+                    self.select(torch.zeros((n, S), **f32))
+                self.target_heads(s, noise=torch.zeros((B, A), **f32))
+                zs, zsa = self.fixed(s, a)
+            except RuntimeError as e:
+                raise PlanError(f"fused TD7 passes: {e}") from e
+            try:
+                t = FusedTrain(self, B)
+                one = torch.zeros((B, 1), **f32)
+                t.encoder(s, a, s)
+                for ph in (0, 1, 2):
+                    t.critic(s, a, zs, zsa, torch.zeros((B, 2), **f32), one, one, phase=ph)
+                for ph in (0, 1, 2):
+                    t.actor(ph, s, zs)
+                self.train_ok = True
+            except RuntimeError as e:  # inference fused, the update per layer
+                self.train_error = str(e)
+        finally:
+            lib.td7f_probe(0)
+            for p, g in zip(params, grads):
+                p.grad = g
 
     def _build(self):
         L, p = self.L, self.prec

@@ -391,7 +391,7 @@ class VecTrainer:
 
     def _target_prefetch_flags(self):
         L = self.agent.learner
-        ok = (self.prefetch_targets and self._prefetching() and L.fused is not None and self.iters > 0
+        ok = (self.prefetch_targets and self._prefetching() and L.fused_train and self.iters > 0
               and (not self.dp or self.dp_inline))
         pre_in = ok and L.prefetch_ready(self._cur)
         pre_out = ok and L.training_steps % L.hp.target_update_rate != 0
@@ -477,7 +477,7 @@ class VecTrainer:
         L = self.agent.learner
         rb = self.agent.replay_buffer
         return (self.us_after_critic and not self.dp and self._prefetching() and not self._pre_out
-                and L.fused is not None and rb.device_rng and rb.batch_size <= 1024)
+                and L.fused_train and rb.device_rng and rb.batch_size <= 1024)
 
     def _prio_stream_get(self):
         if getattr(self, "_prio_stream", None) is None:

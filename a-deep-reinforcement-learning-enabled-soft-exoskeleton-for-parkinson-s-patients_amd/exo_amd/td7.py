@@ -21,6 +21,7 @@ adds the replay buffer, the checkpoint policy and data parallelism.
 import copy
 import ctypes
 import os
+import warnings
 from dataclasses import dataclass, field
 from typing import Callable
 
@@ -618,7 +619,10 @@ class TD7Learner:
         if os.environ.get("EXO_TD7_FUSED", "1") != "0" and self._device_rng:
             from . import fused as _fused
             if _fused.supported(self):
-                self.fused = _fused.FusedNets(self)
+                try:
+                    self.fused = _fused.FusedNets(self)
+                except _fused.PlanError as e:  # the per-layer kernels run this shape
+                    warnings.warn(f"{e}; the per-layer kernels run this network")
 
     ENC_LAYERS = ("zs1", "zs2", "zs3", "zsa1", "zsa2", "zsa3")
 
@@ -735,8 +739,16 @@ class TD7Learner:
             encoder_loss = ops.mse_loss(pred_zs.float(), next_zs.float())
             encoder_loss.backward()
 
+    @property
+    def fused_train(self):
+        """The update's passes run fused (FusedNets.train_ok: every gradient
+        pass's plan fits; a learner whose actor pass does not -- e.g. the Pink
+        agent's 300-wide actor -- keeps the fused select_action and trains on
+        the per-layer kernels)."""
+        return self.fused is not None and self.fused.train_ok
+
     def phase_grads(self, state, action, next_state, reward, not_done, noise=None):
-        if self.fused is not None and state.is_cuda:
+        if self.fused_train and state.is_cuda:
             return self._phase_grads_fused(state, action, next_state, reward, not_done, noise)
         hp = self.hp
         # ---- encoder (:219-228)
@@ -1009,7 +1021,7 @@ class TD7Learner:
     def prefetch_targets(self, state, action, next_state, slot):
         """fixed(s, a) and the target heads of (s') for the batch in `slot`, on
         the current stream (fixed on a branch beside the target chain)."""
-        if self.fused is None:
+        if not self.fused_train:
             raise RuntimeError("prefetch_targets: the fused TD7 path only")
         fz = self.fused
         zs, zsa, qt = self._pre_slot(slot, state.shape[0])
@@ -1080,7 +1092,7 @@ class TD7Learner:
 
     def phase_actor_grads(self, state, action):
         """:268-277 with the just-updated critic."""
-        if self.fused is not None and state.is_cuda and not self.offline:
+        if self.fused_train and state.is_cuda and not self.offline:
             # fused: actor forward (unless prefetched on its branch), the critic
             # heads back to the action / zsa inputs, the zsa and actor backward,
             # then the actor's weight gradients (one grouped launch)

@@ -671,6 +671,13 @@ int td7f_adam_pack(int32_t prec, int32_t nopt, float *const *p_dev, float *const
                    const float *weight_decay, int32_t nseg, const float *const *g_dev, const int64_t *off,
                    const int32_t *n, const int32_t *opt, int32_t njobs, const td7f_pack_job *jobs,
                    const int32_t *job_seg, uint32_t *ticket_dev, void *stream);
+/* Plan-only mode for the calling host thread (on != 0): every td7f_* pass
+ * below validates its arguments and its shared-memory plan and returns without
+ * launching (EXO_EINVAL when a network shape's images do not fit one
+ * workgroup's LDS).  The host side probes each pass once when it builds the
+ * fused passes for a learner (TD7_multi_agent.py:148-190, Agent.__init__) and
+ * keeps the per-layer kernels for a shape the fused plan cannot hold. */
+int td7f_probe(int32_t on);
 /* Agent.select_action_batch (TD7_multi_agent.py:192-209 batched): actor(obs,
  * fixed_encoder.zs(obs)) + Gaussian exploration noise -> act_out [n][A].
  * enc: zs1..zs3, actor: l0..l3.  wg_cap > 0 (16-row tiles): at most that

@@ -38,8 +38,12 @@ def _rel(x, y):
 
 def _learner(precision, width):
     torch.manual_seed(3)
-    hp = Hyperparameters() if width is None else Hyperparameters(zs_dim=width, enc_hdim=width, critic_hdim=width,
-                                                                 actor_hdim=width)
+    if width is None:
+        hp = Hyperparameters()
+    elif isinstance(width, dict):  # uneven widths
+        hp = Hyperparameters(**width)
+    else:
+        hp = Hyperparameters(zs_dim=width, enc_hdim=width, critic_hdim=width, actor_hdim=width)
     from exo_amd import fused
     f0 = fused.FUSED_F32
     fused.FUSED_F32 = precision == "fp32"  # read when the learner builds its fused nets
@@ -47,6 +51,9 @@ def _learner(precision, width):
         L = TD7Learner(80, 7, hp, device="cuda", precision=precision)
     finally:
         fused.FUSED_F32 = f0
+    if L.fused is None and isinstance(width, dict):
+        pytest.skip("this shape's fused plan does not fit: the per-layer kernels run it "
+                    "(test_uneven_widths_probe_or_fall_back)")
     assert L.fused is not None
     # non-trivial target / fixed nets: perturb them away from the live ones
     g = torch.Generator(device="cuda").manual_seed(5)
@@ -80,8 +87,14 @@ def test_fixed_embeddings_match_per_layer(precision, width, B):
     assert _rel(zsa, zsa_ref) < _tol(precision), _rel(zsa, zsa_ref)
 
 
+# ZS_WIDE: zs_dim well above actor_hdim, where fp32's action output no longer
+# fits the overlay region of td7f_target and gets its own
+ZS_WIDE = dict(zs_dim=300, enc_hdim=300, critic_hdim=320, actor_hdim=260)
+
+
 @pytest.mark.parametrize("precision,width,B", [("bf16", None, 1024), ("bf16", None, 1000), ("fp16", None, 1024),
-                                               ("bf16", 256, 520), ("fp32", None, 1024), ("fp32", None, 1000)])
+                                               ("bf16", 256, 520), ("fp32", None, 1024), ("fp32", None, 1000),
+                                               ("fp32", ZS_WIDE, 520), ("bf16", ZS_WIDE, 520)])
 def test_target_chain_matches_per_layer(precision, width, B):
     L = _learner(precision, width)
     ns, _ = _inputs(B, 1)
@@ -219,3 +232,47 @@ def test_critic_split_launches_equal_one_launch(monkeypatch, precision):
         out.append(st)
     for i, (a, b) in enumerate(zip(*out)):
         torch.testing.assert_close(b, a, rtol=0, atol=0, msg=f"tensor {i}")
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_uneven_widths_probe_or_fall_back(precision):
+    """fp32 with zs_dim well above actor_hdim made td7f_target
+    return EINVAL at its first call.  The target pass now overlays its output
+    image on X | CATA there, and FusedNets.probe runs every pass once in
+    plan-only mode (td7f_probe) when the learner builds them: an inference
+    pass that does not fit falls back to the per-layer kernels at
+    construction, a gradient pass that does not (here the actor's, 260 wide:
+    not a multiple of 16) keeps fused inference and a per-layer update.
+    Either way one training step runs and leaves finite weights."""
+    import warnings
+    from exo_amd import fused
+    from exo_amd.td7 import TD7Learner
+    torch.manual_seed(4)
+    f0 = fused.FUSED_F32
+    fused.FUSED_F32 = True
+    try:
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            L = TD7Learner(80, 7, Hyperparameters(**ZS_WIDE, batch_size=64), device="cuda", precision=precision)
+    finally:
+        fused.FUSED_F32 = f0
+    fell_back = any("per-layer kernels run this network" in str(x.message) for x in w)
+    assert (L.fused is None) == fell_back
+    print(precision, "per-layer fallback" if L.fused is None else
+          f"fused inference, {'fused' if L.fused_train else 'per-layer'} update")
+    if L.fused is not None and not L.fused_train:
+        assert "EINVAL" in L.fused.train_error
+    B = 8 * 64
+    g = torch.Generator(device="cuda").manual_seed(2)
+    s, ns = torch.randn(B, 80, device="cuda", generator=g), torch.randn(B, 80, device="cuda", generator=g)
+    a = torch.rand(B, 7, device="cuda", generator=g) * 2 - 1
+    r, nd = torch.rand(B, 1, device="cuda", generator=g), torch.ones(B, 1, device="cuda")
+    L.update(s, a, ns, r, nd, update_actor=True)
+    torch.cuda.synchronize()
+    for m in (L.actor, L.critic, L.encoder):
+        assert all(torch.isfinite(p).all() for p in m.parameters())
+    if L.fused is not None:
+        qt = L.fused.target_heads(ns, torch.zeros(B, 7, device="cuda"))
+        zs, zsa = L.fused.fixed(s, a)
+        torch.cuda.synchronize()
+        assert torch.isfinite(qt).all() and torch.isfinite(zs).all() and torch.isfinite(zsa).all()
