@@ -775,6 +775,7 @@ def main():
             if dist_on:
                 dist.barrier()
             torch.cuda.synchronize()
+            s0 = trainer.env_steps_total() if trainer.budget else None
             t = time.perf_counter()
             n = 0
             for _ in range(round_len):
@@ -786,6 +787,8 @@ def main():
             dt = torch.tensor([time.perf_counter() - t], device=dev, dtype=torch.float64)
             if dist_on:
                 dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+            if s0 is not None:  # step budget: step() returns 0, the device counts the env-steps
+                n = trainer.env_steps_total() - s0
             return float(dt), n, round_len
         while not trainer.next_step_resets():
             trainer.step()
