@@ -27,6 +27,7 @@ import numpy as np
 import torch
 
 from . import _native as nat
+from . import td7 as _td7
 from .td7 import ENC_STEP_BRANCH
 
 
@@ -194,6 +195,13 @@ class ForkJoinAudit:
             raise CaptureForkError(f"{len(bad)} stream(s) forked from the capture stream were not joined back "
                                    "before capture end")
         return False
+
+
+# r05: where the rollout branch (select_action -> env step -> replay insert)
+# forks from the iteration.  The iteration's first ~90 us are CU-throughput
+# bound (DESIGN.md 4 "TD7 fused", r05 schedule): EXO_ROLLOUT_AFTER="fixed"
+# forks it after the fixed embeddings' pass instead of at the iteration start.
+ROLLOUT_AFTER = os.environ.get("EXO_ROLLOUT_AFTER", "")
 
 
 class VecTrainer:
@@ -429,9 +437,19 @@ class VecTrainer:
         if getattr(self, "_rollout_stream", None) is None:
             self._rollout_stream = torch.cuda.Stream(device=self.device)
         br = self._rollout_stream
-        br.wait_stream(cur)
-        with torch.cuda.stream(br):
-            self._rollout()
+
+        def rollout_branch(cur=cur, br=br):
+            br.wait_stream(cur)
+            with torch.cuda.stream(br):
+                self._rollout()
+        L = ag.learner
+        late = (ROLLOUT_AFTER == "fixed" and L.fused_train and L.pre_in is None and not self._pre_in
+                and not _td7.TARGET_ON_MAIN)
+        if late:
+            # forked after the fixed pass (TD7Learner.after_fixed): see ROLLOUT_AFTER
+            L.after_fixed = rollout_branch
+        else:
+            rollout_branch()
         self._us_done = False
         if self._us_after_critic():
             # the priority update + next sample on its branch as soon as the
@@ -450,6 +468,8 @@ class VecTrainer:
             ag.learner.after_critic = fork
         self._prio = ag.learner.phase_grads(*self._batch)
         ag.learner.after_critic = None
+        if ag.learner.after_fixed is not None:
+            raise RuntimeError("VecTrainer: the rollout branch was not forked (no fixed pass in phase_grads)")
         cur.wait_stream(br)
 
     # LAP.update_priority reads only the sampled indices and the new priorities

@@ -48,6 +48,19 @@ TARGET_ON_MAIN = os.environ.get("EXO_TD7_TARGET_ON_MAIN", "0") == "1"
 # fp32 (profiles/r05m_raw) -- its 128 workgroups take CUs from the target chain
 # it runs beside.  EXO_CRITIC_SPLIT=1 turns it on.
 CRITIC_SPLIT = os.environ.get("EXO_CRITIC_SPLIT", "0") == "1"
+# r05: when the encoder update's branch starts.  The iteration's first ~90 us
+# are CU-throughput bound (select_action 256 workgroups x ~40 us, fixed, the
+# target chain's first pass and the encoder pass 64 x ~50 / ~48 / ~108 us:
+# ~23 k CU-us on 256 CUs, and target_a -- the critical chain -- ends when that
+# work drains, wherever it starts); the encoder pass has the most slack (only
+# its own step at the iteration's end reads it).  EXO_ENC_AFTER: "fixed" (the
+# default) forks it after the fixed embeddings' pass: 0.2946-0.3003 vs
+# 0.2976-0.3083 ms per iteration over 3 same-box A/B runs (profiles/r05_sched,
+# target_a 78 -> 55 us in the loop's trace); "target" after the target chain
+# (0.3064-0.3066: no gain); "0" at the iteration start (r04 layout).
+ENC_AFTER = os.environ.get("EXO_ENC_AFTER", "fixed")
+if ENC_AFTER == "0":
+    ENC_AFTER = ""
 # fused optimiser step + weight repack (td7f_adam_pack); EXO_ADAM_PACK=0: two launches
 ADAM_PACK = os.environ.get("EXO_ADAM_PACK", "1") != "0"
 # graph-replayed trainer on one GPU, fused: the encoder's weight gradients and
@@ -918,25 +931,39 @@ class TD7Learner:
             qt = fz.target_heads(next_state, noise)
             cur.wait_stream(fside)
         else:
-            if branch:
-                side, tside = stream("_side"), stream("_tside")
+            def encoder_branch():
+                side = stream("_side")
                 with torch.cuda.stream(side):
                     tr.encoder(state, action, next_state)
                     if enc_step:
                         tr.wgrad_encoder(adam=wg_adam)
                         if inline:
                             self.sync.avg_(tr.enc_grad)
+                return side
+
+            if branch:
+                if not ENC_AFTER:
+                    side = encoder_branch()
+                tside = stream("_tside")
                 with torch.cuda.stream(tside):
                     qt = fz.target_heads(next_state, noise)
             else:
                 tr.encoder(state, action, next_state)
                 qt = fz.target_heads(next_state, noise)
             zs, zsa = fz.fixed(state, action)
+            hook, self.after_fixed = self.after_fixed, None
+            if hook is not None:  # the trainer's rollout branch (VecTrainer._pre, EXO_ROLLOUT_AFTER)
+                hook()
             if branch and self.prefetch_actor and self.actor_branch:
                 aside = stream("_aside")
                 with torch.cuda.stream(aside):
                     tr.actor(0, state, zs)
                 self._actor_fused_pre = True
+            if branch and ENC_AFTER == "fixed":
+                side = encoder_branch()  # forks from the iteration's stream after the fixed pass
+            elif branch and ENC_AFTER:
+                cur.wait_stream(tside)
+                side = encoder_branch()  # ... after the target chain (and the fixed pass)
             if branch and CRITIC_SPLIT:
                 # the critic's forward now, beside the target chain
                 tr.critic(state, action, zs, zsa, qt, reward, not_done, phase=1)
@@ -998,6 +1025,7 @@ class TD7Learner:
     # prefetched slot), and Agent.train()'s own updates drop them too.
     pre_in = None  # slot whose prefetched inputs the next phase_grads reads (set by the trainer)
     after_critic = None  # called with the critic pass's |td| right after it (set by the trainer)
+    after_fixed = None  # called right after the fixed pass is captured (set by the trainer)
 
     def _pre_slot(self, slot, B):
         bufs = getattr(self, "_pre_bufs", None)
