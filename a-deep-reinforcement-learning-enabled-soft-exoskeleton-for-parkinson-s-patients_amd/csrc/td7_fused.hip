@@ -649,8 +649,9 @@ int td7f_probe(int32_t on) {
 }
 
 int td7f_select(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7f_lin *actor, const float *obs,
-                int32_t n, const td7f_noise *noise, float *out, int32_t wg_cap, void *stream) {
-    if (!prec_ok(prec) || !act || !enc || !actor || !obs || !noise || !out || n <= 0 || wg_cap < 0)
+                int32_t n, const td7f_noise *noise, float *out, int32_t wg_cap, int32_t rt, void *stream) {
+    if (!prec_ok(prec) || !act || !enc || !actor || !obs || !noise || !out || n <= 0 || wg_cap < 0 || rt < 0 ||
+        rt > 2)
         return EXO_EINVAL;
     const int kd = kd_of(prec);
     td7f_lin all[7] = {enc[0], enc[1], enc[2], actor[0], actor[1], actor[2], actor[3]};
@@ -673,12 +674,16 @@ int td7f_select(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7
     // 32-row tiles above 8,192 envs (more than two 16-row workgroups per CU:
     // the weights are then streamed half as often; configs[3]'s 16,384 envs
     // 0.452 vs 0.494 ms per iteration, profiles/r04q_raw); 16-row tiles below
-    // (4,096 envs: one workgroup per CU).  EXO_SELECT_RT=1|2 forces one (read
-    // per call: tests switch it).
+    // (4,096 envs: one workgroup per CU); `rt` 1 | 2 asks for one (the
+    // overlapped training pairs run select_action on their critical chain
+    // beside the update's passes: 32-row tiles, half the workgroups and weight
+    // bytes, 0.249-0.255 vs 0.259-0.265 ms per iteration, profiles/r05_sched).
+    // EXO_SELECT_RT=1|2 overrides (read per call: tests switch it).
     const char *rt_env = getenv("EXO_SELECT_RT");
     // (fp32: 16-row tiles only -- a 32-row tile's fp32 images exceed the LDS)
     const int RT = prec == PREC_F32 ? 1
-                   : rt_env && (rt_env[0] == '1' || rt_env[0] == '2') ? rt_env[0] - '0' : (n > 8192 ? 2 : 1);
+                   : rt_env && (rt_env[0] == '1' || rt_env[0] == '2') ? rt_env[0] - '0'
+                   : rt ? rt : (n > 8192 ? 2 : 1);
     const int rows = RT * TR, hmax = std::max(enc[0].n_out, std::max(enc[1].n_out, std::max(a.Ha, actor[1].n_out)));
     Bump b(RT);
     a.X = b.r16(rows, ld16(a.S, kd));

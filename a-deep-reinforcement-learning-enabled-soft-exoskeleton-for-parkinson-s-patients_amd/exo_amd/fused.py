@@ -305,7 +305,7 @@ class FusedNets:
 
     # ------------------------------------------------------------- passes
     @torch.no_grad()
-    def select(self, obs, scale=1.0, dec_count=None, world=1, wg_cap=None):
+    def select(self, obs, scale=1.0, dec_count=None, world=1, wg_cap=None, rt=None):
         """select_action_batch with Gaussian exploration (one launch): actor(obs,
         fixed_encoder.zs(obs)) + N(0, exploration_noise) per element, clamped,
         times max_action; exploration_noise decreases once per env (dec_count:
@@ -323,10 +323,11 @@ class FusedNets:
         else:
             nz = self._noise(L._explore_rng, L.exploration_noise_t, dec * n, 0.0, scale)
         fe, ac = self.nets["fixed_encoder"].layers, self.nets["actor"].layers
-        # wg_cap: at most this many workgroups per launch (None / 0: one launch)
+        # wg_cap: at most this many workgroups per launch (None / 0: one launch);
+        # rt: rows per tile / 16 (None / 0: the library's pick)
         nat.check(nat.lib().td7f_select(self.prec, self.act, _lin_array(fe[:3]), self.nets["actor"].array,
                                         nat.ptr(obs), n, ctypes.byref(nz), nat.ptr(out), int(wg_cap or 0),
-                                        nat.stream_ptr(obs.device)), "td7f_select")
+                                        int(rt or 0), nat.stream_ptr(obs.device)), "td7f_select")
         return out
 
     def _img(self, B):

@@ -20,6 +20,7 @@ so it is captured once into HIP graphs and replayed:
 Host-side bookkeeping left outside the graphs: the env reset at the end of a
 round, the target-network refresh every 250 steps (:284-293).
 """
+import contextlib
 import os
 import threading
 
@@ -27,6 +28,7 @@ import numpy as np
 import torch
 
 from . import _native as nat
+from .graphs import new_graph
 from . import td7 as _td7
 from .td7 import ENC_STEP_BRANCH
 
@@ -42,7 +44,7 @@ def graph_reductions_ok(device, rows=1024, cols=300, replays=3):
     s.wait_stream(torch.cuda.current_stream(device))
     with torch.cuda.stream(s):
         x.sum(0)
-        g = torch.cuda.CUDAGraph()
+        g = new_graph()
         with torch.cuda.graph(g, stream=s):
             out = x.sum(0)
     torch.cuda.current_stream(device).wait_stream(s)
@@ -309,11 +311,26 @@ class VecTrainer:
             return int(env)
         return 128 if self.agent.learner.precision == "fp32" else None
 
+    # select_action's row tiles in this loop (16-bit operands; fp32 keeps 16
+    # rows): with overlapped pairs (below) the second iteration's select_action
+    # is on the pair's critical chain beside the update's passes, where 32-row
+    # tiles (half the workgroups, half the weight bytes) run it sooner: 0.249-
+    # 0.255 vs 0.259-0.265 ms per iteration (profiles/r05_sched); unpaired they
+    # measured even (r03).  Not bit-identical to 16-row tiles (another fp32
+    # summation order: ~1 % of the actions differ in the last bf16 bits).
+    # EXO_LOOP_SELECT_RT: 2 (default), 1, or 0 (the library's pick).
+    loop_select_rt = int(os.environ.get("EXO_LOOP_SELECT_RT", "2"))
+
+    def _select_rt(self):
+        if self.agent.learner.precision == "fp32":
+            return None
+        return self.loop_select_rt or None
+
     def _rollout(self):
         ag = self.agent
         obs = self.obs
         act = ag.select_action_batch(obs, timestep=self.k_dev if self.exploration == "pink" else None,
-                                     dec_count=self.active_count, wg_cap=self._select_cap())
+                                     dec_count=self.active_count, wg_cap=self._select_cap(), rt=self._select_rt())
         nobs, rew, done, info = self.env.step(act, active=self.active, out=self._outs[self._cur],
                                               obs_cur=obs if self.budget else None)
         ag.replay_buffer.add_batch(obs, act, nobs, rew, done, self.strata, self.active)
@@ -440,6 +457,8 @@ class VecTrainer:
 
         def rollout_branch(cur=cur, br=br):
             br.wait_stream(cur)
+            if self._overlap_wait is not None:  # overlapped pair: after the previous actor step
+                br.wait_stream(self._overlap_wait)
             with torch.cuda.stream(br):
                 self._rollout()
         L = ag.learner
@@ -511,9 +530,26 @@ class VecTrainer:
             self._us_done = False
             ag.learner.phase_steps(flat_grad, grad_scale)
             if update_actor:
-                ag.learner.phase_actor_grads(self._batch[0], self._batch[1])
+                with self._actor_ctx():
+                    ag.learner.phase_actor_grads(self._batch[0], self._batch[1])
             return
         self._pside = None
+        if update_actor and self._actor_stream is not None:
+            # overlapped pair, first iteration: the actor branch captured before
+            # the priority update's, so the graph's stream assignment (first
+            # child inherits its parent's queue) keeps the actor passes off the
+            # queue the next iteration's update chain inherits from the sample
+            ag.learner.phase_steps(flat_grad, grad_scale)
+            with self._actor_ctx():
+                ag.learner.phase_actor_grads(self._batch[0], self._batch[1])
+            cur = torch.cuda.current_stream(self.device)
+            if getattr(self, "_prio_stream", None) is None:
+                self._prio_stream = torch.cuda.Stream(device=self.device)
+            self._pside = self._prio_stream
+            self._pside.wait_stream(cur)
+            with torch.cuda.stream(self._pside):
+                self._update_and_sample_next()
+            return
         if self.prio_branch and not self.dp and (update_actor or self.prio_branch_all):
             cur = torch.cuda.current_stream(self.device)
             if getattr(self, "_prio_stream", None) is None:
@@ -527,7 +563,20 @@ class VecTrainer:
             ag.learner.phase_steps(flat_grad, grad_scale)
             self._update_and_sample_next()
         if update_actor:
-            ag.learner.phase_actor_grads(self._batch[0], self._batch[1])
+            with self._actor_ctx():
+                ag.learner.phase_actor_grads(self._batch[0], self._batch[1])
+
+    # overlapped pairs (below): the first iteration's actor passes on a stream
+    # of their own, which the next iteration's rollout and critic step wait for
+    _actor_stream = None
+    _overlap_wait = None
+
+    def _actor_ctx(self):
+        st = self._actor_stream
+        if st is None:
+            return contextlib.nullcontext()
+        st.wait_stream(torch.cuda.current_stream(self.device))
+        return torch.cuda.stream(st)
 
     def _update_and_sample_next(self):
         """LAP.update_priority of this iteration's batch, then (prefetching) the
@@ -560,7 +609,8 @@ class VecTrainer:
 
     def _post(self, update_actor, flat_grad=None, grad_scale=1.0):
         if update_actor:
-            self.agent.learner.phase_actor_step(flat_grad, grad_scale)
+            with self._actor_ctx():
+                self.agent.learner.phase_actor_step(flat_grad, grad_scale)
 
     def _inline(self, update_actor, rollout=True):
         """One iteration with the data-parallel collectives in line (RCCL,
@@ -636,7 +686,7 @@ class VecTrainer:
         parts = []
         with torch.cuda.stream(s):
             if not self.dp or self.dp_inline:
-                g = torch.cuda.CUDAGraph()
+                g = new_graph()
                 with torch.cuda.graph(g, pool=pool, stream=s), ForkJoinAudit(s):
                     if self.dp_inline:
                         self._inline(update_actor, rollout)
@@ -651,7 +701,7 @@ class VecTrainer:
                 # grads are allocated inside the capture), so the all-reduces
                 # work on flat buckets packed/unpacked inside the graphs.
                 L, S = self.agent.learner, self.agent.sync
-                g1, g2, g3 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                g1, g2, g3 = new_graph(), new_graph(), new_graph()
                 with torch.cuda.graph(g1, pool=pool, stream=s), ForkJoinAudit(s):
                     self._pre(rollout)
                     flat_c = S.pack(L.grad_params())
@@ -696,45 +746,86 @@ class VecTrainer:
     # graph launch per two iterations.  Only where no host work falls between
     # them: no target refresh, no episode-round reset, no prefetch flags.
     pair_graphs = os.environ.get("EXO_PAIR_GRAPHS", "0") == "1"
+    # r05, overlapped pairs (EXO_OVERLAP_PAIRS=1; one GPU, fused update, policy
+    # freq 2): an actor iteration and the critic-only iteration after it as one
+    # graph in which the second iteration's target chain, fixed embeddings and
+    # encoder update start as soon as the first one's priority update + next
+    # sample (their batch) and encoder step are in -- beside the first one's
+    # actor passes -- while its rollout (select_action reads the new actor and
+    # the priority update's max_priority) and its critic step (the actor
+    # passes read the critic's weights) wait for the actor branch.  The same
+    # launches on the same inputs: bit-identical to the unpaired graphs.
+    # On by default since r05: 0.249-0.269 vs 0.287-0.288 ms per iteration
+    # (profiles/r05_sched); EXO_OVERLAP_PAIRS=0 turns it off.
+    overlap_pairs = os.environ.get("EXO_OVERLAP_PAIRS", "1") == "1"
     _pair_second = False
 
     def _pair_ok(self):
         L = self.agent.learner
-        return (self.pair_graphs and self.use_graphs and not self.dp and self.iters >= self.warmup_eager
+        if self.overlap_pairs and not self.pair_graphs:
+            # overlapped pairs start at an actor iteration (fused update only)
+            if not (L.fused_train and L.training_steps % L.hp.policy_freq == 0 and L.hp.policy_freq == 2):
+                return False
+        elif not self.pair_graphs:
+            return False
+        return (self.use_graphs and not self.dp and self.iters >= self.warmup_eager
                 and not (self._pre_in or self._pre_out)
                 and L.training_steps % L.hp.target_update_rate != 0
                 and (self.episodes == "async" or self.k + 1 < self.round_len))
 
-    def _pair_key(self, ua, ua2):
-        return ("pair", ua, ua2, self._cur)
+    def _pair_key(self, ua, ua2, overlap=False):
+        return ("pair", ua, ua2, self._cur) + (("overlap",) if overlap else ())
 
-    def _run_pair(self, ua, ua2):
+    def _run_pair(self, ua, ua2, overlap=False):
         """This iteration and the next as one graph (captured on first use per
-        policy-update parities and observation buffer)."""
+        policy-update parities and observation buffer).  overlap (an actor
+        iteration, then a critic-only one; see overlap_pairs): the first
+        iteration's actor passes on a branch of their own that only the second
+        iteration's rollout and critic step wait for."""
         L = self.agent.learner
-        key = self._pair_key(ua, ua2)
+        key = self._pair_key(ua, ua2, overlap)
         g = self.graphs.get(key)
         if g is None:
             s = torch.cuda.Stream(device=self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
-            g = torch.cuda.CUDAGraph()
+            g = new_graph()
             cur0 = self._cur
-            with torch.cuda.stream(s):
-                with torch.cuda.graph(g, stream=s), ForkJoinAudit(s):
-                    for i, u in enumerate((ua, ua2)):
-                        L.prefetch_actor = u
-                        self._pre(True)
-                        self._mid(u, rollout=True)
-                        self._post(u)
-                        self._join_prio()
-                        if i == 0:
-                            self._cur ^= 1
-                            self.iters += 1  # the second half is never iteration 0
+            keep = []
+            if overlap and getattr(self, "_astream", None) is None:
+                self._astream = torch.cuda.Stream(device=self.device)
+            try:
+                with torch.cuda.stream(s):
+                    with torch.cuda.graph(g, stream=s), ForkJoinAudit(s):
+                        for i, u in enumerate((ua, ua2)):
+                            L.prefetch_actor = u
+                            if overlap and i == 0:
+                                self._actor_stream = self._astream
+                            if overlap and i == 1:
+                                self._actor_stream = None
+                                self._overlap_wait = self._astream
+                                L.before_critic_step = lambda st=self._astream: (
+                                    torch.cuda.current_stream(self.device).wait_stream(st))
+                            self._pre(True)
+                            self._mid(u, rollout=True)
+                            self._post(u)
+                            self._join_prio()
+                            if i == 0:
+                                # the first iteration's tensors its actor branch
+                                # still reads stay allocated through the capture
+                                keep.append(L._fixed_zs)
+                                self._cur ^= 1
+                                self.iters += 1  # the second half is never iteration 0
+                        if overlap:
+                            s.wait_stream(self._astream)
+            finally:
+                self._actor_stream = self._overlap_wait = None
+                L.before_critic_step = None
             torch.cuda.current_stream(self.device).wait_stream(s)
             self._cur = cur0
             self.iters -= 1
             L.prefetch_actor = ua
             self.graphs[key] = g
+            self._pair_keep = getattr(self, "_pair_keep", []) + keep
         g.replay()
 
     # ------------------------------------------------------------- step
@@ -751,12 +842,27 @@ class VecTrainer:
         counter, host sync)."""
         return int(self._steps_total.item())
 
+    # Pair graphs run two iterations' GPU work at the first one's step(): only
+    # inside a run the caller announced (plan), so no step() ever does work
+    # past the last call the caller makes.
+    _horizon = None
+
+    def plan(self, n):
+        """Announce that step() will be called n more times in a row (None:
+        unknown, every step() one iteration's work).  Pair graphs -- the
+        overlapped pairs, on by default -- start only where at least two
+        announced calls remain."""
+        self._horizon = None if n is None else int(n)
+
     def step(self):
         """One training iteration; returns the number of active env-steps (with
         a step budget: 0, the count stays on the device, env_steps_total();
         async episodes without a budget: every env, N)."""
         ag = self.agent
         L = ag.learner
+        horizon = self._horizon
+        if horizon is not None:
+            self._horizon = horizon - 1
         if self._pair_second:  # its GPU work ran with the previous step's pair graph
             self._pair_second = False
             L.training_steps += 1
@@ -773,11 +879,13 @@ class VecTrainer:
         self._pre_in, self._pre_out = self._target_prefetch_flags()
         if not self.use_graphs or self.iters < self.warmup_eager:
             self._eager(update_actor)
-        elif (self._pair_ok() and self._key(update_actor, True) in self.graphs
+        elif (horizon is not None and horizon >= 2 and self._pair_ok() and self._key(update_actor, True) in self.graphs
               and ((L.training_steps + 1) % ag.hp.policy_freq == 0, 1 - self._cur, False, False) in self.graphs):
             # (both halves captured alone first: their warm-up created every
             # buffer the pair capture needs)
-            self._run_pair(update_actor, (L.training_steps + 1) % ag.hp.policy_freq == 0)
+            ua2 = (L.training_steps + 1) % ag.hp.policy_freq == 0
+            self._run_pair(update_actor, ua2,
+                           overlap=self.overlap_pairs and update_actor and not ua2 and L.fused_train)
             self._pair_second = True
         elif self._key(update_actor, True) not in self.graphs:
             self._capture(update_actor)
@@ -830,7 +938,7 @@ class VecTrainer:
         ag, L = self.agent, self.agent.learner
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
-        g = torch.cuda.CUDAGraph()
+        g = new_graph()
         with torch.cuda.stream(s):
             with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"), ForkJoinAudit(s):
                 L.update_targets_device()
@@ -1122,7 +1230,7 @@ class RefScheduleTrainer(VecTrainer):
         if g is None:
             s = torch.cuda.Stream(device=self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
-            g = torch.cuda.CUDAGraph()
+            g = new_graph()
             cur0 = self._cur
             with torch.cuda.stream(s):
                 with torch.cuda.graph(g, stream=s), ForkJoinAudit(s):
@@ -1153,7 +1261,7 @@ class RefScheduleTrainer(VecTrainer):
             if g is None:
                 s = torch.cuda.Stream(device=self.device)
                 s.wait_stream(torch.cuda.current_stream(self.device))
-                g = torch.cuda.CUDAGraph()
+                g = new_graph()
                 with torch.cuda.stream(s):
                     with torch.cuda.graph(g, stream=s), ForkJoinAudit(s):
                         self._rollout_ref(random)

@@ -33,6 +33,7 @@ import torch.nn.functional as F
 
 from . import _native as nat
 from . import ops
+from .graphs import new_graph
 from .ops import avg_l1_norm
 
 # fused schedule variant (r03, off): the critic target chain on the update's
@@ -484,7 +485,7 @@ class GradSync:
         s = torch.cuda.Stream(device=device)
         side, prio = torch.cuda.Stream(device=device), torch.cuda.Stream(device=device)
         s.wait_stream(cur)
-        g = torch.cuda.CUDAGraph()
+        g = new_graph()
         captured = True
         try:
             with torch.cuda.stream(s):
@@ -974,6 +975,9 @@ class TD7Learner:
         hook, self.after_critic = self.after_critic, None
         if hook is not None:  # the trainer's priority update, from |td| (VecTrainer._fork_update_sample)
             hook(tr.td)
+        hook, self.before_critic_step = self.before_critic_step, None
+        if hook is not None:  # the trainer's overlapped pairs: the previous actor passes read the critic
+            hook()
         if enc_step:
             priority = tr.wgrad_critic(adam=wg_adam)
             self._enc_step_pending = True
@@ -1026,6 +1030,7 @@ class TD7Learner:
     pre_in = None  # slot whose prefetched inputs the next phase_grads reads (set by the trainer)
     after_critic = None  # called with the critic pass's |td| right after it (set by the trainer)
     after_fixed = None  # called right after the fixed pass is captured (set by the trainer)
+    before_critic_step = None  # called before the critic's weight-gradient + step launch (set by the trainer)
 
     def _pre_slot(self, slot, B):
         bufs = getattr(self, "_pre_bufs", None)
@@ -1406,7 +1411,7 @@ class Agent:
 
     @torch.no_grad()
     def select_action_batch(self, obs, use_checkpoint=False, use_exploration=True, timestep=None, dec_count=None,
-                            wg_cap=None):
+                            wg_cap=None, rt=None):
         """Device-resident batched actions for the vectorised loop (no host sync).
         timestep (int64 device tensor [1]): Pink-noise exploration -- column
         `timestep` of the episode's noise (init_episode_noise_device) is added
@@ -1422,7 +1427,8 @@ class Agent:
         fz = self.learner.fused
         if fz is not None and use_exploration and timestep is None and not use_checkpoint and obs.is_cuda:
             # zs, actor and the noise in one launch
-            return fz.select(obs, scale=self.max_action, dec_count=dec_count, world=self.sync.world, wg_cap=wg_cap)
+            return fz.select(obs, scale=self.max_action, dec_count=dec_count, world=self.sync.world, wg_cap=wg_cap,
+                             rt=rt)
         a = self.learner.act(obs, use_checkpoint)
         if use_exploration and timestep is not None:
             col = self.noise_dev.index_select(1, timestep).t()           # [1, action_dim]

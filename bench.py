@@ -304,7 +304,8 @@ def critic_gemm_timing(agent, reps=20, replays=10):
         fn()
         st = torch.cuda.Stream(device=dev)
         st.wait_stream(torch.cuda.current_stream(dev))
-        g = torch.cuda.CUDAGraph()
+        from exo_amd.graphs import new_graph
+        g = new_graph()
         with torch.cuda.stream(st):
             with torch.cuda.graph(g, stream=st):
                 for _ in range(reps):
@@ -353,7 +354,8 @@ def fused_critic_timing(agent, reps=20, replays=10):
     fn()
     st = torch.cuda.Stream(device=dev)
     st.wait_stream(torch.cuda.current_stream(dev))
-    gr = torch.cuda.CUDAGraph()
+    from exo_amd.graphs import new_graph
+    gr = new_graph()
     with torch.cuda.stream(st):
         with torch.cuda.graph(gr, stream=st):
             for _ in range(reps):
@@ -418,8 +420,10 @@ def sync_rounds(env, dev, args, hp, group=None, warm=40):
     ag = Agent(80, 7, 1, env_num=8, hp=hp, device=dev, precision=args.precision, n_envs=env.n, graph_safe=True,
                process_group=group)
     tr = VecTrainer(env, ag, episodes="sync")
+    tr.plan(warm)
     for _ in range(warm):
         tr.step()
+    tr.plan(None)
     while not tr.next_step_resets():
         tr.step()
 
@@ -430,6 +434,7 @@ def sync_rounds(env, dev, args, hp, group=None, warm=40):
         torch.cuda.synchronize()
 
     sync_all()
+    tr.plan(None if tr.budget else tr.round_len)  # the round's iterations (pair graphs inside)
     t = time.perf_counter()
     n, its = tr.step(), 1
     while not tr.next_step_resets():
@@ -589,9 +594,11 @@ def td7_variants(env, dev, args, iters=60, warmup=8):
         finally:
             fused.FUSED_F32 = f0
         tr = VecTrainer(env, ag, use_graphs=True)
+        tr.plan(warmup)
         for _ in range(warmup):
             tr.step()
         torch.cuda.synchronize()
+        tr.plan(iters)
         t0 = time.perf_counter()
         for _ in range(iters):
             tr.step()
@@ -776,6 +783,7 @@ def main():
                 dist.barrier()
             torch.cuda.synchronize()
             s0 = trainer.env_steps_total() if trainer.budget else None
+            trainer.plan(round_len)
             t = time.perf_counter()
             n = 0
             for _ in range(round_len):
@@ -790,12 +798,14 @@ def main():
             if s0 is not None:  # step budget: step() returns 0, the device counts the env-steps
                 n = trainer.env_steps_total() - s0
             return float(dt), n, round_len
+        trainer.plan(None)
         while not trainer.next_step_resets():
             trainer.step()
         torch.cuda.synchronize()
         if dist_on:
             dist.barrier()
         torch.cuda.synchronize()
+        trainer.plan(None if trainer.budget else round_len)
         t = time.perf_counter()
         n = trainer.step()  # the episode reset and the round's first iteration
         its = 1
@@ -827,6 +837,8 @@ def main():
         settle = int(os.environ.get("EXO_DIST_SETTLE_ITERS", "0"))
         for _ in range(settle):
             one_step(False)
+    if trainer is not None:
+        trainer.plan(args.warmup)
     for _ in range(args.warmup):
         one_step(False)
     torch.cuda.synchronize()
@@ -839,6 +851,8 @@ def main():
     if clock is not None:
         clock.zero_()
         torch.cuda.synchronize()
+    if trainer is not None:
+        trainer.plan(args.steps)  # the window's iterations: pair graphs never run past it
     t0 = time.perf_counter()
     env_steps = 0
     for _ in range(args.steps):

@@ -683,9 +683,11 @@ int td7f_probe(int32_t on);
  * enc: zs1..zs3, actor: l0..l3.  wg_cap > 0 (16-row tiles): at most that
  * many workgroups per launch, the tiles in back-to-back launches (same
  * results; the noise state advances once); 0: one launch.  The environment
- * variable EXO_SELECT_WG_CAP, when set, overrides wg_cap (experiments). */
+ * variable EXO_SELECT_WG_CAP, when set, overrides wg_cap (experiments).
+ * rt: rows per tile in units of 16 -- 0 picks (32 above 8,192 rows), 1 or 2
+ * asks (16-bit operands; fp32 always 16); EXO_SELECT_RT overrides. */
 int td7f_select(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7f_lin *actor, const float *obs_dev,
-                int32_t n, const td7f_noise *noise, float *act_out_dev, int32_t wg_cap, void *stream);
+                int32_t n, const td7f_noise *noise, float *act_out_dev, int32_t wg_cap, int32_t rt, void *stream);
 /* The critic target chain (TD7_multi_agent.py:233-241): fixed_target_zs(s'),
  * next_action = actor_target(s', zs) + clipped noise, fixed_target_zsa and both
  * heads of critic_target -> qt_dev [B][2].  tenc: zs1..zs3, zsa1..zsa3;

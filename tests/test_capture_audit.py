@@ -43,7 +43,8 @@ def test_forgotten_join_is_reported_and_capture_survives():
     s, br = torch.cuda.Stream(), torch.cuda.Stream()
     x = torch.zeros(16, device="cuda")
     s.wait_stream(torch.cuda.current_stream())
-    g = torch.cuda.CUDAGraph()
+    from exo_amd.graphs import new_graph
+    g = new_graph()
     with torch.cuda.stream(s):
         with pytest.raises(CaptureForkError):
             with torch.cuda.graph(g, stream=s), ForkJoinAudit(s):

@@ -48,7 +48,8 @@ def test_split_encoder_pass_is_bit_identical(precision, width, B):
     # graph-captured: three launches per replay, three replays
     st = torch.cuda.Stream()
     st.wait_stream(torch.cuda.current_stream())
-    gr = torch.cuda.CUDAGraph()
+    from exo_amd.graphs import new_graph
+    gr = new_graph()
     with torch.cuda.stream(st):
         with torch.cuda.graph(gr, stream=st):
             for _ in range(3):

@@ -350,7 +350,8 @@ def test_step_clock_brackets_every_step_launch():
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
-                graph = torch.cuda.CUDAGraph()
+                from exo_amd.graphs import new_graph
+                graph = new_graph()
                 with torch.cuda.graph(graph, stream=s):
                     env.step(act, out=o)
             torch.cuda.current_stream().wait_stream(s)

@@ -167,6 +167,7 @@ def test_fused_trainer_graph_replay_equals_eager(precision):
             fused.FUSED_F32 = f0
         assert ag.learner.fused is not None
         tr = VecTrainer(env, ag, use_graphs=graphs)
+        tr.plan(12)  # graphs: the overlapped pairs (r05) inside the announced run
         for _ in range(12):
             tr.step()
         torch.cuda.synchronize()
@@ -174,6 +175,7 @@ def test_fused_trainer_graph_replay_equals_eager(precision):
                     for p in m.parameters()])
         if graphs:
             assert tr.graphs, "the graph-replayed trainer captured no graph"
+            assert any(k[-1] == "overlap" for k in tr.graphs), "no overlapped pair ran"
     for a, b in zip(*out):
         torch.testing.assert_close(b, a, rtol=0, atol=0)
 
@@ -276,3 +278,24 @@ def test_uneven_widths_probe_or_fall_back(precision):
         zs, zsa = L.fused.fixed(s, a)
         torch.cuda.synchronize()
         assert torch.isfinite(qt).all() and torch.isfinite(zs).all() and torch.isfinite(zsa).all()
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp16"])
+def test_select_row_tiles_argument(precision):
+    """td7f_select's rt argument (r05: the training loop asks for 32-row tiles
+    at 4,096 envs): 16- and 32-row tiles draw the same noise per row and agree
+    to the fused passes' bound (another fp32 summation order flips an
+    occasional 16-bit rounding of a hidden activation), and both match the
+    per-layer path (test_select_action_matches_per_layer[..-2])."""
+    L = _learner(precision, None)
+    s, _ = _inputs(4096, 11)
+    sigma = float(L.exploration_noise_t)
+    outs = []
+    st0 = L._explore_rng.state.clone()
+    for rt in (1, 2):
+        L.exploration_noise_t.fill_(sigma)
+        L._explore_rng.state.copy_(st0)  # the same noise draws
+        outs.append(L.fused.select(s, scale=1.0, rt=rt))
+    torch.cuda.synchronize()
+    assert _rel(outs[1], outs[0]) < REL, _rel(outs[1], outs[0])
+    assert float((outs[1] - outs[0]).abs().max()) < 2e-2

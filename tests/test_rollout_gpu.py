@@ -130,6 +130,7 @@ def test_pair_graphs_are_bit_identical(monkeypatch, episodes):
         monkeypatch.setattr(VecTrainer, "pair_graphs", pair)
         monkeypatch.setenv("EXO_EPISODES", episodes)
         tr, env, ag = _make(True, seed=4)
+        tr.plan(17)  # pairs only inside an announced run
         obs = []
         for _ in range(17):
             tr.step()
@@ -144,3 +145,68 @@ def test_pair_graphs_are_bit_identical(monkeypatch, episodes):
         torch.testing.assert_close(b, a, rtol=0, atol=0)
     torch.testing.assert_close(r1, r0, rtol=0, atol=0)
     assert any(k[0] == "pair" for k in t1.graphs) and not any(k[0] == "pair" for k in t0.graphs)
+
+
+@pytest.mark.parametrize("episodes", ["sync", "async"])
+def test_overlapped_pairs_are_bit_identical(monkeypatch, episodes):
+    """EXO_OVERLAP_PAIRS (r05): an actor iteration and the critic-only one after
+    it in one graph, the second's target chain / fixed / encoder passes beside
+    the first's actor passes (its rollout and critic step wait for them).  The
+    same launches on the same inputs: weights, observations, replay rows and
+    sum trees bit for bit against one graph per iteration, through target
+    refreshes (target_update_rate 5: unpaired graphs around them).  Fused
+    bf16 passes (the overlap needs the fused update), 256-wide nets."""
+    from exo_amd import VecExoskeletonEnv
+    from exo_amd.rollout import VecTrainer
+    from exo_amd.td7 import Agent, Hyperparameters
+    res = []
+    for overlap in (False, True):
+        monkeypatch.setattr(VecTrainer, "overlap_pairs", overlap)
+        monkeypatch.setenv("EXO_EPISODES", episodes)
+        torch.manual_seed(6)
+        hp = Hyperparameters(zs_dim=256, enc_hdim=256, critic_hdim=256, actor_hdim=256, batch_size=32,
+                             target_update_rate=5)
+        env = VecExoskeletonEnv(256, seed=6)
+        ag = Agent(80, 7, 1, hp=hp, env_num=8, buffer_size=4096, graph_safe=True, precision="bf16")
+        assert ag.learner.fused_train
+        tr = VecTrainer(env, ag)
+        tr.plan(20)  # pairs only inside an announced run (20: the last pair ends at it)
+        obs = []
+        for _ in range(20):
+            tr.step()
+            obs.append(tr.obs.clone())
+        torch.cuda.synchronize()
+        L = ag.learner
+        res.append((tr, obs, [p.detach().clone() for m in (L.actor, L.critic, L.encoder) for p in m.parameters()],
+                    ag.replay_buffer.state.clone(), ag.replay_buffer._tree.clone()))
+    (t0, o0, w0, r0, s0), (t1, o1, w1, r1, s1) = res
+    for i, (a, b) in enumerate(zip(o0, o1)):
+        torch.testing.assert_close(b, a, rtol=0, atol=0, msg=f"iteration {i}")
+    for a, b in zip(w0, w1):
+        torch.testing.assert_close(b, a, rtol=0, atol=0)
+    torch.testing.assert_close(r1, r0, rtol=0, atol=0)
+    torch.testing.assert_close(s1, s0, rtol=0, atol=0)
+    assert any(k[-1] == "overlap" for k in t1.graphs) and not any(k[0] == "pair" for k in t0.graphs)
+
+
+def test_pairs_never_run_past_the_announced_steps(monkeypatch):
+    """Without plan() every step() is exactly one iteration's GPU work (no
+    pair graph); with plan(n) a pair starts only where two announced calls
+    remain, so after n calls exactly n iterations have run: the same weights
+    as n unpaired iterations (n odd and even)."""
+    from exo_amd.rollout import VecTrainer
+    monkeypatch.setattr(VecTrainer, "pair_graphs", True)
+    for n in (12, 13):
+        res = []
+        for planned in (False, True):
+            tr, env, ag = _make(True, seed=8)
+            if planned:
+                tr.plan(n)
+            for _ in range(n):
+                tr.step()
+            torch.cuda.synchronize()
+            assert any(k[0] == "pair" for k in tr.graphs) == planned
+            assert ag.learner.training_steps == n
+            res.append([p.detach().clone() for p in ag.learner.critic.parameters()])
+        for a, b in zip(*res):
+            torch.testing.assert_close(b, a, rtol=0, atol=0)
