@@ -720,7 +720,7 @@ class VecTrainer:
                 parts = [g1, g2, g3, flat_c, flat_a]
         torch.cuda.current_stream(self.device).wait_stream(s)
         self.graphs[self._key(update_actor, rollout)] = parts
-        if self.dp_inline and self._refresh_graph is None:
+        if self._graph_refresh() and self._refresh_graph is None:
             self._capture_refresh()
         # capture records but does not execute: run the iteration now
         self._replay(update_actor, rollout)
@@ -910,14 +910,22 @@ class VecTrainer:
     # captured ones -- the first such eager all-reduce of a process cost 96 ms
     # (31-35 ms in later processes) of host time, GPU idle, at training step
     # 250: the first RCCL process's slow mode of r04 (profiles/r05rccl_raw).
+    # One GPU as well (r05): the eager refresh's first run inside a timed
+    # window cost ~8 ms of one-time host work (0.277 vs 0.256 ms per iteration
+    # over a 400-iteration window on a fresh box, profiles/r05_sched/r05x);
+    # the graph is captured with the first iteration graphs.  Eager-collective
+    # data parallelism (gloo) keeps the eager refresh.
     _refresh_graph = None
+
+    def _graph_refresh(self):
+        return self.use_graphs and (not self.dp or self.dp_inline)
 
     def _refresh_targets(self):
         ag = self.agent
         L = ag.learner
         if L.training_steps % L.hp.target_update_rate != 0:
             return False
-        if not (self.dp_inline and self.use_graphs):
+        if not self._graph_refresh():
             L.maybe_update_targets()
             ag.replay_buffer.reset_max_priority()
             ag.sync.max_(ag.replay_buffer._maxp)
