@@ -204,6 +204,16 @@ class ForkJoinAudit:
 # bound (DESIGN.md 4 "TD7 fused", r05 schedule): EXO_ROLLOUT_AFTER="fixed"
 # forks it after the fixed embeddings' pass instead of at the iteration start.
 ROLLOUT_AFTER = os.environ.get("EXO_ROLLOUT_AFTER", "")
+# r05, the captured order (bit-identical either way): EXO_TRAIN_FIRST (default
+# on) captures the rollout branch after the target chain (still forked from
+# the iteration's start), so the graph's first node -- which runs on the
+# launch stream's queue, where the other queues' first nodes wait for a
+# cross-queue start -- is the critical chain's target pass: 0.2535-0.2537 vs
+# 0.2571-0.2577 ms per iteration (profiles/r05_sched/r05o);
+# EXO_PAIR_CRITIC_AFTER_SELECT=1 makes an overlapped pair's second critic pass
+# wait for that iteration's select_action: 0.2616-0.2618, off.
+TRAIN_FIRST = os.environ.get("EXO_TRAIN_FIRST", "1") == "1"
+PAIR_CRITIC_AFTER_SELECT = os.environ.get("EXO_PAIR_CRITIC_AFTER_SELECT", "0") == "1"
 
 
 class VecTrainer:
@@ -331,6 +341,9 @@ class VecTrainer:
         obs = self.obs
         act = ag.select_action_batch(obs, timestep=self.k_dev if self.exploration == "pink" else None,
                                      dec_count=self.active_count, wg_cap=self._select_cap(), rt=self._select_rt())
+        if self._overlap_wait is not None and PAIR_CRITIC_AFTER_SELECT:
+            self._select_done = torch.cuda.Event()
+            self._select_done.record(torch.cuda.current_stream(self.device))
         nobs, rew, done, info = self.env.step(act, active=self.active, out=self._outs[self._cur],
                                               obs_cur=obs if self.budget else None)
         ag.replay_buffer.add_batch(obs, act, nobs, rew, done, self.strata, self.active)
@@ -464,11 +477,32 @@ class VecTrainer:
         L = ag.learner
         late = (ROLLOUT_AFTER == "fixed" and L.fused_train and L.pre_in is None and not self._pre_in
                 and not _td7.TARGET_ON_MAIN)
+        first = (TRAIN_FIRST and not late and L.fused_train and L.pre_in is None and not self._pre_in
+                 and not _td7.TARGET_ON_MAIN and L.overlap)
         if late:
             # forked after the fixed pass (TD7Learner.after_fixed): see ROLLOUT_AFTER
             L.after_fixed = rollout_branch
+        elif first:
+            # forked from the iteration's start, captured after the target chain
+            # (TD7Learner.after_target): see TRAIN_FIRST
+            ev0 = torch.cuda.Event()
+            ev0.record(cur)
+
+            def rollout_from_start(ev0=ev0, br=br):
+                br.wait_event(ev0)
+                if self._overlap_wait is not None:
+                    br.wait_stream(self._overlap_wait)
+                with torch.cuda.stream(br):
+                    self._rollout()
+            L.after_target = rollout_from_start
         else:
             rollout_branch()
+        if self._overlap_wait is not None and PAIR_CRITIC_AFTER_SELECT:
+            # overlapped pair, second iteration: its critic pass after its
+            # select_action (which is on the pair's critical chain)
+            def critic_after_select():
+                torch.cuda.current_stream(self.device).wait_event(self._select_done)
+            L.before_critic = critic_after_select
         self._us_done = False
         if self._us_after_critic():
             # the priority update + next sample on its branch as soon as the
@@ -487,8 +521,9 @@ class VecTrainer:
             ag.learner.after_critic = fork
         self._prio = ag.learner.phase_grads(*self._batch)
         ag.learner.after_critic = None
-        if ag.learner.after_fixed is not None:
-            raise RuntimeError("VecTrainer: the rollout branch was not forked (no fixed pass in phase_grads)")
+        if ag.learner.after_fixed is not None or ag.learner.after_target is not None:
+            raise RuntimeError("VecTrainer: the rollout branch was not forked (no fixed / target pass in phase_grads)")
+        ag.learner.before_critic = None
         cur.wait_stream(br)
 
     # LAP.update_priority reads only the sampled indices and the new priorities

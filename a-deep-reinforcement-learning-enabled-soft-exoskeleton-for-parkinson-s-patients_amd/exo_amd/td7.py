@@ -948,6 +948,9 @@ class TD7Learner:
                 tside = stream("_tside")
                 with torch.cuda.stream(tside):
                     qt = fz.target_heads(next_state, noise)
+                hook, self.after_target = self.after_target, None
+                if hook is not None:  # the trainer's rollout branch (VecTrainer._pre, EXO_TRAIN_FIRST)
+                    hook()
             else:
                 tr.encoder(state, action, next_state)
                 qt = fz.target_heads(next_state, noise)
@@ -971,6 +974,9 @@ class TD7Learner:
                 critic_phase = 2
             if branch:
                 cur.wait_stream(tside)
+        hook, self.before_critic = self.before_critic, None
+        if hook is not None:  # the trainer's overlapped pairs (EXO_PAIR_CRITIC_AFTER_SELECT)
+            hook()
         tr.critic(state, action, zs, zsa, qt, reward, not_done, phase=critic_phase)
         hook, self.after_critic = self.after_critic, None
         if hook is not None:  # the trainer's priority update, from |td| (VecTrainer._fork_update_sample)
@@ -1030,6 +1036,8 @@ class TD7Learner:
     pre_in = None  # slot whose prefetched inputs the next phase_grads reads (set by the trainer)
     after_critic = None  # called with the critic pass's |td| right after it (set by the trainer)
     after_fixed = None  # called right after the fixed pass is captured (set by the trainer)
+    after_target = None  # called right after the target chain is captured (set by the trainer)
+    before_critic = None  # called before the critic pass is captured (set by the trainer)
     before_critic_step = None  # called before the critic's weight-gradient + step launch (set by the trainer)
 
     def _pre_slot(self, slot, B):
