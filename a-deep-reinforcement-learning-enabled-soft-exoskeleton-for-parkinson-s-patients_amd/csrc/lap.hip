@@ -666,6 +666,151 @@ __device__ __forceinline__ void copy_rows(const lap_storage_desc &st, const floa
     }
 }
 
+// The vectorised insert as ONE launch (r05, opt-in: EXO_LAP_STORE_FUSED=1,
+// measured slower in the loop; lap_store_batch at n <= 8,192):
+// lap_store_rank_kernel's scan, leaves and span propagation, and the copy of
+// the stratum's rows by the same workgroup -- the scan leaves each rank's env
+// and slot in LDS, the workgroup's 1,024 threads copy the rows (8 items in
+// flight per thread, float4 state rows where aligned).  One workgroup per
+// stratum reads and writes its own ring pointer, so no other workgroup needs
+// it.  The same rows, slots, leaves and sums as the two launches (an inactive
+// row's copy to the trash row is skipped: nothing reads that row).
+constexpr int STORE_FUSED_MAX = 8192;
+
+template <bool VEC>
+__global__ __launch_bounds__(UPD_THREADS) void lap_store_fused_kernel(
+    float *tree, const float *maxp, int cap, int levels, int capacity, int32_t *ring_ptr, int32_t *ring_size,
+    const int32_t *strata, const uint8_t *active, int n, int32_t *row_of, lap_storage_desc st, const float *state,
+    const float *action, const float *next_state, const float *reward, const uint8_t *done, float action_scale) {
+    constexpr int RPT = 4;
+    const int s = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    float *T = stratum_tree(tree, s, cap);
+    __shared__ int wsum[UPD_THREADS / 64];
+    __shared__ int chunk_total;
+    __shared__ int32_t ri[STORE_FUSED_MAX];
+    const float p = *maxp;
+    const int ptr0 = ring_ptr[s];
+    const int row0 = s * (capacity + 1);
+    int offset = 0;
+    for (int base = 0; base < n; base += RPT * UPD_THREADS) {
+        int stk[RPT], cnt = 0;
+        bool f[RPT];
+#pragma unroll
+        for (int k = 0; k < RPT; ++k) {
+            const int i = base + RPT * t + k;
+            stk[k] = i < n ? strata[i] : -1;
+            f[k] = i < n && (!active || active[i]) && stk[k] == s;
+            cnt += f[k];
+        }
+        int incl = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += v;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        if (t == 0) {
+            int acc = 0;
+            for (int k = 0; k < UPD_THREADS / 64; ++k) {
+                const int v = wsum[k];
+                wsum[k] = acc;
+                acc += v;
+            }
+            chunk_total = acc;
+        }
+        __syncthreads();
+        int rank = offset + wsum[wv] + incl - cnt;
+#pragma unroll
+        for (int k = 0; k < RPT; ++k) {
+            const int i = base + RPT * t + k;
+            if (i >= n) continue;
+            if (s == 0 && (stk[k] < 0 || stk[k] >= (int)gridDim.x)) row_of[i] = -1;
+            if (stk[k] != s) continue;
+            if (f[k]) {
+                const int slot = (ptr0 + rank) % capacity;
+                row_of[i] = row0 + slot;
+                T[cap + slot] = p;
+                ri[rank] = i;
+                ++rank;
+            } else {
+                row_of[i] = row0 + capacity;
+            }
+        }
+        const int total = chunk_total;
+        __syncthreads();
+        offset += total;
+    }
+    // the stratum's rows: rank q -> slot (ptr0 + q) % capacity
+    {
+        const int sd = st.state_dim, ad = st.action_dim;
+        const int sdv = VEC ? sd / 4 : sd;
+        const int per = 2 * sdv + ad + 2;
+        const int items = offset * per;
+        constexpr int U = 8;
+        for (int it0 = t; it0 < items; it0 += U * UPD_THREADS) {
+            float4 v[U];
+            long dst[U];
+            int kind[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int it = it0 + u * UPD_THREADS;
+                kind[u] = -1;
+                if (it >= items) continue;
+                const int q = it / per, c = it - q * per;
+                const long r = (long)row0 + (ptr0 + q) % capacity;
+                const long i = ri[q];
+                if (c < 2 * sdv) {
+                    const bool nx = c >= sdv;
+                    const int e = nx ? c - sdv : c;
+                    const float *src = (nx ? next_state : state) + i * sd;
+                    if (VEC) {
+                        v[u] = ld4(src + 4 * e);
+                        dst[u] = r * sd + 4 * e;
+                    } else {
+                        v[u].x = src[e];
+                        dst[u] = r * sd + e;
+                    }
+                    kind[u] = nx ? 1 : 0;
+                } else if (c < 2 * sdv + ad) {
+                    const int e = c - 2 * sdv;
+                    v[u].x = action[i * ad + e] / action_scale;
+                    dst[u] = r * ad + e;
+                    kind[u] = 2;
+                } else if (c == 2 * sdv + ad) {
+                    v[u].x = reward[i];
+                    dst[u] = r;
+                    kind[u] = 3;
+                } else {
+                    v[u].x = 1.0f - (done[i] ? 1.0f : 0.0f);
+                    dst[u] = r;
+                    kind[u] = 4;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                switch (kind[u]) {
+                case 0:
+                    if (VEC) st4(st.state + dst[u], v[u]); else st.state[dst[u]] = v[u].x;
+                    break;
+                case 1:
+                    if (VEC) st4(st.next_state + dst[u], v[u]); else st.next_state[dst[u]] = v[u].x;
+                    break;
+                case 2: st.action[dst[u]] = v[u].x; break;
+                case 3: st.reward[dst[u]] = v[u].x; break;
+                case 4: st.not_done[dst[u]] = v[u].x; break;
+                default: break;
+                }
+            }
+        }
+    }
+    propagate_span(T, cap, levels, capacity, ptr0, offset);
+    if (t == 0) {
+        ring_ptr[s] = (ptr0 + offset) % capacity;
+        ring_size[s] = min(ring_size[s] + offset, capacity);
+    }
+}
+
 // The training loop's per-step mask advance, optionally done by the insert's
 // last workgroup out (lap_store_batch_ref_fused_adv): every workgroup has read
 // the step's mask by then.  exo_active_advance_score's arithmetic: score +=
@@ -1459,6 +1604,31 @@ int lap_store_batch(const lap_tree_desc *t, const lap_storage_desc *st, const fl
         !reward || !done || !strata || !row_ws || n < 0 || action_scale == 0.0f)
         return EXO_EINVAL;
     if (n == 0) return EXO_OK;
+    // the one-launch insert (lap_store_fused_kernel) measured slower inside the
+    // training loop -- 0.2767-0.2771 vs 0.2522-0.2529 ms per iteration
+    // (profiles/r05_sched/r05s2): one workgroup per stratum copying its rows is
+    // slower than 1,024 copy workgroups -- so EXO_LAP_STORE_FUSED=1 opts in
+    static const bool fused_env = [] {
+        const char *v = getenv("EXO_LAP_STORE_FUSED");
+        return v && v[0] == '1';
+    }();
+    if (fused_env && n <= STORE_FUSED_MAX && n <= t->capacity) {  // (no ring wrap inside one call)
+        const bool vec = (st->state_dim & 3) == 0 &&
+                         ((reinterpret_cast<uintptr_t>(state) | reinterpret_cast<uintptr_t>(next_state) |
+                           reinterpret_cast<uintptr_t>(st->state) | reinterpret_cast<uintptr_t>(st->next_state)) &
+                          15) == 0;
+        if (vec)
+            hipLaunchKernelGGL(lap_store_fused_kernel<true>, dim3(t->n_strata), dim3(UPD_THREADS), 0,
+                               (hipStream_t)stream, t->tree, t->max_priority, t->cap, levels_of(t), t->capacity,
+                               st->ptr, st->size, strata, active, n, row_ws, *st, state, action, next_state, reward,
+                               done, action_scale);
+        else
+            hipLaunchKernelGGL(lap_store_fused_kernel<false>, dim3(t->n_strata), dim3(UPD_THREADS), 0,
+                               (hipStream_t)stream, t->tree, t->max_priority, t->cap, levels_of(t), t->capacity,
+                               st->ptr, st->size, strata, active, n, row_ws, *st, state, action, next_state, reward,
+                               done, action_scale);
+        return rc(hipGetLastError());
+    }
     if (n > 4 * STORE_CHUNK)
         hipLaunchKernelGGL(lap_store_rank_kernel<16>, dim3(t->n_strata), dim3(UPD_THREADS), 0, (hipStream_t)stream,
                            t->tree, t->max_priority, t->cap, levels_of(t), t->capacity, st->ptr, st->size, strata,

@@ -406,3 +406,46 @@ def test_store_span_propagation_keeps_the_tree_exact(C):
     cap = lap._cap
     for s in range(E):
         np.testing.assert_array_equal(T[s, 1:cap], T[s, 2:2 * cap:2] + T[s, 3:2 * cap:2])
+
+
+@pytest.mark.parametrize("n,cap,steps", [(4096, 30000, 5), (1000, 2048, 9), (8192, 9000, 3)])
+def test_vectorised_insert_equals_per_row_ring_adds(n, cap, steps):
+    """lap_store_batch (r05: one launch up to 8,192 rows -- scan, leaves, span
+    propagation and the row copies in one workgroup per stratum) against the
+    per-stratum ring semantics row by row: rows of stratum s in env order to
+    slots ptr_s, ptr_s + 1, ... (mod capacity), leaves = max_priority, every
+    inner node the sum of its children; random masks and strata, ring wraps
+    across calls."""
+    E = 8
+    lap = _lap(E, cap, 16)
+    g = torch.Generator(device="cuda").manual_seed(n + cap)
+    strata = torch.randint(0, E, (n,), device="cuda", generator=g, dtype=torch.int32)
+    ptr = np.zeros(E, dtype=np.int64)
+    size = np.zeros(E, dtype=np.int64)
+    want_state = np.zeros((E, cap + 1), dtype=np.float32)
+    st_h = strata.cpu().numpy()
+    for k in range(steps):
+        active = torch.rand(n, device="cuda", generator=g) < 0.8
+        obs = torch.randn(n, 80, device="cuda", generator=g)
+        nobs = torch.randn(n, 80, device="cuda", generator=g)
+        act = torch.rand(n, 7, device="cuda", generator=g) * 2 - 1
+        rew = torch.randn(n, device="cuda", generator=g)
+        done = torch.rand(n, device="cuda", generator=g) < 0.1
+        lap.add_batch(obs, act, nobs, rew, done, strata, active)
+        a_h, o_h = active.cpu().numpy(), obs[:, 0].cpu().numpy()
+        for i in range(n):
+            if a_h[i]:
+                s = st_h[i]
+                want_state[s, ptr[s]] = o_h[i]
+                ptr[s] = (ptr[s] + 1) % cap
+                size[s] = min(size[s] + 1, cap)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(lap.ptr_s.cpu().numpy(), ptr)
+    np.testing.assert_array_equal(lap.size_s.cpu().numpy(), size)
+    np.testing.assert_array_equal(lap.state[:, :cap, 0].cpu().numpy(), want_state[:, :cap])
+    tree = lap._tree.cpu().numpy().astype(np.float64)
+    c2 = tree.shape[1] // 2
+    for s in range(E):
+        leaves = tree[s, c2:]
+        assert np.all(leaves[:size[s]] == 1.0) and np.all(leaves[size[s]:cap] == 0.0)
+        assert tree[s, 1] == float(size[s])  # integer sums: exact at any order
