@@ -608,9 +608,10 @@ class VecTrainer:
 
     def _actor_ctx(self):
         st = self._actor_stream
-        if st is None:
+        cur = torch.cuda.current_stream(self.device)
+        if st is None or cur.cuda_stream == st.cuda_stream:  # (already on it: no self-wait in the capture)
             return contextlib.nullcontext()
-        st.wait_stream(torch.cuda.current_stream(self.device))
+        st.wait_stream(cur)
         return torch.cuda.stream(st)
 
     def _update_and_sample_next(self):
@@ -668,6 +669,24 @@ class VecTrainer:
             if getattr(self, "_prio_stream", None) is None:
                 self._prio_stream = torch.cuda.Stream(device=self.device)
             self._pside = self._prio_stream
+            if update_actor and self._actor_stream is not None:
+                # overlapped pair, first iteration: the critic bucket, the
+                # actor branch (its bucket's all-reduce and step on it), then
+                # the priority update + sample and its MAX -- the actor branch
+                # captured before the priority update's (see _mid); the
+                # collectives' capture order is still one order on every rank
+                flat_c = L.allreduce_phase_grads(self._batch[0].shape[0])
+                L.phase_steps(flat_c, 1.0)
+                with self._actor_ctx():
+                    L.phase_actor_grads(self._batch[0], self._batch[1])
+                    flat_a = L.allreduce_actor_grads()
+                    self._post(update_actor, flat_a, 1.0)
+                self._pside.wait_stream(cur)
+                with torch.cuda.stream(self._pside):
+                    self._update_and_sample_next()
+                    S.max_(ag.replay_buffer._maxp)
+                self._join_prio()
+                return
             self._pside.wait_stream(cur)
             with torch.cuda.stream(self._pside):
                 self._update_and_sample_next()
@@ -803,7 +822,8 @@ class VecTrainer:
                 return False
         elif not self.pair_graphs:
             return False
-        return (self.use_graphs and not self.dp and self.iters >= self.warmup_eager
+        return (self.use_graphs and (not self.dp or (self.dp_inline and self.overlap_pairs and not self.pair_graphs))
+                and self.iters >= self.warmup_eager
                 and not (self._pre_in or self._pre_out)
                 and L.training_steps % L.hp.target_update_rate != 0
                 and (self.episodes == "async" or self.k + 1 < self.round_len))
@@ -840,10 +860,13 @@ class VecTrainer:
                                 self._overlap_wait = self._astream
                                 L.before_critic_step = lambda st=self._astream: (
                                     torch.cuda.current_stream(self.device).wait_stream(st))
-                            self._pre(True)
-                            self._mid(u, rollout=True)
-                            self._post(u)
-                            self._join_prio()
+                            if self.dp_inline:
+                                self._inline(u, True)
+                            else:
+                                self._pre(True)
+                                self._mid(u, rollout=True)
+                                self._post(u)
+                                self._join_prio()
                             if i == 0:
                                 # the first iteration's tensors its actor branch
                                 # still reads stay allocated through the capture

@@ -1104,6 +1104,11 @@ def main():
             res["td7_variants"] = td7_variants(env, dev, args)
         if dp_sync is not None:
             res["dp_layout"] = dp_layout(trainer)
+        if trainer is not None:
+            # the graph-replayed loop's schedule ("The training
+            # iteration's schedule"): an actor iteration and the next one per
+            # graph, the second's update beside the first's actor passes
+            res["overlapped_pairs"] = any(isinstance(k, tuple) and k[-1] == "overlap" for k in trainer.graphs)
         if ref_sched is not None:
             res["reference_schedule"] = ref_sched
         if sync_cmp is not None:

@@ -177,7 +177,7 @@ def test_rccl_inline_layout_is_bit_identical_to_the_one_gpu_graph(monkeypatch):
     from exo_amd.rollout import VecTrainer
     from exo_amd.td7 import Agent, Hyperparameters
 
-    def run(group, capture="1"):
+    def run(group, capture="1", planned=False):
         monkeypatch.setenv("EXO_FORCE_DIST", "1" if group is not None else "0")
         monkeypatch.setenv("EXO_DP_CAPTURE", capture)
         torch.manual_seed(11)
@@ -185,6 +185,8 @@ def test_rccl_inline_layout_is_bit_identical_to_the_one_gpu_graph(monkeypatch):
         ag = Agent(80, 7, 1, env_num=8, precision="bf16", n_envs=512, process_group=group, graph_safe=True,
                    buffer_size=8192, hp=Hyperparameters(target_update_rate=5))
         tr = VecTrainer(env, ag)
+        if planned:  # the overlapped pairs (r05), collectives captured inside them
+            tr.plan(14)
         for _ in range(14):
             tr.step()
         torch.cuda.synchronize()
@@ -199,14 +201,15 @@ def test_rccl_inline_layout_is_bit_identical_to_the_one_gpu_graph(monkeypatch):
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1,
                             device_id=torch.device("cuda", 0))
     try:
-        for capture, inline in (("1", True), ("0", False)):
-            tr, st = run(dist.group.WORLD, capture)
+        for capture, inline, planned in (("1", True, False), ("1", True, True), ("0", False, False)):
+            tr, st = run(dist.group.WORLD, capture, planned)
             assert tr.dp and tr.dp_inline is inline
             if inline:
-                assert all(len(parts) == 1 for parts in tr.graphs.values())
+                assert all(len(parts) == 1 for k, parts in tr.graphs.items() if k[0] != "pair")
+                assert any(k[-1] == "overlap" for k in tr.graphs) == planned
                 assert tr._refresh_graph is not None
             for i, (x, y) in enumerate(zip(ref, st)):
-                torch.testing.assert_close(y, x, rtol=0, atol=0, msg=f"tensor {i} (capture={capture})")
+                torch.testing.assert_close(y, x, rtol=0, atol=0, msg=f"tensor {i} (capture={capture}, pairs={planned})")
     finally:
         dist.destroy_process_group()
 
