@@ -1339,11 +1339,33 @@ class RefScheduleTrainer(VecTrainer):
         self._cur ^= 1
 
     # ----------------------------------------------------------- training
+    def _burst_flags(self, burst):
+        """The step's burst-prefetch flags (read the batch the previous step
+        sampled / sample the next one) and batch slot."""
+        self._train_pin = self.burst_prefetch and self._burst_i > 0
+        self._train_pout = self.burst_prefetch and self._burst_i + 1 < burst
+        if self._train_pin:
+            self._bslot ^= 1
+
+    # r05: overlapped pairs inside the update bursts too -- an actor step and
+    # the critic-only step after it as one graph, the second's passes beside
+    # the first's actor passes (VecTrainer.overlap_pairs; with burst prefetch
+    # only: the second step's batch is then sampled by the first into the
+    # other slot, and the slot it samples into itself is the first's, written
+    # after its critic step, which waits for the first's actor branch)
+    _tpair_second = False
+
     def train_step(self):
         """One Agent.train() (TD7_multi_agent.py:211-293 with the LAP sample and
         priority update, TD7_buffer_multi_agent.py:65-117) as a graph replay."""
         ag, L = self.agent, self.agent.learner
         L.training_steps += 1
+        if self._tpair_second:  # its GPU work ran with the previous step's pair graph
+            self._tpair_second = False
+            self._burst_i += 1
+            self._refresh_targets()
+            self._train_iters += 1
+            return
         update_actor = L.training_steps % ag.hp.policy_freq == 0
         L.prefetch_actor = update_actor
         self._pre_in = self._pre_out = False
@@ -1351,15 +1373,18 @@ class RefScheduleTrainer(VecTrainer):
         # the burst's position (maybe_train_and_checkpoint runs
         # timesteps_since_update steps back to back, run_round zeroes _burst_i)
         burst = int(ag.timesteps_since_update)
-        self._train_pin = self.burst_prefetch and self._burst_i > 0
-        self._train_pout = self.burst_prefetch and self._burst_i + 1 < burst
-        if self._train_pin:
-            self._bslot ^= 1
+        bslot0 = self._bslot
+        self._burst_flags(burst)
         # both policy-update parities run eagerly once before their capture
         if not self.use_graphs or self._train_iters < max(2, self.warmup_eager):
             self._eager(update_actor, rollout=False)
         elif self._key(update_actor, False) not in self.graphs:
             self._capture(update_actor, rollout=False)
+        elif self._train_pair_ok(update_actor, burst):
+            key_a = self._key(True, False)
+            self._bslot = bslot0
+            self._run_train_pair(key_a, burst)
+            self._tpair_second = True
         else:
             self._replay(update_actor, rollout=False)
         L.prefetch_actor = False
@@ -1367,6 +1392,69 @@ class RefScheduleTrainer(VecTrainer):
         self._train_pin = self._train_pout = False
         self._refresh_targets()
         self._train_iters += 1
+
+    def _train_pair_ok(self, update_actor, burst):
+        L = self.agent.learner
+        if not (self.overlap_pairs and update_actor and self.burst_prefetch and self._train_pout
+                and self._burst_i + 2 <= burst and L.fused_train and L.hp.policy_freq == 2
+                and L.training_steps % L.hp.target_update_rate != 0 and (not self.dp or self.dp_inline)):
+            return False
+        # the second step's own graph exists (its warm-up allocated what the pair reads)
+        pin2, pout2 = True, self._burst_i + 2 < burst
+        return ("train", False, pin2, pout2, 1 - self._bslot) in self.graphs
+
+    def _run_train_pair(self, key_a, burst):
+        """Steps _burst_i (actor) and _burst_i + 1 (critic only) of the burst as
+        one graph; the flags and slot of each set as train_step sets them."""
+        L = self.agent.learner
+        i0, b0 = self._burst_i, self._bslot
+
+        def half(i):  # the host state train_step sets for step i0 + i
+            self._bslot = b0
+            self._burst_i = i0
+            self._burst_flags(burst)
+            if i == 1:
+                self._burst_i = i0 + 1
+                self._burst_flags(burst)
+
+        key = ("tpair",) + key_a + (i0 + 2 < burst,)
+        g = self.graphs.get(key)
+        if g is None:
+            s = torch.cuda.Stream(device=self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            g = new_graph()
+            keep = []
+            if getattr(self, "_astream", None) is None:
+                self._astream = torch.cuda.Stream(device=self.device)
+            try:
+                with torch.cuda.stream(s):
+                    with torch.cuda.graph(g, stream=s), ForkJoinAudit(s):
+                        for i, u in enumerate((True, False)):
+                            half(i)
+                            L.prefetch_actor = u
+                            self._actor_stream = self._astream if i == 0 else None
+                            if i == 1:
+                                L.before_critic_step = lambda st=self._astream: (
+                                    torch.cuda.current_stream(self.device).wait_stream(st))
+                            if self.dp_inline:
+                                self._inline(u, False)
+                            else:
+                                self._pre(False)
+                                self._mid(u, rollout=False)
+                                self._post(u)
+                                self._join_prio()
+                            if i == 0:
+                                keep.append(L._fixed_zs)  # read by the actor branch
+                        s.wait_stream(self._astream)
+            finally:
+                self._actor_stream = None
+                L.before_critic_step = None
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            self.graphs[key] = g
+            self._pair_keep = getattr(self, "_pair_keep", []) + keep
+        g.replay()
+        half(1)  # the host state after both steps: the second's slot
+        self._burst_i = i0
 
     # -------------------------------------------------------------- round
     def save_round(self):

@@ -293,8 +293,11 @@ def test_burst_prefetch_is_bit_identical(monkeypatch):
     from exo_amd.rollout import RefScheduleTrainer
     from exo_amd.td7 import Agent
     out = []
-    for on in ("0", "1"):
+    for on, pairs in (("0", False), ("1", False), ("1", True)):
         monkeypatch.setenv("EXO_BURST_PREFETCH", on)
+        # r05: with prefetch, an actor step and the critic-only step after it
+        # run as one overlapped graph inside a burst (RefScheduleTrainer._run_train_pair)
+        monkeypatch.setattr(RefScheduleTrainer, "overlap_pairs", pairs)
         torch.manual_seed(0)
         env = VecExoskeletonEnv(64, seed=5)
         agent = Agent(80, 7, 1, learning_steps=100000, env_num=E, buffer_size=2 * BUF, precision="bf16", n_envs=64)
@@ -305,13 +308,15 @@ def test_burst_prefetch_is_bit_identical(monkeypatch):
         L = agent.learner
         out.append(([p.detach().clone() for m in (L.actor, L.critic, L.encoder) for p in m.parameters()],
                     agent.replay_buffer._tree.clone(), [dict(t) for t in tr.trace], tr))
-    (w0, t0, d0, tr0), (w1, t1, d1, tr1) = out
-    for a, b in zip(w0, w1):
-        torch.testing.assert_close(b, a, rtol=0, atol=0)
-    torch.testing.assert_close(t1, t0, rtol=0, atol=0)
-    assert d0 == d1
+    (w0, t0, d0, tr0), (w1, t1, d1, tr1), (w2, t2, d2, tr2) = out
+    for w, t, d in ((w1, t1, d1), (w2, t2, d2)):
+        for a, b in zip(w0, w):
+            torch.testing.assert_close(b, a, rtol=0, atol=0)
+        torch.testing.assert_close(t, t0, rtol=0, atol=0)
+        assert d0 == d
     assert any(len(k) == 5 for k in tr1.graphs if k[0] == "train")
     assert not any(len(k) == 5 for k in tr0.graphs if k[0] == "train")
+    assert any(k[0] == "tpair" for k in tr2.graphs) and not any(k[0] == "tpair" for k in tr1.graphs)
 
 
 def test_per_round_save_reloads_to_the_trainers_weights(tmp_path):
