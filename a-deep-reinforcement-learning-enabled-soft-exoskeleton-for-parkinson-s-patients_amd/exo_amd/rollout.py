@@ -261,12 +261,16 @@ class VecTrainer:
         # graph (GradSync.graph_capturable; EXO_DP_CAPTURE=0 or gloo: three
         # graphs per iteration with eager all-reduces between them)
         self.dp_inline = bool(self.dp and use_graphs and agent.sync.graph_capturable(self.device))
-        # the env step shares the GPU with the TD7 passes: packed into half the
-        # CUs (512-thread workgroups) unless the caller chose a kernel variant.
-        # Only where 'auto' runs the row-parallel kernel (N <= 16,384): above it
-        # the two-lane kernel is the fast one (65,536 envs: 106 vs 291 us)
+        # the env step beside the TD7 passes: EXO_TRAIN_STEP_SHARED=1 packs it
+        # into half the CUs (512-thread workgroups, r02: 306 vs 316 us per
+        # iteration then).  Off since r05: with the overlapped pairs the second
+        # iteration's env step is on the pair's critical chain, where the
+        # 256-thread shape's own speed wins -- 0.2493-0.2496 vs 0.2526-0.2531 ms
+        # per iteration (profiles/r05_sched/r05sh).  Only where 'auto' runs the
+        # row-parallel kernel (N <= 16,384): above it the two-lane kernel is the
+        # fast one (65,536 envs: 106 vs 291 us)
         if (shared_step and getattr(env, "step_variant", None) == "auto" and env.n <= 16384
-                and os.environ.get("EXO_TRAIN_STEP_SHARED", "1") == "1"):
+                and os.environ.get("EXO_TRAIN_STEP_SHARED", "0") == "1"):
             env.set_step_variant("rows_shared")
         self.last_actions = None
         # exploration: "gaussian" (TD7_multi_agent.py select_action) or "pink"

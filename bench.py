@@ -878,8 +878,8 @@ def main():
         kern_ms, kern_active = float(np.mean([a.elapsed_time(b) for a, b in ev])), env_steps / args.steps
     else:   # train mode: the env kernel is inside graph replays; time it separately afterwards
         # the roofline kernel: the env step's default shape alone (the shape
-        # profiles/*_env kernel stats time); the trainer runs the rows_shared
-        # shape beside the TD7 passes -- timed alone too, reported with it
+        # profiles/*_env kernel stats time); a trainer that runs another shape
+        # (EXO_TRAIN_STEP_SHARED=1: rows_shared) has it timed alone too, reported with it
         nk = min(args.kernel_timing_steps, int(Ls.min()) - 3)
         # configs[3] / [4]: one whole round of the loop's launches (every round
         # position once: the launch time varies ~5x with which stiff

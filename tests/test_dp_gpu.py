@@ -201,7 +201,6 @@ def _single_process_two_shards(iters, precision, envs=4096):
     for r in range(2):
         torch.manual_seed(7 + r)
         env = VecExoskeletonEnv(envs, seed=1000 + r)
-        env.set_step_variant("rows_shared")  # VecTrainer's shape beside the TD7 passes
         ag = Agent(80, 7, 1, env_num=8, hp=hp, precision=precision, n_envs=envs,
                    buffer_size=max(8192, iters * envs // 8))
         ag.replay_buffer._rng.fold(r)
