@@ -1608,10 +1608,9 @@ int lap_store_batch(const lap_tree_desc *t, const lap_storage_desc *st, const fl
     // training loop -- 0.2767-0.2771 vs 0.2522-0.2529 ms per iteration
     // (profiles/r05_sched/r05s2): one workgroup per stratum copying its rows is
     // slower than 1,024 copy workgroups -- so EXO_LAP_STORE_FUSED=1 opts in
-    static const bool fused_env = [] {
-        const char *v = getenv("EXO_LAP_STORE_FUSED");
-        return v && v[0] == '1';
-    }();
+    // (read per call: the parity test switches it)
+    const char *fused_var = getenv("EXO_LAP_STORE_FUSED");
+    const bool fused_env = fused_var && fused_var[0] == '1';
     if (fused_env && n <= STORE_FUSED_MAX && n <= t->capacity) {  // (no ring wrap inside one call)
         const bool vec = (st->state_dim & 3) == 0 &&
                          ((reinterpret_cast<uintptr_t>(state) | reinterpret_cast<uintptr_t>(next_state) |

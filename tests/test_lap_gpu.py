@@ -408,14 +408,17 @@ def test_store_span_propagation_keeps_the_tree_exact(C):
         np.testing.assert_array_equal(T[s, 1:cap], T[s, 2:2 * cap:2] + T[s, 3:2 * cap:2])
 
 
+@pytest.mark.parametrize("fused", ["0", "1"])
 @pytest.mark.parametrize("n,cap,steps", [(4096, 30000, 5), (1000, 2048, 9), (8192, 9000, 3)])
-def test_vectorised_insert_equals_per_row_ring_adds(n, cap, steps):
+def test_vectorised_insert_equals_per_row_ring_adds(n, cap, steps, fused, monkeypatch):
     """lap_store_batch (r05: one launch up to 8,192 rows -- scan, leaves, span
     propagation and the row copies in one workgroup per stratum) against the
     per-stratum ring semantics row by row: rows of stratum s in env order to
     slots ptr_s, ptr_s + 1, ... (mod capacity), leaves = max_priority, every
     inner node the sum of its children; random masks and strata, ring wraps
-    across calls."""
+    across calls.  fused: the opt-in one-launch insert (EXO_LAP_STORE_FUSED=1,
+    measured slower in the loop) against the same semantics."""
+    monkeypatch.setenv("EXO_LAP_STORE_FUSED", fused)
     E = 8
     lap = _lap(E, cap, 16)
     g = torch.Generator(device="cuda").manual_seed(n + cap)
