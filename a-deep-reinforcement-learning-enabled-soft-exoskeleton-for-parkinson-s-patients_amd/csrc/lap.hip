@@ -1737,6 +1737,32 @@ int lap_update_sample_rng(const lap_tree_desc *t, const lap_storage_desc *st, co
     return gather_after(t, st, batch, idx_out, out_state, out_action, out_next_state, out_reward, out_not_done, stream);
 }
 
+int lap_update_sample_idx(const lap_tree_desc *t, const lap_storage_desc *st, const int32_t *idx_in,
+                          const float *prio, int32_t batch, uint64_t seed, uint32_t tag, unsigned long long *counter,
+                          uint32_t *ticket, int32_t *idx_out, void *stream) {
+    if (!valid(t) || !st || !st->size || !idx_in || !prio || !counter || !ticket || !idx_out || batch <= 0 ||
+        batch > UPD_THREADS)
+        return EXO_EINVAL;
+    hipLaunchKernelGGL(lap_update_sample_kernel, dim3(t->n_strata), dim3(UPD_THREADS), 0, (hipStream_t)stream,
+                       t->tree, t->max_priority, t->cap, levels_of(t), t->capacity, idx_in, prio, batch, st->size,
+                       *st, SampleRng{seed, tag, counter, ticket}, idx_out, nullptr, nullptr, nullptr, nullptr,
+                       nullptr, TdPrio{nullptr, 0.f, 0.f, nullptr}, false);
+    return rc(hipGetLastError());
+}
+
+int lap_gather_rows(const lap_tree_desc *t, const lap_storage_desc *st, int32_t batch, const int32_t *idx,
+                    float *out_state, float *out_action, float *out_next_state, float *out_reward,
+                    float *out_not_done, void *stream) {
+    if (!valid(t) || !st || !st->state || !st->action || !st->next_state || !st->reward || !st->not_done || !idx ||
+        batch <= 0 || !out_state || !out_action || !out_next_state || !out_reward || !out_not_done)
+        return EXO_EINVAL;
+    const int total = t->n_strata * batch;
+    hipLaunchKernelGGL(lap_gather_kernel, dim3((total + GATHER_DRAWS - 1) / GATHER_DRAWS), dim3(256), 0,
+                       (hipStream_t)stream, *st, t->capacity, idx, batch, total, out_state, out_action,
+                       out_next_state, out_reward, out_not_done);
+    return rc(hipGetLastError());
+}
+
 int lap_update_sample_td(const lap_tree_desc *t, const lap_storage_desc *st, const int32_t *idx_in, const float *td,
                          float alpha, float min_priority, float *prio_out, int32_t batch, uint64_t seed, uint32_t tag,
                          unsigned long long *counter, uint32_t *ticket, int32_t *idx_out, float *out_state,

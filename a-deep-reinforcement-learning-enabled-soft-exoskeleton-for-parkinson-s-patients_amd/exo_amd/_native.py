@@ -156,6 +156,10 @@ EXPORTS = {
     "lap_update_sample_rng": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, ctypes.c_uint64,
                                         ctypes.c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_void_p, c_void_p, c_void_p]),
+    "lap_update_sample_idx": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, ctypes.c_uint64,
+                                        ctypes.c_uint32, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "lap_gather_rows": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                  c_void_p, c_void_p]),
     "lap_update_sample_td": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float, ctypes.c_float,
                                        c_void_p, c_int32, ctypes.c_uint64, ctypes.c_uint32, c_void_p, c_void_p,
                                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -305,18 +305,34 @@ class LAP:
     # r04); EXO_LAP_FUSED=0: the two launches
     fuse_update_sample = os.environ.get("EXO_LAP_FUSED", "1") != "0"
 
-    def update_priority_and_sample(self, priority, ind=None, slot=None):
+    def update_priority_and_sample(self, priority, ind=None, slot=None, before_gather=None):
         """update_priority(priority, ind) then sample(slot), the same values; one
         launch with the device RNG (the sampled batch in the slot's buffers,
-        self.ind = its indices)."""
+        self.ind = its indices).  before_gather (a callable, r05): two launches
+        instead -- the update and the indices, then before_gather() (the caller's
+        stream waits), then the rows gathered (lap_update_sample_idx +
+        lap_gather_rows, bit-identical)."""
         ind = self.ind if ind is None else ind
         if not (self.device_rng and self.fuse_update_sample and self.batch_size <= 1024):
             self.update_priority(priority, ind)
+            if before_gather is not None:
+                before_gather()
             return self.sample(slot)
         pr = priority.detach().to(torch.float32).reshape(-1).contiguous()
         assert pr.numel() == ind.numel()
         batch, idx = self._slot(slot)
         r = self._rng
+        if before_gather is not None:
+            nat.check(nat.lib().lap_update_sample_idx(ctypes.byref(self._desc), ctypes.byref(self._store), nat.ptr(ind),
+                                                      nat.ptr(pr), ind.shape[1], r.seed, r.tag, r.counter_ptr,
+                                                      r.ticket_ptr, nat.ptr(idx), self._stream()),
+                      "lap_update_sample_idx")
+            before_gather()
+            nat.check(nat.lib().lap_gather_rows(ctypes.byref(self._desc), ctypes.byref(self._store), ind.shape[1],
+                                                nat.ptr(idx), *[nat.ptr(t) for t in batch], self._stream()),
+                      "lap_gather_rows")
+            self.ind = idx
+            return batch
         nat.check(nat.lib().lap_update_sample_rng(ctypes.byref(self._desc), ctypes.byref(self._store), nat.ptr(ind),
                                                   nat.ptr(pr), ind.shape[1], r.seed, r.tag, r.counter_ptr,
                                                   r.ticket_ptr, nat.ptr(idx), *[nat.ptr(t) for t in batch],

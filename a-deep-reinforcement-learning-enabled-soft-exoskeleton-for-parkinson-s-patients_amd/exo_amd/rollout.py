@@ -213,6 +213,7 @@ ROLLOUT_AFTER = os.environ.get("EXO_ROLLOUT_AFTER", "")
 # EXO_PAIR_CRITIC_AFTER_SELECT=1 makes an overlapped pair's second critic pass
 # wait for that iteration's select_action: 0.2616-0.2618, off.
 TRAIN_FIRST = os.environ.get("EXO_TRAIN_FIRST", "1") == "1"
+EARLY_LAP = os.environ.get("EXO_EARLY_LAP", "1") == "1"
 PAIR_CRITIC_AFTER_SELECT = os.environ.get("EXO_PAIR_CRITIC_AFTER_SELECT", "0") == "1"
 
 
@@ -351,6 +352,9 @@ class VecTrainer:
         nobs, rew, done, info = self.env.step(act, active=self.active, out=self._outs[self._cur],
                                               obs_cur=obs if self.budget else None)
         ag.replay_buffer.add_batch(obs, act, nobs, rew, done, self.strata, self.active)
+        if self._early_on:  # the tree is current from here (see EARLY_LAP)
+            self._ins_ev = torch.cuda.Event()
+            self._ins_ev.record(torch.cuda.current_stream(self.device))
         self._advance()
         self.last_actions = act
 
@@ -441,6 +445,7 @@ class VecTrainer:
 
     def _pre(self, rollout=True):
         ag = self.agent
+        self._early_on = False
         # one GPU: the encoder's gradients and step stay on its branch, joined
         # at the end of the iteration (_join_prio)
         ag.learner.defer_side_join = ENC_STEP_BRANCH and (not self.dp or self.dp_inline)
@@ -460,6 +465,7 @@ class VecTrainer:
             self._ind = rb.ind
             self._prio = ag.learner.phase_grads(*self._batch)
             return
+        self._early_on = self._early_lap()
         if self._prefetching():
             self._batch, self._ind = rb._slot(slot)  # sampled by the previous iteration
             if self._pre_in:
@@ -528,7 +534,10 @@ class VecTrainer:
         if ag.learner.after_fixed is not None or ag.learner.after_target is not None:
             raise RuntimeError("VecTrainer: the rollout branch was not forked (no fixed / target pass in phase_grads)")
         ag.learner.before_critic = None
-        cur.wait_stream(br)
+        if self._early_on:
+            self._br_pending = br  # joined by the sample's gather / the actor passes / the iteration's end
+        else:
+            cur.wait_stream(br)
 
     # LAP.update_priority reads only the sampled indices and the new priorities
     # and writes only the sum trees, which nothing else in the iteration reads
@@ -562,9 +571,32 @@ class VecTrainer:
             self._prio_stream = torch.cuda.Stream(device=self.device)
         return self._prio_stream
 
+    # r05: in a critic-only iteration the priority update + next sample's
+    # indices wait only for this iteration's insert (the tree current: its
+    # rank launch), not for the row copies, the episode advance and the
+    # resets after it; the rows are gathered once the rollout branch has
+    # joined.  Bit-identical (lap_update_sample_idx + lap_gather_rows).  An
+    # actor iteration joins the rollout before its actor passes (select_action
+    # reads the actor they update).  EXO_EARLY_LAP=0: the whole rollout first.
+    _early_on = False
+    _br_pending = None
+    _ins_ev = None
+
+    def _early_lap(self):
+        rb = self.agent.replay_buffer
+        return (EARLY_LAP and not self.dp and self._prefetching() and not self._us_after_critic()
+                and not self._pre_out and rb.device_rng and rb.fuse_update_sample and rb.batch_size <= 1024)
+
+    def _join_rollout(self):
+        if self._br_pending is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._br_pending)
+            self._br_pending = None
+
     def _mid(self, update_actor, flat_grad=None, grad_scale=1.0, rollout=True):
         ag = self.agent
         self._mid_rollout = rollout
+        if update_actor:
+            self._join_rollout()
         if self._us_done:  # the priority update already runs on its branch (_pre)
             self._us_done = False
             ag.learner.phase_steps(flat_grad, grad_scale)
@@ -629,7 +661,12 @@ class VecTrainer:
             # this step's optimiser steps (RefScheduleTrainer.train_step)
             rb.update_priority_and_sample(self._prio, self._ind, 1 - self._bslot)
         elif self._prefetching() and self._mid_rollout:
-            rb.update_priority_and_sample(self._prio, self._ind, 1 - self._cur)
+            if self._br_pending is not None and self._ins_ev is not None:
+                torch.cuda.current_stream(self.device).wait_event(self._ins_ev)
+                rb.update_priority_and_sample(self._prio, self._ind, 1 - self._cur, before_gather=self._join_rollout)
+            else:
+                self._join_rollout()
+                rb.update_priority_and_sample(self._prio, self._ind, 1 - self._cur)
             if self._pre_out:
                 b = rb._slot(1 - self._cur)[0]
                 self.agent.learner.prefetch_targets(b[0], b[1], b[2], 1 - self._cur)
@@ -637,6 +674,7 @@ class VecTrainer:
             rb.update_priority(self._prio, self._ind)
 
     def _join_prio(self):
+        self._join_rollout()
         if getattr(self, "_pside", None) is not None:
             torch.cuda.current_stream(self.device).wait_stream(self._pside)
             self._pside = None

@@ -418,6 +418,18 @@ int lap_update_sample_rng(const lap_tree_desc *t, const lap_storage_desc *st, co
                           float *out_action, float *out_next_state, float *out_reward, float *out_not_done,
                           void *stream);
 
+/* lap_update_sample_rng in two launches (r05): the priority update and the
+ * next sample's indices (idx_out [n_strata][batch]), then the rows of those
+ * indices gathered from the storage -- so a caller can start the first once the
+ * tree is current (this step's inserts ranked) and the second once the rows
+ * are (its copies done).  Together bit-identical to lap_update_sample_rng
+ * (TD7_buffer_multi_agent.py:113-117, then :65-111). */
+int lap_update_sample_idx(const lap_tree_desc *t, const lap_storage_desc *st, const int32_t *idx_in,
+                          const float *prio, int32_t batch, uint64_t seed, uint32_t tag, unsigned long long *counter,
+                          uint32_t *ticket, int32_t *idx_out, void *stream);
+int lap_gather_rows(const lap_tree_desc *t, const lap_storage_desc *st, int32_t batch, const int32_t *idx,
+                    float *out_state, float *out_action, float *out_next_state, float *out_reward,
+                    float *out_not_done, void *stream);
 /* lap_update_sample_rng with the priorities computed in the launch from the
  * critic pass's |td| of both heads (td [B][2], B = n_strata x batch):
  * prio = max(|td0|, |td1|, min_priority)^alpha (TD7_multi_agent.py:259, the
