@@ -953,14 +953,7 @@ __global__ __launch_bounds__(UPD_THREADS) void lap_store_ref_fused_kernel(
         copy_rows<VEC>(st, state, action, next_state, reward, done, action_scale, &carry_i, &carry_slot, s, capacity,
                        0, 1, 1, lane, 64);
     const int n_act = offset;
-#if defined(LAP_PHASE_EXIT) && LAP_PHASE_EXIT == 11
-    return;
-#endif
-#if defined(LAP_PHASE_EXIT) && LAP_PHASE_EXIT == 12
-    if (false) {
-#else
     if (part == 0 && n_act > 0) {
-#endif
         __shared__ float span_buf[2 * SPAN_LDS], span_edge[2 * SPAN_LEVELS];
         __syncthreads();
         const long long last = mult_below(count0 + n_act - 1, E) - m0;  // slots ptr0 .. ptr0 + last
