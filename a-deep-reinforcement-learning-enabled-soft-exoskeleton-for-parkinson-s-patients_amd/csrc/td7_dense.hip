@@ -41,6 +41,10 @@ extern template void launch_fwd_big_p<PREC_BF16, false>(const GemmArgs &, dim3, 
 extern template void launch_fwd_big_p<PREC_F16, false>(const GemmArgs &, dim3, int, hipStream_t);
 extern template void launch_fwd_big_p<PREC_BF16, true>(const GemmArgs &, dim3, int, hipStream_t);
 extern template void launch_fwd_big_p<PREC_F16, true>(const GemmArgs &, dim3, int, hipStream_t);
+extern template void launch_fwd_xl_p<PREC_BF16, false>(const GemmArgs &, dim3, bool, hipStream_t);
+extern template void launch_fwd_xl_p<PREC_F16, false>(const GemmArgs &, dim3, bool, hipStream_t);
+extern template void launch_fwd_xl_p<PREC_BF16, true>(const GemmArgs &, dim3, bool, hipStream_t);
+extern template void launch_fwd_xl_p<PREC_F16, true>(const GemmArgs &, dim3, bool, hipStream_t);
 TD7_EXTERN(PREC_F32)
 TD7_EXTERN(PREC_BF16)
 TD7_EXTERN(PREC_F16)
@@ -147,6 +151,27 @@ int launch_fwd(const GemmArgs &a, int groups_grid, int prec, hipStream_t s, bool
         const bool lds128 = !big && !a.a16 && prec != PREC_F32 && lds_on && a.J >= 64 &&
                             ((t64 >= 256 && a.R >= 256) || (t64 >= 2048 && a.R >= 64)) && t128 >= 256;
         if (!(big && big_bm == 128 && a.b16) && !lds128) return EXO_ERANGE;
+    }
+    // 16-bit X and W at >= 256 tiles of 256 x 256 (r05): dense_fwd_xl8_kernel
+    // where K % 64 == 0, else dense_fwd_xl_kernel; EXO_FWD_XL=0 keeps
+    // dense_fwd_big_kernel, EXO_FWD_XL=1 dense_fwd_xl_kernel everywhere
+    static const int xl_v = [] {
+        const char *e = std::getenv("EXO_FWD_XL");
+        return (e && (e[0] == '0' || e[0] == '1')) ? e[0] - '0' : 2;
+    }();
+    const bool xl_on = xl_v != 0, xl_dma = xl_v == 2 && a.R % XL_BK == 0;
+    const long txl = (long)((a.I + XL_BM - 1) / XL_BM) * ((a.J + XL_BN - 1) / XL_BN) * groups_grid;
+    if (big && xl_on && a.a16 && a.b16 && txl >= 256 &&
+        (!a.c16 || (a.csj == 1 && a.csi % 8 == 0 && a.csg % 8 == 0 && ((uintptr_t)a.c16 & 15) == 0))) {
+        dim3 grid((a.J + XL_BN - 1) / XL_BN, (a.I + XL_BM - 1) / XL_BM, groups_grid);
+        if (cat) {
+            if (prec == PREC_BF16) launch_fwd_xl_p<PREC_BF16, true>(a, grid, xl_dma, s);
+            else launch_fwd_xl_p<PREC_F16, true>(a, grid, xl_dma, s);
+        } else {
+            if (prec == PREC_BF16) launch_fwd_xl_p<PREC_BF16, false>(a, grid, xl_dma, s);
+            else launch_fwd_xl_p<PREC_F16, false>(a, grid, xl_dma, s);
+        }
+        return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
     }
     if (big) {
         dim3 grid((a.J + big_bn - 1) / big_bn, (a.I + big_bm - 1) / big_bm, groups_grid);

@@ -1193,6 +1193,420 @@ __global__ __launch_bounds__(512) void dense_fwd_big_kernel(GemmArgs a) {
     }
 }
 
+// ---- forward, 256 x 256 tiles on 32x32x16 MFMAs (r05) --------------------
+// The wide configuration's inference chain (16-bit X, W and Y: the a16 / b16
+// / c16 operands of td7_dense_fwd_h) at 65,536 rows, where
+// dense_fwd_big_kernel ran at 380-520 TFLOP/s (65,536 x 1,024 x 1,024 /
+// 2,048; tools/wide_gemm_compare.py).  Two kernels:
+//  - dense_fwd_xl8_kernel (K % 64 == 0, the default): 8 waves of 128 x 64,
+//    LDS-DMA staging, below;
+//  - dense_fwd_xl_kernel (any K % 8 == 0): 4 waves each owning a 128 x 128
+//    tile as 4 x 4 accumulators (all 256 accumulator registers, one wave per
+//    SIMD), register-staged slices software pipelined into the MFMA bursts.
+// Both: slices of BK = 64 through a double-buffered LDS stage (128 KB,
+// dynamic), 16-byte chunks of a row XOR-swizzled, the output tile staged
+// through the same LDS so the 16-bit stores are whole 16-byte rows.  Lane l of
+// a 32x32x16 MFMA holds A[row l & 31][k = 8 (l >> 5) + j] and B[k = 8 (l >> 5)
+// + j][col l & 31]; C[row (r & 3) + 8 (r >> 2) + 4 (l >> 5)][col l & 31] in
+// accumulator register r.  Measured (r05, profiles/r05_xl): at 65,536 x
+// 1,024 x 1,024 dense_fwd_big_kernel 289 us per call (ops.dense, 16-bit in
+// and out), dense_fwd_xl_kernel 252, dense_fwd_xl8_kernel 194; the first
+// xl cut (no software pipelining) 269, xl8 with a 4-stage ring of 32-deep
+// halves 203, s_setprio around the MFMA bursts +-0 -- not kept.
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+constexpr int XL_BM = 256, XL_BN = 256, XL_BK = 64, XL_CH = XL_BK / 8;
+constexpr int XL_LDS = 2 * (XL_BM + XL_BN) * XL_CH * 16;  // 128 KB
+
+template <int P>
+__device__ __forceinline__ floatx16 mfma32_k16(uint32_t4 a, uint32_t4 b, floatx16 c) {
+    if constexpr (P == PREC_F16)
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(halfx8_t, a), __builtin_bit_cast(halfx8_t, b),
+                                                      c, 0, 0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a),
+                                                       __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+}
+
+template <int EP, int P, bool CAT, bool CHF>
+__global__ __launch_bounds__(256) void dense_fwd_xl_kernel(GemmArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t4 xl_smem[];
+    constexpr int BM = XL_BM, BN = XL_BN, BK = XL_BK, CH = XL_CH;
+    uint32_t4 *const As = xl_smem, *const Bs = xl_smem + 2 * BM * CH;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w >> 1, wn = w & 1;
+    const int l31 = lane & 31, lh = lane >> 5;
+    const int3 tile = xcd_tile();
+    const int i0 = tile.y * BM, j0 = tile.x * BN, g = tile.z;
+    const int K = a.R, nk = (K + BK - 1) / BK;
+    const int lr = t >> 3, lc = t & 7;  // this thread's chunks: rows lr + 32 j, chunk column lc
+    const int wsw = lr * CH + (lc ^ (lr & 7));  // its LDS chunk in row lr (rows lr + 32 j: + 32 j CH)
+    const __amdgpu_buffer_rsrc_t rb = rsrc(reinterpret_cast<const float *>(a.b16 + (long)g * a.J * a.R));
+    __amdgpu_buffer_rsrc_t ra = CAT ? rsrc(a.cat.p[0]) : rsrc(reinterpret_cast<const float *>(a.a16 + g * a.A.sg));
+    int lda = CAT ? a.cat.ld[0] : (int)a.A.si, kbase = 0, seg = 0;
+    uint32_t4 xa[8], xb[8];
+    auto gseg = [&](int kt) {
+        if constexpr (CAT) {  // the slice's segment (boundaries are multiples of BK)
+            const int s = cat_seg(a.cat, kt * BK);
+            if (s != seg || kt == 0) {
+                seg = s;
+                const float *p = a.cat.p[0];
+                long gs = a.cat.sg[0];
+                int ld = a.cat.ld[0], kb = 0;
+#pragma unroll
+                for (int m = 1; m < CAT_MAX; ++m)
+                    if (s == m) p = a.cat.p[m], gs = a.cat.sg[m], ld = a.cat.ld[m], kb = a.cat.kb[m];
+                ra = rsrc(reinterpret_cast<const float *>(reinterpret_cast<const uint16_t *>(p) + g * gs));
+                lda = ld;
+                kbase = kb;
+            }
+        }
+    };
+    // chunk j of slice kt (past the last slice: zeros, no access)
+    auto ga = [&](int kt, int j) {
+        const int k = kt * BK + 8 * lc, row = i0 + lr + 32 * j;
+        xa[j] = __builtin_amdgcn_raw_buffer_load_b128(ra, (k < K && row < a.I) ? (row * lda + k - kbase) * 2 : BUF_OOB,
+                                                      0, 0);
+    };
+    auto gb = [&](int kt, int j) {
+        const int k = kt * BK + 8 * lc, col = j0 + lr + 32 * j;
+        xb[j] = __builtin_amdgcn_raw_buffer_load_b128(rb, (k < K && col < a.J) ? (col * a.R + k) * 2 : BUF_OOB, 0, 0);
+    };
+    auto gload = [&](int kt) {
+        gseg(kt);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ga(kt, j);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) gb(kt, j);
+    };
+    auto lwrite = [&](int buf) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            As[buf * BM * CH + wsw + 32 * j * CH] = xa[j];
+            Bs[buf * BN * CH + wsw + 32 * j * CH] = xb[j];
+        }
+    };
+    floatx16 acc[4][4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[x][y][e] = 0.f;
+    // this lane's fragments of k-step ks (16 columns) of an LDS slice
+    auto frag = [&](const uint32_t4 *A, const uint32_t4 *B, int ks, uint32_t4 (&af)[4], uint32_t4 (&bf)[4]) {
+        const int ch = 2 * ks + lh;
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+            const int r = wm * 128 + 32 * x + l31;
+            af[x] = A[r * CH + (ch ^ (r & 7))];
+        }
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+            const int r = wn * 128 + 32 * y + l31;
+            bf[y] = B[r * CH + (ch ^ (r & 7))];
+        }
+    };
+    auto mma = [&](const uint32_t4 (&af)[4], const uint32_t4 (&bf)[4]) {
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+            for (int y = 0; y < 4; ++y) acc[x][y] = mfma32_k16<P>(af[x], bf[y], acc[x][y]);
+    };
+    gload(0);
+    lwrite(0);
+    if (nk > 1) gload(1);
+    __syncthreads();
+    // software pipelined: k-step ks + 1's fragments are read while ks's 16
+    // MFMAs run, and the next slice's chunks (loaded a slice earlier) go
+    // to the other LDS buffer between them, each register reloaded with
+    // slice kt + 2 as soon as it is written -- branch-free (past the last
+    // slice the loads return zeros and the writes land in the idle
+    // buffer), so the schedule hints below see the whole slice
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1, nxt = cur ^ 1;
+        const uint32_t4 *A = As + cur * BM * CH, *B = Bs + cur * BN * CH;
+        uint32_t4 *An = As + nxt * BM * CH + wsw, *Bn = Bs + nxt * BN * CH + wsw;
+        gseg(kt + 2);
+        uint32_t4 f[2][2][4];
+        frag(A, B, 0, f[0][0], f[0][1]);
+#pragma unroll
+        for (int ks = 0; ks < BK / 16; ++ks) {
+            if (ks + 1 < BK / 16) frag(A, B, ks + 1, f[(ks + 1) & 1][0], f[(ks + 1) & 1][1]);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int j = 2 * ks + h;
+                An[32 * j * CH] = xa[j];
+                Bn[32 * j * CH] = xb[j];
+                ga(kt + 2, j);
+                gb(kt + 2, j);
+            }
+            mma(f[ks & 1][0], f[ks & 1][1]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // LDS read
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // LDS write
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // global load
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            }
+        }
+        __syncthreads();
+    }
+    // epilogue: bias + activation
+    if constexpr (CHF) {
+        // the 256 x 256 tile of 16-bit values through the LDS stage ([row][256],
+        // 512-byte rows), then whole 16-byte chunks out
+        uint16_t *Cs = reinterpret_cast<uint16_t *>(xl_smem);
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+            const int cl = wn * 128 + 32 * y + l31, col = j0 + cl;
+            const float bv = (a.bias && col < a.J) ? a.bias[g * a.bsg + col] : 0.f;
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int rl = wm * 128 + 32 * x + (e & 3) + 8 * (e >> 2) + 4 * lh;
+                    Cs[rl * BN + cl] = to_half_bits<P>(act_fwd_t<EP>(acc[x][y][e] + bv));
+                }
+        }
+        __syncthreads();
+        const uint32_t4 *C4 = reinterpret_cast<const uint32_t4 *>(Cs);
+        for (int q = t; q < BM * (BN / 8); q += 256) {
+            const int rl = q / (BN / 8), cc = q - rl * (BN / 8);
+            const int row = i0 + rl, col = j0 + 8 * cc;
+            if (row >= a.I || col >= a.J) continue;
+            const long at = g * a.csg + (long)row * a.csi + col;  // (csj == 1: rows contiguous)
+            if (col + 8 <= a.J) {
+                *reinterpret_cast<uint32_t4 *>(a.c16 + at) = C4[q];
+            } else {
+                for (int e = 0; e < a.J - col; ++e) a.c16[at + e] = Cs[rl * BN + 8 * cc + e];
+            }
+        }
+    } else {
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+            const int col = j0 + wn * 128 + 32 * y + l31;
+            if (col >= a.J) continue;
+            const float bv = a.bias ? a.bias[g * a.bsg + col] : 0.f;
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int row = i0 + wm * 128 + 32 * x + (e & 3) + 8 * (e >> 2) + 4 * lh;
+                    if (row < a.I) a.C[g * a.csg + (long)row * a.csi + (long)col * a.csj] = act_fwd_t<EP>(acc[x][y][e] + bv);
+                }
+        }
+    }
+}
+
+// bias + activation of the 8 waves' 128 x 64 accumulators (4 x 2 of 32x32);
+// a 16-bit output through the LDS stage as whole 16-byte rows (the stage
+// must be idle: every wave past its last fragment read, no DMA in flight)
+template <int EP, int P, bool CHF>
+__device__ __forceinline__ void xl8_epilogue(const GemmArgs &a, floatx16 (&acc)[4][2], int i0, int j0, int g) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t4 xl_smem[];
+    constexpr int BM = XL_BM, BN = XL_BN;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w >> 2, wn = w & 3;
+    const int l31 = lane & 31, lh = lane >> 5;
+    if constexpr (CHF) {
+        uint16_t *Cs = reinterpret_cast<uint16_t *>(xl_smem);
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+            const int cl = wn * 64 + 32 * y + l31, col = j0 + cl;
+            const float bv = (a.bias && col < a.J) ? a.bias[g * a.bsg + col] : 0.f;
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int rl = wm * 128 + 32 * x + (e & 3) + 8 * (e >> 2) + 4 * lh;
+                    Cs[rl * BN + cl] = to_half_bits<P>(act_fwd_t<EP>(acc[x][y][e] + bv));
+                }
+        }
+        __syncthreads();
+        const uint32_t4 *C4 = reinterpret_cast<const uint32_t4 *>(Cs);
+        for (int q = t; q < BM * (BN / 8); q += 512) {
+            const int rl = q / (BN / 8), cc = q - rl * (BN / 8);
+            const int row = i0 + rl, col = j0 + 8 * cc;
+            if (row >= a.I || col >= a.J) continue;
+            const long at = g * a.csg + (long)row * a.csi + col;  // (csj == 1: rows contiguous)
+            if (col + 8 <= a.J) {
+                *reinterpret_cast<uint32_t4 *>(a.c16 + at) = C4[q];
+            } else {
+                for (int e = 0; e < a.J - col; ++e) a.c16[at + e] = Cs[rl * BN + 8 * cc + e];
+            }
+        }
+    } else {
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+            const int col = j0 + wn * 64 + 32 * y + l31;
+            if (col >= a.J) continue;
+            const float bv = a.bias ? a.bias[g * a.bsg + col] : 0.f;
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int row = i0 + wm * 128 + 32 * x + (e & 3) + 8 * (e >> 2) + 4 * lh;
+                    if (row < a.I) a.C[g * a.csg + (long)row * a.csi + (long)col * a.csj] = act_fwd_t<EP>(acc[x][y][e] + bv);
+                }
+        }
+    }
+}
+
+// The same 256 x 256 tile with 8 waves (2 per SIMD: one wave's LDS reads
+// hide behind the other's MFMAs) of 128 x 64 each (4 x 2 accumulators of
+// 32x32x16, 128 accumulator registers), and LDS-DMA staging: every slice
+// goes global -> LDS by buffer_load ... lds (no VGPR round trip, no
+// ds_write pass), 8 pieces of 8 rows x 128 B per wave and slice.  A piece's
+// LDS image is lane-linear, so the XOR swizzle of dense_fwd_xl_kernel is
+// applied on the SOURCE side (lane l of a piece loads chunk (l & 7) ^ (row &
+// 7) into slot l & 7); the fragment reads are the same.  Two LDS buffers:
+// slice kt + 1 is in flight while slice kt is multiplied; the barrier at the
+// end of a slice waits for it (the only vmcnt(0) of the loop).
+template <int EP, int P, bool CAT, bool CHF>
+__global__ __launch_bounds__(512) void dense_fwd_xl8_kernel(GemmArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t4 xl_smem[];
+    constexpr int BM = XL_BM, BN = XL_BN, BK = XL_BK, CH = XL_CH;
+    uint32_t4 *const As = xl_smem, *const Bs = xl_smem + 2 * BM * CH;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w >> 2, wn = w & 3;
+    const int l31 = lane & 31, lh = lane >> 5;
+    const int3 tile = xcd_tile();
+    const int i0 = tile.y * BM, j0 = tile.x * BN, g = tile.z;
+    const int K = a.R, nk = (K + BK - 1) / BK;
+    // this lane's piece geometry: row 8 p + pr of the tile; its slot lane & 7
+    // holds chunk (lane & 7) ^ (((8 p + pr) >> 1) & 7) = (lane & 7) ^ (4 (p & 1) +
+    // (pr >> 1)) -- rows of one parity get 8 distinct slots, so the 16 lanes of
+    // a fragment read's pass (16 consecutive rows, one chunk) hit 16 distinct
+    // 16-byte bank groups (a (r & 7) swizzle pairs rows r and r + 8: 2-way)
+    const int pr = lane >> 3;
+    auto pcol = [&](int p) { return (lane & 7) ^ (((p & 1) << 2) | (pr >> 1)); };
+    const __amdgpu_buffer_rsrc_t rb = rsrc(reinterpret_cast<const float *>(a.b16 + (long)g * a.J * a.R));
+    __amdgpu_buffer_rsrc_t ra = CAT ? rsrc(a.cat.p[0]) : rsrc(reinterpret_cast<const float *>(a.a16 + g * a.A.sg));
+    int lda = CAT ? a.cat.ld[0] : (int)a.A.si, kbase = 0, seg = 0;
+    auto gseg = [&](int kt) {
+        if constexpr (CAT) {  // the slice's segment (boundaries are multiples of BK)
+            const int s = cat_seg(a.cat, kt * BK);
+            if (s != seg || kt == 0) {
+                seg = s;
+                const float *p = a.cat.p[0];
+                long gs = a.cat.sg[0];
+                int ld = a.cat.ld[0], kb = 0;
+#pragma unroll
+                for (int m = 1; m < CAT_MAX; ++m)
+                    if (s == m) p = a.cat.p[m], gs = a.cat.sg[m], ld = a.cat.ld[m], kb = a.cat.kb[m];
+                ra = rsrc(reinterpret_cast<const float *>(reinterpret_cast<const uint16_t *>(p) + g * gs));
+                lda = ld;
+                kbase = kb;
+            }
+        }
+    };
+    // slice kt into LDS buffer buf: this wave's pieces p = 4 w + i of A and B.
+    // K % 64 == 0 (the launcher's condition), so every chunk is inside K; a
+    // row past I or a column past J starts at BUF_OOB (unsigned offsets: the
+    // load returns zeros), no per-load select
+    uint32_t brow[4], bcol[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = 8 * (4 * w + i) + pr;
+        bcol[i] = j0 + r < a.J ? (uint32_t)((j0 + r) * a.R + 8 * pcol(4 * w + i)) * 2u : (uint32_t)BUF_OOB;
+    }
+    auto rows = [&]() {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = 8 * (4 * w + i) + pr;
+            brow[i] = i0 + r < a.I ? (uint32_t)((i0 + r) * lda + 8 * pcol(4 * w + i) - kbase) * 2u : (uint32_t)BUF_OOB;
+        }
+    };
+    rows();
+    auto issue = [&](int kt, int buf) {
+        if constexpr (CAT) {
+            const int s0 = seg;
+            gseg(kt);
+            if (seg != s0) rows();
+        }
+        const uint32_t kb = (uint32_t)kt * BK * 2u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int p = 4 * w + i;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                ra, (__attribute__((address_space(3))) void *)(As + buf * BM * CH + p * 64), 16, brow[i] + kb, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rb, (__attribute__((address_space(3))) void *)(Bs + buf * BN * CH + p * 64), 16, bcol[i] + kb, 0, 0, 0);
+        }
+    };
+    floatx16 acc[4][2];
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[x][y][e] = 0.f;
+    auto frag = [&](const uint32_t4 *A, const uint32_t4 *B, int ks, uint32_t4 (&af)[4], uint32_t4 (&bf)[2]) {
+        const int ch = 2 * ks + lh;
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+            const int r = wm * 128 + 32 * x + l31;
+            af[x] = A[r * CH + (ch ^ ((r >> 1) & 7))];
+        }
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+            const int r = wn * 64 + 32 * y + l31;
+            bf[y] = B[r * CH + (ch ^ ((r >> 1) & 7))];
+        }
+    };
+    if constexpr (CAT) gseg(0), rows();
+    issue(0, 0);
+    // the LDS-DMA's completion is this wave's vmcnt; __syncthreads() alone
+    // does not wait for it
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < nk) issue(kt + 1, cur ^ 1);
+        const uint32_t4 *A = As + cur * BM * CH, *B = Bs + cur * BN * CH;
+        uint32_t4 fa[2][4], fb[2][2];
+        frag(A, B, 0, fa[0], fb[0]);
+#pragma unroll
+        for (int ks = 0; ks < BK / 16; ++ks) {
+            if (ks + 1 < BK / 16) frag(A, B, ks + 1, fa[(ks + 1) & 1], fb[(ks + 1) & 1]);
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int y = 0; y < 2; ++y) acc[x][y] = mfma32_k16<P>(fa[ks & 1][x], fb[ks & 1][y], acc[x][y]);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    xl8_epilogue<EP, P, CHF>(a, acc, i0, j0, g);
+}
+
+template <int EP, int P, bool CAT, bool CHF>
+void launch_fwd_xl_one(const GemmArgs &a, dim3 grid, bool dma, hipStream_t s) {
+    if (dma) {
+        (void)hipFuncSetAttribute((const void *)dense_fwd_xl8_kernel<EP, P, CAT, CHF>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, XL_LDS);
+        hipLaunchKernelGGL((dense_fwd_xl8_kernel<EP, P, CAT, CHF>), grid, dim3(512), XL_LDS, s, a);
+    } else {
+        (void)hipFuncSetAttribute((const void *)dense_fwd_xl_kernel<EP, P, CAT, CHF>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, XL_LDS);
+        hipLaunchKernelGGL((dense_fwd_xl_kernel<EP, P, CAT, CHF>), grid, dim3(256), XL_LDS, s, a);
+    }
+}
+
+// dma: dense_fwd_xl8_kernel (K % 64 == 0), else dense_fwd_xl_kernel
+template <int P, bool CAT>
+void launch_fwd_xl_p(const GemmArgs &a, dim3 grid, bool dma, hipStream_t s) {
+#define FWD_XL(EPv)                                                                                                \
+    (a.c16 ? launch_fwd_xl_one<EPv, P, CAT, true>(a, grid, dma, s) : launch_fwd_xl_one<EPv, P, CAT, false>(a, grid, dma, s))
+    switch (a.act) {
+    case ACT_RELU: FWD_XL(ACT_RELU); break;
+    case ACT_ELU: FWD_XL(ACT_ELU); break;
+    case ACT_TANH: FWD_XL(ACT_TANH); break;
+    default: FWD_XL(ACT_NONE); break;
+    }
+#undef FWD_XL
+}
+
 template <int P, bool CAT>
 void launch_fwd_big_p(const GemmArgs &a, dim3 grid, int bm, hipStream_t s) {
 #define FWD_BIG(EPv)                                                                                               \

@@ -49,6 +49,17 @@ def test_two_rank_training_keeps_replicas_in_sync():
     assert res["value"] > 0
 
 
+def _failure_text(out):
+    """A failed child's story: the error lines of its stderr (a watchdog's
+    stack trace otherwise buries the message), its stdout tail and the tail
+    of stderr."""
+    err = out.stderr.splitlines()
+    keys = ("Error", "error", "HIP", "NCCL", "RCCL", "Timeout", "timed out", "Traceback")
+    lines = [l for l in err if any(k in l for k in keys) and "frame #" not in l]
+    return ("\n".join(lines[:40]) + "\n--- stdout tail ---\n" + out.stdout[-1500:]
+            + "\n--- stderr tail ---\n" + out.stderr[-1500:])
+
+
 def test_rccl_data_parallel_layout_at_world_one():
     """The RCCL branch the multi-GPU runs take, on a one-GPU box: torchrun with
     one rank and EXO_FORCE_DIST=1 -- bench.py initialises the nccl (RCCL)
@@ -64,7 +75,7 @@ def test_rccl_data_parallel_layout_at_world_one():
            "--steps", "20", "--warmup", "8", "--envs", "512", "--no-cpu-baseline", "--no-td7-variants",
            "--no-reference-schedule", "--kernel-timing-steps", "5"]
     out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=REPO)
-    assert out.returncode == 0, out.stderr[-4000:]
+    assert out.returncode == 0, _failure_text(out)
     res = json.loads([l for l in out.stdout.splitlines() if l.startswith('{"metric')][-1])
     assert res["n_gpus"] == 1
     assert "DP all-reduce" in res["config"]["parallelism"]

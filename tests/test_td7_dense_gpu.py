@@ -534,3 +534,42 @@ def test_inference_chain_with_16bit_activations_is_bit_identical(prec):
     half = torch.bfloat16 if prec == "bf16" else torch.float16
     assert zsh.dtype == half and torch.equal(zsh, zs32.to(half))
     assert ah.dtype == torch.float32 and torch.equal(ah, a32)
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+@pytest.mark.parametrize("m,n,k,cat,half_out", [(16384, 1024, 1024, False, True), (16500, 1000, 1024, False, True),
+                                                (16384, 1024, 1024, False, False), (16384, 1024, 1032, False, True),
+                                                (16400, 1024, 1024, True, True), (16384, 520, 2048, False, True)])
+def test_xl_forward_kernel_is_the_gemm_of_rounded_operands(prec, m, n, k, cat, half_out):
+    """The 256 x 256-tile forward of 16-bit inference chains (r05:
+    dense_fwd_xl8_kernel, LDS-DMA staging, at >= 256 such tiles and K % 64 ==
+    0; dense_fwd_xl_kernel otherwise -- K = 1,032 here): 16-bit X (and
+    16-bit [a | zs] segments), ragged M and N (16,500 x 1,000: partial tiles
+    both ways), 16-bit or fp32 output -- the GEMM of the rounded operands with
+    fp32 accumulation + ELU, to fp32 summation-order tolerance (1e-4; the
+    16-bit output to one rounding of it).  Unlike the 256 x 128 kernel it is
+    not bit-identical to the fp32-activation chain (32x32x16 MFMAs sum in
+    another order)."""
+    from exo_amd import ops
+    torch.manual_seed(m + n + k)
+    dt = _ROUND[prec]
+    w = torch.randn(n, k, device="cuda") / k ** 0.5
+    b = torch.randn(n, device="cuda")
+    if cat:
+        parts = [torch.randn(m, 256, device="cuda").to(dt), torch.randn(m, k - 256, device="cuda").to(dt)]
+        with ops.matrix_precision(prec), torch.no_grad():
+            y = ops.dense_cat(parts, w, b, 2, half_out=half_out)
+        x = torch.cat(parts, -1)
+    else:
+        x = torch.randn(m, k, device="cuda").to(dt)
+        with ops.matrix_precision(prec), torch.no_grad():
+            y = ops.dense(x, w, b, 2, half_out=half_out)
+    assert y.dtype == (dt if half_out else torch.float32)
+    ref = torch.nn.functional.elu(x.float() @ w.to(dt).float().t() + b)
+    if half_out:
+        # within one 16-bit rounding of the fp32 result
+        ulp = 2.0 ** -8 if prec == "bf16" else 2.0 ** -11
+        excess = (y.float() - ref).abs() - ulp * ref.abs()
+        assert float(excess.max()) <= 1e-4, float(excess.max())
+    else:
+        torch.testing.assert_close(y, ref, rtol=1e-4, atol=1e-4)
