@@ -880,7 +880,7 @@ def main():
         # the roofline kernel: the env step's default shape alone (the shape
         # profiles/*_env kernel stats time); a trainer that runs another shape
         # (EXO_TRAIN_STEP_SHARED=1: rows_shared) has it timed alone too, reported with it
-        nk = min(args.kernel_timing_steps, int(Ls.min()) - 3)
+        nk = max(1, min(args.kernel_timing_steps, int(Ls.min()) - 3))  # (>= 1 launch: a rate needs one)
         # configs[3] / [4]: one whole round of the loop's launches (every round
         # position once: the launch time varies ~5x with which stiff
         # domain-randomised envs are still running, profiles/r03_dr)
