@@ -41,6 +41,8 @@ extern template void launch_fwd_big_p<PREC_BF16, false>(const GemmArgs &, dim3, 
 extern template void launch_fwd_big_p<PREC_F16, false>(const GemmArgs &, dim3, int, hipStream_t);
 extern template void launch_fwd_big_p<PREC_BF16, true>(const GemmArgs &, dim3, int, hipStream_t);
 extern template void launch_fwd_big_p<PREC_F16, true>(const GemmArgs &, dim3, int, hipStream_t);
+extern template void launch_fwd_p<PREC_BF16, false, true>(const GemmArgs &, dim3, int, int, int, int, hipStream_t);
+extern template void launch_fwd_p<PREC_F16, false, true>(const GemmArgs &, dim3, int, int, int, int, hipStream_t);
 extern template void launch_fwd_xl_p<PREC_BF16, false>(const GemmArgs &, dim3, bool, hipStream_t);
 extern template void launch_fwd_xl_p<PREC_F16, false>(const GemmArgs &, dim3, bool, hipStream_t);
 extern template void launch_fwd_xl_p<PREC_BF16, true>(const GemmArgs &, dim3, bool, hipStream_t);
@@ -145,11 +147,18 @@ int launch_fwd(const GemmArgs &a, int groups_grid, int prec, hipStream_t s, bool
     // 16-bit weights, or a 16-bit output of the 128 x 128 LDS kernel (fp32 X:
     // the K = 80 first layers); anything else is the caller's fp32 fallback
     if (cat && a.a16 && !a.c16) return EXO_ERANGE;  // 16-bit segments: the CHF variant only
-    if (a.a16 || a.c16) {
-        const long t64 = (long)((a.I + 63) / 64) * ((a.J + 63) / 64) * groups_grid;
+    // 16-bit X into a layer the fp32 path gives dense_fwd_kernel (neither the
+    // big nor the LDS-tiled kernel; e.g. the actor's 7-wide tanh head after a
+    // 16-bit l2): its AH variant, the same operands and order (r05)
+    const long t64x = (long)((a.I + 63) / 64) * ((a.J + 63) / 64) * groups_grid;
+    const bool lds_would = prec != PREC_F32 && lds_on && a.J >= 64 &&
+                           ((t64x >= 256 && a.R >= 256) || (t64x >= 2048 && a.R >= 64));
+    const bool small_h = a.a16 && !a.c16 && !cat && prec != PREC_F32 && !big && !lds_would &&
+                         a.A.si % 4 == 0 && a.A.sg % 4 == 0 && ((uintptr_t)a.a16 & 7) == 0;
+    if ((a.a16 || a.c16) && !small_h) {
         const long t128 = (long)((a.I + 127) / 128) * ((a.J + 127) / 128) * groups_grid;
         const bool lds128 = !big && !a.a16 && prec != PREC_F32 && lds_on && a.J >= 64 &&
-                            ((t64 >= 256 && a.R >= 256) || (t64 >= 2048 && a.R >= 64)) && t128 >= 256;
+                            ((t64x >= 256 && a.R >= 256) || (t64x >= 2048 && a.R >= 64)) && t128 >= 256;
         if (!(big && big_bm == 128 && a.b16) && !lds128) return EXO_ERANGE;
     }
     // 16-bit X and W at >= 256 tiles of 256 x 256 (r05): dense_fwd_xl8_kernel
@@ -221,6 +230,9 @@ int launch_fwd(const GemmArgs &a, int groups_grid, int prec, hipStream_t s, bool
         if (prec == PREC_BF16) launch_fwd_p<PREC_BF16, true>(a, grid, tm, tn, kw, wsteps, s);
         else if (prec == PREC_F16) launch_fwd_p<PREC_F16, true>(a, grid, tm, tn, kw, wsteps, s);
         else launch_fwd_p<PREC_F32, true>(a, grid, tm, tn, kw, wsteps, s);
+    } else if (small_h) {
+        if (prec == PREC_BF16) launch_fwd_p<PREC_BF16, false, true>(a, grid, tm, tn, kw, wsteps, s);
+        else launch_fwd_p<PREC_F16, false, true>(a, grid, tm, tn, kw, wsteps, s);
     } else {
         if (prec == PREC_BF16) launch_fwd_p<PREC_BF16, false>(a, grid, tm, tn, kw, wsteps, s);
         else if (prec == PREC_F16) launch_fwd_p<PREC_F16, false>(a, grid, tm, tn, kw, wsteps, s);

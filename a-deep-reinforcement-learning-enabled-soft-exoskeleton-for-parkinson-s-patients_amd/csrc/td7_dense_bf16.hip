@@ -7,6 +7,7 @@ template void launch_wgrad_p<PREC_BF16, false>(const WgradArgs &, dim3, int, int
 template void launch_fwd_p<PREC_BF16, false>(const GemmArgs &, dim3, int, int, int, int, hipStream_t);
 template void launch_wgrad_p<PREC_BF16, true>(const WgradArgs &, dim3, int, int, int, hipStream_t);
 template void launch_fwd_p<PREC_BF16, true>(const GemmArgs &, dim3, int, int, int, int, hipStream_t);
+template void launch_fwd_p<PREC_BF16, false, true>(const GemmArgs &, dim3, int, int, int, int, hipStream_t);
 template void launch_fwd_norm_p<PREC_BF16, false>(const GemmArgs &, dim3, float *, float *, float, hipStream_t);
 template void launch_fwd_norm_p<PREC_BF16, true>(const GemmArgs &, dim3, float *, float *, float, hipStream_t);
 template void launch_fwd_lds_p<PREC_BF16, false>(const GemmArgs &, dim3, int, hipStream_t);

@@ -433,16 +433,27 @@ void launch_gemm_p(const GemmArgs &a, dim3 grid, int nw, hipStream_t s) {
 // trips instead of one per step; the tail (K % 16) is a range-checked step.
 // (2x2 waves per workgroup sharing X / W rows through L1 measured slower than
 // one wave per workgroup with this remap.)
-template <int EP, int GS, int TM, int TN, int KW, int P, bool CAT>
+// 16-bit X element (the a16 operand) as the float it equals
+template <int P>
+__device__ __forceinline__ uint32_t half_bits_to_float_bits(uint32_t h) {
+    if constexpr (P == PREC_F16) return __float_as_uint((float)__builtin_bit_cast(_Float16, (uint16_t)h));
+    else return h << 16;
+}
+
+template <int EP, int GS, int TM, int TN, int KW, int P, bool CAT, bool AH = false>
 __global__ __launch_bounds__(64 * KW) void dense_fwd_kernel(GemmArgs a) {
     // a (16 TM) x (16 TN) tile per workgroup; per 16-wide step TM + TN b128
     // loads feed 4 TM TN MFMAs.  KW waves split the reduction (halves, summed
-    // through LDS at the end).
+    // through LDS at the end).  AH (r05): X is the 16-bit a16 operand (an
+    // inference chain's 16-bit activations), 8-byte loads of the same 4
+    // values the fp32 path rounds to -- the same MFMA operands in the same
+    // order, bit-identical output.
     constexpr bool SPLIT = TM * TN == 1; // 1x1: two accumulators break the MFMA dependency chain
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
     const int3 tile = xcd_tile();
     const int i0 = tile.y * 16 * TM, j0 = tile.x * 16 * TN, g = tile.z;
-    const __amdgpu_buffer_rsrc_t ra = rsrc(a.A.p), rb = rsrc(a.B.p);
+    const __amdgpu_buffer_rsrc_t ra = AH ? rsrc(reinterpret_cast<const float *>(a.a16)) : rsrc(a.A.p),
+                                 rb = rsrc(a.B.p);
     int abase[TM], bbase[TN];
     bool arow[TM], bcol[TN];
     int arowi[TM];
@@ -502,6 +513,11 @@ __global__ __launch_bounds__(64 * KW) void dense_fwd_kernel(GemmArgs a) {
                     const auto v = ld_cat(x, r, live & arow[x]);
 #pragma unroll
                     for (int jj = 0; jj < 4; ++jj) av[s][x][jj] = v[jj];
+                } else if constexpr (AH) {
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b64(ra, (live & arow[x]) ? (abase[x] + r) * 2 : BUF_OOB, 0, 0);
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj)
+                        av[s][x][jj] = half_bits_to_float_bits<P>((v[jj >> 1] >> (16 * (jj & 1))) & 0xffffu);
                 } else {
                     const auto v = __builtin_amdgcn_raw_buffer_load_b128(ra, (live & arow[x]) ? (abase[x] + r) * 4 : BUF_OOB, 0, 0);
 #pragma unroll
@@ -576,6 +592,10 @@ __global__ __launch_bounds__(64 * KW) void dense_fwd_kernel(GemmArgs a) {
             for (int x = 0; x < TM; ++x) {
                 if constexpr (CAT) { // the chunk r .. r+3 lies in one segment
                     xa[x][jj] = (arow[x] & (r + jj < a.R)) ? cat_ptr(arowi[x], r)[jj] : 0.f;
+                } else if constexpr (AH) {
+                    const bool ok = arow[x] & (r + jj < a.R);
+                    xa[x][jj] = __uint_as_float(half_bits_to_float_bits<P>(
+                        __builtin_amdgcn_raw_buffer_load_b16(ra, ok ? (abase[x] + r + jj) * 2 : BUF_OOB, 0, 0)));
                 } else {
                     xa[x][jj] = ldb(ra, arow[x] & (r + jj < a.R), abase[x] + r + jj);
                 }
@@ -1872,17 +1892,17 @@ void launch_wgrad_p(const WgradArgs &a, dim3 grid, int va, int nw, int act, hipS
 #undef WG_NW
 }
 
-template <int P, bool CAT>
+template <int P, bool CAT, bool AH = false>
 void launch_fwd_p(const GemmArgs &a, dim3 grid, int tm, int tn, int kw, int wsteps, hipStream_t s) {
 #define FWD_GS(EPv, TMv, TNv, KWv)                                                                              \
     do {                                                                                                      \
         const dim3 blk(64 * KWv);                                                                             \
-        if (wsteps <= 5) hipLaunchKernelGGL((dense_fwd_kernel<EPv, 5, TMv, TNv, KWv, P, CAT>), grid, blk, 0, s, a); \
+        if (wsteps <= 5) hipLaunchKernelGGL((dense_fwd_kernel<EPv, 5, TMv, TNv, KWv, P, CAT, AH>), grid, blk, 0, s, a); \
         else if (TMv * TNv == 1 && wsteps <= 20)                                                              \
-            hipLaunchKernelGGL((dense_fwd_kernel<EPv, 20, TMv, TNv, KWv, P, CAT>), grid, blk, 0, s, a);            \
+            hipLaunchKernelGGL((dense_fwd_kernel<EPv, 20, TMv, TNv, KWv, P, CAT, AH>), grid, blk, 0, s, a);        \
         else if (TMv * TNv == 1)                                                                              \
-            hipLaunchKernelGGL((dense_fwd_kernel<EPv, 10, TMv, TNv, KWv, P, CAT>), grid, blk, 0, s, a);            \
-        else hipLaunchKernelGGL((dense_fwd_kernel<EPv, 5, TMv, TNv, KWv, P, CAT>), grid, blk, 0, s, a);             \
+            hipLaunchKernelGGL((dense_fwd_kernel<EPv, 10, TMv, TNv, KWv, P, CAT, AH>), grid, blk, 0, s, a);        \
+        else hipLaunchKernelGGL((dense_fwd_kernel<EPv, 5, TMv, TNv, KWv, P, CAT, AH>), grid, blk, 0, s, a);         \
     } while (0)
 #define FWD_LAUNCH(EPv)                                                                 \
     do {                                                                                \

@@ -140,13 +140,13 @@ class Actor(nn.Module):
             a = self.activ(self.l1(a))
             a = self.activ(self.l2(a))
             return torch.tanh(self.l3(a))
-        # inference at the wide configuration's sizes: l0's norm and l1's
-        # output handed on as the 16-bit values l1 / l2 round them to
-        # (ops.dense_norm / dense half_out; zs too when the caller asked
+        # inference at the wide configuration's sizes: l0's norm, l1's and
+        # l2's outputs handed on as the 16-bit values l1 / l2 / l3 round them
+        # to (ops.dense_norm / dense half_out; zs too when the caller asked
         # Encoder.zs for it)
         a = ops.dense_norm([state], self.l0.weight, self.l0.bias, half_out=True)
         a = ops.dense_cat([a, zs], self.l1.weight, self.l1.bias, act, half_out=True)
-        a = ops.dense(a, self.l2.weight, self.l2.bias, act)
+        a = ops.dense(a, self.l2.weight, self.l2.bias, act, half_out=True)
         return ops.dense(a, self.l3.weight, self.l3.bias, ops.ACT_CODES["tanh"])
 
 

@@ -573,3 +573,26 @@ def test_xl_forward_kernel_is_the_gemm_of_rounded_operands(prec, m, n, k, cat, h
         assert float(excess.max()) <= 1e-4, float(excess.max())
     else:
         torch.testing.assert_close(y, ref, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+@pytest.mark.parametrize("m,n,k", [(8192, 7, 1024), (65536, 7, 1024), (8200, 7, 1000), (9000, 20, 260)])
+def test_small_head_reading_16bit_x_is_bit_identical(prec, m, n, k):
+    """r05: a 16-bit X into a layer the fp32 path runs on dense_fwd_kernel
+    (the actor's 7-wide tanh head l3 after a 16-bit l2 on the wide select
+    chain) takes its AH variant -- 8-byte loads of the values the fp32 path
+    rounds to: bit-identical to feeding the same values as fp32, at both
+    tilings (16 x 16 below 2,048 tiles, 32 x 32 above), K with a 16-wide
+    tail (1,000) and a 20-wide head."""
+    from exo_amd import ops
+    torch.manual_seed(m + n + k)
+    dt = _ROUND[prec]
+    x16 = torch.randn(m, k, device="cuda").to(dt)
+    w = torch.randn(n, k, device="cuda") / k ** 0.5
+    b = torch.randn(n, device="cuda")
+    with ops.matrix_precision(prec), torch.no_grad():
+        y16 = ops._dense_h(x16, w, b, ops.ACT_CODES["tanh"], False)  # the kernel itself (None = EXO_ERANGE)
+        y32 = ops.dense(x16.float(), w, b, ops.ACT_CODES["tanh"])
+        y_op = ops.dense(x16, w, b, ops.ACT_CODES["tanh"])
+    assert y16 is not None and y16.dtype == torch.float32
+    assert torch.equal(y16, y32) and torch.equal(y_op, y32)
