@@ -17,7 +17,6 @@ parameter whose gradient sits at the rounding noise can flip the sign of an
 early Adam update (a step of ~2 lr); such entries may number at most 1e-3 of
 all and move by at most 2 lr per update."""
 import os
-import socket
 import sys
 
 import numpy as np
@@ -33,11 +32,8 @@ TOL = {"fp32": (2e-5, 2e-6), "bf16": (1e-4, 1e-5)}
 
 
 def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    from _ports import free_port
+    return free_port()
 
 
 def _learner(precision, sync=None, seed=0):

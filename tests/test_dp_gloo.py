@@ -2,7 +2,6 @@
 ranks that see different halves of a batch must end bit-close to one process
 that sees the whole batch, and stay identical to each other."""
 import os
-import socket
 import sys
 
 import numpy as np
@@ -14,11 +13,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    from _ports import free_port
+    return free_port()
 
 
 def _hp():

@@ -12,7 +12,6 @@
   global max_priority."""
 import json
 import os
-import socket
 import subprocess
 import sys
 
@@ -27,11 +26,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    from _ports import free_port
+    return free_port()
 
 
 def test_two_rank_training_keeps_replicas_in_sync():
@@ -91,7 +87,7 @@ def _run_workers(tmp_path, world, mode, extra, timeout=900):
            "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(REPO, "tests", "dp_worker.py"),
            "--mode", mode, "--out", str(tmp_path)] + extra
     out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=REPO)
-    assert out.returncode == 0, out.stderr[-4000:]
+    assert out.returncode == 0, _failure_text(out)
     return [json.load(open(os.path.join(tmp_path, f"out_r{r}.json"))) for r in range(world)]
 
 
