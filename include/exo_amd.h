@@ -570,8 +570,12 @@ int td7_dense_fwd_cat_w16(int32_t nseg, const float *const *xs_dev, const long *
  * or Y (y16_dev) as 16-bit values of the MFMA operand type -- exactly what the
  * consumer rounds its operand to, so a chain is bit-identical with half the
  * activation bytes; the fp32 pointer of a 16-bit operand is null.  Only where
- * the large-layer kernel runs: EXO_ERANGE otherwise (the caller falls back to
- * fp32).  w16_dev required. */
+ * the large-layer kernels run (r05: the 256 x 256-tile kernels for 16-bit X
+ * and W at >= 256 such tiles -- summed in another order than the 128 x 256
+ * kernel the fp32 chain takes there, so within fp32 tolerance rather than
+ * bit-identical) or, for a 16-bit X with an fp32 Y, where the fp32 path takes
+ * the small-tile kernel (a narrow head: bit-identical): EXO_ERANGE otherwise
+ * (the caller falls back to fp32).  w16_dev required. */
 int td7_dense_fwd_h(const float *x_dev, const uint16_t *x16_dev, long xsg, long ldx, const float *w_dev,
                     const float *b_dev, float *y_dev, uint16_t *y16_dev, long ysg, long ldy, int32_t groups, int32_t m,
                     int32_t n, int32_t k, int32_t act, const uint16_t *w16_dev, void *stream);
