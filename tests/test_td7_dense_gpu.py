@@ -596,3 +596,29 @@ def test_small_head_reading_16bit_x_is_bit_identical(prec, m, n, k):
         y_op = ops.dense(x16, w, b, ops.ACT_CODES["tanh"])
     assert y16 is not None and y16.dtype == torch.float32
     assert torch.equal(y16, y32) and torch.equal(y_op, y32)
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_xl_forward_grouped_through_the_abi(prec):
+    """td7_dense_fwd_h with two groups (W [2, N, K], X [2, M, K], both 16-bit)
+    at the 256 x 256-tile sizes: each group's output equals that group's GEMM
+    of the rounded operands (the grid's z = group; ops never sends groups
+    here, the C ABI allows it)."""
+    from exo_amd import _native as nat
+    from exo_amd import ops
+    torch.manual_seed(11)
+    dt = _ROUND[prec]
+    G, m, n, k = 2, 16400, 1024, 1024
+    x16 = torch.randn(G, m, k, device="cuda").to(dt)
+    w = torch.randn(G, n, k, device="cuda") / k ** 0.5
+    b = torch.randn(G, n, device="cuda")
+    w16 = w.to(dt)
+    y16 = torch.empty(G, m, n, device="cuda", dtype=dt)
+    rc = nat.lib().td7_dense_fwd_h(None, nat.ptr(x16), m * k, k, nat.ptr(w), nat.ptr(b), None, nat.ptr(y16), m * n, n,
+                                   G, m, n, k, 2 | ops.PRECISIONS[prec] << 8, nat.ptr(w16),
+                                   nat.stream_ptr(x16.device))
+    assert rc == 0
+    ref = torch.nn.functional.elu(x16.float() @ w16.float().transpose(-1, -2) + b.unsqueeze(-2))
+    ulp = 2.0 ** -8 if prec == "bf16" else 2.0 ** -11
+    excess = (y16.float() - ref).abs() - ulp * ref.abs()
+    assert float(excess.max()) <= 1e-4, float(excess.max())
