@@ -1249,10 +1249,13 @@ __global__ __launch_bounds__(UPD_THREADS) void lap_ref_commit_tree_kernel(float 
                                                                           int capacity, const long long *ref,
                                                                           long long total, int E) {
     const long long ptr0 = ref[0], count0 = ref[1];
-    const long long adv = mult_below(count0 + total, E) - mult_below(count0, E);
-    if (adv <= 0) return;
+    if (total <= 0) return;
+    // the round's adds land in slots ptr0 .. ptr0 + last: the last add's slot
+    // is ptr0 + adv (not ptr0 + adv - 1) unless count0 + total - 1 is a
+    // multiple of E -- the same span as the per-step insert's (:959)
+    const long long last = mult_below(count0 + total - 1, E) - mult_below(count0, E);
     propagate_span(stratum_tree(tree, blockIdx.x, cap), cap, levels, capacity, (int)ptr0,
-                   (int)min(adv, (long long)capacity));
+                   (int)min(last + 1, (long long)capacity));
 }
 
 // the pointer and sizes after the round
@@ -1528,8 +1531,9 @@ int gather_after(const lap_tree_desc *t, const lap_storage_desc *st, int batch, 
 }
 
 bool valid(const lap_tree_desc *t) {
+    // cap <= 2^MAXLV: prefix_sum unrolls MAXLV levels
     return t && t->tree && t->max_priority && t->n_strata > 0 && t->capacity > 0 && t->cap >= t->capacity &&
-           (t->cap & (t->cap - 1)) == 0;
+           (t->cap & (t->cap - 1)) == 0 && t->cap <= (1 << MAXLV);
 }
 
 } // namespace

@@ -42,6 +42,8 @@ class LAP:
         self.normalize_actions = max_action if normalize_actions else 1
         self.prioritized = True
         E, C = self.num_envs, self.max_size
+        if C > 1 << 24:  # csrc/lap.hip prefix_sum walks at most 24 levels
+            raise ValueError(f"LAP: max_size {C} above 2^24 rows per stratum")
         f32 = dict(device=self.device, dtype=torch.float32)
         self.state = torch.zeros((E, C + 1, state_dim), **f32)
         self.action = torch.zeros((E, C + 1, action_dim), **f32)

@@ -775,7 +775,12 @@ class VecTrainer:
 
     def _capture(self, update_actor, rollout=True):
         """Capture this parity's iteration (rollout=False: a training step
-        alone); the capture itself performs one real iteration."""
+        alone), then run it (a capture records, it does not execute)."""
+        self._capture_graph(update_actor, rollout)
+        self._replay(update_actor, rollout)
+
+    def _capture_graph(self, update_actor, rollout=True):
+        """Record this parity's iteration graph(s) under its key; nothing runs."""
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         pool = None  # one private pool per parity: the two parities replay in alternation
@@ -818,8 +823,6 @@ class VecTrainer:
         self.graphs[self._key(update_actor, rollout)] = parts
         if self._graph_refresh() and self._refresh_graph is None:
             self._capture_refresh()
-        # capture records but does not execute: run the iteration now
-        self._replay(update_actor, rollout)
 
     def _replay(self, update_actor, rollout=True):
         parts = self.graphs[self._key(update_actor, rollout)]
@@ -879,54 +882,59 @@ class VecTrainer:
         iteration, then a critic-only one; see overlap_pairs): the first
         iteration's actor passes on a branch of their own that only the second
         iteration's rollout and critic step wait for."""
+        g = self.graphs.get(self._pair_key(ua, ua2, overlap))
+        if g is None:
+            g = self._capture_pair(ua, ua2, overlap)
+        g.replay()
+
+    def _capture_pair(self, ua, ua2, overlap=False):
+        """Record the pair graph of _run_pair under its key; nothing runs."""
         L = self.agent.learner
         key = self._pair_key(ua, ua2, overlap)
-        g = self.graphs.get(key)
-        if g is None:
-            s = torch.cuda.Stream(device=self.device)
-            s.wait_stream(torch.cuda.current_stream(self.device))
-            g = new_graph()
-            cur0 = self._cur
-            keep = []
-            if overlap and getattr(self, "_astream", None) is None:
-                self._astream = torch.cuda.Stream(device=self.device)
-            try:
-                with torch.cuda.stream(s):
-                    with torch.cuda.graph(g, stream=s), ForkJoinAudit(s):
-                        for i, u in enumerate((ua, ua2)):
-                            L.prefetch_actor = u
-                            if overlap and i == 0:
-                                self._actor_stream = self._astream
-                            if overlap and i == 1:
-                                self._actor_stream = None
-                                self._overlap_wait = self._astream
-                                L.before_critic_step = lambda st=self._astream: (
-                                    torch.cuda.current_stream(self.device).wait_stream(st))
-                            if self.dp_inline:
-                                self._inline(u, True)
-                            else:
-                                self._pre(True)
-                                self._mid(u, rollout=True)
-                                self._post(u)
-                                self._join_prio()
-                            if i == 0:
-                                # the first iteration's tensors its actor branch
-                                # still reads stay allocated through the capture
-                                keep.append(L._fixed_zs)
-                                self._cur ^= 1
-                                self.iters += 1  # the second half is never iteration 0
-                        if overlap:
-                            s.wait_stream(self._astream)
-            finally:
-                self._actor_stream = self._overlap_wait = None
-                L.before_critic_step = None
-            torch.cuda.current_stream(self.device).wait_stream(s)
-            self._cur = cur0
-            self.iters -= 1
-            L.prefetch_actor = ua
-            self.graphs[key] = g
-            self._pair_keep = getattr(self, "_pair_keep", []) + keep
-        g.replay()
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        g = new_graph()
+        cur0 = self._cur
+        keep = []
+        if overlap and getattr(self, "_astream", None) is None:
+            self._astream = torch.cuda.Stream(device=self.device)
+        try:
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s), ForkJoinAudit(s):
+                    for i, u in enumerate((ua, ua2)):
+                        L.prefetch_actor = u
+                        if overlap and i == 0:
+                            self._actor_stream = self._astream
+                        if overlap and i == 1:
+                            self._actor_stream = None
+                            self._overlap_wait = self._astream
+                            L.before_critic_step = lambda st=self._astream: (
+                                torch.cuda.current_stream(self.device).wait_stream(st))
+                        if self.dp_inline:
+                            self._inline(u, True)
+                        else:
+                            self._pre(True)
+                            self._mid(u, rollout=True)
+                            self._post(u)
+                            self._join_prio()
+                        if i == 0:
+                            # the first iteration's tensors its actor branch
+                            # still reads stay allocated through the capture
+                            keep.append(L._fixed_zs)
+                            self._cur ^= 1
+                            self.iters += 1  # the second half is never iteration 0
+                    if overlap:
+                        s.wait_stream(self._astream)
+        finally:
+            self._actor_stream = self._overlap_wait = None
+            L.before_critic_step = None
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        self._cur = cur0
+        self.iters -= 1
+        L.prefetch_actor = ua
+        self.graphs[key] = g
+        self._pair_keep = getattr(self, "_pair_keep", []) + keep
+        return g
 
     # ------------------------------------------------------------- step
     def next_step_resets(self):
@@ -953,6 +961,47 @@ class VecTrainer:
         overlapped pairs, on by default -- start only where at least two
         announced calls remain."""
         self._horizon = None if n is None else int(n)
+
+    def prepare(self):
+        """Record, without running them, the graphs the announced steps (plan)
+        replay: the next two iterations' graphs and, where they will run as an
+        overlapped pair, the pair graph (r06, VERDICT r5 item 2: the pair was
+        captured on first use, inside the caller's timed window).  A capture
+        records and does not execute, so the trainer's state and every tensor
+        stay as they were; only host-side capture bookkeeping is done here.
+        Needs the eager warm-up iterations done (their buffers) and no pair
+        half pending.  Returns the number of graphs recorded."""
+        L = self.agent.learner
+        if (not self.use_graphs or self.iters < self.warmup_eager or self._pair_second
+                or self.prefetch_targets):
+            return 0
+        pf = L.hp.policy_freq
+        saved = (L.training_steps, L.prefetch_actor, self._pre_in, self._pre_out, self._cur, self.iters, self.k)
+        made = 0
+        try:
+            self._pre_in = self._pre_out = False
+            for _ in range(2):  # the next two iterations alone (the pair's halves)
+                L.training_steps += 1
+                ua = L.training_steps % pf == 0
+                L.prefetch_actor = ua
+                if self._key(ua, True) not in self.graphs:
+                    self._capture_graph(ua)
+                    made += 1
+                self._cur ^= 1
+                self.iters += 1
+            L.training_steps, self._cur, self.iters = saved[0], saved[4], saved[5]
+            L.training_steps += 1
+            ua, ua2 = L.training_steps % pf == 0, (L.training_steps + 1) % pf == 0
+            if self._horizon is not None and self._horizon >= 2 and self._pair_ok():
+                overlap = self.overlap_pairs and ua and not ua2 and L.fused_train
+                if self._pair_key(ua, ua2, overlap) not in self.graphs:
+                    L.prefetch_actor = ua
+                    self._capture_pair(ua, ua2, overlap)
+                    made += 1
+        finally:
+            (L.training_steps, L.prefetch_actor, self._pre_in, self._pre_out, self._cur, self.iters,
+             self.k) = saved
+        return made
 
     def step(self):
         """One training iteration; returns the number of active env-steps (with

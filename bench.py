@@ -433,8 +433,9 @@ def sync_rounds(env, dev, args, hp, group=None, warm=40):
             dist.barrier(group)
         torch.cuda.synchronize()
 
-    sync_all()
     tr.plan(None if tr.budget else tr.round_len)  # the round's iterations (pair graphs inside)
+    tr.prepare()
+    sync_all()
     t = time.perf_counter()
     n, its = tr.step(), 1
     while not tr.next_step_resets():
@@ -597,8 +598,9 @@ def td7_variants(env, dev, args, iters=60, warmup=8):
         tr.plan(warmup)
         for _ in range(warmup):
             tr.step()
-        torch.cuda.synchronize()
         tr.plan(iters)
+        tr.prepare()
+        torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(iters):
             tr.step()
@@ -778,12 +780,13 @@ def main():
         episode ends), so exactly round_len (344) consecutive iterations, their
         in-place resets included, are timed the same way."""
         if trainer.episodes == "async":
+            trainer.plan(round_len)
+            trainer.prepare()
             torch.cuda.synchronize()
             if dist_on:
                 dist.barrier()
             torch.cuda.synchronize()
             s0 = trainer.env_steps_total() if trainer.budget else None
-            trainer.plan(round_len)
             t = time.perf_counter()
             n = 0
             for _ in range(round_len):
@@ -801,11 +804,12 @@ def main():
         trainer.plan(None)
         while not trainer.next_step_resets():
             trainer.step()
+        trainer.plan(None if trainer.budget else round_len)
+        trainer.prepare()
         torch.cuda.synchronize()
         if dist_on:
             dist.barrier()
         torch.cuda.synchronize()
-        trainer.plan(None if trainer.budget else round_len)
         t = time.perf_counter()
         n = trainer.step()  # the episode reset and the round's first iteration
         its = 1
@@ -841,6 +845,12 @@ def main():
         trainer.plan(args.warmup)
     for _ in range(args.warmup):
         one_step(False)
+    prepared = 0
+    if trainer is not None:
+        # the graphs the window replays recorded (not run) before it starts: the
+        # overlapped pair's capture landed inside a short window
+        trainer.plan(args.steps)
+        prepared = trainer.prepare()
     torch.cuda.synchronize()
     if dist_on:
         dist.barrier()
@@ -960,6 +970,7 @@ def main():
             "value": round_value,
             "unit": "env-steps/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "dist_settle_iterations": settle,
+            "graphs_prepared": prepared,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f64" if agent is None else f"f64 sim + {args.precision} TD7",

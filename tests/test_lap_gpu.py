@@ -452,3 +452,66 @@ def test_vectorised_insert_equals_per_row_ring_adds(n, cap, steps, fused, monkey
         leaves = tree[s, c2:]
         assert np.all(leaves[:size[s]] == 1.0) and np.all(leaves[size[s]:cap] == 0.0)
         assert tree[s, 1] == float(size[s])  # integer sums: exact at any order
+
+
+@pytest.mark.parametrize("E,C,n,rows,p_act", [(8, 40, 37, 9, 0.5), (8, 4096, 300, 12, 0.9), (4, 23, 11, 7, 0.15),
+                                             (8, 5000, 4096, 4, 0.97)])
+def test_planned_round_equals_per_step_reference_inserts(E, C, n, rows, p_act):
+    """lap_ref_plan + lap_ref_step per row + lap_ref_commit (the reference
+    schedule's planned rollout inserts, r05) against add_batch_ref per row (the
+    per-step inserts, pinned to the sequential adds above): storage, every tree
+    node, pointer and sizes bit for bit after every round, and every internal
+    node exactly left + right.  Rounds cover the last add landing one slot past
+    ptr0 + adv - 1 (count0 + total - 1 not a multiple of E), a
+    round with fewer adds than E, an empty round and a ring that wraps."""
+    rng = np.random.default_rng(C + n)
+    a, b = _lap(E, C, 16), _lap(E, C, 16)
+    T = lambda x: torch.as_tensor(x, device="cuda")  # noqa: E731
+    strata = T(rng.integers(0, E, n).astype(np.int32))
+    kk = torch.zeros((2,), dtype=torch.int64, device="cuda")
+    wrapped = False
+    for rnd in range(8):
+        p = [p_act, 2.0 / (n * rows), 0.0, p_act, 0.6, p_act, 1.0, 0.3][rnd]
+        table = rng.random((rows, n)) < p
+        if rnd == 1:
+            table[:] = False
+            table[rows // 2, : max(1, E // 2 - 1)] = True  # fewer adds than strata
+        if rnd == 5:  # a max_priority other than 1 for this round's leaves
+            pr = torch.full((E * 16,), 2.5 + rnd, device="cuda")
+            for lap in (a, b):
+                lap.update_priority(pr, ind=torch.zeros((E, 16), dtype=torch.int32, device="cuda"))
+        tb = T(table.astype(np.uint8))
+        counts = tb.sum(1).to(torch.int64)
+        offs, total = torch.cumsum(counts, 0) - counts, int(counts.sum())
+        plan = torch.full((rows, n), -1, dtype=torch.int32, device="cuda")
+        kk.zero_()
+        b.ref_plan(tb, strata, offs, total, plan)
+        active_b = tb[0].clone()
+        for k in range(rows):
+            st, nx = T(rng.normal(size=(n, 80)).astype(np.float32)), T(rng.normal(size=(n, 80)).astype(np.float32))
+            ac = T(rng.uniform(-1, 1, (n, 7)).astype(np.float32))
+            rw, dn = T(rng.normal(size=n).astype(np.float32)), T(rng.random(n) < 0.1)
+            a.add_batch_ref(st, ac, nx, rw, dn, strata, tb[k])
+            b.ref_step(plan, tb, kk, k % 2, st, ac, nx, rw, dn, strata, active_b)
+        b.ref_commit(plan, strata, total)
+        torch.cuda.synchronize()
+        ptr, count, _ = a.ref_pointer()
+        assert b.ref_pointer() == a.ref_pointer(), rnd
+        wrapped |= count > C
+        for name in ("state", "action", "next_state", "reward", "not_done"):
+            torch.testing.assert_close(getattr(b, name)[:, :C], getattr(a, name)[:, :C], rtol=0, atol=0,
+                                       msg=f"{name} round {rnd}")
+        torch.testing.assert_close(b._tree, a._tree, rtol=0, atol=0, msg=f"tree round {rnd}")
+        assert torch.equal(a.size_s, b.size_s)
+        tr, cap = b._tree.cpu().numpy(), b._cap
+        for s in range(E):
+            np.testing.assert_array_equal(tr[s, 1:cap], tr[s, 2:2 * cap:2] + tr[s, 3:2 * cap:2])
+    assert wrapped or C >= 4096
+
+
+def test_lap_rejects_trees_deeper_than_the_prefix_walk():
+    """prefix_sum unrolls 24 levels: a stratum capacity above 2^24 is refused
+     instead of sampling against a truncated prefix total."""
+    from exo_amd.replay import LAP
+    with pytest.raises(ValueError):
+        LAP(80, 7, "cuda", 1, max_size=(1 << 24) + 1, batch_size=4)

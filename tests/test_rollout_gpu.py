@@ -210,3 +210,51 @@ def test_pairs_never_run_past_the_announced_steps(monkeypatch):
             res.append([p.detach().clone() for p in ag.learner.critic.parameters()])
         for a, b in zip(*res):
             torch.testing.assert_close(b, a, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("episodes", ["sync", "async"])
+def test_prepare_records_the_window_graphs_without_running_them(monkeypatch, episodes):
+    """VecTrainer.prepare (r06): after the eager warm-up,
+    plan(n) + prepare() records the graphs the next n steps replay -- the two
+    single-iteration graphs and the overlapped pair -- without running them, so
+    those n steps capture nothing and the run is bit-identical to the same
+    steps without prepare (weights, observations, replay rows, sum trees)."""
+    from exo_amd import VecExoskeletonEnv
+    from exo_amd.rollout import VecTrainer
+    from exo_amd.td7 import Agent, Hyperparameters
+    monkeypatch.setenv("EXO_EPISODES", episodes)
+    res = []
+    for prep in (False, True):
+        torch.manual_seed(6)
+        hp = Hyperparameters(zs_dim=256, enc_hdim=256, critic_hdim=256, actor_hdim=256, batch_size=32)
+        env = VecExoskeletonEnv(256, seed=6)
+        ag = Agent(80, 7, 1, hp=hp, env_num=8, buffer_size=4096, graph_safe=True, precision="bf16")
+        tr = VecTrainer(env, ag)
+        tr.plan(3)
+        for _ in range(3):  # the eager warm-up iterations only
+            tr.step()
+        tr.plan(12)
+        if prep:
+            assert not tr.graphs
+            made = tr.prepare()
+            assert made == 3 and len(tr.graphs) == 3 and any(k[-1] == "overlap" for k in tr.graphs)
+            assert ag.learner.training_steps == 3 and tr.iters == 3
+            keys = set(tr.graphs)
+            assert tr.prepare() == 0
+        obs = []
+        for _ in range(12):
+            tr.step()
+            obs.append(tr.obs.clone())
+        torch.cuda.synchronize()
+        if prep:
+            assert set(tr.graphs) == keys
+        L = ag.learner
+        res.append((obs, [p.detach().clone() for m in (L.actor, L.critic, L.encoder) for p in m.parameters()],
+                    ag.replay_buffer.state.clone(), ag.replay_buffer._tree.clone()))
+    (o0, w0, r0, s0), (o1, w1, r1, s1) = res
+    for i, (a, b) in enumerate(zip(o0, o1)):
+        torch.testing.assert_close(b, a, rtol=0, atol=0, msg=f"iteration {i}")
+    for a, b in zip(w0, w1):
+        torch.testing.assert_close(b, a, rtol=0, atol=0)
+    torch.testing.assert_close(r1, r0, rtol=0, atol=0)
+    torch.testing.assert_close(s1, s0, rtol=0, atol=0)
