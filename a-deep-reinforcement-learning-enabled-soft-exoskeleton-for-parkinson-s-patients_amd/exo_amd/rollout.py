@@ -28,7 +28,7 @@ import numpy as np
 import torch
 
 from . import _native as nat
-from .graphs import new_graph
+from .graphs import capture, new_graph
 from . import td7 as _td7
 from .td7 import ENC_STEP_BRANCH
 
@@ -45,7 +45,7 @@ def graph_reductions_ok(device, rows=1024, cols=300, replays=3):
     with torch.cuda.stream(s):
         x.sum(0)
         g = new_graph()
-        with torch.cuda.graph(g, stream=s):
+        with capture(g, stream=s):
             out = x.sum(0)
     torch.cuda.current_stream(device).wait_stream(s)
     for _ in range(replays):
@@ -59,27 +59,25 @@ def graph_reductions_ok(device, rows=1024, cols=300, replays=3):
     return True
 
 
-# Graphs of finished trainers kept alive until the process ends (retire_graphs).
-_RETIRED = []
-
-
 def retire_graphs(trainer):
-    """Move a finished trainer's captured graphs to a process-wide keep-alive
-    list instead of destroying them.  Every graph exec owns up to 4 runtime
-    streams spread over the GPU_MAX_HW_QUEUES = 4 hardware queues; destroying
-    execs frees them unevenly, after which the HIP runtime (ROCm 7.0 CLR,
-    first-launch stream assignment of a graph exec) can place two of a new
-    exec's streams on the launch stream's queue, skip both and read past its
-    stream array -- the round-4 segfault in hipGraphLaunch (DESIGN.md 4,
-    "The graph-replay crash").  Call with the device idle."""
+    """Release a finished trainer's captured graphs: their execs and memory
+    pools are freed and ballast streams replace the runtime streams they held
+    (exo_amd.graphs.release_graphs; destroying execs without the ballast can
+    leave the hardware-queue loads uneven, after which the ROCm 7.0 runtime's
+    launch of a later exec reads past its stream vector -- DESIGN.md 4, "The
+    graph-replay crash").  Synchronises the device.  Returns the number of
+    graphs released."""
+    from .graphs import release_graphs
+    objs = []
     for name in ("graphs", "_round_graphs"):
         g = getattr(trainer, name, None)
         if isinstance(g, dict) and g:
-            _RETIRED.append(dict(g))
+            objs.append(dict(g))
             g.clear()
     if trainer.__dict__.get("_refresh_graph") is not None:
-        _RETIRED.append(trainer._refresh_graph)
+        objs.append(trainer._refresh_graph)
         trainer._refresh_graph = None
+    return release_graphs(*objs)
 
 
 def _np_median(x):
@@ -788,7 +786,7 @@ class VecTrainer:
         with torch.cuda.stream(s):
             if not self.dp or self.dp_inline:
                 g = new_graph()
-                with torch.cuda.graph(g, pool=pool, stream=s), ForkJoinAudit(s):
+                with capture(g, pool=pool, stream=s), ForkJoinAudit(s):
                     if self.dp_inline:
                         self._inline(update_actor, rollout)
                     else:
@@ -803,18 +801,18 @@ class VecTrainer:
                 # work on flat buckets packed/unpacked inside the graphs.
                 L, S = self.agent.learner, self.agent.sync
                 g1, g2, g3 = new_graph(), new_graph(), new_graph()
-                with torch.cuda.graph(g1, pool=pool, stream=s), ForkJoinAudit(s):
+                with capture(g1, pool=pool, stream=s), ForkJoinAudit(s):
                     self._pre(rollout)
                     flat_c = S.pack(L.grad_params())
                 pool = g1.pool()
                 flat_a = None
                 scale = 1.0 / S.world
-                with torch.cuda.graph(g2, pool=pool, stream=s), ForkJoinAudit(s):
+                with capture(g2, pool=pool, stream=s), ForkJoinAudit(s):
                     self._mid(update_actor, flat_c, scale, rollout)  # the optimisers read the reduced bucket in place
                     if update_actor:
                         flat_a = S.pack(L.grad_params(actor=True))
                 if update_actor:  # no actor step at this parity: nothing to capture
-                    with torch.cuda.graph(g3, pool=pool, stream=s), ForkJoinAudit(s):
+                    with capture(g3, pool=pool, stream=s), ForkJoinAudit(s):
                         self._post(update_actor, flat_a, scale)
                 else:
                     g3 = None
@@ -900,7 +898,7 @@ class VecTrainer:
             self._astream = torch.cuda.Stream(device=self.device)
         try:
             with torch.cuda.stream(s):
-                with torch.cuda.graph(g, stream=s), ForkJoinAudit(s):
+                with capture(g, stream=s), ForkJoinAudit(s):
                     for i, u in enumerate((ua, ua2)):
                         L.prefetch_actor = u
                         if overlap and i == 0:
@@ -1097,7 +1095,7 @@ class VecTrainer:
         s.wait_stream(torch.cuda.current_stream(self.device))
         g = new_graph()
         with torch.cuda.stream(s):
-            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"), ForkJoinAudit(s):
+            with capture(g, stream=s, capture_error_mode="thread_local"), ForkJoinAudit(s):
                 L.update_targets_device()
                 ag.replay_buffer.reset_max_priority()
                 ag.sync.max_(ag.replay_buffer._maxp)
@@ -1390,7 +1388,7 @@ class RefScheduleTrainer(VecTrainer):
             g = new_graph()
             cur0 = self._cur
             with torch.cuda.stream(s):
-                with torch.cuda.graph(g, stream=s), ForkJoinAudit(s):
+                with capture(g, stream=s), ForkJoinAudit(s):
                     for _ in range(self.round_len):
                         self._rollout_ref(random, overlap=self.round_overlap)
                         self._cur ^= 1
@@ -1420,7 +1418,7 @@ class RefScheduleTrainer(VecTrainer):
                 s.wait_stream(torch.cuda.current_stream(self.device))
                 g = new_graph()
                 with torch.cuda.stream(s):
-                    with torch.cuda.graph(g, stream=s), ForkJoinAudit(s):
+                    with capture(g, stream=s), ForkJoinAudit(s):
                         self._rollout_ref(random)
                 torch.cuda.current_stream(self.device).wait_stream(s)
                 self.graphs[key] = g
@@ -1519,7 +1517,7 @@ class RefScheduleTrainer(VecTrainer):
                 self._astream = torch.cuda.Stream(device=self.device)
             try:
                 with torch.cuda.stream(s):
-                    with torch.cuda.graph(g, stream=s), ForkJoinAudit(s):
+                    with capture(g, stream=s), ForkJoinAudit(s):
                         for i, u in enumerate((True, False)):
                             half(i)
                             L.prefetch_actor = u

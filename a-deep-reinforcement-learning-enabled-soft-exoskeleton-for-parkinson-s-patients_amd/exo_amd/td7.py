@@ -21,6 +21,7 @@ adds the replay buffer, the checkpoint policy and data parallelism.
 import copy
 import ctypes
 import os
+import sys
 import warnings
 from dataclasses import dataclass, field
 from typing import Callable
@@ -33,7 +34,7 @@ import torch.nn.functional as F
 
 from . import _native as nat
 from . import ops
-from .graphs import new_graph
+from .graphs import capture, new_graph
 from .ops import avg_l1_norm
 
 # fused schedule variant (r03, off): the critic target chain on the update's
@@ -468,63 +469,100 @@ class GradSync:
         return self._capture_ok
 
     def _capture_selftest(self, device, replays=3):
-        """The iteration's collective pattern (VecTrainer._inline) captured and
-        replayed at this world size: an AVG on a forked branch (the encoder
-        bucket), an AVG on the capture stream (the critic bucket), a MAX on a
-        second branch forked after it (max_priority), an AVG on the capture
-        stream again (the actor bucket), each branch joined at the end -- so a
+        """The training graphs' collective pattern captured and replayed at
+        this world size, before any training graph is captured -- so a
         cross-stream ordering the runtime or RCCL mishandles at world > 1
-        shows here, before any training graph is captured."""
+        shows here.  Iteration 1 (VecTrainer._inline): an AVG on a forked
+        branch (the encoder bucket), an AVG on the capture stream (the critic
+        bucket), a MAX on a second branch forked after it (max_priority), and
+        -- the overlapped pair's order (r06) -- the actor
+        bucket's AVG on a third branch beside iteration 2's encoder AVG on a
+        fourth; iteration 2's critic AVG after the actor branch; every branch
+        joined at the end.  Every collective goes through the process group's
+        one stream, so the graph orders them as captured, the same order on
+        every rank.  Bounded: if the capture or the replays have not finished
+        after EXO_DP_SELFTEST_TIMEOUT seconds (default 120) the process exits
+        (status 3) with a message instead of hanging the job -- EXO_DP_CAPTURE=0
+        skips the self-test and runs the eager-collective layout."""
+        import threading
         xe = torch.zeros(4096, device=device)
         xc = torch.zeros(1024, device=device)
         xa = torch.zeros(256, device=device)
+        xe2 = torch.zeros(4096, device=device)
+        xc2 = torch.zeros(1024, device=device)
         y = torch.zeros(1, device=device)
         self.avg_(xe)  # eager first: communicator set up outside the capture
         dist.all_reduce(y, op=dist.ReduceOp.MAX, group=self.group)
-        cur = torch.cuda.current_stream(device)
-        s = torch.cuda.Stream(device=device)
-        side, prio = torch.cuda.Stream(device=device), torch.cuda.Stream(device=device)
-        s.wait_stream(cur)
-        g = new_graph()
-        captured = True
+        torch.cuda.synchronize(device)
+        limit = float(os.environ.get("EXO_DP_SELFTEST_TIMEOUT", "120"))
+
+        def _hung():
+            sys.stderr.write(f"[exo_amd] rank {self.rank}: the captured-collective self-test (GradSync."
+                             f"_capture_selftest) did not finish within {limit:.0f} s at world {self.world}; "
+                             "exiting. EXO_DP_CAPTURE=0 runs the eager-collective layout instead.\n")
+            sys.stderr.flush()
+            os._exit(3)
+        timer = threading.Timer(limit, _hung)
+        timer.daemon = True
+        timer.start()
         try:
-            with torch.cuda.stream(s):
-                with torch.cuda.graph(g, stream=s):
-                    side.wait_stream(s)
-                    with torch.cuda.stream(side):
-                        xe.mul_(2.0)
-                        self.avg_(xe)
-                    xc.add_(1.0)
-                    self.avg_(xc)
-                    prio.wait_stream(s)
-                    with torch.cuda.stream(prio):
-                        dist.all_reduce(y, op=dist.ReduceOp.MAX, group=self.group)
-                    self.avg_(xa)
-                    s.wait_stream(side)
-                    s.wait_stream(prio)
-        except Exception:
-            captured = False
-        cur.wait_stream(s)
-        # a replay runs the collectives: only if EVERY rank captured them
-        flag = torch.tensor([1.0 if captured else 0.0], device=device)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
-        if float(flag) != 1.0:
-            return False
-        ok = True
-        for k in range(replays):
-            r = float(self.rank + 1 + k)
-            xe.fill_(r)
-            xc.fill_(r)
-            xa.fill_(r)
-            y.fill_(float(self.rank + 2 * k))
-            g.replay()
-            torch.cuda.synchronize(device)
-            want = (self.world + 1) / 2.0 + k  # the mean of rank + 1 + k
-            ok = (ok and bool((xe - 2 * want).abs().max() <= 2e-5 * want)
-                  and bool((xc - (want + 1)).abs().max() <= 1e-5 * (want + 1))
-                  and bool((xa - want).abs().max() <= 1e-5 * want) and float(y) == self.world - 1 + 2 * k)
-        del g
-        return ok
+            cur = torch.cuda.current_stream(device)
+            s = torch.cuda.Stream(device=device)
+            side, prio = torch.cuda.Stream(device=device), torch.cuda.Stream(device=device)
+            abr, side2 = torch.cuda.Stream(device=device), torch.cuda.Stream(device=device)
+            s.wait_stream(cur)
+            g = new_graph()
+            captured = True
+            try:
+                with torch.cuda.stream(s):
+                    with capture(g, stream=s):
+                        side.wait_stream(s)
+                        with torch.cuda.stream(side):
+                            xe.mul_(2.0)
+                            self.avg_(xe)
+                        xc.add_(1.0)
+                        self.avg_(xc)
+                        prio.wait_stream(s)
+                        with torch.cuda.stream(prio):
+                            dist.all_reduce(y, op=dist.ReduceOp.MAX, group=self.group)
+                        abr.wait_stream(s)
+                        with torch.cuda.stream(abr):  # iteration 1's actor bucket on its branch
+                            xa.mul_(3.0)
+                            self.avg_(xa)
+                        side2.wait_stream(s)
+                        with torch.cuda.stream(side2):  # beside it, iteration 2's encoder bucket
+                            xe2.add_(xc)
+                            self.avg_(xe2)
+                        s.wait_stream(abr)  # iteration 2's critic step waits for the actor branch
+                        xc2.add_(xa[:1])
+                        self.avg_(xc2)
+                        for b in (side, prio, side2):
+                            s.wait_stream(b)
+            except Exception:
+                captured = False
+            cur.wait_stream(s)
+            # a replay runs the collectives: only if EVERY rank captured them
+            flag = torch.tensor([1.0 if captured else 0.0], device=device)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+            if float(flag) != 1.0:
+                return False
+            ok = True
+            for k in range(replays):
+                r = float(self.rank + 1 + k)
+                for t in (xe, xc, xa, xe2, xc2):
+                    t.fill_(r)
+                y.fill_(float(self.rank + 2 * k))
+                g.replay()
+                torch.cuda.synchronize(device)
+                want = (self.world + 1) / 2.0 + k  # the mean of rank + 1 + k
+                # xe2 = mean(r + (r + 1) averaged) = want + want + 1; xc2 = mean(r + 3 want)
+                checks = ((xe, 2 * want), (xc, want + 1), (xa, 3 * want), (xe2, 2 * want + 1), (xc2, 4 * want))
+                ok = ok and all(bool((t - v).abs().max() <= 2e-5 * v) for t, v in checks)
+                ok = ok and float(y) == self.world - 1 + 2 * k
+            del g
+            return ok
+        finally:
+            timer.cancel()
 
     def allreduce_grads(self, params):
         if not self.active:

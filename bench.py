@@ -38,7 +38,7 @@ sys.path.insert(0, PKG)
 os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
 # the reference schedule's burst steps sample the next batch at their end
 # (RefScheduleTrainer.burst_prefetch; 74.5 vs 75.6 ms per burst): on here,
-# where every finished phase's graphs are retired (_release), not destroyed
+# where every finished phase's graphs are released with ballast streams (_release)
 os.environ.setdefault("EXO_BURST_PREFETCH", "1")
 
 import numpy as np  # noqa: E402
@@ -304,10 +304,10 @@ def critic_gemm_timing(agent, reps=20, replays=10):
         fn()
         st = torch.cuda.Stream(device=dev)
         st.wait_stream(torch.cuda.current_stream(dev))
-        from exo_amd.graphs import new_graph
+        from exo_amd.graphs import capture, new_graph
         g = new_graph()
         with torch.cuda.stream(st):
-            with torch.cuda.graph(g, stream=st):
+            with capture(g, stream=st):
                 for _ in range(reps):
                     fn()
         torch.cuda.current_stream(dev).wait_stream(st)
@@ -354,10 +354,10 @@ def fused_critic_timing(agent, reps=20, replays=10):
     fn()
     st = torch.cuda.Stream(device=dev)
     st.wait_stream(torch.cuda.current_stream(dev))
-    from exo_amd.graphs import new_graph
+    from exo_amd.graphs import capture, new_graph
     gr = new_graph()
     with torch.cuda.stream(st):
-        with torch.cuda.graph(gr, stream=st):
+        with capture(gr, stream=st):
             for _ in range(reps):
                 fn()
     torch.cuda.current_stream(dev).wait_stream(st)
@@ -387,13 +387,12 @@ REFERENCE_ENV_STEPS_PER_UPDATE = 2257 / 283
 
 
 def _release(tr):
-    """Retire a finished phase's graphs with the device idle: moved to the
-    process-wide keep-alive list (exo_amd.rollout.retire_graphs), not destroyed.
-    Destroying graph execs releases their runtime streams unevenly over the
-    4 hardware queues, and the HIP runtime's first-launch stream assignment
-    of a later graph then over-reads its stream array when two of its streams
-    share the launch stream's queue -- the round-4 segfault in hipGraphLaunch
-    ("The graph-replay crash")."""
+    """Release a finished phase's graphs with the device idle
+    (exo_amd.rollout.retire_graphs: execs and memory pools destroyed, then
+    ballast streams created so the runtime streams they held are replaced on
+    the least-loaded hardware queues -- destroying execs alone can make the
+    ROCm 7.0 runtime's launch of a later graph read past its stream vector,
+    DESIGN.md 4, "The graph-replay crash")."""
     from exo_amd.rollout import retire_graphs
     torch.cuda.synchronize()
     retire_graphs(tr)
@@ -943,7 +942,7 @@ def main():
         finite = {n: bool(torch.isfinite(torch.cat([p.detach().reshape(-1) for p in m.parameters()])).all())
                   for n, m in (("actor", agent.learner.actor), ("critic", agent.learner.critic),
                                ("encoder", agent.learner.encoder))}
-    dp_sync = dp_ck = None
+    dp_sync = dp_ck = dp_lay_ranks = None
     ref_sched = None
     if agent is not None and args.mode == "train" and not args.no_reference_schedule:
         # every rank (collectives inside); rank 0 reports
@@ -961,6 +960,13 @@ def main():
         dist.all_gather(allck, ck)
         dp_sync = all(torch.equal(allck[0], x) for x in allck)
         dp_ck = [x.tolist() for x in allck]
+        # every rank's layout: in-graph collectives, overlapped pairs
+        lay = torch.tensor([float(trainer.dp_inline) if trainer is not None else -1.0,
+                            float(any(isinstance(k, tuple) and k[-1] == "overlap" for k in trainer.graphs))
+                            if trainer is not None else -1.0], device=dev)
+        all_lay = [torch.zeros_like(lay) for _ in range(world)]
+        dist.all_gather(all_lay, lay)
+        dp_lay_ranks = [x.tolist() for x in all_lay]
     if rank == 0:
         active_avg = kern_active
         achieved = BYTES_PER_ENV_STEP * active_avg / (kern_ms * 1e-3) / 1e9
@@ -1115,6 +1121,9 @@ def main():
             res["td7_variants"] = td7_variants(env, dev, args)
         if dp_sync is not None:
             res["dp_layout"] = dp_layout(trainer)
+            res["dp_layout_per_rank"] = [("one graph, collectives captured (RCCL)" if a == 1.0 else
+                                          "three graphs, eager collectives") for a, _ in dp_lay_ranks]
+            res["overlapped_pairs_per_rank"] = [b == 1.0 for _, b in dp_lay_ranks]
         if trainer is not None:
             # the graph-replayed loop's schedule ("The training
             # iteration's schedule"): an actor iteration and the next one per

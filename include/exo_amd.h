@@ -818,6 +818,19 @@ int td7f_wgrad_adam(int32_t prec, int32_t njobs, const td7f_wg_job *jobs, int64_
                     const float *lr, const float *beta1, const float *beta2, const float *eps,
                     const float *weight_decay, const td7f_wg_adam *adam, uint32_t *ticket_dev, void *stream);
 
+/* ---------------------------------------------------------- HIP runtime
+ * No reference counterpart: a workaround for the ROCm 7.0 graph-launch defect
+ * ("The graph-replay crash").  Creates n non-blocking streams on
+ * the current device and keeps them for the life of the process, so that the
+ * streams released by destroyed graph execs are replaced on the least-loaded
+ * hardware queues.  Returns the number of ballast streams held (>= 0) or
+ * EXO_E*.  exo_amd.graphs.release_graphs calls it after destroying execs. */
+int exo_stream_ballast(int32_t n);
+/* 1 + the sum over the nodes of a captured hipGraph_t of (dependents - 1): an
+ * upper bound on its parallel branches, i.e. on the streams its exec owns
+ * (diagnostic for the ballast count). */
+int exo_graph_branch_bound(void *graph, int32_t *out);
+
 #ifdef __cplusplus
 }
 #endif

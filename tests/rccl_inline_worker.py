@@ -58,7 +58,8 @@ def main():
         for capture, inline, planned in (("1", True, False), ("1", True, True), ("0", False, False)):
             tr, st = run(dist.group.WORLD, capture, planned)
             assert tr.dp and tr.dp_inline is inline
-            if inline:
+            if inline:  # the extended captured-collective self-test (GradSync._capture_selftest) ran and passed
+                assert tr.agent.sync._capture_ok is True
                 assert all(len(parts) == 1 for k, parts in tr.graphs.items() if k[0] != "pair")
                 assert any(k[-1] == "overlap" for k in tr.graphs) == planned
                 assert tr._refresh_graph is not None

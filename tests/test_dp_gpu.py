@@ -45,10 +45,19 @@ def test_two_rank_training_keeps_replicas_in_sync():
     assert res["value"] > 0
 
 
-def _failure_text(out):
+def _failure_text(out, name="child"):
     """A failed child's story: the error lines of its stderr (a watchdog's
     stack trace otherwise buries the message), its stdout tail and the tail
-    of stderr."""
+    of stderr.  The whole stdout and stderr are kept in
+    gpurun_out/<name>.log (the r05 watchdog abort's log
+    was lost)."""
+    try:
+        d = os.path.join(REPO, "gpurun_out")
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, f"{name}.log"), "w") as f:
+            f.write(f"returncode {out.returncode}\n--- stdout ---\n{out.stdout}\n--- stderr ---\n{out.stderr}")
+    except OSError:
+        pass
     err = out.stderr.splitlines()
     keys = ("Error", "error", "HIP", "NCCL", "RCCL", "Timeout", "timed out", "Traceback")
     lines = [l for l in err if any(k in l for k in keys) and "frame #" not in l]
@@ -64,19 +73,22 @@ def test_rccl_data_parallel_layout_at_world_one():
     all-reduces, the max_priority MAX reduction and the replica checksum
     all_gather on RCCL between the graphs (RCCL refuses two ranks on one
     device, so world 1 is the most of that path one GPU can run)."""
-    env = dict(os.environ, EXO_FORCE_DIST="1")
+    # NCCL_DEBUG=WARN: RCCL's own message for an asynchronous error reaches stderr
+    env = dict(os.environ, EXO_FORCE_DIST="1", NCCL_DEBUG="WARN")
     env.pop("EXO_DIST_BACKEND", None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
            "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(REPO, "bench.py"),
            "--steps", "20", "--warmup", "8", "--envs", "512", "--no-cpu-baseline", "--no-td7-variants",
            "--no-reference-schedule", "--kernel-timing-steps", "5"]
     out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=REPO)
-    assert out.returncode == 0, _failure_text(out)
+    assert out.returncode == 0, _failure_text(out, "rccl_world1_bench_child")
     res = json.loads([l for l in out.stdout.splitlines() if l.startswith('{"metric')][-1])
     assert res["n_gpus"] == 1
     assert "DP all-reduce" in res["config"]["parallelism"]
     assert res["dp_weights_in_sync"] is True
     assert res["dp_layout"] == "one graph, collectives captured (RCCL)"
+    assert res["dp_layout_per_rank"] == ["one graph, collectives captured (RCCL)"]
+    assert res["overlapped_pairs_per_rank"] == [True]
     assert res["weights_finite"] is True, res["weights_finite"]
     assert res["value"] > 0
 
