@@ -516,29 +516,33 @@ class GradSync:
             try:
                 with torch.cuda.stream(s):
                     with capture(g, stream=s):
-                        side.wait_stream(s)
-                        with torch.cuda.stream(side):
-                            xe.mul_(2.0)
-                            self.avg_(xe)
-                        xc.add_(1.0)
-                        self.avg_(xc)
-                        prio.wait_stream(s)
-                        with torch.cuda.stream(prio):
-                            dist.all_reduce(y, op=dist.ReduceOp.MAX, group=self.group)
-                        abr.wait_stream(s)
-                        with torch.cuda.stream(abr):  # iteration 1's actor bucket on its branch
-                            xa.mul_(3.0)
-                            self.avg_(xa)
-                        side2.wait_stream(s)
-                        with torch.cuda.stream(side2):  # beside it, iteration 2's encoder bucket
-                            xe2.add_(xc)
-                            self.avg_(xe2)
-                        s.wait_stream(abr)  # iteration 2's critic step waits for the actor branch
-                        xc2.add_(xa[:1])
-                        self.avg_(xc2)
-                        for b in (side, prio, side2):
-                            s.wait_stream(b)
-            except Exception:
+                        try:
+                            side.wait_stream(s)
+                            with torch.cuda.stream(side):
+                                xe.mul_(2.0)
+                                self.avg_(xe)
+                            xc.add_(1.0)
+                            self.avg_(xc)
+                            prio.wait_stream(s)
+                            with torch.cuda.stream(prio):
+                                dist.all_reduce(y, op=dist.ReduceOp.MAX, group=self.group)
+                            abr.wait_stream(s)
+                            with torch.cuda.stream(abr):  # iteration 1's actor bucket on its branch
+                                xa.mul_(3.0)
+                                self.avg_(xa)
+                            side2.wait_stream(s)
+                            with torch.cuda.stream(side2):  # beside it, iteration 2's encoder bucket
+                                xe2.add_(xc[:1])
+                                self.avg_(xe2)
+                            s.wait_stream(abr)  # iteration 2's critic step waits for the actor branch
+                            xc2.add_(xa[:1])
+                            self.avg_(xc2)
+                        finally:  # every branch joined, also when the capture failed: the capture ends
+                            for b in (side, prio, abr, side2):
+                                s.wait_stream(b)
+            except Exception as e:  # noqa: BLE001 -- any refusal: the eager layout, said why
+                warnings.warn(f"GradSync: the captured-collective self-test could not capture ({e!r}); "
+                              "the eager-collective layout will run")
                 captured = False
             cur.wait_stream(s)
             # a replay runs the collectives: only if EVERY rank captured them

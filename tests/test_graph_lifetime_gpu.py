@@ -20,10 +20,13 @@ pytestmark = pytest.mark.gpu
 
 
 def _forked_graph(side, branches, ctr):
-    """A root on the capture stream, branches - 1 forked side streams each
-    adding into its own counter slot, joined back (the repro's shapes)."""
+    """A root on the capture stream side[0], branches - 1 forked side streams
+    side[1:] each adding into its own counter slot, joined back (the repro's
+    shapes).  The five streams are taken once: torch's stream pool hands the
+    same 32 streams out in turn, so a new one per call would alias a side
+    stream and merge two branches."""
     from exo_amd.graphs import capture, new_graph
-    s = torch.cuda.Stream()
+    s, side = side[0], side[1:]
     s.wait_stream(torch.cuda.current_stream())
     g = new_graph()
     with torch.cuda.stream(s):
@@ -33,6 +36,7 @@ def _forked_graph(side, branches, ctr):
                 side[b - 1].wait_stream(s)
                 with torch.cuda.stream(side[b - 1]):
                     ctr[b].add_(1)
+            ctr[0].add_(1)  # the capture stream's own branch
             for b in range(1, branches):
                 s.wait_stream(side[b - 1])
             ctr[7].add_(1)
@@ -48,7 +52,7 @@ def test_release_graphs_keeps_later_launches_safe():
     branches."""
     from exo_amd.graphs import branch_bound, release_graphs
     rng = random.Random(1)
-    side = [torch.cuda.Stream() for _ in range(4)]
+    side = [torch.cuda.Stream() for _ in range(5)]
     ctr = torch.zeros(8, dtype=torch.int64, device="cuda")
     want = [0] * 8
     live = []
@@ -66,7 +70,7 @@ def test_release_graphs_keeps_later_launches_safe():
             live = [x for x in live if all(x is not y for y in gone)]
         for g, b in live:
             g.replay()
-            want[0] += 1
+            want[0] += 2
             for k in range(1, b):
                 want[k] += 1
             want[7] += 1
