@@ -43,10 +43,10 @@ extern template void launch_fwd_big_p<PREC_BF16, true>(const GemmArgs &, dim3, i
 extern template void launch_fwd_big_p<PREC_F16, true>(const GemmArgs &, dim3, int, hipStream_t);
 extern template void launch_fwd_p<PREC_BF16, false, true>(const GemmArgs &, dim3, int, int, int, int, hipStream_t);
 extern template void launch_fwd_p<PREC_F16, false, true>(const GemmArgs &, dim3, int, int, int, int, hipStream_t);
-extern template void launch_fwd_xl_p<PREC_BF16, false>(const GemmArgs &, dim3, bool, hipStream_t);
-extern template void launch_fwd_xl_p<PREC_F16, false>(const GemmArgs &, dim3, bool, hipStream_t);
-extern template void launch_fwd_xl_p<PREC_BF16, true>(const GemmArgs &, dim3, bool, hipStream_t);
-extern template void launch_fwd_xl_p<PREC_F16, true>(const GemmArgs &, dim3, bool, hipStream_t);
+extern template void launch_fwd_xl_p<PREC_BF16, false>(const GemmArgs &, dim3, int, hipStream_t);
+extern template void launch_fwd_xl_p<PREC_F16, false>(const GemmArgs &, dim3, int, hipStream_t);
+extern template void launch_fwd_xl_p<PREC_BF16, true>(const GemmArgs &, dim3, int, hipStream_t);
+extern template void launch_fwd_xl_p<PREC_F16, true>(const GemmArgs &, dim3, int, hipStream_t);
 TD7_EXTERN(PREC_F32)
 TD7_EXTERN(PREC_BF16)
 TD7_EXTERN(PREC_F16)
@@ -97,6 +97,18 @@ int launch_wgrad(const WgradArgs &a, int groups, int act, int prec, hipStream_t 
         else launch_wgrad_p<PREC_F32, false>(a, grid, va, nw, act, s);
     }
     return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
+}
+
+// the 256 x 256-tile forward's kernel: EXO_FWD_XL (0 dense_fwd_big_kernel,
+// 1 dense_fwd_xl_kernel, 2 dense_fwd_xl8_kernel, 3 dense_fwd_xl9_kernel; the
+// K % 64 == 0 kernels fall back to 1 elsewhere), td7_dense_set_xl at run time
+static int g_fwd_xl = -1;
+static int fwd_xl_variant() {
+    if (g_fwd_xl < 0) {
+        const char *e = std::getenv("EXO_FWD_XL");
+        g_fwd_xl = (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 2;
+    }
+    return g_fwd_xl;
 }
 
 int launch_fwd(const GemmArgs &a, int groups_grid, int prec, hipStream_t s, bool cat = false) {
@@ -164,21 +176,21 @@ int launch_fwd(const GemmArgs &a, int groups_grid, int prec, hipStream_t s, bool
     // 16-bit X and W at >= 256 tiles of 256 x 256 (r05): dense_fwd_xl8_kernel
     // where K % 64 == 0, else dense_fwd_xl_kernel; EXO_FWD_XL=0 keeps
     // dense_fwd_big_kernel, EXO_FWD_XL=1 dense_fwd_xl_kernel everywhere
-    static const int xl_v = [] {
-        const char *e = std::getenv("EXO_FWD_XL");
-        return (e && (e[0] == '0' || e[0] == '1')) ? e[0] - '0' : 2;
-    }();
-    const bool xl_on = xl_v != 0, xl_dma = xl_v == 2 && a.R % XL_BK == 0;
+    // (r06: EXO_FWD_XL=3 dense_fwd_xl9_kernel, the k-step LDS ring;
+    // td7_dense_set_xl switches it at run time for same-process A/Bs)
+    const int xl_v = fwd_xl_variant();
+    const bool xl_on = xl_v != 0;
+    const int xl_var = (xl_v >= 2 && a.R % XL_BK == 0) ? xl_v : 1;
     const long txl = (long)((a.I + XL_BM - 1) / XL_BM) * ((a.J + XL_BN - 1) / XL_BN) * groups_grid;
     if (big && xl_on && a.a16 && a.b16 && txl >= 256 &&
         (!a.c16 || (a.csj == 1 && a.csi % 8 == 0 && a.csg % 8 == 0 && ((uintptr_t)a.c16 & 15) == 0))) {
         dim3 grid((a.J + XL_BN - 1) / XL_BN, (a.I + XL_BM - 1) / XL_BM, groups_grid);
         if (cat) {
-            if (prec == PREC_BF16) launch_fwd_xl_p<PREC_BF16, true>(a, grid, xl_dma, s);
-            else launch_fwd_xl_p<PREC_F16, true>(a, grid, xl_dma, s);
+            if (prec == PREC_BF16) launch_fwd_xl_p<PREC_BF16, true>(a, grid, xl_var, s);
+            else launch_fwd_xl_p<PREC_F16, true>(a, grid, xl_var, s);
         } else {
-            if (prec == PREC_BF16) launch_fwd_xl_p<PREC_BF16, false>(a, grid, xl_dma, s);
-            else launch_fwd_xl_p<PREC_F16, false>(a, grid, xl_dma, s);
+            if (prec == PREC_BF16) launch_fwd_xl_p<PREC_BF16, false>(a, grid, xl_var, s);
+            else launch_fwd_xl_p<PREC_F16, false>(a, grid, xl_var, s);
         }
         return hipGetLastError() == hipSuccess ? EXO_OK : EXO_EDEVICE;
     }
@@ -296,6 +308,13 @@ Operand plain(const float *p, long sg, long si, long sr) {
 using namespace td7dense;
 
 extern "C" {
+
+int td7_dense_set_xl(int32_t variant) {
+    const int prev = td7dense::fwd_xl_variant();
+    if (variant < 0 || variant > 3) return EXO_EINVAL;
+    td7dense::g_fwd_xl = variant;
+    return prev;
+}
 
 /* Forward of G grouped dense layers: Y[g] = act(X[g] W[g]^T + b[g]).
  * X: [G][M][K] with group stride xsg (0 = one X shared by all groups) and row

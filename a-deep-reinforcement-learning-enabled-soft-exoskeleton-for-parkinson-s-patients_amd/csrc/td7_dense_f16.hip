@@ -14,6 +14,6 @@ template void launch_fwd_lds_p<PREC_F16, false>(const GemmArgs &, dim3, int, hip
 template void launch_fwd_lds_p<PREC_F16, true>(const GemmArgs &, dim3, int, hipStream_t);
 template void launch_fwd_big_p<PREC_F16, false>(const GemmArgs &, dim3, int, hipStream_t);
 template void launch_fwd_big_p<PREC_F16, true>(const GemmArgs &, dim3, int, hipStream_t);
-template void launch_fwd_xl_p<PREC_F16, false>(const GemmArgs &, dim3, bool, hipStream_t);
-template void launch_fwd_xl_p<PREC_F16, true>(const GemmArgs &, dim3, bool, hipStream_t);
+template void launch_fwd_xl_p<PREC_F16, false>(const GemmArgs &, dim3, int, hipStream_t);
+template void launch_fwd_xl_p<PREC_F16, true>(const GemmArgs &, dim3, int, hipStream_t);
 } // namespace td7dense

@@ -1600,9 +1600,157 @@ __global__ __launch_bounds__(512) void dense_fwd_xl8_kernel(GemmArgs a) {
     xl8_epilogue<EP, P, CHF>(a, acc, i0, j0, g);
 }
 
+// r06: the same 256 x 256 tile, 8 waves and MFMA order as dense_fwd_xl8_kernel,
+// staged through a ring of 9 LDS slots of ONE k-step each (16 KB: the 16-deep
+// k range of the tile's 256 A rows and 256 B columns, 2 chunks of 16 bytes per
+// row) instead of two 64-deep slices: the LDS-DMA of k-step s + 7 is issued
+// while k-step s is multiplied, so 7 k-steps (112 KB) are in flight per CU
+// where xl8 had one slice (64 KB) and drained it at every slice end
+// (vmcnt(0) + barrier: its DMA alone took 155 us of the 194, profiles/r05_xl).
+// Per k-step: issue DMA(s + 7) -> s_waitcnt vmcnt(12) (this wave's DMA of
+// k-step s + 1 retired: 6 k-steps x 2 instructions issued after it) -> raw
+// s_barrier (every wave's DMA of s + 1 retired: RAW) -> fragment reads of s + 1
+// -> s_waitcnt lgkmcnt(6) (the reads of s, issued one iteration earlier) ->
+// the 8 MFMAs of s.  WAR: DMA(s + 7) overwrites the slot of k-step s - 2, whose
+// fragments were read in iteration s - 3 and retired in iteration s - 2,
+// before barrier s - 1 that every wave passed before issuing it.  Past the
+// last k-step the DMAs read at BUF_OOB (zeros) into slots nothing reads, so
+// the vmcnt counts stay exact.  Slot layout: row r (A rows, then B columns) at
+// 32 bytes, chunk c in 16-byte slot c ^ ((r >> 3) & 1) -- a fragment read's
+// 16-lane pass (16 consecutive rows, one chunk) covers all 16 slots of a
+// 256-byte bank row; the DMA writes lane-linear (lane l: row 32 w + (l >> 1),
+// slot l & 1) with the chunk permuted on the SOURCE side.  All LDS is the one
+// dynamic array (a second __shared__ object can make hipcc drain vmcnt).
+constexpr int XL9_NS = 9, XL9_D = 7;  // slots; k-steps issued ahead (<= NS - 2, see WAR)
+constexpr int XL9_SLOT = 1024;        // uint32_t4 per slot (16 KB: 256 A rows + 256 B rows x 32 bytes)
+constexpr int XL9_LDS = XL9_NS * XL9_SLOT * 16;  // 144 KB (the epilogue's 128 KB output stage fits)
+
 template <int EP, int P, bool CAT, bool CHF>
-void launch_fwd_xl_one(const GemmArgs &a, dim3 grid, bool dma, hipStream_t s) {
-    if (dma) {
+__global__ __launch_bounds__(512) void dense_fwd_xl9_kernel(GemmArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t4 xl_smem[];
+    constexpr int NS = XL9_NS, D = XL9_D, SLOT = XL9_SLOT;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w >> 2, wn = w & 3;
+    const int l31 = lane & 31, lh = lane >> 5;
+    const int3 tile = xcd_tile();
+    const int i0 = tile.y * XL_BM, j0 = tile.x * XL_BN, g = tile.z;
+    const int K = a.R, nks = K / 16;  // K % 64 == 0 (the launcher's condition)
+    // the rows this lane stages: A row / B column 32 w + (lane >> 1), chunk
+    // (lane & 1) ^ ((row >> 3) & 1) of each k-step
+    const int sr = 32 * w + (lane >> 1);
+    const int sc = (lane & 1) ^ ((sr >> 3) & 1);
+    const __amdgpu_buffer_rsrc_t rb = rsrc(reinterpret_cast<const float *>(a.b16 + (long)g * a.J * a.R));
+    __amdgpu_buffer_rsrc_t ra = CAT ? rsrc(a.cat.p[0]) : rsrc(reinterpret_cast<const float *>(a.a16 + g * a.A.sg));
+    int lda = CAT ? a.cat.ld[0] : (int)a.A.si, kbase = 0, seg = 0;
+    auto gseg = [&](int kt) {
+        if constexpr (CAT) {  // the k-step's segment (boundaries are multiples of 64)
+            const int s = cat_seg(a.cat, kt * 16);
+            if (s != seg || kt == 0) {
+                seg = s;
+                const float *p = a.cat.p[0];
+                long gs = a.cat.sg[0];
+                int ld = a.cat.ld[0], kb = 0;
+#pragma unroll
+                for (int m = 1; m < CAT_MAX; ++m)
+                    if (s == m) p = a.cat.p[m], gs = a.cat.sg[m], ld = a.cat.ld[m], kb = a.cat.kb[m];
+                ra = rsrc(reinterpret_cast<const float *>(reinterpret_cast<const uint16_t *>(p) + g * gs));
+                lda = ld;
+                kbase = kb;
+            }
+        }
+    };
+    const bool arow = i0 + sr < a.I, bcol = j0 + sr < a.J;
+    const uint32_t bbase = bcol ? (uint32_t)((j0 + sr) * a.R + 8 * sc) * 2u : 0u;
+    uint32_t abase = 0;
+    auto rows = [&]() { abase = arow ? (uint32_t)((i0 + sr) * lda + 8 * sc - kbase) * 2u : 0u; };
+    rows();
+    int slot_issue = 0;  // (s + D) % NS for the next issue
+    auto issue = [&](int s) {
+        uint32_t oa = (uint32_t)BUF_OOB, ob = (uint32_t)BUF_OOB;
+        if (s < nks) {
+            if constexpr (CAT) {
+                const int s0 = seg;
+                gseg(s);
+                if (seg != s0) rows();
+            }
+            const uint32_t kb = (uint32_t)s * 32u;  // 16 k x 2 bytes
+            if (arow) oa = abase + kb;
+            if (bcol) ob = bbase + kb;
+        }
+        uint32_t4 *sl = xl_smem + slot_issue * SLOT;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void *)(sl + w * 64), 16, oa,
+                                                 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (__attribute__((address_space(3))) void *)(sl + 512 + w * 64), 16,
+                                                 ob, 0, 0, 0);
+        slot_issue = slot_issue + 1 == NS ? 0 : slot_issue + 1;
+    };
+    // this lane's fragment addresses inside a slot (uint32_t4 units)
+    int fa_off[4], fb_off[2];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+        const int r = wm * 128 + 32 * x + l31;
+        fa_off[x] = r * 2 + (lh ^ ((r >> 3) & 1));
+    }
+#pragma unroll
+    for (int y = 0; y < 2; ++y) {
+        const int r = wn * 64 + 32 * y + l31;
+        fb_off[y] = 512 + r * 2 + (lh ^ ((r >> 3) & 1));
+    }
+    auto frag = [&](int slot, uint32_t4 (&af)[4], uint32_t4 (&bf)[2]) {
+        const uint32_t4 *sl = xl_smem + slot * SLOT;
+#pragma unroll
+        for (int x = 0; x < 4; ++x) af[x] = sl[fa_off[x]];
+#pragma unroll
+        for (int y = 0; y < 2; ++y) bf[y] = sl[fb_off[y]];
+    };
+    floatx16 acc[4][2];
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[x][y][e] = 0.f;
+    if constexpr (CAT) gseg(0), rows();
+#pragma unroll
+    for (int s = 0; s < D; ++s) issue(s);
+    // k-step 0 retired (6 k-steps x 2 DMAs after it), every wave's
+    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    uint32_t4 fa[2][4], fb[2][2];
+    frag(0, fa[0], fb[0]);
+    int slot_read = 1;  // slot of k-step s + 1
+    // two k-steps per trip: the fragment registers alternate by parity (no
+    // runtime-indexed register arrays); nks is even (K % 64 == 0)
+    for (int s = 0; s < nks; s += 2) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            issue(s + h + D);
+            asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            frag(slot_read, fa[h ^ 1], fb[h ^ 1]);  // k-step s + h + 1 (past the end: a slot nothing uses)
+            slot_read = slot_read + 1 == NS ? 0 : slot_read + 1;
+            asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");  // the reads of k-step s + h
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int y = 0; y < 2; ++y) acc[x][y] = mfma32_k16<P>(fa[h][x], fb[h][y], acc[x][y]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    // every DMA (the phantom ones included) and every fragment read retired,
+    // every wave past its last read: the stage is idle for the epilogue
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    xl8_epilogue<EP, P, CHF>(a, acc, i0, j0, g);
+}
+
+template <int EP, int P, bool CAT, bool CHF>
+void launch_fwd_xl_one(const GemmArgs &a, dim3 grid, int variant, hipStream_t s) {
+    if (variant == 3) {
+        (void)hipFuncSetAttribute((const void *)dense_fwd_xl9_kernel<EP, P, CAT, CHF>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, XL9_LDS);
+        hipLaunchKernelGGL((dense_fwd_xl9_kernel<EP, P, CAT, CHF>), grid, dim3(512), XL9_LDS, s, a);
+    } else if (variant == 2) {
         (void)hipFuncSetAttribute((const void *)dense_fwd_xl8_kernel<EP, P, CAT, CHF>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, XL_LDS);
         hipLaunchKernelGGL((dense_fwd_xl8_kernel<EP, P, CAT, CHF>), grid, dim3(512), XL_LDS, s, a);
@@ -1613,11 +1761,13 @@ void launch_fwd_xl_one(const GemmArgs &a, dim3 grid, bool dma, hipStream_t s) {
     }
 }
 
-// dma: dense_fwd_xl8_kernel (K % 64 == 0), else dense_fwd_xl_kernel
+// variant 3: dense_fwd_xl9_kernel, 2: dense_fwd_xl8_kernel (both K % 64 == 0),
+// else dense_fwd_xl_kernel
 template <int P, bool CAT>
-void launch_fwd_xl_p(const GemmArgs &a, dim3 grid, bool dma, hipStream_t s) {
+void launch_fwd_xl_p(const GemmArgs &a, dim3 grid, int variant, hipStream_t s) {
 #define FWD_XL(EPv)                                                                                                \
-    (a.c16 ? launch_fwd_xl_one<EPv, P, CAT, true>(a, grid, dma, s) : launch_fwd_xl_one<EPv, P, CAT, false>(a, grid, dma, s))
+    (a.c16 ? launch_fwd_xl_one<EPv, P, CAT, true>(a, grid, variant, s)                                             \
+           : launch_fwd_xl_one<EPv, P, CAT, false>(a, grid, variant, s))
     switch (a.act) {
     case ACT_RELU: FWD_XL(ACT_RELU); break;
     case ACT_ELU: FWD_XL(ACT_ELU); break;

@@ -139,6 +139,7 @@ EXPORTS = {
     "lap_reset_max": (c_int32, [c_void_p, c_void_p]),
     "lap_totals": (c_int32, [c_void_p, c_void_p, c_void_p]),
     "exo_stream_ballast": (c_int32, [c_int32]),
+    "td7_dense_set_xl": (c_int32, [c_int32]),
     "exo_graph_branch_bound": (c_int32, [c_void_p, c_void_p]),
     "lap_store_batch": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_void_p, ctypes.c_float, c_int32, c_void_p, c_void_p]),

@@ -579,6 +579,13 @@ int td7_dense_fwd_cat_w16(int32_t nseg, const float *const *xs_dev, const long *
 int td7_dense_fwd_h(const float *x_dev, const uint16_t *x16_dev, long xsg, long ldx, const float *w_dev,
                     const float *b_dev, float *y_dev, uint16_t *y16_dev, long ysg, long ldy, int32_t groups, int32_t m,
                     int32_t n, int32_t k, int32_t act, const uint16_t *w16_dev, void *stream);
+/* The 256 x 256-tile forward kernel of td7_dense_fwd_h / _cat_h (no
+ * reference counterpart: kernel selection for same-process A/Bs): 0 the
+ * 128 x 256 big kernel, 1 dense_fwd_xl_kernel, 2 dense_fwd_xl8_kernel (two
+ * 64-deep LDS-DMA slices), 3 dense_fwd_xl9_kernel (a 9-slot ring of one
+ * k-step each); the environment's EXO_FWD_XL is the default.  Returns the
+ * previous setting or EXO_EINVAL. */
+int td7_dense_set_xl(int32_t variant);
 /* td7_dense_fwd_cat_h: xs16 = 1 takes every segment as 16-bit values (the
  * AvgL1Norm outputs of td7_avgl1norm_fwd_h), 0 as fp32. */
 int td7_dense_fwd_cat_h(int32_t nseg, const void *const *xs_dev, int32_t xs16, const long *xsg, const long *ldx,

@@ -536,14 +536,27 @@ def test_inference_chain_with_16bit_activations_is_bit_identical(prec):
     assert ah.dtype == torch.float32 and torch.equal(ah, a32)
 
 
+@pytest.fixture(params=[2, 3], ids=["xl8", "xl9"])
+def xl_variant(request):
+    """The 256 x 256-tile forward's kernel (td7_dense_set_xl): 2 the two-slice
+    LDS-DMA kernel (r05), 3 the k-step ring (r06)."""
+    from exo_amd import _native as nat
+    prev = nat.lib().td7_dense_set_xl(request.param)
+    yield request.param
+    nat.lib().td7_dense_set_xl(prev)
+
+
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
 @pytest.mark.parametrize("m,n,k,cat,half_out", [(16384, 1024, 1024, False, True), (16500, 1000, 1024, False, True),
                                                 (16384, 1024, 1024, False, False), (16384, 1024, 1032, False, True),
-                                                (16400, 1024, 1024, True, True), (16384, 520, 2048, False, True)])
-def test_xl_forward_kernel_is_the_gemm_of_rounded_operands(prec, m, n, k, cat, half_out):
+                                                (16400, 1024, 1024, True, True), (16384, 520, 2048, False, True),
+                                                (65536, 256, 64, False, True), (16384, 1024, 320, True, True)])
+def test_xl_forward_kernel_is_the_gemm_of_rounded_operands(prec, m, n, k, cat, half_out, xl_variant):
     """The 256 x 256-tile forward of 16-bit inference chains (r05:
     dense_fwd_xl8_kernel, LDS-DMA staging, at >= 256 such tiles and K % 64 ==
-    0; dense_fwd_xl_kernel otherwise -- K = 1,032 here): 16-bit X (and
+    0; r06: dense_fwd_xl9_kernel, the k-step LDS ring, the same tiles;
+    dense_fwd_xl_kernel otherwise -- K = 1,032 here; K = 64 and 320: shorter
+    than the ring's 7 k-steps in flight, the phantom DMAs past the end): 16-bit X (and
     16-bit [a | zs] segments), ragged M and N (16,500 x 1,000: partial tiles
     both ways), 16-bit or fp32 output -- the GEMM of the rounded operands with
     fp32 accumulation + ELU, to fp32 summation-order tolerance (1e-4; the
