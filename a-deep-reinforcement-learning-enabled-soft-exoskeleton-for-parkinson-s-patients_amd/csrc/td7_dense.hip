@@ -106,7 +106,7 @@ static int g_fwd_xl = -1;
 static int fwd_xl_variant() {
     if (g_fwd_xl < 0) {
         const char *e = std::getenv("EXO_FWD_XL");
-        g_fwd_xl = (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 2;
+        g_fwd_xl = (e && e[0] >= '0' && e[0] <= '7') ? e[0] - '0' : 2;
     }
     return g_fwd_xl;
 }
@@ -311,7 +311,7 @@ extern "C" {
 
 int td7_dense_set_xl(int32_t variant) {
     const int prev = td7dense::fwd_xl_variant();
-    if (variant < 0 || variant > 3) return EXO_EINVAL;
+    if (variant < 0 || variant > 7) return EXO_EINVAL;
     td7dense::g_fwd_xl = variant;
     return prev;
 }

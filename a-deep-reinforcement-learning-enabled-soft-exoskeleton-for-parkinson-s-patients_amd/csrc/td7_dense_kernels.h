@@ -1621,19 +1621,28 @@ __global__ __launch_bounds__(512) void dense_fwd_xl8_kernel(GemmArgs a) {
 // 256-byte bank row; the DMA writes lane-linear (lane l: row 32 w + (l >> 1),
 // slot l & 1) with the chunk permuted on the SOURCE side.  All LDS is the one
 // dynamic array (a second __shared__ object can make hipcc drain vmcnt).
-constexpr int XL9_NS = 9, XL9_D = 7;  // slots; k-steps issued ahead (<= NS - 2, see WAR)
-constexpr int XL9_SLOT = 1024;        // uint32_t4 per slot (16 KB: 256 A rows + 256 B rows x 32 bytes)
-constexpr int XL9_LDS = XL9_NS * XL9_SLOT * 16;  // 144 KB (the epilogue's 128 KB output stage fits)
+// Ring geometry: NS slots of MK k-steps each.  EARLY: the DMA of slot it + D
+// is issued before the iteration's barrier (D = NS - 2: the overwritten slot
+// was last read two iterations back); else after it (D = NS - 1).  Either
+// way the wait at the top of iteration it is for slot it + 1's DMA, so the
+// fragments of the next slot's first k-step are read while this slot's last
+// k-step is multiplied.
+constexpr int XL9_KSLOT = 1024;  // uint32_t4 per k-step in a slot (16 KB)
+constexpr int xl9_lds(int ns, int mk) { return ns * mk * XL9_KSLOT * 16; }
 
-template <int EP, int P, bool CAT, bool CHF>
+template <int EP, int P, bool CAT, bool CHF, int NS, int MK, bool EARLY>
 __global__ __launch_bounds__(512) void dense_fwd_xl9_kernel(GemmArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t4 xl_smem[];
-    constexpr int NS = XL9_NS, D = XL9_D, SLOT = XL9_SLOT;
+    constexpr int D = EARLY ? NS - 2 : NS - 1, KS = XL9_KSLOT, SLOT = MK * KS;
+    // the wait for slot it + 1 at the top of iteration it leaves these DMA
+    // instructions of this wave in flight (2 per k-step)
+    constexpr int VM = 2 * MK * (EARLY ? D - 1 : D - 2);
+    static_assert(D >= 2 && VM <= 62, "ring geometry");
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w >> 2, wn = w & 3;
     const int l31 = lane & 31, lh = lane >> 5;
     const int3 tile = xcd_tile();
     const int i0 = tile.y * XL_BM, j0 = tile.x * XL_BN, g = tile.z;
-    const int K = a.R, nks = K / 16;  // K % 64 == 0 (the launcher's condition)
+    const int K = a.R, nit = K / (16 * MK);  // K % 64 == 0 (the launcher's condition)
     // the rows this lane stages: A row / B column 32 w + (lane >> 1), chunk
     // (lane & 1) ^ ((row >> 3) & 1) of each k-step
     const int sr = 32 * w + (lane >> 1);
@@ -1641,10 +1650,10 @@ __global__ __launch_bounds__(512) void dense_fwd_xl9_kernel(GemmArgs a) {
     const __amdgpu_buffer_rsrc_t rb = rsrc(reinterpret_cast<const float *>(a.b16 + (long)g * a.J * a.R));
     __amdgpu_buffer_rsrc_t ra = CAT ? rsrc(a.cat.p[0]) : rsrc(reinterpret_cast<const float *>(a.a16 + g * a.A.sg));
     int lda = CAT ? a.cat.ld[0] : (int)a.A.si, kbase = 0, seg = 0;
-    auto gseg = [&](int kt) {
+    auto gseg = [&](int kstep) {
         if constexpr (CAT) {  // the k-step's segment (boundaries are multiples of 64)
-            const int s = cat_seg(a.cat, kt * 16);
-            if (s != seg || kt == 0) {
+            const int s = cat_seg(a.cat, kstep * 16);
+            if (s != seg || kstep == 0) {
                 seg = s;
                 const float *p = a.cat.p[0];
                 long gs = a.cat.sg[0];
@@ -1663,27 +1672,31 @@ __global__ __launch_bounds__(512) void dense_fwd_xl9_kernel(GemmArgs a) {
     uint32_t abase = 0;
     auto rows = [&]() { abase = arow ? (uint32_t)((i0 + sr) * lda + 8 * sc - kbase) * 2u : 0u; };
     rows();
-    int slot_issue = 0;  // (s + D) % NS for the next issue
-    auto issue = [&](int s) {
-        uint32_t oa = (uint32_t)BUF_OOB, ob = (uint32_t)BUF_OOB;
-        if (s < nks) {
-            if constexpr (CAT) {
-                const int s0 = seg;
-                gseg(s);
-                if (seg != s0) rows();
-            }
-            const uint32_t kb = (uint32_t)s * 32u;  // 16 k x 2 bytes
-            if (arow) oa = abase + kb;
-            if (bcol) ob = bbase + kb;
-        }
+    int slot_issue = 0;  // (it + D) % NS for the next issue
+    auto issue = [&](int it) {
         uint32_t4 *sl = xl_smem + slot_issue * SLOT;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void *)(sl + w * 64), 16, oa,
-                                                 0, 0, 0);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (__attribute__((address_space(3))) void *)(sl + 512 + w * 64), 16,
-                                                 ob, 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < MK; ++j) {
+            const int ks = it * MK + j;
+            uint32_t oa = (uint32_t)BUF_OOB, ob = (uint32_t)BUF_OOB;
+            if (it < nit) {
+                if constexpr (CAT) {
+                    const int s0 = seg;
+                    gseg(ks);
+                    if (seg != s0) rows();
+                }
+                const uint32_t kb = (uint32_t)ks * 32u;  // 16 k x 2 bytes
+                if (arow) oa = abase + kb;
+                if (bcol) ob = bbase + kb;
+            }
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                ra, (__attribute__((address_space(3))) void *)(sl + j * KS + w * 64), 16, oa, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rb, (__attribute__((address_space(3))) void *)(sl + j * KS + 512 + w * 64), 16, ob, 0, 0, 0);
+        }
         slot_issue = slot_issue + 1 == NS ? 0 : slot_issue + 1;
     };
-    // this lane's fragment addresses inside a slot (uint32_t4 units)
+    // this lane's fragment addresses inside a k-step block (uint32_t4 units)
     int fa_off[4], fb_off[2];
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
@@ -1695,12 +1708,11 @@ __global__ __launch_bounds__(512) void dense_fwd_xl9_kernel(GemmArgs a) {
         const int r = wn * 64 + 32 * y + l31;
         fb_off[y] = 512 + r * 2 + (lh ^ ((r >> 3) & 1));
     }
-    auto frag = [&](int slot, uint32_t4 (&af)[4], uint32_t4 (&bf)[2]) {
-        const uint32_t4 *sl = xl_smem + slot * SLOT;
+    auto frag = [&](const uint32_t4 *kb, uint32_t4 (&af)[4], uint32_t4 (&bf)[2]) {
 #pragma unroll
-        for (int x = 0; x < 4; ++x) af[x] = sl[fa_off[x]];
+        for (int x = 0; x < 4; ++x) af[x] = kb[fa_off[x]];
 #pragma unroll
-        for (int y = 0; y < 2; ++y) bf[y] = sl[fb_off[y]];
+        for (int y = 0; y < 2; ++y) bf[y] = kb[fb_off[y]];
     };
     floatx16 acc[4][2];
 #pragma unroll
@@ -1711,30 +1723,40 @@ __global__ __launch_bounds__(512) void dense_fwd_xl9_kernel(GemmArgs a) {
             for (int e = 0; e < 16; ++e) acc[x][y][e] = 0.f;
     if constexpr (CAT) gseg(0), rows();
 #pragma unroll
-    for (int s = 0; s < D; ++s) issue(s);
-    // k-step 0 retired (6 k-steps x 2 DMAs after it), every wave's
-    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    for (int it = 0; it < D; ++it) issue(it);
+    // slot 0's DMA retired (D - 1 slots after it), every wave's
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * MK * (D - 1)) : "memory");
     __builtin_amdgcn_s_barrier();
     uint32_t4 fa[2][4], fb[2][2];
-    frag(0, fa[0], fb[0]);
-    int slot_read = 1;  // slot of k-step s + 1
-    // two k-steps per trip: the fragment registers alternate by parity (no
-    // runtime-indexed register arrays); nks is even (K % 64 == 0)
-    for (int s = 0; s < nks; s += 2) {
+    frag(xl_smem, fa[0], fb[0]);
+    int slot_next = 1;  // slot of iteration it + 1
+    int slot_cur = 0;
+    // two k-steps per trip when MK == 1 (register parity = k-step parity)
+    constexpr int TRIP = MK == 1 ? 2 : 1;
+    for (int it0 = 0; it0 < nit; it0 += TRIP) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            issue(s + h + D);
-            asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        for (int h = 0; h < TRIP; ++h) {
+            const int it = it0 + h;
+            if constexpr (EARLY) issue(it + D);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM) : "memory");
             __builtin_amdgcn_s_barrier();
-            frag(slot_read, fa[h ^ 1], fb[h ^ 1]);  // k-step s + h + 1 (past the end: a slot nothing uses)
-            slot_read = slot_read + 1 == NS ? 0 : slot_read + 1;
-            asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");  // the reads of k-step s + h
-            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (!EARLY) issue(it + D);
 #pragma unroll
-            for (int x = 0; x < 4; ++x)
+            for (int j = 0; j < MK; ++j) {
+                const int par = (MK == 1 ? h : j) & 1;
+                // k-step it * MK + j + 1's fragments (past the end: a slot nothing uses)
+                const uint32_t4 *nk = j + 1 < MK ? xl_smem + slot_cur * SLOT + (j + 1) * KS : xl_smem + slot_next * SLOT;
+                frag(nk, fa[par ^ 1], fb[par ^ 1]);
+                asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");  // k-step it * MK + j's reads
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                for (int y = 0; y < 2; ++y) acc[x][y] = mfma32_k16<P>(fa[h][x], fb[h][y], acc[x][y]);
-            __builtin_amdgcn_sched_barrier(0);
+                for (int x = 0; x < 4; ++x)
+#pragma unroll
+                    for (int y = 0; y < 2; ++y) acc[x][y] = mfma32_k16<P>(fa[par][x], fb[par][y], acc[x][y]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            slot_cur = slot_next;
+            slot_next = slot_next + 1 == NS ? 0 : slot_next + 1;
         }
     }
     // every DMA (the phantom ones included) and every fragment read retired,
@@ -1744,12 +1766,26 @@ __global__ __launch_bounds__(512) void dense_fwd_xl9_kernel(GemmArgs a) {
     xl8_epilogue<EP, P, CHF>(a, acc, i0, j0, g);
 }
 
+template <int EP, int P, bool CAT, bool CHF, int NS, int MK, bool EARLY>
+void launch_xl9(const GemmArgs &a, dim3 grid, hipStream_t s) {
+    constexpr int lds = xl9_lds(NS, MK);
+    (void)hipFuncSetAttribute((const void *)dense_fwd_xl9_kernel<EP, P, CAT, CHF, NS, MK, EARLY>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL((dense_fwd_xl9_kernel<EP, P, CAT, CHF, NS, MK, EARLY>), grid, dim3(512), lds, s, a);
+}
+
 template <int EP, int P, bool CAT, bool CHF>
 void launch_fwd_xl_one(const GemmArgs &a, dim3 grid, int variant, hipStream_t s) {
     if (variant == 3) {
-        (void)hipFuncSetAttribute((const void *)dense_fwd_xl9_kernel<EP, P, CAT, CHF>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, XL9_LDS);
-        hipLaunchKernelGGL((dense_fwd_xl9_kernel<EP, P, CAT, CHF>), grid, dim3(512), XL9_LDS, s, a);
+        launch_xl9<EP, P, CAT, CHF, 9, 1, true>(a, grid, s);
+    } else if (variant == 4) {
+        launch_xl9<EP, P, CAT, CHF, 9, 1, false>(a, grid, s);
+    } else if (variant == 5) {
+        launch_xl9<EP, P, CAT, CHF, 10, 1, false>(a, grid, s);
+    } else if (variant == 6) {
+        launch_xl9<EP, P, CAT, CHF, 5, 2, false>(a, grid, s);
+    } else if (variant == 7) {
+        launch_xl9<EP, P, CAT, CHF, 4, 2, false>(a, grid, s);
     } else if (variant == 2) {
         (void)hipFuncSetAttribute((const void *)dense_fwd_xl8_kernel<EP, P, CAT, CHF>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, XL_LDS);

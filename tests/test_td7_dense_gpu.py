@@ -536,7 +536,7 @@ def test_inference_chain_with_16bit_activations_is_bit_identical(prec):
     assert ah.dtype == torch.float32 and torch.equal(ah, a32)
 
 
-@pytest.fixture(params=[2, 3], ids=["xl8", "xl9"])
+@pytest.fixture(params=[2, 3, 4, 5, 6, 7], ids=["xl8", "xl9", "v4", "v5", "v6", "v7"])
 def xl_variant(request):
     """The 256 x 256-tile forward's kernel (td7_dense_set_xl): 2 the two-slice
     LDS-DMA kernel (r05), 3 the k-step ring (r06)."""
