@@ -100,13 +100,14 @@ int launch_wgrad(const WgradArgs &a, int groups, int act, int prec, hipStream_t 
 }
 
 // the 256 x 256-tile forward's kernel: EXO_FWD_XL (0 dense_fwd_big_kernel,
-// 1 dense_fwd_xl_kernel, 2 dense_fwd_xl8_kernel, 3 dense_fwd_xl9_kernel; the
-// K % 64 == 0 kernels fall back to 1 elsewhere), td7_dense_set_xl at run time
+// 1 dense_fwd_xl_kernel, 2 dense_fwd_xl8_kernel; the K % 64 == 0 kernel
+// falls back to 1 elsewhere), td7_dense_set_xl at run time (r06: the A/Bs of
+// profiles/r06_xl ran two more 256 x 256 kernels through it)
 static int g_fwd_xl = -1;
 static int fwd_xl_variant() {
     if (g_fwd_xl < 0) {
         const char *e = std::getenv("EXO_FWD_XL");
-        g_fwd_xl = (e && e[0] >= '0' && e[0] <= '7') ? e[0] - '0' : 2;
+        g_fwd_xl = (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 2;
     }
     return g_fwd_xl;
 }
@@ -176,8 +177,7 @@ int launch_fwd(const GemmArgs &a, int groups_grid, int prec, hipStream_t s, bool
     // 16-bit X and W at >= 256 tiles of 256 x 256 (r05): dense_fwd_xl8_kernel
     // where K % 64 == 0, else dense_fwd_xl_kernel; EXO_FWD_XL=0 keeps
     // dense_fwd_big_kernel, EXO_FWD_XL=1 dense_fwd_xl_kernel everywhere
-    // (r06: EXO_FWD_XL=3 dense_fwd_xl9_kernel, the k-step LDS ring;
-    // td7_dense_set_xl switches it at run time for same-process A/Bs)
+    // (td7_dense_set_xl switches it at run time for same-process A/Bs)
     const int xl_v = fwd_xl_variant();
     const bool xl_on = xl_v != 0;
     const int xl_var = (xl_v >= 2 && a.R % XL_BK == 0) ? xl_v : 1;
@@ -311,7 +311,7 @@ extern "C" {
 
 int td7_dense_set_xl(int32_t variant) {
     const int prev = td7dense::fwd_xl_variant();
-    if (variant < 0 || variant > 7) return EXO_EINVAL;
+    if (variant < 0 || variant > 2) return EXO_EINVAL;
     td7dense::g_fwd_xl = variant;
     return prev;
 }

@@ -1600,193 +1600,9 @@ __global__ __launch_bounds__(512) void dense_fwd_xl8_kernel(GemmArgs a) {
     xl8_epilogue<EP, P, CHF>(a, acc, i0, j0, g);
 }
 
-// r06: the same 256 x 256 tile, 8 waves and MFMA order as dense_fwd_xl8_kernel,
-// staged through a ring of 9 LDS slots of ONE k-step each (16 KB: the 16-deep
-// k range of the tile's 256 A rows and 256 B columns, 2 chunks of 16 bytes per
-// row) instead of two 64-deep slices: the LDS-DMA of k-step s + 7 is issued
-// while k-step s is multiplied, so 7 k-steps (112 KB) are in flight per CU
-// where xl8 had one slice (64 KB) and drained it at every slice end
-// (vmcnt(0) + barrier: its DMA alone took 155 us of the 194, profiles/r05_xl).
-// Per k-step: issue DMA(s + 7) -> s_waitcnt vmcnt(12) (this wave's DMA of
-// k-step s + 1 retired: 6 k-steps x 2 instructions issued after it) -> raw
-// s_barrier (every wave's DMA of s + 1 retired: RAW) -> fragment reads of s + 1
-// -> s_waitcnt lgkmcnt(6) (the reads of s, issued one iteration earlier) ->
-// the 8 MFMAs of s.  WAR: DMA(s + 7) overwrites the slot of k-step s - 2, whose
-// fragments were read in iteration s - 3 and retired in iteration s - 2,
-// before barrier s - 1 that every wave passed before issuing it.  Past the
-// last k-step the DMAs read at BUF_OOB (zeros) into slots nothing reads, so
-// the vmcnt counts stay exact.  Slot layout: row r (A rows, then B columns) at
-// 32 bytes, chunk c in 16-byte slot c ^ ((r >> 3) & 1) -- a fragment read's
-// 16-lane pass (16 consecutive rows, one chunk) covers all 16 slots of a
-// 256-byte bank row; the DMA writes lane-linear (lane l: row 32 w + (l >> 1),
-// slot l & 1) with the chunk permuted on the SOURCE side.  All LDS is the one
-// dynamic array (a second __shared__ object can make hipcc drain vmcnt).
-// Ring geometry: NS slots of MK k-steps each.  EARLY: the DMA of slot it + D
-// is issued before the iteration's barrier (D = NS - 2: the overwritten slot
-// was last read two iterations back); else after it (D = NS - 1).  Either
-// way the wait at the top of iteration it is for slot it + 1's DMA, so the
-// fragments of the next slot's first k-step are read while this slot's last
-// k-step is multiplied.
-constexpr int XL9_KSLOT = 1024;  // uint32_t4 per k-step in a slot (16 KB)
-constexpr int xl9_lds(int ns, int mk) { return ns * mk * XL9_KSLOT * 16; }
-
-template <int EP, int P, bool CAT, bool CHF, int NS, int MK, bool EARLY>
-__global__ __launch_bounds__(512) void dense_fwd_xl9_kernel(GemmArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t4 xl_smem[];
-    constexpr int D = EARLY ? NS - 2 : NS - 1, KS = XL9_KSLOT, SLOT = MK * KS;
-    // the wait for slot it + 1 at the top of iteration it leaves these DMA
-    // instructions of this wave in flight (2 per k-step)
-    constexpr int VM = 2 * MK * (EARLY ? D - 1 : D - 2);
-    static_assert(D >= 2 && VM <= 62, "ring geometry");
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w >> 2, wn = w & 3;
-    const int l31 = lane & 31, lh = lane >> 5;
-    const int3 tile = xcd_tile();
-    const int i0 = tile.y * XL_BM, j0 = tile.x * XL_BN, g = tile.z;
-    const int K = a.R, nit = K / (16 * MK);  // K % 64 == 0 (the launcher's condition)
-    // the rows this lane stages: A row / B column 32 w + (lane >> 1), chunk
-    // (lane & 1) ^ ((row >> 3) & 1) of each k-step
-    const int sr = 32 * w + (lane >> 1);
-    const int sc = (lane & 1) ^ ((sr >> 3) & 1);
-    const __amdgpu_buffer_rsrc_t rb = rsrc(reinterpret_cast<const float *>(a.b16 + (long)g * a.J * a.R));
-    __amdgpu_buffer_rsrc_t ra = CAT ? rsrc(a.cat.p[0]) : rsrc(reinterpret_cast<const float *>(a.a16 + g * a.A.sg));
-    int lda = CAT ? a.cat.ld[0] : (int)a.A.si, kbase = 0, seg = 0;
-    auto gseg = [&](int kstep) {
-        if constexpr (CAT) {  // the k-step's segment (boundaries are multiples of 64)
-            const int s = cat_seg(a.cat, kstep * 16);
-            if (s != seg || kstep == 0) {
-                seg = s;
-                const float *p = a.cat.p[0];
-                long gs = a.cat.sg[0];
-                int ld = a.cat.ld[0], kb = 0;
-#pragma unroll
-                for (int m = 1; m < CAT_MAX; ++m)
-                    if (s == m) p = a.cat.p[m], gs = a.cat.sg[m], ld = a.cat.ld[m], kb = a.cat.kb[m];
-                ra = rsrc(reinterpret_cast<const float *>(reinterpret_cast<const uint16_t *>(p) + g * gs));
-                lda = ld;
-                kbase = kb;
-            }
-        }
-    };
-    const bool arow = i0 + sr < a.I, bcol = j0 + sr < a.J;
-    const uint32_t bbase = bcol ? (uint32_t)((j0 + sr) * a.R + 8 * sc) * 2u : 0u;
-    uint32_t abase = 0;
-    auto rows = [&]() { abase = arow ? (uint32_t)((i0 + sr) * lda + 8 * sc - kbase) * 2u : 0u; };
-    rows();
-    int slot_issue = 0;  // (it + D) % NS for the next issue
-    auto issue = [&](int it) {
-        uint32_t4 *sl = xl_smem + slot_issue * SLOT;
-#pragma unroll
-        for (int j = 0; j < MK; ++j) {
-            const int ks = it * MK + j;
-            uint32_t oa = (uint32_t)BUF_OOB, ob = (uint32_t)BUF_OOB;
-            if (it < nit) {
-                if constexpr (CAT) {
-                    const int s0 = seg;
-                    gseg(ks);
-                    if (seg != s0) rows();
-                }
-                const uint32_t kb = (uint32_t)ks * 32u;  // 16 k x 2 bytes
-                if (arow) oa = abase + kb;
-                if (bcol) ob = bbase + kb;
-            }
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                ra, (__attribute__((address_space(3))) void *)(sl + j * KS + w * 64), 16, oa, 0, 0, 0);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                rb, (__attribute__((address_space(3))) void *)(sl + j * KS + 512 + w * 64), 16, ob, 0, 0, 0);
-        }
-        slot_issue = slot_issue + 1 == NS ? 0 : slot_issue + 1;
-    };
-    // this lane's fragment addresses inside a k-step block (uint32_t4 units)
-    int fa_off[4], fb_off[2];
-#pragma unroll
-    for (int x = 0; x < 4; ++x) {
-        const int r = wm * 128 + 32 * x + l31;
-        fa_off[x] = r * 2 + (lh ^ ((r >> 3) & 1));
-    }
-#pragma unroll
-    for (int y = 0; y < 2; ++y) {
-        const int r = wn * 64 + 32 * y + l31;
-        fb_off[y] = 512 + r * 2 + (lh ^ ((r >> 3) & 1));
-    }
-    auto frag = [&](const uint32_t4 *kb, uint32_t4 (&af)[4], uint32_t4 (&bf)[2]) {
-#pragma unroll
-        for (int x = 0; x < 4; ++x) af[x] = kb[fa_off[x]];
-#pragma unroll
-        for (int y = 0; y < 2; ++y) bf[y] = kb[fb_off[y]];
-    };
-    floatx16 acc[4][2];
-#pragma unroll
-    for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int y = 0; y < 2; ++y)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[x][y][e] = 0.f;
-    if constexpr (CAT) gseg(0), rows();
-#pragma unroll
-    for (int it = 0; it < D; ++it) issue(it);
-    // slot 0's DMA retired (D - 1 slots after it), every wave's
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * MK * (D - 1)) : "memory");
-    __builtin_amdgcn_s_barrier();
-    uint32_t4 fa[2][4], fb[2][2];
-    frag(xl_smem, fa[0], fb[0]);
-    int slot_next = 1;  // slot of iteration it + 1
-    int slot_cur = 0;
-    // two k-steps per trip when MK == 1 (register parity = k-step parity)
-    constexpr int TRIP = MK == 1 ? 2 : 1;
-    for (int it0 = 0; it0 < nit; it0 += TRIP) {
-#pragma unroll
-        for (int h = 0; h < TRIP; ++h) {
-            const int it = it0 + h;
-            if constexpr (EARLY) issue(it + D);
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM) : "memory");
-            __builtin_amdgcn_s_barrier();
-            if constexpr (!EARLY) issue(it + D);
-#pragma unroll
-            for (int j = 0; j < MK; ++j) {
-                const int par = (MK == 1 ? h : j) & 1;
-                // k-step it * MK + j + 1's fragments (past the end: a slot nothing uses)
-                const uint32_t4 *nk = j + 1 < MK ? xl_smem + slot_cur * SLOT + (j + 1) * KS : xl_smem + slot_next * SLOT;
-                frag(nk, fa[par ^ 1], fb[par ^ 1]);
-                asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");  // k-step it * MK + j's reads
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int x = 0; x < 4; ++x)
-#pragma unroll
-                    for (int y = 0; y < 2; ++y) acc[x][y] = mfma32_k16<P>(fa[par][x], fb[par][y], acc[x][y]);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            slot_cur = slot_next;
-            slot_next = slot_next + 1 == NS ? 0 : slot_next + 1;
-        }
-    }
-    // every DMA (the phantom ones included) and every fragment read retired,
-    // every wave past its last read: the stage is idle for the epilogue
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __syncthreads();
-    xl8_epilogue<EP, P, CHF>(a, acc, i0, j0, g);
-}
-
-template <int EP, int P, bool CAT, bool CHF, int NS, int MK, bool EARLY>
-void launch_xl9(const GemmArgs &a, dim3 grid, hipStream_t s) {
-    constexpr int lds = xl9_lds(NS, MK);
-    (void)hipFuncSetAttribute((const void *)dense_fwd_xl9_kernel<EP, P, CAT, CHF, NS, MK, EARLY>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipLaunchKernelGGL((dense_fwd_xl9_kernel<EP, P, CAT, CHF, NS, MK, EARLY>), grid, dim3(512), lds, s, a);
-}
-
 template <int EP, int P, bool CAT, bool CHF>
 void launch_fwd_xl_one(const GemmArgs &a, dim3 grid, int variant, hipStream_t s) {
-    if (variant == 3) {
-        launch_xl9<EP, P, CAT, CHF, 9, 1, true>(a, grid, s);
-    } else if (variant == 4) {
-        launch_xl9<EP, P, CAT, CHF, 9, 1, false>(a, grid, s);
-    } else if (variant == 5) {
-        launch_xl9<EP, P, CAT, CHF, 10, 1, false>(a, grid, s);
-    } else if (variant == 6) {
-        launch_xl9<EP, P, CAT, CHF, 5, 2, false>(a, grid, s);
-    } else if (variant == 7) {
-        launch_xl9<EP, P, CAT, CHF, 4, 2, false>(a, grid, s);
-    } else if (variant == 2) {
+    if (variant == 2) {
         (void)hipFuncSetAttribute((const void *)dense_fwd_xl8_kernel<EP, P, CAT, CHF>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, XL_LDS);
         hipLaunchKernelGGL((dense_fwd_xl8_kernel<EP, P, CAT, CHF>), grid, dim3(512), XL_LDS, s, a);
@@ -1797,8 +1613,7 @@ void launch_fwd_xl_one(const GemmArgs &a, dim3 grid, int variant, hipStream_t s)
     }
 }
 
-// variant 3: dense_fwd_xl9_kernel, 2: dense_fwd_xl8_kernel (both K % 64 == 0),
-// else dense_fwd_xl_kernel
+// variant 2: dense_fwd_xl8_kernel (K % 64 == 0), else dense_fwd_xl_kernel
 template <int P, bool CAT>
 void launch_fwd_xl_p(const GemmArgs &a, dim3 grid, int variant, hipStream_t s) {
 #define FWD_XL(EPv)                                                                                                \

@@ -582,9 +582,8 @@ int td7_dense_fwd_h(const float *x_dev, const uint16_t *x16_dev, long xsg, long 
 /* The 256 x 256-tile forward kernel of td7_dense_fwd_h / _cat_h (no
  * reference counterpart: kernel selection for same-process A/Bs): 0 the
  * 128 x 256 big kernel, 1 dense_fwd_xl_kernel, 2 dense_fwd_xl8_kernel (two
- * 64-deep LDS-DMA slices), 3 dense_fwd_xl9_kernel (a 9-slot ring of one
- * k-step each); the environment's EXO_FWD_XL is the default.  Returns the
- * previous setting or EXO_EINVAL. */
+ * 64-deep LDS-DMA slices); the environment's EXO_FWD_XL is the default.
+ * Returns the previous setting or EXO_EINVAL. */
 int td7_dense_set_xl(int32_t variant);
 /* td7_dense_fwd_cat_h: xs16 = 1 takes every segment as 16-bit values (the
  * AvgL1Norm outputs of td7_avgl1norm_fwd_h), 0 as fp32. */
