@@ -89,6 +89,15 @@ struct Urdf {           // filled on the host (exo_create) and passed by value
     double com3[3];     // auxlink3 CoM in its frame (exo_v3.urdf:84)
     double lo[5], hi[5];// revolute limits (exo_v3.urdf:17,37,57,77,97)
     double kz[14][3];   // prismatic joints 5..18: axis (0 0 1) of the joint frame in the parent frame
+    // row-parallel step (exo_step_rp.hip): lane r's actuator j = min(r, 6) anchor
+    // rows, [0..2] U.xyz (links 9, 12) or U.kbase (the base-fixed links) of
+    // K_LINK[2j], [3..5] U.xyz of K_LINK[2j + 1] -- read per lane with the
+    // kernel-start loads instead of a runtime index per link
+    double anc[8][6];
+    // and its joint-target limits (finish_solve): lane r < 5 drives joint
+    // (r == 0 ? 1 : r == 1 ? 2 : r == 2 ? 0 : r): {lo, hi} of the joint, then
+    // check_movement_boundaries' degree bounds (joints 0..3; 0 for the rest)
+    double lim[8][4];
 };
 
 // Multibody physics mode (csrc/exo_multibody.hip): <inertial> data of the arm
@@ -507,10 +516,25 @@ inline void build_urdf(Urdf &U) {
         for (int a = 0; a < 3; ++a) U.xyz[j][a] = J_XYZ[j][a];
     for (int k = 0; k < 5; ++k)
         for (int a = 0; a < 3; ++a) U.kbase[k][a] = J_XYZ[14 + k][a] + (a == 2 ? 0.1 : 0.0);
+    for (int r = 0; r < 8; ++r) {
+        const int j = r < 7 ? r : 6, l1 = K_LINK[2 * j], l2 = K_LINK[2 * j + 1];
+        for (int a = 0; a < 3; ++a) {
+            U.anc[r][a] = l1 >= 14 ? U.kbase[l1 - 14][a] : U.xyz[l1][a];
+            U.anc[r][3 + a] = U.xyz[l2][a];
+        }
+    }
     U.com3[0] = 0.0; U.com3[1] = 0.5; U.com3[2] = -0.0;
     const double lo[5] = {-1.3962633609772, -0.69813168048859, -2.6441738605499, -0.034906584769487, -1.5184364318848};
     const double hi[5] = {1.3962633609772, 2.8187066316605, 0.78539800643921, 2.6179938726127, 1.3962633609772};
     for (int j = 0; j < 5; ++j) { U.lo[j] = lo[j]; U.hi[j] = hi[j]; }
+    const double blo[4] = {-80, -40, -151.5, -10}, bhi[4] = {80, 160.5, 33.5, 150}; // Exoskeleton_env.py:594-605
+    for (int r = 0; r < 8; ++r) {
+        const int jt = (r == 0) ? 1 : (r == 1) ? 2 : (r == 2) ? 0 : r;
+        U.lim[r][0] = jt < 5 ? U.lo[jt] : 0.0;
+        U.lim[r][1] = jt < 5 ? U.hi[jt] : 0.0;
+        U.lim[r][2] = jt < 4 ? blo[jt] : 0.0;
+        U.lim[r][3] = jt < 4 ? bhi[jt] : 0.0;
+    }
 }
 
 } // namespace exo

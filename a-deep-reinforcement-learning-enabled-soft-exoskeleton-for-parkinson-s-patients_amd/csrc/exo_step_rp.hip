@@ -39,7 +39,7 @@ __device__ unsigned long long *g_exo_stamps;
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                             \
         __builtin_amdgcn_sched_barrier(0);                                                                        \
         if (g_exo_stamps && (threadIdx.x & 63) == __builtin_amdgcn_readfirstlane(threadIdx.x & 63))               \
-            g_exo_stamps[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + (k)] = _t;                                                      \
+            g_exo_stamps[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + (k)] = _t;                 \
     } while (0)
 // RK45 step attempts (accepted + rejected) of each env's two solves, [2][N]
 // (tools/rk45_hist.py: the configs[3] slowest-env histogram)
@@ -343,12 +343,26 @@ __device__ __forceinline__ void rk_load(const Dev &S, int e, int sub, int grp, R
     s.in_step = (fl & 2) != 0;
 }
 
-// CoM of link `link` (one of the 14 actuator anchors) given the FK frames.
-__device__ __forceinline__ void anchor(const Urdf &U, int link, const double *R2, const double *p0, const double *R4,
-                                       const double *p3, double *o) {
-    if (link == 5 || link == 6) xform(R4, p3, U.xyz[link], o);
-    else if (link >= 14) { o[0] = U.kbase[link - 14][0]; o[1] = U.kbase[link - 14][1]; o[2] = U.kbase[link - 14][2]; }
-    else xform(R2, p0, U.xyz[link], o);
+// CoMs of the lane's two k-links (actuator j: K_LINK[2j], K_LINK[2j + 1])
+// from the FK frames, given their rows v1, v2 (U.anc, loaded with the
+// kernel-start batch).  The first anchors of actuators 0, 1 (links 9, 12) sit
+// on the humerus, those of 2..6 on the base (U.kbase); the second anchors of
+// actuators 0, 1 (links 5, 6) on the forearm, those of 2..6 on the humerus.
+// Same operands and operations as the per-link form (a runtime index into the
+// by-value kernel argument per link, U.xyz[link], compiled to a load from the
+// kernarg segment behind a vmcnt(0) in each divergent branch): bit-identical.
+__device__ __forceinline__ void anchors(int j, const double *v1, const double *v2, const double *R2,
+                                        const double *p0, const double *R4, const double *p3, double *k1, double *k2) {
+    double h1[3], f2[3], h2[3];
+    xform(R2, p0, v1, h1);
+    xform(R4, p3, v2, f2);
+    xform(R2, p0, v2, h2);
+    const bool arm = j < 2;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        k1[d] = arm ? h1[d] : v1[d];
+        k2[d] = arm ? f2[d] : h2[d];
+    }
 }
 
 // The solve of this lane's row with the selected RHS exchange (template PULL
@@ -400,34 +414,53 @@ __device__ __forceinline__ RowM load_rows(const Dev &S, int e, int r, int gbase)
     return M0;
 }
 
+// The actuated lane r's joint (:421-433): lane r holds q[r]; joint 0
+// (shoulder z) <- q[2], 1 (y) <- q[0], 2 (x) <- q[1], 3 (elbow y) <- q[3],
+// 4 <- q[4] (lanes 5..7: r, unused)
+__device__ __forceinline__ int lane_joint(int r) { return (r == 0) ? 1 : (r == 1) ? 2 : (r == 2) ? 0 : r; }
+
+// The operands of finish_solve that do not depend on the solve, loaded before
+// it instead of after it (each was a memory latency on the slowest wave's
+// tail): the imu sample of the lane's joint at counter c (issued right before
+// the solve), and the joint's position before the motor step (with the
+// kernel-start batch; only this lane writes it, after the solve).
+struct Targets {
+    double imu_v, q0;
+    double lim[4];  // U.lim[r]: the joint's {lo, hi} and the boundary check's degree bounds
+};
+__device__ __forceinline__ void load_lims(const Urdf &U, int r, Targets &tg) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tg.lim[k] = U.lim[r][k];
+}
+__device__ __forceinline__ double imu_at(const Dev &S, int motion, int joint, int c) {
+    const int col = (joint == 0) ? 4 : (joint == 1) ? 3 : (joint == 2) ? 2 : (joint == 3) ? 0 : 1;
+    return S.imu[((size_t)motion * 5 + col) * S.Lmax + c];
+}
+
 // After a solve of the step whose counter was c (:417-433): the amplitude
 // into info (both groups), then -- actuated group -- the joint targets, the
 // idealised motor step or the multibody targets, and the
 // joint-range violation count.
-__device__ __forceinline__ void finish_solve(const Dev &S, const Urdf &U, int e, int grp, int r, int ebase, int c,
-                                             int motion, double qr, float *info) {
+__device__ __forceinline__ void finish_solve(const Dev &S, const Urdf &U, int e, int grp, int r, int ebase,
+                                             const Targets &tg, double qr, float *info) {
     const int N = S.N;
     const double qdeg = qr * (180 / PI); // :417-418
     if (info && r < 7) info[(size_t)e * INFO + (grp == 0 ? 14 : 28) + r] = (float)qdeg;
     if (grp != 0) return;
     // ---- :421-433 joint targets and the idealised motor step
-    // lane r holds q[r]: joint 0 (shoulder z) <- q[2], 1 (y) <- q[0], 2 (x) <- q[1], 3 (elbow y) <- q[3]
-    const int joint = (r == 0) ? 1 : (r == 1) ? 2 : (r == 2) ? 0 : r; // r = 3, 4 -> joints 3, 4
-    const double *imu = S.imu + (size_t)motion * 5 * S.Lmax;
-    const int col = (joint == 0) ? 4 : (joint == 1) ? 3 : (joint == 2) ? 2 : (joint == 3) ? 0 : 1;
-    const double ang = imu[col * S.Lmax + c] + (joint < 4 ? qdeg : 0.0);
+    const int joint = lane_joint(r);
+    const double ang = tg.imu_v + (joint < 4 ? qdeg : 0.0);
     bool viol = false;
     if (r < 5) {
         if (S.mb_tgt) { // multibody mode: exo_multibody_kernel runs stepSimulation next
             S.mb_tgt[(size_t)joint * N + e] = ang * (PI / 180);
             if (r == 0) S.mb_flag[e] = 1;
         } else {
-            const double q0 = S.phys_q[(size_t)joint * N + e];
+            const double q0 = tg.q0;
             const double nq = q0 + 0.1 * (ang * (PI / 180) - q0);
-            S.phys_q[(size_t)joint * N + e] = fmin(fmax(nq, U.lo[joint]), U.hi[joint]);
+            S.phys_q[(size_t)joint * N + e] = fmin(fmax(nq, tg.lim[0]), tg.lim[1]);
         }
-        const double lo[4] = {-80, -40, -151.5, -10}, hi[4] = {80, 160.5, 33.5, 150};
-        if (joint < 4) viol = !(lo[joint] < ang && ang < hi[joint]); // check_movement_boundaries (:594-605)
+        if (joint < 4) viol = !(tg.lim[2] < ang && ang < tg.lim[3]); // check_movement_boundaries (:594-605)
     }
     const unsigned long long m = __ballot(viol);
     if (r == 0 && ((m >> ebase) & 0xFull)) S.viol[e] += 1;
@@ -448,8 +481,13 @@ __device__ void resume_env(const Dev &S, const Urdf &U, int e, int sub, int grp,
     const bool mine = (pend >> grp) & 1;
     int res = 1;
     RkState st;
+    Targets tg{0.0, 0.0};
     if (mine) {
         const RowM M0 = load_rows(S, e, r, gbase);
+        const int joint = lane_joint(r);
+        tg.imu_v = imu_at(S, S.motion[e], joint, S.counts[e] - 1);
+        tg.q0 = S.phys_q[(size_t)(joint < 5 ? joint : 4) * S.N + e];
+        load_lims(U, r, tg);
         double T;
         rk_load(S, e, sub, grp, st, T);
         res = solve_rows<PULL, EPB>(M0, r, T, st, false, S.budget);
@@ -462,7 +500,7 @@ __device__ void resume_env(const Dev &S, const Urdf &U, int e, int sub, int grp,
 #ifdef EXO_STAMPS
     if (g_exo_rksteps && r == 0) g_exo_rksteps[(size_t)grp * S.N + e] = st.guard;  // the solve's total attempts
 #endif
-    finish_solve(S, U, e, grp, r, ebase, S.counts[e] - 1, S.motion[e], st.q, info);
+    finish_solve(S, U, e, grp, r, ebase, tg, st.q, info);
 }
 
 // 16 envs (4 wavefronts) per workgroup: the state is SoA over envs, so one
@@ -497,9 +535,15 @@ __global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
     const float *a = act + (size_t)e * ACT;
 
     // ---- forward kinematics of the state left by the last stepSimulation (all lanes)
-    double q5[5], refo[6], refn[6];
-#pragma unroll
-    for (int j = 0; j < 5; ++j) q5[j] = S.phys_q[(size_t)j * N + e];
+    // the five joint sincos are spread over the env's lanes (lane sub takes
+    // joint sub % 5) and shared through wave-private LDS slots: one sincos
+    // chain per lane instead of five in a row (ocml's sincos ends in a
+    // divergent-branch check, so five calls did not overlap)
+    __shared__ double2 s_fk[64 * EPB / 4];
+    const int jt = lane_joint(r), jq = jt < 5 ? jt : 4;
+    const double qk = S.phys_q[(size_t)(sub % 5) * N + e];
+    const double qj = S.phys_q[(size_t)jq * N + e];  // this lane's joint before the motor step (finish_solve)
+    double refo[6], refn[6];
 #pragma unroll
     for (int j = 0; j < 6; ++j) refo[j] = S.ref[(size_t)j * N + e];
     // ---- every other load of the step, issued now: one memory latency for the
@@ -511,6 +555,12 @@ __global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
     for (int d = 0; d < 3; ++d) {
         sh1[d] = S.shift[(size_t)((2 * j) * 3 + d) * N + e];
         sh2[d] = S.shift[(size_t)((2 * j + 1) * 3 + d) * N + e];
+    }
+    double av1[3], av2[3];  // this lane's anchor rows (anchors())
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        av1[d] = U.anc[r][d];
+        av2[d] = U.anc[r][3 + d];
     }
     const double pa_j = S.prev_a[(size_t)j * N + e];
     const double pa2_j = S.prev2_a[(size_t)j * N + e];
@@ -525,16 +575,31 @@ __global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
     for (int d = 0; d < 3; ++d) posv_old[d] = S.posv[(size_t)(j * 3 + d) * N + e];
     const RowM M0 = load_rows(S, e, r, gbase);
     const int seq = S.seq[e], motion = S.motion[e];
+    Targets tg;
+    tg.q0 = qj;
+    load_lims(U, r, tg);
+#ifdef EXO_STAMPS_MEMWAIT
+    // diagnostic: when the kernel-start loads have all returned (serialises the prologue)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    STAMP(8);
+#endif
     double R2[9], R4[9], p0[3], p3[3];
     {
-        double Rt[9], R0[9], R1[9], R3[9], s, cc;
+        double sk, ck;
+        sincos(qk, &sk, &ck);
+        s_fk[threadIdx.x] = make_double2(sk, ck);
+        __builtin_amdgcn_wave_barrier();
+        double2 sc[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) sc[k] = s_fk[(threadIdx.x & ~15u) + k];  // lane k of the env: joint k
+        double Rt[9], R0[9], R1[9], R3[9];
         p0[0] = U.xyz[0][0]; p0[1] = U.xyz[0][1]; p0[2] = U.xyz[0][2] + 0.1;
-        sincos(q5[0], &s, &cc); mul_rz(U.Ro[0], cc, s, R0);
-        matmul3(R0, U.Ro[1], Rt); sincos(q5[1], &s, &cc); mul_rz(Rt, cc, s, R1);
-        matmul3(R1, U.Ro[2], Rt); sincos(q5[2], &s, &cc); mul_rz(Rt, cc, s, R2);
+        mul_rz(U.Ro[0], sc[0].y, sc[0].x, R0);
+        matmul3(R0, U.Ro[1], Rt); mul_rz(Rt, sc[1].y, sc[1].x, R1);
+        matmul3(R1, U.Ro[2], Rt); mul_rz(Rt, sc[2].y, sc[2].x, R2);
         xform(R2, p0, U.xyz[3], p3);
-        matmul3(R2, U.Ro[3], Rt); sincos(q5[3], &s, &cc); mul_rz(Rt, cc, s, R3);
-        matmul3(R3, U.Ro[4], Rt); sincos(q5[4], &s, &cc); mul_rz(Rt, cc, s, R4);
+        matmul3(R2, U.Ro[3], Rt); mul_rz(Rt, sc[3].y, sc[3].x, R3);
+        matmul3(R3, U.Ro[4], Rt); mul_rz(Rt, sc[4].y, sc[4].x, R4);
         refn[0] = p0[0]; refn[1] = p0[1]; refn[2] = p0[2];
         xform(R3, p3, U.com3, &refn[3]);
     }
@@ -544,10 +609,9 @@ __global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
     double k1[3], k2[3], tx, ty, tz;
     float pv[3];
     {
-        const int kl1 = klink(2 * j), kl2 = klink(2 * j + 1);
-        anchor(U, kl1, R2, p0, R4, p3, k1);
-        anchor(U, kl2, R2, p0, R4, p3, k2);
+        anchors(j, av1, av2, R2, p0, R4, p3, k1, k2);
         if (S.mb_q) { // multibody mode: the k-links sit at their prismatic joint positions
+            const int kl1 = klink(2 * j), kl2 = klink(2 * j + 1);
             slide(U, kl1, R2, R4, S.mb_q[(size_t)kl1 * N + e], k1);
             slide(U, kl2, R2, R4, S.mb_q[(size_t)kl2 * N + e], k2);
         }
@@ -676,6 +740,10 @@ __global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
         }
     }
 
+    // the imu sample for the joint targets, loaded now: its latency runs under
+    // the solve (no vector-memory wait inside it); at kernel start its address
+    // waited for `motion`, which stalled the in-order wave before the FK
+    tg.imu_v = imu_at(S, motion, jt, c);  // every lane: in bounds, used by the actuated rows < 5
     STAMP(3);
     // ---- the two joint ODE solves (:409-414), one row per lane
     const double T = (r < 7) ? (grp == 0 ? Ta_r : tr_r) : 0.0;
@@ -695,7 +763,7 @@ __global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
     STAMP(4);
     // a failed solve (step below the spacing of t, or the device's 4,096-attempt
     // guard) continues from its last accepted q, as scipy's sol.y[:, -1]
-    finish_solve(S, U, e, grp, r, ebase, c, motion, st.q, info);
+    finish_solve(S, U, e, grp, r, ebase, tg, st.q, info);
     STAMP(5);
 }
 

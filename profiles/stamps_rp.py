@@ -7,7 +7,7 @@ import json
 import os
 import sys
 
-os.environ["EXO_AMD_LIB"] = "libexo_amd_stamps.so"
+os.environ.setdefault("EXO_AMD_LIB", "libexo_amd_stamps.so")
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                 "a-deep-reinforcement-learning-enabled-soft-exoskeleton-for-parkinson-s-patients_amd"))
 import numpy as np  # noqa: E402
@@ -21,7 +21,7 @@ env = VecExoskeletonEnv(N, seed=1)
 env.set_step_variant("rows")
 env.reset()
 blocks = (N + 3) // 4
-buf = torch.zeros(blocks * 8, dtype=torch.int64, device="cuda")
+buf = torch.zeros(blocks * 16, dtype=torch.int64, device="cuda")
 lib = nat.lib()
 lib.exo_debug_set_stamps.argtypes = [ctypes.c_void_p]
 out = env.new_outputs(True)
@@ -33,14 +33,22 @@ for k in range(60):
     env.step(torch.rand((N, 7), device="cuda") * 2 - 1, out=out)
     torch.cuda.synchronize()
     if k >= 50:
-        st = buf.view(blocks, 8)[:, :6].cpu().numpy().astype(np.int64)
+        st = buf.view(blocks, 16)[:, :6].cpu().numpy().astype(np.int64)
         d = np.diff(st, axis=1)
         tot = st[:, 5] - st[:, 0]
         for i, p in enumerate(phases):
             res.setdefault(p, []).append(float(np.median(d[:, i])))
         res.setdefault("total_median", []).append(float(np.median(tot)))
         res.setdefault("total_max", []).append(float(np.max(tot)))
-        full = buf.view(blocks, 8).cpu().numpy().astype(np.int64)
+        w = int(np.argmax(tot))  # the slowest wave's phases
+        for i, p in enumerate(phases):
+            res.setdefault("slowest:" + p, []).append(float(d[w, i]))
+        res.setdefault("ode_p90", []).append(float(np.percentile(d[:, 3], 90)))
+        res.setdefault("ode_max", []).append(float(np.max(d[:, 3])))
+        full = buf.view(blocks, 16).cpu().numpy().astype(np.int64)
+        if (full[:, 8] > 0).all():  # EXO_STAMPS_MEMWAIT build: all kernel-start loads returned
+            res.setdefault("memwait_median", []).append(float(np.median(full[:, 8] - full[:, 0])))
+            res.setdefault("memwait_max", []).append(float(np.max(full[:, 8] - full[:, 0])))
         if (full[:, 6] > 0).all() and (full[:, 7] > 0).all():  # sub-phases of torques+reward+obs+state
             res.setdefault("sub:torque_table", []).append(float(np.median(full[:, 6] - full[:, 2])))
             res.setdefault("sub:sync+reward", []).append(float(np.median(full[:, 7] - full[:, 6])))
