@@ -633,25 +633,29 @@ __global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
         tz = fx * r1 - fy * r0;
     }
     STAMP(2);
-    // torque table of the env: pull the actuated group's lanes 0..6
-    double tau[7][3];
-#pragma unroll
-    for (int jj = 0; jj < 7; ++jj) {
-        tau[jj][0] = shfl_d(tx, ebase + jj);
-        tau[jj][1] = shfl_d(ty, ebase + jj);
-        tau[jj][2] = shfl_d(tz, ebase + jj);
+    // the torque sums of :394-400 through wave-private LDS slots: every lane
+    // stores its actuator's (tx, ty, tz); lane r < 3 reads component {1, 0,
+    // 2}[r] of actuators 3, 4, 5, 7, 6 (lanes 2, 3, 4, 6, 5) and sums them in
+    // that order, lane 3 takes |ty| of actuators 1 and 2 -- 7 reads where the
+    // whole 7 x 3 table took 42 permutes (same sums: bit-identical)
+    __shared__ double s_tq[3][64 * EPB / 4];
+    s_tq[0][threadIdx.x] = tx;
+    s_tq[1][threadIdx.x] = ty;
+    s_tq[2][threadIdx.x] = tz;
+    __builtin_amdgcn_wave_barrier();
+    double at_r;
+    {
+        const unsigned eb = threadIdx.x & ~15u;  // the env's lane 0
+        const double *col = s_tq[r == 1 ? 0 : (r == 2 ? 2 : 1)];
+        const double t0 = col[eb], t1 = col[eb + 1], t2 = col[eb + 2], t3 = col[eb + 3], t4 = col[eb + 4],
+                     t5 = col[eb + 5], t6 = col[eb + 6];
+        at_r = r < 3 ? t2 + t3 + t4 + t6 + t5 : (r == 3 ? fabs(t0) - fabs(t1) : 0.0);
     }
     STAMP(6);
-    double at[4]; // :394-400, actuator order 3, 4, 5, 7, 6
-    at[0] = tau[2][1] + tau[3][1] + tau[4][1] + tau[6][1] + tau[5][1];
-    at[1] = tau[2][0] + tau[3][0] + tau[4][0] + tau[6][0] + tau[5][0];
-    at[2] = tau[2][2] + tau[3][2] + tau[4][2] + tau[6][2] + tau[5][2];
-    at[3] = fabs(tau[0][1]) - fabs(tau[1][1]);
     // per-lane values of this lane's actuator j / joint row r (dynamic indices
     // into small register arrays would go to scratch)
     const double F_j = (((double)a[j] + 1) / 2) * (j < 2 ? maxE : maxS); // :256-266
     const double tr_r = (r < 7) ? tr_j : 0.0;
-    const double at_r = (r == 0) ? at[0] : (r == 1) ? at[1] : (r == 2) ? at[2] : (r == 3) ? at[3] : 0.0;
     const double Ta_r = tr_r + at_r;
     // every lane has read the carried state it needs; lanes of this env now
     // overwrite it (counts, ref, posv, prev actions, later the joints)
@@ -681,17 +685,26 @@ __global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
         g_sm = group_sum(live ? d * d : 0.0);
     }
 
+    // the four exponential reward terms (:341-366) on lanes 0..3 of the group
+    // (one division chain and one exp per lane where lane 0 ran all four),
+    // gathered into lane 0 by quad broadcasts; each term's operations as in
+    // the one-lane form (r_sm's 0.05 * exp(.) commutes exactly)
+    double r_k;
+    {
+        const double eps = 1e-10, Msum = maxE + maxS, naxes = c_naxes, sm = g_sm / 7;
+        const double num = r == 0 ? g_unw : r == 1 ? -g_st + eps : r == 2 ? g_sa : sm;
+        const double den = r == 0 ? Msum / 4 / naxes : r == 1 ? naxes : r == 2 ? Msum / 2 : Msum / 4;
+        const double q = num / den;
+        const double y = exp(r == 1 ? q : -q + eps);
+        r_k = y * (r == 0 ? 0.5 : r == 1 ? 0.9 : 0.05);
+    }
+    const double r_tor = dpp_d<0x55>(r_k), r_ctl = dpp_d<0xAA>(r_k), r_sm = dpp_d<0xFF>(r_k);  // lanes 1, 2, 3 of the quad
+
     // ---- reward, done, observation, info, carried state (:341-366, :448-469, :487-570)
     if (grp == 0) {
         if (r == 0) {
-            const double eps = 1e-10, Msum = maxE + maxS, naxes = c_naxes;
-            const double unw = g_unw, st = g_st, sa = g_sa, sm = g_sm / 7;
-            const int nred = (int)g_nred;
-            const double r_unw = exp(-(unw / (Msum / 4 / naxes)) + eps) * 0.5;
-            const double r_tor = exp((-st + eps) / naxes) * 0.9;
-            const double r_axis = nred * 0.5;
-            const double r_ctl = exp(-(sa / (Msum / 2)) + eps) * 0.05;
-            const double r_sm = 0.05 * exp(-(sm / (Msum / 4)) + eps);
+            const double r_unw = r_k;
+            const double r_axis = (int)g_nred * 0.5;
             rew[e] = (float)((r_axis + r_tor + r_sm + r_ctl + r_unw) / c_maxrew);
             done[e] = (uint8_t)(c + 1 >= L - 1);
             if (info) {
