@@ -92,11 +92,14 @@ struct RowM {
 __device__ __forceinline__ double shfl_d(double x, int src) { return __shfl(x, src, 64); }
 
 // DPP lane moves of a double (two dword moves, VALU only: no LDS round trip)
+// (every control used here -- quad_perm, row_half_mirror -- reads a valid lane
+// of the same row, so bound_ctrl and the old value never apply: mov_dpp
+// without the zeroed old operand the update form materialised per move)
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double x) {
     const long long v = __double_as_longlong(x);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(v & 0xffffffffLL), CTRL, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(v >> 32), CTRL, 0xF, 0xF, false);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(v & 0xffffffffLL), CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(v >> 32), CTRL, 0xF, 0xF, true);
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
@@ -799,7 +802,11 @@ hipError_t launch_exo_step_rp(const Dev &S, const Urdf &U, const float *act, flo
     // LDS slots, 16-byte writes / reads (default: 26.8 vs 31.1 us at 4,096 envs,
     // profiles/r02f_raw/ab_pull.txt); 0 = LDS permutes (ds_bpermute, 4 32-bit
     // moves per (q, v) pull); 1 = DPP lane moves (slower still: two dword moves
-    // per fp64 pull plus the DPP hazard waits -- 38.2 vs 34.9 us against 0)
+    // per fp64 pull plus the DPP hazard waits -- 38.2 vs 34.9 us against 0);
+    // r06: the slots for (q, v) and DPP moves for r (the second exchange of a
+    // stage) tied the slots alone in the 256-thread shape (22.1-22.3 us) and
+    // lost in the shared one (27.4 vs 26.9: two waves per SIMD share the
+    // VALU), bit-identical -- not kept (profiles/r06_step/r06p)
     static const int pull = [] {
         const char *v = getenv("EXO_RP_GATHER");
         return v ? atoi(v) : 2;
