@@ -576,7 +576,6 @@ __global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
     float posv_old[3];
 #pragma unroll
     for (int d = 0; d < 3; ++d) posv_old[d] = S.posv[(size_t)(j * 3 + d) * N + e];
-    const RowM M0 = load_rows(S, e, r, gbase);
     const int seq = S.seq[e], motion = S.motion[e];
     Targets tg;
     tg.q0 = qj;
@@ -668,6 +667,11 @@ __global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
     // store above it) instead of a workgroup barrier, which also waited for the
     // other waves of the workgroup
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // the ODE's matrix rows (12 loads, nothing in this kernel writes them),
+    // issued only now: they return under the reward / observation / state
+    // phase instead of queueing with the kernel-start batch the FK and the
+    // actuators wait for
+    const RowM M0 = load_rows(S, e, r, gbase);
 
     // reward terms (:341-366), term i on lane r = i of the actuated group (no
     // divergent per-term branches in one lane: every lane takes its two
