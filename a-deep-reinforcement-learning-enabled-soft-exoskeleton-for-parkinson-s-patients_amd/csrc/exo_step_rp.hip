@@ -567,16 +567,10 @@ __global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
     }
     const double pa_j = S.prev_a[(size_t)j * N + e];
     const double pa2_j = S.prev2_a[(size_t)j * N + e];
-    const double tr_j = S.tremor[((size_t)c * 7 + j) * N + e];
-    const int r4 = r & 3;  // tremor rows 0..3 of the observation at c - 1, c + 1
-    const double tm1 = S.tremor[((size_t)(c > 0 ? c - 1 : 0) * 7 + r4) * N + e];
-    const double tp1 = S.tremor[((size_t)(c + 1) * 7 + r4) * N + e];
-    const double c_naxes = cfg(S, C_NAXES, e), c_maxrew = cfg(S, C_MAXREW, e);
-    const double c_nrm = j < 2 ? cfg(S, C_MAXE0, e) : cfg(S, C_MAXS0, e);
     float posv_old[3];
 #pragma unroll
     for (int d = 0; d < 3; ++d) posv_old[d] = S.posv[(size_t)(j * 3 + d) * N + e];
-    const int seq = S.seq[e], motion = S.motion[e];
+    const int motion = S.motion[e];
     Targets tg;
     tg.q0 = qj;
     load_lims(U, r, tg);
@@ -605,6 +599,16 @@ __global__ __launch_bounds__(64 * EPB / 4) void exo_step_rp_kernel(
         refn[0] = p0[0]; refn[1] = p0[1]; refn[2] = p0[2];
         xform(R3, p3, U.com3, &refn[3]);
     }
+    // read-only operands of the reward, the observation and the solve's
+    // torque, issued after the FK (the kernel-start batch above is what the FK
+    // and the actuators wait for; these return under the actuator phase)
+    const double tr_j = S.tremor[((size_t)c * 7 + j) * N + e];
+    const int r4 = r & 3;  // tremor rows 0..3 of the observation at c - 1, c + 1
+    const double tm1 = S.tremor[((size_t)(c > 0 ? c - 1 : 0) * 7 + r4) * N + e];
+    const double tp1 = S.tremor[((size_t)(c + 1) * 7 + r4) * N + e];
+    const double c_naxes = cfg(S, C_NAXES, e), c_maxrew = cfg(S, C_MAXREW, e);
+    const double c_nrm = j < 2 ? cfg(S, C_MAXE0, e) : cfg(S, C_MAXS0, e);
+    const int seq = S.seq[e];
 
     STAMP(1);
     // ---- actuator j = r (lanes r == 7 duplicate actuator 6 and discard it)
