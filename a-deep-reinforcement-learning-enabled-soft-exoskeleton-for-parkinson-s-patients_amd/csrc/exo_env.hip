@@ -56,24 +56,44 @@ struct Draws {
     }
 };
 
-// Invert a small dense matrix (Gauss-Jordan, partial pivoting), fp64.
+// Invert a small dense matrix (Gauss-Jordan, partial pivoting), fp64.  Every
+// index is a compile-time one (the pivot row swap is a select per row): with
+// `a[p * n + j]` for the runtime pivot p the arrays lived in scratch memory,
+// 46 scratch accesses on the reset's serial tail (r06).  Same operations in
+// the same order: bit-identical.
 template <int n>
-__device__ void invert(double *a /* n*n, destroyed */, double *inv) {
+__device__ __forceinline__ void invert(double *a /* n*n, destroyed */, double *inv) {
+#pragma unroll
     for (int i = 0; i < n * n; ++i) inv[i] = (i % (n + 1) == 0) ? 1.0 : 0.0;
+#pragma unroll
     for (int k = 0; k < n; ++k) {
         int p = k;
-        for (int i = k + 1; i < n; ++i)
-            if (fabs(a[i * n + k]) > fabs(a[p * n + k])) p = i;
-        if (p != k)
+        double best = fabs(a[k * n + k]);
+#pragma unroll
+        for (int i = k + 1; i < n; ++i) {
+            const double v = fabs(a[i * n + k]);
+            if (v > best) { best = v; p = i; }
+        }
+#pragma unroll
+        for (int i = k + 1; i < n; ++i) {
+            const bool sw = p == i;
+#pragma unroll
             for (int j = 0; j < n; ++j) {
-                double t = a[k * n + j]; a[k * n + j] = a[p * n + j]; a[p * n + j] = t;
-                t = inv[k * n + j]; inv[k * n + j] = inv[p * n + j]; inv[p * n + j] = t;
+                const double t = a[k * n + j], u = inv[k * n + j];
+                a[k * n + j] = sw ? a[i * n + j] : t;
+                a[i * n + j] = sw ? t : a[i * n + j];
+                inv[k * n + j] = sw ? inv[i * n + j] : u;
+                inv[i * n + j] = sw ? u : inv[i * n + j];
             }
+        }
         const double r = 1.0 / a[k * n + k];
+#pragma unroll
         for (int j = 0; j < n; ++j) { a[k * n + j] *= r; inv[k * n + j] *= r; }
+#pragma unroll
         for (int i = 0; i < n; ++i) {
             if (i == k) continue;
             const double m = a[i * n + k];
+#pragma unroll
             for (int j = 0; j < n; ++j) { a[i * n + j] -= m * a[k * n + j]; inv[i * n + j] -= m * inv[k * n + j]; }
         }
     }

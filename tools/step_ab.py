@@ -77,8 +77,19 @@ def main():
         torch.cuda.synchronize()
         if k:  # the first round warms up
             times.append(e0.elapsed_time(e1) / args.n * 1000.0)
+    # the bulk reset (exo_reset_kernel over every env), n back-to-back calls per round
+    rtimes = []
+    for k in range(4):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            env.reset()
+        e1.record()
+        torch.cuda.synchronize()
+        if k:
+            rtimes.append(e0.elapsed_time(e1) / 10 * 1000.0)
     res = {"lib": os.environ.get("EXO_AMD_LIB", "libexo_amd.so"), "envs": N, "variant": args.variant, "us_per_launch": times,
-           "best_us": min(times), "median_us": float(np.median(times))}
+           "best_us": min(times), "median_us": float(np.median(times)), "reset_us": rtimes}
     print(json.dumps(res))
     with open(args.out + ".json", "w") as f:
         json.dump(res, f)
