@@ -314,6 +314,7 @@ struct SelectArgs {
     R32 F, TW, FT;
     int lds_bytes;
     int tile0, ticket;  // fp32 chunked launches: first row tile; 1 = take the noise ticket
+    void *zimg;         // split launches (ZM 1 / 2): the rows' normalised zs in operand type, [n][Z]
 };
 
 #define RING_START(first)      \
@@ -327,7 +328,14 @@ __device__ __forceinline__ R32 rows_of(R32 r, int t) { return R32{r.off + t * TR
 // launches of at most its workgroup cap each (the same per-row arithmetic and
 // Philox elements); only the last launch takes the noise ticket, so sigma and
 // the call counter advance once, after every tile has drawn.
-template <int P, int TH, int RT>
+// ZM (r06, td7f_select_part): 0 the whole pass; 1 the fixed encoder's zs only,
+// its normalised image stored to a.zimg (no actor, no noise); 2 the actor from
+// that image (the zs layers skipped).  zs needs only the fixed encoder, which
+// changes at target refreshes alone, so a training loop can run the ZM 1 half
+// as soon as the observations exist and only the ZM 2 half after the actor
+// step; the image is the operand-type values ZM 0 leaves in CAT, so 1 + 2 ==
+// 0 bit for bit (same row tiles).
+template <int P, int TH, int RT, int ZM = 0>
 __global__ __launch_bounds__(NTH) void select_kernel(SelectArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     constexpr int rows = RT * TR;
@@ -340,22 +348,57 @@ __global__ __launch_bounds__(NTH) void select_kernel(SelectArgs a) {
     FSTAMP(si);
     RowStage so[RT];
     ThinStage<THIN_NC> tw;
+    using E = typename Ty<P>::E;
+    static_assert(RT * TR * (int)sizeof(E) <= 64, "ZM 2 staging: 16 rows x 512 words at most");
 #pragma unroll
     for (int t = 0; t < RT; ++t) row_issue(so[t], a.obs, a.S, a.S, row0 + t * TR, a.n);
-    thin_issue(tw, a.ac[3].w, a.ac[3].ldw, 0, false, a.A, a.ac[3].K);
-    RING_START(a.zs[0]);
+    if constexpr (ZM != 1) thin_issue(tw, a.ac[3].w, a.ac[3].ldw, 0, false, a.A, a.ac[3].K);
+    // ZM 2: this workgroup's zs image rows in 4-byte words (Z * EB % 4 == 0,
+    // at most 16 rows x 512 words per 512 threads: checked on the host),
+    // loaded with the observations
+    const int zw = a.Z * (int)sizeof(E) / 4;
+    constexpr int ZPT = ZM == 2 ? (16 * 512 + NTH - 1) / NTH : 1;
+    uint32_t zv[ZPT];
+    if constexpr (ZM == 2) {
+        const uint32_t *zi = (const uint32_t *)a.zimg;
+#pragma unroll
+        for (int u = 0; u < ZPT; ++u) {
+            const int k = threadIdx.x + u * NTH, r = k / zw, c = k - r * zw;
+            zv[u] = (r < rows && row0 + r < a.n) ? zi[(long)(row0 + r) * zw + c] : 0u;
+        }
+    }
+    RING_START(ZM == 2 ? a.ac[0] : a.zs[0]);
     zero_lds(lds, a.lds_bytes);
     __syncthreads();
 #pragma unroll
     for (int t = 0; t < RT; ++t) row_put16<P>(lds, so[t], rows_of(a.X, t), 0, a.S, row0 + t * TR, a.n);
-    thin_put<P>(lds, tw, a.TW, a.A, a.ac[3].K);
+    if constexpr (ZM != 1) thin_put<P>(lds, tw, a.TW, a.A, a.ac[3].K);
+    if constexpr (ZM == 2) {
+#pragma unroll
+        for (int u = 0; u < ZPT; ++u) {
+            const int k = threadIdx.x + u * NTH, r = k / zw, c = k - r * zw;
+            if (r < rows) *(uint32_t *)(pe<P>(lds, a.CAT, r, a.Ha) + c * (4 / (int)sizeof(E))) = zv[u];
+        }
+    }
     __syncthreads();
-    // zs = fixed_encoder.zs(obs) (:93-97) -> CAT[:, Ha:Ha+Z]
-    layer_fwd<P, RT, TH>(lds, R, a.X, a.zs[0], &a.zs[1], a.act_enc, a.H1, 0, NO32, nullptr, 0, row0, a.n, si);
-    layer_fwd<P, RT, TH>(lds, R, a.H1, a.zs[1], &a.zs[2], a.act_enc, a.H2, 0, NO32, nullptr, 0, row0, a.n, si);
-    layer_fwd<P, RT, TH>(lds, R, a.H2, a.zs[2], &a.ac[0], ACT_NONE, NO16, 0, a.F, nullptr, 0, row0, a.n, si);
-    norm_fwd<P>(lds, a.F, a.Z, rows, 1e-8f, a.CAT, a.Ha, NO16, 0, NO32, nullptr, 0, nullptr, nullptr, row0, a.n);
-    __syncthreads();
+    if constexpr (ZM != 2) {
+        // zs = fixed_encoder.zs(obs) (:93-97) -> CAT[:, Ha:Ha+Z]
+        layer_fwd<P, RT, TH>(lds, R, a.X, a.zs[0], &a.zs[1], a.act_enc, a.H1, 0, NO32, nullptr, 0, row0, a.n, si);
+        layer_fwd<P, RT, TH>(lds, R, a.H1, a.zs[1], &a.zs[2], a.act_enc, a.H2, 0, NO32, nullptr, 0, row0, a.n, si);
+        layer_fwd<P, RT, TH>(lds, R, a.H2, a.zs[2], ZM == 1 ? (const Lin *)nullptr : &a.ac[0], ACT_NONE, NO16, 0, a.F,
+                             nullptr, 0, row0, a.n, si);
+        norm_fwd<P>(lds, a.F, a.Z, rows, 1e-8f, a.CAT, a.Ha, NO16, 0, NO32, nullptr, 0, nullptr, nullptr, row0, a.n);
+        __syncthreads();
+    }
+    if constexpr (ZM == 1) {
+        uint32_t *zo = (uint32_t *)a.zimg;
+        for (int k = threadIdx.x; k < rows * zw; k += NTH) {
+            const int r = k / zw, c = k - r * zw;
+            if (row0 + r < a.n)
+                zo[(long)(row0 + r) * zw + c] = *(const uint32_t *)(pe<P>(lds, a.CAT, r, a.Ha) + c * (4 / (int)sizeof(E)));
+        }
+        return;
+    }
     // actor (:72-77): AvgL1Norm(l0(s)) | zs -> l1 -> l2 -> tanh(l3)
     layer_fwd<P, RT, TH>(lds, R, a.X, a.ac[0], &a.ac[1], ACT_NONE, NO16, 0, a.F, nullptr, 0, row0, a.n, si);
     norm_fwd<P>(lds, a.F, a.Ha, rows, 1e-8f, a.CAT, 0, NO16, 0, NO32, nullptr, 0, nullptr, nullptr, row0, a.n);
@@ -648,10 +691,37 @@ int td7f_probe(int32_t on) {
     return EXO_OK;
 }
 
-int td7f_select(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7f_lin *actor, const float *obs,
-                int32_t n, const td7f_noise *noise, float *out, int32_t wg_cap, int32_t rt, void *stream) {
-    if (!prec_ok(prec) || !act || !enc || !actor || !obs || !noise || !out || n <= 0 || wg_cap < 0 || rt < 0 ||
-        rt > 2)
+}  // extern "C"
+
+namespace {
+// the select kernel of (precision, weight-tile count, row tiles, split mode)
+template <int ZM>
+int select_one(int prec, int th, int RT, dim3 g, int lds, const SelectArgs &a, hipStream_t st) {
+    using namespace td7f;
+    if (prec == PREC_F32)
+        return th == 5 ? launch(select_kernel<PREC_F32, 5, 1, ZM>, g, lds, a, st)
+                       : launch(select_kernel<PREC_F32, 4, 1, ZM>, g, lds, a, st);
+    if (RT == 2)
+        return prec == PREC_BF16 ? (th == 5 ? launch(select_kernel<PREC_BF16, 5, 2, ZM>, g, lds, a, st)
+                                            : launch(select_kernel<PREC_BF16, 4, 2, ZM>, g, lds, a, st))
+                                 : (th == 5 ? launch(select_kernel<PREC_F16, 5, 2, ZM>, g, lds, a, st)
+                                            : launch(select_kernel<PREC_F16, 4, 2, ZM>, g, lds, a, st));
+    return prec == PREC_BF16 ? (th == 5 ? launch(select_kernel<PREC_BF16, 5, 1, ZM>, g, lds, a, st)
+                                        : launch(select_kernel<PREC_BF16, 4, 1, ZM>, g, lds, a, st))
+                             : (th == 5 ? launch(select_kernel<PREC_F16, 5, 1, ZM>, g, lds, a, st)
+                                        : launch(select_kernel<PREC_F16, 4, 1, ZM>, g, lds, a, st));
+}
+int select_mode(int zm, int prec, int th, int RT, dim3 g, int lds, const SelectArgs &a, hipStream_t st) {
+    return zm == 1 ? select_one<1>(prec, th, RT, g, lds, a, st)
+         : zm == 2 ? select_one<2>(prec, th, RT, g, lds, a, st)
+                   : select_one<0>(prec, th, RT, g, lds, a, st);
+}
+
+int select_impl(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7f_lin *actor, const float *obs,
+                int32_t n, const td7f_noise *noise, float *out, int32_t wg_cap, int32_t rt, void *zimg, int zm,
+                void *stream) {
+    if (!prec_ok(prec) || !act || !enc || !actor || !obs || n <= 0 || wg_cap < 0 || rt < 0 || rt > 2 || zm < 0 ||
+        zm > 2 || (zm != 1 && (!noise || !out)) || (zm != 0 && !zimg))
         return EXO_EINVAL;
     const int kd = kd_of(prec);
     td7f_lin all[7] = {enc[0], enc[1], enc[2], actor[0], actor[1], actor[2], actor[3]};
@@ -670,7 +740,10 @@ int td7f_select(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7
     a.Ha = actor[0].n_out;
     if (actor[0].n_in != a.S || actor[1].n_in != a.Ha + a.Z || a.A > THIN_NC || a.S > NTH) return EXO_EINVAL;
     a.out = out;
-    a.nz = noise_of(*noise);
+    if (zm != 1) a.nz = noise_of(*noise);
+    a.zimg = zimg;
+    if (zm != 0 && (((long)a.Z * (prec == PREC_F32 ? 4 : 2)) % 4 || ((long)a.Ha * (prec == PREC_F32 ? 4 : 2)) % 4 || a.Z > 512))
+        return EXO_EINVAL;  // the image moves in 4-byte words, at most 512 per row
     // 32-row tiles above 8,192 envs (more than two 16-row workgroups per CU:
     // the weights are then streamed half as often; configs[3]'s 16,384 envs
     // 0.452 vs 0.494 ms per iteration, profiles/r04q_raw); 16-row tiles below
@@ -716,31 +789,29 @@ int td7f_select(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7
             a.tile0 = t0;
             a.ticket = t0 + cap >= ntiles;
             const dim3 g(std::min(cap, ntiles - t0));
-            const int rc = prec == PREC_F32 ? (th == 5 ? launch(select_kernel<PREC_F32, 5, 1>, g, b.off, a, st)
-                                                       : launch(select_kernel<PREC_F32, 4, 1>, g, b.off, a, st))
-                           : prec == PREC_BF16 ? (th == 5 ? launch(select_kernel<PREC_BF16, 5, 1>, g, b.off, a, st)
-                                                          : launch(select_kernel<PREC_BF16, 4, 1>, g, b.off, a, st))
-                                               : (th == 5 ? launch(select_kernel<PREC_F16, 5, 1>, g, b.off, a, st)
-                                                          : launch(select_kernel<PREC_F16, 4, 1>, g, b.off, a, st));
+            const int rc = select_mode(zm, prec, th, 1, g, b.off, a, st);
             if (rc != EXO_OK) return rc;
         }
         return EXO_OK;
     }
     a.tile0 = 0;
     a.ticket = 1;
-    const dim3 grid(ntiles);
-    if (prec == PREC_F32)
-        return th == 5 ? launch(select_kernel<PREC_F32, 5, 1>, grid, b.off, a, st)
-                       : launch(select_kernel<PREC_F32, 4, 1>, grid, b.off, a, st);
-    if (RT == 2)
-        return prec == PREC_BF16 ? (th == 5 ? launch(select_kernel<PREC_BF16, 5, 2>, grid, b.off, a, st)
-                                            : launch(select_kernel<PREC_BF16, 4, 2>, grid, b.off, a, st))
-                                 : (th == 5 ? launch(select_kernel<PREC_F16, 5, 2>, grid, b.off, a, st)
-                                            : launch(select_kernel<PREC_F16, 4, 2>, grid, b.off, a, st));
-    return prec == PREC_BF16 ? (th == 5 ? launch(select_kernel<PREC_BF16, 5, 1>, grid, b.off, a, st)
-                                        : launch(select_kernel<PREC_BF16, 4, 1>, grid, b.off, a, st))
-                             : (th == 5 ? launch(select_kernel<PREC_F16, 5, 1>, grid, b.off, a, st)
-                                        : launch(select_kernel<PREC_F16, 4, 1>, grid, b.off, a, st));
+    return select_mode(zm, prec, th, RT, dim3(ntiles), b.off, a, st);
+}
+}  // namespace
+
+extern "C" {
+
+int td7f_select(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7f_lin *actor, const float *obs,
+                int32_t n, const td7f_noise *noise, float *out, int32_t wg_cap, int32_t rt, void *stream) {
+    return select_impl(prec, act, enc, actor, obs, n, noise, out, wg_cap, rt, nullptr, 0, stream);
+}
+
+int td7f_select_part(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7f_lin *actor, const float *obs,
+                     int32_t n, const td7f_noise *noise, float *out, int32_t wg_cap, int32_t rt, void *zimg,
+                     int32_t mode, void *stream) {
+    if (mode != 1 && mode != 2) return EXO_EINVAL;
+    return select_impl(prec, act, enc, actor, obs, n, noise, out, wg_cap, rt, zimg, mode, stream);
 }
 
 int td7f_target(int32_t prec, const int32_t *act, const td7f_lin *tenc, const td7f_lin *tactor,

@@ -234,6 +234,8 @@ EXPORTS = {
     "td7f_probe": (c_int32, [c_int32]),
     "td7f_select": (c_int32, [c_int32, P(c_int32), P(TD7FLin), P(TD7FLin), c_void_p, c_int32, P(TD7FNoise), c_void_p,
                               c_int32, c_int32, c_void_p]),
+    "td7f_select_part": (c_int32, [c_int32, P(c_int32), P(TD7FLin), P(TD7FLin), c_void_p, c_int32, P(TD7FNoise),
+                                   c_void_p, c_int32, c_int32, c_void_p, c_int32, c_void_p]),
     "td7f_target": (c_int32, [c_int32, P(c_int32), P(TD7FLin), P(TD7FLin), P(TD7FLin), c_void_p, c_int32,
                               P(TD7FNoise), c_void_p, c_void_p, c_void_p]),
     "td7f_fixed": (c_int32, [c_int32, P(c_int32), P(TD7FLin), c_void_p, c_void_p, c_int32, c_void_p, c_void_p,

@@ -304,8 +304,38 @@ class FusedNets:
                          dec_count.data_ptr() if dec_count is not None else None)
 
     # ------------------------------------------------------------- passes
+    def zs_image(self, n):
+        """the [n][zs_dim] operand-type buffer select_zs fills (allocated on the
+        first call, which must come before any graph capture that uses it)"""
+        Z = self.L.hp.zs_dim
+        buf = getattr(self, "_zs_img", None)
+        if buf is None or buf.shape[0] < n:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("FusedNets.zs_image: allocate it eagerly before graph capture")
+            buf = self._zs_img = torch.empty((n, Z), dtype=_etype(self.prec), device=self.dev)
+        return buf[:n]
+
     @torch.no_grad()
-    def select(self, obs, scale=1.0, dec_count=None, world=1, wg_cap=None, rt=None):
+    def select_zs(self, obs, wg_cap=None, rt=None):
+        """The fixed encoder's half of select (td7f_select_part mode 1):
+        fixed_encoder.zs(obs) (TD7_multi_agent.py:93-97), normalised, into
+        zs_image(n) -- no actor, no noise, no exploration-state change.  The
+        fixed encoder changes only at target refreshes, so a training loop can
+        run this as soon as the observations exist and the actor half, select
+        (..., zs_img=), after the actor step: the pair is select bit for bit
+        (same rt)."""
+        self.refresh("fixed_encoder")
+        obs = obs.contiguous()
+        n = obs.shape[0]
+        img = self.zs_image(n)
+        fe = self.nets["fixed_encoder"].layers
+        nat.check(nat.lib().td7f_select_part(self.prec, self.act, _lin_array(fe[:3]), self.nets["actor"].array,
+                                             nat.ptr(obs), n, None, None, int(wg_cap or 0), int(rt or 0),
+                                             nat.ptr(img), 1, nat.stream_ptr(obs.device)), "td7f_select_part")
+        return img
+
+    @torch.no_grad()
+    def select(self, obs, scale=1.0, dec_count=None, world=1, wg_cap=None, rt=None, zs_img=None):
         """select_action_batch with Gaussian exploration (one launch): actor(obs,
         fixed_encoder.zs(obs)) + N(0, exploration_noise) per element, clamped,
         times max_action; exploration_noise decreases once per env (dec_count:
@@ -313,7 +343,7 @@ class FusedNets:
         of a vectorised step; times `world`, the data-parallel ranks stepping
         as many envs each)."""
         L = self.L
-        self.refresh("fixed_encoder", "actor")
+        self.refresh(*(("actor",) if zs_img is not None else ("fixed_encoder", "actor")))
         obs = obs.contiguous()
         n = obs.shape[0]
         out = torch.empty((n, L.actor.l3.out_features), dtype=torch.float32, device=obs.device)
@@ -325,6 +355,12 @@ class FusedNets:
         fe, ac = self.nets["fixed_encoder"].layers, self.nets["actor"].layers
         # wg_cap: at most this many workgroups per launch (None / 0: one launch);
         # rt: rows per tile / 16 (None / 0: the library's pick)
+        if zs_img is not None:  # the actor half after select_zs (td7f_select_part mode 2)
+            nat.check(nat.lib().td7f_select_part(self.prec, self.act, _lin_array(fe[:3]), self.nets["actor"].array,
+                                                 nat.ptr(obs), n, ctypes.byref(nz), nat.ptr(out), int(wg_cap or 0),
+                                                 int(rt or 0), nat.ptr(zs_img), 2, nat.stream_ptr(obs.device)),
+                      "td7f_select_part")
+            return out
         nat.check(nat.lib().td7f_select(self.prec, self.act, _lin_array(fe[:3]), self.nets["actor"].array,
                                         nat.ptr(obs), n, ctypes.byref(nz), nat.ptr(out), int(wg_cap or 0),
                                         int(rt or 0), nat.stream_ptr(obs.device)), "td7f_select")

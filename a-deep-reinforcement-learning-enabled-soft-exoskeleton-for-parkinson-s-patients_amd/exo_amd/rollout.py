@@ -339,11 +339,33 @@ class VecTrainer:
             return None
         return self.loop_select_rt or None
 
-    def _rollout(self):
+    # r06: in the overlapped pair's second iteration select_action's fixed-
+    # encoder half (zs of the observations, td7f_select_part mode 1) runs from
+    # the iteration's start; only its actor half waits for the first
+    # iteration's actor step.  Bit-identical (the two halves are the one-launch
+    # pass split at its zs image).  Same box, 3 / 2 alternations
+    # (profiles/r06_split_select): fp32 0.4005-0.4107 vs 0.4222-0.4242 ms per
+    # iteration -- on by default there; bf16 0.2504-0.2525 vs 0.2418-0.2459
+    # (the zs half's 128 workgroups beside the second iteration's target chain
+    # cost more than the shorter select saves) -- off.  EXO_SPLIT_SELECT:
+    # "auto" (fp32 only), "1" (always), "0" (never).
+    split_select = os.environ.get("EXO_SPLIT_SELECT", "auto")
+
+    def _split_select_ok(self):
+        L = self.agent.learner
+        on = self.split_select == "1" or (self.split_select == "auto" and L.precision == "fp32")
+        return on and L.fused is not None and self.exploration == "gaussian" and self.obs.is_cuda
+
+    def _select_zs(self):
+        """the zs half of this iteration's select_action (see split_select)"""
+        return self.agent.learner.fused.select_zs(self.obs, wg_cap=self._select_cap(), rt=self._select_rt())
+
+    def _rollout(self, zs_img=None):
         ag = self.agent
         obs = self.obs
         act = ag.select_action_batch(obs, timestep=self.k_dev if self.exploration == "pink" else None,
-                                     dec_count=self.active_count, wg_cap=self._select_cap(), rt=self._select_rt())
+                                     dec_count=self.active_count, wg_cap=self._select_cap(), rt=self._select_rt(),
+                                     zs_img=zs_img)
         if self._overlap_wait is not None and PAIR_CRITIC_AFTER_SELECT:
             self._select_done = torch.cuda.Event()
             self._select_done.record(torch.cuda.current_stream(self.device))
@@ -476,12 +498,18 @@ class VecTrainer:
             self._rollout_stream = torch.cuda.Stream(device=self.device)
         br = self._rollout_stream
 
+        split = self._overlap_wait is not None and self._split_select_ok()  # (its image: _capture_pair)
+
         def rollout_branch(cur=cur, br=br):
             br.wait_stream(cur)
+            zimg = None
+            if split:  # select_action's zs half needs only the observations
+                with torch.cuda.stream(br):
+                    zimg = self._select_zs()
             if self._overlap_wait is not None:  # overlapped pair: after the previous actor step
                 br.wait_stream(self._overlap_wait)
             with torch.cuda.stream(br):
-                self._rollout()
+                self._rollout(zs_img=zimg)
         L = ag.learner
         late = (ROLLOUT_AFTER == "fixed" and L.fused_train and L.pre_in is None and not self._pre_in
                 and not _td7.TARGET_ON_MAIN)
@@ -498,10 +526,14 @@ class VecTrainer:
 
             def rollout_from_start(ev0=ev0, br=br):
                 br.wait_event(ev0)
+                zimg = None
+                if split:
+                    with torch.cuda.stream(br):
+                        zimg = self._select_zs()
                 if self._overlap_wait is not None:
                     br.wait_stream(self._overlap_wait)
                 with torch.cuda.stream(br):
-                    self._rollout()
+                    self._rollout(zs_img=zimg)
             L.after_target = rollout_from_start
         else:
             rollout_branch()
@@ -896,6 +928,8 @@ class VecTrainer:
         keep = []
         if overlap and getattr(self, "_astream", None) is None:
             self._astream = torch.cuda.Stream(device=self.device)
+        if overlap and self._split_select_ok():
+            L.fused.zs_image(self.n)  # the split select's zs image, allocated before the capture
         try:
             with torch.cuda.stream(s):
                 with capture(g, stream=s), ForkJoinAudit(s):

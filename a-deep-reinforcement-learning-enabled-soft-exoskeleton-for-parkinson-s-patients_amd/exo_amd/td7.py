@@ -1461,7 +1461,7 @@ class Agent:
 
     @torch.no_grad()
     def select_action_batch(self, obs, use_checkpoint=False, use_exploration=True, timestep=None, dec_count=None,
-                            wg_cap=None, rt=None):
+                            wg_cap=None, rt=None, zs_img=None):
         """Device-resident batched actions for the vectorised loop (no host sync).
         timestep (int64 device tensor [1]): Pink-noise exploration -- column
         `timestep` of the episode's noise (init_episode_noise_device) is added
@@ -1478,7 +1478,9 @@ class Agent:
         if fz is not None and use_exploration and timestep is None and not use_checkpoint and obs.is_cuda:
             # zs, actor and the noise in one launch
             return fz.select(obs, scale=self.max_action, dec_count=dec_count, world=self.sync.world, wg_cap=wg_cap,
-                             rt=rt)
+                             rt=rt, zs_img=zs_img)
+        if zs_img is not None:
+            raise ValueError("select_action_batch: zs_img needs the fused Gaussian-exploration path")
         a = self.learner.act(obs, use_checkpoint)
         if use_exploration and timestep is not None:
             col = self.noise_dev.index_select(1, timestep).t()           # [1, action_dim]

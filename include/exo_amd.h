@@ -710,6 +710,17 @@ int td7f_probe(int32_t on);
  * asks (16-bit operands; fp32 always 16); EXO_SELECT_RT overrides. */
 int td7f_select(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7f_lin *actor, const float *obs_dev,
                 int32_t n, const td7f_noise *noise, float *act_out_dev, int32_t wg_cap, int32_t rt, void *stream);
+/* td7f_select in two launches (r06): mode 1 computes fixed_encoder.zs(obs)
+ * (TD7_multi_agent.py:93-97) and stores its normalised rows, in the operand
+ * type, to zs_img_dev [n][zs_dim] (noise and act_out unused, the noise state
+ * untouched); mode 2 runs the actor (:72-77) and the exploration noise from
+ * that image.  Mode 1 then mode 2 with the same rt == td7f_select bit for
+ * bit; the zs half needs only the fixed encoder, so a training loop can run
+ * it before the actor step.  zs_dim <= 512, zs_dim and actor l0's width
+ * even at 16-bit operands. */
+int td7f_select_part(int32_t prec, const int32_t *act, const td7f_lin *enc, const td7f_lin *actor,
+                     const float *obs_dev, int32_t n, const td7f_noise *noise, float *act_out_dev, int32_t wg_cap,
+                     int32_t rt, void *zs_img_dev, int32_t mode, void *stream);
 /* The critic target chain (TD7_multi_agent.py:233-241): fixed_target_zs(s'),
  * next_action = actor_target(s', zs) + clipped noise, fixed_target_zsa and both
  * heads of critic_target -> qt_dev [B][2].  tenc: zs1..zs3, zsa1..zsa3;

@@ -299,3 +299,29 @@ def test_select_row_tiles_argument(precision):
     torch.cuda.synchronize()
     assert _rel(outs[1], outs[0]) < REL, _rel(outs[1], outs[0])
     assert float((outs[1] - outs[0]).abs().max()) < 2e-2
+
+
+@pytest.mark.parametrize("precision,rt,cap", [("bf16", 1, 0), ("bf16", 2, 0), ("fp16", 2, 0), ("fp32", 1, 0),
+                                              ("fp32", 1, 100)])
+def test_split_select_equals_one_launch(precision, rt, cap):
+    """td7f_select_part (r06): the fixed encoder's zs half (mode 1, into the
+    zs image) then the actor half from it (mode 2) -- the actions bit for bit
+    those of the one-launch td7f_select at the same row tiles, the Philox call
+    counter and exploration_noise advanced once (by the actor half only), the
+    zs half alone leaving both untouched; with the fp32 workgroup cap too."""
+    L = _learner(precision, None)
+    obs, _ = _inputs(4096, 13)
+    rng = L._explore_rng
+    st0, sig0 = rng.state.clone(), float(L.exploration_noise_t)
+    one = L.fused.select(obs, scale=1.0, rt=rt, wg_cap=cap)
+    torch.cuda.synchronize()
+    st1, sig1 = rng.state.clone(), float(L.exploration_noise_t)
+    rng.state.copy_(st0)
+    L.exploration_noise_t.fill_(sig0)
+    img = L.fused.select_zs(obs, rt=rt, wg_cap=cap)
+    torch.cuda.synchronize()
+    assert torch.equal(rng.state, st0) and float(L.exploration_noise_t) == sig0
+    two = L.fused.select(obs, scale=1.0, rt=rt, wg_cap=cap, zs_img=img)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(two, one, rtol=0, atol=0)
+    assert torch.equal(rng.state, st1) and float(L.exploration_noise_t) == sig1
