@@ -357,8 +357,11 @@ class VecTrainer:
         return on and L.fused is not None and self.exploration == "gaussian" and self.obs.is_cuda
 
     def _select_zs(self):
-        """the zs half of this iteration's select_action (see split_select)"""
-        return self.agent.learner.fused.select_zs(self.obs, wg_cap=self._select_cap(), rt=self._select_rt())
+        """the zs half of this iteration's select_action (see split_select;
+        EXO_SPLIT_ZS_CAP: its own workgroup cap, default the loop's)"""
+        cap = os.environ.get("EXO_SPLIT_ZS_CAP")
+        return self.agent.learner.fused.select_zs(self.obs, wg_cap=int(cap) if cap is not None else self._select_cap(),
+                                                  rt=self._select_rt())
 
     def _rollout(self, zs_img=None):
         ag = self.agent
