@@ -1,6 +1,4 @@
 """The HIP-graph-replayed training iteration (exo_amd.rollout.VecTrainer)."""
-import os
-
 import numpy as np
 import pytest
 import torch
@@ -149,12 +147,8 @@ def test_pair_graphs_are_bit_identical(monkeypatch, episodes):
     assert any(k[0] == "pair" for k in t1.graphs) and not any(k[0] == "pair" for k in t0.graphs)
 
 
-# (the "env" fork's cases run when EXO_TEST_SPLIT_FORK_ENV=1: tools/_ab/split_fork_ab.sh)
-_FORK_CASES = [("sync", "1", "env"), ("async", "1", "env")] if os.environ.get("EXO_TEST_SPLIT_FORK_ENV") == "1" else []
-
-
 @pytest.mark.parametrize("episodes,split,fork", [("sync", "0", "start"), ("async", "0", "start"),
-                                                 ("sync", "1", "start"), ("async", "1", "start")] + _FORK_CASES)
+                                                 ("sync", "1", "start"), ("async", "1", "start")])
 def test_overlapped_pairs_are_bit_identical(monkeypatch, episodes, split, fork):
     """EXO_OVERLAP_PAIRS (r05): an actor iteration and the critic-only one after
     it in one graph, the second's target chain / fixed / encoder passes beside
