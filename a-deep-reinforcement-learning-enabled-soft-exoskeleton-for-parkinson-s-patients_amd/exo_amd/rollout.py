@@ -350,12 +350,6 @@ class VecTrainer:
     # cost more than the shorter select saves) -- off.  EXO_SPLIT_SELECT:
     # "auto" (fp32 only), "1" (always), "0" (never).
     split_select = os.environ.get("EXO_SPLIT_SELECT", "auto")
-    # where the zs half forks: "start" (the second iteration's start) or "env"
-    # (right after the first iteration's env step and episode advance wrote
-    # the observations it reads, on a branch of its own)
-    split_fork = os.environ.get("EXO_SPLIT_FORK", "start")
-    _zs_fork_pending = False
-    _obs_ev = None
 
     def _split_select_ok(self):
         L = self.agent.learner
@@ -368,23 +362,6 @@ class VecTrainer:
         cap = os.environ.get("EXO_SPLIT_ZS_CAP")
         return self.agent.learner.fused.select_zs(self.obs, wg_cap=int(cap) if cap is not None else self._select_cap(),
                                                   rt=self._select_rt())
-
-    def _split_zs(self, br):
-        """launch the zs half for the rollout branch br: on br itself (split_fork
-        "start"), or on a branch forked where the previous rollout wrote the
-        observations and joined into br (split_fork "env"); returns the image"""
-        ev, self._obs_ev = self._obs_ev, None
-        if ev is None:
-            with torch.cuda.stream(br):
-                return self._select_zs()
-        if getattr(self, "_zs_stream", None) is None:
-            self._zs_stream = torch.cuda.Stream(device=self.device)
-        zst = self._zs_stream
-        zst.wait_event(ev)
-        with torch.cuda.stream(zst):
-            img = self._select_zs()
-        br.wait_stream(zst)
-        return img
 
     def _rollout(self, zs_img=None):
         ag = self.agent
@@ -403,10 +380,6 @@ class VecTrainer:
             self._ins_ev.record(torch.cuda.current_stream(self.device))
         self._advance()
         self.last_actions = act
-        if self._zs_fork_pending:  # the next select's observations are final here (split_fork "env")
-            self._zs_fork_pending = False
-            self._obs_ev = torch.cuda.Event()
-            self._obs_ev.record(torch.cuda.current_stream(self.device))
 
     def _advance(self, rew=None, score=None):
         """The next step's active mask and count on the device (exo_active_advance);
@@ -534,7 +507,8 @@ class VecTrainer:
             br.wait_stream(cur)
             zimg = None
             if split:  # select_action's zs half needs only the observations
-                zimg = self._split_zs(br)
+                with torch.cuda.stream(br):
+                    zimg = self._select_zs()
             if self._overlap_wait is not None:  # overlapped pair: after the previous actor step
                 br.wait_stream(self._overlap_wait)
             with torch.cuda.stream(br):
@@ -557,7 +531,8 @@ class VecTrainer:
                 br.wait_event(ev0)
                 zimg = None
                 if split:
-                    zimg = self._split_zs(br)
+                    with torch.cuda.stream(br):
+                        zimg = self._select_zs()
                 if self._overlap_wait is not None:
                     br.wait_stream(self._overlap_wait)
                 with torch.cuda.stream(br):
@@ -965,7 +940,6 @@ class VecTrainer:
                         L.prefetch_actor = u
                         if overlap and i == 0:
                             self._actor_stream = self._astream
-                            self._zs_fork_pending = self._split_select_ok() and self.split_fork == "env"
                         if overlap and i == 1:
                             self._actor_stream = None
                             self._overlap_wait = self._astream
@@ -988,7 +962,6 @@ class VecTrainer:
                         s.wait_stream(self._astream)
         finally:
             self._actor_stream = self._overlap_wait = None
-            self._zs_fork_pending, self._obs_ev = False, None
             L.before_critic_step = None
         torch.cuda.current_stream(self.device).wait_stream(s)
         self._cur = cur0

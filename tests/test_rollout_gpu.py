@@ -147,9 +147,8 @@ def test_pair_graphs_are_bit_identical(monkeypatch, episodes):
     assert any(k[0] == "pair" for k in t1.graphs) and not any(k[0] == "pair" for k in t0.graphs)
 
 
-@pytest.mark.parametrize("episodes,split,fork", [("sync", "0", "start"), ("async", "0", "start"),
-                                                 ("sync", "1", "start"), ("async", "1", "start")])
-def test_overlapped_pairs_are_bit_identical(monkeypatch, episodes, split, fork):
+@pytest.mark.parametrize("episodes,split", [("sync", "0"), ("async", "0"), ("sync", "1"), ("async", "1")])
+def test_overlapped_pairs_are_bit_identical(monkeypatch, episodes, split):
     """EXO_OVERLAP_PAIRS (r05): an actor iteration and the critic-only one after
     it in one graph, the second's target chain / fixed / encoder passes beside
     the first's actor passes (its rollout and critic step wait for them).  The
@@ -158,14 +157,11 @@ def test_overlapped_pairs_are_bit_identical(monkeypatch, episodes, split, fork):
     refreshes (target_update_rate 5: unpaired graphs around them).  Fused
     bf16 passes (the overlap needs the fused update), 256-wide nets.  split
     "1" (r06): the second iteration's select_action in two launches, its zs
-    half from the iteration's start or, fork "env", from where the first
-    iteration's env step and episode advance wrote the observations
-    (EXO_SPLIT_SELECT, EXO_SPLIT_FORK)."""
+    half from the iteration's start (EXO_SPLIT_SELECT)."""
     from exo_amd import VecExoskeletonEnv
     from exo_amd.rollout import VecTrainer
     from exo_amd.td7 import Agent, Hyperparameters
     monkeypatch.setattr(VecTrainer, "split_select", split)
-    monkeypatch.setattr(VecTrainer, "split_fork", fork)
     res = []
     for overlap in (False, True):
         monkeypatch.setattr(VecTrainer, "overlap_pairs", overlap)
